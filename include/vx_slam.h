@@ -1,0 +1,197 @@
+/*
+ * vx_slam.h — C ABI of the MI355X-native (gfx950) VisionX-SLAM hot path.
+ *
+ * One shared library (visionx-slam_amd/lib/libvxslam.so) exports these entry points.  They
+ * are plain C: pointers, sizes and status codes, no C++/torch types, no exceptions across the
+ * boundary.  Every call returns VX_OK (0) or a negative VX_ERR_*; vx_last_error() gives text.
+ *
+ * Reference interfaces replaced (paths relative to QinZiwen/VisionX-SLAM):
+ *   vx_orb_extract        <- FeatureExtractor::Extract(Frame&)   core/feature/feature_extractor.h:15
+ *                            ORBExtractor::Extract               core/feature/orb_extractor.cpp:9-27
+ *                            ORBExtractor(n=1000, 1.2f, 8)       core/feature/orb_extractor.h:11-13
+ *   vx_match_knn2_ratio   <- FeatureMatcher::Match(last, curr, matches)
+ *                                                                core/feature/feature_matcher.h:11-12
+ *                            ORBMatcher::Match + Options         core/feature/orb_matcher.cpp:11-43,
+ *                                                                orb_matcher.h:11-14
+ *   vx_ba_optimize_map    <- LocalBA::Optimize(map, ref_kf)      core/backend/local_ba.h:23,
+ *                                                                local_ba.cpp:95-278
+ *                            LocalBA::Options                    core/backend/local_ba.h:12-19
+ *
+ * The host-side C++ adapters that keep the reference call surface (same class names and
+ * signatures) are in visionx-slam_amd/host/; the bindings a reference maintainer adds are in
+ * INTEGRATION.md.
+ *
+ * Threading: a vx_ctx is not thread-safe; use one per calling thread (the reference calls the
+ * hot path from its single tracking thread, core/system/system.cpp:39-52).  Synchronous calls
+ * return after results are in caller memory.  *_async calls enqueue on the context's HIP stream
+ * and work on device-resident data; vx_synchronize() / the *_fetch calls complete them.
+ */
+#ifndef VX_SLAM_H
+#define VX_SLAM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VX_OK 0
+#define VX_ERR_INVALID (-1)   /* bad argument */
+#define VX_ERR_HIP (-2)       /* HIP runtime failure (message in vx_last_error) */
+#define VX_ERR_CAPACITY (-3)  /* caller buffer too small; *n_out holds the required count */
+#define VX_ERR_COMM (-4)      /* RCCL failure */
+#define VX_ERR_STATE (-5)     /* call sequence error (e.g. fetch before extract) */
+
+#define VX_MAX_SLOTS 4        /* device-resident keypoint/descriptor slots per context */
+
+typedef struct vx_ctx vx_ctx;
+
+/* cv::KeyPoint fields the reference keeps (orb_extractor.cpp:19-24 keeps pt and response;
+ * octave and angle are exported too so callers can reproduce cv::KeyPoint). */
+typedef struct {
+    float x, y;        /* level-0 pixel coordinates */
+    float response;    /* Harris response (HARRIS_SCORE) */
+    float angle;       /* degrees [0, 360), intensity centroid */
+    int32_t octave;    /* pyramid level */
+} vx_keypoint;
+
+/* cv::DMatch with imgIdx = 0 */
+typedef struct {
+    int32_t query_idx, train_idx;
+    float distance;
+} vx_match;
+
+/* cv::ORB::create(n_features, scale_factor, n_levels) with OpenCV's remaining defaults
+ * (edgeThreshold 31, firstLevel 0, WTA_K 2, HARRIS_SCORE, patchSize 31, fastThreshold 20). */
+typedef struct {
+    int32_t n_features;      /* 1000 (orb_extractor.h:11) */
+    float scale_factor;      /* 1.2f */
+    int32_t n_levels;        /* 8   */
+    int32_t fast_threshold;  /* 20  */
+    int32_t edge_threshold;  /* 31  */
+} vx_orb_params;
+
+/* ---------------------------------------------------------------- context */
+int vx_version(void);
+int vx_create(int device, vx_ctx** out);
+void vx_destroy(vx_ctx* ctx);
+const char* vx_last_error(const vx_ctx* ctx);
+void* vx_stream(vx_ctx* ctx);          /* the context's hipStream_t */
+int vx_synchronize(vx_ctx* ctx);
+void vx_orb_default_params(vx_orb_params* p);
+/* Copies the compiled-in rBRIEF pattern (bit_pattern_31_, 256 x {x1,y1,x2,y2}). */
+int vx_orb_pattern(int32_t* out_1024);
+
+/* ---------------------------------------------------------------- ORB extraction
+ * img: 8UC1 gray or 8UC3/8UC4 BGR(A) rows of row_stride bytes.  Keypoints are emitted level by
+ * level (octave ascending) and in raster order inside a level; the keypoint SET per level is
+ * exactly OpenCV's (retainBest keeps {response >= k-th largest}), the order inside a level is
+ * canonical instead of the libstdc++ nth_element permutation.  out_desc gets
+ * N rows of 32 bytes.  Returns VX_ERR_CAPACITY (with *n_out = N) if N > cap. */
+int vx_orb_extract(vx_ctx* ctx, const vx_orb_params* params, const uint8_t* img, int width,
+                   int height, int channels, int64_t row_stride, vx_keypoint* out_kp,
+                   uint8_t* out_desc, int cap, int* n_out);
+/* Device-resident variant: d_img is device memory; results stay in `slot`. */
+int vx_orb_extract_async(vx_ctx* ctx, const vx_orb_params* params, const uint8_t* d_img,
+                         int width, int height, int channels, int64_t row_stride, int slot);
+int vx_orb_fetch(vx_ctx* ctx, int slot, vx_keypoint* out_kp, uint8_t* out_desc, int cap,
+                 int* n_out);
+/* Device pointers of a slot's descriptor rows and its device-side count (for interop). */
+int vx_orb_slot_device(vx_ctx* ctx, int slot, const uint8_t** d_desc, const int32_t** d_count);
+
+/* ---------------------------------------------------------------- matching
+ * knnMatch(query = last frame, train = current frame, k = 2) + ratio test
+ * (m1.distance < ratio * m2.distance), matches in ascending query index. */
+int vx_match_knn2_ratio(vx_ctx* ctx, const uint8_t* query_desc, int n_query,
+                        const uint8_t* train_desc, int n_train, float ratio, vx_match* out,
+                        int cap, int* n_out);
+/* Device-resident variant matching two extraction slots (counts read on device). */
+int vx_match_slots_async(vx_ctx* ctx, int query_slot, int train_slot, float ratio);
+int vx_match_fetch(vx_ctx* ctx, vx_match* out, int cap, int* n_out);
+
+/* ---------------------------------------------------------------- local bundle adjustment
+ * A flattened snapshot of visionx::Map (map.h:13-35): keyframes with their Feature vectors
+ * (frame.h:16-23) and landmarks with their observation maps (landmark.h:300-318).  Keyframes may
+ * be in any order (the reference's std::map sorts them by id).  kf_pose and lm_pos are updated
+ * in place, exactly as Frame::SetPose / Landmark::SetPosition would be. */
+typedef struct {
+    int32_t n_kf;
+    const uint64_t* kf_id;
+    double* kf_pose;             /* 7 per KF: qx qy qz qw tx ty tz (T_cw, world -> camera) */
+    const double* kf_intr;       /* 4 per KF: fx fy cx cy */
+    const uint8_t* kf_has_cam;   /* Frame::GetCamera() != nullptr */
+    const int64_t* kf_feat_ptr;  /* n_kf + 1, CSR into the feature arrays */
+    const double* feat_uv;       /* 2 per feature */
+    const uint64_t* feat_lm_id;  /* Feature::landmark_id_ */
+    const uint8_t* feat_flags;   /* bit0 has_landmark, bit1 is_outlier */
+    int32_t n_lm;
+    const uint64_t* lm_id;
+    double* lm_pos;              /* 3 per landmark */
+    const uint8_t* lm_bad;
+    const int64_t* lm_obs_ptr;   /* n_lm + 1, CSR of (kf id, feature index) observations */
+    const uint64_t* obs_kf_id;
+    const uint64_t* obs_feat_idx;
+} vx_map_view;
+
+typedef struct {                 /* LocalBA::Options, local_ba.h:12-19 */
+    int32_t window_size;         /* 5 */
+    int32_t max_iterations;      /* 5 */
+    int32_t min_pose_observations;   /* 20 */
+    int32_t min_point_observations;  /* 2 */
+    double huber_delta;          /* 5.0 */
+    double max_reproj_error;     /* 5.0 */
+} vx_ba_options;
+
+typedef struct {
+    int32_t iterations;          /* outer iterations executed (including the one that broke) */
+    int32_t n_window_kf, n_landmarks;
+    double cost[16];             /* pose-stage total_cost per iteration */
+    int32_t obs[16];             /* pose-stage total_obs per iteration */
+    double gate_margin;          /* unused by the GPU path (set to -1) */
+    int32_t status;              /* 0 optimised, 1 early return (no KF pair / no landmark) */
+} vx_ba_stats;
+
+void vx_ba_default_options(vx_ba_options* o);
+int vx_ba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
+                       const vx_ba_options* opt, vx_ba_stats* stats);
+
+/* Staged form: plan = window selection + device CSR upload (host work of local_ba.cpp:95-137);
+ * run = the iterations on the device from the plan's initial state (repeatable);
+ * fetch = download + scatter back into `map` (may be NULL to only read stats).
+ * shard_count > 1 keeps only this rank's landmark shard (landmark id hash) and all-reduces the
+ * per-keyframe normal equations over the communicator set by vx_comm_init. */
+typedef struct vx_ba_plan vx_ba_plan;
+int vx_ba_plan_create(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
+                      const vx_ba_options* opt, int shard_rank, int shard_count,
+                      vx_ba_plan** out);
+int vx_ba_plan_run_async(vx_ctx* ctx, vx_ba_plan* plan);
+int vx_ba_plan_fetch(vx_ctx* ctx, vx_ba_plan* plan, vx_map_view* map, vx_ba_stats* stats);
+void vx_ba_plan_destroy(vx_ba_plan* plan);
+/* sizes of the device problem: n_kf, n_lm (local shard), n_pose_obs, n_lm_obs */
+int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out4);
+/* Host-only dry run of vx_ba_plan_create (needs no device): out8 = {status, n_window_kf,
+ * n_landmarks (all shards), n_kf, n_opt (local optimisable), n_lm (local table), n_pose_obs,
+ * n_lm_obs}; lm_map_idx / kf_map_idx (optional) receive the local tables as map indices. */
+int vx_ba_plan_inspect(const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
+                       const vx_ba_options* opt, int shard_rank, int shard_count, int64_t* out8,
+                       int32_t* lm_map_idx, int cap_lm, int32_t* kf_map_idx, int cap_kf);
+/* Landmark -> shard assignment used by sharded plans (splitmix64(id) mod shard_count). */
+uint32_t vx_ba_shard_of(uint64_t lm_id, int shard_count);
+
+/* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
+int vx_comm_unique_id(uint8_t* out_128);
+int vx_comm_init(vx_ctx* ctx, const uint8_t* id_128, int nranks, int rank);
+
+/* ---------------------------------------------------------------- profiling
+ * When enabled, the library brackets its kernels with hipEvents on its own stream; read back
+ * accumulated milliseconds and launch counts per stage (names via vx_prof_name). */
+int vx_prof_enable(vx_ctx* ctx, int on);
+int vx_prof_count(void);
+const char* vx_prof_name(int stage);
+int vx_prof_read(vx_ctx* ctx, double* ms, int64_t* launches, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VX_SLAM_H */

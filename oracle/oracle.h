@@ -1,0 +1,116 @@
+/*
+ * oracle.h — CPU restatement of VisionX-SLAM's hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / CPU baseline.  The product (visionx-slam_amd/) never
+ * links or calls it.
+ *
+ * What it restates (reference = /root/reference, QinZiwen/VisionX-SLAM @ 2026-02-13):
+ *   - ORBExtractor::Extract (core/feature/orb_extractor.cpp:9-27), i.e.
+ *     cv::ORB::create(n, 1.2f, 8)->detectAndCompute(img, noArray(), kps, desc)
+ *     (orb_extractor.cpp:6,13).  The arithmetic lives in OpenCV 4.x (vcpkg port opencv4 at
+ *     builtin-baseline 25b458671af03578e6a34edd8f0d1ac85e084df4, vcpkg.json:4,8-11), which is
+ *     NOT present in this container.  The restatement follows the published OpenCV 4.x
+ *     algorithm.  PARITY VS REAL OPENCV IS UNPINNED: the reference
+ *     ships no tests, fixtures or golden vectors for this path.
+ *   - ORBMatcher::Match (core/feature/orb_matcher.cpp:11-43): BFMatcher(NORM_HAMMING)
+ *     knnMatch(k=2) + ratio test.  Unpinned vs OpenCV for the same reason.
+ *   - LocalBA::Optimize (core/backend/local_ba.cpp:95-278) + ProjectToPixel
+ *     (core/common/projection.h:11-31), line for line, with Eigen LDLT and Sophus SE3::exp
+ *     restated.  Pinned by the reference source itself (fully visible).
+ */
+#pragma once
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    float x, y;       /* level-0 pixel coordinates (pt *= layerScale, OpenCV computeKeyPoints) */
+    float response;   /* Harris response */
+    float angle;      /* degrees, fastAtan2 */
+    int32_t octave;
+} orc_keypoint;
+
+typedef struct {
+    int32_t query_idx, train_idx;
+    float distance;
+} orc_match;
+
+/* Order of keypoints inside one pyramid level.
+ *  ORC_ORDER_STL    : the std::nth_element / std::partition permutation of OpenCV's
+ *                     KeyPointsFilter::retainBest as compiled against THIS libstdc++.
+ *  ORC_ORDER_RASTER : the same keypoint set in raster order (y, then x) — the canonical order
+ *                     emitted by the GPU path.                                               */
+enum { ORC_ORDER_STL = 0, ORC_ORDER_RASTER = 1 };
+
+int orc_orb_quotas(int n_features, float scale_factor, int n_levels, int32_t* quotas);
+int orc_orb_level_sizes(int w, int h, float scale_factor, int n_levels, int32_t* lw, int32_t* lh,
+                        float* scales);
+/* gray + INTER_LINEAR_EXACT pyramid; levels packed back to back (level l at offset sum_{k<l} w_k*h_k) */
+int orc_orb_pyramid(const uint8_t* img, int w, int h, int channels, int64_t row_stride,
+                    float scale_factor, int n_levels, uint8_t* out, int64_t out_cap);
+/* FAST-9/16 + 3x3 NMS on one level, raster order; xys = (x,y,score) triples */
+int orc_fast_nms(const uint8_t* img, int w, int h, int threshold, int32_t* xys, int cap, int* n_out);
+/* FAST score map before NMS (0 = not a corner) */
+int orc_fast_scores(const uint8_t* img, int w, int h, int threshold, uint8_t* out);
+float orc_harris(const uint8_t* img, int w, int h, int x, int y);
+float orc_ic_angle(const uint8_t* img, int w, int h, int x, int y);
+float orc_fast_atan2(float y, float x);
+/* GaussianBlur(7x7, sigma 2, BORDER_REFLECT_101) of one level (float separable path) */
+int orc_blur_level(const uint8_t* img, int w, int h, uint8_t* out);
+
+int orc_orb_extract(const uint8_t* img, int w, int h, int channels, int64_t row_stride,
+                    int n_features, float scale_factor, int n_levels, int fast_threshold,
+                    const int32_t* pattern /* 256*4 ints */, int order,
+                    orc_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+
+/* BFMatcher::knnMatch(k=2) raw result per query: (train idx, dist) x 2, -1 when absent */
+int orc_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx2, int32_t* dist2);
+/* ORBMatcher::Match: returns count, matches in ascending query order */
+int orc_match_knn2_ratio(const uint8_t* q, int nq, const uint8_t* t, int nt, float ratio,
+                         orc_match* out, int cap, int* n_out);
+
+/* ---- LocalBA on a flattened snapshot of visionx::Map ---- */
+typedef struct {
+    /* keyframes (any order; the reference's std::map orders them by id) */
+    int32_t n_kf;
+    const uint64_t* kf_id;
+    double* kf_pose;            /* 7 per KF: qx qy qz qw tx ty tz (Sophus SE3d T_cw, world->camera) */
+    const double* kf_intr;      /* 4 per KF: fx fy cx cy (Camera getters, camera.h:29-32) */
+    const uint8_t* kf_has_cam;  /* Frame::GetCamera() != nullptr */
+    const int64_t* kf_feat_ptr; /* n_kf+1 CSR into the feature arrays */
+    const double* feat_uv;      /* 2 per feature: Feature::position */
+    const uint64_t* feat_lm_id; /* Feature::landmark_id_ */
+    const uint8_t* feat_flags;  /* bit0 has_landmark, bit1 is_outlier */
+    /* landmarks (Map::landmarks_) */
+    int32_t n_lm;
+    const uint64_t* lm_id;
+    double* lm_pos;             /* 3 per landmark */
+    const uint8_t* lm_bad;
+    const int64_t* lm_obs_ptr;  /* n_lm+1 CSR: Landmark::observations_ (kf_id -> feature idx) */
+    const uint64_t* obs_kf_id;
+    const uint64_t* obs_feat_idx;
+} orc_map_view;
+
+typedef struct {
+    int32_t window_size, max_iterations, min_pose_observations, min_point_observations;
+    double huber_delta, max_reproj_error;
+} orc_ba_options;
+
+typedef struct {
+    int32_t iterations;          /* outer iterations executed (including the breaking one) */
+    int32_t n_window_kf, n_landmarks;
+    double cost[16];             /* total_cost per iteration */
+    int32_t obs[16];             /* total_obs per iteration */
+    double gate_margin;          /* min over all evaluations of | |e| - max_reproj_error | */
+    int32_t status;              /* 0 ran, 1 early return (no map / <2 KF / no landmarks) */
+} orc_ba_stats;
+
+int orc_ba_optimize_map(orc_map_view* map, uint64_t ref_kf_id, int has_ref,
+                        const orc_ba_options* opt, orc_ba_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif

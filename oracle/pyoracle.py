@@ -1,0 +1,212 @@
+"""ctypes binding of oracle/build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, as the
+checker / CPU baseline.  See oracle.h for what is restated and how it is pinned.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+PATTERN_PATH = os.path.join(os.path.dirname(HERE), "tests", "golden", "orb_bit_pattern_31.txt")
+
+ORDER_STL, ORDER_RASTER = 0, 1
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"),
+                           ("octave", "<i4")])
+MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("distance", "<f4")])
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = C.CDLL(LIB_PATH)
+        _lib.orc_harris.restype = C.c_float
+        _lib.orc_ic_angle.restype = C.c_float
+        _lib.orc_fast_atan2.restype = C.c_float
+        _lib.orc_fast_atan2.argtypes = [C.c_float, C.c_float]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def load_pattern() -> np.ndarray:
+    rows = [l.split() for l in open(PATTERN_PATH) if not l.startswith("#")]
+    return np.array(rows, dtype=np.int32).reshape(-1)
+
+
+def quotas(n, scale=1.2, levels=8):
+    q = np.zeros(levels, np.int32)
+    lib().orc_orb_quotas(n, C.c_float(scale), levels, _p(q))
+    return q
+
+
+def level_sizes(w, h, scale=1.2, levels=8):
+    lw = np.zeros(levels, np.int32)
+    lh = np.zeros(levels, np.int32)
+    s = np.zeros(levels, np.float32)
+    lib().orc_orb_level_sizes(w, h, C.c_float(scale), levels, _p(lw), _p(lh), _p(s))
+    return lw, lh, s
+
+
+def pyramid(img, scale=1.2, levels=8):
+    img = np.ascontiguousarray(img)
+    h, w = img.shape[:2]
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    lw, lh, _ = level_sizes(w, h, scale, levels)
+    tot = int((lw.astype(np.int64) * lh).sum())
+    out = np.zeros(tot, np.uint8)
+    rc = lib().orc_orb_pyramid(_p(img), w, h, ch, C.c_int64(img.strides[0]), C.c_float(scale),
+                               levels, _p(out), C.c_int64(tot))
+    assert rc == 0
+    res, off = [], 0
+    for a, b in zip(lw, lh):
+        res.append(out[off:off + a * b].reshape(b, a))
+        off += a * b
+    return res
+
+
+def fast_nms(level, threshold=20):
+    level = np.ascontiguousarray(level, np.uint8)
+    h, w = level.shape
+    cap = w * h // 2 + 16
+    xys = np.zeros((cap, 3), np.int32)
+    n = C.c_int(0)
+    rc = lib().orc_fast_nms(_p(level), w, h, threshold, _p(xys), cap, C.byref(n))
+    assert rc == 0
+    return xys[:n.value].copy()
+
+
+def fast_scores(level, threshold=20):
+    level = np.ascontiguousarray(level, np.uint8)
+    out = np.zeros_like(level)
+    lib().orc_fast_scores(_p(level), level.shape[1], level.shape[0], threshold, _p(out))
+    return out
+
+
+def harris(level, x, y):
+    level = np.ascontiguousarray(level, np.uint8)
+    return lib().orc_harris(_p(level), level.shape[1], level.shape[0], int(x), int(y))
+
+
+def ic_angle(level, x, y):
+    level = np.ascontiguousarray(level, np.uint8)
+    return lib().orc_ic_angle(_p(level), level.shape[1], level.shape[0], int(x), int(y))
+
+
+def fast_atan2(y, x):
+    return lib().orc_fast_atan2(float(y), float(x))
+
+
+def blur_level(level):
+    level = np.ascontiguousarray(level, np.uint8)
+    out = np.zeros_like(level)
+    lib().orc_blur_level(_p(level), level.shape[1], level.shape[0], _p(out))
+    return out
+
+
+def orb_extract(img, n_features=1000, scale=1.2, levels=8, fast_threshold=20,
+                order=ORDER_RASTER, pattern=None):
+    img = np.ascontiguousarray(img)
+    h, w = img.shape[:2]
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    pat = load_pattern() if pattern is None else np.ascontiguousarray(pattern, np.int32)
+    cap = 4 * n_features + 64
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = C.c_int(0)
+    rc = lib().orc_orb_extract(_p(img), w, h, ch, C.c_int64(img.strides[0]), n_features,
+                               C.c_float(scale), levels, fast_threshold, _p(pat), order, _p(kps),
+                               _p(desc), cap, C.byref(n))
+    assert rc == 0, rc
+    return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def knn2(q, t):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.int32)
+    lib().orc_knn2(_p(q), len(q), _p(t), len(t), _p(idx), _p(dist))
+    return idx, dist
+
+
+def match(q, t, ratio=0.8):
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    out = np.zeros(max(len(q), 1), MATCH_DTYPE)
+    n = C.c_int(0)
+    rc = lib().orc_match_knn2_ratio(_p(q), len(q), _p(t), len(t), C.c_float(ratio), _p(out),
+                                    len(out), C.byref(n))
+    assert rc == 0
+    return out[:n.value].copy()
+
+
+# ---------------------------------------------------------------------------- LocalBA
+class MapView(C.Structure):
+    _fields_ = [("n_kf", C.c_int32), ("kf_id", C.c_void_p), ("kf_pose", C.c_void_p),
+                ("kf_intr", C.c_void_p), ("kf_has_cam", C.c_void_p), ("kf_feat_ptr", C.c_void_p),
+                ("feat_uv", C.c_void_p), ("feat_lm_id", C.c_void_p), ("feat_flags", C.c_void_p),
+                ("n_lm", C.c_int32), ("lm_id", C.c_void_p), ("lm_pos", C.c_void_p),
+                ("lm_bad", C.c_void_p), ("lm_obs_ptr", C.c_void_p), ("obs_kf_id", C.c_void_p),
+                ("obs_feat_idx", C.c_void_p)]
+
+
+class BAOptions(C.Structure):
+    _fields_ = [("window_size", C.c_int32), ("max_iterations", C.c_int32),
+                ("min_pose_observations", C.c_int32), ("min_point_observations", C.c_int32),
+                ("huber_delta", C.c_double), ("max_reproj_error", C.c_double)]
+
+
+class BAStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("n_window_kf", C.c_int32), ("n_landmarks", C.c_int32),
+                ("cost", C.c_double * 16), ("obs", C.c_int32 * 16), ("gate_margin", C.c_double),
+                ("status", C.c_int32)]
+
+
+def map_view(m, cls=MapView):
+    """Build a MapView over the arrays of a synth.BAMap (kf_pose / lm_pos are updated in place)."""
+    keys = [f[0] for f in cls._fields_]
+    v = cls()
+    for k in keys:
+        if k in ("n_kf", "n_lm"):
+            setattr(v, k, int(m["kf_id" if k == "n_kf" else "lm_id"].shape[0]))
+        else:
+            a = m[k]
+            assert a.flags["C_CONTIGUOUS"], k
+            setattr(v, k, a.ctypes.data)
+    return v
+
+
+def ba_options(window=5, iters=5, min_pose=20, min_point=2, huber=5.0, max_err=5.0):
+    return BAOptions(window, iters, min_pose, min_point, huber, max_err)
+
+
+def ba_optimize(m, opts=None, ref_kf_id=None):
+    """Runs the oracle LocalBA on a synth.BAMap in place; returns BAStats."""
+    if opts is None:
+        opts = ba_options(window=m.get("window", 5))
+    v = map_view(m)
+    st = BAStats()
+    ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+    has_ref = 0 if ref is None else 1
+    rc = lib().orc_ba_optimize_map(C.byref(v), C.c_uint64(0 if ref is None else int(ref)), has_ref,
+                                   C.byref(opts), C.byref(st))
+    assert rc == 0
+    return st

@@ -1,0 +1,99 @@
+"""Regenerates the golden vectors in tests/golden/ from the CPU restatement (oracle/).
+
+    python tests/golden/make_golden.py
+
+Inputs are seeded synthetic data from vxslam.synth (the TUM sequences are not available); each
+fixture stores a sha256 of its regenerated input so a test notices if the generator drifts.
+These vectors pin the GPU path to the oracle and guard the oracle against regressions.  They do
+NOT pin anything to real OpenCV (unavailable offline): ORB/BF parity vs OpenCV is unpinned.
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
+
+import pyoracle as O  # noqa: E402
+from vxslam import synth  # noqa: E402
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+# ---- ORB cases: (name, seed, h, w, channels, n_features)
+ORB_CASES = [
+    ("vga_bgr_n1000", 0x5EED0002, 480, 640, 3, 1000),
+    ("vga_gray_n2000", 0x5EED0003, 480, 640, 1, 2000),
+    ("qqvga_bgr_n500", 0x5EED0004, 120, 160, 3, 500),
+    ("odd_bgra_n700", 0x5EED0005, 301, 419, 4, 700),
+]
+
+
+def orb_input(seed, h, w, ch):
+    f = synth.make_frames(seed, 1, h, w)[0]
+    if ch == 1:
+        return np.ascontiguousarray(f[:, :, 1])
+    if ch == 4:
+        return np.ascontiguousarray(np.concatenate([f, np.full((h, w, 1), 7, np.uint8)], -1))
+    return f
+
+
+# ---- BA cases: (name, seed, n_kf, n_lm, n_old, huber, max_err, iters)
+BA_CASES = [
+    ("w5_lm500", 101, 5, 500, 2, 5.0, 5.0, 5),
+    ("w10_lm2000", 102, 10, 2000, 3, 5.0, 5.0, 5),
+    ("w10_huber2", 103, 10, 2000, 3, 2.0, 5.0, 5),
+]
+
+
+def match_input(seed, n):
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    q = base.copy()
+    flip = rng.integers(0, 2, (n, 32), dtype=np.uint8) & rng.integers(0, 2, (n, 32), dtype=np.uint8)
+    t = (base ^ (flip * rng.integers(1, 256, (n, 32), dtype=np.uint8) * (rng.random((n, 32)) < 0.15))).astype(np.uint8)
+    t = t[rng.permutation(n)]
+    t[5] = t[9]          # planted exact tie between train rows
+    t[100:110] = t[200]  # many equal rows
+    return q, t
+
+
+def main():
+    out = {}
+    for name, seed, h, w, ch, n in ORB_CASES:
+        img = orb_input(seed, h, w, ch)
+        kps, desc = O.orb_extract(img, n, order=O.ORDER_RASTER)
+        out[f"orb_{name}_sha"] = np.frombuffer(sha(img).encode(), np.uint8)
+        out[f"orb_{name}_kp"] = kps
+        out[f"orb_{name}_desc"] = desc
+    np.savez_compressed(os.path.join(HERE, "orb_golden.npz"), **out)
+
+    q, t = match_input(77, 512)
+    idx, dist = O.knn2(q, t)
+    m = O.match(q, t)
+    np.savez_compressed(os.path.join(HERE, "match_golden.npz"), q=q, t=t, idx=idx, dist=dist, matches=m)
+
+    out = {}
+    for name, seed, nk, nl, nold, hub, merr, iters in BA_CASES:
+        mp = synth.make_ba_map(seed, nk, nl, n_old_kf=nold)
+        out[f"ba_{name}_sha"] = np.frombuffer(sha(np.concatenate([mp["kf_pose"].ravel(), mp["lm_pos"].ravel()])).encode(), np.uint8)
+        st = O.ba_optimize(mp, O.ba_options(window=nk, iters=iters, huber=hub, max_err=merr))
+        out[f"ba_{name}_pose"] = mp["kf_pose"]
+        out[f"ba_{name}_lm"] = mp["lm_pos"]
+        out[f"ba_{name}_stats"] = np.array([st.iterations, st.n_window_kf, st.n_landmarks, st.status], np.int64)
+        out[f"ba_{name}_cost"] = np.array(st.cost[:st.iterations])
+        out[f"ba_{name}_obs"] = np.array(st.obs[:st.iterations], np.int64)
+        out[f"ba_{name}_margin"] = np.array([st.gate_margin])
+    np.savez_compressed(os.path.join(HERE, "ba_golden.npz"), **out)
+    for f in ("orb_golden.npz", "match_golden.npz", "ba_golden.npz"):
+        print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

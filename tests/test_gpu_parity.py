@@ -1,0 +1,251 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU restatement on the same inputs.
+
+Bars (BASELINE.json north_star):
+  * ORB keypoints (all fields) and descriptor bits: bit-exact.
+  * matches (query, train, distance): identical.
+  * LocalBA poses / landmarks: |gpu - cpu| <= 1e-4 * max(|cpu|, 1e-3) per component, identical
+    iteration counts and per-iteration observation counts (no gate flips).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from vxslam import synth
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import make_golden as G  # noqa: E402
+
+BA_RTOL = 1e-4  # relative tolerance on final pose parameters / landmarks (north_star)
+
+
+def _orb_params(vxslam, n):
+    return vxslam.default_orb_params(n_features=n)
+
+
+def _assert_orb_equal(kg, dg, kc, dc):
+    assert len(kg) == len(kc), (len(kg), len(kc))
+    for f in ("octave", "x", "y", "response", "angle"):
+        bad = np.nonzero(kg[f] != kc[f])[0]
+        assert bad.size == 0, (f, bad[:5], kg[bad[:5]], kc[bad[:5]])
+    bad = np.nonzero((dg != dc).any(1))[0]
+    assert bad.size == 0, ("descriptor rows differ", bad[:10])
+
+
+# ---------------------------------------------------------------------------- ORB
+@pytest.mark.parametrize("case", G.ORB_CASES, ids=[c[0] for c in G.ORB_CASES])
+def test_orb_golden_gpu(ctx, case):
+    import vxslam
+
+    g = np.load(os.path.join(HERE, "golden", "orb_golden.npz"))
+    name, seed, h, w, ch, n = case
+    img = G.orb_input(seed, h, w, ch)
+    kps, desc = ctx.orb_extract(img, _orb_params(vxslam, n))
+    _assert_orb_equal(kps, desc, g[f"orb_{name}_kp"], g[f"orb_{name}_desc"])
+
+
+@pytest.mark.parametrize("seed,h,w,n", [(11, 480, 640, 1000), (12, 480, 640, 2000), (13, 960, 1280, 4000),
+                                        (14, 333, 517, 800), (15, 64, 80, 100), (16, 200, 200, 300)])
+def test_orb_random_frames(ctx, oracle, seed, h, w, n):
+    import vxslam
+
+    img = synth.make_frames(seed, 1, h, w)[0]
+    kps, desc = ctx.orb_extract(img, _orb_params(vxslam, n))
+    kc, dc = oracle.orb_extract(img, n, order=oracle.ORDER_RASTER)
+    _assert_orb_equal(kps, desc, kc, dc)
+
+
+def test_orb_edge_inputs(ctx, oracle):
+    import vxslam
+
+    p = _orb_params(vxslam, 500)
+    flat = np.full((240, 320), 90, np.uint8)                  # no corners at all
+    k, d = ctx.orb_extract(flat, p)
+    assert len(k) == 0
+    tiny = synth.make_texture(3, 40, 50)                      # every level inside the 31 px border
+    k, d = ctx.orb_extract(tiny, p)
+    assert len(k) == 0
+    # heavy FAST / Harris ties: a quantised checkerboard-like texture
+    yy, xx = np.mgrid[0:240, 0:320]
+    chk = (((yy // 7) + (xx // 9)) % 2 * 120 + 60).astype(np.uint8)
+    for img in (chk, np.ascontiguousarray(chk[:, ::-1])):
+        k, d = ctx.orb_extract(img, p)
+        kc, dc = oracle.orb_extract(img, 500, order=oracle.ORDER_RASTER)
+        _assert_orb_equal(k, d, kc, dc)
+    # strided input (row_stride > width * channels): a view into a wider buffer
+    big = synth.make_frames(21, 1, 480, 700)[0]
+    view = big[:, 20:660]
+    assert not view.flags["C_CONTIGUOUS"]
+    k, d = ctx.orb_extract(np.ascontiguousarray(view), p)
+    kc, dc = oracle.orb_extract(np.ascontiguousarray(view), 500, order=oracle.ORDER_RASTER)
+    _assert_orb_equal(k, d, kc, dc)
+
+
+def test_orb_repeatable_and_params_switch(ctx):
+    import vxslam
+
+    img = synth.make_frames(31, 1)[0]
+    a = ctx.orb_extract(img, _orb_params(vxslam, 1000))
+    b = ctx.orb_extract(img, _orb_params(vxslam, 2000))
+    c = ctx.orb_extract(img, _orb_params(vxslam, 1000))
+    assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1])
+    assert len(b[0]) > len(a[0])
+
+
+def test_orb_invalid_arguments(ctx):
+    import vxslam
+
+    img = synth.make_frames(32, 1, 120, 160)[0]
+    with pytest.raises(vxslam.VxError):
+        ctx.orb_extract(img, vxslam.default_orb_params(n_levels=0))
+    with pytest.raises(vxslam.VxError):
+        ctx.orb_extract(img, vxslam.default_orb_params(edge_threshold=5))
+    with pytest.raises(vxslam.VxError) as e:
+        ctx.orb_extract(synth.make_frames(33, 1)[0], vxslam.default_orb_params(n_features=1000), cap=10)
+    assert e.value.code == vxslam.VX_ERR_CAPACITY
+
+
+# ---------------------------------------------------------------------------- matching
+def test_match_golden_gpu(ctx):
+    g = np.load(os.path.join(HERE, "golden", "match_golden.npz"))
+    m = ctx.match(g["q"], g["t"])
+    assert np.array_equal(m, g["matches"])
+
+
+@pytest.mark.parametrize("nq,nt", [(1000, 1000), (2000, 2000), (4000, 4000), (3, 1), (1, 2), (70, 4100)])
+def test_match_random(ctx, oracle, nq, nt):
+    rng = np.random.default_rng(nq * 7 + nt)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    q = t[rng.integers(0, nt, nq)] ^ (rng.random((nq, 32)) < 0.05).astype(np.uint8) * rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    if nt > 20:
+        t[7] = t[13]
+    assert np.array_equal(ctx.match(q, t), oracle.match(q, t))
+
+
+def test_match_empty_and_ties(ctx, oracle):
+    z = np.zeros((0, 32), np.uint8)
+    q = np.zeros((5, 32), np.uint8)
+    assert len(ctx.match(z, q)) == 0 and len(ctx.match(q, z)) == 0
+    t = np.zeros((300, 32), np.uint8)        # all rows equal: d1 == d2 -> never kept
+    assert len(ctx.match(q, t)) == 0
+    t[150, 0] = 1                            # unique nearest... but 299 others at d = 0
+    assert np.array_equal(ctx.match(q, t), oracle.match(q, t))
+
+
+# ---------------------------------------------------------------------------- async slots
+def test_slot_pipeline_matches_sync(ctx, oracle):
+    import torch
+    import vxslam
+
+    frames = synth.make_frames(41, 2)
+    p = _orb_params(vxslam, 2000)
+    d = torch.from_numpy(frames).cuda()
+    torch.cuda.synchronize()
+    for s in range(2):
+        ctx.orb_extract_async(d[s].data_ptr(), 640, 480, 3, 640 * 3, s, p)
+    ctx.match_slots_async(0, 1)
+    m = ctx.match_fetch()
+    k0, d0 = ctx.orb_fetch(0)
+    k1, d1 = ctx.orb_fetch(1)
+    kc0, dc0 = oracle.orb_extract(frames[0], 2000, order=oracle.ORDER_RASTER)
+    kc1, dc1 = oracle.orb_extract(frames[1], 2000, order=oracle.ORDER_RASTER)
+    _assert_orb_equal(k0, d0, kc0, dc0)
+    _assert_orb_equal(k1, d1, kc1, dc1)
+    assert np.array_equal(m, oracle.match(dc0, dc1))
+    assert len(m) > 500  # consecutive frames really match
+
+
+# ---------------------------------------------------------------------------- LocalBA
+def _canon(q):
+    q = q.copy()
+    neg = q[:, 3] < 0
+    q[neg] *= -1
+    return q
+
+
+def _assert_ba_close(m_gpu, m_cpu, st_gpu, st_cpu):
+    assert st_gpu.status == st_cpu.status
+    assert st_gpu.n_window_kf == st_cpu.n_window_kf and st_gpu.n_landmarks == st_cpu.n_landmarks
+    assert st_gpu.iterations == st_cpu.iterations
+    assert list(st_gpu.obs[:st_gpu.iterations]) == list(st_cpu.obs[:st_cpu.iterations])  # no gate flips
+    for a, b in zip(st_gpu.cost[:st_gpu.iterations], st_cpu.cost[:st_cpu.iterations]):
+        assert abs(a - b) <= 1e-6 * abs(b)
+    pg, pc = m_gpu["kf_pose"].copy(), m_cpu["kf_pose"].copy()
+    pg[:, :4], pc[:, :4] = _canon(pg[:, :4]), _canon(pc[:, :4])
+    for a, b in ((pg, pc), (m_gpu["lm_pos"], m_cpu["lm_pos"])):
+        err = np.abs(a - b) / np.maximum(np.abs(b), 1e-3)
+        assert err.max() <= BA_RTOL, err.max()
+
+
+def _ba_case(ctx, oracle, m, opts_kw, ref=None):
+    import vxslam
+
+    mc = m.copy()
+    st_c = oracle.ba_optimize(mc, oracle.ba_options(**opts_kw), ref_kf_id=ref)
+    if st_c.status == 0 and st_c.gate_margin < 1e-8:
+        pytest.skip(f"gate margin {st_c.gate_margin} too small for a stable comparison")
+    mg = m.copy()
+    st_g = ctx.ba_optimize(mg, vxslam.default_ba_options(**opts_kw), ref_kf_id=ref)
+    _assert_ba_close(mg, mc, st_g, st_c)
+    return st_g
+
+
+@pytest.mark.parametrize("case", G.BA_CASES, ids=[c[0] for c in G.BA_CASES])
+def test_ba_golden_gpu(ctx, case):
+    import vxslam
+
+    g = np.load(os.path.join(HERE, "golden", "ba_golden.npz"))
+    name, seed, nk, nl, nold, hub, merr, iters = case
+    mp = synth.make_ba_map(seed, nk, nl, n_old_kf=nold)
+    st = ctx.ba_optimize(mp, vxslam.default_ba_options(window=nk, iters=iters, huber=hub, max_err=merr))
+    assert [st.iterations, st.n_window_kf, st.n_landmarks, st.status] == g[f"ba_{name}_stats"].tolist()
+    assert list(st.obs[:st.iterations]) == g[f"ba_{name}_obs"].tolist()
+    ref = {"kf_pose": g[f"ba_{name}_pose"], "lm_pos": g[f"ba_{name}_lm"]}
+    pg, pc = mp["kf_pose"].copy(), ref["kf_pose"].copy()
+    pg[:, :4], pc[:, :4] = _canon(pg[:, :4]), _canon(pc[:, :4])
+    assert (np.abs(pg - pc) / np.maximum(np.abs(pc), 1e-3)).max() <= BA_RTOL
+    assert (np.abs(mp["lm_pos"] - ref["lm_pos"]) / np.maximum(np.abs(ref["lm_pos"]), 1e-3)).max() <= BA_RTOL
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
+def test_ba_baseline_configs(ctx, oracle, cfg):
+    nk, nl, ns = synth.ba_config(cfg)
+    m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=ns * 2)
+    st = _ba_case(ctx, oracle, m, dict(window=nk))
+    assert st.status == 0 and st.iterations >= 2
+
+
+def test_ba_variants(ctx, oracle):
+    m = synth.make_ba_map(201, 12, 2500, n_old_kf=4)
+    _ba_case(ctx, oracle, m, dict(window=8))                                   # window < keyframes
+    _ba_case(ctx, oracle, m, dict(window=8), ref=int(m["kf_id"][-3]))         # older reference KF
+    _ba_case(ctx, oracle, m, dict(window=12, huber=1.5, max_err=4.0))         # Huber weights active
+    _ba_case(ctx, oracle, m, dict(window=12, iters=20))                       # stop rule / many iters
+    _ba_case(ctx, oracle, m, dict(window=12, min_pose=2000))                  # every pose step skipped
+    mm = m.copy()
+    mm["kf_has_cam"][-2] = 0                                                   # keyframe without camera
+    _ba_case(ctx, oracle, mm, dict(window=12))
+    st = _ba_case(ctx, oracle, m, dict(window=12), ref=int(m["kf_id"][0]))    # < 2 keyframes
+    assert st.status == 1
+
+
+def test_ba_plan_is_repeatable(ctx, oracle):
+    import vxslam
+
+    nk, nl, ns = synth.ba_config("C3")
+    m = synth.make_ba_map(77, nk, nl)
+    plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk))
+    outs = []
+    for _ in range(3):
+        plan.run_async()
+        mm = m.copy()
+        plan.fetch(mm)
+        outs.append(mm)
+    for o in outs[1:]:
+        assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
+    info = plan.info()
+    assert info["n_kf"] == nk and info["n_pose_obs"] > 50000

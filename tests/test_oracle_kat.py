@@ -1,0 +1,347 @@
+"""Known-answer tests of the CPU restatement (oracle/) — no GPU.
+
+The reference ships no tests or golden vectors for its hot path, so the
+oracle is pinned here by hand-derived answers and by independent re-derivations from the
+published definitions (FAST score by brute force over thresholds, blur against a float64
+convolution, the Gauss-Newton step against a numpy solve, ...).  ORB/BF parity against real
+OpenCV stays "unpinned": OpenCV is not available offline.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from vxslam import synth
+
+
+# ---------------------------------------------------------------------------- ORB pieces
+def test_quotas_and_level_sizes(oracle):
+    # SURVEY.md §8a A0 / A1.2 values (computeKeyPoints quotas, ORB layer sizes)
+    assert oracle.quotas(1000).tolist() == [217, 181, 151, 126, 105, 87, 73, 60]
+    assert oracle.quotas(2000).tolist() == [434, 362, 302, 251, 209, 175, 145, 122]
+    lw, lh, s = oracle.level_sizes(640, 480)
+    assert lw.tolist() == [640, 533, 444, 370, 309, 257, 214, 179]
+    assert lh.tolist() == [480, 400, 333, 278, 231, 193, 161, 134]
+    assert int((lw.astype(np.int64) * lh).sum()) == 950532
+    lw, lh, _ = oracle.level_sizes(1280, 960)
+    assert int((lw.astype(np.int64) * lh).sum()) == 3805248
+
+
+def test_gray_fixed_point(oracle):
+    img = np.zeros((8, 8, 3), np.uint8)
+    img[0, :] = (255, 0, 0)      # B
+    img[1, :] = (0, 255, 0)      # G
+    img[2, :] = (0, 0, 255)      # R
+    img[3, :] = (255, 255, 255)
+    img[4, :] = (10, 20, 30)
+    g = oracle.pyramid(img, levels=1)[0]
+    assert g[0, 0] == (255 * 1868 + 8192) >> 14 == 29
+    assert g[1, 0] == (255 * 9617 + 8192) >> 14 == 150
+    assert g[2, 0] == (255 * 4899 + 8192) >> 14 == 76
+    assert g[3, 0] == 255
+    assert g[4, 0] == (10 * 1868 + 20 * 9617 + 30 * 4899 + 8192) >> 14
+
+
+def _linear_exact_np(src, dw, dh):
+    """Independent numpy statement of resize(INTER_LINEAR_EXACT) for 8U."""
+    sh, sw = src.shape
+
+    def coeffs(s, d):
+        inv = d / s
+        scale = 1.0 / inv
+        f = scale * (np.arange(d) + 0.5) - 0.5
+        i = np.floor(f).astype(np.int64)
+        a = np.rint((f - i) * 256).astype(np.int64)
+        ofs = np.where(i < 0, 0, np.where(i >= s - 1, s - 1, i))
+        c1 = np.where((i >= 0) & (i < s - 1), a, 0)
+        return ofs, 256 - c1, c1
+
+    xo, xc0, xc1 = coeffs(sw, dw)
+    yo, yc0, yc1 = coeffs(sh, dh)
+    s = src.astype(np.int64)
+    hz = s[:, xo] * xc0 + s[:, np.minimum(xo + 1, sw - 1)] * xc1
+    v = hz[yo] * yc0[:, None] + hz[np.minimum(yo + 1, sh - 1)] * yc1[:, None]
+    return np.minimum((v + 32768) >> 16, 255).astype(np.uint8)
+
+
+def test_pyramid_matches_independent_fixed_point(oracle):
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (97, 131), dtype=np.uint8)
+    pyr = oracle.pyramid(img, levels=6)
+    for l in range(1, 6):
+        exp = _linear_exact_np(pyr[l - 1], pyr[l].shape[1], pyr[l].shape[0])
+        assert np.array_equal(pyr[l], exp), l
+    const = np.full((100, 120), 77, np.uint8)
+    for lv in oracle.pyramid(const):
+        assert (lv == 77).all()
+
+
+RING = [(0, 3), (1, 3), (2, 2), (3, 1), (3, 0), (3, -1), (2, -2), (1, -3), (0, -3), (-1, -3),
+        (-2, -2), (-3, -1), (-3, 0), (-3, 1), (-2, 2), (-1, 3)]
+
+
+def _fast_score_bruteforce(img, thr):
+    """Score = max t >= thr such that >= 9 contiguous ring pixels are all > v+t or all < v-t
+    (the definition cornerScore<16> implements); 0 when not a corner at thr."""
+    h, w = img.shape
+    im = img.astype(np.int32)
+    v = im[3:h - 3, 3:w - 3]
+    ring = np.stack([im[3 + dy:h - 3 + dy, 3 + dx:w - 3 + dx] for dx, dy in RING])
+    out = np.zeros((h, w), np.int32)
+    best = np.zeros_like(v)
+    for t in range(thr, 256):
+        for sign in (1, -1):
+            hit = (ring > v + t) if sign > 0 else (ring < v - t)
+            hh = np.concatenate([hit, hit[:8]])
+            run = np.zeros_like(v, dtype=bool)
+            for s in range(16):
+                run |= hh[s:s + 9].all(axis=0)
+            best = np.where(run, t, best)
+    out[3:h - 3, 3:w - 3] = best
+    return out
+
+
+def test_fast_score_matches_definition(oracle):
+    rng = np.random.default_rng(11)
+    for thr in (20, 5):
+        img = (rng.integers(0, 4, (36, 40)) * 60 + rng.integers(0, 30, (36, 40))).astype(np.uint8)
+        got = oracle.fast_scores(img, thr).astype(np.int32)
+        exp = _fast_score_bruteforce(img, thr)
+        assert np.array_equal(got, exp)
+
+
+def test_fast_corner_known_score(oracle):
+    img = np.full((32, 32), 200, np.uint8)
+    for k in range(9):  # 9 contiguous dark ring pixels, d = 100
+        dx, dy = RING[k]
+        img[16 + dy, 16 + dx] = 100
+    assert oracle.fast_scores(img, 20)[16, 16] == 99
+
+
+def test_fast_nms_is_strict_and_raster(oracle):
+    img = synth.make_texture(5, 90, 120)
+    sc = oracle.fast_scores(img, 20).astype(np.int32)
+    kps = oracle.fast_nms(img, 20)
+    keys = kps[:, 1] * 1000 + kps[:, 0]
+    assert (np.diff(keys) > 0).all()  # raster order
+    pad = np.pad(sc, 1)
+    exp = []
+    for y in range(img.shape[0]):
+        for x in range(img.shape[1]):
+            s = sc[y, x]
+            if s and all(s > pad[y + 1 + dy, x + 1 + dx] for dy in (-1, 0, 1) for dx in (-1, 0, 1)
+                         if dy or dx):
+                exp.append((x, y, s))
+    assert kps.tolist() == [list(e) for e in exp]
+
+
+def test_harris_independent(oracle):
+    rng = np.random.default_rng(2)
+    img = rng.integers(0, 256, (40, 40), dtype=np.uint8)
+    im = img.astype(np.int64)
+    for (x, y) in [(10, 10), (20, 17), (30, 25)]:
+        a = b = c = 0
+        for yy in range(y - 3, y + 4):
+            for xx in range(x - 3, x + 4):
+                ix = (im[yy, xx + 1] - im[yy, xx - 1]) * 2 + (im[yy - 1, xx + 1] - im[yy - 1, xx - 1]) + \
+                     (im[yy + 1, xx + 1] - im[yy + 1, xx - 1])
+                iy = (im[yy + 1, xx] - im[yy - 1, xx]) * 2 + (im[yy + 1, xx - 1] - im[yy - 1, xx - 1]) + \
+                     (im[yy + 1, xx + 1] - im[yy - 1, xx + 1])
+                a += ix * ix
+                b += iy * iy
+                c += ix * iy
+        f = np.float32
+        scale = f(1) / f(4 * 7 * 255.0)
+        s4 = scale * scale * scale * scale
+        exp = (f(a) * f(b) - f(c) * f(c) - f(0.04) * (f(a) + f(b)) * (f(a) + f(b))) * s4
+        assert oracle.harris(img, x, y) == exp
+
+
+def test_fast_atan2(oracle):
+    assert oracle.fast_atan2(0.0, 1.0) == 0.0
+    assert abs(oracle.fast_atan2(1.0, 0.0) - 90.0) < 1e-4
+    assert abs(oracle.fast_atan2(0.0, -1.0) - 180.0) < 1e-4
+    assert abs(oracle.fast_atan2(-1.0, 0.0) - 270.0) < 1e-4
+    assert abs(oracle.fast_atan2(1.0, 1.0) - 45.0) < 0.01
+    rng = np.random.default_rng(0)
+    for y, x in rng.normal(size=(200, 2)) * 1000:
+        ref = math.degrees(math.atan2(y, x)) % 360.0
+        got = oracle.fast_atan2(float(np.float32(y)), float(np.float32(x)))
+        d = abs(got - ref)
+        assert min(d, 360 - d) < 0.02
+
+
+def test_ic_angle_on_ramp(oracle):
+    x = np.arange(64)
+    img = np.tile((x * 3).astype(np.uint8), (64, 1))  # brightness grows with x -> angle 0
+    assert oracle.ic_angle(img, 32, 32) == 0.0
+    img_t = np.ascontiguousarray(img.T)                # grows with y -> 90 degrees
+    assert abs(oracle.ic_angle(img_t, 32, 32) - 90.0) < 1e-3
+
+
+def test_blur_constant_and_float64_reference(oracle):
+    const = np.full((40, 50), 123, np.uint8)
+    assert (oracle.blur_level(const) == 123).all()
+    from scipy import ndimage
+
+    rng = np.random.default_rng(9)
+    img = rng.integers(0, 256, (37, 45), dtype=np.uint8)
+    k = np.exp(-np.arange(-3, 4) ** 2 / 8.0)
+    k /= k.sum()
+    ref = ndimage.correlate1d(img.astype(np.float64), k, axis=1, mode="mirror")
+    ref = ndimage.correlate1d(ref, k, axis=0, mode="mirror")
+    got = oracle.blur_level(img).astype(np.int32)
+    assert np.abs(got - np.rint(ref)).max() <= 1
+
+
+def test_orb_stl_and_raster_orders_hold_the_same_set(oracle):
+    img = synth.make_frames(7, 1)[0]
+    a, da = oracle.orb_extract(img, 1000, order=oracle.ORDER_STL)
+    b, db = oracle.orb_extract(img, 1000, order=oracle.ORDER_RASTER)
+    assert len(a) == len(b)
+    ka = np.lexsort((a["x"], a["y"], a["octave"]))
+    kb = np.lexsort((b["x"], b["y"], b["octave"]))
+    assert np.array_equal(a[ka], b[kb])
+    assert np.array_equal(da[ka], db[kb])
+    # raster order inside each level, level-major
+    oc = b["octave"]
+    assert (np.diff(oc) >= 0).all()
+    for l in range(8):
+        s = b[oc == l]
+        key = s["y"].astype(np.float64) * 1e5 + s["x"]
+        assert (np.diff(key) > 0).all()
+
+
+def test_orb_quota_and_border(oracle):
+    img = synth.make_frames(8, 1)[0]
+    kps, desc = oracle.orb_extract(img, 1000)
+    q = oracle.quotas(1000)
+    counts = np.bincount(kps["octave"], minlength=8)
+    assert (counts <= q + 2).all() and counts.sum() >= 900
+    _, _, s = oracle.level_sizes(640, 480)
+    lw, lh, _ = oracle.level_sizes(640, 480)
+    for k in kps:
+        l = k["octave"]
+        xl = np.float32(k["x"]) * (np.float32(1) / s[l])
+        yl = np.float32(k["y"]) * (np.float32(1) / s[l])
+        assert 31 <= round(float(xl)) < lw[l] - 31 and 31 <= round(float(yl)) < lh[l] - 31
+    assert desc.shape == (len(kps), 32)
+
+
+# ---------------------------------------------------------------------------- matching
+def test_hamming_known_answers(oracle):
+    q = np.zeros((1, 32), np.uint8)
+    t = np.stack([np.full(32, 255, np.uint8), np.zeros(32, np.uint8), np.zeros(32, np.uint8)])
+    idx, dist = oracle.knn2(q, t)
+    assert dist.tolist() == [[0, 0]] and idx.tolist() == [[1, 2]]   # ties: lower train idx first
+    idx, dist = oracle.knn2(q, t[:1])
+    assert dist[0, 0] == 256 and idx[0, 1] == -1
+    assert len(oracle.match(q, t[:1])) == 0                         # knn.size() < 2 -> skipped
+    # ratio test: d1 < 0.8 * d2
+    t2 = np.zeros((2, 32), np.uint8)
+    t2[0, 0] = 0b1111          # d = 4
+    t2[1, :1] = 0b11111        # d = 5 -> 4 < 4.0 false
+    assert len(oracle.match(q, t2)) == 0
+    t2[1, 1] = 1               # d = 6 -> 4 < 4.8 true
+    m = oracle.match(q, t2)
+    assert m.tolist() == [(0, 0, 4.0)]
+
+
+def test_knn_bruteforce(oracle):
+    rng = np.random.default_rng(4)
+    q = rng.integers(0, 256, (50, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, (80, 32), dtype=np.uint8)
+    t[10] = t[70]  # planted tie
+    idx, dist = oracle.knn2(q, t)
+    bits = np.unpackbits(q[:, None, :] ^ t[None, :, :], axis=-1).sum(-1)
+    for i in range(len(q)):
+        order = np.lexsort((np.arange(len(t)), bits[i]))
+        assert idx[i].tolist() == order[:2].tolist()
+        assert dist[i].tolist() == bits[i][order[:2]].tolist()
+
+
+# ---------------------------------------------------------------------------- LocalBA
+def test_ba_noise_free_map_is_a_fixed_point(oracle):
+    m = synth.make_ba_map(1, 6, 400, noise_px=0.0, rot_deg=0.0, trans_m=0.0, lm_sigma=0.0,
+                          frac_outlier=0.0, frac_bad=0.0, n_old_kf=0)
+    before = m.copy()
+    st = oracle.ba_optimize(m, oracle.ba_options(window=6))
+    assert st.status == 0
+    assert np.abs(m["kf_pose"] - before["kf_pose"]).max() < 1e-9
+    assert np.abs(m["lm_pos"] - before["lm_pos"]).max() < 1e-9
+
+
+def _quat_to_mat(q):
+    return synth.quat_to_mat(np.asarray(q))
+
+
+def test_ba_pose_step_matches_numpy_gauss_newton_with_reference_sign(oracle):
+    """After one iteration the pose equals exp(dx) * T with dx = LDLT(J^T J + 1e-6 I)^-1 (-J^T e)
+    (local_ba.cpp:176-202): derived here independently in numpy."""
+    m = synth.make_ba_map(2, 3, 300, n_old_kf=0, frac_outlier=0.0, frac_bad=0.0, frac_single=0.0)
+    opts = oracle.ba_options(window=3, iters=1)
+    m0 = m.copy()
+    oracle.ba_optimize(m, opts)
+    fx, fy, cx, cy = m0["kf_intr"][0]
+    lm_index = {int(i): n for n, i in enumerate(m0["lm_id"])}
+    for k in range(3):
+        q, t = m0["kf_pose"][k, :4], m0["kf_pose"][k, 4:]
+        R = _quat_to_mat(q)
+        H = np.zeros((6, 6))
+        b = np.zeros(6)
+        for f in range(m0["kf_feat_ptr"][k], m0["kf_feat_ptr"][k + 1]):
+            if not (m0["feat_flags"][f] & 1) or (m0["feat_flags"][f] & 2):
+                continue
+            l = lm_index.get(int(m0["feat_lm_id"][f]))
+            if l is None or m0["lm_bad"][l]:
+                continue
+            pc = R @ m0["lm_pos"][l] + t
+            u = fx * pc[0] / pc[2] + cx
+            v = fy * pc[1] / pc[2] + cy
+            e = m0["feat_uv"][f] - np.array([u, v])
+            if np.linalg.norm(e) > 5.0:
+                continue
+            x, y, z = pc
+            Jp = np.array([[fx / z, 0, -fx * x / z ** 2], [0, fy / z, -fy * y / z ** 2]])
+            hat = np.array([[0, -z, y], [z, 0, -x], [-y, x, 0]])
+            J = Jp @ np.hstack([np.eye(3), -hat])
+            H += J.T @ J
+            b += -J.T @ e
+        dx = np.linalg.solve(H + 1e-6 * np.eye(6), b)
+        # Sophus exp(dx) * T
+        w = dx[3:]
+        th = np.linalg.norm(w)
+        K = np.array([[0, -w[2], w[1]], [w[2], 0, -w[0]], [-w[1], w[0], 0]])
+        Rd = np.eye(3) + math.sin(th) / th * K + (1 - math.cos(th)) / th ** 2 * K @ K
+        V = np.eye(3) + (1 - math.cos(th)) / th ** 2 * K + (th - math.sin(th)) / th ** 3 * K @ K
+        R_new = Rd @ R
+        t_new = Rd @ t + V @ dx[:3]
+        got_R = _quat_to_mat(m["kf_pose"][k, :4])
+        assert np.abs(got_R - R_new).max() < 1e-9
+        assert np.abs(m["kf_pose"][k, 4:] - t_new).max() < 1e-9
+
+
+def test_ba_window_selection_and_early_returns(oracle):
+    m = synth.make_ba_map(3, 8, 500, n_old_kf=4)
+    st = oracle.ba_optimize(m.copy(), oracle.ba_options(window=5))
+    assert st.status == 0 and st.n_window_kf == 5
+    # ref keyframe older than the newest: window ends at the ref id
+    ids = m["kf_id"]
+    st = oracle.ba_optimize(m.copy(), oracle.ba_options(window=5), ref_kf_id=int(ids[6]))
+    assert st.n_window_kf == 5
+    # only one keyframe <= ref -> no optimisation (keyframes.size() < 2)
+    mm = m.copy()
+    st = oracle.ba_optimize(mm, oracle.ba_options(window=5), ref_kf_id=int(ids[0]))
+    assert st.status == 1 and np.array_equal(mm["kf_pose"], m["kf_pose"])
+    # min_point_observations too high -> landmarks empty -> return
+    st = oracle.ba_optimize(m.copy(), oracle.ba_options(window=5, min_point=50))
+    assert st.status == 1
+
+
+def test_ba_reference_sign_diverges(oracle):
+    """The reference's step sign makes in-range residuals grow, so observations
+    leave the 5 px gate iteration after iteration: reproduce that behaviour, do not fix it."""
+    m = synth.make_ba_map(4, 10, 2000)
+    st = oracle.ba_optimize(m, oracle.ba_options(window=10))
+    obs = list(st.obs[:st.iterations])
+    assert st.iterations == 5 and all(a > b for a, b in zip(obs, obs[1:]))

@@ -1,0 +1,202 @@
+// match.hip — brute-force Hamming kNN-2 + ratio test on gfx950 (FeatureMatcher::Match drop-in).
+//
+// Replaces ORBMatcher::Match (core/feature/orb_matcher.cpp:11-43): BFMatcher(NORM_HAMMING)
+// knnMatch(desc_last, desc_curr, k = 2) then keep knn[0] when m1.distance < nn_ratio *
+// m2.distance.  OpenCV's top-K insertion keeps, per query, the two smallest (distance, train
+// index) pairs in lexicographic order (ties -> lower train index).  That order is
+// a total order, so the GPU splits the train set into chunks, keeps a per-(query, chunk) top-2
+// of packed keys (distance << 22 | train index) and merges chunks with the same min/med3
+// update — bit-identical to the sequential scan whatever the chunking.
+//
+//   k_knn_partial  one thread per query (32 B in 8 VGPRs), a chunk of train rows staged in LDS
+//                  and read as wave-uniform broadcasts; per pair 8 v_xor + 8 v_bcnt + 2 v_min/
+//                  v_med3: VALU-popcount bound.
+//   k_knn_merge    one block: merge chunk partials, ratio test, ordered compaction (ascending
+//                  query index) by block scan.
+#include "vx_internal.hpp"
+
+namespace vx {
+namespace {
+
+constexpr int kQB = 256;      // queries per block (one per thread)
+constexpr int kTC = 64;       // train rows per chunk
+constexpr int kMergeBlock = 1024;
+constexpr unsigned kNone = 0xffffffffu;
+
+__global__ __launch_bounds__(kQB) void k_knn_partial(const uint8_t* __restrict__ q,
+                                                     const int* __restrict__ nq_p, int nq_host,
+                                                     const uint8_t* __restrict__ t,
+                                                     const int* __restrict__ nt_p, int nt_host,
+                                                     int n_chunks_cap, uint2* __restrict__ partial,
+                                                     int q_stride) {
+    __shared__ uint4 st[kTC * 2];
+    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;  // device count clamped to capacity
+    const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
+    const int chunk = blockIdx.y;
+    const int t0 = chunk * kTC;
+    const int qi = blockIdx.x * kQB + threadIdx.x;
+    if (blockIdx.x * kQB >= nq || t0 >= nt) return;  // block-uniform
+    const int tn = min(kTC, nt - t0);
+    for (int i = threadIdx.x; i < tn * 2; i += kQB)
+        st[i] = reinterpret_cast<const uint4*>(t + (long long)t0 * 32)[i];
+    __syncthreads();
+    if (qi >= nq) return;
+    const uint4 a0 = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[0];
+    const uint4 a1 = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[1];
+    unsigned k1 = kNone, k2 = kNone;
+    for (int j = 0; j < tn; ++j) {
+        const uint4 b0 = st[2 * j], b1 = st[2 * j + 1];
+        unsigned d = __builtin_popcount(a0.x ^ b0.x);
+        d += __builtin_popcount(a0.y ^ b0.y);
+        d += __builtin_popcount(a0.z ^ b0.z);
+        d += __builtin_popcount(a0.w ^ b0.w);
+        d += __builtin_popcount(a1.x ^ b1.x);
+        d += __builtin_popcount(a1.y ^ b1.y);
+        d += __builtin_popcount(a1.z ^ b1.z);
+        d += __builtin_popcount(a1.w ^ b1.w);
+        const unsigned key = (d << 22) | (unsigned)(t0 + j);
+        k2 = max(min(k1, key), min(k2, max(k1, key)));  // second smallest of {k1, k2, key}
+        k1 = min(k1, key);
+    }
+    partial[(long long)chunk * q_stride + qi] = make_uint2(k1, k2);
+    (void)n_chunks_cap;
+}
+
+template <int NT>
+__device__ __forceinline__ int scan_excl(int v, int* sh, int& total) {
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < NT; o <<= 1) {
+        const int x = t >= o ? sh[t - o] : 0;
+        __syncthreads();
+        sh[t] += x;
+        __syncthreads();
+    }
+    total = sh[NT - 1];
+    const int incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(kMergeBlock) void k_knn_merge(const uint2* __restrict__ partial,
+                                                           const int* __restrict__ nq_p, int nq_host,
+                                                           const int* __restrict__ nt_p, int nt_host,
+                                                           int q_stride, float ratio,
+                                                           vx_match* __restrict__ out,
+                                                           int* __restrict__ out_count) {
+    __shared__ int sh[kMergeBlock];
+    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
+    const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
+    const int nchunks = (nt + kTC - 1) / kTC;
+    int written = 0;
+    for (int base = 0; base < nq; base += kMergeBlock) {
+        const int qi = base + threadIdx.x;
+        unsigned k1 = kNone, k2 = kNone;
+        if (qi < nq) {
+            for (int c = 0; c < nchunks; ++c) {
+                const uint2 p = partial[(long long)c * q_stride + qi];
+                k2 = max(min(k1, p.x), min(k2, max(k1, p.x)));
+                k1 = min(k1, p.x);
+                k2 = max(min(k1, p.y), min(k2, max(k1, p.y)));
+                k1 = min(k1, p.y);
+            }
+        }
+        int keep = 0;
+        if (qi < nq && k2 != kNone) {
+            const float d1 = (float)(k1 >> 22), d2 = (float)(k2 >> 22);
+            keep = d1 < ratio * d2;
+        }
+        int cnt;
+        const int pos = scan_excl<kMergeBlock>(keep, sh, cnt);
+        if (keep) {
+            vx_match m;
+            m.query_idx = qi;
+            m.train_idx = (int)(k1 & 0x3fffffu);
+            m.distance = (float)(k1 >> 22);
+            out[written + pos] = m;
+        }
+        written += cnt;
+    }
+    if (threadIdx.x == 0) *out_count = written;
+}
+
+int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt,
+                  const int* dnt, int nt_host, int q_cap, int t_cap, float ratio) {
+    const int n_chunks = (t_cap + kTC - 1) / kTC;
+    const int q_stride = q_cap;
+    VX_HIP(c, c->partial.ensure((size_t)n_chunks * q_stride * sizeof(uint2) + 16));
+    VX_HIP(c, c->matches.ensure((size_t)std::max(q_cap, 1) * sizeof(vx_match)));
+    VX_HIP(c, c->match_count.ensure(16));
+    c->match_cap = q_cap;
+    {
+        ProfScope ps(c, kStMatchPartial);
+        hipLaunchKernelGGL(k_knn_partial, dim3((q_cap + kQB - 1) / kQB, n_chunks), dim3(kQB), 0, c->stream, dq,
+                           dnq, nq_host, dt, dnt, nt_host, n_chunks, c->partial.as<uint2>(), q_stride);
+        VX_LAUNCH_CHECK(c, "k_knn_partial");
+    }
+    {
+        ProfScope ps(c, kStMatchMerge);
+        hipLaunchKernelGGL(k_knn_merge, dim3(1), dim3(kMergeBlock), 0, c->stream, c->partial.as<uint2>(), dnq,
+                           nq_host, dnt, nt_host, q_stride, ratio, c->matches.as<vx_match>(),
+                           c->match_count.as<int>());
+        VX_LAUNCH_CHECK(c, "k_knn_merge");
+    }
+    c->match_valid = true;
+    return VX_OK;
+}
+
+}  // namespace
+}  // namespace vx
+
+using namespace vx;
+
+extern "C" {
+
+int vx_match_slots_async(vx_ctx* c, int qs, int ts, float ratio) {
+    if (!c) return VX_ERR_INVALID;
+    if (qs < 0 || qs >= VX_MAX_SLOTS || ts < 0 || ts >= VX_MAX_SLOTS || !c->slots[qs].valid ||
+        !c->slots[ts].valid)
+        return set_error(c, VX_ERR_STATE, "match slots %d/%d hold no extraction", qs, ts);
+    const Slot& a = c->slots[qs];
+    const Slot& b = c->slots[ts];
+    return match_enqueue(c, a.desc.as<uint8_t>(), a.count.as<int>(), a.cap, b.desc.as<uint8_t>(),
+                         b.count.as<int>(), b.cap, a.cap, b.cap, ratio);
+}
+
+int vx_match_fetch(vx_ctx* c, vx_match* out, int cap, int* n_out) {
+    if (!c || !n_out) return VX_ERR_INVALID;
+    if (!c->match_valid) return set_error(c, VX_ERR_STATE, "no match enqueued");
+    int n = 0;
+    VX_HIP(c, hipMemcpyAsync(&n, c->match_count.p, sizeof n, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) prof_collect(c);
+    *n_out = n;
+    if (n > cap) return set_error(c, VX_ERR_CAPACITY, "need %d matches, cap %d", n, cap);
+    if (n > 0 && out) {
+        VX_HIP(c, hipMemcpyAsync(out, c->matches.p, (size_t)n * sizeof(vx_match), hipMemcpyDeviceToHost,
+                                 c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    return VX_OK;
+}
+
+int vx_match_knn2_ratio(vx_ctx* c, const uint8_t* q, int nq, const uint8_t* t, int nt, float ratio,
+                        vx_match* out, int cap, int* n_out) {
+    if (!c || !n_out) return VX_ERR_INVALID;
+    *n_out = 0;
+    if (nq < 0 || nt < 0) return set_error(c, VX_ERR_INVALID, "negative descriptor count");
+    if (nq == 0 || nt == 0) return VX_OK;  // desc1.empty() || desc2.empty() -> 0 (orb_matcher.cpp:18-20)
+    if (!q || !t) return set_error(c, VX_ERR_INVALID, "null descriptors");
+    if (nt > (1 << 22)) return set_error(c, VX_ERR_INVALID, "train set larger than 2^22 rows");
+    VX_HIP(c, hipSetDevice(c->device));
+    VX_HIP(c, c->mq.ensure((size_t)nq * 32));
+    VX_HIP(c, c->mt.ensure((size_t)nt * 32));
+    VX_HIP(c, hipMemcpyAsync(c->mq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, c->stream));
+    VX_HIP(c, hipMemcpyAsync(c->mt.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, c->stream));
+    int rc = match_enqueue(c, c->mq.as<uint8_t>(), nullptr, nq, c->mt.as<uint8_t>(), nullptr, nt, nq, nt, ratio);
+    if (rc) return rc;
+    return vx_match_fetch(c, out, cap, n_out);
+}
+
+}  // extern "C"

@@ -1,0 +1,943 @@
+// orb.hip — ORB feature extraction on gfx950 (FeatureExtractor::Extract drop-in).
+//
+// Replaces ORBExtractor::Extract (core/feature/orb_extractor.cpp:9-27), i.e.
+// cv::ORB::create(n, 1.2f, 8)->detectAndCompute(img, noArray(), kps, desc).  The pipeline
+//  is re-designed as a chain of wavefront kernels on one HIP stream:
+//
+//   k_gray            BGR(A)->gray level 0, fixed point (A.1)
+//   k_resize x (L-1)  INTER_LINEAR_EXACT pyramid, 8.8 / 16.16 fixed point (A.1)
+//   k_fast            all levels in one launch: full-width row bands staged in LDS with a 4 px
+//                     halo; FAST-9/16 corner test as 16-bit ring masks, cornerScore<16>, strict
+//                     3x3 NMS, border filter, ordered (raster) compaction by block scan, Harris
+//                     7x7 from the same LDS tile, per-level score histogram (A.3, A.4)
+//   k_blur            GaussianBlur 7x7 sigma 2, float separable, reflect-101, all levels (A.5)
+//   k_select          one workgroup per level: retainBest(2q) by FAST score via the histogram,
+//                     retainBest(q) by Harris via an exact 4-pass radix select; both keep the
+//                     OpenCV set {response >= k-th largest} in raster order (A.3)
+//   k_describe        one wavefront per keypoint: intensity-centroid angle (fastAtan2), rotated
+//                     BRIEF sampling of the blurred level, 256 comparisons packed by 4 ballots
+//                     into the 32-byte descriptor (A.4, A.6)
+//
+// Every integer stage is exact; float stages are compiled with -ffp-contract=off and follow the
+// OpenCV operation order, so results are bit-identical to the CPU restatement in oracle/.
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+#include "vx_internal.hpp"
+
+#include "orb_pattern_31.inc"
+
+namespace vx {
+namespace {
+
+constexpr int kBlock = 256;
+
+__constant__ signed char c_pattern[1024];
+__constant__ int c_umax[16];
+
+struct LevelArgs {
+    int L;
+    int lw[kMaxLevels], lh[kMaxLevels];
+    long long off[kMaxLevels];
+    float scale[kMaxLevels], inv_scale[kMaxLevels];
+    int quota[kMaxLevels];
+    int band_rows;
+    int nbands[kMaxLevels], band_base[kMaxLevels], band_cap[kMaxLevels];
+    long long cand_base[kMaxLevels];
+    int level_cap[kMaxLevels];
+    int fast_threshold, edge, out_cap;
+    // blur tiling
+    int btx[kMaxLevels], bty[kMaxLevels], bbase[kMaxLevels];
+    float gk[7];
+};
+
+// ------------------------------------------------------------------------------ gray
+__global__ void k_gray(const uint8_t* __restrict__ img, int W, int ch, long long stride,
+                       uint8_t* __restrict__ out) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= W) return;
+    const uint8_t* s = img + (long long)y * stride + (long long)x * ch;
+    uint8_t g;
+    if (ch == 1)
+        g = s[0];
+    else
+        g = (uint8_t)((s[0] * 1868 + s[1] * 9617 + s[2] * 4899 + (1 << 13)) >> 14);
+    out[(long long)y * W + x] = g;
+}
+
+// ------------------------------------------------------------------------------ resize
+__global__ void k_resize(const uint8_t* __restrict__ src, int sw, int sh, uint8_t* __restrict__ dst,
+                         int dw, const int4* __restrict__ xt, const int4* __restrict__ yt) {
+    const int x = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = blockIdx.y;
+    if (x >= dw) return;
+    const int4 cx = xt[x];
+    const int4 cy = yt[y];
+    const uint8_t* r0 = src + (long long)cy.x * sw;
+    const uint8_t* r1 = src + (long long)min(cy.x + 1, sh - 1) * sw;
+    const int x1 = min(cx.x + 1, sw - 1);
+    const uint32_t h0 = (uint32_t)(r0[cx.x] * cx.y + r0[x1] * cx.z);
+    const uint32_t h1 = (uint32_t)(r1[cx.x] * cx.y + r1[x1] * cx.z);
+    const uint32_t v = h0 * (uint32_t)cy.y + h1 * (uint32_t)cy.z;
+    dst[(long long)y * dw + x] = (uint8_t)min((v + 32768u) >> 16, 255u);
+}
+
+// ------------------------------------------------------------------------------ FAST
+// ring offsets (x, y), FAST_t<16> makeOffsets
+__device__ __forceinline__ int ring_dx(int k) {
+    const int t[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    return t[k];
+}
+__device__ __forceinline__ int ring_dy(int k) {
+    const int t[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    return t[k];
+}
+
+__device__ __forceinline__ bool has_run9(uint32_t m16) {
+    const uint32_t m = m16 | (m16 << 16);
+    uint32_t r = m & (m >> 1);   // runs >= 2
+    r &= r >> 2;                 // >= 4
+    r &= r >> 4;                 // >= 8
+    r &= m >> 8;                 // >= 9
+    return r != 0;
+}
+
+// FAST test + cornerScore<16>; returns 0 for non-corners.  t = tile base at the pixel.
+__device__ int fast_score(const uint8_t* t, int stride, int thr) {
+    const int v = t[0];
+    int p[16];
+    uint32_t bright = 0, dark = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        p[k] = t[ring_dy(k) * stride + ring_dx(k)];
+        bright |= (uint32_t)(p[k] > v + thr) << k;
+        dark |= (uint32_t)(p[k] < v - thr) << k;
+    }
+    if (!has_run9(bright) && !has_run9(dark)) return 0;
+    int d[25];
+#pragma unroll
+    for (int k = 0; k < 25; ++k) d[k] = v - p[k & 15];
+    int a0 = thr;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int a = min(d[k + 1], d[k + 2]);
+        a = min(a, d[k + 3]);
+        a = min(a, d[k + 4]);
+        a = min(a, d[k + 5]);
+        a = min(a, d[k + 6]);
+        a = min(a, d[k + 7]);
+        a = min(a, d[k + 8]);
+        a0 = max(a0, min(a, d[k]));
+        a0 = max(a0, min(a, d[k + 9]));
+    }
+    int b0 = -a0;
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        int b = max(d[k + 1], d[k + 2]);
+        b = max(b, d[k + 3]);
+        b = max(b, d[k + 4]);
+        b = max(b, d[k + 5]);
+        b = max(b, d[k + 6]);
+        b = max(b, d[k + 7]);
+        b = max(b, d[k + 8]);
+        b0 = min(b0, max(b, d[k]));
+        b0 = min(b0, max(b, d[k + 9]));
+    }
+    return -b0 - 1;
+}
+
+// HarrisResponses(blockSize 7, k 0.04f) from an LDS tile; t = tile base at the keypoint.
+__device__ float harris_tile(const uint8_t* t, int s) {
+    int a = 0, b = 0, c = 0;
+    for (int i = -3; i <= 3; ++i)
+#pragma unroll
+        for (int j = -3; j <= 3; ++j) {
+            const uint8_t* p = t + i * s + j;
+            const int Ix = (p[1] - p[-1]) * 2 + (p[-s + 1] - p[-s - 1]) + (p[s + 1] - p[s - 1]);
+            const int Iy = (p[s] - p[-s]) * 2 + (p[s - 1] - p[-s - 1]) + (p[s + 1] - p[-s + 1]);
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+    const float s4 = scale * scale * scale * scale;
+    const float fa = (float)a, fb = (float)b, fc = (float)c;
+    return (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+}
+
+template <int NT>
+__device__ __forceinline__ int block_exclusive_scan(int v, int* sh, int& total) {
+    // sh: NT ints of scratch. Hillis-Steele in LDS (NT <= 1024).
+    const int t = threadIdx.x;
+    sh[t] = v;
+    __syncthreads();
+    for (int o = 1; o < NT; o <<= 1) {
+        const int x = t >= o ? sh[t - o] : 0;
+        __syncthreads();
+        sh[t] += x;
+        __syncthreads();
+    }
+    total = sh[NT - 1];
+    const int incl = sh[t];
+    __syncthreads();
+    return incl - v;
+}
+
+struct CandRec {  // 16 B per FAST candidate / selected keypoint
+    unsigned xy;  // x | y << 16
+    int score;
+    float harris;
+    int pad;
+};
+
+__global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr, LevelArgs a,
+                                                 CandRec* __restrict__ cand,
+                                                 int* __restrict__ band_count,
+                                                 int* __restrict__ hist) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int b = blockIdx.x;
+    int l = 0;
+    while (l + 1 < a.L && b >= a.band_base[l + 1]) ++l;
+    const int W = a.lw[l], H = a.lh[l];
+    const uint8_t* img = pyr + a.off[l];
+    const int R = a.band_rows;
+    const int y0 = (b - a.band_base[l]) * R;
+    const int TW = W + 8;
+    uint8_t* tile = smem;                                 // (R+8) x TW
+    uint8_t* sc = smem + (R + 8) * TW;                     // (R+2) x W scores
+    int* shist = (int*)(smem + (((R + 8) * TW + (R + 2) * W + 15) & ~15));  // 256
+    int* sscan = shist + 256;                              // kBlock
+    const int tid = threadIdx.x;
+
+    for (int i = tid; i < 256; i += kBlock) shist[i] = 0;
+    for (int i = tid; i < (R + 8) * TW; i += kBlock) {
+        const int r = i / TW, c = i - r * TW;
+        const int gy = min(max(y0 - 4 + r, 0), H - 1);
+        const int gx = min(max(c - 4, 0), W - 1);
+        tile[i] = img[(long long)gy * W + gx];
+    }
+    __syncthreads();
+    const int thr = a.fast_threshold;
+    for (int i = tid; i < (R + 2) * W; i += kBlock) {
+        const int rr = i / W, x = i - rr * W;
+        const int y = y0 - 1 + rr;
+        int s = 0;
+        if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3)
+            s = fast_score(tile + (rr + 3) * TW + x + 4, TW, thr);
+        sc[i] = (uint8_t)s;
+    }
+    __syncthreads();
+    // NMS + border filter over the band's R x W pixels, contiguous raster chunk per thread.
+    const int npx = R * W;
+    const int chunk = (npx + kBlock - 1) / kBlock;
+    const int p0 = tid * chunk, p1 = min(p0 + chunk, npx);
+    const int e = a.edge;
+    auto is_cand = [&](int p, int& sout) -> bool {
+        const int r = p / W, x = p - r * W;
+        const int y = y0 + r;
+        if (y >= H || y < e || y >= H - e || x < e || x >= W - e) return false;
+        const uint8_t* q = sc + (r + 1) * W + x;
+        const int s = q[0];
+        if (!s) return false;
+        if (!(s > q[-1] && s > q[1] && s > q[-W - 1] && s > q[-W] && s > q[-W + 1] &&
+              s > q[W - 1] && s > q[W] && s > q[W + 1]))
+            return false;
+        sout = s;
+        return true;
+    };
+    int cnt = 0;
+    for (int p = p0; p < p1; ++p) {
+        int s;
+        cnt += is_cand(p, s);
+    }
+    int total;
+    int pos = block_exclusive_scan<kBlock>(cnt, sscan, total);
+    CandRec* out = cand + a.cand_base[l] + (long long)(b - a.band_base[l]) * a.band_cap[l];
+    for (int p = p0; p < p1; ++p) {
+        int s;
+        if (!is_cand(p, s)) continue;
+        const int r = p / W, x = p - r * W;
+        CandRec c;
+        c.xy = (unsigned)x | ((unsigned)(y0 + r) << 16);
+        c.score = s;
+        c.harris = harris_tile(tile + (r + 4) * TW + x + 4, TW);
+        c.pad = 0;
+        out[pos++] = c;
+        atomicAdd(&shist[s], 1);
+    }
+    if (tid == 0) band_count[b] = total;
+    __syncthreads();
+    for (int i = tid; i < 256; i += kBlock)
+        if (shist[i]) atomicAdd(&hist[l * 256 + i], shist[i]);
+}
+
+// ------------------------------------------------------------------------------ blur
+__global__ __launch_bounds__(kBlock) void k_blur(const uint8_t* __restrict__ pyr,
+                                                 uint8_t* __restrict__ blur, LevelArgs a) {
+    constexpr int TXo = 64, TYo = 16;
+    __shared__ uint8_t sin_[(TYo + 6) * (TXo + 6)];
+    __shared__ float srow[(TYo + 6) * TXo];
+    const int b = blockIdx.x;
+    int l = 0;
+    while (l + 1 < a.L && b >= a.bbase[l + 1]) ++l;
+    const int W = a.lw[l], H = a.lh[l];
+    const int t = b - a.bbase[l];
+    const int tx = t % a.btx[l], ty = t / a.btx[l];
+    const int x0 = tx * TXo, y0 = ty * TYo;
+    const uint8_t* img = pyr + a.off[l];
+    auto refl = [](int p, int n) {
+        if (n == 1) return 0;
+        while (p < 0 || p >= n) {
+            if (p < 0) p = -p;
+            if (p >= n) p = 2 * n - 2 - p;
+        }
+        return p;
+    };
+    for (int i = threadIdx.x; i < (TYo + 6) * (TXo + 6); i += kBlock) {
+        const int r = i / (TXo + 6), c = i - r * (TXo + 6);
+        sin_[i] = img[(long long)refl(y0 - 3 + r, H) * W + refl(x0 - 3 + c, W)];
+    }
+    __syncthreads();
+    const float k0 = a.gk[0], k1 = a.gk[1], k2 = a.gk[2], k3 = a.gk[3], k4 = a.gk[4],
+                k5 = a.gk[5], k6 = a.gk[6];
+    for (int i = threadIdx.x; i < (TYo + 6) * TXo; i += kBlock) {
+        const int r = i / TXo, c = i - r * TXo;
+        const uint8_t* p = sin_ + r * (TXo + 6) + c;
+        float s = k0 * (float)p[0];
+        s += k1 * (float)p[1];
+        s += k2 * (float)p[2];
+        s += k3 * (float)p[3];
+        s += k4 * (float)p[4];
+        s += k5 * (float)p[5];
+        s += k6 * (float)p[6];
+        srow[i] = s;
+    }
+    __syncthreads();
+    uint8_t* out = blur + a.off[l];
+    for (int i = threadIdx.x; i < TYo * TXo; i += kBlock) {
+        const int r = i / TXo, c = i - r * TXo;
+        const int x = x0 + c, y = y0 + r;
+        if (x >= W || y >= H) continue;
+        const float* q = srow + (r + 3) * TXo + c;
+        float s = k3 * q[0] + 0.0f;
+        s += k4 * (q[TXo] + q[-TXo]);
+        s += k5 * (q[2 * TXo] + q[-2 * TXo]);
+        s += k6 * (q[3 * TXo] + q[-3 * TXo]);
+        const int v = __float2int_rn(s);
+        out[(long long)y * W + x] = (uint8_t)min(255, max(0, v));
+    }
+}
+
+// ------------------------------------------------------------------------------ select
+__device__ __forceinline__ unsigned f2key(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(unsigned k) {
+    const unsigned u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    return __uint_as_float(u);
+}
+
+constexpr int kSelBlock = 1024;
+
+__global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict__ cand,
+                                                      const int* __restrict__ band_count,
+                                                      const int* __restrict__ hist, LevelArgs a,
+                                                      CandRec* __restrict__ stage,
+                                                      int* __restrict__ level_count) {
+    __shared__ int sscan[kSelBlock];
+    __shared__ int sband[1024 + 1];
+    __shared__ int sh[257];
+    __shared__ int s_misc[8];
+    const int l = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int nb = a.nbands[l];
+    const CandRec* c0 = cand + a.cand_base[l];
+    CandRec* kept = stage + 2 * a.cand_base[l];                 // retainBest(2q) result
+    CandRec* fin = stage + 2 * a.cand_base[l] + a.level_cap[l]; // retainBest(q) result
+    // band prefix (nb <= 1024 checked on the host)
+    int tot;
+    {
+        const int v = tid < nb ? band_count[a.band_base[l] + tid] : 0;
+        const int ex = block_exclusive_scan<kSelBlock>(v, sscan, tot);
+        if (tid < nb) sband[tid] = ex;
+        if (tid == 0) sband[nb] = tot;
+    }
+    __syncthreads();
+    const int n = tot;
+    const int q = a.quota[l];
+    const int k1 = 2 * q;
+    // ---- retainBest(k1) by FAST score: threshold from the level histogram
+    if (tid == 0) s_misc[0] = 0;
+    if (tid < 256) sh[tid] = hist[l * 256 + tid];
+    __syncthreads();
+    int thr1 = 0;
+    bool keep_none = false;
+    if (k1 == 0) {
+        keep_none = n > 0;  // retainBest(0) clears
+    } else if (n > k1) {
+        // suffix sums: cum[s] = sum_{b >= s} hist[b]; thr1 = max s with cum[s] >= k1
+        if (tid < 256) sscan[tid] = sh[255 - tid];
+        __syncthreads();
+        for (int o = 1; o < 256; o <<= 1) {
+            const int x = (tid < 256 && tid >= o) ? sscan[tid - o] : 0;
+            __syncthreads();
+            if (tid < 256) sscan[tid] += x;
+            __syncthreads();
+        }
+        // sscan[i] = cum[255 - i]; find smallest i with cum >= k1 -> s = 255 - i
+        if (tid < 256) {
+            const bool ok = sscan[tid] >= k1;
+            const bool prev = tid > 0 ? sscan[tid - 1] >= k1 : false;
+            if (ok && !prev) s_misc[0] = 255 - tid;
+        }
+        __syncthreads();
+        thr1 = s_misc[0];
+        __syncthreads();
+    }
+    // ---- gather kept candidates in raster order
+    int K1 = 0;
+    if (!keep_none) {
+        for (int base = 0; base < n; base += kSelBlock) {
+            const int j = base + tid;
+            CandRec r{};
+            int f = 0;
+            if (j < n) {
+                int lo = 0, hi = nb - 1;  // band with sband[bi] <= j < sband[bi+1]
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (sband[mid] <= j) lo = mid; else hi = mid - 1;
+                }
+                r = c0[(long long)lo * a.band_cap[l] + (j - sband[lo])];
+                f = r.score >= thr1;
+            }
+            int cnt;
+            const int pos = block_exclusive_scan<kSelBlock>(f, sscan, cnt);
+            if (f) kept[K1 + pos] = r;
+            K1 += cnt;
+        }
+    }
+    __syncthreads();
+    // ---- retainBest(q) by Harris
+    int K2 = 0;
+    if (q > 0 && K1 > 0) {
+        float thr2 = -INFINITY;
+        if (K1 > q) {
+            // exact k-th largest (k = q) of the float keys: 4-pass radix select, 8 bits per pass
+            unsigned prefix = 0, mask = 0;
+            int k = q;
+            for (int shift = 24; shift >= 0; shift -= 8) {
+                if (tid < 256) sh[tid] = 0;
+                __syncthreads();
+                for (int j = tid; j < K1; j += kSelBlock) {
+                    const unsigned key = f2key(kept[j].harris);
+                    if ((key & mask) == prefix) atomicAdd(&sh[(key >> shift) & 255], 1);
+                }
+                __syncthreads();
+                // descending digit suffix sums
+                if (tid < 256) sscan[tid] = sh[255 - tid];
+                __syncthreads();
+                for (int o = 1; o < 256; o <<= 1) {
+                    const int x = (tid < 256 && tid >= o) ? sscan[tid - o] : 0;
+                    __syncthreads();
+                    if (tid < 256) sscan[tid] += x;
+                    __syncthreads();
+                }
+                if (tid < 256) {
+                    const bool ok = sscan[tid] >= k;
+                    const bool prev = tid > 0 ? sscan[tid - 1] >= k : false;
+                    if (ok && !prev) {
+                        s_misc[1] = 255 - tid;                         // digit
+                        s_misc[2] = tid > 0 ? sscan[tid - 1] : 0;      // count above the digit
+                    }
+                }
+                __syncthreads();
+                const unsigned digit = (unsigned)s_misc[1];
+                k -= s_misc[2];
+                prefix |= digit << shift;
+                mask |= 255u << shift;
+                __syncthreads();
+            }
+            thr2 = key2f(prefix);
+        }
+        for (int base = 0; base < K1; base += kSelBlock) {
+            const int j = base + tid;
+            CandRec r{};
+            int f = 0;
+            if (j < K1) {
+                r = kept[j];
+                f = r.harris >= thr2;
+            }
+            int cnt;
+            const int pos = block_exclusive_scan<kSelBlock>(f, sscan, cnt);
+            if (f) fin[K2 + pos] = r;
+            K2 += cnt;
+        }
+    }
+    if (tid == 0) level_count[l] = K2;
+}
+
+// ------------------------------------------------------------------------------ describe
+__device__ __forceinline__ float ocv_fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
+    const float p3 = -0.3258083974640975f * (float)(180 / M_PI);
+    const float p5 = 0.1555786518463281f * (float)(180 / M_PI);
+    const float p7 = -0.04432655554792128f * (float)(180 / M_PI);
+    const float ax = fabsf(x), ay = fabsf(y);
+    float r, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        r = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        r = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) r = 180.f - r;
+    if (y < 0) r = 360.f - r;
+    return r;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__ pyr,
+                                                     const uint8_t* __restrict__ blur,
+                                                     const CandRec* __restrict__ stage,
+                                                     const int* __restrict__ level_count,
+                                                     LevelArgs a, vx_keypoint* __restrict__ kp,
+                                                     uint8_t* __restrict__ desc,
+                                                     int* __restrict__ slot_count) {
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    int total = 0, l = -1, j = 0;
+    for (int i = 0; i < a.L; ++i) {
+        const int c = level_count[i];
+        if (l < 0 && w < total + c) {
+            l = i;
+            j = w - total;
+        }
+        total += c;
+    }
+    if (w == 0 && lane == 0) {
+        slot_count[0] = total;
+        slot_count[1] = total > a.out_cap;
+    }
+    if (l < 0 || w >= a.out_cap) return;
+    const CandRec r = stage[2 * a.cand_base[l] + a.level_cap[l] + j];
+    const int W = a.lw[l];
+    const int xl = (int)(r.xy & 0xffffu), yl = (int)(r.xy >> 16);
+    const uint8_t* img = pyr + a.off[l];
+    // ICAngles (half_k 15): lane v+15 sums row v of the circular patch
+    int m10 = 0, m01 = 0;
+    if (lane < 31) {
+        const int v = lane - 15;
+        const int d = c_umax[v < 0 ? -v : v];
+        const uint8_t* row = img + (long long)(yl + v) * W + xl;
+        int s = 0, su = 0;
+        for (int u = -d; u <= d; ++u) {
+            const int p = row[u];
+            s += p;
+            su += u * p;
+        }
+        m10 = su;
+        m01 = v * s;
+    }
+    m10 = wave_sum(m10);
+    m01 = wave_sum(m01);
+    const float angle = ocv_fast_atan2((float)m01, (float)m10);
+    // computeOrbDescriptors
+    const float sc = a.scale[l];
+    const float px = (float)xl * sc, py = (float)yl * sc;
+    const float inv = a.inv_scale[l];
+    const int cx = __float2int_rn(px * inv), cy = __float2int_rn(py * inv);
+    float ang = angle;
+    ang *= (float)(M_PI / 180.f);
+    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+    const uint8_t* ctr = blur + a.off[l] + (long long)cy * W + cx;
+    unsigned long long words[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int bit = lane + 64 * s;
+        int v[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int pi = 2 * bit + e;
+            const float qx = (float)c_pattern[2 * pi], qy = (float)c_pattern[2 * pi + 1];
+            const float x = qx * ca - qy * sa;
+            const float y = qx * sa + qy * ca;
+            v[e] = ctr[(long long)__float2int_rn(y) * W + __float2int_rn(x)];
+        }
+        words[s] = __ballot(v[0] < v[1]);
+    }
+    const long long o = (long long)w;
+    if (lane < 4) {
+        const unsigned long long wv = lane == 0 ? words[0] : lane == 1 ? words[1] : lane == 2 ? words[2] : words[3];
+        reinterpret_cast<unsigned long long*>(desc + o * 32)[lane] = wv;
+    }
+    if (lane == 0) {
+        vx_keypoint k;
+        k.x = px;
+        k.y = py;
+        k.response = r.harris;
+        k.angle = angle;
+        k.octave = l;
+        kp[o] = k;
+    }
+}
+
+// ------------------------------------------------------------------------------ host side
+inline int cv_round_host(double v) { return (int)std::nearbyint(v); }
+inline int cv_floor_host(double v) { int i = (int)v; return i - (i > v); }
+inline int cv_ceil_host(double v) { int i = (int)v; return i + (i < v); }
+
+void linear_table(int src, int dst, std::vector<int4>& t) {
+    t.resize(dst);
+    const double inv = (double)dst / (double)src;
+    const double scale = 1.0 / inv;
+    for (int d = 0; d < dst; ++d) {
+        const double f = scale * ((double)d + 0.5) - 0.5;
+        const int i = cv_floor_host(f);
+        if (i >= 0 && src > 1) {
+            if (i < src - 1) {
+                const int al = cv_round_host((f - (double)i) * 256.0);
+                t[d] = make_int4(i, 256 - al, al, 0);
+            } else {
+                t[d] = make_int4(src - 1, 256, 0, 0);
+            }
+        } else {
+            t[d] = make_int4(0, 256, 0, 0);
+        }
+    }
+}
+
+// (float) of getGaussianKernelBitExact(7, sigma 2)
+void gauss_taps(float k[7]) {
+    double v[3], sum = 0;
+    for (int i = 0, x = -6; i < 3; ++i, x += 2) {
+        v[i] = std::exp((double)(x * x) * (-0.125 / 4.0));
+        sum += v[i];
+    }
+    sum = sum * 2 + 1;
+    const double mul = 1.0 / sum;
+    for (int i = 0; i < 3; ++i) k[i] = k[6 - i] = (float)(v[i] * mul);
+    k[3] = (float)(1.0 * mul);
+}
+
+bool g_constants_uploaded[64] = {false};
+
+int upload_constants(vx_ctx* c) {
+    if (c->device >= 0 && c->device < 64 && g_constants_uploaded[c->device]) return VX_OK;
+    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kBitPattern31, sizeof(kBitPattern31)));
+    int umax[16] = {0};
+    const int half = 15;
+    const int vmax = cv_floor_host(half * std::sqrt(2.f) / 2 + 1);
+    const int vmin = cv_ceil_host(half * std::sqrt(2.f) / 2);
+    for (int v = 0; v <= vmax; ++v) umax[v] = cv_round_host(std::sqrt((double)half * half - v * v));
+    for (int v = half, v0 = 0; v >= vmin; --v) {
+        while (umax[v0] == umax[v0 + 1]) ++v0;
+        umax[v] = v0;
+        ++v0;
+    }
+    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, sizeof(umax)));
+    if (c->device >= 0 && c->device < 64) g_constants_uploaded[c->device] = true;
+    return VX_OK;
+}
+
+LevelArgs level_args(const OrbGeometry& g) {
+    LevelArgs a;
+    std::memset(&a, 0, sizeof a);
+    a.L = g.L;
+    for (int l = 0; l < g.L; ++l) {
+        a.lw[l] = g.lw[l];
+        a.lh[l] = g.lh[l];
+        a.off[l] = g.off[l];
+        a.scale[l] = g.scale[l];
+        a.inv_scale[l] = g.inv_scale[l];
+        a.quota[l] = g.quota[l];
+        a.nbands[l] = g.nbands[l];
+        a.band_base[l] = g.band_base[l];
+        a.band_cap[l] = g.band_cap[l];
+        a.cand_base[l] = g.cand_base[l];
+        a.level_cap[l] = g.level_cap[l];
+    }
+    a.band_rows = g.band_rows;
+    a.fast_threshold = std::min(std::max(g.p.fast_threshold, 0), 255);
+    a.edge = g.p.edge_threshold;
+    a.out_cap = g.out_cap;
+    int bb = 0;
+    for (int l = 0; l < g.L; ++l) {
+        a.btx[l] = (g.lw[l] + 63) / 64;
+        a.bty[l] = (g.lh[l] + 15) / 16;
+        a.bbase[l] = bb;
+        bb += a.btx[l] * a.bty[l];
+    }
+    gauss_taps(a.gk);
+    return a;
+}
+
+int blur_blocks(const LevelArgs& a) {
+    int n = 0;
+    for (int l = 0; l < a.L; ++l) n += a.btx[l] * a.bty[l];
+    return n;
+}
+
+bool same_params(const vx_orb_params& x, const vx_orb_params& y) {
+    return x.n_features == y.n_features && x.scale_factor == y.scale_factor &&
+           x.n_levels == y.n_levels && x.fast_threshold == y.fast_threshold &&
+           x.edge_threshold == y.edge_threshold;
+}
+
+int validate_params(vx_ctx* c, const vx_orb_params* p, int w, int h) {
+    if (!p) return set_error(c, VX_ERR_INVALID, "null params");
+    if (p->n_levels < 1 || p->n_levels > kMaxLevels)
+        return set_error(c, VX_ERR_INVALID, "n_levels must be in [1, %d]", kMaxLevels);
+    if (!(p->scale_factor > 1.0f)) return set_error(c, VX_ERR_INVALID, "scale_factor must be > 1");
+    if (p->n_features < 0) return set_error(c, VX_ERR_INVALID, "n_features < 0");
+    if (p->edge_threshold < 19)
+        return set_error(c, VX_ERR_INVALID, "edge_threshold must be >= 19 (descriptor footprint)");
+    if (w < 1 || h < 1 || w > 4096 || h > 4096)
+        return set_error(c, VX_ERR_INVALID, "image size %dx%d outside [1, 4096]", w, h);
+    return VX_OK;
+}
+
+}  // namespace
+
+int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
+    int rc = validate_params(c, p, w, h);
+    if (rc) return rc;
+    if (c->geo_valid && c->geo.W == w && c->geo.H == h && same_params(c->geo.p, *p)) return VX_OK;
+    VX_HIP(c, hipSetDevice(c->device));
+    rc = upload_constants(c);
+    if (rc) return rc;
+    OrbGeometry g;
+    g.W = w;
+    g.H = h;
+    g.p = *p;
+    g.L = p->n_levels;
+    // level geometry (ORB_Impl::detectAndCompute): s_l = (float)pow((double)scaleFactor, l)
+    const double sf = (double)p->scale_factor;
+    int64_t off = 0;
+    for (int l = 0; l < g.L; ++l) {
+        const float s = (float)std::pow(sf, (double)l);
+        const float inv = 1.0f / s;
+        g.scale[l] = s;
+        g.inv_scale[l] = inv;
+        g.lw[l] = std::max(1, (int)std::nearbyintf((float)w * inv));
+        g.lh[l] = std::max(1, (int)std::nearbyintf((float)h * inv));
+        g.off[l] = off;
+        off += ((int64_t)g.lw[l] * g.lh[l] + 255) & ~int64_t(255);
+    }
+    g.pyr_bytes = off;
+    // quotas (computeKeyPoints)
+    {
+        const float factor = (float)(1.0 / sf);
+        float nd = (float)p->n_features * (1 - factor) /
+                   (1 - (float)std::pow((double)factor, (double)g.L));
+        int sum = 0;
+        for (int l = 0; l < g.L - 1; ++l) {
+            g.quota[l] = (int)std::nearbyintf(nd);
+            sum += g.quota[l];
+            nd *= factor;
+        }
+        g.quota[g.L - 1] = std::max(p->n_features - sum, 0);
+    }
+    // resize tables
+    std::vector<int4> all, t;
+    for (int l = 1; l < g.L; ++l) {
+        linear_table(g.lw[l - 1], g.lw[l], t);
+        g.xtab[l] = (int64_t)all.size();
+        all.insert(all.end(), t.begin(), t.end());
+        linear_table(g.lh[l - 1], g.lh[l], t);
+        g.ytab[l] = (int64_t)all.size();
+        all.insert(all.end(), t.begin(), t.end());
+    }
+    g.tab_entries = (int64_t)all.size();
+    // FAST bands
+    g.band_rows = 8;
+    int bands = 0;
+    int64_t cb = 0;
+    g.max_w = 0;
+    for (int l = 0; l < g.L; ++l) {
+        g.nbands[l] = (g.lh[l] + g.band_rows - 1) / g.band_rows;
+        if (g.nbands[l] > 1024) return set_error(c, VX_ERR_INVALID, "too many bands");
+        g.band_base[l] = bands;
+        bands += g.nbands[l];
+        g.band_cap[l] = (g.band_rows / 2 + 1) * (g.lw[l] / 2 + 1);
+        g.level_cap[l] = g.band_cap[l] * g.nbands[l];
+        g.cand_base[l] = cb;
+        cb += g.level_cap[l];
+        g.max_w = std::max(g.max_w, g.lw[l]);
+    }
+    g.total_bands = bands;
+    g.cand_total = cb;
+    g.out_cap = 2 * p->n_features + 256;
+
+    VX_HIP(c, c->tabs.ensure(std::max<int64_t>(1, g.tab_entries) * sizeof(int4)));
+    if (!all.empty())
+        VX_HIP(c, hipMemcpy(c->tabs.p, all.data(), all.size() * sizeof(int4), hipMemcpyHostToDevice));
+    VX_HIP(c, c->pyr.ensure(g.pyr_bytes));
+    VX_HIP(c, c->blur.ensure(g.pyr_bytes));
+    VX_HIP(c, c->cand.ensure(g.cand_total * sizeof(CandRec)));
+    VX_HIP(c, c->stage.ensure(2 * g.cand_total * sizeof(CandRec)));
+    VX_HIP(c, c->band_count.ensure(bands * sizeof(int)));
+    VX_HIP(c, c->hist.ensure(g.L * 256 * sizeof(int)));
+    VX_HIP(c, c->level_count.ensure(kMaxLevels * sizeof(int)));
+    for (auto& s : c->slots) {
+        s.valid = false;
+        VX_HIP(c, s.kp.ensure((size_t)g.out_cap * sizeof(vx_keypoint)));
+        VX_HIP(c, s.desc.ensure((size_t)g.out_cap * 32));
+        VX_HIP(c, s.count.ensure(16));
+        s.cap = g.out_cap;
+    }
+    c->geo = g;
+    c->geo_valid = true;
+    return VX_OK;
+}
+
+static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t stride, int slot) {
+    const OrbGeometry& g = c->geo;
+    const LevelArgs a = level_args(g);
+    uint8_t* pyr = c->pyr.as<uint8_t>();
+    Slot& s = c->slots[slot];
+    {
+        ProfScope ps(c, kStGray);
+        hipLaunchKernelGGL(k_gray, dim3((g.W + kBlock - 1) / kBlock, g.H), dim3(kBlock), 0, c->stream,
+                           d_img, g.W, channels, (long long)stride, pyr);
+        VX_LAUNCH_CHECK(c, "k_gray");
+    }
+    {
+        ProfScope ps(c, kStResize);
+        const int4* tabs = c->tabs.as<int4>();
+        for (int l = 1; l < g.L; ++l) {
+            hipLaunchKernelGGL(k_resize, dim3((g.lw[l] + kBlock - 1) / kBlock, g.lh[l]), dim3(kBlock), 0,
+                               c->stream, pyr + g.off[l - 1], g.lw[l - 1], g.lh[l - 1], pyr + g.off[l],
+                               g.lw[l], tabs + g.xtab[l], tabs + g.ytab[l]);
+            VX_LAUNCH_CHECK(c, "k_resize");
+        }
+    }
+    VX_HIP(c, hipMemsetAsync(c->hist.p, 0, g.L * 256 * sizeof(int), c->stream));
+    {
+        ProfScope ps(c, kStFast);
+        const int R = g.band_rows;
+        const size_t lds = (((size_t)(R + 8) * (g.max_w + 8) + (size_t)(R + 2) * g.max_w + 15) & ~size_t(15)) +
+                           (256 + kBlock) * sizeof(int);
+        hipLaunchKernelGGL(k_fast, dim3(g.total_bands), dim3(kBlock), lds, c->stream, pyr, a,
+                           c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>());
+        VX_LAUNCH_CHECK(c, "k_fast");
+    }
+    {
+        ProfScope ps(c, kStBlur);
+        hipLaunchKernelGGL(k_blur, dim3(blur_blocks(a)), dim3(kBlock), 0, c->stream, pyr,
+                           c->blur.as<uint8_t>(), a);
+        VX_LAUNCH_CHECK(c, "k_blur");
+    }
+    {
+        ProfScope ps(c, kStSelect);
+        hipLaunchKernelGGL(k_select, dim3(g.L), dim3(kSelBlock), 0, c->stream, c->cand.as<CandRec>(),
+                           c->band_count.as<int>(), c->hist.as<int>(), a, c->stage.as<CandRec>(),
+                           c->level_count.as<int>());
+        VX_LAUNCH_CHECK(c, "k_select");
+    }
+    {
+        ProfScope ps(c, kStDescribe);
+        const int waves_per_block = kBlock / 64;
+        hipLaunchKernelGGL(k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block), dim3(kBlock),
+                           0, c->stream, pyr, c->blur.as<uint8_t>(), c->stage.as<CandRec>(),
+                           c->level_count.as<int>(), a, s.kp.as<vx_keypoint>(), s.desc.as<uint8_t>(),
+                           s.count.as<int>());
+        VX_LAUNCH_CHECK(c, "k_describe");
+    }
+    s.valid = true;
+    return VX_OK;
+}
+
+}  // namespace vx
+
+using namespace vx;
+
+extern "C" {
+
+void vx_orb_default_params(vx_orb_params* p) {
+    if (!p) return;
+    p->n_features = 1000;
+    p->scale_factor = 1.2f;
+    p->n_levels = 8;
+    p->fast_threshold = 20;
+    p->edge_threshold = 31;
+}
+
+int vx_orb_pattern(int32_t* out) {
+    if (!out) return VX_ERR_INVALID;
+    for (int i = 0; i < 1024; ++i) out[i] = kBitPattern31[i];
+    return VX_OK;
+}
+
+int vx_orb_extract_async(vx_ctx* c, const vx_orb_params* p, const uint8_t* d_img, int w, int h,
+                         int channels, int64_t stride, int slot) {
+    if (!c) return VX_ERR_INVALID;
+    if (slot < 0 || slot >= VX_MAX_SLOTS) return set_error(c, VX_ERR_INVALID, "bad slot %d", slot);
+    if (!d_img) return set_error(c, VX_ERR_INVALID, "null image");
+    if (channels != 1 && channels != 3 && channels != 4)
+        return set_error(c, VX_ERR_INVALID, "channels must be 1, 3 or 4");
+    if (stride < (int64_t)w * channels) return set_error(c, VX_ERR_INVALID, "row stride too small");
+    int rc = orb_prepare(c, p, w, h);
+    if (rc) return rc;
+    return orb_enqueue(c, d_img, channels, stride, slot);
+}
+
+int vx_orb_fetch(vx_ctx* c, int slot, vx_keypoint* out_kp, uint8_t* out_desc, int cap, int* n_out) {
+    if (!c || !n_out) return VX_ERR_INVALID;
+    if (slot < 0 || slot >= VX_MAX_SLOTS || !c->slots[slot].valid)
+        return set_error(c, VX_ERR_STATE, "slot %d holds no extraction", slot);
+    Slot& s = c->slots[slot];
+    int cnt[2];
+    VX_HIP(c, hipMemcpyAsync(cnt, s.count.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) prof_collect(c);
+    *n_out = cnt[0];
+    if (cnt[1]) return set_error(c, VX_ERR_CAPACITY, "keypoints %d exceed slot capacity %d", cnt[0], s.cap);
+    if (cnt[0] > cap) return set_error(c, VX_ERR_CAPACITY, "need %d keypoints, cap %d", cnt[0], cap);
+    if (cnt[0] > 0) {
+        if (out_kp)
+            VX_HIP(c, hipMemcpyAsync(out_kp, s.kp.p, (size_t)cnt[0] * sizeof(vx_keypoint),
+                                     hipMemcpyDeviceToHost, c->stream));
+        if (out_desc)
+            VX_HIP(c, hipMemcpyAsync(out_desc, s.desc.p, (size_t)cnt[0] * 32, hipMemcpyDeviceToHost, c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    return VX_OK;
+}
+
+int vx_orb_slot_device(vx_ctx* c, int slot, const uint8_t** d_desc, const int32_t** d_count) {
+    if (!c || slot < 0 || slot >= VX_MAX_SLOTS || !c->slots[slot].valid) return VX_ERR_INVALID;
+    if (d_desc) *d_desc = c->slots[slot].desc.as<uint8_t>();
+    if (d_count) *d_count = c->slots[slot].count.as<int32_t>();
+    return VX_OK;
+}
+
+int vx_orb_extract(vx_ctx* c, const vx_orb_params* p, const uint8_t* img, int w, int h, int channels,
+                   int64_t stride, vx_keypoint* out_kp, uint8_t* out_desc, int cap, int* n_out) {
+    if (!c || !img || !n_out) return VX_ERR_INVALID;
+    *n_out = 0;
+    if (channels != 1 && channels != 3 && channels != 4)
+        return set_error(c, VX_ERR_INVALID, "channels must be 1, 3 or 4");
+    if (stride < (int64_t)w * channels) return set_error(c, VX_ERR_INVALID, "row stride too small");
+    int rc = orb_prepare(c, p, w, h);
+    if (rc) return rc;
+    const size_t packed = (size_t)w * channels;
+    VX_HIP(c, c->img_in.ensure(packed * h));
+    VX_HIP(c, hipMemcpy2DAsync(c->img_in.p, packed, img, (size_t)stride, packed, h, hipMemcpyHostToDevice,
+                               c->stream));
+    rc = orb_enqueue(c, c->img_in.as<uint8_t>(), channels, (int64_t)packed, 0);
+    if (rc) return rc;
+    return vx_orb_fetch(c, 0, out_kp, out_desc, cap, n_out);
+}
+
+}  // extern "C"

@@ -1,0 +1,179 @@
+// vx_ctx.cpp — context lifetime, error reporting, stage profiling and the RCCL communicator.
+#include <cstdarg>
+#include <cstring>
+
+#include "vx_internal.hpp"
+
+namespace vx {
+
+int set_error(vx_ctx* c, int code, const char* fmt, ...) {
+    if (c) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        c->err = buf;
+    }
+    return code;
+}
+
+int hip_fail(vx_ctx* c, hipError_t e, const char* what) {
+    return set_error(c, VX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+static hipEvent_t get_event(vx_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+ProfScope::ProfScope(vx_ctx* c_, int st) : c(c_), stage(st) {
+    if (!c->prof) return;
+    a = get_event(c);
+    if (a) (void)hipEventRecord(a, c->stream);
+}
+
+ProfScope::~ProfScope() {
+    if (!c->prof || !a) return;
+    hipEvent_t b = get_event(c);
+    if (!b) return;
+    (void)hipEventRecord(b, c->stream);
+    c->pending.push_back({a, b, stage});
+}
+
+void prof_collect(vx_ctx* c) {
+    for (auto& pe : c->pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(pe.b) == hipSuccess && hipEventElapsedTime(&ms, pe.a, pe.b) == hipSuccess) {
+            c->prof_ms[pe.stage] += ms;
+            c->prof_n[pe.stage] += 1;
+        }
+        c->event_pool.push_back(pe.a);
+        c->event_pool.push_back(pe.b);
+    }
+    c->pending.clear();
+}
+
+}  // namespace vx
+
+static const char* kStageNames[vx::kStCount] = {
+    "orb_gray",       "orb_resize",    "orb_fast_harris", "orb_select",  "orb_blur",
+    "orb_describe",   "match_partial", "match_merge",     "ba_reset",    "ba_pose_partial",
+    "ba_pose_sum",    "ba_allreduce",  "ba_pose_solve",   "ba_landmark"};
+
+extern "C" {
+
+int vx_version(void) { return 100; }
+
+int vx_create(int device, vx_ctx** out) {
+    if (!out) return VX_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return VX_ERR_HIP;
+    if (device < 0 || device >= n) return VX_ERR_INVALID;
+    if (hipSetDevice(device) != hipSuccess) return VX_ERR_HIP;
+    auto* c = new vx_ctx();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return VX_ERR_HIP;
+    }
+    *out = c;
+    return VX_OK;
+}
+
+void vx_destroy(vx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    vx::prof_collect(c);
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+#ifndef VX_NO_RCCL
+    if (c->comm) ncclCommDestroy(c->comm);
+#endif
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* vx_last_error(const vx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* vx_stream(vx_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int vx_synchronize(vx_ctx* c) {
+    if (!c) return VX_ERR_INVALID;
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) vx::prof_collect(c);
+    return VX_OK;
+}
+
+int vx_prof_enable(vx_ctx* c, int on) {
+    if (!c) return VX_ERR_INVALID;
+    if (!on) {
+        (void)hipStreamSynchronize(c->stream);
+        vx::prof_collect(c);
+    }
+    c->prof = on != 0;
+    return VX_OK;
+}
+
+int vx_prof_count(void) { return vx::kStCount; }
+
+const char* vx_prof_name(int s) { return (s >= 0 && s < vx::kStCount) ? kStageNames[s] : ""; }
+
+int vx_prof_read(vx_ctx* c, double* ms, int64_t* launches, int reset) {
+    if (!c) return VX_ERR_INVALID;
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    vx::prof_collect(c);
+    for (int i = 0; i < vx::kStCount; ++i) {
+        if (ms) ms[i] = c->prof_ms[i];
+        if (launches) launches[i] = c->prof_n[i];
+        if (reset) {
+            c->prof_ms[i] = 0;
+            c->prof_n[i] = 0;
+        }
+    }
+    return VX_OK;
+}
+
+int vx_comm_unique_id(uint8_t* out) {
+#ifndef VX_NO_RCCL
+    if (!out) return VX_ERR_INVALID;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return VX_ERR_COMM;
+    static_assert(sizeof(id) == 128, "ncclUniqueId size");
+    std::memcpy(out, &id, 128);
+    return VX_OK;
+#else
+    (void)out;
+    return VX_ERR_COMM;
+#endif
+}
+
+int vx_comm_init(vx_ctx* c, const uint8_t* id128, int nranks, int rank) {
+    if (!c || !id128 || nranks < 1 || rank < 0 || rank >= nranks) return VX_ERR_INVALID;
+#ifndef VX_NO_RCCL
+    VX_HIP(c, hipSetDevice(c->device));
+    ncclUniqueId id;
+    std::memcpy(&id, id128, 128);
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+    if (r != ncclSuccess)
+        return vx::set_error(c, VX_ERR_COMM, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    c->nranks = nranks;
+    c->rank = rank;
+    return VX_OK;
+#else
+    return VX_ERR_COMM;
+#endif
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+// vx_internal.hpp — context, device buffers, error plumbing and stage profiling shared by the
+// ORB, matching and bundle-adjustment translation units of libvxslam.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "vx_slam.h"
+
+#ifndef VX_NO_RCCL
+#include <rccl/rccl.h>
+#endif
+
+namespace vx {
+
+constexpr int kMaxLevels = 12;
+
+// Profiling stages (vx_prof_*).
+enum Stage : int {
+    kStGray = 0,
+    kStResize,
+    kStFast,
+    kStSelect,
+    kStBlur,
+    kStDescribe,
+    kStMatchPartial,
+    kStMatchMerge,
+    kStBaReset,
+    kStBaPose,
+    kStBaPoseSum,
+    kStBaAllreduce,
+    kStBaSolve,
+    kStBaLandmark,
+    kStCount
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    // grow-only; returns hipSuccess or the allocation error
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t ensure(size_t want) {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+};
+
+// Host-computed geometry of one ORB configuration (image size + params).  Mirrors the layer
+// layout of ORB_Impl::detectAndCompute (levels stored unpadded, back to back).
+struct OrbGeometry {
+    int W = 0, H = 0;
+    vx_orb_params p{};
+    int L = 0;
+    int lw[kMaxLevels], lh[kMaxLevels];
+    int64_t off[kMaxLevels];        // byte offset of level l in the pyramid buffer
+    float scale[kMaxLevels], inv_scale[kMaxLevels];
+    int quota[kMaxLevels];
+    int64_t pyr_bytes = 0;
+    // resize tables for levels 1..L-1: int4 {ofs, c0, c1, 0} per destination column / row
+    int64_t xtab[kMaxLevels], ytab[kMaxLevels];
+    int64_t tab_entries = 0;
+    // FAST bands: band_rows rows x full width per workgroup
+    int band_rows = 8;
+    int nbands[kMaxLevels];
+    int band_base[kMaxLevels];     // first band index of level l
+    int total_bands = 0;
+    int band_cap[kMaxLevels];      // candidate capacity per band of level l
+    int64_t cand_base[kMaxLevels]; // first candidate slot of level l
+    int64_t cand_total = 0;
+    int level_cap[kMaxLevels];     // candidate capacity of level l (for the selection staging)
+    int max_w = 0;
+    int out_cap = 0;               // keypoint capacity of one slot
+};
+
+struct Slot {
+    DevBuf kp, desc, count;  // vx_keypoint[cap], uint8[cap*32], int32[4] {n, overflow, ..}
+    int cap = 0;
+    bool valid = false;
+};
+
+struct ProfEvent {
+    hipEvent_t a, b;
+    int stage;
+};
+
+}  // namespace vx
+
+struct vx_ba_plan;
+
+struct vx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // ---- ORB
+    vx::OrbGeometry geo;
+    bool geo_valid = false;
+    vx::DevBuf img_in, pyr, blur, tabs, cand, band_count, hist, stage, level_count;
+    vx::Slot slots[VX_MAX_SLOTS];
+
+    // ---- matching
+    vx::DevBuf mq, mt, mq_n, partial, matches, match_count;
+    vx::PinnedBuf host_stage;
+    int match_cap = 0;
+    bool match_valid = false;
+
+    // ---- profiling
+    bool prof = false;
+    std::vector<vx::ProfEvent> pending;
+    std::vector<hipEvent_t> event_pool;
+    double prof_ms[vx::kStCount] = {0};
+    int64_t prof_n[vx::kStCount] = {0};
+
+    // ---- multi-GPU
+#ifndef VX_NO_RCCL
+    ncclComm_t comm = nullptr;
+#endif
+    int nranks = 1, rank = 0;
+};
+
+namespace vx {
+
+int set_error(vx_ctx* c, int code, const char* fmt, ...);
+int hip_fail(vx_ctx* c, hipError_t e, const char* what);
+
+// Event bracket around launches of one stage (no-op when profiling is off).
+struct ProfScope {
+    vx_ctx* c;
+    int stage;
+    hipEvent_t a = nullptr;
+    ProfScope(vx_ctx* c_, int st);
+    ~ProfScope();
+};
+void prof_collect(vx_ctx* c);
+
+int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h);
+
+}  // namespace vx
+
+#define VX_HIP(ctx, call)                                       \
+    do {                                                        \
+        hipError_t e__ = (call);                                \
+        if (e__ != hipSuccess) return vx::hip_fail(ctx, e__, #call); \
+    } while (0)
+
+#define VX_LAUNCH_CHECK(ctx, what)                              \
+    do {                                                        \
+        hipError_t e__ = hipGetLastError();                     \
+        if (e__ != hipSuccess) return vx::hip_fail(ctx, e__, what); \
+    } while (0)

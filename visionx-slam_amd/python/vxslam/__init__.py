@@ -1,0 +1,324 @@
+"""ctypes binding of libvxslam.so (include/vx_slam.h) for tests, smoke and bench.
+
+There is no Python fallback: if the HIP library is missing or fails to load, every entry point
+raises.  Names mirror the reference call surface: ``ORBExtractor.extract`` (FeatureExtractor::
+Extract, core/feature/feature_extractor.h:15), ``ORBMatcher.match`` (FeatureMatcher::Match,
+core/feature/feature_matcher.h:11-12) and ``LocalBA.optimize`` (LocalBA::Optimize,
+core/backend/local_ba.h:23).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libvxslam.so")
+HEADER_PATH = os.path.join(REPO_ROOT, "include", "vx_slam.h")
+
+VX_OK, VX_ERR_INVALID, VX_ERR_HIP, VX_ERR_CAPACITY, VX_ERR_COMM, VX_ERR_STATE = 0, -1, -2, -3, -4, -5
+MAX_SLOTS = 4
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"),
+                           ("octave", "<i4")])
+MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("distance", "<f4")])
+
+
+class VxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"vx error {code}: {msg}")
+        self.code = code
+
+
+class OrbParams(C.Structure):
+    _fields_ = [("n_features", C.c_int32), ("scale_factor", C.c_float), ("n_levels", C.c_int32),
+                ("fast_threshold", C.c_int32), ("edge_threshold", C.c_int32)]
+
+
+class MapView(C.Structure):
+    _fields_ = [("n_kf", C.c_int32), ("kf_id", C.c_void_p), ("kf_pose", C.c_void_p),
+                ("kf_intr", C.c_void_p), ("kf_has_cam", C.c_void_p), ("kf_feat_ptr", C.c_void_p),
+                ("feat_uv", C.c_void_p), ("feat_lm_id", C.c_void_p), ("feat_flags", C.c_void_p),
+                ("n_lm", C.c_int32), ("lm_id", C.c_void_p), ("lm_pos", C.c_void_p),
+                ("lm_bad", C.c_void_p), ("lm_obs_ptr", C.c_void_p), ("obs_kf_id", C.c_void_p),
+                ("obs_feat_idx", C.c_void_p)]
+
+
+class BAOptions(C.Structure):
+    _fields_ = [("window_size", C.c_int32), ("max_iterations", C.c_int32),
+                ("min_pose_observations", C.c_int32), ("min_point_observations", C.c_int32),
+                ("huber_delta", C.c_double), ("max_reproj_error", C.c_double)]
+
+
+class BAStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("n_window_kf", C.c_int32), ("n_landmarks", C.c_int32),
+                ("cost", C.c_double * 16), ("obs", C.c_int32 * 16), ("gate_margin", C.c_double),
+                ("status", C.c_int32)]
+
+
+EXPORTS = [
+    "vx_version", "vx_create", "vx_destroy", "vx_last_error", "vx_stream", "vx_synchronize",
+    "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
+    "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
+    "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
+    "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info",
+    "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
+    "vx_prof_read",
+]
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", PKG_ROOT, "-j8"], check=True)
+
+
+def lib():
+    """Load libvxslam.so (fails loudly: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        L.vx_last_error.restype = C.c_char_p
+        L.vx_last_error.argtypes = [C.c_void_p]
+        L.vx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.vx_destroy.argtypes = [C.c_void_p]
+        L.vx_stream.restype = C.c_void_p
+        L.vx_stream.argtypes = [C.c_void_p]
+        L.vx_synchronize.argtypes = [C.c_void_p]
+        L.vx_prof_name.restype = C.c_char_p
+        L.vx_ba_plan_destroy.argtypes = [C.c_void_p]
+        L.vx_ba_plan_destroy.restype = None
+        L.vx_orb_default_params.restype = None
+        L.vx_ba_default_options.restype = None
+        L.vx_ba_shard_of.restype = C.c_uint32
+        L.vx_ba_shard_of.argtypes = [C.c_uint64, C.c_int]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def default_orb_params(n_features=1000, scale_factor=1.2, n_levels=8, fast_threshold=20,
+                       edge_threshold=31):
+    return OrbParams(n_features, scale_factor, n_levels, fast_threshold, edge_threshold)
+
+
+def default_ba_options(window=5, iters=5, min_pose=20, min_point=2, huber=5.0, max_err=5.0):
+    return BAOptions(window, iters, min_pose, min_point, huber, max_err)
+
+
+def map_view(m) -> MapView:
+    """MapView over the arrays of a synth.BAMap (kf_pose / lm_pos are written in place)."""
+    v = MapView()
+    for name, _ in MapView._fields_:
+        if name == "n_kf":
+            v.n_kf = int(m["kf_id"].shape[0])
+        elif name == "n_lm":
+            v.n_lm = int(m["lm_id"].shape[0])
+        else:
+            a = m[name]
+            assert a.flags["C_CONTIGUOUS"], name
+            setattr(v, name, a.ctypes.data)
+    return v
+
+
+def pattern() -> np.ndarray:
+    out = np.zeros(1024, np.int32)
+    rc = lib().vx_orb_pattern(_p(out))
+    assert rc == 0
+    return out
+
+
+def ba_plan_inspect(m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1) -> dict:
+    """Host-only dry run of vx_ba_plan_create (no device needed)."""
+    opts = opts or default_ba_options(window=m.get("window", 5))
+    ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+    v = map_view(m)
+    out = np.zeros(8, np.int64)
+    lm = np.zeros(max(int(m["lm_id"].shape[0]), 1), np.int32)
+    kf = np.zeros(max(int(m["kf_id"].shape[0]), 1), np.int32)
+    rc = lib().vx_ba_plan_inspect(C.byref(v), C.c_uint64(0 if ref is None else int(ref)), 0 if ref is None else 1,
+                                  C.byref(opts), shard_rank, shard_count, _p(out), _p(lm), len(lm), _p(kf), len(kf))
+    if rc != VX_OK:
+        raise VxError(rc, "vx_ba_plan_inspect failed")
+    keys = ["status", "n_window_kf", "n_landmarks", "n_kf", "n_opt", "n_lm", "n_pose_obs", "n_lm_obs"]
+    d = {k: int(x) for k, x in zip(keys, out)}
+    d["lm_map_idx"] = lm[:d["n_lm"]].copy()
+    d["kf_map_idx"] = kf[:d["n_kf"]].copy()
+    return d
+
+
+def ba_shard_of(lm_id: int, shard_count: int) -> int:
+    return int(lib().vx_ba_shard_of(C.c_uint64(int(lm_id)), int(shard_count)))
+
+
+class Context:
+    """One vx_ctx = one device + one HIP stream (not thread-safe, like the reference's tracking
+    thread owning the hot path, core/system/system.cpp:39-52)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        rc = lib().vx_create(int(device), C.byref(self._h))
+        if rc != VX_OK:
+            raise VxError(rc, f"vx_create(device={device}) failed")
+
+    def close(self):
+        if self._h:
+            lib().vx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != VX_OK:
+            raise VxError(rc, lib().vx_last_error(self._h).decode())
+        return rc
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def stream(self) -> int:
+        return lib().vx_stream(self._h)
+
+    def synchronize(self):
+        self._check(lib().vx_synchronize(self._h))
+
+    # ---------------------------------------------------------------- ORB
+    def orb_extract(self, img: np.ndarray, params: OrbParams | None = None, cap: int | None = None):
+        img = np.ascontiguousarray(img)
+        h, w = img.shape[:2]
+        ch = 1 if img.ndim == 2 else img.shape[2]
+        params = params or default_orb_params()
+        cap = cap or (2 * params.n_features + 256)
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int(0)
+        self._check(lib().vx_orb_extract(self._h, C.byref(params), _p(img), w, h, ch,
+                                         C.c_int64(img.strides[0]), _p(kps), _p(desc), cap,
+                                         C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def orb_extract_async(self, d_img_ptr: int, w: int, h: int, channels: int, row_stride: int,
+                          slot: int, params: OrbParams | None = None):
+        params = params or default_orb_params()
+        self._check(lib().vx_orb_extract_async(self._h, C.byref(params), C.c_void_p(d_img_ptr), w, h,
+                                               channels, C.c_int64(row_stride), slot))
+
+    def orb_fetch(self, slot: int, cap: int = 8192):
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int(0)
+        self._check(lib().vx_orb_fetch(self._h, slot, _p(kps), _p(desc), cap, C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    # ---------------------------------------------------------------- matching
+    def match(self, q: np.ndarray, t: np.ndarray, ratio: float = 0.8):
+        q = np.ascontiguousarray(q, np.uint8)
+        t = np.ascontiguousarray(t, np.uint8)
+        cap = max(len(q), 1)
+        out = np.zeros(cap, MATCH_DTYPE)
+        n = C.c_int(0)
+        self._check(lib().vx_match_knn2_ratio(self._h, _p(q), len(q), _p(t), len(t),
+                                              C.c_float(ratio), _p(out), cap, C.byref(n)))
+        return out[:n.value].copy()
+
+    def match_slots_async(self, q_slot: int, t_slot: int, ratio: float = 0.8):
+        self._check(lib().vx_match_slots_async(self._h, q_slot, t_slot, C.c_float(ratio)))
+
+    def match_fetch(self, cap: int = 8192):
+        out = np.zeros(cap, MATCH_DTYPE)
+        n = C.c_int(0)
+        self._check(lib().vx_match_fetch(self._h, _p(out), cap, C.byref(n)))
+        return out[:n.value].copy()
+
+    # ---------------------------------------------------------------- bundle adjustment
+    def ba_optimize(self, m, opts: BAOptions | None = None, ref_kf_id=None) -> BAStats:
+        opts = opts or default_ba_options(window=m.get("window", 5))
+        ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+        v = map_view(m)
+        st = BAStats()
+        self._check(lib().vx_ba_optimize_map(self._h, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
+                                             0 if ref is None else 1, C.byref(opts), C.byref(st)))
+        return st
+
+    def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1):
+        return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
+
+    # ---------------------------------------------------------------- multi-GPU
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        rc = lib().vx_comm_unique_id(buf)
+        if rc != VX_OK:
+            raise VxError(rc, "ncclGetUniqueId failed")
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(lib().vx_comm_init(self._h, buf, nranks, rank))
+
+    # ---------------------------------------------------------------- profiling
+    def prof_enable(self, on=True):
+        self._check(lib().vx_prof_enable(self._h, 1 if on else 0))
+
+    def prof_read(self, reset=True) -> dict:
+        n = lib().vx_prof_count()
+        ms = (C.c_double * n)()
+        cnt = (C.c_int64 * n)()
+        self._check(lib().vx_prof_read(self._h, ms, cnt, 1 if reset else 0))
+        return {lib().vx_prof_name(i).decode(): (ms[i], cnt[i]) for i in range(n)}
+
+
+class BAPlan:
+    """vx_ba_plan: host window selection + device CSR upload, repeatable device runs."""
+
+    def __init__(self, ctx: Context, m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1):
+        self.ctx = ctx
+        self.m = m
+        self.opts = opts or default_ba_options(window=m.get("window", 5))
+        ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+        self._h = C.c_void_p()
+        v = map_view(m)
+        ctx._check(lib().vx_ba_plan_create(ctx.handle, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
+                                           0 if ref is None else 1, C.byref(self.opts), shard_rank,
+                                           shard_count, C.byref(self._h)))
+
+    def info(self):
+        out = np.zeros(4, np.int64)
+        rc = lib().vx_ba_plan_info(self._h, _p(out))
+        assert rc == 0
+        return dict(n_kf=int(out[0]), n_lm=int(out[1]), n_pose_obs=int(out[2]), n_lm_obs=int(out[3]))
+
+    def run_async(self):
+        self.ctx._check(lib().vx_ba_plan_run_async(self.ctx.handle, self._h))
+
+    def fetch(self, m=None) -> BAStats:
+        st = BAStats()
+        v = map_view(m) if m is not None else None
+        self.ctx._check(lib().vx_ba_plan_fetch(self.ctx.handle, self._h, C.byref(v) if v is not None else None,
+                                               C.byref(st)))
+        return st
+
+    def close(self):
+        if self._h:
+            lib().vx_ba_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
