@@ -185,8 +185,10 @@ int vx_comm_init(vx_ctx* ctx, const uint8_t* id_128, int nranks, int rank);
 
 /* ---------------------------------------------------------------- profiling
  * When enabled, the library brackets its kernels with hipEvents on its own stream; read back
- * accumulated milliseconds and launch counts per stage (names via vx_prof_name). */
-int vx_prof_enable(vx_ctx* ctx, int on);
+ * accumulated milliseconds and launch counts per stage (names via vx_prof_name).
+ * stage_mask: 0 = off, -1 = every stage, otherwise bit s enables stage s only (so a timed run
+ * can bracket just the kernel it reports without perturbing the others). */
+int vx_prof_enable(vx_ctx* ctx, int stage_mask);
 int vx_prof_count(void);
 const char* vx_prof_name(int stage);
 int vx_prof_read(vx_ctx* ctx, double* ms, int64_t* launches, int reset);

@@ -234,6 +234,7 @@ extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_
         kfs.push_back(it->second);
     }
     std::reverse(kfs.begin(), kfs.end());
+    st->n_window_kf = (int)kfs.size();
     if (kfs.size() < 2) return 0;
     std::unordered_set<uint64_t> local_ids;
     for (int k : kfs) local_ids.insert(m->kf_id[k]);

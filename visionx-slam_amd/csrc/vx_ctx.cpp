@@ -34,7 +34,7 @@ static hipEvent_t get_event(vx_ctx* c) {
 }
 
 ProfScope::ProfScope(vx_ctx* c_, int st) : c(c_), stage(st) {
-    if (!c->prof) return;
+    if (!c->prof || !((c->prof_mask >> st) & 1u)) return;
     a = get_event(c);
     if (a) (void)hipEventRecord(a, c->stream);
 }
@@ -112,13 +112,14 @@ int vx_synchronize(vx_ctx* c) {
     return VX_OK;
 }
 
-int vx_prof_enable(vx_ctx* c, int on) {
+int vx_prof_enable(vx_ctx* c, int mask) {
     if (!c) return VX_ERR_INVALID;
-    if (!on) {
+    if (!mask) {
         (void)hipStreamSynchronize(c->stream);
         vx::prof_collect(c);
     }
-    c->prof = on != 0;
+    c->prof = mask != 0;
+    c->prof_mask = (unsigned)mask;
     return VX_OK;
 }
 

@@ -137,6 +137,7 @@ struct vx_ctx {
 
     // ---- profiling
     bool prof = false;
+    unsigned prof_mask = 0;
     std::vector<vx::ProfEvent> pending;
     std::vector<hipEvent_t> event_pool;
     double prof_ms[vx::kStCount] = {0};

@@ -271,8 +271,18 @@ class Context:
         self._check(lib().vx_comm_init(self._h, buf, nranks, rank))
 
     # ---------------------------------------------------------------- profiling
-    def prof_enable(self, on=True):
-        self._check(lib().vx_prof_enable(self._h, 1 if on else 0))
+    def prof_enable(self, on=True, stages=None):
+        """on=False disables; stages=None brackets every stage, else an iterable of stage names."""
+        if not on:
+            mask = 0
+        elif stages is None:
+            mask = -1
+        else:
+            names = [lib().vx_prof_name(i).decode() for i in range(lib().vx_prof_count())]
+            mask = 0
+            for s in stages:
+                mask |= 1 << names.index(s)
+        self._check(lib().vx_prof_enable(self._h, mask))
 
     def prof_read(self, reset=True) -> dict:
         n = lib().vx_prof_count()
