@@ -173,6 +173,15 @@ int corner_score(const Img& im, int x, int y, int threshold) {
 // FAST_t<16>: >=9 contiguous ring pixels all darker than v-t or all brighter than v+t.
 bool is_corner(const Img& im, int x, int y, int t) {
     const int v = im.at(y, x);
+    // FAST_t's exact pre-test: any 9-arc contains one pixel of every opposite pair (k, k+8).
+    auto cls = [&](int k) {
+        const int p = im.at(y + kRing[k][1], x + kRing[k][0]);
+        return (p < v - t ? 1 : 0) | (p > v + t ? 2 : 0);
+    };
+    int d = cls(0) | cls(8);
+    if (!d) return false;
+    d &= cls(4) | cls(12);
+    if (!d) return false;
     for (int sign = 0; sign < 2; ++sign) {
         int count = 0;
         for (int k = 0; k < 25; ++k) {
@@ -366,6 +375,39 @@ uint8_t blur_at(const Img& im, int x, int y, const float k[7]) {
     return (uint8_t)std::min(255, std::max(0, r));
 }
 
+// Whole-level blur with exactly blur_at's arithmetic (same taps, same summation order), written
+// as two separable passes so the CPU baseline is not dominated by recomputation.
+void blur_image(const Img& im, Img& out, const float k[7]) {
+    const int W = im.w, H = im.h;
+    out.w = W; out.h = H; out.px.resize((size_t)W * H);
+    std::vector<int> xi((size_t)W + 6);
+    for (int x = -3; x < W + 3; ++x) xi[x + 3] = reflect101(x, W);
+    std::vector<float> rows((size_t)W * H);
+    for (int y = 0; y < H; ++y) {
+        const uint8_t* r = im.row(y);
+        float* o = rows.data() + (size_t)y * W;
+        for (int x = 0; x < W; ++x) {
+            const int* ix = xi.data() + x;
+            float s = k[0] * (float)r[ix[0]];
+            for (int j = 1; j < 7; ++j) s += k[j] * (float)r[ix[j]];
+            o[x] = s;
+        }
+    }
+    for (int y = 0; y < H; ++y) {
+        const float* rr[7];
+        for (int d = -3; d <= 3; ++d) rr[d + 3] = rows.data() + (size_t)reflect101(y + d, H) * W;
+        uint8_t* o = out.px.data() + (size_t)y * W;
+        for (int x = 0; x < W; ++x) {
+            float s = k[3] * rr[3][x] + 0.0f;
+            s += k[4] * (rr[4][x] + rr[2][x]);
+            s += k[5] * (rr[5][x] + rr[1][x]);
+            s += k[6] * (rr[6][x] + rr[0][x]);
+            const int v = cv_roundf(s);
+            o[x] = (uint8_t)std::min(255, std::max(0, v));
+        }
+    }
+}
+
 struct OrbParams {
     int n_features = 1000;
     float scale_factor = 1.2f;
@@ -499,9 +541,11 @@ int orc_orb_extract(const uint8_t* img, int w, int h, int channels, int64_t stri
     // computeOrbDescriptors on the blurred levels (WTA_K 2, bit_pattern_31_).
     float gk[7];
     gauss_taps(gk);
+    std::vector<Img> blurred(n_levels);
+    for (int l = 0; l < n_levels; ++l) blur_image(pyr[l], blurred[l], gk);
     for (int i = 0; i < n; ++i) {
         const KeyPoint& k = sel[i];
-        const Img& im = pyr[k.octave];
+        const Img& im = blurred[k.octave];
         const float scale = 1.f / g.scale[k.octave];
         float angle = k.angle;
         angle *= (float)(M_PI / 180.f);
@@ -512,7 +556,7 @@ int orc_orb_extract(const uint8_t* img, int w, int h, int channels, int64_t stri
             const float px = (float)pattern[2 * idx], py = (float)pattern[2 * idx + 1];
             const float x = px * a - py * b;
             const float y = px * b + py * a;
-            return (int)blur_at(im, cx + cv_roundf(x), cy + cv_roundf(y), gk);
+            return (int)im.at(cy + cv_roundf(y), cx + cv_roundf(x));
         };
         for (int byte = 0; byte < 32; ++byte) {
             int val = 0;

@@ -1,0 +1,42 @@
+"""Per-kernel HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs).
+
+FETCH_SIZE / WRITE_SIZE are in KB.  MI355X_MICROARCH.md §HBM: on gfx950 FETCH_SIZE reports exactly
+half the bytes of a wide coalesced streaming read (128-B requests tallied at 64 B), so the fetch
+side is doubled; WRITE_SIZE is taken as reported.  Output: {stage: bytes per launch}.
+"""
+import collections
+import csv
+import json
+import re
+import sys
+
+STAGE = {"k_gray": "orb_gray", "k_resize": "orb_resize", "k_fast": "orb_fast_harris", "k_select": "orb_select",
+         "k_blur": "orb_blur", "k_describe": "orb_describe", "k_knn_partial": "match_partial",
+         "k_knn_merge": "match_merge", "k_ba_reset": "ba_reset", "k_pose_partial": "ba_pose_partial",
+         "k_pose_sum": "ba_pose_sum", "k_pose_solve": "ba_pose_solve", "k_landmark": "ba_landmark"}
+
+
+def agg(path, counter):
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        m = re.search(r"\b(k_[a-z0-9_]+)\(", r["Kernel_Name"])
+        if m:
+            d[m.group(1)].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in d.items()}
+
+
+def main(fetch_csv, write_csv, out_json):
+    f = agg(fetch_csv, "FETCH_SIZE")
+    w = agg(write_csv, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(f) | set(w)):
+        b = 2.0 * f.get(k, 0.0) * 1024 + w.get(k, 0.0) * 1024
+        res[STAGE.get(k, k)] = int(b)
+        print(f"{k:16s} fetch {f.get(k, 0):10.1f} KB (x2 corrected)  write {w.get(k, 0):10.1f} KB  -> {b / 1e3:10.1f} kB/launch")
+    json.dump(res, open(out_json, "w"), indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
