@@ -85,7 +85,8 @@ class Dist:
             import torch.distributed as dist
 
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group(backend="gloo")
+            if not dist.is_initialized():
+                dist.init_process_group(backend="gloo")  # control plane only; data path is RCCL
             self.pg = dist
         if n_gpus != self.world:
             log(f"note: --gpus {n_gpus} but WORLD_SIZE {self.world}; using WORLD_SIZE")

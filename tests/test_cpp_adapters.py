@@ -1,0 +1,108 @@
+"""The C++ drop-in adapters (visionx::ORBExtractor / ORBMatcher / LocalBA over the C ABI) driven
+the way core/frontend/tracking.cpp drives the reference classes, through tests/cpp/adapter_driver.
+
+CPU: LocalBA::Flatten (the host gather that replaces local_ba.cpp:71-137's map walk) selects the
+same window / landmark set as the oracle.  GPU: Extract / Match / Optimize through the adapters
+equal the CPU restatement (bit-exact ORB and matches, BA within 1e-4).
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from vxslam import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "visionx-slam_amd", "build", "adapter_driver")
+
+MAP_KEYS = ["kf_id", "kf_pose", "kf_intr", "kf_has_cam", "kf_feat_ptr", "feat_uv", "feat_lm_id", "feat_flags",
+            "lm_id", "lm_pos", "lm_bad", "lm_obs_ptr", "obs_kf_id", "obs_feat_idx"]
+
+
+@pytest.fixture(scope="module")
+def driver():
+    if not os.path.exists(DRIVER):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "visionx-slam_amd"), "-j8"], check=True)
+    return DRIVER
+
+
+def run(driver, *args):
+    out = subprocess.run([driver, *map(str, args)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    return out.stdout.split()
+
+
+def dump_map(m, d):
+    for k in MAP_KEYS:
+        np.ascontiguousarray(m[k]).tofile(os.path.join(d, k + ".bin"))
+
+
+def test_flatten_selects_the_reference_window(driver, oracle, tmp_path):
+    import vxslam
+
+    m = synth.make_ba_map(9, 8, 1200, n_old_kf=4)
+    dump_map(m, tmp_path)
+    for ref_idx, window in [(-1, 5), (-3, 5), (-1, 12), (0, 5)]:
+        ref = int(m["kf_id"][ref_idx])
+        n_kf, n_lm, n_obs = map(int, run(driver, "ba", tmp_path, window, 5, ref, "flatten"))
+        flat_kf = np.fromfile(os.path.join(tmp_path, "flat_kf_id.out"), np.uint64)
+        d = vxslam.ba_plan_inspect(m, vxslam.default_ba_options(window=window), ref_kf_id=ref)
+        assert n_kf == d["n_window_kf"] == len(flat_kf)
+        exp = np.sort(m["kf_id"][m["kf_id"] <= ref])[-window:]
+        assert np.array_equal(flat_kf, exp)
+        # every landmark referenced by a window feature that exists in the map is carried
+        flat_lm = set(np.fromfile(os.path.join(tmp_path, "flat_lm_id.out"), np.uint64).tolist())
+        sel = np.isin(np.repeat(np.arange(len(m["kf_id"])), np.diff(m["kf_feat_ptr"])),
+                      np.nonzero(np.isin(m["kf_id"], exp))[0])
+        ref_ids = set(m["feat_lm_id"][sel & (m["feat_flags"] & 1 == 1)].tolist()) & set(m["lm_id"].tolist())
+        assert flat_lm == ref_ids
+
+
+@pytest.mark.gpu
+def test_adapter_extract_and_match(driver, oracle, tmp_path):
+    frames = synth.make_frames(91, 2)
+    descs = []
+    for i, f in enumerate(frames):
+        f.tofile(os.path.join(tmp_path, f"img{i}.bin"))
+        n = int(run(driver, "extract", os.path.join(tmp_path, f"img{i}.bin"), 480, 640, 3, 1500,
+                    os.path.join(tmp_path, f"f{i}"))[0])
+        pos = np.fromfile(os.path.join(tmp_path, f"f{i}.pos"), np.float64).reshape(-1, 2)
+        resp = np.fromfile(os.path.join(tmp_path, f"f{i}.resp"), np.float32)
+        desc = np.fromfile(os.path.join(tmp_path, f"f{i}.desc"), np.uint8).reshape(-1, 32)
+        kc, dc = oracle.orb_extract(f, 1500, order=oracle.ORDER_RASTER)
+        assert n == len(kc)
+        # Feature.position = Eigen::Vector2d(kp.pt.x, kp.pt.y), response = kp.response
+        assert np.array_equal(pos[:, 0], kc["x"].astype(np.float64))
+        assert np.array_equal(pos[:, 1], kc["y"].astype(np.float64))
+        assert np.array_equal(resp, kc["response"])
+        assert np.array_equal(desc, dc)
+        descs.append(dc)
+        desc.tofile(os.path.join(tmp_path, f"d{i}.bin"))
+    n = int(run(driver, "match", os.path.join(tmp_path, "d0.bin"), len(descs[0]), os.path.join(tmp_path, "d1.bin"),
+                len(descs[1]), os.path.join(tmp_path, "m.bin"))[0])
+    got = np.fromfile(os.path.join(tmp_path, "m.bin"), np.float32).reshape(-1, 3)
+    exp = oracle.match(descs[0], descs[1])
+    assert n == len(exp)
+    assert np.array_equal(got[:, 0].astype(np.int32), exp["query_idx"])
+    assert np.array_equal(got[:, 1].astype(np.int32), exp["train_idx"])
+    assert np.array_equal(got[:, 2], exp["distance"])
+
+
+@pytest.mark.gpu
+def test_adapter_local_ba(driver, oracle, tmp_path):
+    m = synth.make_ba_map(92, 10, 2000, n_old_kf=3)
+    dump_map(m, tmp_path)
+    ref = int(m["kf_id"][-1])
+    status, iters, nkf, nlm = map(int, run(driver, "ba", tmp_path, 10, 5, ref))
+    mc = m.copy()
+    st = oracle.ba_optimize(mc, oracle.ba_options(window=10), ref_kf_id=ref)
+    assert (status, iters, nkf, nlm) == (st.status, st.iterations, st.n_window_kf, st.n_landmarks)
+    pose = np.fromfile(os.path.join(tmp_path, "kf_pose.out"), np.float64).reshape(-1, 7)
+    lm = np.fromfile(os.path.join(tmp_path, "lm_pos.out"), np.float64).reshape(-1, 3)
+    for a, b in ((pose, mc["kf_pose"]), (lm, mc["lm_pos"])):
+        a, b = a.copy(), b.copy()
+        if a.shape[1] == 7:
+            a[a[:, 3] < 0, :4] *= -1
+            b[b[:, 3] < 0, :4] *= -1
+        assert (np.abs(a - b) / np.maximum(np.abs(b), 1e-3)).max() <= 1e-4

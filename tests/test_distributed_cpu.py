@@ -1,0 +1,134 @@
+"""The N > 1 path on CPU with torch.distributed gloo, world_size 2 (no GPU).
+
+* bench.py's distributed harness: barrier-bracketed timing, max over ranks.
+* landmark-sharded BA: each rank's host plan (vx_ba_plan_inspect) owns a disjoint
+  landmark shard; the per-keyframe normal equations of the pose stage computed from each shard
+  and summed by an all-reduce equal the unsharded ones.  On the GPU the same reduction is one
+  ncclAllReduce(sum, f64) of the 32-double keyframe blocks per iteration (ba.hip).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _spawn(fn, world=2):
+    import torch.multiprocessing as mp
+
+    port = _free_port()
+    mp.spawn(fn, args=(world, port), nprocs=world, join=True)
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    for p in (os.path.join(ROOT, "visionx-slam_amd", "python"), ROOT):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def _timing_worker(rank, world, port):
+    import time
+
+    dist = _init(rank, world, port)
+    import bench
+
+    d = bench.Dist(world)
+    assert d.world == world and d.rank == rank
+    calls = []
+
+    def step(i):
+        calls.append(i)
+        time.sleep(0.002 * (rank + 1))  # rank 1 is slower: the reported time must be rank 1's
+
+    el = bench.timed_loop(step, 5, 2, lambda: None, d)
+    assert calls == list(range(7))
+    assert el >= 5 * 0.004 * 0.9
+    uid = d.broadcast_bytes(b"x" * 128 if rank == 0 else None)
+    assert uid == b"x" * 128
+    dist.destroy_process_group()
+
+
+def test_bench_harness_max_over_ranks():
+    _spawn(_timing_worker)
+
+
+def pose_normal_equations(m, opts_window, lm_subset=None):
+    """Per-window-keyframe 29-term blocks of the first pose stage (local_ba.cpp:160-190), numpy."""
+    from vxslam import synth
+
+    ids = m["kf_id"]
+    order = np.argsort(ids)
+    win = order[-opts_window:]
+    lm_index = {int(i): n for n, i in enumerate(m["lm_id"])}
+    out = np.zeros((len(win), 29))
+    for r, k in enumerate(win):
+        q, t = m["kf_pose"][k, :4], m["kf_pose"][k, 4:]
+        R = synth.quat_to_mat(q)
+        fx, fy, cx, cy = m["kf_intr"][k]
+        for f in range(m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]):
+            fl = m["feat_flags"][f]
+            if not (fl & 1) or (fl & 2):
+                continue
+            l = lm_index.get(int(m["feat_lm_id"][f]))
+            if l is None or m["lm_bad"][l] or (lm_subset is not None and l not in lm_subset):
+                continue
+            pc = R @ m["lm_pos"][l] + t
+            if pc[2] <= 1e-6:
+                continue
+            e = m["feat_uv"][f] - np.array([fx * pc[0] / pc[2] + cx, fy * pc[1] / pc[2] + cy])
+            if np.linalg.norm(e) > 5.0:
+                continue
+            x, y, z = pc
+            Jp = np.array([[fx / z, 0, -fx * x / z ** 2], [0, fy / z, -fy * y / z ** 2]])
+            J = Jp @ np.hstack([np.eye(3), -np.array([[0, -z, y], [z, 0, -x], [-y, x, 0]])])
+            H = J.T @ J
+            out[r, :21] += H[np.triu_indices(6)]
+            out[r, 21:27] += -J.T @ e
+            out[r, 27] += e @ e
+            out[r, 28] += 1
+    return out
+
+
+def _shard_worker(rank, world, port):
+    dist = _init(rank, world, port)
+    import torch
+
+    import vxslam
+    from vxslam import synth
+
+    m = synth.make_ba_map(17, 6, 600, n_old_kf=2)
+    opts = vxslam.default_ba_options(window=6)
+    mine = vxslam.ba_plan_inspect(m, opts, shard_rank=rank, shard_count=world)
+    full = vxslam.ba_plan_inspect(m, opts)
+    part = pose_normal_equations(m, 6, set(mine["lm_map_idx"].tolist()))
+    assert int(part[:, 28].sum()) <= full["n_pose_obs"]
+    t = torch.from_numpy(part.copy())
+    dist.all_reduce(t)
+    ref = pose_normal_equations(m, 6)
+    got = t.numpy()
+    assert np.allclose(got, ref, rtol=1e-9, atol=1e-9 * np.abs(ref).max())
+    counts = torch.tensor([mine["n_opt"], mine["n_pose_obs"], mine["n_lm_obs"]], dtype=torch.int64)
+    dist.all_reduce(counts)
+    assert counts.tolist() == [full["n_opt"], full["n_pose_obs"], full["n_lm_obs"]]
+    dist.destroy_process_group()
+
+
+def test_sharded_pose_normal_equations_allreduce():
+    _spawn(_shard_worker)

@@ -7,20 +7,21 @@
 //
 //   host   plan:  SelectKeyFrames (:71-91) + landmark filtering (:106-137) + the per-observation
 //                 validity checks that are static during Optimize (:160-167, :215-233) ->
-//                 keyframe-major pose observations (uv, landmark slot) cut into <= 256-obs chunks,
-//                 landmark-major observations (uv, keyframe row); uploaded once.
-//   device run (per iteration it, all kernels early-exit once the stop rule fired):
-//     k_pose_partial  one thread per observation: ProjectToPixel (projection.h:11-31), residual,
-//                     gate, Huber, 2x6 PoseJacobian, the 21 + 6 + 2 normal-equation terms; wave
-//                     shuffle + LDS reduction into one 29-double partial per chunk
-//     k_pose_sum      per keyframe, its chunk partials summed in chunk order
-//     [RCCL]          ncclAllReduce(sum, f64) of the per-keyframe blocks when landmarks are sharded
-//                     over GPUs (one collective per iteration, 32 doubles per keyframe)
-//     k_pose_solve    one thread per keyframe: H += 1e-6 I, Eigen-style pivoted LDLT, finite
-//                     check, T <- exp(dx) T (Sophus), rotation matrix for the landmark stage; the
-//                     ordered total cost / observation count and the stop rule (device flag)
-//     k_landmark      one thread per landmark: 2x3 Jacobian Jp*R, 3x3 normal equations, LDLT,
-//                     p += dp
+//                 keyframe-major pose observations (uv, landmark slot) and landmark-major
+//                 observations (uv, keyframe row); uploaded once, replayed by every run.
+//   device run (per iteration it; every kernel early-exits once the stop rule has fired):
+//     k_pose_kf        one workgroup per keyframe: each thread projects its observations
+//                      (ProjectToPixel, projection.h:11-31), gates, weights and accumulates the
+//                      21 + 6 + 2 normal-equation terms of the 2x6 PoseJacobian in registers; one
+//                      fixed-order workgroup reduction writes the keyframe's 29-term block
+//     [sharded only]   ncclAllReduce(sum, f64) of the per-keyframe blocks over the landmark
+//                      shards (one collective per iteration, 32 doubles per keyframe)
+//     k_landmark_solve every workgroup first solves ALL window keyframes redundantly (one lane per
+//                      keyframe: H += 1e-6 I, Eigen-style pivoted LDLT, finite check, T <- exp(dx) T)
+//                      into LDS — bitwise identical in every workgroup — then runs one landmark
+//                      per thread (2x3 Jacobian Jp*R, 3x3 normal equations, LDLT, p += dp) against
+//                      those poses; workgroup 0 publishes the poses and evaluates the stop rule.
+//                      Windows beyond kMaxKfLds keyframes use k_pose_solve_g + k_landmark instead.
 // The step keeps the reference's sign (b = -J^T e, :185 and :253): this is a drop-in, not a fix.
 #include <algorithm>
 #include <cmath>
@@ -34,13 +35,14 @@
 namespace vx {
 namespace {
 
-constexpr int kChunk = 256;     // pose observations per chunk / block
-constexpr int kNTerms = 29;     // 21 H (upper) + 6 b + cost + count
-constexpr int kStride = 32;     // doubles per partial / keyframe block
+constexpr int kPoseBlock = 256;  // threads per keyframe workgroup
+constexpr int kNTerms = 29;      // 21 H (upper) + 6 b + cost + count
+constexpr int kStride = 32;      // doubles per keyframe block
 constexpr int kMaxIter = 64;
+constexpr int kMaxKfLds = 512;   // keyframes whose poses fit the LDS of k_landmark_solve
 
 struct BAState {
-    int active[kMaxIter + 1];   // active[it]: iteration it runs
+    int active[kMaxIter + 1];  // active[it]: iteration it runs
     int iterations;
     int pad;
     double last_cost;
@@ -49,21 +51,21 @@ struct BAState {
 };
 
 struct BAArgs {
-    int n_kf, n_opt, n_lm, n_chunks;
-    int min_pose_obs, min_point_obs, max_iter, pad;
+    int n_kf, n_opt, n_lm, pad0;
+    int min_pose_obs, min_point_obs, max_iter, pad1;
     double huber, max_err;
     const double* kf_pose0;  // 8 per KF: qx qy qz qw tx ty tz 0
     double* kf_pose;
     const double* kf_intr;   // 4 per KF
     double* kf_rot;          // 9 per KF (rotation matrix of the current pose)
+    const int* kf_flags;     // bit0: keyframe has a camera
+    const int* kf_obs_ptr;   // n_kf + 1, CSR into the pose observations
+    double* kf_sums;         // n_kf * kStride normal-equation blocks (all-reduced when sharded)
+    double* kf_cost;         // 2 per KF: pose-stage cost and observation count
     const double* lm_pos0;   // 4 per landmark
     double* lm_pos;
     const double2* pobs_uv;
     const int* pobs_lm;
-    const int4* chunks;      // {kf, begin, end, 0}
-    const int* kf_chunk_ptr; // n_kf + 1
-    double* chunk_part;      // n_chunks * kStride
-    double* kf_sums;         // n_kf * kStride
     const int* lobs_ptr;     // n_opt + 1
     const int* lobs_kf;
     const double2* lobs_uv;
@@ -86,6 +88,7 @@ __device__ __forceinline__ D3 se3_apply(const double* T, D3 p) {
     return {p.x + w * uv.x + c.x + T[4], p.y + w * uv.y + c.y + T[5], p.z + w * uv.z + c.z + T[6]};
 }
 
+// Eigen Quaternion::toRotationMatrix
 __device__ __forceinline__ void rot_from_quat(const double* q, double* R) {
     const double tx = 2.0 * q[0], ty = 2.0 * q[1], tz = 2.0 * q[2];
     const double twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
@@ -176,112 +179,14 @@ __device__ __forceinline__ void ldlt_solve(double* A, const double* b, double* x
             if (tr[k] == bi) { const double t = x[k]; x[k] = x[bi]; x[bi] = t; }
 }
 
-// upper-triangle index table of the 6x6 pose Hessian
+// upper-triangle index of the 6x6 pose Hessian
 __device__ __forceinline__ int hidx(int i, int j) {  // i <= j
     return i * 6 - (i * (i - 1)) / 2 + (j - i);
 }
 
-__global__ void k_ba_reset(BAArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n_kf * 8) a.kf_pose[i] = a.kf_pose0[i];
-    if (i < a.n_lm * 4) a.lm_pos[i] = a.lm_pos0[i];
-    if (i < a.n_kf) {
-        double R[9];
-        rot_from_quat(a.kf_pose0 + 8 * i, R);
-        for (int k = 0; k < 9; ++k) a.kf_rot[9 * i + k] = R[k];
-    }
-    if (i == 0) {
-        BAState* s = a.state;
-        for (int k = 0; k <= kMaxIter; ++k) s->active[k] = k == 0 ? 1 : 0;
-        s->iterations = 0;
-        s->last_cost = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
-        for (int k = 0; k < 16; ++k) { s->cost[k] = 0; s->obs[k] = 0; }
-    }
-}
-
-__global__ __launch_bounds__(kChunk) void k_pose_partial(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
-    __shared__ double red[kChunk / 64][kNTerms];
-    const int4 ch = a.chunks[blockIdx.x];
-    const int k = ch.x;
-    const int i = ch.y + threadIdx.x;
-    double v[kNTerms];
-#pragma unroll
-    for (int t = 0; t < kNTerms; ++t) v[t] = 0.0;
-    if (i < ch.z) {
-        const double* T = a.kf_pose + 8 * k;
-        const double* C = a.kf_intr + 4 * k;
-        const int s = a.pobs_lm[i];
-        const double2 uv = a.pobs_uv[i];
-        const double* P = a.lm_pos + 4 * s;
-        const D3 pc = se3_apply(T, {P[0], P[1], P[2]});
-        if (pc.z > 1e-6) {
-            const double inv_z = 1.0 / pc.z;
-            const double x = pc.x * inv_z, y = pc.y * inv_z;
-            const double fx = C[0], fy = C[1];
-            const double e0 = uv.x - (fx * x + C[2]);
-            const double e1 = uv.y - (fy * y + C[3]);
-            const double en = sqrt(e0 * e0 + e1 * e1);
-            if (!(en > a.max_err)) {
-                const double w = en <= a.huber ? 1.0 : a.huber / en;
-                const double z = pc.z, z2 = z * z;
-                const double jp0 = fx / z, jp2 = -fx * pc.x / z2, jp4 = fy / z, jp5 = -fy * pc.y / z2;
-                // J = Jp * [I | -hat(pc)] (local_ba.cpp:55-62), formed as the 2x3 * 3x6 product
-                const double Jp[6] = {jp0, 0.0, jp2, 0.0, jp4, jp5};
-                const double S[18] = {1, 0, 0, 0, pc.z, -pc.y, 0, 1, 0, -pc.z, 0, pc.x, 0, 0, 1, pc.y, -pc.x, 0};
-                double J0[6], J1[6];
-#pragma unroll
-                for (int c = 0; c < 6; ++c) {
-                    J0[c] = Jp[0] * S[c] + Jp[1] * S[6 + c] + Jp[2] * S[12 + c];
-                    J1[c] = Jp[3] * S[c] + Jp[4] * S[6 + c] + Jp[5] * S[12 + c];
-                }
-#pragma unroll
-                for (int r = 0; r < 6; ++r)
-#pragma unroll
-                    for (int c = r; c < 6; ++c) v[hidx(r, c)] = (w * J0[r]) * J0[c] + (w * J1[r]) * J1[c];
-#pragma unroll
-                for (int r = 0; r < 6; ++r) v[21 + r] = w * ((-J0[r]) * e0 + (-J1[r]) * e1);
-                v[27] = w * (e0 * e0 + e1 * e1);
-                v[28] = 1.0;
-            }
-        }
-    }
-    // wave reduction (xor butterfly), then across the 4 waves through LDS
-#pragma unroll
-    for (int t = 0; t < kNTerms; ++t) {
-        double x = v[t];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        v[t] = x;
-    }
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
-#pragma unroll
-        for (int t = 0; t < kNTerms; ++t) red[wv][t] = v[t];
-    }
-    __syncthreads();
-    if (threadIdx.x < kNTerms) {
-        double s = red[0][threadIdx.x];
-#pragma unroll
-        for (int w2 = 1; w2 < kChunk / 64; ++w2) s += red[w2][threadIdx.x];
-        a.chunk_part[(long long)blockIdx.x * kStride + threadIdx.x] = s;
-    }
-}
-
-__global__ void k_pose_sum(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
-    const int k = blockIdx.x;
-    const int t = threadIdx.x;  // 32 threads, term t
-    if (t >= kStride) return;
-    double s = 0.0;
-    if (t < kNTerms)
-        for (int c = a.kf_chunk_ptr[k]; c < a.kf_chunk_ptr[k + 1]; ++c) s += a.chunk_part[(long long)c * kStride + t];
-    a.kf_sums[(long long)k * kStride + t] = s;
-}
-
 // Sophus SE3::exp(dx) * T, written into T (8 doubles)
 __device__ void se3_left_update(const double* dx, double* T) {
-    const double eps = 1e-10;
+    const double eps = 1e-10;  // Sophus::Constants<double>::epsilon()
     const double wx = dx[3], wy = dx[4], wz = dx[5];
     const double theta_sq = wx * wx + wy * wy + wz * wz;
     double theta, imag, real;
@@ -315,73 +220,170 @@ __device__ void se3_left_update(const double* dx, double* T) {
     }
     const double et[3] = {V[0] * dx[0] + V[1] * dx[1] + V[2] * dx[2], V[3] * dx[0] + V[4] * dx[1] + V[5] * dx[2],
                           V[6] * dx[0] + V[7] * dx[1] + V[8] * dx[2]};
-    // q <- normalize(eq * q)
+    // q <- normalize(eq * q)   (Sophus SO3 product + normalize)
     const double ax = eq[0], ay = eq[1], az = eq[2], aw = eq[3];
     const double bx = T[0], by = T[1], bz = T[2], bw = T[3];
-    double q[4] = {aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
-                   aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz};
+    const double q[4] = {aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
+                         aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz};
     const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
     // t <- et + rotate(eq, t)
-    double rt[8] = {eq[0], eq[1], eq[2], eq[3], 0, 0, 0, 0};
+    const double rt[8] = {eq[0], eq[1], eq[2], eq[3], 0, 0, 0, 0};
     const D3 r = se3_apply(rt, {T[4], T[5], T[6]});
     T[0] = q[0] / n; T[1] = q[1] / n; T[2] = q[2] / n; T[3] = q[3] / n;
     T[4] = et[0] + r.x; T[5] = et[1] + r.y; T[6] = et[2] + r.z;
 }
 
-constexpr int kSolveBlock = 256;
-
-__global__ __launch_bounds__(kSolveBlock) void k_pose_solve(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
-    __shared__ double s_cost[kSolveBlock];
-    __shared__ int s_obs[kSolveBlock];
-    // per-thread partial totals over its keyframes k = t, t + 256, ... (ascending k)
-    double cost = 0.0;
-    int obs_tot = 0;
-    for (int k = threadIdx.x; k < a.n_kf; k += kSolveBlock) {
-        const double* S = a.kf_sums + (long long)k * kStride;
-        const int obs = (int)S[28];
-        cost += S[27];
-        obs_tot += obs;
-        double* T = a.kf_pose + 8 * k;
-        if (obs >= a.min_pose_obs) {
-            double H[36], b[6], dx[6];
+// Pose step of one keyframe from its summed terms S (local_ba.cpp:192-202): skipped below
+// min_pose_observations or without a camera; T updated in place, R = its rotation (:249).
+__device__ __forceinline__ void solve_pose(const BAArgs& a, int k, const double* S, double* T, double* R) {
+    const int obs = (int)S[28];
+    if (obs >= a.min_pose_obs && (a.kf_flags[k] & 1)) {
+        double H[36], b[6], dx[6];
 #pragma unroll
-            for (int r = 0; r < 6; ++r)
+        for (int r = 0; r < 6; ++r)
 #pragma unroll
-                for (int c = 0; c < 6; ++c) H[6 * r + c] = r <= c ? S[hidx(r, c)] : S[hidx(c, r)];
+            for (int c = 0; c < 6; ++c) H[6 * r + c] = r <= c ? S[hidx(r, c)] : S[hidx(c, r)];
 #pragma unroll
-            for (int r = 0; r < 6; ++r) { H[7 * r] += 1e-6; b[r] = S[21 + r]; }
-            ldlt_solve<6>(H, b, dx);
-            bool fin = true;
-#pragma unroll
-            for (int r = 0; r < 6; ++r) fin = fin && isfinite(dx[r]);
-            if (fin) se3_left_update(dx, T);
+        for (int r = 0; r < 6; ++r) {
+            H[7 * r] += 1e-6;
+            b[r] = S[21 + r];
         }
-        double R[9];
-        rot_from_quat(T, R);
-        for (int q = 0; q < 9; ++q) a.kf_rot[9 * k + q] = R[q];
+        ldlt_solve<6>(H, b, dx);
+        bool fin = true;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) fin = fin && isfinite(dx[r]);
+        if (fin) se3_left_update(dx, T);
     }
-    s_cost[threadIdx.x] = cost;
-    s_obs[threadIdx.x] = obs_tot;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double total = 0.0;
-        int tobs = 0;
-        for (int t = 0; t < kSolveBlock; ++t) { total += s_cost[t]; tobs += s_obs[t]; }
+    rot_from_quat(T, R);
+}
+
+// Relative-cost stop rule (local_ba.cpp:269-276) -> active[it + 1].
+__device__ void stop_rule(const BAArgs& a, int it, double total, int tobs) {
+    BAState* s = a.state;
+    if (it < 16) {
+        s->cost[it] = total;
+        s->obs[it] = tobs;
+    }
+    s->iterations = it + 1;
+    const double last = s->last_cost;
+    const bool stop = tobs == 0 || fabs(last - total) < 1e-6 * last;
+    if (!stop) s->last_cost = total;
+    s->active[it + 1] = (!stop && it + 1 < a.max_iter) ? 1 : 0;
+}
+
+// Ordered (fixed-tree) pose-stage totals over the keyframes; the calling wave must be complete.
+__device__ void totals_and_stop(const BAArgs& a, int it, int lane) {
+    double total = 0.0;
+    int tobs = 0;
+    for (int j = lane; j < a.n_kf; j += 64) {
+        total += a.kf_cost[2 * j];
+        tobs += (int)a.kf_cost[2 * j + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        total += __shfl_xor(total, o, 64);
+        tobs += __shfl_xor(tobs, o, 64);
+    }
+    if (lane == 0) stop_rule(a, it, total, tobs);
+}
+
+__global__ void k_ba_reset(BAArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < a.n_kf * 8) a.kf_pose[i] = a.kf_pose0[i];
+    if (i < a.n_lm * 4) a.lm_pos[i] = a.lm_pos0[i];
+    if (i < a.n_kf) {
+        double R[9];
+        rot_from_quat(a.kf_pose0 + 8 * i, R);
+        for (int k = 0; k < 9; ++k) a.kf_rot[9 * i + k] = R[k];
+    }
+    if (i == 0) {
         BAState* s = a.state;
-        if (it < 16) { s->cost[it] = total; s->obs[it] = tobs; }
-        s->iterations = it + 1;
-        const double last = s->last_cost;
-        const bool stop = tobs == 0 || fabs(last - total) < 1e-6 * last;
-        if (!stop) s->last_cost = total;
-        s->active[it + 1] = (!stop && it + 1 < a.max_iter) ? 1 : 0;
+        for (int k = 0; k <= kMaxIter; ++k) s->active[k] = k == 0 ? 1 : 0;
+        s->iterations = 0;
+        s->last_cost = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
+        for (int k = 0; k < 16; ++k) { s->cost[k] = 0; s->obs[k] = 0; }
     }
 }
 
-__global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
+// Pose stage (local_ba.cpp:145-190): one workgroup per keyframe.  Each thread accumulates the 29
+// terms of its observations (strided) in registers; a fixed-order wave butterfly + LDS tree
+// reduces them into kf_sums[k].
+__global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     if (!a.state->active[it]) return;
-    const int l = blockIdx.x * blockDim.x + threadIdx.x;
-    if (l >= a.n_opt) return;
+    __shared__ double red[kPoseBlock / 64][kNTerms];
+    const int k = blockIdx.x;
+    const int i0 = a.kf_obs_ptr[k], i1 = a.kf_obs_ptr[k + 1];
+    double T[8], C[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) T[j] = a.kf_pose[8 * k + j];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) C[j] = a.kf_intr[4 * k + j];
+    const double fx = C[0], fy = C[1];
+    double v[kNTerms];
+#pragma unroll
+    for (int t = 0; t < kNTerms; ++t) v[t] = 0.0;
+#pragma unroll 2
+    for (int i = i0 + (int)threadIdx.x; i < i1; i += kPoseBlock) {
+        const int s = a.pobs_lm[i];
+        const double2 uv = a.pobs_uv[i];
+        const double* P = a.lm_pos + 4 * s;
+        const D3 pc = se3_apply(T, {P[0], P[1], P[2]});
+        if (!(pc.z > 1e-6)) continue;
+        const double inv_z = 1.0 / pc.z;
+        const double x = pc.x * inv_z, y = pc.y * inv_z;
+        const double e0 = uv.x - (fx * x + C[2]);
+        const double e1 = uv.y - (fy * y + C[3]);
+        const double en = sqrt(e0 * e0 + e1 * e1);
+        if (en > a.max_err) continue;
+        const double w = en <= a.huber ? 1.0 : a.huber / en;
+        const double z = pc.z, z2 = z * z;
+        const double jp0 = fx / z, jp2 = -fx * pc.x / z2, jp4 = fy / z, jp5 = -fy * pc.y / z2;
+        // J = Jp * [I | -hat(pc)] (local_ba.cpp:55-62), formed as the 2x3 * 3x6 product
+        const double Jp[6] = {jp0, 0.0, jp2, 0.0, jp4, jp5};
+        const double S[18] = {1, 0, 0, 0, pc.z, -pc.y, 0, 1, 0, -pc.z, 0, pc.x, 0, 0, 1, pc.y, -pc.x, 0};
+        double J0[6], J1[6];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {
+            J0[c] = Jp[0] * S[c] + Jp[1] * S[6 + c] + Jp[2] * S[12 + c];
+            J1[c] = Jp[3] * S[c] + Jp[4] * S[6 + c] + Jp[5] * S[12 + c];
+        }
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) v[hidx(r, c)] += (w * J0[r]) * J0[c] + (w * J1[r]) * J1[c];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) v[21 + r] += w * ((-J0[r]) * e0 + (-J1[r]) * e1);
+        v[27] += w * (e0 * e0 + e1 * e1);
+        v[28] += 1.0;
+    }
+#pragma unroll
+    for (int t = 0; t < kNTerms; ++t) {
+        double x = v[t];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        v[t] = x;
+    }
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) {
+#pragma unroll
+        for (int t = 0; t < kNTerms; ++t) red[wv][t] = v[t];
+    }
+    __syncthreads();
+    if (threadIdx.x < kStride) {
+        double s = 0.0;
+        if (threadIdx.x < kNTerms) {
+            s = red[0][threadIdx.x];
+#pragma unroll
+            for (int w2 = 1; w2 < kPoseBlock / 64; ++w2) s += red[w2][threadIdx.x];
+        }
+        a.kf_sums[(long long)k * kStride + threadIdx.x] = s;
+    }
+}
+
+// Landmark step of landmark l (local_ba.cpp:205-267) against keyframe tables T/R/C (LDS or
+// global memory).
+__device__ __forceinline__ void landmark_step(const BAArgs& a, int l, const double* sT, const double* sR,
+                                              const double* sC) {
     double* Pp = a.lm_pos + 4 * l;
     const D3 P{Pp[0], Pp[1], Pp[2]};
     double h00 = 0, h01 = 0, h02 = 0, h11 = 0, h12 = 0, h22 = 0, b0 = 0, b1 = 0, b2 = 0;
@@ -389,8 +391,8 @@ __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
     for (int o = a.lobs_ptr[l]; o < a.lobs_ptr[l + 1]; ++o) {
         const int k = a.lobs_kf[o];
         const double2 uv = a.lobs_uv[o];
-        const double* T = a.kf_pose + 8 * k;
-        const double* C = a.kf_intr + 4 * k;
+        const double* T = sT + 8 * k;
+        const double* C = sC + 4 * k;
         const D3 pc = se3_apply(T, P);
         if (!(pc.z > 1e-6)) continue;
         const double inv_z = 1.0 / pc.z;
@@ -403,7 +405,7 @@ __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
         const double w = en <= a.huber ? 1.0 : a.huber / en;
         const double z = pc.z, z2 = z * z;
         const double jp0 = fx / z, jp2 = -fx * pc.x / z2, jp4 = fy / z, jp5 = -fy * pc.y / z2;
-        const double* R = a.kf_rot + 9 * k;
+        const double* R = sR + 9 * k;
         double J0[3], J1[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
@@ -432,6 +434,72 @@ __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
     Pp[2] = P.z + dp[2];
 }
 
+// Pose solve of every window keyframe (redundantly in each workgroup) + landmark stage, one launch.
+__global__ __launch_bounds__(256) void k_landmark_solve(BAArgs a, int it) {
+    if (!a.state->active[it]) return;
+    extern __shared__ __attribute__((aligned(16))) double kf_lds[];  // n_kf x (8 T + 9 R + 4 C)
+    double* sT = kf_lds;
+    double* sR = kf_lds + 8 * a.n_kf;
+    double* sC = sR + 9 * a.n_kf;
+    const int tid = threadIdx.x;
+    for (int k = tid; k < a.n_kf; k += blockDim.x) {
+        double S[kStride];
+#pragma unroll
+        for (int t = 0; t < kNTerms; ++t) S[t] = a.kf_sums[(long long)k * kStride + t];
+        double T[8], R[9];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) T[j] = a.kf_pose[8 * k + j];
+        solve_pose(a, k, S, T, R);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sT[8 * k + j] = T[j];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) sR[9 * k + j] = R[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sC[4 * k + j] = a.kf_intr[4 * k + j];
+        if (blockIdx.x == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a.kf_pose[8 * k + j] = T[j];
+#pragma unroll
+            for (int j = 0; j < 9; ++j) a.kf_rot[9 * k + j] = R[j];
+            a.kf_cost[2 * k] = S[27];
+            a.kf_cost[2 * k + 1] = S[28];
+        }
+    }
+    __syncthreads();  // also makes block 0's kf_cost stores visible inside block 0
+    if (blockIdx.x == 0 && tid < 64) totals_and_stop(a, it, tid);
+    const int l = blockIdx.x * blockDim.x + tid;
+    if (l < a.n_opt) landmark_step(a, l, sT, sR, sC);
+}
+
+// Large-window fallback (n_kf > kMaxKfLds): one thread per keyframe solves into global memory...
+__global__ __launch_bounds__(256) void k_pose_solve_g(BAArgs a, int it) {
+    if (!a.state->active[it]) return;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n_kf) return;
+    double S[kStride];
+#pragma unroll
+    for (int t = 0; t < kNTerms; ++t) S[t] = a.kf_sums[(long long)k * kStride + t];
+    double T[8], R[9];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) T[j] = a.kf_pose[8 * k + j];
+    solve_pose(a, k, S, T, R);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a.kf_pose[8 * k + j] = T[j];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) a.kf_rot[9 * k + j] = R[j];
+    a.kf_cost[2 * k] = S[27];
+    a.kf_cost[2 * k + 1] = S[28];
+}
+
+// ... and the landmark stage reads the poses from global memory; wave 0 of block 0 evaluates
+// the stop rule (active[it + 1] is read by no block of this launch).
+__global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
+    if (!a.state->active[it]) return;
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < 64) totals_and_stop(a, it, threadIdx.x);
+    if (l < a.n_opt) landmark_step(a, l, a.kf_pose, a.kf_rot, a.kf_intr);
+}
+
 inline uint64_t splitmix64(uint64_t x) {
     x += 0x9e3779b97f4a7c15ull;
     x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -448,11 +516,11 @@ struct vx_ba_plan {
     int status = 1;
     int shard_rank = 0, shard_count = 1;
     int n_window_kf = 0, n_landmarks_global = 0;
-    int n_kf = 0, n_opt = 0, n_lm = 0, n_chunks = 0;
+    int n_kf = 0, n_opt = 0, n_lm = 0;
     int64_t n_pose_obs = 0, n_lm_obs = 0;
     std::vector<int> kf_map_idx, lm_map_idx;
-    vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, lm_pos0, lm_pos, pobs_uv, pobs_lm, chunks,
-        kf_chunk_ptr, chunk_part, kf_sums, lobs_ptr, lobs_kf, lobs_uv, state;
+    vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags, kf_obs_ptr, kf_sums, kf_cost, lm_pos0, lm_pos,
+        pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_uv, state;
     bool ran = false;
 };
 
@@ -464,7 +532,6 @@ BAArgs make_args(vx_ba_plan* p) {
     a.n_kf = p->n_kf;
     a.n_opt = p->n_opt;
     a.n_lm = p->n_lm;
-    a.n_chunks = p->n_chunks;
     a.min_pose_obs = p->opt.min_pose_observations;
     a.min_point_obs = p->opt.min_point_observations;
     a.max_iter = p->opt.max_iterations;
@@ -474,14 +541,14 @@ BAArgs make_args(vx_ba_plan* p) {
     a.kf_pose = p->kf_pose.as<double>();
     a.kf_intr = p->kf_intr.as<double>();
     a.kf_rot = p->kf_rot.as<double>();
+    a.kf_flags = p->kf_flags.as<int>();
+    a.kf_obs_ptr = p->kf_obs_ptr.as<int>();
+    a.kf_sums = p->kf_sums.as<double>();
+    a.kf_cost = p->kf_cost.as<double>();
     a.lm_pos0 = p->lm_pos0.as<double>();
     a.lm_pos = p->lm_pos.as<double>();
     a.pobs_uv = p->pobs_uv.as<double2>();
     a.pobs_lm = p->pobs_lm.as<int>();
-    a.chunks = p->chunks.as<int4>();
-    a.kf_chunk_ptr = p->kf_chunk_ptr.as<int>();
-    a.chunk_part = p->chunk_part.as<double>();
-    a.kf_sums = p->kf_sums.as<double>();
     a.lobs_ptr = p->lobs_ptr.as<int>();
     a.lobs_kf = p->lobs_kf.as<int>();
     a.lobs_uv = p->lobs_uv.as<double2>();
@@ -560,37 +627,31 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     p->kf_map_idx = win;
     std::vector<double> pose0((size_t)nk * 8, 0.0), intr((size_t)nk * 4, 0.0);
     std::vector<double2> puv;
-    std::vector<int> plm;
-    std::vector<int4> chunks;
-    std::vector<int> kf_chunk_ptr(nk + 1, 0);
+    std::vector<int> plm, kf_obs_ptr(nk + 1, 0), kf_flags(nk, 0);
     for (int r = 0; r < nk; ++r) {
         const int k = win[r];
         for (int j = 0; j < 7; ++j) pose0[8 * r + j] = m->kf_pose[7 * k + j];
         for (int j = 0; j < 4; ++j) intr[4 * r + j] = m->kf_intr[4 * k + j];
-        const int begin = (int)puv.size();
-        if (m->kf_has_cam[k]) {
-            for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) {
-                const uint8_t fl = m->feat_flags[f];
-                if (!(fl & 1) || (fl & 2)) continue;
-                auto it = lm_by_id.find(m->feat_lm_id[f]);
-                if (it == lm_by_id.end()) continue;
-                const int l = it->second;
-                if (m->lm_bad[l] || !owned(l)) continue;
-                if (slot_of[l] < 0) {
-                    slot_of[l] = (int)p->lm_map_idx.size();
-                    p->lm_map_idx.push_back(l);
-                }
-                puv.push_back(make_double2(m->feat_uv[2 * f], m->feat_uv[2 * f + 1]));
-                plm.push_back(slot_of[l]);
+        kf_flags[r] = m->kf_has_cam[k] ? 1 : 0;
+        kf_obs_ptr[r] = (int)puv.size();
+        if (!m->kf_has_cam[k]) continue;
+        for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) {
+            const uint8_t fl = m->feat_flags[f];
+            if (!(fl & 1) || (fl & 2)) continue;
+            auto it = lm_by_id.find(m->feat_lm_id[f]);
+            if (it == lm_by_id.end()) continue;
+            const int l = it->second;
+            if (m->lm_bad[l] || !owned(l)) continue;
+            if (slot_of[l] < 0) {
+                slot_of[l] = (int)p->lm_map_idx.size();
+                p->lm_map_idx.push_back(l);
             }
+            puv.push_back(make_double2(m->feat_uv[2 * f], m->feat_uv[2 * f + 1]));
+            plm.push_back(slot_of[l]);
         }
-        const int end = (int)puv.size();
-        kf_chunk_ptr[r] = (int)chunks.size();
-        for (int s = begin; s < end; s += kChunk) chunks.push_back(make_int4(r, s, std::min(end, s + kChunk), 0));
     }
-    kf_chunk_ptr[nk] = (int)chunks.size();
+    kf_obs_ptr[nk] = (int)puv.size();
     p->n_lm = (int)p->lm_map_idx.size();
-    p->n_chunks = (int)chunks.size();
     p->n_pose_obs = (int64_t)puv.size();
     std::vector<double> lm0((size_t)std::max(p->n_lm, 1) * 4, 0.0);
     for (int s = 0; s < p->n_lm; ++s)
@@ -625,19 +686,19 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     int rc;
     if ((rc = upload(c, p->kf_pose0, pose0))) return rc;
     if ((rc = upload(c, p->kf_intr, intr))) return rc;
+    if ((rc = upload(c, p->kf_flags, kf_flags))) return rc;
+    if ((rc = upload(c, p->kf_obs_ptr, kf_obs_ptr))) return rc;
     if ((rc = upload(c, p->lm_pos0, lm0))) return rc;
     if ((rc = upload(c, p->pobs_uv, puv))) return rc;
     if ((rc = upload(c, p->pobs_lm, plm))) return rc;
-    if ((rc = upload(c, p->chunks, chunks))) return rc;
-    if ((rc = upload(c, p->kf_chunk_ptr, kf_chunk_ptr))) return rc;
     if ((rc = upload(c, p->lobs_ptr, lptr))) return rc;
     if ((rc = upload(c, p->lobs_kf, lkf))) return rc;
     if ((rc = upload(c, p->lobs_uv, luv))) return rc;
     VX_HIP(c, p->kf_pose.ensure((size_t)nk * 8 * sizeof(double)));
     VX_HIP(c, p->kf_rot.ensure((size_t)nk * 9 * sizeof(double)));
-    VX_HIP(c, p->lm_pos.ensure(lm0.size() * sizeof(double)));
-    VX_HIP(c, p->chunk_part.ensure((size_t)std::max(p->n_chunks, 1) * kStride * sizeof(double)));
     VX_HIP(c, p->kf_sums.ensure((size_t)nk * kStride * sizeof(double)));
+    VX_HIP(c, p->kf_cost.ensure((size_t)nk * 2 * sizeof(double)));
+    VX_HIP(c, p->lm_pos.ensure(lm0.size() * sizeof(double)));
     VX_HIP(c, p->state.ensure(sizeof(BAState)));
     return VX_OK;
 }
@@ -647,7 +708,8 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
         p->ran = true;
         return VX_OK;
     }
-    if (p->shard_count > 1) {
+    const bool sharded = p->shard_count > 1;
+    if (sharded) {
 #ifndef VX_NO_RCCL
         if (!c->comm || c->nranks != p->shard_count || c->rank != p->shard_rank)
             return set_error(c, VX_ERR_STATE, "sharded plan needs vx_comm_init(%d ranks)", p->shard_count);
@@ -662,33 +724,31 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
         hipLaunchKernelGGL(k_ba_reset, dim3((n + 255) / 256), dim3(256), 0, c->stream, a);
         VX_LAUNCH_CHECK(c, "k_ba_reset");
     }
+    const bool lds_poses = p->n_kf <= kMaxKfLds;
+    const size_t lds = (size_t)p->n_kf * 21 * sizeof(double);
+    const int lm_blocks = std::max(1, (p->n_opt + 255) / 256);
     for (int it = 0; it < p->opt.max_iterations; ++it) {
-        if (p->n_chunks > 0) {
-            ProfScope ps(c, kStBaPose);
-            hipLaunchKernelGGL(k_pose_partial, dim3(p->n_chunks), dim3(kChunk), 0, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_pose_partial");
-        }
         {
-            ProfScope ps(c, kStBaPoseSum);
-            hipLaunchKernelGGL(k_pose_sum, dim3(p->n_kf), dim3(kStride), 0, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_pose_sum");
+            ProfScope ps(c, kStBaPose);
+            hipLaunchKernelGGL(k_pose_kf, dim3(p->n_kf), dim3(kPoseBlock), 0, c->stream, a, it);
+            VX_LAUNCH_CHECK(c, "k_pose_kf");
         }
 #ifndef VX_NO_RCCL
-        if (p->shard_count > 1) {
+        if (sharded) {
             ProfScope ps(c, kStBaAllreduce);
             ncclResult_t r = ncclAllReduce(p->kf_sums.p, p->kf_sums.p, (size_t)p->n_kf * kStride, ncclDouble,
                                            ncclSum, c->comm, c->stream);
             if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
         }
 #endif
-        {
-            ProfScope ps(c, kStBaSolve);
-            hipLaunchKernelGGL(k_pose_solve, dim3(1), dim3(kSolveBlock), 0, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_pose_solve");
-        }
-        if (p->n_opt > 0) {
-            ProfScope ps(c, kStBaLandmark);
-            hipLaunchKernelGGL(k_landmark, dim3((p->n_opt + 255) / 256), dim3(256), 0, c->stream, a, it);
+        ProfScope ps(c, kStBaLandmark);
+        if (lds_poses) {
+            hipLaunchKernelGGL(k_landmark_solve, dim3(lm_blocks), dim3(256), lds, c->stream, a, it);
+            VX_LAUNCH_CHECK(c, "k_landmark_solve");
+        } else {
+            hipLaunchKernelGGL(k_pose_solve_g, dim3((p->n_kf + 255) / 256), dim3(256), 0, c->stream, a, it);
+            VX_LAUNCH_CHECK(c, "k_pose_solve_g");
+            hipLaunchKernelGGL(k_landmark, dim3(lm_blocks), dim3(256), 0, c->stream, a, it);
             VX_LAUNCH_CHECK(c, "k_landmark");
         }
     }
@@ -760,7 +820,10 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
         VX_HIP(c, hipStreamSynchronize(c->stream));
         if (c->prof) prof_collect(c);
         s.iterations = hs.iterations;
-        for (int i = 0; i < 16; ++i) { s.cost[i] = hs.cost[i]; s.obs[i] = hs.obs[i]; }
+        for (int i = 0; i < 16; ++i) {
+            s.cost[i] = hs.cost[i];
+            s.obs[i] = hs.obs[i];
+        }
         if (m) {
             for (int r = 0; r < p->n_kf; ++r)
                 for (int j = 0; j < 7; ++j) m->kf_pose[7 * p->kf_map_idx[r] + j] = pose[8 * r + j];

@@ -79,34 +79,46 @@ __device__ __forceinline__ int scan_excl(int v, int* sh, int& total) {
     return incl - v;
 }
 
-__global__ __launch_bounds__(kMergeBlock) void k_knn_merge(const uint2* __restrict__ partial,
-                                                           const int* __restrict__ nq_p, int nq_host,
-                                                           const int* __restrict__ nt_p, int nt_host,
-                                                           int q_stride, float ratio,
-                                                           vx_match* __restrict__ out,
-                                                           int* __restrict__ out_count) {
-    __shared__ int sh[kMergeBlock];
+// Per-query merge of the chunk partials + ratio test, one thread per query over many blocks.
+// best[qi] = winning key when the query passes the ratio test, kNone otherwise.
+__global__ __launch_bounds__(256) void k_knn_merge(const uint2* __restrict__ partial,
+                                                   const int* __restrict__ nq_p, int nq_host,
+                                                   const int* __restrict__ nt_p, int nt_host,
+                                                   int q_stride, float ratio,
+                                                   unsigned* __restrict__ best) {
     const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
     const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
+    const int qi = blockIdx.x * 256 + threadIdx.x;
+    if (qi >= nq) return;
     const int nchunks = (nt + kTC - 1) / kTC;
+    unsigned k1 = kNone, k2 = kNone;
+    for (int c = 0; c < nchunks; ++c) {
+        const uint2 p = partial[(long long)c * q_stride + qi];
+        k2 = max(min(k1, p.x), min(k2, max(k1, p.x)));
+        k1 = min(k1, p.x);
+        k2 = max(min(k1, p.y), min(k2, max(k1, p.y)));
+        k1 = min(k1, p.y);
+    }
+    bool keep = false;
+    if (k2 != kNone) {  // knn.size() == 2 (orb_matcher.cpp:28)
+        const float d1 = (float)(k1 >> 22), d2 = (float)(k2 >> 22);
+        keep = d1 < ratio * d2;  // orb_matcher.cpp:33
+    }
+    best[qi] = keep ? k1 : kNone;
+}
+
+// Ordered compaction (ascending query index) of the per-query results, one block.
+__global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __restrict__ best,
+                                                             const int* __restrict__ nq_p, int nq_host,
+                                                             vx_match* __restrict__ out,
+                                                             int* __restrict__ out_count) {
+    __shared__ int sh[kMergeBlock];
+    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
     int written = 0;
     for (int base = 0; base < nq; base += kMergeBlock) {
         const int qi = base + threadIdx.x;
-        unsigned k1 = kNone, k2 = kNone;
-        if (qi < nq) {
-            for (int c = 0; c < nchunks; ++c) {
-                const uint2 p = partial[(long long)c * q_stride + qi];
-                k2 = max(min(k1, p.x), min(k2, max(k1, p.x)));
-                k1 = min(k1, p.x);
-                k2 = max(min(k1, p.y), min(k2, max(k1, p.y)));
-                k1 = min(k1, p.y);
-            }
-        }
-        int keep = 0;
-        if (qi < nq && k2 != kNone) {
-            const float d1 = (float)(k1 >> 22), d2 = (float)(k2 >> 22);
-            keep = d1 < ratio * d2;
-        }
+        const unsigned k1 = qi < nq ? best[qi] : kNone;
+        const int keep = k1 != kNone;
         int cnt;
         const int pos = scan_excl<kMergeBlock>(keep, sh, cnt);
         if (keep) {
@@ -125,7 +137,7 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
                   const int* dnt, int nt_host, int q_cap, int t_cap, float ratio) {
     const int n_chunks = (t_cap + kTC - 1) / kTC;
     const int q_stride = q_cap;
-    VX_HIP(c, c->partial.ensure((size_t)n_chunks * q_stride * sizeof(uint2) + 16));
+    VX_HIP(c, c->partial.ensure((size_t)n_chunks * q_stride * sizeof(uint2) + (size_t)q_cap * sizeof(unsigned) + 16));
     VX_HIP(c, c->matches.ensure((size_t)std::max(q_cap, 1) * sizeof(vx_match)));
     VX_HIP(c, c->match_count.ensure(16));
     c->match_cap = q_cap;
@@ -137,10 +149,13 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
     }
     {
         ProfScope ps(c, kStMatchMerge);
-        hipLaunchKernelGGL(k_knn_merge, dim3(1), dim3(kMergeBlock), 0, c->stream, c->partial.as<uint2>(), dnq,
-                           nq_host, dnt, nt_host, q_stride, ratio, c->matches.as<vx_match>(),
-                           c->match_count.as<int>());
+        unsigned* best = reinterpret_cast<unsigned*>(c->partial.as<uint2>() + (size_t)n_chunks * q_stride);
+        hipLaunchKernelGGL(k_knn_merge, dim3((q_cap + 255) / 256), dim3(256), 0, c->stream, c->partial.as<uint2>(),
+                           dnq, nq_host, dnt, nt_host, q_stride, ratio, best);
         VX_LAUNCH_CHECK(c, "k_knn_merge");
+        hipLaunchKernelGGL(k_knn_compact, dim3(1), dim3(kMergeBlock), 0, c->stream, best, dnq, nq_host,
+                           c->matches.as<vx_match>(), c->match_count.as<int>());
+        VX_LAUNCH_CHECK(c, "k_knn_compact");
     }
     c->match_valid = true;
     return VX_OK;

@@ -6,9 +6,9 @@
 //
 //   k_gray            BGR(A)->gray level 0, fixed point (A.1)
 //   k_resize x (L-1)  INTER_LINEAR_EXACT pyramid, 8.8 / 16.16 fixed point (A.1)
-//   k_fast            all levels in one launch: full-width row bands staged in LDS with a 4 px
+//   k_fast            all levels in one launch: 64x16 tiles staged in LDS with a 4 px
 //                     halo; FAST-9/16 corner test as 16-bit ring masks, cornerScore<16>, strict
-//                     3x3 NMS, border filter, ordered (raster) compaction by block scan, Harris
+//                     3x3 NMS, border filter, raster-ordered cells by wave ballot, wave-parallel Harris
 //                     7x7 from the same LDS tile, per-level score histogram (A.3, A.4)
 //   k_blur            GaussianBlur 7x7 sigma 2, float separable, reflect-101, all levels (A.5)
 //   k_select          one workgroup per level: retainBest(2q) by FAST score via the histogram,
@@ -42,10 +42,10 @@ struct LevelArgs {
     long long off[kMaxLevels];
     float scale[kMaxLevels], inv_scale[kMaxLevels];
     int quota[kMaxLevels];
-    int band_rows;
-    int nbands[kMaxLevels], band_base[kMaxLevels], band_cap[kMaxLevels];
-    long long cand_base[kMaxLevels];
-    int level_cap[kMaxLevels];
+    int ntx[kMaxLevels], tile_base[kMaxLevels];     // FAST tiles (64 x 16) per level
+    long long cell_base[kMaxLevels];                // first (row, tile column) cell of level l
+    long long stage_base[kMaxLevels];               // selection staging of level l
+    int level_cap[kMaxLevels];                      // max NMS corners of level l
     int fast_threshold, edge, out_cap;
     // blur tiling
     int btx[kMaxLevels], bty[kMaxLevels], bbase[kMaxLevels];
@@ -148,43 +148,6 @@ __device__ int fast_score(const uint8_t* t, int stride, int thr) {
     return -b0 - 1;
 }
 
-// HarrisResponses(blockSize 7, k 0.04f) from an LDS tile; t = tile base at the keypoint.
-__device__ float harris_tile(const uint8_t* t, int s) {
-    int a = 0, b = 0, c = 0;
-    for (int i = -3; i <= 3; ++i)
-#pragma unroll
-        for (int j = -3; j <= 3; ++j) {
-            const uint8_t* p = t + i * s + j;
-            const int Ix = (p[1] - p[-1]) * 2 + (p[-s + 1] - p[-s - 1]) + (p[s + 1] - p[s - 1]);
-            const int Iy = (p[s] - p[-s]) * 2 + (p[s - 1] - p[-s - 1]) + (p[s + 1] - p[-s + 1]);
-            a += Ix * Ix;
-            b += Iy * Iy;
-            c += Ix * Iy;
-        }
-    const float scale = 1.f / ((1 << 2) * 7 * 255.f);
-    const float s4 = scale * scale * scale * scale;
-    const float fa = (float)a, fb = (float)b, fc = (float)c;
-    return (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
-}
-
-template <int NT>
-__device__ __forceinline__ int block_exclusive_scan(int v, int* sh, int& total) {
-    // sh: NT ints of scratch. Hillis-Steele in LDS (NT <= 1024).
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int o = 1; o < NT; o <<= 1) {
-        const int x = t >= o ? sh[t - o] : 0;
-        __syncthreads();
-        sh[t] += x;
-        __syncthreads();
-    }
-    total = sh[NT - 1];
-    const int incl = sh[t];
-    __syncthreads();
-    return incl - v;
-}
-
 struct CandRec {  // 16 B per FAST candidate / selected keypoint
     unsigned xy;  // x | y << 16
     int score;
@@ -192,85 +155,127 @@ struct CandRec {  // 16 B per FAST candidate / selected keypoint
     int pad;
 };
 
+// Wave-scan based exclusive block scan (NT/64 waves, one barrier pair).  sh: >= NT/64 ints.
+template <int NT>
+__device__ __forceinline__ int block_scan_excl(int v, int* sh, int& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) sh[w] = x;
+    __syncthreads();
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) {
+        const int s = sh[i];
+        tot += s;
+        pre += i < w ? s : 0;
+    }
+    total = tot;
+    __syncthreads();
+    return pre + x - v;
+}
+
+// FAST-9/16 + strict 3x3 NMS + border filter + Harris, all levels in one launch.
+// Block = 64 x 16 output tile (4 px halo staged in LDS).  Output is written per cell = (row,
+// tile column) with a fixed capacity of 32 (strict NMS keeps at most every other pixel of a
+// 64 px row segment), so cell order == raster order and the per-row compaction is one ballot.
+constexpr int kTX = 64, kTY = 16, kCellCap = 32;
+constexpr int kTW = kTX + 8, kTH = kTY + 8;   // staged tile
+constexpr int kSW = kTX + 2, kSH = kTY + 2;   // score tile
+
 __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr, LevelArgs a,
                                                  CandRec* __restrict__ cand,
-                                                 int* __restrict__ band_count,
+                                                 int* __restrict__ cell_count,
                                                  int* __restrict__ hist) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ uint8_t tile[kTH * kTW];
+    __shared__ uint8_t sc[kSH * kSW];
+    __shared__ int s_list[kTY * kCellCap];   // (cell slot << 16) | (row << 8) | local x
+    __shared__ int s_n;
     const int b = blockIdx.x;
     int l = 0;
-    while (l + 1 < a.L && b >= a.band_base[l + 1]) ++l;
+    while (l + 1 < a.L && b >= a.tile_base[l + 1]) ++l;
     const int W = a.lw[l], H = a.lh[l];
     const uint8_t* img = pyr + a.off[l];
-    const int R = a.band_rows;
-    const int y0 = (b - a.band_base[l]) * R;
-    const int TW = W + 8;
-    uint8_t* tile = smem;                                 // (R+8) x TW
-    uint8_t* sc = smem + (R + 8) * TW;                     // (R+2) x W scores
-    int* shist = (int*)(smem + (((R + 8) * TW + (R + 2) * W + 15) & ~15));  // 256
-    int* sscan = shist + 256;                              // kBlock
-    const int tid = threadIdx.x;
-
-    for (int i = tid; i < 256; i += kBlock) shist[i] = 0;
-    for (int i = tid; i < (R + 8) * TW; i += kBlock) {
-        const int r = i / TW, c = i - r * TW;
+    const int t = b - a.tile_base[l];
+    const int ntx = a.ntx[l];
+    const int tx = t % ntx, ty = t / ntx;
+    const int x0 = tx * kTX, y0 = ty * kTY;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid == 0) s_n = 0;
+    for (int i = tid; i < kTH * kTW; i += kBlock) {
+        const int r = i / kTW, c = i - r * kTW;
         const int gy = min(max(y0 - 4 + r, 0), H - 1);
-        const int gx = min(max(c - 4, 0), W - 1);
+        const int gx = min(max(x0 - 4 + c, 0), W - 1);
         tile[i] = img[(long long)gy * W + gx];
     }
     __syncthreads();
     const int thr = a.fast_threshold;
-    for (int i = tid; i < (R + 2) * W; i += kBlock) {
-        const int rr = i / W, x = i - rr * W;
-        const int y = y0 - 1 + rr;
+    for (int i = tid; i < kSH * kSW; i += kBlock) {
+        const int r = i / kSW, c = i - r * kSW;
+        const int y = y0 - 1 + r, x = x0 - 1 + c;
         int s = 0;
-        if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3)
-            s = fast_score(tile + (rr + 3) * TW + x + 4, TW, thr);
+        if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) s = fast_score(tile + (r + 3) * kTW + c + 3, kTW, thr);
         sc[i] = (uint8_t)s;
     }
     __syncthreads();
-    // NMS + border filter over the band's R x W pixels, contiguous raster chunk per thread.
-    const int npx = R * W;
-    const int chunk = (npx + kBlock - 1) / kBlock;
-    const int p0 = tid * chunk, p1 = min(p0 + chunk, npx);
     const int e = a.edge;
-    auto is_cand = [&](int p, int& sout) -> bool {
-        const int r = p / W, x = p - r * W;
-        const int y = y0 + r;
-        if (y >= H || y < e || y >= H - e || x < e || x >= W - e) return false;
-        const uint8_t* q = sc + (r + 1) * W + x;
-        const int s = q[0];
-        if (!s) return false;
-        if (!(s > q[-1] && s > q[1] && s > q[-W - 1] && s > q[-W] && s > q[-W + 1] &&
-              s > q[W - 1] && s > q[W] && s > q[W + 1]))
-            return false;
-        sout = s;
-        return true;
-    };
-    int cnt = 0;
-    for (int p = p0; p < p1; ++p) {
-        int s;
-        cnt += is_cand(p, s);
+    for (int r = wv; r < kTY; r += kBlock / 64) {
+        const int y = y0 + r, x = x0 + lane;
+        bool is_c = false;
+        if (y >= e && y < H - e && x >= e && x < W - e) {
+            const uint8_t* q = sc + (r + 1) * kSW + lane + 1;
+            const int s = q[0];
+            is_c = s && s > q[-1] && s > q[1] && s > q[-kSW - 1] && s > q[-kSW] && s > q[-kSW + 1] &&
+                   s > q[kSW - 1] && s > q[kSW] && s > q[kSW + 1];
+        }
+        const unsigned long long m = __ballot(is_c);
+        if (y < H && lane == 0) cell_count[a.cell_base[l] + y * ntx + tx] = __popcll(m);
+        if (is_c) {
+            const int rank = __popcll(m & ((1ull << lane) - 1ull));
+            const int j = atomicAdd(&s_n, 1);
+            s_list[j] = (rank << 16) | (r << 8) | lane;
+        }
     }
-    int total;
-    int pos = block_exclusive_scan<kBlock>(cnt, sscan, total);
-    CandRec* out = cand + a.cand_base[l] + (long long)(b - a.band_base[l]) * a.band_cap[l];
-    for (int p = p0; p < p1; ++p) {
-        int s;
-        if (!is_cand(p, s)) continue;
-        const int r = p / W, x = p - r * W;
-        CandRec c;
-        c.xy = (unsigned)x | ((unsigned)(y0 + r) << 16);
-        c.score = s;
-        c.harris = harris_tile(tile + (r + 4) * TW + x + 4, TW);
-        c.pad = 0;
-        out[pos++] = c;
-        atomicAdd(&shist[s], 1);
-    }
-    if (tid == 0) band_count[b] = total;
     __syncthreads();
-    for (int i = tid; i < 256; i += kBlock)
-        if (shist[i]) atomicAdd(&hist[l * 256 + i], shist[i]);
+    // Harris 7x7 (HarrisResponses): one wave per candidate, lane < 49 takes one window pixel.
+    const int n = s_n;
+    const int dy = lane / 7 - 3, dx = lane % 7 - 3;
+    for (int j = wv; j < n; j += kBlock / 64) {
+        const int v = s_list[j];
+        const int xl = v & 255, r = (v >> 8) & 255, rank = v >> 16;
+        int ia = 0, ib = 0, ic = 0;
+        if (lane < 49) {
+            const uint8_t* p = tile + (r + 4 + dy) * kTW + xl + 4 + dx;
+            const int Ix = (p[1] - p[-1]) * 2 + (p[-kTW + 1] - p[-kTW - 1]) + (p[kTW + 1] - p[kTW - 1]);
+            const int Iy = (p[kTW] - p[-kTW]) * 2 + (p[kTW - 1] - p[-kTW - 1]) + (p[kTW + 1] - p[-kTW + 1]);
+            ia = Ix * Ix;
+            ib = Iy * Iy;
+            ic = Ix * Iy;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            ia += __shfl_xor(ia, o, 64);
+            ib += __shfl_xor(ib, o, 64);
+            ic += __shfl_xor(ic, o, 64);
+        }
+        if (lane == 0) {
+            const float scale = 1.f / ((1 << 2) * 7 * 255.f);
+            const float s4 = scale * scale * scale * scale;
+            const float fa = (float)ia, fb = (float)ib, fc = (float)ic;
+            const int s = sc[(r + 1) * kSW + xl + 1];
+            CandRec c;
+            c.xy = (unsigned)(x0 + xl) | ((unsigned)(y0 + r) << 16);
+            c.score = s;
+            c.harris = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
+            c.pad = 0;
+            cand[(long long)(a.cell_base[l] + (y0 + r) * ntx + tx) * kCellCap + rank] = c;
+            atomicAdd(&hist[l * 256 + s], 1);
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------ blur
@@ -342,81 +347,78 @@ __device__ __forceinline__ float key2f(unsigned k) {
 
 constexpr int kSelBlock = 1024;
 
+// Descending-digit search over a 256-bin histogram held by threads 0..255: returns (via the
+// block) the largest digit d with count(bins >= d) >= k, and the count strictly above d.
+__device__ __forceinline__ void find_digit(int bin_count_desc, int k, int* sh, int* s_out) {
+    int tot;
+    const int ex = block_scan_excl<kSelBlock>(bin_count_desc, sh, tot);
+    const int tid = threadIdx.x;
+    if (tid < 256 && ex < k && ex + bin_count_desc >= k) {
+        s_out[0] = 255 - tid;
+        s_out[1] = ex;
+    }
+    __syncthreads();
+}
+
+// One workgroup per level: retainBest(2q) by FAST score, then retainBest(q) by Harris, both as
+// the exact OpenCV sets {response >= k-th largest}, kept in raster (cell) order.
 __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict__ cand,
-                                                      const int* __restrict__ band_count,
+                                                      const int* __restrict__ cell_count,
                                                       const int* __restrict__ hist, LevelArgs a,
                                                       CandRec* __restrict__ stage,
                                                       int* __restrict__ level_count) {
-    __shared__ int sscan[kSelBlock];
-    __shared__ int sband[1024 + 1];
-    __shared__ int sh[257];
-    __shared__ int s_misc[8];
+    __shared__ int sw[kSelBlock / 64];
+    __shared__ int sh[256];
+    __shared__ int s_out[2];
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
-    const int nb = a.nbands[l];
-    const CandRec* c0 = cand + a.cand_base[l];
-    CandRec* kept = stage + 2 * a.cand_base[l];                 // retainBest(2q) result
-    CandRec* fin = stage + 2 * a.cand_base[l] + a.level_cap[l]; // retainBest(q) result
-    // band prefix (nb <= 1024 checked on the host)
-    int tot;
-    {
-        const int v = tid < nb ? band_count[a.band_base[l] + tid] : 0;
-        const int ex = block_exclusive_scan<kSelBlock>(v, sscan, tot);
-        if (tid < nb) sband[tid] = ex;
-        if (tid == 0) sband[nb] = tot;
-    }
-    __syncthreads();
-    const int n = tot;
+    const int ncell = a.lh[l] * a.ntx[l];
+    const long long cbase = a.cell_base[l];
+    CandRec* kept = stage + a.stage_base[l];                      // retainBest(2q) result
+    CandRec* fin = stage + a.stage_base[l] + a.level_cap[l];      // retainBest(q) result
     const int q = a.quota[l];
     const int k1 = 2 * q;
-    // ---- retainBest(k1) by FAST score: threshold from the level histogram
-    if (tid == 0) s_misc[0] = 0;
-    if (tid < 256) sh[tid] = hist[l * 256 + tid];
-    __syncthreads();
-    int thr1 = 0;
-    bool keep_none = false;
-    if (k1 == 0) {
-        keep_none = n > 0;  // retainBest(0) clears
-    } else if (n > k1) {
-        // suffix sums: cum[s] = sum_{b >= s} hist[b]; thr1 = max s with cum[s] >= k1
-        if (tid < 256) sscan[tid] = sh[255 - tid];
-        __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {
-            const int x = (tid < 256 && tid >= o) ? sscan[tid - o] : 0;
-            __syncthreads();
-            if (tid < 256) sscan[tid] += x;
-            __syncthreads();
-        }
-        // sscan[i] = cum[255 - i]; find smallest i with cum >= k1 -> s = 255 - i
-        if (tid < 256) {
-            const bool ok = sscan[tid] >= k1;
-            const bool prev = tid > 0 ? sscan[tid - 1] >= k1 : false;
-            if (ok && !prev) s_misc[0] = 255 - tid;
-        }
-        __syncthreads();
-        thr1 = s_misc[0];
-        __syncthreads();
+    // ---- level histogram of FAST scores (border-passing NMS corners) -> n and thr1
+    const int hv = tid < 256 ? hist[l * 256 + 255 - tid] : 0;
+    int n;
+    {
+        int ex = block_scan_excl<kSelBlock>(hv, sw, n);
+        (void)ex;
     }
-    // ---- gather kept candidates in raster order
+    int thr1 = 0;
+    if (n > k1 && k1 > 0) {
+        if (tid == 0) s_out[0] = 0;
+        find_digit(hv, k1, sw, s_out);
+        thr1 = s_out[0];
+    }
+    // ---- gather kept candidates (score >= thr1) in raster order
     int K1 = 0;
-    if (!keep_none) {
-        for (int base = 0; base < n; base += kSelBlock) {
-            const int j = base + tid;
-            CandRec r{};
-            int f = 0;
-            if (j < n) {
-                int lo = 0, hi = nb - 1;  // band with sband[bi] <= j < sband[bi+1]
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (sband[mid] <= j) lo = mid; else hi = mid - 1;
-                }
-                r = c0[(long long)lo * a.band_cap[l] + (j - sband[lo])];
-                f = r.score >= thr1;
+    if (k1 > 0) {
+        // each thread owns kCellsPer consecutive cells: all their counts are loaded at once
+        // (static register indices), so one pass costs two dependent load steps, not 2 per cell
+        constexpr int kCellsPer = 6;
+        for (int base = 0; base < ncell; base += kSelBlock * kCellsPer) {
+            const int c0 = base + tid * kCellsPer;
+            int cnts[kCellsPer];
+#pragma unroll
+            for (int j = 0; j < kCellsPer; ++j) cnts[j] = (c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
+            int kc = 0;
+#pragma unroll
+            for (int j = 0; j < kCellsPer; ++j) {
+                const CandRec* cr = cand + (cbase + c0 + j) * kCellCap;
+                for (int i = 0; i < cnts[j]; ++i) kc += cr[i].score >= thr1;
             }
-            int cnt;
-            const int pos = block_exclusive_scan<kSelBlock>(f, sscan, cnt);
-            if (f) kept[K1 + pos] = r;
-            K1 += cnt;
+            int tot;
+            int pos = K1 + block_scan_excl<kSelBlock>(kc, sw, tot);
+#pragma unroll
+            for (int j = 0; j < kCellsPer; ++j) {
+                const CandRec* cr = cand + (cbase + c0 + j) * kCellCap;
+                for (int i = 0; i < cnts[j]; ++i) {
+                    const CandRec r = cr[i];
+                    if (r.score >= thr1) kept[pos++] = r;
+                }
+            }
+            K1 += tot;
         }
     }
     __syncthreads();
@@ -425,7 +427,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     if (q > 0 && K1 > 0) {
         float thr2 = -INFINITY;
         if (K1 > q) {
-            // exact k-th largest (k = q) of the float keys: 4-pass radix select, 8 bits per pass
+            // exact q-th largest float key: 4-pass radix select, 8 bits per pass
             unsigned prefix = 0, mask = 0;
             int k = q;
             for (int shift = 24; shift >= 0; shift -= 8) {
@@ -436,26 +438,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
                     if ((key & mask) == prefix) atomicAdd(&sh[(key >> shift) & 255], 1);
                 }
                 __syncthreads();
-                // descending digit suffix sums
-                if (tid < 256) sscan[tid] = sh[255 - tid];
-                __syncthreads();
-                for (int o = 1; o < 256; o <<= 1) {
-                    const int x = (tid < 256 && tid >= o) ? sscan[tid - o] : 0;
-                    __syncthreads();
-                    if (tid < 256) sscan[tid] += x;
-                    __syncthreads();
-                }
-                if (tid < 256) {
-                    const bool ok = sscan[tid] >= k;
-                    const bool prev = tid > 0 ? sscan[tid - 1] >= k : false;
-                    if (ok && !prev) {
-                        s_misc[1] = 255 - tid;                         // digit
-                        s_misc[2] = tid > 0 ? sscan[tid - 1] : 0;      // count above the digit
-                    }
-                }
-                __syncthreads();
-                const unsigned digit = (unsigned)s_misc[1];
-                k -= s_misc[2];
+                const int v = tid < 256 ? sh[255 - tid] : 0;
+                find_digit(v, k, sw, s_out);
+                const unsigned digit = (unsigned)s_out[0];
+                k -= s_out[1];
                 prefix |= digit << shift;
                 mask |= 255u << shift;
                 __syncthreads();
@@ -471,7 +457,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
                 f = r.harris >= thr2;
             }
             int cnt;
-            const int pos = block_exclusive_scan<kSelBlock>(f, sscan, cnt);
+            const int pos = block_scan_excl<kSelBlock>(f, sw, cnt);
             if (f) fin[K2 + pos] = r;
             K2 += cnt;
         }
@@ -530,7 +516,7 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
         slot_count[1] = total > a.out_cap;
     }
     if (l < 0 || w >= a.out_cap) return;
-    const CandRec r = stage[2 * a.cand_base[l] + a.level_cap[l] + j];
+    const CandRec r = stage[a.stage_base[l] + a.level_cap[l] + j];
     const int W = a.lw[l];
     const int xl = (int)(r.xy & 0xffffu), yl = (int)(r.xy >> 16);
     const uint8_t* img = pyr + a.off[l];
@@ -661,13 +647,12 @@ LevelArgs level_args(const OrbGeometry& g) {
         a.scale[l] = g.scale[l];
         a.inv_scale[l] = g.inv_scale[l];
         a.quota[l] = g.quota[l];
-        a.nbands[l] = g.nbands[l];
-        a.band_base[l] = g.band_base[l];
-        a.band_cap[l] = g.band_cap[l];
-        a.cand_base[l] = g.cand_base[l];
+        a.ntx[l] = g.ntx[l];
+        a.tile_base[l] = g.tile_base[l];
+        a.cell_base[l] = g.cell_base[l];
+        a.stage_base[l] = g.stage_base[l];
         a.level_cap[l] = g.level_cap[l];
     }
-    a.band_rows = g.band_rows;
     a.fast_threshold = std::min(std::max(g.p.fast_threshold, 0), 255);
     a.edge = g.p.edge_threshold;
     a.out_cap = g.out_cap;
@@ -759,24 +744,25 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
         all.insert(all.end(), t.begin(), t.end());
     }
     g.tab_entries = (int64_t)all.size();
-    // FAST bands
-    g.band_rows = 8;
-    int bands = 0;
-    int64_t cb = 0;
+    // FAST tiles / cells and selection staging
+    int tiles = 0;
+    int64_t cells = 0, stg = 0;
     g.max_w = 0;
     for (int l = 0; l < g.L; ++l) {
-        g.nbands[l] = (g.lh[l] + g.band_rows - 1) / g.band_rows;
-        if (g.nbands[l] > 1024) return set_error(c, VX_ERR_INVALID, "too many bands");
-        g.band_base[l] = bands;
-        bands += g.nbands[l];
-        g.band_cap[l] = (g.band_rows / 2 + 1) * (g.lw[l] / 2 + 1);
-        g.level_cap[l] = g.band_cap[l] * g.nbands[l];
-        g.cand_base[l] = cb;
-        cb += g.level_cap[l];
+        g.ntx[l] = (g.lw[l] + kTX - 1) / kTX;
+        g.nty[l] = (g.lh[l] + kTY - 1) / kTY;
+        g.tile_base[l] = tiles;
+        tiles += g.ntx[l] * g.nty[l];
+        g.cell_base[l] = cells;
+        cells += (int64_t)g.lh[l] * g.ntx[l];
+        g.level_cap[l] = (g.lw[l] / 2 + 1) * (g.lh[l] / 2 + 1);
+        g.stage_base[l] = stg;
+        stg += 2 * (int64_t)g.level_cap[l];
         g.max_w = std::max(g.max_w, g.lw[l]);
     }
-    g.total_bands = bands;
-    g.cand_total = cb;
+    g.total_tiles = tiles;
+    g.cells_total = cells;
+    g.stage_total = stg;
     g.out_cap = 2 * p->n_features + 256;
 
     VX_HIP(c, c->tabs.ensure(std::max<int64_t>(1, g.tab_entries) * sizeof(int4)));
@@ -784,9 +770,9 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
         VX_HIP(c, hipMemcpy(c->tabs.p, all.data(), all.size() * sizeof(int4), hipMemcpyHostToDevice));
     VX_HIP(c, c->pyr.ensure(g.pyr_bytes));
     VX_HIP(c, c->blur.ensure(g.pyr_bytes));
-    VX_HIP(c, c->cand.ensure(g.cand_total * sizeof(CandRec)));
-    VX_HIP(c, c->stage.ensure(2 * g.cand_total * sizeof(CandRec)));
-    VX_HIP(c, c->band_count.ensure(bands * sizeof(int)));
+    VX_HIP(c, c->cand.ensure(g.cells_total * kCellCap * sizeof(CandRec)));
+    VX_HIP(c, c->stage.ensure(g.stage_total * sizeof(CandRec)));
+    VX_HIP(c, c->band_count.ensure(g.cells_total * sizeof(int)));
     VX_HIP(c, c->hist.ensure(g.L * 256 * sizeof(int)));
     VX_HIP(c, c->level_count.ensure(kMaxLevels * sizeof(int)));
     for (auto& s : c->slots) {
@@ -825,10 +811,7 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
     VX_HIP(c, hipMemsetAsync(c->hist.p, 0, g.L * 256 * sizeof(int), c->stream));
     {
         ProfScope ps(c, kStFast);
-        const int R = g.band_rows;
-        const size_t lds = (((size_t)(R + 8) * (g.max_w + 8) + (size_t)(R + 2) * g.max_w + 15) & ~size_t(15)) +
-                           (256 + kBlock) * sizeof(int);
-        hipLaunchKernelGGL(k_fast, dim3(g.total_bands), dim3(kBlock), lds, c->stream, pyr, a,
+        hipLaunchKernelGGL(k_fast, dim3(g.total_tiles), dim3(kBlock), 0, c->stream, pyr, a,
                            c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>());
         VX_LAUNCH_CHECK(c, "k_fast");
     }

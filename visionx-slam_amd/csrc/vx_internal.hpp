@@ -90,15 +90,15 @@ struct OrbGeometry {
     // resize tables for levels 1..L-1: int4 {ofs, c0, c1, 0} per destination column / row
     int64_t xtab[kMaxLevels], ytab[kMaxLevels];
     int64_t tab_entries = 0;
-    // FAST bands: band_rows rows x full width per workgroup
-    int band_rows = 8;
-    int nbands[kMaxLevels];
-    int band_base[kMaxLevels];     // first band index of level l
-    int total_bands = 0;
-    int band_cap[kMaxLevels];      // candidate capacity per band of level l
-    int64_t cand_base[kMaxLevels]; // first candidate slot of level l
-    int64_t cand_total = 0;
-    int level_cap[kMaxLevels];     // candidate capacity of level l (for the selection staging)
+    // FAST tiles (64 x 16 pixels per workgroup) and output cells (row x tile column)
+    int ntx[kMaxLevels], nty[kMaxLevels];
+    int tile_base[kMaxLevels];     // first tile (workgroup) of level l
+    int total_tiles = 0;
+    int64_t cell_base[kMaxLevels]; // first cell of level l
+    int64_t cells_total = 0;
+    int level_cap[kMaxLevels];     // max strict-NMS corners of level l
+    int64_t stage_base[kMaxLevels];// selection staging (2 * level_cap records) of level l
+    int64_t stage_total = 0;
     int max_w = 0;
     int out_cap = 0;               // keypoint capacity of one slot
 };

@@ -1,0 +1,109 @@
+// feature.h — the reference's plugin interfaces and their MI355X implementations.
+//
+//   FeatureExtractor  core/feature/feature_extractor.h:10-16   (virtual void Extract(Frame&))
+//   FeatureMatcher    core/feature/feature_matcher.h:7-13      (virtual int Match(last, curr, matches))
+//   ORBExtractor      core/feature/orb_extractor.h:9-19        -> vx_orb_extract (include/vx_slam.h)
+//   ORBMatcher        core/feature/orb_matcher.h:11-26         -> vx_match_knn2_ratio
+//   LocalBA           core/backend/local_ba.h:10-27            -> vx_ba_optimize_map
+//
+// Same class names, constructor defaults and member signatures as the reference, so
+// core/system/system.cpp:15-16 and core/frontend/tracking.cpp:25-34 compile against them
+// unchanged.  Device work goes through one vx_ctx per calling thread (the reference runs the hot
+// path on its single tracking thread, core/system/system.cpp:39-52).
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "vx_slam.h"
+#include "visionx/frame.h"
+
+namespace visionx {
+
+class FeatureExtractor {
+public:
+    using Ptr = std::shared_ptr<FeatureExtractor>;
+    virtual ~FeatureExtractor() = default;
+    virtual void Extract(Frame& frame) = 0;
+};
+
+class FeatureMatcher {
+public:
+    using Ptr = std::shared_ptr<FeatureMatcher>;
+    virtual ~FeatureMatcher() = default;
+    virtual int Match(const Frame::Ptr& last, const Frame::Ptr& curr, std::vector<DMatch>& matches) = 0;
+};
+
+class ORBExtractor : public FeatureExtractor {
+public:
+    ORBExtractor(int n_features = 1000, float scale_factor = 1.2f, int n_levels = 8);
+    void Extract(Frame& frame) override;
+
+private:
+    vx_orb_params params_;
+    std::vector<vx_keypoint> kp_;
+    std::vector<uint8_t> desc_;
+};
+
+class ORBMatcher : public FeatureMatcher {
+public:
+    struct Options {
+        float nn_ratio = 0.8f;
+        int min_matches = 50;
+    };
+    ORBMatcher() : ORBMatcher(Options()) {}
+    explicit ORBMatcher(const Options& options);
+    int Match(const Frame::Ptr& last, const Frame::Ptr& curr, std::vector<DMatch>& matches) override;
+
+private:
+    Options options_;
+    std::vector<vx_match> buf_;
+};
+
+// Flattened window of a Map (what LocalBA::Optimize can read or write), laid out as vx_map_view.
+struct FlatMap {
+    std::vector<uint64_t> kf_id;
+    std::vector<double> kf_pose, kf_intr;
+    std::vector<uint8_t> kf_has_cam;
+    std::vector<int64_t> kf_feat_ptr;
+    std::vector<double> feat_uv;
+    std::vector<uint64_t> feat_lm_id;
+    std::vector<uint8_t> feat_flags;
+    std::vector<uint64_t> lm_id;
+    std::vector<double> lm_pos;
+    std::vector<uint8_t> lm_bad;
+    std::vector<int64_t> lm_obs_ptr;
+    std::vector<uint64_t> obs_kf_id, obs_feat_idx;
+    std::vector<Frame::Ptr> frames;        // keyframes in kf_id order
+    std::vector<Landmark::Ptr> landmarks;  // landmarks in lm_id order
+    vx_map_view view();                    // pointers into the vectors above
+};
+
+class LocalBA {
+public:
+    struct Options {
+        int window_size = 5;
+        int max_iterations = 5;
+        int min_pose_observations = 20;
+        int min_point_observations = 2;
+        double huber_delta = 5.0;
+        double max_reproj_error = 5.0;
+    };
+    explicit LocalBA(const Options& options) : options_(options) {}
+    void Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf);
+
+    // The keyframes SelectKeyFrames picks (local_ba.cpp:71-91), every landmark their features
+    // reference, and those landmarks' full observation maps.
+    static FlatMap Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size);
+    const vx_ba_stats& LastStats() const { return stats_; }
+
+private:
+    Options options_;
+    vx_ba_stats stats_{};
+};
+
+namespace vxhost {
+vx_ctx* ThreadContext();  // the calling thread's context (device $VX_DEVICE, default 0)
+}
+
+}  // namespace visionx
