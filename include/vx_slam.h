@@ -14,7 +14,7 @@
  *                            ORBMatcher::Match + Options         core/feature/orb_matcher.cpp:11-43,
  *                                                                orb_matcher.h:11-14
  *   vx_ba_optimize_map    <- LocalBA::Optimize(map, ref_kf)      core/backend/local_ba.h:23,
- *                                                                local_ba.cpp:95-278
+ *                                                                local_ba.cpp:66-249
  *                            LocalBA::Options                    core/backend/local_ba.h:12-19
  *
  * The host-side C++ adapters that keep the reference call surface (same class names and
@@ -111,8 +111,8 @@ int vx_match_slots_async(vx_ctx* ctx, int query_slot, int train_slot, float rati
 int vx_match_fetch(vx_ctx* ctx, vx_match* out, int cap, int* n_out);
 
 /* ---------------------------------------------------------------- local bundle adjustment
- * A flattened snapshot of visionx::Map (map.h:13-35): keyframes with their Feature vectors
- * (frame.h:16-23) and landmarks with their observation maps (landmark.h:300-318).  Keyframes may
+ * A flattened snapshot of visionx::Map (map.h:13-34): keyframes with their Feature vectors
+ * (frame.h:16-23) and landmarks with their observation maps (landmark.h:12-68).  Keyframes may
  * be in any order (the reference's std::map sorts them by id).  kf_pose and lm_pos are updated
  * in place, exactly as Frame::SetPose / Landmark::SetPosition would be. */
 typedef struct {
@@ -156,7 +156,7 @@ void vx_ba_default_options(vx_ba_options* o);
 int vx_ba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                        const vx_ba_options* opt, vx_ba_stats* stats);
 
-/* Staged form: plan = window selection + device CSR upload (host work of local_ba.cpp:95-137);
+/* Staged form: plan = window selection + device CSR upload (host work of local_ba.cpp:66-108);
  * run = the iterations on the device from the plan's initial state (repeatable);
  * fetch = download + scatter back into `map` (may be NULL to only read stats).
  * shard_count > 1 keeps only this rank's landmark shard (landmark id hash) and all-reduces the

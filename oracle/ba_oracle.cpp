@@ -1,16 +1,16 @@
 // ba_oracle.cpp — CPU restatement of LocalBA::Optimize.  TEST INFRASTRUCTURE ONLY.
 //
-// Line-for-line restatement of /root/reference/core/backend/local_ba.cpp:95-278 (alternating
+// Line-for-line restatement of /root/reference/core/backend/local_ba.cpp:66-249 (alternating
 // pose / landmark Gauss-Newton, including the reference's b = -J^T e step sign :185,:253, the
 // 5 px gate :177,:243 and the relative-cost stop :269-276), ProjectToPixel
 // (core/common/projection.h:11-31), ProjectionJacobian / PoseJacobian / HuberWeight
-// (local_ba.cpp:44-69) and SelectKeyFrames (:71-91).  Third-party pieces restated from their
+// (local_ba.cpp:15-40) and SelectKeyFrames (:42-62).  Third-party pieces restated from their
 // published algorithms (Eigen 3 / Sophus, unpinned versions, vcpkg.json):
 //   - Eigen::LDLT (diagonal pivoting, ldlt_inplace::unblocked + _solve_impl),
 //   - Sophus::SE3d::exp / SO3::expAndTheta, SO3 product with renormalisation,
 //     quaternion point rotation (Eigen _transformVector), Quaternion::toRotationMatrix.
 // The landmark-observation iteration order of the reference is std::unordered_map order
-// (landmark.h:316-318) and therefore implementation-defined; this oracle uses the snapshot
+// (landmark.h:47-48,65) and therefore implementation-defined; this oracle uses the snapshot
 // order.  Build: -O2 -ffp-contract=off.
 #include "oracle.h"
 
@@ -106,7 +106,7 @@ SE3 se3_exp(const double a[6]) {
     return T;
 }
 
-// exp(dx) * T   (local_ba.cpp:202)
+// exp(dx) * T   (local_ba.cpp:173)
 SE3 left_update(const double dx[6], const SE3& T) {
     const SE3 E = se3_exp(dx);
     SE3 R;
@@ -187,14 +187,14 @@ inline bool project(const Cam& c, const SE3& T, const Vec3& pw, double uv[2], Ve
     return true;
 }
 
-// ProjectionJacobian (local_ba.cpp:44-53), row-major 2x3
+// ProjectionJacobian (local_ba.cpp:15-24), row-major 2x3
 inline void proj_jac(const Cam& c, const Vec3& pc, double J[6]) {
     const double x = pc.x, y = pc.y, z = pc.z, z2 = z * z;
     J[0] = c.fx / z; J[1] = 0.0;        J[2] = -c.fx * x / z2;
     J[3] = 0.0;      J[4] = c.fy / z;   J[5] = -c.fy * y / z2;
 }
 
-// PoseJacobian (local_ba.cpp:55-62): Jp * [I | -hat(pc)], row-major 2x6
+// PoseJacobian (local_ba.cpp:26-33): Jp * [I | -hat(pc)], row-major 2x6
 inline void pose_jac(const Cam& c, const Vec3& pc, double J[12]) {
     double Jp[6];
     proj_jac(c, pc, Jp);
@@ -206,7 +206,7 @@ inline void pose_jac(const Cam& c, const Vec3& pc, double J[12]) {
             J[6 * r + col] = Jp[3 * r] * S[col] + Jp[3 * r + 1] * S[6 + col] + Jp[3 * r + 2] * S[12 + col];
 }
 
-inline double huber(double e, double d) { return e <= d ? 1.0 : d / e; }  // local_ba.cpp:64-69
+inline double huber(double e, double d) { return e <= d ? 1.0 : d / e; }  // local_ba.cpp:35-40
 
 }  // namespace
 
@@ -225,7 +225,7 @@ extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_
     std::unordered_map<uint64_t, int> lm_by_id;
     for (int i = 0; i < m->n_lm; ++i) lm_by_id[m->lm_id[i]] = i;
 
-    // SelectKeyFrames (local_ba.cpp:71-91)
+    // SelectKeyFrames (local_ba.cpp:42-62)
     const int window = std::max(1, (int)opt->window_size);
     const uint64_t max_id = has_ref ? ref_kf_id : kf_by_id.rbegin()->first;
     std::vector<int> kfs;
@@ -239,7 +239,7 @@ extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_
     std::unordered_set<uint64_t> local_ids;
     for (int k : kfs) local_ids.insert(m->kf_id[k]);
 
-    // landmark set (local_ba.cpp:112-137)
+    // landmark set (local_ba.cpp:83-108)
     std::unordered_set<uint64_t> lm_ids;
     for (int k : kfs)
         for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f)
@@ -282,7 +282,7 @@ extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_
         int total_obs = 0;
         st->iterations = iter + 1;
 
-        // === Pose optimization (fix landmarks) === local_ba.cpp:145-203
+        // === Pose optimization (fix landmarks) === local_ba.cpp:116-174
         for (int k : kfs) {
             if (!m->kf_has_cam[k]) continue;
             const Cam cam = cam_of(k);
@@ -320,7 +320,7 @@ extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_
             set_pose(k, left_update(dx, pose_of(k)));
         }
 
-        // === Landmark optimization (fix poses) === local_ba.cpp:205-267
+        // === Landmark optimization (fix poses) === local_ba.cpp:176-238
         for (int l : lms) {
             if (m->lm_bad[l]) continue;
             double H[9] = {0}, b[3] = {0};

@@ -15,7 +15,7 @@
  *     ships no tests, fixtures or golden vectors for this path.
  *   - ORBMatcher::Match (core/feature/orb_matcher.cpp:11-43): BFMatcher(NORM_HAMMING)
  *     knnMatch(k=2) + ratio test.  Unpinned vs OpenCV for the same reason.
- *   - LocalBA::Optimize (core/backend/local_ba.cpp:95-278) + ProjectToPixel
+ *   - LocalBA::Optimize (core/backend/local_ba.cpp:66-249) + ProjectToPixel
  *     (core/common/projection.h:11-31), line for line, with Eigen LDLT and Sophus SE3::exp
  *     restated.  Pinned by the reference source itself (fully visible).
  */

@@ -1,7 +1,7 @@
 """The C++ drop-in adapters (visionx::ORBExtractor / ORBMatcher / LocalBA over the C ABI) driven
 the way core/frontend/tracking.cpp drives the reference classes, through tests/cpp/adapter_driver.
 
-CPU: LocalBA::Flatten (the host gather that replaces local_ba.cpp:71-137's map walk) selects the
+CPU: LocalBA::Flatten (the host gather that replaces local_ba.cpp:42-108's map walk) selects the
 same window / landmark set as the oracle.  GPU: Extract / Match / Optimize through the adapters
 equal the CPU restatement (bit-exact ORB and matches, BA within 1e-4).
 """

@@ -70,7 +70,7 @@ def test_bench_harness_max_over_ranks():
 
 
 def pose_normal_equations(m, opts_window, lm_subset=None):
-    """Per-window-keyframe 29-term blocks of the first pose stage (local_ba.cpp:160-190), numpy."""
+    """Per-window-keyframe 29-term blocks of the first pose stage (local_ba.cpp:131-161), numpy."""
     from vxslam import synth
 
     ids = m["kf_id"]

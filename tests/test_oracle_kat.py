@@ -277,7 +277,7 @@ def _quat_to_mat(q):
 
 def test_ba_pose_step_matches_numpy_gauss_newton_with_reference_sign(oracle):
     """After one iteration the pose equals exp(dx) * T with dx = LDLT(J^T J + 1e-6 I)^-1 (-J^T e)
-    (local_ba.cpp:176-202): derived here independently in numpy."""
+    (local_ba.cpp:146-173): derived here independently in numpy."""
     m = synth.make_ba_map(2, 3, 300, n_old_kf=0, frac_outlier=0.0, frac_bad=0.0, frac_single=0.0)
     opts = oracle.ba_options(window=3, iters=1)
     m0 = m.copy()

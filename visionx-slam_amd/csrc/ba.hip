@@ -1,12 +1,12 @@
 // ba.hip — sliding-window bundle adjustment on gfx950 (LocalBA::Optimize drop-in).
 //
-// Replaces LocalBA::Optimize (core/backend/local_ba.cpp:95-278).  The reference alternates a
-// per-keyframe 6x6 Gauss-Newton step with landmarks fixed (:145-203) and a per-landmark 3x3 step
-// with poses fixed (:205-267), up to max_iterations times with a relative-cost stop (:269-276).
+// Replaces LocalBA::Optimize (core/backend/local_ba.cpp:66-249).  The reference alternates a
+// per-keyframe 6x6 Gauss-Newton step with landmarks fixed (:116-174) and a per-landmark 3x3 step
+// with poses fixed (:176-238), up to max_iterations times with a relative-cost stop (:240-247).
 // Both stages are embarrassingly parallel, so the device problem is two CSR views of the window:
 //
-//   host   plan:  SelectKeyFrames (:71-91) + landmark filtering (:106-137) + the per-observation
-//                 validity checks that are static during Optimize (:160-167, :215-233) ->
+//   host   plan:  SelectKeyFrames (:42-62) + landmark filtering (:93-104) + the per-observation
+//                 validity checks that are static during Optimize (:131-138, :186-204) ->
 //                 keyframe-major pose observations (uv, landmark slot) and landmark-major
 //                 observations (uv, keyframe row); uploaded once, replayed by every run.
 //   device run (per iteration it; every kernel early-exits once the stop rule has fired):
@@ -22,7 +22,7 @@
 //                      per thread (2x3 Jacobian Jp*R, 3x3 normal equations, LDLT, p += dp) against
 //                      those poses; workgroup 0 publishes the poses and evaluates the stop rule.
 //                      Windows beyond kMaxKfLds keyframes use k_pose_solve_g + k_landmark instead.
-// The step keeps the reference's sign (b = -J^T e, :185 and :253): this is a drop-in, not a fix.
+// The step keeps the reference's sign (b = -J^T e, :156 and :224): this is a drop-in, not a fix.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -233,8 +233,8 @@ __device__ void se3_left_update(const double* dx, double* T) {
     T[4] = et[0] + r.x; T[5] = et[1] + r.y; T[6] = et[2] + r.z;
 }
 
-// Pose step of one keyframe from its summed terms S (local_ba.cpp:192-202): skipped below
-// min_pose_observations or without a camera; T updated in place, R = its rotation (:249).
+// Pose step of one keyframe from its summed terms S (local_ba.cpp:163-173): skipped below
+// min_pose_observations or without a camera; T updated in place, R = its rotation (:173, :220).
 __device__ __forceinline__ void solve_pose(const BAArgs& a, int k, const double* S, double* T, double* R) {
     const int obs = (int)S[28];
     if (obs >= a.min_pose_obs && (a.kf_flags[k] & 1)) {
@@ -257,7 +257,7 @@ __device__ __forceinline__ void solve_pose(const BAArgs& a, int k, const double*
     rot_from_quat(T, R);
 }
 
-// Relative-cost stop rule (local_ba.cpp:269-276) -> active[it + 1].
+// Relative-cost stop rule (local_ba.cpp:240-247) -> active[it + 1].
 __device__ void stop_rule(const BAArgs& a, int it, double total, int tobs) {
     BAState* s = a.state;
     if (it < 16) {
@@ -305,7 +305,7 @@ __global__ void k_ba_reset(BAArgs a) {
     }
 }
 
-// Pose stage (local_ba.cpp:145-190): one workgroup per keyframe.  Each thread accumulates the 29
+// Pose stage (local_ba.cpp:116-161): one workgroup per keyframe.  Each thread accumulates the 29
 // terms of its observations (strided) in registers; a fixed-order wave butterfly + LDS tree
 // reduces them into kf_sums[k].
 __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
         const double w = en <= a.huber ? 1.0 : a.huber / en;
         const double z = pc.z, z2 = z * z;
         const double jp0 = fx / z, jp2 = -fx * pc.x / z2, jp4 = fy / z, jp5 = -fy * pc.y / z2;
-        // J = Jp * [I | -hat(pc)] (local_ba.cpp:55-62), formed as the 2x3 * 3x6 product
+        // J = Jp * [I | -hat(pc)] (local_ba.cpp:26-33), formed as the 2x3 * 3x6 product
         const double Jp[6] = {jp0, 0.0, jp2, 0.0, jp4, jp5};
         const double S[18] = {1, 0, 0, 0, pc.z, -pc.y, 0, 1, 0, -pc.z, 0, pc.x, 0, 0, 1, pc.y, -pc.x, 0};
         double J0[6], J1[6];
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     }
 }
 
-// Landmark step of landmark l (local_ba.cpp:205-267) against keyframe tables T/R/C (LDS or
+// Landmark step of landmark l (local_ba.cpp:176-238) against keyframe tables T/R/C (LDS or
 // global memory).
 __device__ __forceinline__ void landmark_step(const BAArgs& a, int l, const double* sT, const double* sR,
                                               const double* sC) {
@@ -568,7 +568,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     const vx_ba_options& o = p->opt;
     p->status = 1;
     if (!m || m->n_kf <= 0) return VX_OK;
-    // ---- SelectKeyFrames (local_ba.cpp:71-91): std::map order = ascending id
+    // ---- SelectKeyFrames (local_ba.cpp:42-62): std::map order = ascending id
     std::vector<int> order(m->n_kf);
     for (int i = 0; i < m->n_kf; ++i) order[i] = i;
     std::sort(order.begin(), order.end(), [&](int x, int y) { return m->kf_id[x] < m->kf_id[y]; });
@@ -585,7 +585,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     std::unordered_map<uint64_t, int> win_row;  // kf id -> device row
     for (int r = 0; r < (int)win.size(); ++r) win_row[m->kf_id[win[r]]] = r;
 
-    // ---- landmark set (local_ba.cpp:112-137)
+    // ---- landmark set (local_ba.cpp:83-108)
     std::unordered_map<uint64_t, int> lm_by_id;
     lm_by_id.reserve((size_t)m->n_lm * 2);
     for (int i = 0; i < m->n_lm; ++i) lm_by_id[m->lm_id[i]] = i;
@@ -621,7 +621,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
         }
     p->n_opt = (int)p->lm_map_idx.size();
 
-    // ---- keyframe table + pose-stage CSR (local_ba.cpp:145-190)
+    // ---- keyframe table + pose-stage CSR (local_ba.cpp:116-161)
     const int nk = (int)win.size();
     p->n_kf = nk;
     p->kf_map_idx = win;
@@ -657,7 +657,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     for (int s = 0; s < p->n_lm; ++s)
         for (int j = 0; j < 3; ++j) lm0[4 * s + j] = m->lm_pos[3 * p->lm_map_idx[s] + j];
 
-    // ---- landmark-stage CSR (local_ba.cpp:215-233)
+    // ---- landmark-stage CSR (local_ba.cpp:186-204)
     std::vector<int> lptr(p->n_opt + 1, 0), lkf;
     std::vector<double2> luv;
     for (int s = 0; s < p->n_opt; ++s) {

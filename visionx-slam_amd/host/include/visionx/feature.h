@@ -92,7 +92,7 @@ public:
     explicit LocalBA(const Options& options) : options_(options) {}
     void Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf);
 
-    // The keyframes SelectKeyFrames picks (local_ba.cpp:71-91), every landmark their features
+    // The keyframes SelectKeyFrames picks (local_ba.cpp:42-62), every landmark their features
     // reference, and those landmarks' full observation maps.
     static FlatMap Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size);
     const vx_ba_stats& LastStats() const { return stats_; }

@@ -1,6 +1,6 @@
 // frame.h / camera.h / landmark.h / map.h mirrors — same member names and locking semantics as
 // the reference data model (core/frame/frame.h:16-64, core/camera/camera.h:8-37,
-// core/map/landmark.h:12-68, core/map/map.h:13-35) over the restated value types.
+// core/map/landmark.h:12-68, core/map/map.h:13-34) over the restated value types.
 #pragma once
 
 #include <map>
@@ -116,7 +116,7 @@ private:
     bool is_bad_ = false;
 };
 
-class Map {  // map.h:13-35
+class Map {  // map.h:13-34
 public:
     using Ptr = std::shared_ptr<Map>;
     void InsertKeyFrame(Frame::Ptr frame) {

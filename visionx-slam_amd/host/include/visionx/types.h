@@ -2,8 +2,8 @@
 // (vcpkg.json:5-15), restated so the host adapters build without those libraries.
 //   Vec2d / Vec3d      <- Eigen::Vector2d / Eigen::Vector3d   (frame.h:18, landmark.h:18)
 //   SE3d               <- Sophus::SE3d (unit quaternion x y z w + translation), T_cw
-//   ImageU8            <- cv::Mat 8UC1 / 8UC3 (frame.h:49-50), row-major, owned
-//   DescriptorMat      <- cv::Mat N x 32 CV_8U (frame.h:51-52)
+//   ImageU8            <- cv::Mat 8UC1 / 8UC3 (frame.h:38), row-major, owned
+//   DescriptorMat      <- cv::Mat N x 32 CV_8U (frame.h:43-44)
 //   DMatch             <- cv::DMatch (feature_matcher.h:12)
 #pragma once
 

@@ -134,7 +134,7 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
     FlatMap f;
     const auto& all = map.KeyFrames();
     if (all.empty()) return f;
-    // SelectKeyFrames (local_ba.cpp:71-91)
+    // SelectKeyFrames (local_ba.cpp:42-62)
     const uint64_t max_id = ref_kf ? ref_kf->Id() : all.rbegin()->first;
     const int window = std::max(1, window_size);
     for (auto it = all.rbegin(); it != all.rend() && (int)f.frames.size() < window; ++it) {
@@ -168,7 +168,7 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
     f.lm_obs_ptr.push_back(0);
     for (uint64_t id : ids) {
         auto lm = map.GetLandmark(id);
-        if (!lm) continue;  // GetLandmark -> nullptr: treated as absent, like local_ba.cpp:126,165
+        if (!lm) continue;  // GetLandmark -> nullptr: treated as absent, like local_ba.cpp:96-97,135-136
         const Vec3d p = lm->Position();
         f.landmarks.push_back(lm);
         f.lm_id.push_back(id);
@@ -186,9 +186,9 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
 void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
     stats_ = vx_ba_stats{};
     stats_.status = 1;
-    if (!map) return;                                            // local_ba.cpp:96-98
+    if (!map) return;                                            // local_ba.cpp:67-69
     FlatMap f = Flatten(*map, ref_kf, options_.window_size);
-    if (f.frames.size() < 2) return;                            // local_ba.cpp:102-104
+    if (f.frames.size() < 2) return;                            // local_ba.cpp:73-75
     vx_ba_options o;
     o.window_size = options_.window_size;
     o.max_iterations = options_.max_iterations;
@@ -200,7 +200,7 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
     vx_ctx* c = vxhost::ThreadContext();
     check(c, vx_ba_optimize_map(c, &v, ref_kf ? ref_kf->Id() : 0, ref_kf ? 1 : 0, &o, &stats_), "vx_ba_optimize_map");
     if (stats_.status != 0) return;
-    // scatter: Frame::SetPose / Landmark::SetPosition (local_ba.cpp:202,266)
+    // scatter: Frame::SetPose / Landmark::SetPosition (local_ba.cpp:173,237)
     for (size_t i = 0; i < f.frames.size(); ++i) {
         const double* p = &f.kf_pose[7 * i];
         SE3d T;

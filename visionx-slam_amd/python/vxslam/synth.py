@@ -5,11 +5,11 @@ and parity test runs on data generated here:
 
 * ``make_texture`` / ``make_frames`` — 640x480 (or any size) BGR8 frames cut from one textured
   plane with a small per-frame camera shift, uint16 depth (metres x 5000, tracking.cpp:603).
-* ``make_ba_map`` — a flattened snapshot of ``visionx::Map`` (core/map/map.h:13-35,
+* ``make_ba_map`` — a flattened snapshot of ``visionx::Map`` (core/map/map.h:13-34,
   landmark.h:12-68, frame.h:16-64) holding a sliding BA window: keyframe poses ``T_cw`` on a
   smooth arc, landmarks observed by 2..5 consecutive keyframes, observations = true projection
   + N(0, 0.5 px) truncated at 1.5 px, poses perturbed by ~0.2 deg / 1 cm and landmarks by 1 cm.
-  It also plants the corner cases LocalBA::Optimize handles (local_ba.cpp:95-278): older
+  It also plants the corner cases LocalBA::Optimize handles (local_ba.cpp:66-249): older
   keyframes outside the window, single-observation landmarks (used by the pose stage only),
   bad landmarks, outlier features and features without a landmark.
 
