@@ -8,6 +8,10 @@ One step = one frame through the hot path, everything resident in HBM before tim
   1. ORBExtractor::Extract of a 640x480 BGR8 frame (n_features 2000 at C3)   -> slot i % 2
   2. ORBMatcher::Match(previous frame, this frame): BF Hamming kNN-2 + ratio -> matches
   3. LocalBA::Optimize over the sliding window (C3: 50 KF / 20k landmarks, <= 5 iterations)
+Steps 1-2 run on a frontend context, step 3 on a backend context (own HIP stream) that waits on
+the device for step 2 of the same frame; LocalBA(t) therefore overlaps Extract/Match(t + 1), which
+do not depend on it (--serial puts everything on one stream).  Every step's work completes inside
+the timed region.
 At N GPUs (weak scaling, "rig" workload): every rank runs steps 1-2 on its own camera stream and
 the ranks jointly run ONE global window of N x 50 KF / N x 20k landmarks per step, landmarks
 sharded across ranks with one RCCL all-reduce of the per-keyframe normal equations per
@@ -49,6 +53,8 @@ def stage_bytes(stage, geo, counts):
     N = counts["n_kp"]
     if stage == "orb_gray":
         return W * H * C + W * H
+    if stage == "orb_pyramid":      # BGR in, every level out
+        return W * H * C + sum(px)
     if stage == "orb_resize":       # average over the L-1 launches
         return sum(px[l - 1] + px[l] for l in range(1, len(px))) / (len(px) - 1)
     if stage == "orb_fast_harris":
@@ -180,6 +186,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=30, help="frames timed for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
+    ap.add_argument("--serial", action="store_true",
+                    help="one context/stream for everything (no Extract/Match || LocalBA overlap)")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -189,7 +197,11 @@ def main():
     from vxslam import synth
 
     torch.cuda.set_device(dist.local_rank)
+    # frontend context (tracking: Extract + Match) and backend context (LocalBA), each with its own
+    # HIP stream; BA(t) waits on the device for Match(t) and overlaps Extract/Match(t + 1).
     ctx = vxslam.Context(dist.local_rank)
+    bctx = ctx if args.serial else vxslam.Context(dist.local_rank)
+    ctxs = [ctx] if bctx is ctx else [ctx, bctx]
     cfg = CONFIGS[args.config]
     h, w, nf, nk, nl = cfg
     N = dist.world
@@ -202,8 +214,8 @@ def main():
     opts = vxslam.default_ba_options(window=nk * N)
     if N > 1:
         uid = dist.broadcast_bytes(vxslam.Context.comm_unique_id() if dist.rank == 0 else None)
-        ctx.comm_init(uid, N, dist.rank)
-    plan = ctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N)
+        bctx.comm_init(uid, N, dist.rank)
+    plan = bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N)
     info = plan.info()
     torch.cuda.synchronize()
 
@@ -214,28 +226,36 @@ def main():
     def step(i):
         extract(i)
         ctx.match_slots_async((i + 1) % 2, i % 2)
+        bctx.wait_for(ctx)
         plan.run_async()
 
     extract(-1)  # previous frame for step 0's match
-    sync = ctx.synchronize
+
+    def sync():
+        for c in ctxs:
+            c.synchronize()
 
     # ---- profiling pass (HIP events on the library stream, every stage) -> dominant kernel
     stages = {}
     if not args.no_profile:
-        ctx.prof_enable(True)
+        for c in ctxs:
+            c.prof_enable(True)
         for i in range(args.warmup):
             step(i)
-        prof = ctx.prof_read(reset=True)
-        ctx.prof_enable(False)
+        prof = {}
+        for c in ctxs:
+            prof.update({k: v for k, v in c.prof_read(reset=True).items() if v[1]})
+            c.prof_enable(False)
         stages = {k: (v[0] / max(v[1], 1), v[1] / args.warmup) for k, v in prof.items() if v[1]}
 
-    # ---- the timed region
+    # ---- the timed region (HIP events only around the dominant kernel, on the stream it runs on)
     dominant = max(stages, key=lambda k: stages[k][0] * stages[k][1]) if stages else None
+    dctx = bctx if dominant and dominant.startswith("ba_") else ctx
     if dominant:
-        ctx.prof_enable(True, stages=[dominant])
+        dctx.prof_enable(True, stages=[dominant])
     elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
-    dom_prof = ctx.prof_read(reset=True).get(dominant, (0.0, 0)) if dominant else (0.0, 0)
-    ctx.prof_enable(False)
+    dom_prof = dctx.prof_read(reset=True).get(dominant, (0.0, 0)) if dominant else (0.0, 0)
+    dctx.prof_enable(False)
 
     # counts for the byte formulas
     kps, _ = ctx.orb_fetch((args.warmup + args.steps - 1) % 2)
@@ -262,7 +282,7 @@ def main():
             roofline = {"kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                         "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_ms * 1e3, 2),
-                        "launches_per_step": round(dom_prof[1] / args.steps, 2)}
+                        "launches_per_step": round(dom_prof[1] / (args.steps + args.warmup), 2)}
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if roofline and os.path.exists(pmc):
         try:
@@ -300,6 +320,7 @@ def main():
                              f"(<= 5 alternating iterations), landmark-sharded over {N} GPU(s)"),
                 "frames_per_step": N,
                 "parallelism": f"frames: 1 per rank; BA: landmark shards x{N}" + (" + RCCL all-reduce" if N > 1 else ""),
+                "streams": "1 (serial)" if args.serial else "2: Extract+Match(t+1) || LocalBA(t), BA waits on Match(t)",
                 "ba_window_kf": nk * N,
                 "ba_landmarks": nl * N,
                 "orb_features": nf,
@@ -310,7 +331,8 @@ def main():
         }
         print(json.dumps(out), flush=True)
     plan.close()
-    ctx.close()
+    for c in reversed(ctxs):
+        c.close()
     dist.close()
 
 

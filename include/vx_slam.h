@@ -79,6 +79,12 @@ void vx_destroy(vx_ctx* ctx);
 const char* vx_last_error(const vx_ctx* ctx);
 void* vx_stream(vx_ctx* ctx);          /* the context's hipStream_t */
 int vx_synchronize(vx_ctx* ctx);
+/* Device-side ordering between two contexts of the same device: work enqueued on `ctx` after
+ * this call starts only after everything enqueued on `after` so far has finished (event record on
+ * after's stream + stream wait; the host does not block).  This is how a backend context (the
+ * LocalBA of keyframe t, which needs tracking(t)) overlaps the frontend context's Extract/Match
+ * of frame t+1 — the concurrency ORB-SLAM-style systems get from a separate mapping thread. */
+int vx_stream_wait_ctx(vx_ctx* ctx, vx_ctx* after);
 void vx_orb_default_params(vx_orb_params* p);
 /* Copies the compiled-in rBRIEF pattern (bit_pattern_31_, 256 x {x1,y1,x2,y2}). */
 int vx_orb_pattern(int32_t* out_1024);

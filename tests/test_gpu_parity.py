@@ -225,6 +225,8 @@ def test_ba_variants(ctx, oracle):
     _ba_case(ctx, oracle, m, dict(window=8), ref=int(m["kf_id"][-3]))         # older reference KF
     _ba_case(ctx, oracle, m, dict(window=12, huber=1.5, max_err=4.0))         # Huber weights active
     _ba_case(ctx, oracle, m, dict(window=12, iters=20))                       # stop rule / many iters
+    _ba_case(ctx, oracle, m, dict(window=12, iters=0))                        # nothing runs: initial state
+    _ba_case(ctx, oracle, m, dict(window=12, iters=1))                        # one iteration (odd buffer)
     _ba_case(ctx, oracle, m, dict(window=12, min_pose=2000))                  # every pose step skipped
     mm = m.copy()
     mm["kf_has_cam"][-2] = 0                                                   # keyframe without camera
@@ -249,3 +251,42 @@ def test_ba_plan_is_repeatable(ctx, oracle):
         assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
     info = plan.info()
     assert info["n_kf"] == nk and info["n_pose_obs"] > 50000
+
+
+def test_frontend_backend_contexts_overlap(ctx, oracle):
+    """bench.py's pipeline: Extract/Match on one context, LocalBA on a second context ordered after
+    Match(t) by vx_stream_wait_ctx, so BA(t) runs concurrently with Extract/Match(t + 1).  Results
+    equal the CPU restatement exactly as in the serial case."""
+    import torch
+    import vxslam
+
+    back = vxslam.Context(0)
+    try:
+        frames = synth.make_frames(43, 4)
+        d = torch.from_numpy(frames).cuda()
+        torch.cuda.synchronize()
+        p = _orb_params(vxslam, 2000)
+        m = synth.make_ba_map(78, 10, 2000, n_old_kf=2)
+        opts = dict(window=10)
+        plan = back.ba_plan(m, vxslam.default_ba_options(**opts))
+        for i in range(4):
+            ctx.orb_extract_async(d[i].data_ptr(), 640, 480, 3, 640 * 3, i % 2, p)
+            if i:
+                ctx.match_slots_async((i - 1) % 2, i % 2)
+            back.wait_for(ctx)
+            plan.run_async()
+        mg = m.copy()
+        st_g = plan.fetch(mg)
+        got = ctx.match_fetch()
+        k3, d3 = ctx.orb_fetch(1)
+        _, dc2 = oracle.orb_extract(frames[2], 2000, order=oracle.ORDER_RASTER)
+        kc3, dc3 = oracle.orb_extract(frames[3], 2000, order=oracle.ORDER_RASTER)
+        _assert_orb_equal(k3, d3, kc3, dc3)
+        assert np.array_equal(got, oracle.match(dc2, dc3))
+        mc = m.copy()
+        st_c = oracle.ba_optimize(mc, oracle.ba_options(**opts))
+        _assert_ba_close(mg, mc, st_g, st_c)
+        back.wait_for(back)  # same context: no-op
+        plan.close()
+    finally:
+        back.close()

@@ -55,7 +55,7 @@ struct BAArgs {
     int min_pose_obs, min_point_obs, max_iter, pad1;
     double huber, max_err;
     const double* kf_pose0;  // 8 per KF: qx qy qz qw tx ty tz 0
-    double* kf_pose;
+    double* kf_pose;         // 2 x n_kf x 8: ping-pong by iteration parity (see pose_in / pose_out)
     const double* kf_intr;   // 4 per KF
     double* kf_rot;          // 9 per KF (rotation matrix of the current pose)
     const int* kf_flags;     // bit0: keyframe has a camera
@@ -73,6 +73,19 @@ struct BAArgs {
 };
 
 struct D3 { double x, y, z; };
+
+// Iteration `it` reads the poses of iteration it-1 (the initial poses at it == 0) and writes the
+// other buffer, so no launch ever reads a pose another workgroup of the same launch writes.  The
+// landmarks [n_opt, n_lm) are never optimised (other shards' landmarks) and always read initial.
+__device__ __forceinline__ const double* pose_in(const BAArgs& a, int it) {
+    return it == 0 ? a.kf_pose0 : a.kf_pose + (long long)(it & 1) * a.n_kf * 8;
+}
+__device__ __forceinline__ double* pose_out(const BAArgs& a, int it) {
+    return a.kf_pose + (long long)((it + 1) & 1) * a.n_kf * 8;
+}
+__device__ __forceinline__ const double* lm_in(const BAArgs& a, int it, int s) {
+    return (it == 0 || s >= a.n_opt ? a.lm_pos0 : a.lm_pos) + 4 * (long long)s;
+}
 
 __device__ __forceinline__ D3 cross3(D3 a, D3 b) {
     return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
@@ -257,18 +270,28 @@ __device__ __forceinline__ void solve_pose(const BAArgs& a, int k, const double*
     rot_from_quat(T, R);
 }
 
-// Relative-cost stop rule (local_ba.cpp:240-247) -> active[it + 1].
+// Relative-cost stop rule (local_ba.cpp:240-247) -> active[it + 1].  Iteration 0 starts the run's
+// state (last_cost = numeric_limits<double>::max(), local_ba.cpp:110); a stop clears every later
+// flag, a continue sets the next one (later ones are rewritten before they are read).
 __device__ void stop_rule(const BAArgs& a, int it, double total, int tobs) {
     BAState* s = a.state;
+    if (it == 0)
+        for (int k = 1; k < 16; ++k) {
+            s->cost[k] = 0;
+            s->obs[k] = 0;
+        }
     if (it < 16) {
         s->cost[it] = total;
         s->obs[it] = tobs;
     }
     s->iterations = it + 1;
-    const double last = s->last_cost;
+    const double last = it == 0 ? 1.7976931348623157e308 : s->last_cost;
     const bool stop = tobs == 0 || fabs(last - total) < 1e-6 * last;
     if (!stop) s->last_cost = total;
-    s->active[it + 1] = (!stop && it + 1 < a.max_iter) ? 1 : 0;
+    if (!stop && it + 1 < a.max_iter)
+        s->active[it + 1] = 1;
+    else
+        for (int k = it + 1; k <= a.max_iter; ++k) s->active[k] = 0;
 }
 
 // Ordered (fixed-tree) pose-stage totals over the keyframes; the calling wave must be complete.
@@ -287,20 +310,16 @@ __device__ void totals_and_stop(const BAArgs& a, int it, int lane) {
     if (lane == 0) stop_rule(a, it, total, tobs);
 }
 
+// Only for max_iterations == 0 (nothing runs): the result is the initial state.  Iteration 0 of
+// the kernels below reads the initial arrays directly, so a normal run has no reset launch.
 __global__ void k_ba_reset(BAArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < a.n_kf * 8) a.kf_pose[i] = a.kf_pose0[i];
     if (i < a.n_lm * 4) a.lm_pos[i] = a.lm_pos0[i];
-    if (i < a.n_kf) {
-        double R[9];
-        rot_from_quat(a.kf_pose0 + 8 * i, R);
-        for (int k = 0; k < 9; ++k) a.kf_rot[9 * i + k] = R[k];
-    }
     if (i == 0) {
         BAState* s = a.state;
-        for (int k = 0; k <= kMaxIter; ++k) s->active[k] = k == 0 ? 1 : 0;
+        for (int k = 0; k <= kMaxIter; ++k) s->active[k] = 0;
         s->iterations = 0;
-        s->last_cost = 1.7976931348623157e308;  // std::numeric_limits<double>::max()
         for (int k = 0; k < 16; ++k) { s->cost[k] = 0; s->obs[k] = 0; }
     }
 }
@@ -309,13 +328,14 @@ __global__ void k_ba_reset(BAArgs a) {
 // terms of its observations (strided) in registers; a fixed-order wave butterfly + LDS tree
 // reduces them into kf_sums[k].
 __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
+    if (it > 0 && !a.state->active[it]) return;
     __shared__ double red[kPoseBlock / 64][kNTerms];
     const int k = blockIdx.x;
     const int i0 = a.kf_obs_ptr[k], i1 = a.kf_obs_ptr[k + 1];
+    const double* Tin = pose_in(a, it);
     double T[8], C[4];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) T[j] = a.kf_pose[8 * k + j];
+    for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) C[j] = a.kf_intr[4 * k + j];
     const double fx = C[0], fy = C[1];
@@ -326,7 +346,7 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     for (int i = i0 + (int)threadIdx.x; i < i1; i += kPoseBlock) {
         const int s = a.pobs_lm[i];
         const double2 uv = a.pobs_uv[i];
-        const double* P = a.lm_pos + 4 * s;
+        const double* P = lm_in(a, it, s);
         const D3 pc = se3_apply(T, {P[0], P[1], P[2]});
         if (!(pc.z > 1e-6)) continue;
         const double inv_z = 1.0 / pc.z;
@@ -382,10 +402,11 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
 
 // Landmark step of landmark l (local_ba.cpp:176-238) against keyframe tables T/R/C (LDS or
 // global memory).
-__device__ __forceinline__ void landmark_step(const BAArgs& a, int l, const double* sT, const double* sR,
-                                              const double* sC) {
+__device__ __forceinline__ void landmark_step(const BAArgs& a, int it, int l, const double* sT,
+                                              const double* sR, const double* sC) {
+    const double* Pin = lm_in(a, it, l);
     double* Pp = a.lm_pos + 4 * l;
-    const D3 P{Pp[0], Pp[1], Pp[2]};
+    const D3 P{Pin[0], Pin[1], Pin[2]};
     double h00 = 0, h01 = 0, h02 = 0, h11 = 0, h12 = 0, h22 = 0, b0 = 0, b1 = 0, b2 = 0;
     int obs = 0;
     for (int o = a.lobs_ptr[l]; o < a.lobs_ptr[l + 1]; ++o) {
@@ -423,32 +444,36 @@ __device__ __forceinline__ void landmark_step(const BAArgs& a, int l, const doub
         b2 += w * ((-J0[2]) * e0 + (-J1[2]) * e1);
         ++obs;
     }
-    if (obs < a.min_point_obs) return;
-    double H[9] = {h00 + 1e-6, h01, h02, h01, h11 + 1e-6, h12, h02, h12, h22 + 1e-6};
-    const double b[3] = {b0, b1, b2};
-    double dp[3];
-    ldlt_solve<3>(H, b, dp);
-    if (!(isfinite(dp[0]) && isfinite(dp[1]) && isfinite(dp[2]))) return;
-    Pp[0] = P.x + dp[0];
-    Pp[1] = P.y + dp[1];
-    Pp[2] = P.z + dp[2];
+    D3 out = P;  // skipped landmarks keep their position (written anyway: iteration 0 reads lm_pos0)
+    if (obs >= a.min_point_obs) {
+        double H[9] = {h00 + 1e-6, h01, h02, h01, h11 + 1e-6, h12, h02, h12, h22 + 1e-6};
+        const double b[3] = {b0, b1, b2};
+        double dp[3];
+        ldlt_solve<3>(H, b, dp);
+        if (isfinite(dp[0]) && isfinite(dp[1]) && isfinite(dp[2])) out = {P.x + dp[0], P.y + dp[1], P.z + dp[2]};
+    }
+    Pp[0] = out.x;
+    Pp[1] = out.y;
+    Pp[2] = out.z;
 }
 
 // Pose solve of every window keyframe (redundantly in each workgroup) + landmark stage, one launch.
 __global__ __launch_bounds__(256) void k_landmark_solve(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
+    if (it > 0 && !a.state->active[it]) return;
     extern __shared__ __attribute__((aligned(16))) double kf_lds[];  // n_kf x (8 T + 9 R + 4 C)
     double* sT = kf_lds;
     double* sR = kf_lds + 8 * a.n_kf;
     double* sC = sR + 9 * a.n_kf;
     const int tid = threadIdx.x;
+    const double* Tin = pose_in(a, it);
+    double* Tout = pose_out(a, it);
     for (int k = tid; k < a.n_kf; k += blockDim.x) {
         double S[kStride];
 #pragma unroll
         for (int t = 0; t < kNTerms; ++t) S[t] = a.kf_sums[(long long)k * kStride + t];
         double T[8], R[9];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) T[j] = a.kf_pose[8 * k + j];
+        for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
         solve_pose(a, k, S, T, R);
 #pragma unroll
         for (int j = 0; j < 8; ++j) sT[8 * k + j] = T[j];
@@ -458,7 +483,7 @@ __global__ __launch_bounds__(256) void k_landmark_solve(BAArgs a, int it) {
         for (int j = 0; j < 4; ++j) sC[4 * k + j] = a.kf_intr[4 * k + j];
         if (blockIdx.x == 0) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) a.kf_pose[8 * k + j] = T[j];
+            for (int j = 0; j < 8; ++j) Tout[8 * k + j] = T[j];
 #pragma unroll
             for (int j = 0; j < 9; ++j) a.kf_rot[9 * k + j] = R[j];
             a.kf_cost[2 * k] = S[27];
@@ -468,23 +493,25 @@ __global__ __launch_bounds__(256) void k_landmark_solve(BAArgs a, int it) {
     __syncthreads();  // also makes block 0's kf_cost stores visible inside block 0
     if (blockIdx.x == 0 && tid < 64) totals_and_stop(a, it, tid);
     const int l = blockIdx.x * blockDim.x + tid;
-    if (l < a.n_opt) landmark_step(a, l, sT, sR, sC);
+    if (l < a.n_opt) landmark_step(a, it, l, sT, sR, sC);
 }
 
 // Large-window fallback (n_kf > kMaxKfLds): one thread per keyframe solves into global memory...
 __global__ __launch_bounds__(256) void k_pose_solve_g(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
+    if (it > 0 && !a.state->active[it]) return;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.n_kf) return;
     double S[kStride];
 #pragma unroll
     for (int t = 0; t < kNTerms; ++t) S[t] = a.kf_sums[(long long)k * kStride + t];
+    const double* Tin = pose_in(a, it);
+    double* Tout = pose_out(a, it);
     double T[8], R[9];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) T[j] = a.kf_pose[8 * k + j];
+    for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
     solve_pose(a, k, S, T, R);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) a.kf_pose[8 * k + j] = T[j];
+    for (int j = 0; j < 8; ++j) Tout[8 * k + j] = T[j];
 #pragma unroll
     for (int j = 0; j < 9; ++j) a.kf_rot[9 * k + j] = R[j];
     a.kf_cost[2 * k] = S[27];
@@ -494,10 +521,10 @@ __global__ __launch_bounds__(256) void k_pose_solve_g(BAArgs a, int it) {
 // ... and the landmark stage reads the poses from global memory; wave 0 of block 0 evaluates
 // the stop rule (active[it + 1] is read by no block of this launch).
 __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
-    if (!a.state->active[it]) return;
+    if (it > 0 && !a.state->active[it]) return;
     const int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 64) totals_and_stop(a, it, threadIdx.x);
-    if (l < a.n_opt) landmark_step(a, l, a.kf_pose, a.kf_rot, a.kf_intr);
+    if (l < a.n_opt) landmark_step(a, it, l, pose_out(a, it), a.kf_rot, a.kf_intr);
 }
 
 inline uint64_t splitmix64(uint64_t x) {
@@ -694,7 +721,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     if ((rc = upload(c, p->lobs_ptr, lptr))) return rc;
     if ((rc = upload(c, p->lobs_kf, lkf))) return rc;
     if ((rc = upload(c, p->lobs_uv, luv))) return rc;
-    VX_HIP(c, p->kf_pose.ensure((size_t)nk * 8 * sizeof(double)));
+    VX_HIP(c, p->kf_pose.ensure((size_t)nk * 2 * 8 * sizeof(double)));
     VX_HIP(c, p->kf_rot.ensure((size_t)nk * 9 * sizeof(double)));
     VX_HIP(c, p->kf_sums.ensure((size_t)nk * kStride * sizeof(double)));
     VX_HIP(c, p->kf_cost.ensure((size_t)nk * 2 * sizeof(double)));
@@ -718,7 +745,7 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
 #endif
     }
     const BAArgs a = make_args(p);
-    {
+    if (p->opt.max_iterations == 0) {
         ProfScope ps(c, kStBaReset);
         const int n = std::max(p->n_kf * 8, std::max(p->n_lm, 1) * 4);
         hipLaunchKernelGGL(k_ba_reset, dim3((n + 255) / 256), dim3(256), 0, c->stream, a);
@@ -812,7 +839,10 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
         BAState hs;
         std::vector<double> pose((size_t)p->n_kf * 8), lm((size_t)std::max(p->n_opt, 1) * 4);
         VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
-        VX_HIP(c, hipMemcpyAsync(pose.data(), p->kf_pose.p, pose.size() * sizeof(double), hipMemcpyDeviceToHost,
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+        // the poses of the last iteration run are in ping-pong buffer (iterations & 1)
+        const double* fin = p->kf_pose.as<double>() + (size_t)(hs.iterations & 1) * p->n_kf * 8;
+        VX_HIP(c, hipMemcpyAsync(pose.data(), fin, pose.size() * sizeof(double), hipMemcpyDeviceToHost,
                                  c->stream));
         if (p->n_opt > 0)
             VX_HIP(c, hipMemcpyAsync(lm.data(), p->lm_pos.p, (size_t)p->n_opt * 4 * sizeof(double),

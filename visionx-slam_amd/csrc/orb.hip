@@ -4,8 +4,10 @@
 // cv::ORB::create(n, 1.2f, 8)->detectAndCompute(img, noArray(), kps, desc).  The pipeline
 //  is re-designed as a chain of wavefront kernels on one HIP stream:
 //
-//   k_gray            BGR(A)->gray level 0, fixed point (A.1)
-//   k_resize x (L-1)  INTER_LINEAR_EXACT pyramid, 8.8 / 16.16 fixed point (A.1)
+//   k_pyramid         BGR(A)->gray level 0 (fixed point) and the whole INTER_LINEAR_EXACT pyramid
+//                     (8.8 / 16.16 fixed point) in ONE launch: per level-0 tile, level by level
+//                     through LDS with host-computed halos (A.1); k_gray + k_resize x (L-1) is
+//                     the fallback when the halo does not fit in LDS
 //   k_fast            all levels in one launch: 64x16 tiles staged in LDS with a 4 px
 //                     halo; FAST-9/16 corner test as 16-bit ring masks, cornerScore<16>, strict
 //                     3x3 NMS, border filter, raster-ordered cells by wave ballot, wave-parallel Harris
@@ -50,21 +52,177 @@ struct LevelArgs {
     // blur tiling
     int btx[kMaxLevels], bty[kMaxLevels], bbase[kMaxLevels];
     float gk[7];
+    // fused pyramid: resize tables and tile rectangles (offsets into the int4 table buffer)
+    long long xtab[kMaxLevels], ytab[kMaxLevels];
+    long long pr_x, pr_y;
+    int pr_buf;
 };
 
+// Copies n elements into LDS, element i = load(i), with every load of a thread issued before the
+// first LDS store: one exposed memory latency per KMAX * NT elements instead of one per element
+// (a plain strided loop waits on each load before the next iteration's).
+template <int NT, int KMAX, class T, class F>
+__device__ __forceinline__ void stage_lds(T* __restrict__ dst, int n, F load) {
+    for (int base = 0; base < n; base += NT * KMAX) {
+        T v[KMAX];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int i = base + (int)threadIdx.x + k * NT;
+            v[k] = i < n ? load(i) : T{};
+        }
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            const int i = base + (int)threadIdx.x + k * NT;
+            if (i < n) dst[i] = v[k];
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------ gray
+// cvtColor BGR2GRAY fixed point (B 1868, G 9617, R 4899, >> 14); 1 channel passes through
+__device__ __forceinline__ uint8_t gray_px(const uint8_t* s, int ch) {
+    if (ch == 1) return s[0];
+    return (uint8_t)((s[0] * 1868 + s[1] * 9617 + s[2] * 4899 + (1 << 13)) >> 14);
+}
+
+// INTER_LINEAR_EXACT tap: u16 8.8 horizontal, u32 16.16 vertical, (v + 32768) >> 16
+__device__ __forceinline__ uint8_t lin_px(const uint8_t* r0, const uint8_t* r1, int c0, int c1, int4 cx,
+                                          int4 cy) {
+    const uint32_t h0 = (uint32_t)(r0[c0] * cx.y + r0[c1] * cx.z);
+    const uint32_t h1 = (uint32_t)(r1[c0] * cx.y + r1[c1] * cx.z);
+    const uint32_t v = h0 * (uint32_t)cy.y + h1 * (uint32_t)cy.z;
+    return (uint8_t)min((v + 32768u) >> 16, 255u);
+}
+
+// Unfused path only (the fused k_pyramid zeroes the histograms itself).
 __global__ void k_gray(const uint8_t* __restrict__ img, int W, int ch, long long stride,
-                       uint8_t* __restrict__ out) {
+                       uint8_t* __restrict__ out, int* __restrict__ hist, int hist_n) {
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < hist_n; i += blockDim.x) hist[i] = 0;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= W) return;
-    const uint8_t* s = img + (long long)y * stride + (long long)x * ch;
-    uint8_t g;
-    if (ch == 1)
-        g = s[0];
-    else
-        g = (uint8_t)((s[0] * 1868 + s[1] * 9617 + s[2] * 4899 + (1 << 13)) >> 14);
-    out[(long long)y * W + x] = g;
+    out[(long long)y * W + x] = gray_px(img + (long long)y * stride + (long long)x * ch, ch);
+}
+
+// ------------------------------------------------------------------------------ fused pyramid
+// One launch for gray + every INTER_LINEAR_EXACT level.  Workgroup (tx, ty) owns a level-0 tile
+// and, at level l, the proportional sub-rectangle of level l; it computes, level by level in two
+// LDS ping-pong buffers, every pixel its deeper levels depend on (the "need" rectangle: own +
+// a halo that grows as h <- 1.2 h + 1, prepared on the host from the same coefficient tables),
+// and writes only the pixels it owns.  Each pixel is the same deterministic function of its
+// sources whichever workgroup computes it, so the result is bit-identical to the level chain.
+constexpr int kPyBlock = 1024;  // 64 x 16
+constexpr int kPyTile = 64;     // level-0 tile edge
+constexpr int kPyLdsMax = 64 * 1024;
+
+__global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict__ img, int ch,
+                                                      long long stride, uint8_t* __restrict__ pyr,
+                                                      const int4* __restrict__ tabs, LevelArgs a,
+                                                      int* __restrict__ hist, int hist_n, int raw_bytes) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds_pyr[];
+    __shared__ int4 srx[kMaxLevels], sry[kMaxLevels];
+    __shared__ int sox[kMaxLevels + 1], soy[kMaxLevels + 1];
+    uint8_t* raw = lds_pyr;                       // level-0 need rectangle, BGR(A) bytes
+    uint8_t* cur = raw + raw_bytes;               // ping-pong level buffers
+    uint8_t* prev = cur + a.pr_buf;
+    int* stab = reinterpret_cast<int*>(prev + a.pr_buf);  // packed {ofs | c1 << 16} per level
+    const int tid = threadIdx.x, lx = tid & 63, ly = tid >> 6;
+    const int L = a.L;
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = tid; i < hist_n; i += kPyBlock) hist[i] = 0;
+    if (tid < L) srx[tid] = tabs[a.pr_x + (long long)blockIdx.x * L + tid];
+    if (tid >= 64 && tid < 64 + L) sry[tid - 64] = tabs[a.pr_y + (long long)blockIdx.y * L + tid - 64];
+    __syncthreads();
+    if (tid == 0) {
+        int o = 0;
+        sox[0] = soy[0] = 0;
+        for (int l = 1; l < L; ++l) { sox[l] = o; o += srx[l].y - srx[l].x; }
+        for (int l = 1; l < L; ++l) { soy[l] = o; o += sry[l].y - sry[l].x; }
+        sox[L] = o;  // total entries
+    }
+    __syncthreads();
+    // coefficient tables of this tile's need ranges, every level, all loads in flight at once
+    stage_lds<kPyBlock, 2>(stab, sox[L], [&](int i) {
+        const bool isy = i >= soy[1];
+        int l = 1;
+        if (!isy) { while (l + 1 < L && i >= sox[l + 1]) ++l; }
+        else { while (l + 1 < L && i >= soy[l + 1]) ++l; }
+        const int idx = i - (isy ? soy[l] : sox[l]) + (isy ? sry[l].x : srx[l].x);
+        const int4 e = tabs[(isy ? a.ytab[l] : a.xtab[l]) + idx];
+        return e.x | (e.z << 16);
+    });
+    // level 0: stage the BGR(A) bytes of the need rectangle (row-chunked, all loads in flight)
+    int4 rx = srx[0], ry = sry[0];
+    int px0 = rx.x, py0 = ry.x, pw = rx.y - rx.x, ph = ry.y - ry.x;
+    {
+        const int rb = pw * ch;
+        const uint8_t* src = img + (long long)py0 * stride + (long long)px0 * ch;
+        constexpr int KR = 6, KC = 6;
+        for (int r0 = 0; r0 < ph; r0 += 16 * KR)
+            for (int c0 = 0; c0 < rb; c0 += 64 * KC) {
+                uint8_t v[KR][KC];
+#pragma unroll
+                for (int i = 0; i < KR; ++i)
+#pragma unroll
+                    for (int j = 0; j < KC; ++j) {
+                        const int r = r0 + ly + 16 * i, c = c0 + lx + 64 * j;
+                        v[i][j] = (r < ph && c < rb) ? src[(long long)r * stride + c] : 0;
+                    }
+#pragma unroll
+                for (int i = 0; i < KR; ++i)
+#pragma unroll
+                    for (int j = 0; j < KC; ++j) {
+                        const int r = r0 + ly + 16 * i, c = c0 + lx + 64 * j;
+                        if (r < ph && c < rb) raw[r * rb + c] = v[i][j];
+                    }
+            }
+    }
+    __syncthreads();
+    for (int yy = ly; yy < ph; yy += 16) {
+        const int y = py0 + yy;
+        const bool oy = y >= ry.z && y < ry.w;
+        uint8_t* drow = pyr + (long long)y * a.lw[0];
+        for (int xx = lx; xx < pw; xx += 64) {
+            const int x = px0 + xx;
+            const uint8_t g = gray_px(raw + (yy * pw + xx) * ch, ch);
+            cur[yy * pw + xx] = g;
+            if (oy && x >= rx.z && x < rx.w) drow[x] = g;
+        }
+    }
+    for (int l = 1; l < L; ++l) {
+        uint8_t* t = cur;
+        cur = prev;
+        prev = t;
+        __syncthreads();
+        rx = srx[l];
+        ry = sry[l];
+        const int sw = a.lw[l - 1], sh = a.lh[l - 1], dw = a.lw[l];
+        const int* xt = stab + sox[l] - rx.x;
+        const int* yt = stab + soy[l] - ry.x;
+        const int nw = rx.y - rx.x, nh = ry.y - ry.x;
+        uint8_t* dst = pyr + a.off[l];
+        for (int yy = ly; yy < nh; yy += 16) {
+            const int y = ry.x + yy;
+            const int ey = yt[y];
+            const int4 cy = make_int4(ey & 0xffff, 256 - (ey >> 16), ey >> 16, 0);
+            const uint8_t* r0 = prev + (cy.x - py0) * pw;
+            const uint8_t* r1 = prev + (min(cy.x + 1, sh - 1) - py0) * pw;
+            const bool oy = y >= ry.z && y < ry.w;
+            for (int xx = lx; xx < nw; xx += 64) {
+                const int x = rx.x + xx;
+                const int ex = xt[x];
+                const int4 cx = make_int4(ex & 0xffff, 256 - (ex >> 16), ex >> 16, 0);
+                const uint8_t v = lin_px(r0, r1, cx.x - px0, min(cx.x + 1, sw - 1) - px0, cx, cy);
+                cur[yy * nw + xx] = v;
+                if (oy && x >= rx.z && x < rx.w) dst[(long long)y * dw + x] = v;
+            }
+        }
+        px0 = rx.x;
+        py0 = ry.x;
+        pw = nw;
+        ph = nh;
+    }
 }
 
 // ------------------------------------------------------------------------------ resize
@@ -77,11 +235,7 @@ __global__ void k_resize(const uint8_t* __restrict__ src, int sw, int sh, uint8_
     const int4 cy = yt[y];
     const uint8_t* r0 = src + (long long)cy.x * sw;
     const uint8_t* r1 = src + (long long)min(cy.x + 1, sh - 1) * sw;
-    const int x1 = min(cx.x + 1, sw - 1);
-    const uint32_t h0 = (uint32_t)(r0[cx.x] * cx.y + r0[x1] * cx.z);
-    const uint32_t h1 = (uint32_t)(r1[cx.x] * cx.y + r1[x1] * cx.z);
-    const uint32_t v = h0 * (uint32_t)cy.y + h1 * (uint32_t)cy.z;
-    dst[(long long)y * dw + x] = (uint8_t)min((v + 32768u) >> 16, 255u);
+    dst[(long long)y * dw + x] = lin_px(r0, r1, cx.x, min(cx.x + 1, sw - 1), cx, cy);
 }
 
 // ------------------------------------------------------------------------------ FAST
@@ -148,7 +302,7 @@ __device__ int fast_score(const uint8_t* t, int stride, int thr) {
     return -b0 - 1;
 }
 
-struct CandRec {  // 16 B per FAST candidate / selected keypoint
+struct alignas(16) CandRec {  // 16 B per FAST candidate / selected keypoint
     unsigned xy;  // x | y << 16
     int score;
     float harris;
@@ -206,12 +360,12 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     const int x0 = tx * kTX, y0 = ty * kTY;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     if (tid == 0) s_n = 0;
-    for (int i = tid; i < kTH * kTW; i += kBlock) {
+    stage_lds<kBlock, (kTH * kTW + kBlock - 1) / kBlock>(tile, kTH * kTW, [&](int i) {
         const int r = i / kTW, c = i - r * kTW;
         const int gy = min(max(y0 - 4 + r, 0), H - 1);
         const int gx = min(max(x0 - 4 + c, 0), W - 1);
-        tile[i] = img[(long long)gy * W + gx];
-    }
+        return img[(long long)gy * W + gx];
+    });
     __syncthreads();
     const int thr = a.fast_threshold;
     for (int i = tid; i < kSH * kSW; i += kBlock) {
@@ -300,10 +454,10 @@ __global__ __launch_bounds__(kBlock) void k_blur(const uint8_t* __restrict__ pyr
         }
         return p;
     };
-    for (int i = threadIdx.x; i < (TYo + 6) * (TXo + 6); i += kBlock) {
+    stage_lds<kBlock, ((TYo + 6) * (TXo + 6) + kBlock - 1) / kBlock>(sin_, (TYo + 6) * (TXo + 6), [&](int i) {
         const int r = i / (TXo + 6), c = i - r * (TXo + 6);
-        sin_[i] = img[(long long)refl(y0 - 3 + r, H) * W + refl(x0 - 3 + c, W)];
-    }
+        return img[(long long)refl(y0 - 3 + r, H) * W + refl(x0 - 3 + c, W)];
+    });
     __syncthreads();
     const float k0 = a.gk[0], k1 = a.gk[1], k2 = a.gk[2], k3 = a.gk[3], k4 = a.gk[4],
                 k5 = a.gk[5], k6 = a.gk[6];
@@ -346,6 +500,9 @@ __device__ __forceinline__ float key2f(unsigned k) {
 }
 
 constexpr int kSelBlock = 1024;
+constexpr int kCellsPer = 6;      // max cells per thread per gather pass
+constexpr int kRecBatch = 8;      // candidate records per thread loaded in one batch
+constexpr int kSelRecLds = 2048;  // survivors kept in LDS
 
 // Descending-digit search over a 256-bin histogram held by threads 0..255: returns (via the
 // block) the largest digit d with count(bins >= d) >= k, and the count strictly above d.
@@ -370,6 +527,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     __shared__ int sw[kSelBlock / 64];
     __shared__ int sh[256];
     __shared__ int s_out[2];
+    __shared__ CandRec srec[kSelRecLds];  // retainBest(2q) survivors (32 KB)
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
     const int ncell = a.lh[l] * a.ntx[l];
@@ -391,51 +549,85 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
         find_digit(hv, k1, sw, s_out);
         thr1 = s_out[0];
     }
-    // ---- gather kept candidates (score >= thr1) in raster order
+    // ---- gather kept candidates (score >= thr1) in raster order.  Each thread owns cpt
+    // consecutive cells: their counts are loaded in one batch, then up to kRecBatch of their
+    // records in one batch (a per-record loop would expose one memory latency per record).
+    // Survivors go to LDS (when they fit) and to the global staging list.
     int K1 = 0;
     if (k1 > 0) {
-        // each thread owns kCellsPer consecutive cells: all their counts are loaded at once
-        // (static register indices), so one pass costs two dependent load steps, not 2 per cell
-        constexpr int kCellsPer = 6;
-        for (int base = 0; base < ncell; base += kSelBlock * kCellsPer) {
-            const int c0 = base + tid * kCellsPer;
+        const int cpt = min(kCellsPer, (ncell + kSelBlock - 1) / kSelBlock);
+        for (int base = 0; base < ncell; base += kSelBlock * cpt) {
+            const int c0 = base + tid * cpt;
             int cnts[kCellsPer];
+            int tot = 0;
 #pragma unroll
-            for (int j = 0; j < kCellsPer; ++j) cnts[j] = (c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
+            for (int j = 0; j < kCellsPer; ++j) {
+                cnts[j] = (j < cpt && c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
+            // k-th record of this thread -> cand index
+            auto rec_index = [&](int k) {
+                int j = 0, i = k;
+#pragma unroll
+                for (int jj = 0; jj < kCellsPer; ++jj)
+                    if (j == jj && i >= cnts[jj]) {
+                        i -= cnts[jj];
+                        j = jj + 1;
+                    }
+                return (cbase + c0 + j) * kCellCap + i;
+            };
+            CandRec rr[kRecBatch];
+#pragma unroll
+            for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? cand[rec_index(k)] : CandRec{};
             int kc = 0;
 #pragma unroll
-            for (int j = 0; j < kCellsPer; ++j) {
-                const CandRec* cr = cand + (cbase + c0 + j) * kCellCap;
-                for (int i = 0; i < cnts[j]; ++i) kc += cr[i].score >= thr1;
-            }
-            int tot;
-            int pos = K1 + block_scan_excl<kSelBlock>(kc, sw, tot);
+            for (int k = 0; k < kRecBatch; ++k) kc += (k < tot && rr[k].score >= thr1) ? 1 : 0;
+            for (int k = kRecBatch; k < tot; ++k) kc += cand[rec_index(k)].score >= thr1 ? 1 : 0;
+            int btot;
+            int pos = K1 + block_scan_excl<kSelBlock>(kc, sw, btot);
+            auto put = [&](const CandRec& r) {
+                if (pos < kSelRecLds) srec[pos] = r;
+                kept[pos] = r;
+                ++pos;
+            };
 #pragma unroll
-            for (int j = 0; j < kCellsPer; ++j) {
-                const CandRec* cr = cand + (cbase + c0 + j) * kCellCap;
-                for (int i = 0; i < cnts[j]; ++i) {
-                    const CandRec r = cr[i];
-                    if (r.score >= thr1) kept[pos++] = r;
-                }
+            for (int k = 0; k < kRecBatch; ++k)
+                if (k < tot && rr[k].score >= thr1) put(rr[k]);
+            for (int k = kRecBatch; k < tot; ++k) {
+                const CandRec r = cand[rec_index(k)];
+                if (r.score >= thr1) put(r);
             }
-            K1 += tot;
+            K1 += btot;
         }
     }
     __syncthreads();
-    // ---- retainBest(q) by Harris
+    // ---- retainBest(q) by Harris: exact q-th largest key by a 4-pass radix select over the
+    // survivors (keys held in registers when K1 <= 2 * kSelBlock), then an ordered compaction
     int K2 = 0;
     if (q > 0 && K1 > 0) {
+        const CandRec* kr = K1 <= kSelRecLds ? srec : kept;
         float thr2 = -INFINITY;
         if (K1 > q) {
-            // exact q-th largest float key: 4-pass radix select, 8 bits per pass
+            const bool in_regs = K1 <= 2 * kSelBlock;
+            unsigned key0 = 0, key1 = 0;
+            if (in_regs) {
+                if (tid < K1) key0 = f2key(kr[tid].harris);
+                if (tid + kSelBlock < K1) key1 = f2key(kr[tid + kSelBlock].harris);
+            }
             unsigned prefix = 0, mask = 0;
             int k = q;
             for (int shift = 24; shift >= 0; shift -= 8) {
                 if (tid < 256) sh[tid] = 0;
                 __syncthreads();
-                for (int j = tid; j < K1; j += kSelBlock) {
-                    const unsigned key = f2key(kept[j].harris);
-                    if ((key & mask) == prefix) atomicAdd(&sh[(key >> shift) & 255], 1);
+                if (in_regs) {
+                    if (tid < K1 && (key0 & mask) == prefix) atomicAdd(&sh[(key0 >> shift) & 255], 1);
+                    if (tid + kSelBlock < K1 && (key1 & mask) == prefix) atomicAdd(&sh[(key1 >> shift) & 255], 1);
+                } else {
+                    for (int j = tid; j < K1; j += kSelBlock) {
+                        const unsigned key = f2key(kr[j].harris);
+                        if ((key & mask) == prefix) atomicAdd(&sh[(key >> shift) & 255], 1);
+                    }
                 }
                 __syncthreads();
                 const int v = tid < 256 ? sh[255 - tid] : 0;
@@ -453,7 +645,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
             CandRec r{};
             int f = 0;
             if (j < K1) {
-                r = kept[j];
+                r = kr[j];
                 f = r.harris >= thr2;
             }
             int cnt;
@@ -603,6 +795,93 @@ void linear_table(int src, int dst, std::vector<int4>& t) {
     }
 }
 
+// Rectangles of the fused pyramid along one axis.  For level-0 tile t the owned range of level l
+// is [b(t), b(t+1)) with b(t) = min(n_l, t * kPyTile * n_l / n_0) (a partition of every level);
+// the needed range of level l-1 is the owned range plus every source index (ofs, min(ofs+1,
+// n-1)) of the needed range of level l, taken from the same coefficient tables k_resize uses.
+static void pyramid_axis(const std::vector<int>& n, const std::vector<const int4*>& tab, int tiles,
+                         std::vector<int4>& out) {
+    const int L = (int)n.size();
+    for (int t = 0; t < tiles; ++t) {
+        std::vector<int4> r(L);
+        for (int l = 0; l < L; ++l) {
+            const int64_t lo = std::min<int64_t>(n[l], (int64_t)t * kPyTile * n[l] / n[0]);
+            const int64_t hi = std::min<int64_t>(n[l], (int64_t)(t + 1) * kPyTile * n[l] / n[0]);
+            r[l] = make_int4(0, 0, (int)lo, (int)hi);
+        }
+        r[L - 1].x = r[L - 1].z;
+        r[L - 1].y = r[L - 1].w;
+        for (int l = L - 1; l >= 1; --l) {
+            int lo = r[l - 1].z, hi = r[l - 1].w;
+            if (lo >= hi) lo = INT32_MAX, hi = INT32_MIN;
+            for (int d = r[l].x; d < r[l].y; ++d) {
+                const int s0 = tab[l][d].x;
+                lo = std::min(lo, s0);
+                hi = std::max(hi, std::min(s0 + 1, n[l - 1] - 1) + 1);
+            }
+            if (lo >= hi) lo = hi = 0;
+            r[l - 1].x = lo;
+            r[l - 1].y = hi;
+        }
+        out.insert(out.end(), r.begin(), r.end());
+    }
+}
+
+// Prepares k_pyramid's tables (appended to the coefficient table vector `all`, which already holds
+// the per-level resize tables) and decides whether the largest need rectangle fits in LDS.
+static void pyramid_rects(OrbGeometry& g, std::vector<int4>& all) {
+    g.pyr_fused = false;
+    if (g.L < 2) return;
+    std::vector<int> nw(g.L), nh(g.L);
+    std::vector<const int4*> tx(g.L, nullptr), ty(g.L, nullptr);
+    for (int l = 0; l < g.L; ++l) {
+        nw[l] = g.lw[l];
+        nh[l] = g.lh[l];
+        if (l) {
+            tx[l] = all.data() + g.xtab[l];
+            ty[l] = all.data() + g.ytab[l];
+        }
+    }
+    g.pr_ntx = (g.W + kPyTile - 1) / kPyTile;
+    g.pr_nty = (g.H + kPyTile - 1) / kPyTile;
+    std::vector<int4> rx, ry;
+    pyramid_axis(nw, tx, g.pr_ntx, rx);
+    pyramid_axis(nh, ty, g.pr_nty, ry);
+    int64_t buf = 0;
+    for (int l = 0; l < g.L; ++l) {
+        int mw = 0, mh = 0;
+        for (int t = 0; t < g.pr_ntx; ++t) mw = std::max(mw, rx[t * g.L + l].y - rx[t * g.L + l].x);
+        for (int t = 0; t < g.pr_nty; ++t) mh = std::max(mh, ry[t * g.L + l].y - ry[t * g.L + l].x);
+        buf = std::max<int64_t>(buf, (int64_t)mw * mh);
+    }
+    buf = (buf + 15) & ~int64_t(15);
+    int64_t area0 = 0, tabn = 0, tx_max = 0, ty_max = 0;
+    for (int t = 0; t < g.pr_ntx; ++t) {
+        int64_t s = 0;
+        for (int l = 1; l < g.L; ++l) s += rx[t * g.L + l].y - rx[t * g.L + l].x;
+        tx_max = std::max(tx_max, s);
+    }
+    for (int t = 0; t < g.pr_nty; ++t) {
+        int64_t s = 0;
+        for (int l = 1; l < g.L; ++l) s += ry[t * g.L + l].y - ry[t * g.L + l].x;
+        ty_max = std::max(ty_max, s);
+    }
+    tabn = tx_max + ty_max;
+    for (int tx = 0; tx < g.pr_ntx; ++tx)
+        for (int ty = 0; ty < g.pr_nty; ++ty)
+            area0 = std::max<int64_t>(area0, (int64_t)(rx[tx * g.L].y - rx[tx * g.L].x) * (ry[ty * g.L].y - ry[ty * g.L].x));
+    // worst case 4 channels for the raw level-0 staging
+    if (((area0 * 4 + 15) & ~int64_t(15)) + 2 * buf + 4 * tabn > kPyLdsMax) return;  // level chain instead
+    g.pr_buf = (int)buf;
+    g.pr_area0 = (int)area0;
+    g.pr_tabn = (int)tabn;
+    g.pr_x = (int64_t)all.size();
+    all.insert(all.end(), rx.begin(), rx.end());
+    g.pr_y = (int64_t)all.size();
+    all.insert(all.end(), ry.begin(), ry.end());
+    g.pyr_fused = true;
+}
+
 // (float) of getGaussianKernelBitExact(7, sigma 2)
 void gauss_taps(float k[7]) {
     double v[3], sum = 0;
@@ -664,6 +943,13 @@ LevelArgs level_args(const OrbGeometry& g) {
         bb += a.btx[l] * a.bty[l];
     }
     gauss_taps(a.gk);
+    for (int l = 0; l < g.L; ++l) {
+        a.xtab[l] = g.xtab[l];
+        a.ytab[l] = g.ytab[l];
+    }
+    a.pr_x = g.pr_x;
+    a.pr_y = g.pr_y;
+    a.pr_buf = g.pr_buf;
     return a;
 }
 
@@ -743,6 +1029,7 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
         g.ytab[l] = (int64_t)all.size();
         all.insert(all.end(), t.begin(), t.end());
     }
+    pyramid_rects(g, all);
     g.tab_entries = (int64_t)all.size();
     // FAST tiles / cells and selection staging
     int tiles = 0;
@@ -792,13 +1079,21 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
     const LevelArgs a = level_args(g);
     uint8_t* pyr = c->pyr.as<uint8_t>();
     Slot& s = c->slots[slot];
-    {
-        ProfScope ps(c, kStGray);
-        hipLaunchKernelGGL(k_gray, dim3((g.W + kBlock - 1) / kBlock, g.H), dim3(kBlock), 0, c->stream,
-                           d_img, g.W, channels, (long long)stride, pyr);
-        VX_LAUNCH_CHECK(c, "k_gray");
-    }
-    {
+    const int hist_n = g.L * 256;
+    if (g.pyr_fused) {
+        ProfScope ps(c, kStPyramid);
+        const int raw = (g.pr_area0 * channels + 15) & ~15;
+        hipLaunchKernelGGL(k_pyramid, dim3(g.pr_ntx, g.pr_nty), dim3(kPyBlock), raw + 2 * g.pr_buf + 4 * g.pr_tabn,
+                           c->stream, d_img, channels, (long long)stride, pyr, c->tabs.as<int4>(), a,
+                           c->hist.as<int>(), hist_n, raw);
+        VX_LAUNCH_CHECK(c, "k_pyramid");
+    } else {
+        {
+            ProfScope ps(c, kStGray);
+            hipLaunchKernelGGL(k_gray, dim3((g.W + kBlock - 1) / kBlock, g.H), dim3(kBlock), 0, c->stream,
+                               d_img, g.W, channels, (long long)stride, pyr, c->hist.as<int>(), hist_n);
+            VX_LAUNCH_CHECK(c, "k_gray");
+        }
         ProfScope ps(c, kStResize);
         const int4* tabs = c->tabs.as<int4>();
         for (int l = 1; l < g.L; ++l) {
@@ -808,18 +1103,24 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
             VX_LAUNCH_CHECK(c, "k_resize");
         }
     }
-    VX_HIP(c, hipMemsetAsync(c->hist.p, 0, g.L * 256 * sizeof(int), c->stream));
+    // blur depends only on the pyramid: fork it onto the side stream, join before describe
+    hipStream_t bs = c->stream;
+    if (c->orb_fork) {
+        VX_HIP(c, hipEventRecord(c->fork_ev, c->stream));
+        VX_HIP(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
+        bs = c->side;
+    }
+    {
+        ProfScope ps(c, kStBlur, bs);
+        hipLaunchKernelGGL(k_blur, dim3(blur_blocks(a)), dim3(kBlock), 0, bs, pyr, c->blur.as<uint8_t>(), a);
+        VX_LAUNCH_CHECK(c, "k_blur");
+    }
+    if (c->orb_fork) VX_HIP(c, hipEventRecord(c->join_ev, c->side));
     {
         ProfScope ps(c, kStFast);
         hipLaunchKernelGGL(k_fast, dim3(g.total_tiles), dim3(kBlock), 0, c->stream, pyr, a,
                            c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>());
         VX_LAUNCH_CHECK(c, "k_fast");
-    }
-    {
-        ProfScope ps(c, kStBlur);
-        hipLaunchKernelGGL(k_blur, dim3(blur_blocks(a)), dim3(kBlock), 0, c->stream, pyr,
-                           c->blur.as<uint8_t>(), a);
-        VX_LAUNCH_CHECK(c, "k_blur");
     }
     {
         ProfScope ps(c, kStSelect);
@@ -828,6 +1129,7 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
                            c->level_count.as<int>());
         VX_LAUNCH_CHECK(c, "k_select");
     }
+    if (c->orb_fork) VX_HIP(c, hipStreamWaitEvent(c->stream, c->join_ev, 0));
     {
         ProfScope ps(c, kStDescribe);
         const int waves_per_block = kBlock / 64;

@@ -1,5 +1,6 @@
 // vx_ctx.cpp — context lifetime, error reporting, stage profiling and the RCCL communicator.
 #include <cstdarg>
+#include <cstdlib>
 #include <cstring>
 
 #include "vx_internal.hpp"
@@ -33,17 +34,17 @@ static hipEvent_t get_event(vx_ctx* c) {
     return e;
 }
 
-ProfScope::ProfScope(vx_ctx* c_, int st) : c(c_), stage(st) {
+ProfScope::ProfScope(vx_ctx* c_, int st, hipStream_t on) : c(c_), stage(st), s(on ? on : c_->stream) {
     if (!c->prof || !((c->prof_mask >> st) & 1u)) return;
     a = get_event(c);
-    if (a) (void)hipEventRecord(a, c->stream);
+    if (a) (void)hipEventRecord(a, s);
 }
 
 ProfScope::~ProfScope() {
     if (!c->prof || !a) return;
     hipEvent_t b = get_event(c);
     if (!b) return;
-    (void)hipEventRecord(b, c->stream);
+    (void)hipEventRecord(b, s);
     c->pending.push_back({a, b, stage});
 }
 
@@ -65,7 +66,7 @@ void prof_collect(vx_ctx* c) {
 static const char* kStageNames[vx::kStCount] = {
     "orb_gray",       "orb_resize",    "orb_fast_harris", "orb_select",  "orb_blur",
     "orb_describe",   "match_partial", "match_merge",     "ba_reset",    "ba_pose_partial",
-    "ba_pose_sum",    "ba_allreduce",  "ba_pose_solve",   "ba_landmark"};
+    "ba_pose_sum",    "ba_allreduce",  "ba_pose_solve",   "ba_landmark",    "orb_pyramid"};
 
 extern "C" {
 
@@ -80,10 +81,14 @@ int vx_create(int device, vx_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return VX_ERR_HIP;
     auto* c = new vx_ctx();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) {
+        vx_destroy(c);
         return VX_ERR_HIP;
     }
+    if (const char* f = std::getenv("VX_ORB_FORK")) c->orb_fork = std::atoi(f) != 0;
     *out = c;
     return VX_OK;
 }
@@ -91,13 +96,17 @@ int vx_create(int device, vx_ctx** out) {
 void vx_destroy(vx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->side) (void)hipStreamSynchronize(c->side);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     vx::prof_collect(c);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    for (auto e : {c->order_event, c->fork_ev, c->join_ev})
+        if (e) (void)hipEventDestroy(e);
 #ifndef VX_NO_RCCL
     if (c->comm) ncclCommDestroy(c->comm);
 #endif
-    (void)hipStreamDestroy(c->stream);
+    if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -109,6 +118,18 @@ int vx_synchronize(vx_ctx* c) {
     if (!c) return VX_ERR_INVALID;
     VX_HIP(c, hipStreamSynchronize(c->stream));
     if (c->prof) vx::prof_collect(c);
+    return VX_OK;
+}
+
+int vx_stream_wait_ctx(vx_ctx* c, vx_ctx* after) {
+    if (!c || !after) return VX_ERR_INVALID;
+    if (c == after) return VX_OK;
+    if (c->device != after->device)
+        return vx::set_error(c, VX_ERR_INVALID, "vx_stream_wait_ctx: contexts on devices %d and %d", c->device,
+                             after->device);
+    if (!after->order_event) VX_HIP(c, hipEventCreateWithFlags(&after->order_event, hipEventDisableTiming));
+    VX_HIP(c, hipEventRecord(after->order_event, after->stream));
+    VX_HIP(c, hipStreamWaitEvent(c->stream, after->order_event, 0));
     return VX_OK;
 }
 

@@ -35,6 +35,7 @@ enum Stage : int {
     kStBaAllreduce,
     kStBaSolve,
     kStBaLandmark,
+    kStPyramid,
     kStCount
 };
 
@@ -90,6 +91,14 @@ struct OrbGeometry {
     // resize tables for levels 1..L-1: int4 {ofs, c0, c1, 0} per destination column / row
     int64_t xtab[kMaxLevels], ytab[kMaxLevels];
     int64_t tab_entries = 0;
+    // fused pyramid (k_pyramid): level-0 tiles, per (tile column | tile row, level) int4
+    // {need_lo, need_hi, own_lo, own_hi} at tabs[pr_x] / tabs[pr_y], LDS bytes per ping-pong buffer
+    bool pyr_fused = false;
+    int pr_ntx = 0, pr_nty = 0;
+    int64_t pr_x = 0, pr_y = 0;
+    int pr_buf = 0;
+    int pr_area0 = 0;               // max level-0 need area (pixels)
+    int pr_tabn = 0;                // max packed coefficient entries per tile
     // FAST tiles (64 x 16 pixels per workgroup) and output cells (row x tile column)
     int ntx[kMaxLevels], nty[kMaxLevels];
     int tile_base[kMaxLevels];     // first tile (workgroup) of level l
@@ -121,6 +130,12 @@ struct vx_ba_plan;
 struct vx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipEvent_t order_event = nullptr;  // vx_stream_wait_ctx: recorded on this stream
+    // intra-frame fork/join: k_blur runs on `side` concurrently with FAST + selection
+    hipStream_t side = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    // off by default: with LocalBA on a second context the fork measured 4 % slower (v6)
+    bool orb_fork = false;  // $VX_ORB_FORK=1 enables it
     std::string err;
 
     // ---- ORB
@@ -159,8 +174,9 @@ int hip_fail(vx_ctx* c, hipError_t e, const char* what);
 struct ProfScope {
     vx_ctx* c;
     int stage;
+    hipStream_t s;
     hipEvent_t a = nullptr;
-    ProfScope(vx_ctx* c_, int st);
+    ProfScope(vx_ctx* c_, int st, hipStream_t on = nullptr);  // default: the context stream
     ~ProfScope();
 };
 void prof_collect(vx_ctx* c);

@@ -61,7 +61,7 @@ class BAStats(C.Structure):
 
 EXPORTS = [
     "vx_version", "vx_create", "vx_destroy", "vx_last_error", "vx_stream", "vx_synchronize",
-    "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
+    "vx_stream_wait_ctx", "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
     "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
     "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
     "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info",
@@ -90,6 +90,7 @@ def lib():
         L.vx_stream.restype = C.c_void_p
         L.vx_stream.argtypes = [C.c_void_p]
         L.vx_synchronize.argtypes = [C.c_void_p]
+        L.vx_stream_wait_ctx.argtypes = [C.c_void_p, C.c_void_p]
         L.vx_prof_name.restype = C.c_char_p
         L.vx_ba_plan_destroy.argtypes = [C.c_void_p]
         L.vx_ba_plan_destroy.restype = None
@@ -195,6 +196,10 @@ class Context:
 
     def synchronize(self):
         self._check(lib().vx_synchronize(self._h))
+
+    def wait_for(self, other: "Context"):
+        """Order later work on this context after everything enqueued on `other` (device-side)."""
+        self._check(lib().vx_stream_wait_ctx(self._h, other._h))
 
     # ---------------------------------------------------------------- ORB
     def orb_extract(self, img: np.ndarray, params: OrbParams | None = None, cap: int | None = None):
