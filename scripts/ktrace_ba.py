@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Phase timestamps of the BA kernels (trace build, csrc/vx_ktrace.hpp) on the C3 window.
+
+    make -C visionx-slam_amd trace && VX_LIB=visionx-slam_amd/lib/libvxslam_trace.so python3 scripts/ktrace_ba.py
+
+Runs one iteration (max_iterations = 1) many times; after the last run prints, per recorded slot,
+the median / max over the first 64 workgroups of (slot - that workgroup's first slot) in µs, and
+the spread of the first slot over workgroups (dispatch ramp).
+"""
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
+import vxslam  # noqa: E402
+from vxslam import synth  # noqa: E402
+
+KT_BLOCKS, KT_SLOTS = 64, 16
+
+
+def read():
+    out = np.zeros(KT_BLOCKS * KT_SLOTS, np.int64)
+    assert vxslam.lib().vx_ktrace_read_ba(C.c_void_p(out.ctypes.data)) == 0
+    return out.reshape(KT_BLOCKS, KT_SLOTS)
+
+
+def report(tr, slots, name):
+    base = tr[:, slots[0]]
+    ok = base > 0
+    print(f"{name}: {int(ok.sum())} workgroups traced, start spread {(base[ok].max() - base[ok].min()) / 100:.2f} us")
+    for s in slots[1:]:
+        d = (tr[ok, s] - base[ok]) / 100.0  # 100 MHz ticks -> us
+        print(f"  slot {s:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+
+
+def main():
+    nk, nl, ns = synth.ba_config("C3")
+    m = synth.make_ba_map(0x5EED0003, nk, nl)
+    ctx = vxslam.Context(0)
+    plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk, iters=1))
+    print("plan", plan.info())
+    for _ in range(30):
+        plan.run_async()
+    ctx.synchronize()
+    tr = read()
+    report(tr, [0, 1, 2, 3, 4, 5], "k_pose_kf (1 loads T/C, 2 obs loop, 3 wave reduce, 4 LDS+barrier, 5 store)")
+    report(tr, [8, 9, 10, 11, 13, 12],
+           "k_landmark_solve (9 loads, 10 combine, 11 pose solve, 13 observation terms, 12 per-landmark sum + 3x3 + store)")
+    plan.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

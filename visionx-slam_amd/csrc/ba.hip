@@ -10,18 +10,23 @@
 //                 keyframe-major pose observations (uv, landmark slot) and landmark-major
 //                 observations (uv, keyframe row); uploaded once, replayed by every run.
 //   device run (per iteration it; every kernel early-exits once the stop rule has fired):
-//     k_pose_kf        one workgroup per keyframe: each thread projects its observations
-//                      (ProjectToPixel, projection.h:11-31), gates, weights and accumulates the
-//                      21 + 6 + 2 normal-equation terms of the 2x6 PoseJacobian in registers; one
-//                      fixed-order workgroup reduction writes the keyframe's 29-term block
-//     [sharded only]   ncclAllReduce(sum, f64) of the per-keyframe blocks over the landmark
-//                      shards (one collective per iteration, 32 doubles per keyframe)
-//     k_landmark_solve every workgroup first solves ALL window keyframes redundantly (one lane per
-//                      keyframe: H += 1e-6 I, Eigen-style pivoted LDLT, finite check, T <- exp(dx) T)
-//                      into LDS — bitwise identical in every workgroup — then runs one landmark
-//                      per thread (2x3 Jacobian Jp*R, 3x3 normal equations, LDLT, p += dp) against
-//                      those poses; workgroup 0 publishes the poses and evaluates the stop rule.
+//     k_pose_kf        n_split workgroups per keyframe, each over a slice of its observations
+//                      (about one per thread): project (ProjectToPixel, projection.h:11-31), gate,
+//                      weight, the 21 + 6 + 2 normal-equation terms of the 2x6 PoseJacobian in
+//                      registers; a halving-butterfly wave reduction + LDS tree writes the slice's
+//                      29-term partial block (fixed order: deterministic)
+//     [sharded only]   ncclAllReduce(sum, f64) of the partial blocks over the landmark shards
+//                      (one collective per iteration, 32 doubles per keyframe slice)
+//     k_landmark_solve every workgroup sums the slice partials in slice order and solves ALL window
+//                      keyframes redundantly (one lane per keyframe: H += 1e-6 I, Eigen-style
+//                      pivoted LDLT, finite check, T <- exp(dx) T) into LDS — bitwise identical in
+//                      every workgroup — while its landmark-stage loads are in flight; then one
+//                      thread per landmark OBSERVATION forms its 9 terms (Jp * R), the thread owning
+//                      each landmark sums them in CSR order and solves the 3x3 (p += dp).
+//                      Workgroup 0 publishes the poses and evaluates the stop rule.
 //                      Windows beyond kMaxKfLds keyframes use k_pose_solve_g + k_landmark instead.
+// Iterations alternate two pose buffers (no launch reads what another workgroup of it writes);
+// iteration 0 reads the initial poses / positions directly, so a run needs no reset launch.
 // The step keeps the reference's sign (b = -J^T e, :156 and :224): this is a drop-in, not a fix.
 #include <algorithm>
 #include <cmath>
@@ -31,15 +36,21 @@
 #include <vector>
 
 #include "vx_internal.hpp"
+#include "vx_ktrace.hpp"
 
 namespace vx {
 namespace {
 
-constexpr int kPoseBlock = 256;  // threads per keyframe workgroup
+constexpr int kPoseBlock = 512;  // threads per pose-stage workgroup
 constexpr int kNTerms = 29;      // 21 H (upper) + 6 b + cost + count
 constexpr int kStride = 32;      // doubles per keyframe block
 constexpr int kMaxIter = 64;
-constexpr int kMaxKfLds = 512;   // keyframes whose poses fit the LDS of k_landmark_solve
+constexpr int kMaxKfLds = 256;   // keyframes whose 32-double slots fit the LDS of k_landmark_solve
+constexpr int kMaxSplit = 4;     // pose-stage workgroups per keyframe
+constexpr int kCombine = 6;      // (keyframe, term) pairs per thread per combine pass
+constexpr int kLmBlock = 512;    // k_landmark_solve: threads = max observations = max landmarks
+
+VX_KT_TABLE();
 
 struct BAState {
     int active[kMaxIter + 1];  // active[it]: iteration it runs
@@ -52,7 +63,7 @@ struct BAState {
 
 struct BAArgs {
     int n_kf, n_opt, n_lm, pad0;
-    int min_pose_obs, min_point_obs, max_iter, pad1;
+    int min_pose_obs, min_point_obs, max_iter, n_split;
     double huber, max_err;
     const double* kf_pose0;  // 8 per KF: qx qy qz qw tx ty tz 0
     double* kf_pose;         // 2 x n_kf x 8: ping-pong by iteration parity (see pose_in / pose_out)
@@ -60,7 +71,7 @@ struct BAArgs {
     double* kf_rot;          // 9 per KF (rotation matrix of the current pose)
     const int* kf_flags;     // bit0: keyframe has a camera
     const int* kf_obs_ptr;   // n_kf + 1, CSR into the pose observations
-    double* kf_sums;         // n_kf * kStride normal-equation blocks (all-reduced when sharded)
+    double* kf_part;         // n_kf * n_split * kStride partial normal-equation blocks (all-reduced when sharded)
     double* kf_cost;         // 2 per KF: pose-stage cost and observation count
     const double* lm_pos0;   // 4 per landmark
     double* lm_pos;
@@ -68,11 +79,23 @@ struct BAArgs {
     const int* pobs_lm;
     const int* lobs_ptr;     // n_opt + 1
     const int* lobs_kf;
+    const int* lobs_lm;      // landmark slot of each landmark-stage observation
+    const int* lm_blk;       // k_landmark_solve workgroup -> first landmark (n_blocks + 1)
     const double2* lobs_uv;
     BAState* state;
 };
 
 struct D3 { double x, y, z; };
+
+// 1 / b: v_rcp_f64 and two Newton steps (about 1 ulp) instead of the ~12-instruction IEEE division
+// sequence, which sits on every dependency chain below.  BA parity is a tolerance (1e-4), not a
+// bit pattern; b = 0 / denormal operands do not reach these call sites (gated by the caller).
+__device__ __forceinline__ double frcp(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return r;
+}
 
 // Iteration `it` reads the poses of iteration it-1 (the initial poses at it == 0) and writes the
 // other buffer, so no launch ever reads a pose another workgroup of the same launch writes.  The
@@ -158,8 +181,9 @@ __device__ __forceinline__ void ldlt_solve(double* A, const double* b, double* x
         }
         const double akk = A[k * N + k];
         if (fabs(akk) > 0.0) {
+            const double inv = frcp(akk);
 #pragma unroll
-            for (int i = k + 1; i < N; ++i) A[i * N + k] /= akk;
+            for (int i = k + 1; i < N; ++i) A[i * N + k] *= inv;
         }
     }
 #pragma unroll
@@ -176,7 +200,7 @@ __device__ __forceinline__ void ldlt_solve(double* A, const double* b, double* x
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const double d = A[i * N + i];
-        x[i] = fabs(d) > 2.2250738585072014e-308 ? x[i] / d : 0.0;
+        x[i] = fabs(d) > 2.2250738585072014e-308 ? x[i] * frcp(d) : 0.0;
     }
 #pragma unroll
     for (int i = N - 1; i >= 0; --i) {
@@ -202,7 +226,7 @@ __device__ void se3_left_update(const double* dx, double* T) {
     const double eps = 1e-10;  // Sophus::Constants<double>::epsilon()
     const double wx = dx[3], wy = dx[4], wz = dx[5];
     const double theta_sq = wx * wx + wy * wy + wz * wz;
-    double theta, imag, real;
+    double theta, imag, real, sh = 0.0, ch = 1.0;
     if (theta_sq < eps * eps) {
         theta = 0.0;
         const double t4 = theta_sq * theta_sq;
@@ -210,9 +234,9 @@ __device__ void se3_left_update(const double* dx, double* T) {
         real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * t4;
     } else {
         theta = sqrt(theta_sq);
-        const double half = 0.5 * theta;
-        imag = sin(half) / theta;
-        real = cos(half);
+        sincos(0.5 * theta, &sh, &ch);
+        imag = sh * frcp(theta);
+        real = ch;
     }
     const double eq[4] = {imag * wx, imag * wy, imag * wz, real};
     const double O[9] = {0, -wz, wy, wz, 0, -wx, -wy, wx, 0};
@@ -226,8 +250,10 @@ __device__ void se3_left_update(const double* dx, double* T) {
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 O2[3 * r + c] = O[3 * r] * O[c] + O[3 * r + 1] * O[3 + c] + O[3 * r + 2] * O[6 + c];
-        const double c1 = (1.0 - cos(theta)) / theta_sq;
-        const double c2 = (theta - sin(theta)) / (theta_sq * theta);
+        // 1 - cos(theta) = 2 sin^2(theta/2), sin(theta) = 2 sin(theta/2) cos(theta/2)
+        const double rsq = frcp(theta_sq);
+        const double c1 = (2.0 * sh * sh) * rsq;
+        const double c2 = (theta - 2.0 * sh * ch) * (rsq * frcp(theta));
 #pragma unroll
         for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * O[i] + c2 * O2[i];
     }
@@ -242,7 +268,8 @@ __device__ void se3_left_update(const double* dx, double* T) {
     // t <- et + rotate(eq, t)
     const double rt[8] = {eq[0], eq[1], eq[2], eq[3], 0, 0, 0, 0};
     const D3 r = se3_apply(rt, {T[4], T[5], T[6]});
-    T[0] = q[0] / n; T[1] = q[1] / n; T[2] = q[2] / n; T[3] = q[3] / n;
+    const double rn = frcp(n);
+    T[0] = q[0] * rn; T[1] = q[1] * rn; T[2] = q[2] * rn; T[3] = q[3] * rn;
     T[4] = et[0] + r.x; T[5] = et[1] + r.y; T[6] = et[2] + r.z;
 }
 
@@ -324,14 +351,19 @@ __global__ void k_ba_reset(BAArgs a) {
     }
 }
 
-// Pose stage (local_ba.cpp:116-161): one workgroup per keyframe.  Each thread accumulates the 29
-// terms of its observations (strided) in registers; a fixed-order wave butterfly + LDS tree
-// reduces them into kf_sums[k].
+// Pose stage (local_ba.cpp:116-161): n_split workgroups per keyframe, each over a contiguous
+// slice of the keyframe's observations.  Each thread accumulates the 29 terms of its observations
+// (strided) in registers; a fixed-order wave butterfly + LDS tree reduces them into the slice's
+// partial block kf_part[k * n_split + slice].  Partials are summed later in slice order, so the
+// result is deterministic (and identical on every rank after the sharded all-reduce).
 __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     if (it > 0 && !a.state->active[it]) return;
     __shared__ double red[kPoseBlock / 64][kNTerms];
-    const int k = blockIdx.x;
-    const int i0 = a.kf_obs_ptr[k], i1 = a.kf_obs_ptr[k + 1];
+    VX_KT(0);
+    const int k = blockIdx.x / a.n_split, slice = blockIdx.x - k * a.n_split;
+    const int p0 = a.kf_obs_ptr[k], p1 = a.kf_obs_ptr[k + 1];
+    const int len = (p1 - p0 + a.n_split - 1) / a.n_split;
+    const int i0 = p0 + slice * len, i1 = min(p1, i0 + len);
     const double* Tin = pose_in(a, it);
     double T[8], C[4];
 #pragma unroll
@@ -339,6 +371,7 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) C[j] = a.kf_intr[4 * k + j];
     const double fx = C[0], fy = C[1];
+    VX_KT(1);
     double v[kNTerms];
 #pragma unroll
     for (int t = 0; t < kNTerms; ++t) v[t] = 0.0;
@@ -349,46 +382,59 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
         const double* P = lm_in(a, it, s);
         const D3 pc = se3_apply(T, {P[0], P[1], P[2]});
         if (!(pc.z > 1e-6)) continue;
-        const double inv_z = 1.0 / pc.z;
+        const double inv_z = frcp(pc.z);
         const double x = pc.x * inv_z, y = pc.y * inv_z;
         const double e0 = uv.x - (fx * x + C[2]);
         const double e1 = uv.y - (fy * y + C[3]);
         const double en = sqrt(e0 * e0 + e1 * e1);
         if (en > a.max_err) continue;
-        const double w = en <= a.huber ? 1.0 : a.huber / en;
-        const double z = pc.z, z2 = z * z;
-        const double jp0 = fx / z, jp2 = -fx * pc.x / z2, jp4 = fy / z, jp5 = -fy * pc.y / z2;
-        // J = Jp * [I | -hat(pc)] (local_ba.cpp:26-33), formed as the 2x3 * 3x6 product
-        const double Jp[6] = {jp0, 0.0, jp2, 0.0, jp4, jp5};
-        const double S[18] = {1, 0, 0, 0, pc.z, -pc.y, 0, 1, 0, -pc.z, 0, pc.x, 0, 0, 1, pc.y, -pc.x, 0};
-        double J0[6], J1[6];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-            J0[c] = Jp[0] * S[c] + Jp[1] * S[6 + c] + Jp[2] * S[12 + c];
-            J1[c] = Jp[3] * S[c] + Jp[4] * S[6 + c] + Jp[5] * S[12 + c];
-        }
+        const double w = en <= a.huber ? 1.0 : a.huber * frcp(en);
+        // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
+        // written out without its structural zeros (J0[1] = J1[0] = 0)
+        const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+        const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, jp0 * pc.z - jp2 * pc.x, -jp0 * pc.y};
+        const double J1[6] = {0.0, jp4, jp5, jp5 * pc.y - jp4 * pc.z, -jp5 * pc.x, jp4 * pc.x};
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
-            for (int c = r; c < 6; ++c) v[hidx(r, c)] += (w * J0[r]) * J0[c] + (w * J1[r]) * J1[c];
+            for (int c = r; c < 6; ++c) {
+                const bool u0 = r != 1 && c != 1, u1 = r != 0 && c != 0;  // compile-time after unroll
+                const double t0 = u0 ? (w * J0[r]) * J0[c] : 0.0;
+                const double t1 = u1 ? (w * J1[r]) * J1[c] : 0.0;
+                v[hidx(r, c)] += (u0 && u1) ? t0 + t1 : (u0 ? t0 : t1);
+            }
 #pragma unroll
-        for (int r = 0; r < 6; ++r) v[21 + r] += w * ((-J0[r]) * e0 + (-J1[r]) * e1);
+        for (int r = 0; r < 6; ++r) {
+            const double g = r == 0 ? J0[0] * e0 : (r == 1 ? J1[1] * e1 : J0[r] * e0 + J1[r] * e1);
+            v[21 + r] -= w * g;
+        }
         v[27] += w * (e0 * e0 + e1 * e1);
         v[28] += 1.0;
     }
-#pragma unroll
-    for (int t = 0; t < kNTerms; ++t) {
-        double x = v[t];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-        v[t] = x;
-    }
+    VX_KT(2);
+    // Halving butterfly over the wave: at the stage with mask m each lane keeps half of its
+    // current terms (the half chosen by lane bit m) and adds its partner's copy of that half, so
+    // the 32 (29 used) terms cost 16 + 8 + 4 + 2 + 1 + 1 shuffles instead of 29 x 6.  Afterwards
+    // lanes 2t and 2t + 1 hold term t summed over the wave (fixed order: deterministic).
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (lane == 0) {
+    double r[kStride];
 #pragma unroll
-        for (int t = 0; t < kNTerms; ++t) red[wv][t] = v[t];
+    for (int t = 0; t < kStride; ++t) r[t] = t < kNTerms ? v[t] : 0.0;
+#pragma unroll
+    for (int m = 32, c = kStride; m >= 2; m >>= 1, c >>= 1) {
+        const bool up = (lane & m) != 0;
+#pragma unroll
+        for (int i = 0; i < c / 2; ++i) {
+            const double send = up ? r[i] : r[i + c / 2];
+            const double keep = up ? r[i + c / 2] : r[i];
+            r[i] = keep + __shfl_xor(send, m, 64);
+        }
     }
+    const double tot = r[0] + __shfl_xor(r[0], 1, 64);
+    VX_KT(3);
+    if ((lane & 1) == 0 && (lane >> 1) < kNTerms) red[wv][lane >> 1] = tot;
     __syncthreads();
+    VX_KT(4);
     if (threadIdx.x < kStride) {
         double s = 0.0;
         if (threadIdx.x < kNTerms) {
@@ -396,91 +442,155 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
 #pragma unroll
             for (int w2 = 1; w2 < kPoseBlock / 64; ++w2) s += red[w2][threadIdx.x];
         }
-        a.kf_sums[(long long)k * kStride + threadIdx.x] = s;
+        a.kf_part[(long long)blockIdx.x * kStride + threadIdx.x] = s;
     }
+    VX_KT(5);
 }
 
-// Landmark step of landmark l (local_ba.cpp:176-238) against keyframe tables T/R/C (LDS or
-// global memory).
-__device__ __forceinline__ void landmark_step(const BAArgs& a, int it, int l, const double* sT,
-                                              const double* sR, const double* sC) {
-    const double* Pin = lm_in(a, it, l);
-    double* Pp = a.lm_pos + 4 * l;
-    const D3 P{Pin[0], Pin[1], Pin[2]};
-    double h00 = 0, h01 = 0, h02 = 0, h11 = 0, h12 = 0, h22 = 0, b0 = 0, b1 = 0, b2 = 0;
-    int obs = 0;
-    for (int o = a.lobs_ptr[l]; o < a.lobs_ptr[l + 1]; ++o) {
-        const int k = a.lobs_kf[o];
-        const double2 uv = a.lobs_uv[o];
-        const double* T = sT + 8 * k;
-        const double* C = sC + 4 * k;
-        const D3 pc = se3_apply(T, P);
-        if (!(pc.z > 1e-6)) continue;
-        const double inv_z = 1.0 / pc.z;
-        const double x = pc.x * inv_z, y = pc.y * inv_z;
-        const double fx = C[0], fy = C[1];
-        const double e0 = uv.x - (fx * x + C[2]);
-        const double e1 = uv.y - (fy * y + C[3]);
-        const double en = sqrt(e0 * e0 + e1 * e1);
-        if (en > a.max_err) continue;
-        const double w = en <= a.huber ? 1.0 : a.huber / en;
-        const double z = pc.z, z2 = z * z;
-        const double jp0 = fx / z, jp2 = -fx * pc.x / z2, jp4 = fy / z, jp5 = -fy * pc.y / z2;
-        const double* R = sR + 9 * k;
-        double J0[3], J1[3];
+// Sum of keyframe k's slice partials for term t, in slice order (absent slices add +0.0).
+__device__ __forceinline__ double combine_term(const BAArgs& a, int k, int t) {
+    const double* src = a.kf_part + (long long)k * a.n_split * kStride + t;
+    double v[kMaxSplit];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            J0[c] = jp0 * R[c] + 0.0 * R[3 + c] + jp2 * R[6 + c];
-            J1[c] = 0.0 * R[c] + jp4 * R[3 + c] + jp5 * R[6 + c];
-        }
-        h00 += (w * J0[0]) * J0[0] + (w * J1[0]) * J1[0];
-        h01 += (w * J0[0]) * J0[1] + (w * J1[0]) * J1[1];
-        h02 += (w * J0[0]) * J0[2] + (w * J1[0]) * J1[2];
-        h11 += (w * J0[1]) * J0[1] + (w * J1[1]) * J1[1];
-        h12 += (w * J0[1]) * J0[2] + (w * J1[1]) * J1[2];
-        h22 += (w * J0[2]) * J0[2] + (w * J1[2]) * J1[2];
-        b0 += w * ((-J0[0]) * e0 + (-J1[0]) * e1);
-        b1 += w * ((-J0[1]) * e0 + (-J1[1]) * e1);
-        b2 += w * ((-J0[2]) * e0 + (-J1[2]) * e1);
-        ++obs;
+    for (int c = 0; c < kMaxSplit; ++c) v[c] = c < a.n_split ? src[c * kStride] : 0.0;
+    double s = v[0];
+#pragma unroll
+    for (int c = 1; c < kMaxSplit; ++c) s += v[c];
+    return s;
+}
+
+// The 9 normal-equation terms {H00 H01 H02 H11 H12 H22 b0 b1 b2} of one landmark observation
+// (local_ba.cpp:206-224) against keyframe k of tables T/R/C (strides in doubles), branch-free:
+// returns false for a gated-out observation (behind the camera or beyond max_reproj_error),
+// whose terms are then exactly +0.0.
+__device__ __forceinline__ bool obs_terms(const BAArgs& a, D3 P, int k, double2 uv, const double* T0, int tst,
+                                          const double* R0, int rst, const double* C0, int cst, double* h) {
+    const double* T = T0 + (long long)tst * k;
+    const double* C = C0 + (long long)cst * k;
+    const D3 pc = se3_apply(T, P);
+    const bool front = pc.z > 1e-6;
+    const double inv_z = frcp(pc.z);
+    const double x = pc.x * inv_z, y = pc.y * inv_z;
+    const double fx = C[0], fy = C[1];
+    const double e0 = uv.x - (fx * x + C[2]);
+    const double e1 = uv.y - (fy * y + C[3]);
+    const double en = sqrt(e0 * e0 + e1 * e1);
+    const bool ok = front && !(en > a.max_err);
+    const double w = en <= a.huber ? 1.0 : a.huber * frcp(en);
+    const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+    const double* R = R0 + (long long)rst * k;
+    // J = Jp * R with Jp's structural zeros dropped (local_ba.cpp:219-221)
+    double J0[3], J1[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        J0[c] = jp0 * R[c] + jp2 * R[6 + c];
+        J1[c] = jp4 * R[3 + c] + jp5 * R[6 + c];
     }
-    D3 out = P;  // skipped landmarks keep their position (written anyway: iteration 0 reads lm_pos0)
+    h[0] = ok ? (w * J0[0]) * J0[0] + (w * J1[0]) * J1[0] : 0.0;
+    h[1] = ok ? (w * J0[0]) * J0[1] + (w * J1[0]) * J1[1] : 0.0;
+    h[2] = ok ? (w * J0[0]) * J0[2] + (w * J1[0]) * J1[2] : 0.0;
+    h[3] = ok ? (w * J0[1]) * J0[1] + (w * J1[1]) * J1[1] : 0.0;
+    h[4] = ok ? (w * J0[1]) * J0[2] + (w * J1[1]) * J1[2] : 0.0;
+    h[5] = ok ? (w * J0[2]) * J0[2] + (w * J1[2]) * J1[2] : 0.0;
+    h[6] = ok ? w * ((-J0[0]) * e0 + (-J1[0]) * e1) : 0.0;
+    h[7] = ok ? w * ((-J0[1]) * e0 + (-J1[1]) * e1) : 0.0;
+    h[8] = ok ? w * ((-J0[2]) * e0 + (-J1[2]) * e1) : 0.0;
+    return ok;
+}
+
+// Landmark update from its summed terms (local_ba.cpp:228-237): skipped below min_point_obs or
+// for a non-finite step; the position is written either way (iteration 0 reads lm_pos0).
+__device__ __forceinline__ void lm_update(const BAArgs& a, int l, D3 P, const double* h, int obs) {
+    D3 out = P;
     if (obs >= a.min_point_obs) {
-        double H[9] = {h00 + 1e-6, h01, h02, h01, h11 + 1e-6, h12, h02, h12, h22 + 1e-6};
-        const double b[3] = {b0, b1, b2};
+        double H[9] = {h[0] + 1e-6, h[1], h[2], h[1], h[3] + 1e-6, h[4], h[2], h[4], h[5] + 1e-6};
+        const double b[3] = {h[6], h[7], h[8]};
         double dp[3];
         ldlt_solve<3>(H, b, dp);
         if (isfinite(dp[0]) && isfinite(dp[1]) && isfinite(dp[2])) out = {P.x + dp[0], P.y + dp[1], P.z + dp[2]};
     }
+    double* Pp = a.lm_pos + 4 * l;
     Pp[0] = out.x;
     Pp[1] = out.y;
     Pp[2] = out.z;
 }
 
 // Pose solve of every window keyframe (redundantly in each workgroup) + landmark stage, one launch.
-__global__ __launch_bounds__(256) void k_landmark_solve(BAArgs a, int it) {
+// Workgroup b covers the whole landmarks [lm_blk[b], lm_blk[b+1]) (at most kLmBlock landmarks
+// and kLmBlock observations, packed on the host).  Thread t projects observation o0 + t and
+// leaves its 9 terms in LDS; the thread owning landmark l0 + t then sums its observations' terms
+// in CSR order (the order of the per-landmark loop, local_ba.cpp:186) and solves the 3x3.
+// Every load of the landmark stage is issued first, so it lands during the combine and solve.
+// LDS: one 32-double slot per keyframe (combined normal equations S, then T 8 | R 9 | C 4) and
+// 9 x kLmBlock observation terms.
+__global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
     if (it > 0 && !a.state->active[it]) return;
-    extern __shared__ __attribute__((aligned(16))) double kf_lds[];  // n_kf x (8 T + 9 R + 4 C)
-    double* sT = kf_lds;
-    double* sR = kf_lds + 8 * a.n_kf;
-    double* sC = sR + 9 * a.n_kf;
+    extern __shared__ __attribute__((aligned(16))) double kf_lds[];
+    double* terms = kf_lds + (long long)a.n_kf * kStride;  // [9][kLmBlock]
     const int tid = threadIdx.x;
+    VX_KT(8);
+    const int l0 = a.lm_blk[blockIdx.x], l1 = a.lm_blk[blockIdx.x + 1];
+    const int ob0 = a.lobs_ptr[l0], ob1 = a.lobs_ptr[l1];
+    // this thread's observation ...
+    const int o = ob0 + tid;
+    const bool has_o = o < ob1;
+    const int ol = has_o ? a.lobs_lm[o] : l0;
+    const int ok_kf = has_o ? a.lobs_kf[o] : 0;
+    const double2 ouv = has_o ? a.lobs_uv[o] : make_double2(1e300, 1e300);
+    const double* Po = lm_in(a, it, ol);
+    const D3 PO{Po[0], Po[1], Po[2]};
+    // ... and the landmark it owns
+    const int l = l0 + tid;
+    const bool own = l < l1;
+    const int r0 = own ? a.lobs_ptr[l] - ob0 : 0, r1 = own ? a.lobs_ptr[l + 1] - ob0 : 0;
+    const double* Pl = lm_in(a, it, own ? l : l0);
+    const D3 PL{Pl[0], Pl[1], Pl[2]};
+    VX_KT(9);
+    // slice partials -> S: kCombine (keyframe, term) pairs per thread and pass, all their slice
+    // loads issued together
+    {
+        const int ne = a.n_kf * kNTerms;
+        for (int e0 = tid; e0 < ne; e0 += kCombine * blockDim.x) {
+            double v[kCombine][kMaxSplit];
+#pragma unroll
+            for (int q = 0; q < kCombine; ++q) {
+                const int e = e0 + q * blockDim.x;
+                const int k = e / kNTerms, t = e - k * kNTerms;
+                const double* src = a.kf_part + (long long)k * a.n_split * kStride + t;
+#pragma unroll
+                for (int c = 0; c < kMaxSplit; ++c) v[q][c] = (e < ne && c < a.n_split) ? src[c * kStride] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < kCombine; ++q) {
+                const int e = e0 + q * blockDim.x;
+                if (e >= ne) continue;
+                const int k = e / kNTerms, t = e - k * kNTerms;
+                double s = v[q][0];
+#pragma unroll
+                for (int c = 1; c < kMaxSplit; ++c) s += v[q][c];
+                kf_lds[k * kStride + t] = s;
+            }
+        }
+    }
+    __syncthreads();
+    VX_KT(10);
     const double* Tin = pose_in(a, it);
     double* Tout = pose_out(a, it);
     for (int k = tid; k < a.n_kf; k += blockDim.x) {
-        double S[kStride];
+        double* slot = kf_lds + k * kStride;
+        double S[kNTerms];
 #pragma unroll
-        for (int t = 0; t < kNTerms; ++t) S[t] = a.kf_sums[(long long)k * kStride + t];
+        for (int t = 0; t < kNTerms; ++t) S[t] = slot[t];
         double T[8], R[9];
 #pragma unroll
         for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
         solve_pose(a, k, S, T, R);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sT[8 * k + j] = T[j];
+        for (int j = 0; j < 8; ++j) slot[j] = T[j];
 #pragma unroll
-        for (int j = 0; j < 9; ++j) sR[9 * k + j] = R[j];
+        for (int j = 0; j < 9; ++j) slot[8 + j] = R[j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sC[4 * k + j] = a.kf_intr[4 * k + j];
+        for (int j = 0; j < 4; ++j) slot[17 + j] = a.kf_intr[4 * k + j];
         if (blockIdx.x == 0) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) Tout[8 * k + j] = T[j];
@@ -491,9 +601,29 @@ __global__ __launch_bounds__(256) void k_landmark_solve(BAArgs a, int it) {
         }
     }
     __syncthreads();  // also makes block 0's kf_cost stores visible inside block 0
+    VX_KT(11);
     if (blockIdx.x == 0 && tid < 64) totals_and_stop(a, it, tid);
-    const int l = blockIdx.x * blockDim.x + tid;
-    if (l < a.n_opt) landmark_step(a, it, l, sT, sR, sC);
+    {
+        double h[9];
+        const bool ok = obs_terms(a, PO, ok_kf, ouv, kf_lds, kStride, kf_lds + 8, kStride, kf_lds + 17, kStride, h);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) terms[j * kLmBlock + tid] = h[j];
+        reinterpret_cast<int*>(terms + 9 * kLmBlock)[tid] = (has_o && ok) ? 1 : 0;  // counted observation
+    }
+    __syncthreads();
+    VX_KT(13);
+    if (own) {
+        double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        int obs = 0;
+        const int* okf = reinterpret_cast<const int*>(terms + 9 * kLmBlock);
+        for (int r = r0; r < r1; ++r) {
+#pragma unroll
+            for (int j = 0; j < 9; ++j) h[j] += terms[j * kLmBlock + r];
+            obs += okf[r];
+        }
+        lm_update(a, l, PL, h, obs);
+    }
+    VX_KT(12);
 }
 
 // Large-window fallback (n_kf > kMaxKfLds): one thread per keyframe solves into global memory...
@@ -501,9 +631,9 @@ __global__ __launch_bounds__(256) void k_pose_solve_g(BAArgs a, int it) {
     if (it > 0 && !a.state->active[it]) return;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.n_kf) return;
-    double S[kStride];
+    double S[kNTerms];
 #pragma unroll
-    for (int t = 0; t < kNTerms; ++t) S[t] = a.kf_sums[(long long)k * kStride + t];
+    for (int t = 0; t < kNTerms; ++t) S[t] = combine_term(a, k, t);
     const double* Tin = pose_in(a, it);
     double* Tout = pose_out(a, it);
     double T[8], R[9];
@@ -518,13 +648,24 @@ __global__ __launch_bounds__(256) void k_pose_solve_g(BAArgs a, int it) {
     a.kf_cost[2 * k + 1] = S[28];
 }
 
-// ... and the landmark stage reads the poses from global memory; wave 0 of block 0 evaluates
-// the stop rule (active[it + 1] is read by no block of this launch).
+// ... and the landmark stage reads the poses from global memory, one thread per landmark; wave 0
+// of block 0 evaluates the stop rule (active[it + 1] is read by no block of this launch).
 __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
     if (it > 0 && !a.state->active[it]) return;
     const int l = blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < 64) totals_and_stop(a, it, threadIdx.x);
-    if (l < a.n_opt) landmark_step(a, it, l, pose_out(a, it), a.kf_rot, a.kf_intr);
+    if (l >= a.n_opt) return;
+    const double* Pin = lm_in(a, it, l);
+    const D3 P{Pin[0], Pin[1], Pin[2]};
+    double h[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, t[9];
+    int obs = 0;
+    const double* T0 = pose_out(a, it);
+    for (int o = a.lobs_ptr[l]; o < a.lobs_ptr[l + 1]; ++o) {
+        obs += obs_terms(a, P, a.lobs_kf[o], a.lobs_uv[o], T0, 8, a.kf_rot, 9, a.kf_intr, 4, t) ? 1 : 0;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) h[j] += t[j];
+    }
+    lm_update(a, l, P, h, obs);
 }
 
 inline uint64_t splitmix64(uint64_t x) {
@@ -546,8 +687,10 @@ struct vx_ba_plan {
     int n_kf = 0, n_opt = 0, n_lm = 0;
     int64_t n_pose_obs = 0, n_lm_obs = 0;
     std::vector<int> kf_map_idx, lm_map_idx;
-    vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags, kf_obs_ptr, kf_sums, kf_cost, lm_pos0, lm_pos,
-        pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_uv, state;
+    int n_split = 1;
+    vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags, kf_obs_ptr, kf_part, kf_cost, lm_pos0, lm_pos,
+        pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_lm, lm_blk, lobs_uv, state;
+    int n_lm_blocks = 1;
     bool ran = false;
 };
 
@@ -570,7 +713,8 @@ BAArgs make_args(vx_ba_plan* p) {
     a.kf_rot = p->kf_rot.as<double>();
     a.kf_flags = p->kf_flags.as<int>();
     a.kf_obs_ptr = p->kf_obs_ptr.as<int>();
-    a.kf_sums = p->kf_sums.as<double>();
+    a.kf_part = p->kf_part.as<double>();
+    a.n_split = p->n_split;
     a.kf_cost = p->kf_cost.as<double>();
     a.lm_pos0 = p->lm_pos0.as<double>();
     a.lm_pos = p->lm_pos.as<double>();
@@ -578,6 +722,8 @@ BAArgs make_args(vx_ba_plan* p) {
     a.pobs_lm = p->pobs_lm.as<int>();
     a.lobs_ptr = p->lobs_ptr.as<int>();
     a.lobs_kf = p->lobs_kf.as<int>();
+    a.lobs_lm = p->lobs_lm.as<int>();
+    a.lm_blk = p->lm_blk.as<int>();
     a.lobs_uv = p->lobs_uv.as<double2>();
     a.state = p->state.as<BAState>();
     return a;
@@ -678,6 +824,19 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
         }
     }
     kf_obs_ptr[nk] = (int)puv.size();
+    // workgroups per keyframe: about one observation per thread, from counts every shard sees
+    // alike (the window's landmark features before sharding), so the all-reduced partial layout
+    // is the same on every rank
+    {
+        int64_t mx = 0;
+        for (int k : win)
+            if (m->kf_has_cam[k]) {
+                int64_t n = 0;
+                for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) n += m->feat_flags[f] & 1;
+                mx = std::max(mx, n);
+            }
+        p->n_split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (mx + kPoseBlock - 1) / kPoseBlock));
+    }
     p->n_lm = (int)p->lm_map_idx.size();
     p->n_pose_obs = (int64_t)puv.size();
     std::vector<double> lm0((size_t)std::max(p->n_lm, 1) * 4, 0.0);
@@ -685,7 +844,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
         for (int j = 0; j < 3; ++j) lm0[4 * s + j] = m->lm_pos[3 * p->lm_map_idx[s] + j];
 
     // ---- landmark-stage CSR (local_ba.cpp:186-204)
-    std::vector<int> lptr(p->n_opt + 1, 0), lkf;
+    std::vector<int> lptr(p->n_opt + 1, 0), lkf, llm;
     std::vector<double2> luv;
     for (int s = 0; s < p->n_opt; ++s) {
         const int l = p->lm_map_idx[s];
@@ -702,11 +861,29 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
             const uint8_t fl = m->feat_flags[f];
             if (!(fl & 1) || (fl & 2) || m->feat_lm_id[f] != m->lm_id[l]) continue;
             lkf.push_back(r);
+            llm.push_back(s);
             luv.push_back(make_double2(m->feat_uv[2 * f], m->feat_uv[2 * f + 1]));
         }
         lptr[s + 1] = (int)lkf.size();
     }
     p->n_lm_obs = (int64_t)lkf.size();
+    // k_landmark_solve workgroups: whole landmarks, at most kLmBlock landmarks and observations
+    // each (a window of <= kMaxKfLds keyframes gives a landmark <= kMaxKfLds < kLmBlock of them)
+    std::vector<int> blk{0};
+    {
+        int n_o = 0, n_l = 0;
+        for (int s = 0; s < p->n_opt; ++s) {
+            const int cnt = lptr[s + 1] - lptr[s];
+            if (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock) {
+                blk.push_back(s);
+                n_o = n_l = 0;
+            }
+            n_o += cnt;
+            ++n_l;
+        }
+        blk.push_back(p->n_opt);
+    }
+    p->n_lm_blocks = (int)blk.size() - 1;
     if (!device) return VX_OK;
 
     VX_HIP(c, hipSetDevice(c->device));
@@ -720,10 +897,12 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     if ((rc = upload(c, p->pobs_lm, plm))) return rc;
     if ((rc = upload(c, p->lobs_ptr, lptr))) return rc;
     if ((rc = upload(c, p->lobs_kf, lkf))) return rc;
+    if ((rc = upload(c, p->lobs_lm, llm))) return rc;
+    if ((rc = upload(c, p->lm_blk, blk))) return rc;
     if ((rc = upload(c, p->lobs_uv, luv))) return rc;
     VX_HIP(c, p->kf_pose.ensure((size_t)nk * 2 * 8 * sizeof(double)));
     VX_HIP(c, p->kf_rot.ensure((size_t)nk * 9 * sizeof(double)));
-    VX_HIP(c, p->kf_sums.ensure((size_t)nk * kStride * sizeof(double)));
+    VX_HIP(c, p->kf_part.ensure((size_t)nk * p->n_split * kStride * sizeof(double)));
     VX_HIP(c, p->kf_cost.ensure((size_t)nk * 2 * sizeof(double)));
     VX_HIP(c, p->lm_pos.ensure(lm0.size() * sizeof(double)));
     VX_HIP(c, p->state.ensure(sizeof(BAState)));
@@ -752,25 +931,30 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
         VX_LAUNCH_CHECK(c, "k_ba_reset");
     }
     const bool lds_poses = p->n_kf <= kMaxKfLds;
-    const size_t lds = (size_t)p->n_kf * 21 * sizeof(double);
+    const size_t lds = (size_t)p->n_kf * kStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
+    if (lds_poses && lds > 64 * 1024) {  // up to ~103 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        VX_HIP(c, attr);
+    }
     const int lm_blocks = std::max(1, (p->n_opt + 255) / 256);
     for (int it = 0; it < p->opt.max_iterations; ++it) {
         {
             ProfScope ps(c, kStBaPose);
-            hipLaunchKernelGGL(k_pose_kf, dim3(p->n_kf), dim3(kPoseBlock), 0, c->stream, a, it);
+            hipLaunchKernelGGL(k_pose_kf, dim3(p->n_kf * p->n_split), dim3(kPoseBlock), 0, c->stream, a, it);
             VX_LAUNCH_CHECK(c, "k_pose_kf");
         }
 #ifndef VX_NO_RCCL
         if (sharded) {
             ProfScope ps(c, kStBaAllreduce);
-            ncclResult_t r = ncclAllReduce(p->kf_sums.p, p->kf_sums.p, (size_t)p->n_kf * kStride, ncclDouble,
+            ncclResult_t r = ncclAllReduce(p->kf_part.p, p->kf_part.p, (size_t)p->n_kf * p->n_split * kStride, ncclDouble,
                                            ncclSum, c->comm, c->stream);
             if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
         }
 #endif
         ProfScope ps(c, kStBaLandmark);
         if (lds_poses) {
-            hipLaunchKernelGGL(k_landmark_solve, dim3(lm_blocks), dim3(256), lds, c->stream, a, it);
+            hipLaunchKernelGGL(k_landmark_solve, dim3(p->n_lm_blocks), dim3(kLmBlock), lds, c->stream, a, it);
             VX_LAUNCH_CHECK(c, "k_landmark_solve");
         } else {
             hipLaunchKernelGGL(k_pose_solve_g, dim3((p->n_kf + 255) / 256), dim3(256), 0, c->stream, a, it);
@@ -787,6 +971,8 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
 }  // namespace vx
 
 using namespace vx;
+
+VX_KT_EXPORT(vx_ktrace_read_ba);
 
 extern "C" {
 

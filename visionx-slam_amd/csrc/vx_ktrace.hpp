@@ -1,0 +1,30 @@
+// vx_ktrace.hpp — in-kernel phase timestamps for the trace build only (make trace ->
+// lib/libvxslam_trace.so, -DVX_KTRACE).  VX_KT(slot) drains this wave's outstanding memory
+// operations (s_waitcnt 0, so a phase's loads are charged to it), then lane 0 of workgroups
+// < kKtBlocks records wall_clock64() (100 MHz) into the TU's trace table.  The product library
+// compiles every VX_KT to nothing.
+#pragma once
+
+namespace vx {
+constexpr int kKtBlocks = 64, kKtSlots = 16;
+}
+
+#ifdef VX_KTRACE
+#define VX_KT_TABLE() __device__ long long g_ktrace[vx::kKtBlocks * vx::kKtSlots]
+#define VX_KT(slot)                                                                        \
+    do {                                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                                     \
+        if (threadIdx.x == 0 && blockIdx.x < vx::kKtBlocks)                                \
+            g_ktrace[blockIdx.x * vx::kKtSlots + (slot)] = (long long)wall_clock64();      \
+    } while (0)
+#define VX_KT_EXPORT(name)                                                                 \
+    extern "C" int name(long long* out) {                                                  \
+        return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ktrace), sizeof(g_ktrace)) == hipSuccess ? 0 : -1; \
+    }
+#else
+#define VX_KT_TABLE() static_assert(true, "")
+#define VX_KT(slot) \
+    do {            \
+    } while (0)
+#define VX_KT_EXPORT(name) static_assert(true, "")
+#endif

@@ -16,7 +16,7 @@ import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libvxslam.so")
+LIB_PATH = os.environ.get("VX_LIB") or os.path.join(PKG_ROOT, "lib", "libvxslam.so")  # VX_LIB: trace build
 HEADER_PATH = os.path.join(REPO_ROOT, "include", "vx_slam.h")
 
 VX_OK, VX_ERR_INVALID, VX_ERR_HIP, VX_ERR_CAPACITY, VX_ERR_COMM, VX_ERR_STATE = 0, -1, -2, -3, -4, -5
