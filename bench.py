@@ -5,13 +5,14 @@
     torchrun --nproc-per-node N ... bench.py --gpus N ...
 
 One step = one frame through the hot path, everything resident in HBM before timing starts:
-  1. ORBExtractor::Extract of a 640x480 BGR8 frame (n_features 2000 at C3)   -> slot i % 2
+  1. ORBExtractor::Extract of a 640x480 BGR8 frame (n_features 2000 at C3)   -> slot i % 3
   2. ORBMatcher::Match(previous frame, this frame): BF Hamming kNN-2 + ratio -> matches
   3. LocalBA::Optimize over the sliding window (C3: 50 KF / 20k landmarks, <= 5 iterations)
-Steps 1-2 run on a frontend context, step 3 on a backend context (own HIP stream) that waits on
-the device for step 2 of the same frame; LocalBA(t) therefore overlaps Extract/Match(t + 1), which
-do not depend on it (--serial puts everything on one stream).  Every step's work completes inside
-the timed region.
+Each stage runs on its own context (HIP stream), ordered on the device by events that follow the
+data dependencies (Match(t) after Extract(t), LocalBA(t) after Match(t), Extract(t) after
+Match(t-2) which last read its slot), so Extract(t+1), Match(t) and LocalBA(t-1) overlap
+(--streams 1 puts everything on one stream).  Every step's work completes inside the timed
+region; `latency_ms_per_frame` is one frame alone through the same chain.
 At N GPUs (weak scaling, "rig" workload): every rank runs steps 1-2 on its own camera stream and
 the ranks jointly run ONE global window of N x 50 KF / N x 20k landmarks per step, landmarks
 sharded across ranks with one RCCL all-reduce of the per-keyframe normal equations per
@@ -32,6 +33,11 @@ import numpy as np  # noqa: E402
 
 METRIC = "ms/frame (feature-extract+match + BA solve), 640×480, 50 KF / 20k pts"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+# profiling stage -> the HIP kernel it brackets (the name in the rocprofv3 summaries)
+HIP_KERNEL = {"orb_pyramid": "k_pyramid", "orb_fast_harris": "k_fast", "orb_select": "k_select",
+              "orb_blur": "k_blur", "orb_describe": "k_describe", "match_partial": "k_knn_partial",
+              "match_merge": "k_knn_merge+k_knn_compact", "ba_pose_partial": "k_pose_kf",
+              "ba_landmark": "k_landmark_solve"}
 
 CONFIGS = {
     # name: (height, width, n_features, n_kf, n_lm)
@@ -69,14 +75,16 @@ def stage_bytes(stage, geo, counts):
         return (counts["n_q"] + counts["n_t"]) * 32 + counts["n_q"] * 8 * ((counts["n_t"] + 63) // 64)
     if stage == "match_merge":
         return counts["n_q"] * 8 * ((counts["n_t"] + 63) // 64) + counts["n_match"] * 12
-    if stage == "ba_pose_partial":  # uv 16 + landmark index 4 + landmark position 24 per obs
-        return counts["n_pose_obs"] * 44 + counts["n_chunks"] * 29 * 8
-    if stage == "ba_landmark":      # uv 16 + kf index 4 per obs, position read + write per landmark
-        return counts["n_lm_obs"] * 20 + counts["n_opt"] * (24 + 24 + 8) + counts["n_kf"] * 160
-    if stage == "ba_pose_solve":
-        return counts["n_kf"] * (29 * 8 + 64 + 72)
-    if stage == "ba_pose_sum":
-        return counts["n_chunks"] * 29 * 8 + counts["n_kf"] * 32 * 8
+    if stage == "ba_pose_partial":
+        # per observation: uv 16 + landmark slot 4 + landmark position 24 (gathered); per slice
+        # partial: 32 doubles written; per keyframe: pose 64 + intrinsics 32 read
+        return counts["n_pose_obs"] * 44 + counts["n_kf"] * counts["n_split"] * 256 + counts["n_kf"] * 96
+    if stage == "ba_landmark":
+        # per observation: uv 16 + keyframe 4 + landmark slot 4; per landmark: position read 24 +
+        # written 24 + CSR pointer 4; per keyframe: slice partials 29 x 8 each, pose 64 + intrinsics
+        # 32 read, pose 64 + rotation 72 + cost 16 written (by workgroup 0)
+        return (counts["n_lm_obs"] * 24 + counts["n_opt"] * 52 +
+                counts["n_kf"] * (counts["n_split"] * 232 + 96 + 152))
     return None
 
 
@@ -186,8 +194,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=30, help="frames timed for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
-    ap.add_argument("--serial", action="store_true",
-                    help="one context/stream for everything (no Extract/Match || LocalBA overlap)")
+    ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
+                    help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -197,11 +205,11 @@ def main():
     from vxslam import synth
 
     torch.cuda.set_device(dist.local_rank)
-    # frontend context (tracking: Extract + Match) and backend context (LocalBA), each with its own
-    # HIP stream; BA(t) waits on the device for Match(t) and overlaps Extract/Match(t + 1).
-    ctx = vxslam.Context(dist.local_rank)
-    bctx = ctx if args.serial else vxslam.Context(dist.local_rank)
-    ctxs = [ctx] if bctx is ctx else [ctx, bctx]
+    # one context (HIP stream) per pipeline stage; see Pipeline
+    ectx = vxslam.Context(dist.local_rank)
+    mctx = ectx if args.streams < 3 else vxslam.Context(dist.local_rank)
+    bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank)
+    ctxs = list({id(c): c for c in (ectx, mctx, bctx)}.values())
     cfg = CONFIGS[args.config]
     h, w, nf, nk, nl = cfg
     N = dist.world
@@ -219,17 +227,31 @@ def main():
     info = plan.info()
     torch.cuda.synchronize()
 
+    # Pipeline.  Frame t: Extract(t) on ectx into slot t % 3, Match(t - 1, t) on mctx, LocalBA(t) on
+    # bctx, ordered on the device by events: Match(t) after Extract(t), LocalBA(t) after Match(t),
+    # and Extract(t) after Match(t - 2) (the last reader of the slot it overwrites).  Nothing of
+    # frame t + 1 depends on Match(t) or LocalBA(t), so consecutive frames' stages overlap; with
+    # --streams 1 the same calls run back to back on one stream.
+    ev_e = ectx.event()
+    ev_m = [mctx.event() for _ in range(3)]
+
     def extract(i):
         f = frames_dev[i % args.frames]
-        ctx.orb_extract_async(f.data_ptr(), w, h, 3, w * 3, i % 2, params)
+        ectx.orb_extract_async(f.data_ptr(), w, h, 3, w * 3, i % 3, params)
+
+    for i in (-3, -2, -1):  # fill the three slots (frame -1 is step 0's previous frame)
+        extract(i)
+    slot = [ectx.slot_device(s) for s in range(3)]
 
     def step(i):
+        ectx.wait_event(ev_m[(i + 1) % 3])  # (an event not yet recorded is an immediate no-op)   # Match(i - 2) done with slot i % 3
         extract(i)
-        ctx.match_slots_async((i + 1) % 2, i % 2)
-        bctx.wait_for(ctx)
+        ectx.record(ev_e)
+        mctx.wait_event(ev_e)
+        mctx.match_device_async(slot[(i - 1) % 3], slot[i % 3])
+        mctx.record(ev_m[i % 3])
+        bctx.wait_event(ev_m[i % 3])
         plan.run_async()
-
-    extract(-1)  # previous frame for step 0's match
 
     def sync():
         for c in ctxs:
@@ -248,26 +270,40 @@ def main():
             c.prof_enable(False)
         stages = {k: (v[0] / max(v[1], 1), v[1] / args.warmup) for k, v in prof.items() if v[1]}
 
-    # ---- the timed region (HIP events only around the dominant kernel, on the stream it runs on)
+    # ---- the timed region: no events inside (a timing event pair per launch costs ~25 % here)
+    elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
+
+    # ---- roofline pass: the same K steps again, HIP events around every launch of the dominant
+    # kernel on the stream it runs on (each bracket also spans that launch's dispatch boundary)
     dominant = max(stages, key=lambda k: stages[k][0] * stages[k][1]) if stages else None
-    dctx = bctx if dominant and dominant.startswith("ba_") else ctx
+    dctx = {"ba": bctx, "ma": mctx}.get(dominant[:2] if dominant else "", ectx)
+    dom_prof, elapsed_ev = (0.0, 0), None
     if dominant:
         dctx.prof_enable(True, stages=[dominant])
-    elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
-    dom_prof = dctx.prof_read(reset=True).get(dominant, (0.0, 0)) if dominant else (0.0, 0)
-    dctx.prof_enable(False)
+        elapsed_ev = timed_loop(step, args.steps, 0, sync, dist)
+        dom_prof = dctx.prof_read(reset=True).get(dominant, (0.0, 0))
+        dctx.prof_enable(False)
+
+    # single-frame latency: one step alone through the same dependency chain, host enqueue to done
+    lat = []
+    for i in range(20):
+        sync()
+        t0 = time.perf_counter()
+        step(args.warmup + args.steps + i)
+        sync()
+        lat.append(time.perf_counter() - t0)
+    latency_ms = 1e3 * float(np.median(lat))
 
     # counts for the byte formulas
-    kps, _ = ctx.orb_fetch((args.warmup + args.steps - 1) % 2)
-    matches = ctx.match_fetch()
+    kps, _ = ectx.orb_fetch((args.warmup + args.steps + 19) % 3)
+    matches = mctx.match_fetch()
     st = plan.fetch(None)
     lw = [int(round(w / 1.2 ** l)) for l in range(8)]
     lh = [int(round(h / 1.2 ** l)) for l in range(8)]
     geo = {"W": w, "H": h, "level_px": [a * b for a, b in zip(lw, lh)]}
     counts = {"n_kp": len(kps), "n_cand": 4 * nf, "n_q": len(kps), "n_t": len(kps),
               "n_match": len(matches), "n_pose_obs": info["n_pose_obs"], "n_lm_obs": info["n_lm_obs"],
-              "n_chunks": (info["n_pose_obs"] + 255) // 256 + info["n_kf"], "n_opt": info["n_lm"],
-              "n_kf": info["n_kf"]}
+              "n_split": info["n_split"], "n_opt": info["n_opt"], "n_kf": info["n_kf"]}
 
     frames_total = args.steps * N
     ms_per_step = 1e3 * elapsed / args.steps
@@ -279,10 +315,11 @@ def main():
         nbytes = stage_bytes(dominant, geo, counts)
         if nbytes:
             achieved = nbytes / (avg_ms * 1e-3) / 1e9
-            roofline = {"kernel": dominant, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            roofline = {"kernel": dominant, "hip_kernel": HIP_KERNEL.get(dominant), "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                         "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_ms * 1e3, 2),
-                        "launches_per_step": round(dom_prof[1] / (args.steps + args.warmup), 2)}
+                        "launches_per_step": round(dom_prof[1] / args.steps, 2),
+                        "pass_ms_per_step": round(1e3 * elapsed_ev / args.steps, 4)}
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if roofline and os.path.exists(pmc):
         try:
@@ -320,17 +357,25 @@ def main():
                              f"(<= 5 alternating iterations), landmark-sharded over {N} GPU(s)"),
                 "frames_per_step": N,
                 "parallelism": f"frames: 1 per rank; BA: landmark shards x{N}" + (" + RCCL all-reduce" if N > 1 else ""),
-                "streams": "1 (serial)" if args.serial else "2: Extract+Match(t+1) || LocalBA(t), BA waits on Match(t)",
+                "streams": {1: "1: Extract, Match, LocalBA back to back",
+                            2: "2: Extract+Match | LocalBA (LocalBA(t) after Match(t))",
+                            3: "3: Extract | Match | LocalBA, device events (Match(t) after Extract(t), "
+                               "LocalBA(t) after Match(t), Extract(t) after Match(t-2))"}[args.streams],
                 "ba_window_kf": nk * N,
                 "ba_landmarks": nl * N,
                 "orb_features": nf,
             },
+            # one frame alone through the same dependency chain (host enqueue to completion, median
+            # of 20): the per-frame latency; `value` is the pipelined throughput
+            "latency_ms_per_frame": round(latency_ms, 4),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_us": {k: round(v[0] * 1e3, 2) for k, v in stages.items()},
         }
         print(json.dumps(out), flush=True)
     plan.close()
+    for e in [ev_e] + ev_m:
+        e.close()
     for c in reversed(ctxs):
         c.close()
     dist.close()

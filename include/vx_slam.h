@@ -85,6 +85,13 @@ int vx_synchronize(vx_ctx* ctx);
  * LocalBA of keyframe t, which needs tracking(t)) overlaps the frontend context's Extract/Match
  * of frame t+1 — the concurrency ORB-SLAM-style systems get from a separate mapping thread. */
 int vx_stream_wait_ctx(vx_ctx* ctx, vx_ctx* after);
+/* Device events for finer cross-context ordering (a pipeline that must wait for one specific
+ * earlier step of another context, not for everything enqueued on it so far). */
+typedef struct vx_event vx_event;
+int vx_event_create(vx_ctx* ctx, vx_event** out);
+int vx_event_record(vx_ctx* ctx, vx_event* ev); /* marks everything enqueued on ctx so far */
+int vx_event_wait(vx_ctx* ctx, vx_event* ev);   /* later work on ctx waits for the marked work */
+void vx_event_destroy(vx_event* ev);
 void vx_orb_default_params(vx_orb_params* p);
 /* Copies the compiled-in rBRIEF pattern (bit_pattern_31_, 256 x {x1,y1,x2,y2}). */
 int vx_orb_pattern(int32_t* out_1024);
@@ -103,8 +110,11 @@ int vx_orb_extract_async(vx_ctx* ctx, const vx_orb_params* params, const uint8_t
                          int width, int height, int channels, int64_t row_stride, int slot);
 int vx_orb_fetch(vx_ctx* ctx, int slot, vx_keypoint* out_kp, uint8_t* out_desc, int cap,
                  int* n_out);
-/* Device pointers of a slot's descriptor rows and its device-side count (for interop). */
-int vx_orb_slot_device(vx_ctx* ctx, int slot, const uint8_t** d_desc, const int32_t** d_count);
+/* Device pointers of a slot's descriptor rows and its device-side count, and its row capacity
+ * (for interop and for vx_match_device_async from another context).  Stable until the ORB
+ * geometry (image size / params) of the context changes. */
+int vx_orb_slot_device(vx_ctx* ctx, int slot, const uint8_t** d_desc, const int32_t** d_count,
+                       int32_t* cap);
 
 /* ---------------------------------------------------------------- matching
  * knnMatch(query = last frame, train = current frame, k = 2) + ratio test
@@ -114,6 +124,11 @@ int vx_match_knn2_ratio(vx_ctx* ctx, const uint8_t* query_desc, int n_query,
                         int cap, int* n_out);
 /* Device-resident variant matching two extraction slots (counts read on device). */
 int vx_match_slots_async(vx_ctx* ctx, int query_slot, int train_slot, float ratio);
+/* Device-resident variant over any device descriptor sets whose row counts are device-side
+ * (e.g. another context's slots, vx_orb_slot_device); cap_* bound the rows.  Enqueued on ctx's
+ * stream: order it after the producer with vx_event_wait / vx_stream_wait_ctx. */
+int vx_match_device_async(vx_ctx* ctx, const uint8_t* d_query, const int32_t* d_n_query, int cap_query,
+                          const uint8_t* d_train, const int32_t* d_n_train, int cap_train, float ratio);
 int vx_match_fetch(vx_ctx* ctx, vx_match* out, int cap, int* n_out);
 
 /* ---------------------------------------------------------------- local bundle adjustment
@@ -174,8 +189,9 @@ int vx_ba_plan_create(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, i
 int vx_ba_plan_run_async(vx_ctx* ctx, vx_ba_plan* plan);
 int vx_ba_plan_fetch(vx_ctx* ctx, vx_ba_plan* plan, vx_map_view* map, vx_ba_stats* stats);
 void vx_ba_plan_destroy(vx_ba_plan* plan);
-/* sizes of the device problem: n_kf, n_lm (local shard), n_pose_obs, n_lm_obs */
-int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out4);
+/* sizes of the device problem: out8 = {n_kf, n_lm (local shard), n_pose_obs, n_lm_obs, n_opt,
+ * n_split (pose-stage workgroups per keyframe), n_lm_blocks (landmark-stage workgroups), 0} */
+int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out8);
 /* Host-only dry run of vx_ba_plan_create (needs no device): out8 = {status, n_window_kf,
  * n_landmarks (all shards), n_kf, n_opt (local optimisable), n_lm (local table), n_pose_obs,
  * n_lm_obs}; lm_map_idx / kf_map_idx (optional) receive the local tables as map indices. */

@@ -254,39 +254,59 @@ def test_ba_plan_is_repeatable(ctx, oracle):
 
 
 def test_frontend_backend_contexts_overlap(ctx, oracle):
-    """bench.py's pipeline: Extract/Match on one context, LocalBA on a second context ordered after
-    Match(t) by vx_stream_wait_ctx, so BA(t) runs concurrently with Extract/Match(t + 1).  Results
-    equal the CPU restatement exactly as in the serial case."""
+    """bench.py's pipeline: Extract, Match and LocalBA on three contexts ordered on the device by
+    vx_event_* (Match(t) after Extract(t), LocalBA(t) after Match(t), Extract(t) after Match(t-2),
+    three rotating slots, matching another context's slots via vx_orb_slot_device), so stages of
+    consecutive frames run concurrently.  Every frame's results equal the CPU restatement."""
     import torch
     import vxslam
 
-    back = vxslam.Context(0)
+    mctx, bctx = vxslam.Context(0), vxslam.Context(0)
+    evs = []
     try:
-        frames = synth.make_frames(43, 4)
+        n = 6
+        frames = synth.make_frames(43, n)
         d = torch.from_numpy(frames).cuda()
         torch.cuda.synchronize()
         p = _orb_params(vxslam, 2000)
         m = synth.make_ba_map(78, 10, 2000, n_old_kf=2)
         opts = dict(window=10)
-        plan = back.ba_plan(m, vxslam.default_ba_options(**opts))
-        for i in range(4):
-            ctx.orb_extract_async(d[i].data_ptr(), 640, 480, 3, 640 * 3, i % 2, p)
+        plan = bctx.ba_plan(m, vxslam.default_ba_options(**opts))
+        ev_e, ev_m = ctx.event(), [mctx.event() for _ in range(3)]
+        evs = [ev_e] + ev_m
+        for i in range(3):  # slots must hold an extraction before their device pointers are read
+            ctx.orb_extract_async(d[0].data_ptr(), 640, 480, 3, 640 * 3, i, p)
+        slot = [ctx.slot_device(s) for s in range(3)]
+        desc = {}
+        for i in range(n):
+            ctx.wait_event(ev_m[(i + 1) % 3])
+            ctx.orb_extract_async(d[i].data_ptr(), 640, 480, 3, 640 * 3, i % 3, p)
+            ctx.record(ev_e)
             if i:
-                ctx.match_slots_async((i - 1) % 2, i % 2)
-            back.wait_for(ctx)
+                mctx.wait_event(ev_e)
+                mctx.match_device_async(slot[(i - 1) % 3], slot[i % 3])
+                mctx.record(ev_m[i % 3])
+                bctx.wait_event(ev_m[i % 3])
             plan.run_async()
+            if i >= n - 2:
+                ctx.synchronize()
+                desc[i] = ctx.orb_fetch(i % 3)
         mg = m.copy()
         st_g = plan.fetch(mg)
-        got = ctx.match_fetch()
-        k3, d3 = ctx.orb_fetch(1)
-        _, dc2 = oracle.orb_extract(frames[2], 2000, order=oracle.ORDER_RASTER)
-        kc3, dc3 = oracle.orb_extract(frames[3], 2000, order=oracle.ORDER_RASTER)
-        _assert_orb_equal(k3, d3, kc3, dc3)
-        assert np.array_equal(got, oracle.match(dc2, dc3))
+        got = mctx.match_fetch()
+        _, dc4 = oracle.orb_extract(frames[n - 2], 2000, order=oracle.ORDER_RASTER)
+        kc5, dc5 = oracle.orb_extract(frames[n - 1], 2000, order=oracle.ORDER_RASTER)
+        _assert_orb_equal(*desc[n - 1], kc5, dc5)
+        assert np.array_equal(desc[n - 2][1], dc4)
+        assert np.array_equal(got, oracle.match(dc4, dc5))
         mc = m.copy()
         st_c = oracle.ba_optimize(mc, oracle.ba_options(**opts))
         _assert_ba_close(mg, mc, st_g, st_c)
-        back.wait_for(back)  # same context: no-op
+        bctx.wait_for(mctx)
+        bctx.wait_for(bctx)  # same context: no-op
         plan.close()
     finally:
-        back.close()
+        for e in evs:
+            e.close()
+        bctx.close()
+        mctx.close()

@@ -1081,12 +1081,10 @@ uint32_t vx_ba_shard_of(uint64_t lm_id, int shard_count) {
     return shard_count <= 1 ? 0u : (uint32_t)(vx::splitmix64(lm_id) % (uint64_t)shard_count);
 }
 
-int vx_ba_plan_info(const vx_ba_plan* p, int64_t* out4) {
-    if (!p || !out4) return VX_ERR_INVALID;
-    out4[0] = p->n_kf;
-    out4[1] = p->n_lm;
-    out4[2] = p->n_pose_obs;
-    out4[3] = p->n_lm_obs;
+int vx_ba_plan_info(const vx_ba_plan* p, int64_t* out8) {
+    if (!p || !out8) return VX_ERR_INVALID;
+    const int64_t v[8] = {p->n_kf, p->n_lm, p->n_pose_obs, p->n_lm_obs, p->n_opt, p->n_split, p->n_lm_blocks, 0};
+    for (int i = 0; i < 8; ++i) out8[i] = v[i];
     return VX_OK;
 }
 

@@ -179,6 +179,16 @@ int vx_match_slots_async(vx_ctx* c, int qs, int ts, float ratio) {
                          b.count.as<int>(), b.cap, a.cap, b.cap, ratio);
 }
 
+int vx_match_device_async(vx_ctx* c, const uint8_t* dq, const int32_t* dnq, int q_cap, const uint8_t* dt,
+                          const int32_t* dnt, int t_cap, float ratio) {
+    if (!c) return VX_ERR_INVALID;
+    if (!dq || !dnq || !dt || !dnt || q_cap < 0 || t_cap < 0)
+        return set_error(c, VX_ERR_INVALID, "vx_match_device_async: null buffers or negative capacity");
+    if (t_cap > (1 << 22)) return set_error(c, VX_ERR_INVALID, "train set larger than 2^22 rows");
+    VX_HIP(c, hipSetDevice(c->device));
+    return match_enqueue(c, dq, dnq, q_cap, dt, dnt, t_cap, q_cap, t_cap, ratio);
+}
+
 int vx_match_fetch(vx_ctx* c, vx_match* out, int cap, int* n_out) {
     if (!c || !n_out) return VX_ERR_INVALID;
     if (!c->match_valid) return set_error(c, VX_ERR_STATE, "no match enqueued");

@@ -27,6 +27,7 @@
 #include <cstring>
 
 #include "vx_internal.hpp"
+#include "vx_ktrace.hpp"
 
 #include "orb_pattern_31.inc"
 
@@ -34,6 +35,8 @@ namespace vx {
 namespace {
 
 constexpr int kBlock = 256;
+
+VX_KT_TABLE();
 
 __constant__ signed char c_pattern[1024];
 __constant__ int c_umax[16];
@@ -129,6 +132,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
     int* stab = reinterpret_cast<int*>(prev + a.pr_buf);  // packed {ofs | c1 << 16} per level
     const int tid = threadIdx.x, lx = tid & 63, ly = tid >> 6;
     const int L = a.L;
+    VX_KT(0);
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = tid; i < hist_n; i += kPyBlock) hist[i] = 0;
     if (tid < L) srx[tid] = tabs[a.pr_x + (long long)blockIdx.x * L + tid];
@@ -179,6 +183,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
             }
     }
     __syncthreads();
+    VX_KT(1);
     for (int yy = ly; yy < ph; yy += 16) {
         const int y = py0 + yy;
         const bool oy = y >= ry.z && y < ry.w;
@@ -190,6 +195,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
             if (oy && x >= rx.z && x < rx.w) drow[x] = g;
         }
     }
+    VX_KT(2);
     for (int l = 1; l < L; ++l) {
         uint8_t* t = cur;
         cur = prev;
@@ -223,6 +229,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
         pw = nw;
         ph = nh;
     }
+    VX_KT(3);
 }
 
 // ------------------------------------------------------------------------------ resize
@@ -359,6 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     const int tx = t % ntx, ty = t / ntx;
     const int x0 = tx * kTX, y0 = ty * kTY;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    VX_KT(4);
     if (tid == 0) s_n = 0;
     stage_lds<kBlock, (kTH * kTW + kBlock - 1) / kBlock>(tile, kTH * kTW, [&](int i) {
         const int r = i / kTW, c = i - r * kTW;
@@ -367,6 +375,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
         return img[(long long)gy * W + gx];
     });
     __syncthreads();
+    VX_KT(5);
     const int thr = a.fast_threshold;
     for (int i = tid; i < kSH * kSW; i += kBlock) {
         const int r = i / kSW, c = i - r * kSW;
@@ -376,6 +385,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
         sc[i] = (uint8_t)s;
     }
     __syncthreads();
+    VX_KT(6);
     const int e = a.edge;
     for (int r = wv; r < kTY; r += kBlock / 64) {
         const int y = y0 + r, x = x0 + lane;
@@ -395,6 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
         }
     }
     __syncthreads();
+    VX_KT(7);
     // Harris 7x7 (HarrisResponses): one wave per candidate, lane < 49 takes one window pixel.
     const int n = s_n;
     const int dy = lane / 7 - 3, dx = lane % 7 - 3;
@@ -430,6 +441,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
             atomicAdd(&hist[l * 256 + s], 1);
         }
     }
+    VX_KT(8);
 }
 
 // ------------------------------------------------------------------------------ blur
@@ -439,6 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_blur(const uint8_t* __restrict__ pyr
     __shared__ uint8_t sin_[(TYo + 6) * (TXo + 6)];
     __shared__ float srow[(TYo + 6) * TXo];
     const int b = blockIdx.x;
+    VX_KT(9);
     int l = 0;
     while (l + 1 < a.L && b >= a.bbase[l + 1]) ++l;
     const int W = a.lw[l], H = a.lh[l];
@@ -459,6 +472,7 @@ __global__ __launch_bounds__(kBlock) void k_blur(const uint8_t* __restrict__ pyr
         return img[(long long)refl(y0 - 3 + r, H) * W + refl(x0 - 3 + c, W)];
     });
     __syncthreads();
+    VX_KT(10);
     const float k0 = a.gk[0], k1 = a.gk[1], k2 = a.gk[2], k3 = a.gk[3], k4 = a.gk[4],
                 k5 = a.gk[5], k6 = a.gk[6];
     for (int i = threadIdx.x; i < (TYo + 6) * TXo; i += kBlock) {
@@ -487,6 +501,7 @@ __global__ __launch_bounds__(kBlock) void k_blur(const uint8_t* __restrict__ pyr
         const int v = __float2int_rn(s);
         out[(long long)y * W + x] = (uint8_t)min(255, max(0, v));
     }
+    VX_KT(11);
 }
 
 // ------------------------------------------------------------------------------ select
@@ -530,6 +545,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     __shared__ CandRec srec[kSelRecLds];  // retainBest(2q) survivors (32 KB)
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
+    VX_KT(12);
     const int ncell = a.lh[l] * a.ntx[l];
     const long long cbase = a.cell_base[l];
     CandRec* kept = stage + a.stage_base[l];                      // retainBest(2q) result
@@ -602,6 +618,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
         }
     }
     __syncthreads();
+    VX_KT(13);
     // ---- retainBest(q) by Harris: exact q-th largest key by a 4-pass radix select over the
     // survivors (keys held in registers when K1 <= 2 * kSelBlock), then an ordered compaction
     int K2 = 0;
@@ -640,6 +657,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
             }
             thr2 = key2f(prefix);
         }
+        VX_KT(14);
         for (int base = 0; base < K1; base += kSelBlock) {
             const int j = base + tid;
             CandRec r{};
@@ -655,6 +673,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
         }
     }
     if (tid == 0) level_count[l] = K2;
+    VX_KT(15);
 }
 
 // ------------------------------------------------------------------------------ describe
@@ -1145,6 +1164,10 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
 
 }  // namespace vx
 
+namespace vx {
+VX_KT_EXPORT(vx_ktrace_read_orb);  // extern "C": the namespace does not enter the symbol
+}
+
 using namespace vx;
 
 extern "C" {
@@ -1200,10 +1223,11 @@ int vx_orb_fetch(vx_ctx* c, int slot, vx_keypoint* out_kp, uint8_t* out_desc, in
     return VX_OK;
 }
 
-int vx_orb_slot_device(vx_ctx* c, int slot, const uint8_t** d_desc, const int32_t** d_count) {
+int vx_orb_slot_device(vx_ctx* c, int slot, const uint8_t** d_desc, const int32_t** d_count, int32_t* cap) {
     if (!c || slot < 0 || slot >= VX_MAX_SLOTS || !c->slots[slot].valid) return VX_ERR_INVALID;
     if (d_desc) *d_desc = c->slots[slot].desc.as<uint8_t>();
     if (d_count) *d_count = c->slots[slot].count.as<int32_t>();
+    if (cap) *cap = c->slots[slot].cap;
     return VX_OK;
 }
 

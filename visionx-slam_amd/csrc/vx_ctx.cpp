@@ -81,14 +81,16 @@ int vx_create(int device, vx_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return VX_ERR_HIP;
     auto* c = new vx_ctx();
     c->device = device;
+    if (const char* f = std::getenv("VX_ORB_FORK")) c->orb_fork = std::atoi(f) != 0;
+    // one HIP stream per context (HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues, 4 by
+    // default: streams beyond that share queues and serialise); the fork stream only on request
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess) {
+        (c->orb_fork && (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+                         hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+                         hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess))) {
         vx_destroy(c);
         return VX_ERR_HIP;
     }
-    if (const char* f = std::getenv("VX_ORB_FORK")) c->orb_fork = std::atoi(f) != 0;
     *out = c;
     return VX_OK;
 }
@@ -131,6 +133,41 @@ int vx_stream_wait_ctx(vx_ctx* c, vx_ctx* after) {
     VX_HIP(c, hipEventRecord(after->order_event, after->stream));
     VX_HIP(c, hipStreamWaitEvent(c->stream, after->order_event, 0));
     return VX_OK;
+}
+
+int vx_event_create(vx_ctx* c, vx_event** out) {
+    if (!c || !out) return VX_ERR_INVALID;
+    *out = nullptr;
+    VX_HIP(c, hipSetDevice(c->device));
+    auto* e = new vx_event();
+    e->device = c->device;
+    const hipError_t r = hipEventCreateWithFlags(&e->ev, hipEventDisableTiming);
+    if (r != hipSuccess) {
+        delete e;
+        return vx::hip_fail(c, r, "hipEventCreateWithFlags");
+    }
+    *out = e;
+    return VX_OK;
+}
+
+int vx_event_record(vx_ctx* c, vx_event* e) {
+    if (!c || !e) return VX_ERR_INVALID;
+    if (e->device != c->device) return vx::set_error(c, VX_ERR_INVALID, "vx_event_record: event of device %d", e->device);
+    VX_HIP(c, hipEventRecord(e->ev, c->stream));
+    return VX_OK;
+}
+
+int vx_event_wait(vx_ctx* c, vx_event* e) {
+    if (!c || !e) return VX_ERR_INVALID;
+    if (e->device != c->device) return vx::set_error(c, VX_ERR_INVALID, "vx_event_wait: event of device %d", e->device);
+    VX_HIP(c, hipStreamWaitEvent(c->stream, e->ev, 0));
+    return VX_OK;
+}
+
+void vx_event_destroy(vx_event* e) {
+    if (!e) return;
+    (void)hipEventDestroy(e->ev);
+    delete e;
 }
 
 int vx_prof_enable(vx_ctx* c, int mask) {

@@ -127,6 +127,11 @@ struct ProfEvent {
 
 struct vx_ba_plan;
 
+struct vx_event {
+    int device = 0;
+    hipEvent_t ev = nullptr;
+};
+
 struct vx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;

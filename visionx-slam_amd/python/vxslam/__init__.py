@@ -61,9 +61,10 @@ class BAStats(C.Structure):
 
 EXPORTS = [
     "vx_version", "vx_create", "vx_destroy", "vx_last_error", "vx_stream", "vx_synchronize",
-    "vx_stream_wait_ctx", "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
+    "vx_stream_wait_ctx", "vx_event_create", "vx_event_record", "vx_event_wait", "vx_event_destroy",
+    "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
     "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
-    "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
+    "vx_match_device_async", "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
     "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info",
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read",
@@ -91,6 +92,15 @@ def lib():
         L.vx_stream.argtypes = [C.c_void_p]
         L.vx_synchronize.argtypes = [C.c_void_p]
         L.vx_stream_wait_ctx.argtypes = [C.c_void_p, C.c_void_p]
+        L.vx_event_create.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+        L.vx_event_record.argtypes = [C.c_void_p, C.c_void_p]
+        L.vx_event_wait.argtypes = [C.c_void_p, C.c_void_p]
+        L.vx_event_destroy.argtypes = [C.c_void_p]
+        L.vx_event_destroy.restype = None
+        L.vx_orb_slot_device.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_int32)]
+        L.vx_match_device_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                            C.c_int, C.c_float]
         L.vx_prof_name.restype = C.c_char_p
         L.vx_ba_plan_destroy.argtypes = [C.c_void_p]
         L.vx_ba_plan_destroy.restype = None
@@ -158,6 +168,25 @@ def ba_plan_inspect(m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1) -
 
 def ba_shard_of(lm_id: int, shard_count: int) -> int:
     return int(lib().vx_ba_shard_of(C.c_uint64(int(lm_id)), int(shard_count)))
+
+
+class Event:
+    """A device event (vx_event) for cross-context ordering."""
+
+    def __init__(self, ctx: "Context"):
+        self._h = C.c_void_p()
+        ctx._check(lib().vx_event_create(ctx.handle, C.byref(self._h)))
+
+    def close(self):
+        if self._h:
+            lib().vx_event_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Context:
@@ -243,6 +272,27 @@ class Context:
     def match_slots_async(self, q_slot: int, t_slot: int, ratio: float = 0.8):
         self._check(lib().vx_match_slots_async(self._h, q_slot, t_slot, C.c_float(ratio)))
 
+    def slot_device(self, slot: int):
+        """(device descriptor pointer, device count pointer, row capacity) of an extraction slot."""
+        d, n, cap = C.c_void_p(), C.c_void_p(), C.c_int32()
+        self._check(lib().vx_orb_slot_device(self._h, slot, C.byref(d), C.byref(n), C.byref(cap)))
+        return d.value, n.value, cap.value
+
+    def match_device_async(self, query, train, ratio: float = 0.8):
+        """Match device descriptor sets given as slot_device() triples (possibly of another context)."""
+        (dq, nq, cq), (dt, nt, ct) = query, train
+        self._check(lib().vx_match_device_async(self._h, C.c_void_p(dq), C.c_void_p(nq), cq, C.c_void_p(dt),
+                                                C.c_void_p(nt), ct, C.c_float(ratio)))
+
+    def event(self) -> "Event":
+        return Event(self)
+
+    def record(self, ev: "Event"):
+        self._check(lib().vx_event_record(self._h, ev._h))
+
+    def wait_event(self, ev: "Event"):
+        self._check(lib().vx_event_wait(self._h, ev._h))
+
     def match_fetch(self, cap: int = 8192):
         out = np.zeros(cap, MATCH_DTYPE)
         n = C.c_int(0)
@@ -312,10 +362,11 @@ class BAPlan:
                                            shard_count, C.byref(self._h)))
 
     def info(self):
-        out = np.zeros(4, np.int64)
+        out = np.zeros(8, np.int64)
         rc = lib().vx_ba_plan_info(self._h, _p(out))
         assert rc == 0
-        return dict(n_kf=int(out[0]), n_lm=int(out[1]), n_pose_obs=int(out[2]), n_lm_obs=int(out[3]))
+        keys = ["n_kf", "n_lm", "n_pose_obs", "n_lm_obs", "n_opt", "n_split", "n_lm_blocks"]
+        return {k: int(v) for k, v in zip(keys, out)}
 
     def run_async(self):
         self.ctx._check(lib().vx_ba_plan_run_async(self.ctx.handle, self._h))
