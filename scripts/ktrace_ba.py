@@ -21,19 +21,23 @@ from vxslam import synth  # noqa: E402
 KT_BLOCKS, KT_SLOTS = 64, 16
 
 
-def read():
-    out = np.zeros(KT_BLOCKS * KT_SLOTS, np.int64)
-    assert vxslam.lib().vx_ktrace_read_ba(C.c_void_p(out.ctypes.data)) == 0
-    return out.reshape(KT_BLOCKS, KT_SLOTS)
+def read(fn="vx_ktrace_read_ba"):
+    """(wall_clock64 table, s_memtime table), each [block][slot]"""
+    out = np.zeros(2 * KT_BLOCKS * KT_SLOTS, np.int64)
+    assert getattr(vxslam.lib(), fn)(C.c_void_p(out.ctypes.data)) == 0
+    return out.reshape(2, KT_BLOCKS, KT_SLOTS)
 
 
-def report(tr, slots, name):
+def report(tr2, slots, name):
+    tr, cy = tr2
     base = tr[:, slots[0]]
     ok = base > 0
     print(f"{name}: {int(ok.sum())} workgroups traced, start spread {(base[ok].max() - base[ok].min()) / 100:.2f} us")
     for s in slots[1:]:
         d = (tr[ok, s] - base[ok]) / 100.0  # 100 MHz ticks -> us
-        print(f"  slot {s:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us")
+        c = (cy[ok, s] - cy[ok, slots[0]])
+        clk = np.median(c / np.maximum(d, 1e-3)) / 1e3  # cycles per us -> GHz
+        print(f"  slot {s:2d}: median {np.median(d):7.2f} us  max {d.max():7.2f} us  ({np.median(c):8.0f} cycles, {clk:.2f} GHz)")
 
 
 def main():

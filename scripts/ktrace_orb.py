@@ -3,18 +3,15 @@
 
     make -C visionx-slam_amd trace && VX_LIB=visionx-slam_amd/lib/libvxslam_trace.so python3 scripts/ktrace_orb.py
 """
-import ctypes as C
 import os
 import sys
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 import vxslam  # noqa: E402
 from vxslam import synth  # noqa: E402
-from ktrace_ba import KT_BLOCKS, KT_SLOTS, report  # noqa: E402
+from ktrace_ba import read, report  # noqa: E402
 
 
 def main():
@@ -23,9 +20,7 @@ def main():
     p = vxslam.default_orb_params(n_features=2000)
     for _ in range(30):
         ctx.orb_extract(f, p)
-    out = np.zeros(KT_BLOCKS * KT_SLOTS, np.int64)
-    assert vxslam.lib().vx_ktrace_read_orb(C.c_void_p(out.ctypes.data)) == 0
-    tr = out.reshape(KT_BLOCKS, KT_SLOTS)
+    tr = read("vx_ktrace_read_orb")
     report(tr, [0, 1, 2, 3], "k_pyramid (1 tables + BGR staged, 2 gray level 0, 3 levels 1..L-1)")
     report(tr, [4, 5, 6, 7, 8], "k_fast (5 tile staged, 6 FAST scores, 7 NMS + cells, 8 Harris + stores)")
     report(tr, [9, 10, 11], "k_blur (10 tile staged, 11 both passes + store)")

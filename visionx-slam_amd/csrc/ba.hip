@@ -30,6 +30,7 @@
 // The step keeps the reference's sign (b = -J^T e, :156 and :224): this is a drop-in, not a fix.
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <cstring>
 #include <unordered_map>
 #include <unordered_set>
@@ -43,9 +44,12 @@ namespace {
 
 constexpr int kPoseBlock = 512;  // threads per pose-stage workgroup
 constexpr int kNTerms = 29;      // 21 H (upper) + 6 b + cost + count
-constexpr int kStride = 32;      // doubles per keyframe block
+constexpr int kStride = 32;      // doubles per keyframe block in global memory
+// LDS slot stride of k_landmark_solve: 33, not 32 doubles — a 256-B stride is one full turn of the
+// 64 four-byte LDS banks, so lanes reading different keyframes' slots would all hit one bank
+constexpr int kLdsStride = 33;
 constexpr int kMaxIter = 64;
-constexpr int kMaxKfLds = 256;   // keyframes whose 32-double slots fit the LDS of k_landmark_solve
+constexpr int kMaxKfLds = 256;   // keyframes whose LDS slots fit k_landmark_solve
 constexpr int kMaxSplit = 4;     // pose-stage workgroups per keyframe
 constexpr int kCombine = 6;      // (keyframe, term) pairs per thread per combine pass
 constexpr int kLmBlock = 512;    // k_landmark_solve: threads = max observations = max landmarks
@@ -97,6 +101,97 @@ __device__ __forceinline__ double frcp(double b) {
     return r;
 }
 
+// 1 / sqrt(x): v_rsq_f64 and two Newton steps (x > 0 at the call sites).
+__device__ __forceinline__ double frsq(double x) {
+    double r = __builtin_amdgcn_rsq(x);
+    const double hx = 0.5 * x;
+    r = r * fma(-hx * r, r, 1.5);
+    r = r * fma(-hx * r, r, 1.5);
+    return r;
+}
+
+// 64-bit cross-lane exchanges for the reduction butterfly, on the VALU instead of the LDS crossbar
+// (ds_bpermute): gfx950's v_permlane32/16_swap exchange a register pair across lane halves /
+// 16-lane groups; DPP row_ror:8 and quad_perm give xor 8, 2, 1; ds_swizzle's xor mode gives xor 4.
+__device__ __forceinline__ void swap_lanes32(double& a, double& b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+    a = __hiloint2double(hi[0], lo[0]);
+    b = __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ void swap_lanes16(double& a, double& b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+    a = __hiloint2double(hi[0], lo[0]);
+    b = __hiloint2double(hi[1], lo[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xF, 0xF, false),
+                            __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ double xor4_64(double x) {
+    constexpr int kXor4 = 0x1F | (4 << 10);  // ds_swizzle bitmask mode: and 0x1F, or 0, xor 4
+    return __hiloint2double(__builtin_amdgcn_ds_swizzle(__double2hiint(x), kXor4),
+                            __builtin_amdgcn_ds_swizzle(__double2loint(x), kXor4));
+}
+
+// Halving butterfly over a wave: r holds 32 terms per lane; afterwards lanes 2t and 2t + 1 hold
+// term t summed over the 64 lanes.  Each stage keeps half of the remaining terms (which half is
+// chosen by the lane bit of that stage) and adds the partner's copy of it: 16 + 8 + 4 + 2 + 1 + 1
+// exchanges instead of 32 x 6.  Fixed order, so the result is deterministic.
+__device__ __forceinline__ double wave_sum32(double* r) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // xor 32: lanes < 32 keep terms 0..15
+        swap_lanes32(r[i], r[i + 16]);
+        r[i] = r[i] + r[i + 16];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {   // xor 16
+        swap_lanes16(r[i], r[i + 8]);
+        r[i] = r[i] + r[i + 8];
+    }
+    {
+        const bool up = lane & 8;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {  // xor 8: row rotate by 8 within 16-lane rows
+            const double send = up ? r[i] : r[i + 4], keep = up ? r[i + 4] : r[i];
+            r[i] = keep + dpp64<0x128>(send);
+        }
+    }
+    {
+        const bool up = lane & 4;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const double send = up ? r[i] : r[i + 2], keep = up ? r[i + 2] : r[i];
+            r[i] = keep + xor4_64(send);
+        }
+    }
+    {
+        const bool up = lane & 2;
+        const double send = up ? r[0] : r[1], keep = up ? r[1] : r[0];
+        r[0] = keep + dpp64<0x4E>(send);  // quad_perm [2,3,0,1]: xor 2
+    }
+    return r[0] + dpp64<0xB1>(r[0]);      // quad_perm [1,0,3,2]: xor 1
+}
+
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// Pairwise (tree) sum of v[0..n): log2(n) dependent adds instead of n - 1.
+template <int n>
+__device__ __forceinline__ double tsum(const double* v) {
+    if constexpr (n == 0) return 0.0;
+    else if constexpr (n == 1) return v[0];
+    else return tsum<n / 2>(v) + tsum<n - n / 2>(v + n / 2);
+}
+
 // Iteration `it` reads the poses of iteration it-1 (the initial poses at it == 0) and writes the
 // other buffer, so no launch ever reads a pose another workgroup of the same launch writes.  The
 // landmarks [n_opt, n_lm) are never optimised (other shards' landmarks) and always read initial.
@@ -135,85 +230,51 @@ __device__ __forceinline__ void rot_from_quat(const double* q, double* R) {
     R[6] = txz - twy;         R[7] = tyz + twx;         R[8] = 1.0 - (txx + tyy);
 }
 
-// Eigen::LDLT (lower, diagonal pivoting) compute + solve, row-major N x N in registers.  The
-// pivot permutation is data dependent; every swap is written with compile-time indices under a
-// runtime predicate so the matrix stays in VGPRs (no scratch).
+// Solution of H x = b for the SPD systems of both stages (H = sum w J^T J + 1e-6 I,
+// local_ba.cpp:167-168 and :232-233) by an UNPIVOTED LDL^T with tree-summed dot products.  Eigen's
+// LDLT pivots on the diagonal; on an SPD matrix the factors are the same up to rounding, and the
+// unpivoted form with pairwise sums roughly halves the FP64 dependency chain the solve sits on
+// (each dependent FP64 op costs ~35 cycles on gfx950).  Zero pivots are treated as Eigen does
+// (column left unscaled, solution component 0).  A: row-major N x N, lower triangle read.
 template <int N>
-__device__ __forceinline__ void ldlt_solve(double* A, const double* b, double* x) {
-    int tr[N];
+__device__ __forceinline__ void ldlt_spd_solve(const double* A, const double* b, double* x) {
+    double L[N][N], d[N], inv[N];
+    static_for<0, N>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        double v[N > 1 ? N : 1], t[N > 1 ? N : 1];
 #pragma unroll
-    for (int k = 0; k < N; ++k) {
-        int big = k;
-        double bv = fabs(A[k * N + k]);
+        for (int j = 0; j < k; ++j) v[j] = L[k][j] * d[j];
+#pragma unroll
+        for (int j = 0; j < k; ++j) t[j] = L[k][j] * v[j];
+        d[k] = A[k * N + k] - tsum<k>(t);
+        const bool nz = fabs(d[k]) > 0.0;
+        const double ik = nz ? frcp(d[k]) : 1.0;
+        inv[k] = fabs(d[k]) > 2.2250738585072014e-308 ? frcp(d[k]) : 0.0;
 #pragma unroll
         for (int i = k + 1; i < N; ++i) {
-            const double v = fabs(A[i * N + i]);
-            if (v > bv) { bv = v; big = i; }
+            double u[N > 1 ? N : 1];
+#pragma unroll
+            for (int j = 0; j < k; ++j) u[j] = L[i][j] * v[j];
+            L[i][k] = (A[i * N + k] - tsum<k>(u)) * ik;
         }
-        tr[k] = big;
+    });
+    double y[N];
+    static_for<0, N>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        double u[N > 1 ? N : 1];
 #pragma unroll
-        for (int bi = k + 1; bi < N; ++bi) {
-            if (bi == big) {
+        for (int j = 0; j < i; ++j) u[j] = L[i][j] * y[j];
+        y[i] = b[i] - tsum<i>(u);
+    });
 #pragma unroll
-                for (int j = 0; j < k; ++j) { const double t = A[k * N + j]; A[k * N + j] = A[bi * N + j]; A[bi * N + j] = t; }
+    for (int i = 0; i < N; ++i) y[i] *= inv[i];
+    static_for<0, N>([&](auto rc) {
+        constexpr int i = N - 1 - decltype(rc)::value;
+        double u[N > 1 ? N : 1];
 #pragma unroll
-                for (int i = bi + 1; i < N; ++i) { const double t = A[i * N + k]; A[i * N + k] = A[i * N + bi]; A[i * N + bi] = t; }
-                { const double t = A[k * N + k]; A[k * N + k] = A[bi * N + bi]; A[bi * N + bi] = t; }
-#pragma unroll
-                for (int i = k + 1; i < bi; ++i) { const double t = A[i * N + k]; A[i * N + k] = A[bi * N + i]; A[bi * N + i] = t; }
-            }
-        }
-        if (k > 0) {
-            double temp[N];
-#pragma unroll
-            for (int j = 0; j < k; ++j) temp[j] = A[j * N + j] * A[k * N + j];
-            double s = 0;
-#pragma unroll
-            for (int j = 0; j < k; ++j) s += A[k * N + j] * temp[j];
-            A[k * N + k] -= s;
-#pragma unroll
-            for (int i = k + 1; i < N; ++i) {
-                double t = 0;
-#pragma unroll
-                for (int j = 0; j < k; ++j) t += A[i * N + j] * temp[j];
-                A[i * N + k] -= t;
-            }
-        }
-        const double akk = A[k * N + k];
-        if (fabs(akk) > 0.0) {
-            const double inv = frcp(akk);
-#pragma unroll
-            for (int i = k + 1; i < N; ++i) A[i * N + k] *= inv;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) x[i] = b[i];
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-#pragma unroll
-        for (int bi = k + 1; bi < N; ++bi)
-            if (tr[k] == bi) { const double t = x[k]; x[k] = x[bi]; x[bi] = t; }
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-#pragma unroll
-        for (int r = i + 1; r < N; ++r) x[r] -= x[i] * A[r * N + i];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-        const double d = A[i * N + i];
-        x[i] = fabs(d) > 2.2250738585072014e-308 ? x[i] * frcp(d) : 0.0;
-    }
-#pragma unroll
-    for (int i = N - 1; i >= 0; --i) {
-        double s = 0;
-#pragma unroll
-        for (int j = i + 1; j < N; ++j) s += A[j * N + i] * x[j];
-        x[i] -= s;
-    }
-#pragma unroll
-    for (int k = N - 1; k >= 0; --k)
-#pragma unroll
-        for (int bi = k + 1; bi < N; ++bi)
-            if (tr[k] == bi) { const double t = x[k]; x[k] = x[bi]; x[bi] = t; }
+        for (int j = i + 1; j < N; ++j) u[j - i - 1] = L[j][i] * x[j];
+        x[i] = y[i] - tsum<N - 1 - i>(u);
+    });
 }
 
 // upper-triangle index of the 6x6 pose Hessian
@@ -226,22 +287,37 @@ __device__ void se3_left_update(const double* dx, double* T) {
     const double eps = 1e-10;  // Sophus::Constants<double>::epsilon()
     const double wx = dx[3], wy = dx[4], wz = dx[5];
     const double theta_sq = wx * wx + wy * wy + wz * wz;
-    double theta, imag, real, sh = 0.0, ch = 1.0;
-    if (theta_sq < eps * eps) {
-        theta = 0.0;
-        const double t4 = theta_sq * theta_sq;
-        imag = 0.5 - (1.0 / 48.0) * theta_sq + (1.0 / 3840.0) * t4;
-        real = 1.0 - (1.0 / 8.0) * theta_sq + (1.0 / 384.0) * t4;
+    double imag, real, c1 = 0.0, c2 = 0.0;
+    const double t = theta_sq;
+    const bool tiny = t < eps * eps;  // Sophus: theta < epsilon -> first-order V = R
+    if (tiny) {
+        const double t4 = t * t;
+        imag = 0.5 - (1.0 / 48.0) * t + (1.0 / 3840.0) * t4;
+        real = 1.0 - (1.0 / 8.0) * t + (1.0 / 384.0) * t4;
+    } else if (t < 1e-2) {
+        // theta < 0.1 (every Gauss-Newton step of a converging window): Taylor series in
+        // theta^2 (truncation < 1e-22 relative) of sin(theta/2)/theta, cos(theta/2),
+        // (1 - cos theta)/theta^2 and (theta - sin theta)/theta^3 — no sqrt / sincos / division
+        imag = 0.5 + t * (-1.0 / 48 + t * (1.0 / 3840 + t * (-1.0 / 645120 + t * (1.0 / 185794560 + t * (-1.0 / 81749606400.0)))));
+        real = 1.0 + t * (-1.0 / 8 + t * (1.0 / 384 + t * (-1.0 / 46080 + t * (1.0 / 10321920 + t * (-1.0 / 3715891200.0)))));
+        c1 = 0.5 + t * (-1.0 / 24 + t * (1.0 / 720 + t * (-1.0 / 40320 + t * (1.0 / 3628800 + t * (-1.0 / 479001600.0)))));
+        c2 = 1.0 / 6 + t * (-1.0 / 120 + t * (1.0 / 5040 + t * (-1.0 / 362880 + t * (1.0 / 39916800 + t * (-1.0 / 6227020800.0)))));
     } else {
-        theta = sqrt(theta_sq);
+        const double theta = sqrt(t);
+        double sh, ch;
         sincos(0.5 * theta, &sh, &ch);
-        imag = sh * frcp(theta);
+        const double it = frcp(theta);
+        imag = sh * it;
         real = ch;
+        // 1 - cos theta = 2 sin^2(theta/2), sin theta = 2 sin(theta/2) cos(theta/2)
+        const double rsq = it * it;
+        c1 = (2.0 * sh * sh) * rsq;
+        c2 = (theta - 2.0 * sh * ch) * (rsq * it);
     }
     const double eq[4] = {imag * wx, imag * wy, imag * wz, real};
     const double O[9] = {0, -wz, wy, wz, 0, -wx, -wy, wx, 0};
     double V[9];
-    if (theta < eps) {
+    if (tiny) {
         rot_from_quat(eq, V);
     } else {
         double O2[9];
@@ -250,10 +326,6 @@ __device__ void se3_left_update(const double* dx, double* T) {
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 O2[3 * r + c] = O[3 * r] * O[c] + O[3 * r + 1] * O[3 + c] + O[3 * r + 2] * O[6 + c];
-        // 1 - cos(theta) = 2 sin^2(theta/2), sin(theta) = 2 sin(theta/2) cos(theta/2)
-        const double rsq = frcp(theta_sq);
-        const double c1 = (2.0 * sh * sh) * rsq;
-        const double c2 = (theta - 2.0 * sh * ch) * (rsq * frcp(theta));
 #pragma unroll
         for (int i = 0; i < 9; ++i) V[i] = ((i % 4 == 0) ? 1.0 : 0.0) + c1 * O[i] + c2 * O2[i];
     }
@@ -264,20 +336,19 @@ __device__ void se3_left_update(const double* dx, double* T) {
     const double bx = T[0], by = T[1], bz = T[2], bw = T[3];
     const double q[4] = {aw * bx + ax * bw + ay * bz - az * by, aw * by + ay * bw + az * bx - ax * bz,
                          aw * bz + az * bw + ax * by - ay * bx, aw * bw - ax * bx - ay * by - az * bz};
-    const double n = sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+    const double rn = frsq((q[0] * q[0] + q[1] * q[1]) + (q[2] * q[2] + q[3] * q[3]));
     // t <- et + rotate(eq, t)
     const double rt[8] = {eq[0], eq[1], eq[2], eq[3], 0, 0, 0, 0};
     const D3 r = se3_apply(rt, {T[4], T[5], T[6]});
-    const double rn = frcp(n);
     T[0] = q[0] * rn; T[1] = q[1] * rn; T[2] = q[2] * rn; T[3] = q[3] * rn;
     T[4] = et[0] + r.x; T[5] = et[1] + r.y; T[6] = et[2] + r.z;
 }
 
 // Pose step of one keyframe from its summed terms S (local_ba.cpp:163-173): skipped below
 // min_pose_observations or without a camera; T updated in place, R = its rotation (:173, :220).
-__device__ __forceinline__ void solve_pose(const BAArgs& a, int k, const double* S, double* T, double* R) {
+__device__ __forceinline__ void solve_pose(const BAArgs& a, int flags, const double* S, double* T, double* R) {
     const int obs = (int)S[28];
-    if (obs >= a.min_pose_obs && (a.kf_flags[k] & 1)) {
+    if (obs >= a.min_pose_obs && (flags & 1)) {
         double H[36], b[6], dx[6];
 #pragma unroll
         for (int r = 0; r < 6; ++r)
@@ -288,7 +359,7 @@ __device__ __forceinline__ void solve_pose(const BAArgs& a, int k, const double*
             H[7 * r] += 1e-6;
             b[r] = S[21 + r];
         }
-        ldlt_solve<6>(H, b, dx);
+        ldlt_spd_solve<6>(H, b, dx);
         bool fin = true;
 #pragma unroll
         for (int r = 0; r < 6; ++r) fin = fin && isfinite(dx[r]);
@@ -364,6 +435,16 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     const int p0 = a.kf_obs_ptr[k], p1 = a.kf_obs_ptr[k + 1];
     const int len = (p1 - p0 + a.n_split - 1) / a.n_split;
     const int i0 = p0 + slice * len, i1 = min(p1, i0 + len);
+    // the thread's first observation and its landmark are requested before the pose, so the
+    // dependent gather overlaps the pose / intrinsics loads
+    const int ifirst = i0 + (int)threadIdx.x;
+    D3 P0{0, 0, 0};
+    double2 uv0 = make_double2(0.0, 0.0);
+    if (ifirst < i1) {
+        uv0 = a.pobs_uv[ifirst];
+        const double* P = lm_in(a, it, a.pobs_lm[ifirst]);
+        P0 = {P[0], P[1], P[2]};
+    }
     const double* Tin = pose_in(a, it);
     double T[8], C[4];
 #pragma unroll
@@ -375,20 +456,25 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     double v[kNTerms];
 #pragma unroll
     for (int t = 0; t < kNTerms; ++t) v[t] = 0.0;
-#pragma unroll 2
-    for (int i = i0 + (int)threadIdx.x; i < i1; i += kPoseBlock) {
-        const int s = a.pobs_lm[i];
-        const double2 uv = a.pobs_uv[i];
-        const double* P = lm_in(a, it, s);
-        const D3 pc = se3_apply(T, {P[0], P[1], P[2]});
+    for (int i = ifirst; i < i1; i += kPoseBlock) {
+        D3 Pw = P0;
+        double2 uv = uv0;
+        if (i != ifirst) {
+            uv = a.pobs_uv[i];
+            const double* P = lm_in(a, it, a.pobs_lm[i]);
+            Pw = {P[0], P[1], P[2]};
+        }
+        const D3 pc = se3_apply(T, Pw);
         if (!(pc.z > 1e-6)) continue;
         const double inv_z = frcp(pc.z);
         const double x = pc.x * inv_z, y = pc.y * inv_z;
         const double e0 = uv.x - (fx * x + C[2]);
         const double e1 = uv.y - (fy * y + C[3]);
-        const double en = sqrt(e0 * e0 + e1 * e1);
+        const double e2 = e0 * e0 + e1 * e1;
+        const double re = e2 > 0.0 ? frsq(e2) : 0.0;
+        const double en = e2 * re;  // |e| without a sqrt + division on the chain
         if (en > a.max_err) continue;
-        const double w = en <= a.huber ? 1.0 : a.huber * frcp(en);
+        const double w = en <= a.huber ? 1.0 : a.huber * re;
         // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
         // written out without its structural zeros (J0[1] = J1[0] = 0)
         const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
@@ -412,25 +498,12 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
         v[28] += 1.0;
     }
     VX_KT(2);
-    // Halving butterfly over the wave: at the stage with mask m each lane keeps half of its
-    // current terms (the half chosen by lane bit m) and adds its partner's copy of that half, so
-    // the 32 (29 used) terms cost 16 + 8 + 4 + 2 + 1 + 1 shuffles instead of 29 x 6.  Afterwards
-    // lanes 2t and 2t + 1 hold term t summed over the wave (fixed order: deterministic).
+    // wave reduction of the 29 terms (halving butterfly, wave_sum32)
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double r[kStride];
 #pragma unroll
     for (int t = 0; t < kStride; ++t) r[t] = t < kNTerms ? v[t] : 0.0;
-#pragma unroll
-    for (int m = 32, c = kStride; m >= 2; m >>= 1, c >>= 1) {
-        const bool up = (lane & m) != 0;
-#pragma unroll
-        for (int i = 0; i < c / 2; ++i) {
-            const double send = up ? r[i] : r[i + c / 2];
-            const double keep = up ? r[i + c / 2] : r[i];
-            r[i] = keep + __shfl_xor(send, m, 64);
-        }
-    }
-    const double tot = r[0] + __shfl_xor(r[0], 1, 64);
+    const double tot = wave_sum32(r);
     VX_KT(3);
     if ((lane & 1) == 0 && (lane >> 1) < kNTerms) red[wv][lane >> 1] = tot;
     __syncthreads();
@@ -474,9 +547,11 @@ __device__ __forceinline__ bool obs_terms(const BAArgs& a, D3 P, int k, double2 
     const double fx = C[0], fy = C[1];
     const double e0 = uv.x - (fx * x + C[2]);
     const double e1 = uv.y - (fy * y + C[3]);
-    const double en = sqrt(e0 * e0 + e1 * e1);
+    const double e2 = e0 * e0 + e1 * e1;
+    const double re = e2 > 0.0 ? frsq(e2) : 0.0;
+    const double en = e2 * re;
     const bool ok = front && !(en > a.max_err);
-    const double w = en <= a.huber ? 1.0 : a.huber * frcp(en);
+    const double w = en <= a.huber ? 1.0 : a.huber * re;
     const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
     const double* R = R0 + (long long)rst * k;
     // J = Jp * R with Jp's structural zeros dropped (local_ba.cpp:219-221)
@@ -506,7 +581,7 @@ __device__ __forceinline__ void lm_update(const BAArgs& a, int l, D3 P, const do
         double H[9] = {h[0] + 1e-6, h[1], h[2], h[1], h[3] + 1e-6, h[4], h[2], h[4], h[5] + 1e-6};
         const double b[3] = {h[6], h[7], h[8]};
         double dp[3];
-        ldlt_solve<3>(H, b, dp);
+        ldlt_spd_solve<3>(H, b, dp);
         if (isfinite(dp[0]) && isfinite(dp[1]) && isfinite(dp[2])) out = {P.x + dp[0], P.y + dp[1], P.z + dp[2]};
     }
     double* Pp = a.lm_pos + 4 * l;
@@ -521,12 +596,12 @@ __device__ __forceinline__ void lm_update(const BAArgs& a, int l, D3 P, const do
 // leaves its 9 terms in LDS; the thread owning landmark l0 + t then sums its observations' terms
 // in CSR order (the order of the per-landmark loop, local_ba.cpp:186) and solves the 3x3.
 // Every load of the landmark stage is issued first, so it lands during the combine and solve.
-// LDS: one 32-double slot per keyframe (combined normal equations S, then T 8 | R 9 | C 4) and
+// LDS: one kLdsStride-double slot per keyframe (combined normal equations S, then T 8 | R 9 | C 4) and
 // 9 x kLmBlock observation terms.
 __global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
     if (it > 0 && !a.state->active[it]) return;
     extern __shared__ __attribute__((aligned(16))) double kf_lds[];
-    double* terms = kf_lds + (long long)a.n_kf * kStride;  // [9][kLmBlock]
+    double* terms = kf_lds + (long long)a.n_kf * kLdsStride;  // [9][kLmBlock]
     const int tid = threadIdx.x;
     VX_KT(8);
     const int l0 = a.lm_blk[blockIdx.x], l1 = a.lm_blk[blockIdx.x + 1];
@@ -545,6 +620,18 @@ __global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
     const int r0 = own ? a.lobs_ptr[l] - ob0 : 0, r1 = own ? a.lobs_ptr[l + 1] - ob0 : 0;
     const double* Pl = lm_in(a, it, own ? l : l0);
     const D3 PL{Pl[0], Pl[1], Pl[2]};
+    // ... and the keyframe it solves (pose of the previous iteration, intrinsics, flags): their
+    // load latency also passes during the combine instead of after it
+    double kT[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kC[4] = {0, 0, 0, 0};
+    int kflg = 0;
+    if (tid < a.n_kf) {
+        const double* Tin = pose_in(a, it);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) kT[j] = Tin[8 * tid + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kC[j] = a.kf_intr[4 * tid + j];
+        kflg = a.kf_flags[tid];
+    }
     VX_KT(9);
     // slice partials -> S: kCombine (keyframe, term) pairs per thread and pass, all their slice
     // loads issued together
@@ -568,29 +655,29 @@ __global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
                 double s = v[q][0];
 #pragma unroll
                 for (int c = 1; c < kMaxSplit; ++c) s += v[q][c];
-                kf_lds[k * kStride + t] = s;
+                kf_lds[k * kLdsStride + t] = s;
             }
         }
     }
     __syncthreads();
     VX_KT(10);
-    const double* Tin = pose_in(a, it);
     double* Tout = pose_out(a, it);
-    for (int k = tid; k < a.n_kf; k += blockDim.x) {
-        double* slot = kf_lds + k * kStride;
+    if (tid < a.n_kf) {  // kLmBlock >= kMaxKfLds: one keyframe per thread at most
+        const int k = tid;
+        double* slot = kf_lds + k * kLdsStride;
         double S[kNTerms];
 #pragma unroll
         for (int t = 0; t < kNTerms; ++t) S[t] = slot[t];
         double T[8], R[9];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
-        solve_pose(a, k, S, T, R);
+        for (int j = 0; j < 8; ++j) T[j] = kT[j];
+        solve_pose(a, kflg, S, T, R);
 #pragma unroll
         for (int j = 0; j < 8; ++j) slot[j] = T[j];
 #pragma unroll
         for (int j = 0; j < 9; ++j) slot[8 + j] = R[j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) slot[17 + j] = a.kf_intr[4 * k + j];
+        for (int j = 0; j < 4; ++j) slot[17 + j] = kC[j];
         if (blockIdx.x == 0) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) Tout[8 * k + j] = T[j];
@@ -605,7 +692,8 @@ __global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
     if (blockIdx.x == 0 && tid < 64) totals_and_stop(a, it, tid);
     {
         double h[9];
-        const bool ok = obs_terms(a, PO, ok_kf, ouv, kf_lds, kStride, kf_lds + 8, kStride, kf_lds + 17, kStride, h);
+        const bool ok = obs_terms(a, PO, ok_kf, ouv, kf_lds, kLdsStride, kf_lds + 8, kLdsStride, kf_lds + 17,
+                                  kLdsStride, h);
 #pragma unroll
         for (int j = 0; j < 9; ++j) terms[j * kLmBlock + tid] = h[j];
         reinterpret_cast<int*>(terms + 9 * kLmBlock)[tid] = (has_o && ok) ? 1 : 0;  // counted observation
@@ -639,7 +727,7 @@ __global__ __launch_bounds__(256) void k_pose_solve_g(BAArgs a, int it) {
     double T[8], R[9];
 #pragma unroll
     for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
-    solve_pose(a, k, S, T, R);
+    solve_pose(a, a.kf_flags[k], S, T, R);
 #pragma unroll
     for (int j = 0; j < 8; ++j) Tout[8 * k + j] = T[j];
 #pragma unroll
@@ -931,7 +1019,7 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
         VX_LAUNCH_CHECK(c, "k_ba_reset");
     }
     const bool lds_poses = p->n_kf <= kMaxKfLds;
-    const size_t lds = (size_t)p->n_kf * kStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
+    const size_t lds = (size_t)p->n_kf * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
     if (lds_poses && lds > 64 * 1024) {  // up to ~103 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -939,11 +1027,7 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
     }
     const int lm_blocks = std::max(1, (p->n_opt + 255) / 256);
     for (int it = 0; it < p->opt.max_iterations; ++it) {
-        {
-            ProfScope ps(c, kStBaPose);
-            hipLaunchKernelGGL(k_pose_kf, dim3(p->n_kf * p->n_split), dim3(kPoseBlock), 0, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_pose_kf");
-        }
+        VX_HIP(c, launch(c, kStBaPose, k_pose_kf, dim3(p->n_kf * p->n_split), dim3(kPoseBlock), 0, c->stream, a, it));
 #ifndef VX_NO_RCCL
         if (sharded) {
             ProfScope ps(c, kStBaAllreduce);
@@ -952,11 +1036,11 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
             if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
         }
 #endif
-        ProfScope ps(c, kStBaLandmark);
         if (lds_poses) {
-            hipLaunchKernelGGL(k_landmark_solve, dim3(p->n_lm_blocks), dim3(kLmBlock), lds, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_landmark_solve");
+            VX_HIP(c, launch(c, kStBaLandmark, k_landmark_solve, dim3(p->n_lm_blocks), dim3(kLmBlock), (uint32_t)lds,
+                             c->stream, a, it));
         } else {
+            ProfScope ps(c, kStBaLandmark);
             hipLaunchKernelGGL(k_pose_solve_g, dim3((p->n_kf + 255) / 256), dim3(256), 0, c->stream, a, it);
             VX_LAUNCH_CHECK(c, "k_pose_solve_g");
             hipLaunchKernelGGL(k_landmark, dim3(lm_blocks), dim3(256), 0, c->stream, a, it);

@@ -141,12 +141,8 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
     VX_HIP(c, c->matches.ensure((size_t)std::max(q_cap, 1) * sizeof(vx_match)));
     VX_HIP(c, c->match_count.ensure(16));
     c->match_cap = q_cap;
-    {
-        ProfScope ps(c, kStMatchPartial);
-        hipLaunchKernelGGL(k_knn_partial, dim3((q_cap + kQB - 1) / kQB, n_chunks), dim3(kQB), 0, c->stream, dq,
-                           dnq, nq_host, dt, dnt, nt_host, n_chunks, c->partial.as<uint2>(), q_stride);
-        VX_LAUNCH_CHECK(c, "k_knn_partial");
-    }
+    VX_HIP(c, launch(c, kStMatchPartial, k_knn_partial, dim3((q_cap + kQB - 1) / kQB, n_chunks), dim3(kQB), 0,
+                     c->stream, dq, dnq, nq_host, dt, dnt, nt_host, n_chunks, c->partial.as<uint2>(), q_stride));
     {
         ProfScope ps(c, kStMatchMerge);
         unsigned* best = reinterpret_cast<unsigned*>(c->partial.as<uint2>() + (size_t)n_chunks * q_stride);

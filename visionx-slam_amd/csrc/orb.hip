@@ -1100,12 +1100,10 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
     Slot& s = c->slots[slot];
     const int hist_n = g.L * 256;
     if (g.pyr_fused) {
-        ProfScope ps(c, kStPyramid);
         const int raw = (g.pr_area0 * channels + 15) & ~15;
-        hipLaunchKernelGGL(k_pyramid, dim3(g.pr_ntx, g.pr_nty), dim3(kPyBlock), raw + 2 * g.pr_buf + 4 * g.pr_tabn,
-                           c->stream, d_img, channels, (long long)stride, pyr, c->tabs.as<int4>(), a,
-                           c->hist.as<int>(), hist_n, raw);
-        VX_LAUNCH_CHECK(c, "k_pyramid");
+        VX_HIP(c, launch(c, kStPyramid, k_pyramid, dim3(g.pr_ntx, g.pr_nty), dim3(kPyBlock),
+                         (uint32_t)(raw + 2 * g.pr_buf + 4 * g.pr_tabn), c->stream, d_img, channels,
+                         (long long)stride, pyr, (const int4*)c->tabs.as<int4>(), a, c->hist.as<int>(), hist_n, raw));
     } else {
         {
             ProfScope ps(c, kStGray);
@@ -1129,34 +1127,21 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
         VX_HIP(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
         bs = c->side;
     }
-    {
-        ProfScope ps(c, kStBlur, bs);
-        hipLaunchKernelGGL(k_blur, dim3(blur_blocks(a)), dim3(kBlock), 0, bs, pyr, c->blur.as<uint8_t>(), a);
-        VX_LAUNCH_CHECK(c, "k_blur");
-    }
+    VX_HIP(c, launch(c, kStBlur, k_blur, dim3(blur_blocks(a)), dim3(kBlock), 0, bs, (const uint8_t*)pyr,
+                     c->blur.as<uint8_t>(), a));
     if (c->orb_fork) VX_HIP(c, hipEventRecord(c->join_ev, c->side));
-    {
-        ProfScope ps(c, kStFast);
-        hipLaunchKernelGGL(k_fast, dim3(g.total_tiles), dim3(kBlock), 0, c->stream, pyr, a,
-                           c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>());
-        VX_LAUNCH_CHECK(c, "k_fast");
-    }
-    {
-        ProfScope ps(c, kStSelect);
-        hipLaunchKernelGGL(k_select, dim3(g.L), dim3(kSelBlock), 0, c->stream, c->cand.as<CandRec>(),
-                           c->band_count.as<int>(), c->hist.as<int>(), a, c->stage.as<CandRec>(),
-                           c->level_count.as<int>());
-        VX_LAUNCH_CHECK(c, "k_select");
-    }
+    VX_HIP(c, launch(c, kStFast, k_fast, dim3(g.total_tiles), dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, a,
+                     c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>()));
+    VX_HIP(c, launch(c, kStSelect, k_select, dim3(g.L), dim3(kSelBlock), 0, c->stream,
+                     (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(),
+                     (const int*)c->hist.as<int>(), a, c->stage.as<CandRec>(), c->level_count.as<int>()));
     if (c->orb_fork) VX_HIP(c, hipStreamWaitEvent(c->stream, c->join_ev, 0));
     {
-        ProfScope ps(c, kStDescribe);
         const int waves_per_block = kBlock / 64;
-        hipLaunchKernelGGL(k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block), dim3(kBlock),
-                           0, c->stream, pyr, c->blur.as<uint8_t>(), c->stage.as<CandRec>(),
-                           c->level_count.as<int>(), a, s.kp.as<vx_keypoint>(), s.desc.as<uint8_t>(),
-                           s.count.as<int>());
-        VX_LAUNCH_CHECK(c, "k_describe");
+        VX_HIP(c, launch(c, kStDescribe, k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block),
+                         dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, (const uint8_t*)c->blur.as<uint8_t>(),
+                         (const CandRec*)c->stage.as<CandRec>(), (const int*)c->level_count.as<int>(), a,
+                         s.kp.as<vx_keypoint>(), s.desc.as<uint8_t>(), s.count.as<int>()));
     }
     s.valid = true;
     return VX_OK;

@@ -48,6 +48,17 @@ ProfScope::~ProfScope() {
     c->pending.push_back({a, b, stage});
 }
 
+KTiming prof_kernel_events(vx_ctx* c, int stage) {
+    KTiming t;
+    if (!c->prof || !((c->prof_mask >> stage) & 1u)) return t;
+    t.a = get_event(c);
+    t.b = get_event(c);
+    if (!t.a || !t.b) t.a = t.b = nullptr;
+    return t;
+}
+
+void prof_kernel_done(vx_ctx* c, int stage, KTiming t) { c->pending.push_back({t.a, t.b, stage}); }
+
 void prof_collect(vx_ctx* c) {
     for (auto& pe : c->pending) {
         float ms = 0.f;

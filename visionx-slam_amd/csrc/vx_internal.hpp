@@ -2,6 +2,7 @@
 // ORB, matching and bundle-adjustment translation units of libvxslam.so.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -185,6 +186,28 @@ struct ProfScope {
     ~ProfScope();
 };
 void prof_collect(vx_ctx* c);
+
+// Per-dispatch timing for a single-kernel stage: the events handed to hipExtLaunchKernelGGL carry
+// the dispatch's own start / end timestamps (the duration rocprofv3 reports), not a bracket that
+// also spans the stream's dispatch boundaries.  Both null when the stage is not being profiled.
+struct KTiming {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+KTiming prof_kernel_events(vx_ctx* c, int stage);
+void prof_kernel_done(vx_ctx* c, int stage, KTiming t);
+
+template <class F, class... Args>
+inline hipError_t launch(vx_ctx* c, int stage, F kernel, dim3 grid, dim3 block, uint32_t shm, hipStream_t s,
+                         Args... args) {
+    const KTiming t = prof_kernel_events(c, stage);
+    if (t.a) {
+        hipExtLaunchKernelGGL(kernel, grid, block, shm, s, t.a, t.b, 0, args...);
+        prof_kernel_done(c, stage, t);
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, shm, s, args...);
+    }
+    return hipGetLastError();
+}
 
 int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h);
 

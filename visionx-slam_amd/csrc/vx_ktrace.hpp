@@ -10,12 +10,16 @@ constexpr int kKtBlocks = 64, kKtSlots = 16;
 }
 
 #ifdef VX_KTRACE
-#define VX_KT_TABLE() __device__ long long g_ktrace[vx::kKtBlocks * vx::kKtSlots]
+// table: [block][slot] wall_clock64, then [block][slot] s_memtime (shader clock cycles)
+#define VX_KT_TABLE() __device__ long long g_ktrace[2 * vx::kKtBlocks * vx::kKtSlots]
 #define VX_KT(slot)                                                                        \
     do {                                                                                   \
         __builtin_amdgcn_s_waitcnt(0);                                                     \
-        if (threadIdx.x == 0 && blockIdx.x < vx::kKtBlocks)                                \
+        if (threadIdx.x == 0 && blockIdx.x < vx::kKtBlocks) {                              \
             g_ktrace[blockIdx.x * vx::kKtSlots + (slot)] = (long long)wall_clock64();      \
+            g_ktrace[(vx::kKtBlocks + blockIdx.x) * vx::kKtSlots + (slot)] =               \
+                (long long)__builtin_amdgcn_s_memtime();                                   \
+        }                                                                                  \
     } while (0)
 #define VX_KT_EXPORT(name)                                                                 \
     extern "C" int name(long long* out) {                                                  \
