@@ -14,6 +14,6 @@ import csv, os, re
 tag = os.environ.get("TAG", "dev")
 rows = list(csv.DictReader(open(f"gpurun_out/prof_{tag}/run_kernel_stats.csv")))
 for r in rows:
-    m = re.search(r"\b(k_[a-z0-9_]+)\(", r["Name"]) 
+    m = re.search(r"\b(k_[a-z0-9_]+)(?:<[^>(]*>)?\(", r["Name"]) 
     print(f"{(m.group(1) if m else r['Name'][:30]):22s} calls {r['Calls']:>5s} avg_us {float(r['AverageNs'])/1e3:9.2f} pct {float(r['Percentage']):6.2f}")
 PY

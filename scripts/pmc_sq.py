@@ -8,14 +8,14 @@ import sys
 
 rows = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(sys.argv[1])):
-    m = re.search(r"\b(k_[a-z0-9_]+)\(", r["Kernel_Name"])
+    m = re.search(r"\b(k_[a-z0-9_]+)(?:<[^>(]*>)?\(", r["Kernel_Name"])
     if not m:
         continue
     rows[m.group(1)][r["Counter_Name"]].append(float(r["Counter_Value"]))
 dur = collections.defaultdict(list)
 if len(sys.argv) > 2:
     for r in csv.DictReader(open(sys.argv[2])):
-        m = re.search(r"\b(k_[a-z0-9_]+)\(", r["Kernel_Name"])
+        m = re.search(r"\b(k_[a-z0-9_]+)(?:<[^>(]*>)?\(", r["Kernel_Name"])
         if m:
             dur[m.group(1)].append((float(r["End_Timestamp"]) - float(r["Start_Timestamp"])) / 1e3)
 print(f"{'kernel':18s} {'waves':>7s} {'wave_us':>8s} {'wait%':>6s} {'instw%':>6s} {'active%':>7s} {'busy_us':>8s} {'clk_GHz':>7s}")

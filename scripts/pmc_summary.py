@@ -23,7 +23,7 @@ def agg(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"\b(k_[a-z0-9_]+)\(", r["Kernel_Name"])
+        m = re.search(r"\b(k_[a-z0-9_]+)(?:<[^>(]*>)?\(", r["Kernel_Name"])
         if m:
             d[m.group(1)].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in d.items()}

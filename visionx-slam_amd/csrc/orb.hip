@@ -23,6 +23,7 @@
 // Every integer stage is exact; float stages are compiled with -ffp-contract=off and follow the
 // OpenCV operation order, so results are bit-identical to the CPU restatement in oracle/.
 #include <cfloat>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 
@@ -115,11 +116,16 @@ __global__ void k_gray(const uint8_t* __restrict__ img, int W, int ch, long long
 // a halo that grows as h <- 1.2 h + 1, prepared on the host from the same coefficient tables),
 // and writes only the pixels it owns.  Each pixel is the same deterministic function of its
 // sources whichever workgroup computes it, so the result is bit-identical to the level chain.
-constexpr int kPyBlock = 1024;  // 64 x 16
-constexpr int kPyTile = 64;     // level-0 tile edge
+// Level-0 tile edge and workgroup size (template NT: 512 or 1024 threads, 64 x NT/64) trade
+// parallelism against redundant halo work.  A 1024-thread workgroup occupies a whole CU, so the
+// tile is the smallest edge (>= 32, step 4) whose grid fits the device's CUs in one round
+// (640x480 on 256 CUs: 36 -> 18 x 14 workgroups; measured 13.9 us at 40 vs 17.3 us at 64 and
+// 22.9 us at 32, which needs two rounds).  $VX_PYR_TILE / $VX_PYR_BLOCK override for sweeps.
+constexpr int kPyBlockDef = 1024;
 constexpr int kPyLdsMax = 64 * 1024;
 
-__global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict__ img, int ch,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_pyramid(const uint8_t* __restrict__ img, int ch,
                                                       long long stride, uint8_t* __restrict__ pyr,
                                                       const int4* __restrict__ tabs, LevelArgs a,
                                                       int* __restrict__ hist, int hist_n, int raw_bytes) {
@@ -134,7 +140,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
     const int L = a.L;
     VX_KT(0);
     if (blockIdx.x == 0 && blockIdx.y == 0)
-        for (int i = tid; i < hist_n; i += kPyBlock) hist[i] = 0;
+        for (int i = tid; i < hist_n; i += NT) hist[i] = 0;
     if (tid < L) srx[tid] = tabs[a.pr_x + (long long)blockIdx.x * L + tid];
     if (tid >= 64 && tid < 64 + L) sry[tid - 64] = tabs[a.pr_y + (long long)blockIdx.y * L + tid - 64];
     __syncthreads();
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
     }
     __syncthreads();
     // coefficient tables of this tile's need ranges, every level, all loads in flight at once
-    stage_lds<kPyBlock, 2>(stab, sox[L], [&](int i) {
+    stage_lds<NT, 2048 / NT>(stab, sox[L], [&](int i) {
         const bool isy = i >= soy[1];
         int l = 1;
         if (!isy) { while (l + 1 < L && i >= sox[l + 1]) ++l; }
@@ -156,41 +162,71 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
         const int4 e = tabs[(isy ? a.ytab[l] : a.xtab[l]) + idx];
         return e.x | (e.z << 16);
     });
-    // level 0: stage the BGR(A) bytes of the need rectangle (row-chunked, all loads in flight)
+    // level 0: stage the BGR(A) bytes of the need rectangle as 4-byte-aligned dwords (a byte
+    // load per pixel channel would saturate the vector-memory pipe long before HBM), each LDS row
+    // starting at the dword containing the row's first needed byte.  Only the dword holding the
+    // image's very last byte may extend past the allocation: it is read bytewise.
     int4 rx = srx[0], ry = sry[0];
     int px0 = rx.x, py0 = ry.x, pw = rx.y - rx.x, ph = ry.y - ry.x;
+    const int rb = pw * ch;
+    const int rowdw = (rb + 6) >> 2;  // dwords per LDS row, any start alignment
     {
-        const int rb = pw * ch;
-        const uint8_t* src = img + (long long)py0 * stride + (long long)px0 * ch;
-        constexpr int KR = 6, KC = 6;
-        for (int r0 = 0; r0 < ph; r0 += 16 * KR)
-            for (int c0 = 0; c0 < rb; c0 += 64 * KC) {
-                uint8_t v[KR][KC];
+        // byte offsets (from img) of the image's last byte and of this tile's first needed byte
+        const long long last = (long long)(a.lh[0] - 1) * stride + (long long)a.lw[0] * ch - 1;
+        const long long first = (long long)py0 * stride + (long long)px0 * ch;
+        const int mis0 = (int)(reinterpret_cast<uintptr_t>(img) & 3);
+        uint32_t* rawd = reinterpret_cast<uint32_t*>(raw);
+        constexpr int KR = 96 / (NT / 64), KC = 2;  // one batch covers 96 rows x 128 dwords
+        for (int r0 = 0; r0 < ph; r0 += (NT / 64) * KR)
+            for (int c0 = 0; c0 < rowdw; c0 += 64 * KC) {
+                uint32_t v[KR][KC];
+                unsigned fix = 0;  // elements whose dword would pass the image's last byte
 #pragma unroll
                 for (int i = 0; i < KR; ++i)
 #pragma unroll
                     for (int j = 0; j < KC; ++j) {
-                        const int r = r0 + ly + 16 * i, c = c0 + lx + 64 * j;
-                        v[i][j] = (r < ph && c < rb) ? src[(long long)r * stride + c] : 0;
+                        const int r = r0 + ly + (NT / 64) * i, c = c0 + lx + 64 * j;
+                        const long long ro = first + (long long)r * stride;
+                        const long long off = ro - (long long)((mis0 + ro) & 3) + 4LL * c;  // aligned
+                        const bool in = r < ph && c < rowdw;
+                        const bool safe = in && off + 3 <= last;
+                        v[i][j] = safe ? *reinterpret_cast<const uint32_t*>(img + off) : 0u;
+                        if (in && !safe) fix |= 1u << (i * KC + j);
                     }
+                if (fix) {  // at most one dword of the whole image: bytewise, outside the batch
+#pragma unroll
+                    for (int i = 0; i < KR; ++i)
+#pragma unroll
+                        for (int j = 0; j < KC; ++j)
+                            if (fix & (1u << (i * KC + j))) {
+                                const int r = r0 + ly + (NT / 64) * i, c = c0 + lx + 64 * j;
+                                const long long ro = first + (long long)r * stride;
+                                const long long off = ro - (long long)((mis0 + ro) & 3) + 4LL * c;
+                                for (int q = 0; q < 4; ++q)
+                                    if (off + q <= last) v[i][j] |= (uint32_t)img[off + q] << (8 * q);
+                            }
+                }
 #pragma unroll
                 for (int i = 0; i < KR; ++i)
 #pragma unroll
                     for (int j = 0; j < KC; ++j) {
-                        const int r = r0 + ly + 16 * i, c = c0 + lx + 64 * j;
-                        if (r < ph && c < rb) raw[r * rb + c] = v[i][j];
+                        const int r = r0 + ly + (NT / 64) * i, c = c0 + lx + 64 * j;
+                        if (r < ph && c < rowdw) rawd[r * rowdw + c] = v[i][j];
                     }
             }
     }
     __syncthreads();
     VX_KT(1);
-    for (int yy = ly; yy < ph; yy += 16) {
+    constexpr int RS = NT / 64;  // rows per pass
+    for (int yy = ly; yy < ph; yy += RS) {
         const int y = py0 + yy;
         const bool oy = y >= ry.z && y < ry.w;
         uint8_t* drow = pyr + (long long)y * a.lw[0];
+        const int ra = (int)((reinterpret_cast<uintptr_t>(img) + (uintptr_t)((long long)y * stride + (long long)px0 * ch)) & 3);
+        const uint8_t* rrow = raw + yy * rowdw * 4 + ra;
         for (int xx = lx; xx < pw; xx += 64) {
             const int x = px0 + xx;
-            const uint8_t g = gray_px(raw + (yy * pw + xx) * ch, ch);
+            const uint8_t g = gray_px(rrow + xx * ch, ch);
             cur[yy * pw + xx] = g;
             if (oy && x >= rx.z && x < rx.w) drow[x] = g;
         }
@@ -208,7 +244,7 @@ __global__ __launch_bounds__(kPyBlock) void k_pyramid(const uint8_t* __restrict_
         const int* yt = stab + soy[l] - ry.x;
         const int nw = rx.y - rx.x, nh = ry.y - ry.x;
         uint8_t* dst = pyr + a.off[l];
-        for (int yy = ly; yy < nh; yy += 16) {
+        for (int yy = ly; yy < nh; yy += RS) {
             const int y = ry.x + yy;
             const int ey = yt[y];
             const int4 cy = make_int4(ey & 0xffff, 256 - (ey >> 16), ey >> 16, 0);
@@ -818,14 +854,14 @@ void linear_table(int src, int dst, std::vector<int4>& t) {
 // is [b(t), b(t+1)) with b(t) = min(n_l, t * kPyTile * n_l / n_0) (a partition of every level);
 // the needed range of level l-1 is the owned range plus every source index (ofs, min(ofs+1,
 // n-1)) of the needed range of level l, taken from the same coefficient tables k_resize uses.
-static void pyramid_axis(const std::vector<int>& n, const std::vector<const int4*>& tab, int tiles,
+static void pyramid_axis(const std::vector<int>& n, const std::vector<const int4*>& tab, int tiles, int tile,
                          std::vector<int4>& out) {
     const int L = (int)n.size();
     for (int t = 0; t < tiles; ++t) {
         std::vector<int4> r(L);
         for (int l = 0; l < L; ++l) {
-            const int64_t lo = std::min<int64_t>(n[l], (int64_t)t * kPyTile * n[l] / n[0]);
-            const int64_t hi = std::min<int64_t>(n[l], (int64_t)(t + 1) * kPyTile * n[l] / n[0]);
+            const int64_t lo = std::min<int64_t>(n[l], (int64_t)t * tile * n[l] / n[0]);
+            const int64_t hi = std::min<int64_t>(n[l], (int64_t)(t + 1) * tile * n[l] / n[0]);
             r[l] = make_int4(0, 0, (int)lo, (int)hi);
         }
         r[L - 1].x = r[L - 1].z;
@@ -846,9 +882,14 @@ static void pyramid_axis(const std::vector<int>& n, const std::vector<const int4
     }
 }
 
+// LDS bytes of k_pyramid's raw level-0 staging: h0 rows of ((w0 * ch + 6) / 4) dwords.
+static int64_t pyr_raw_bytes(const OrbGeometry& g, int ch) {
+    return (int64_t)g.pr_h0 * (((int64_t)g.pr_w0 * ch + 6) >> 2) * 4;
+}
+
 // Prepares k_pyramid's tables (appended to the coefficient table vector `all`, which already holds
 // the per-level resize tables) and decides whether the largest need rectangle fits in LDS.
-static void pyramid_rects(OrbGeometry& g, std::vector<int4>& all) {
+static void pyramid_rects(OrbGeometry& g, std::vector<int4>& all, int n_cu) {
     g.pyr_fused = false;
     if (g.L < 2) return;
     std::vector<int> nw(g.L), nh(g.L);
@@ -861,11 +902,23 @@ static void pyramid_rects(OrbGeometry& g, std::vector<int4>& all) {
             ty[l] = all.data() + g.ytab[l];
         }
     }
-    g.pr_ntx = (g.W + kPyTile - 1) / kPyTile;
-    g.pr_nty = (g.H + kPyTile - 1) / kPyTile;
+    g.pr_tile = 64;
+    if (const char* e = std::getenv("VX_PYR_TILE")) {
+        g.pr_tile = std::max(16, std::min(256, std::atoi(e)));
+    } else {
+        for (int t = 32; t <= 256; t += 4)
+            if ((int64_t)((g.W + t - 1) / t) * ((g.H + t - 1) / t) <= n_cu) {
+                g.pr_tile = t;
+                break;
+            }
+    }
+    g.pr_block = kPyBlockDef;
+    if (const char* e = std::getenv("VX_PYR_BLOCK")) g.pr_block = std::atoi(e) == 512 ? 512 : 1024;
+    g.pr_ntx = (g.W + g.pr_tile - 1) / g.pr_tile;
+    g.pr_nty = (g.H + g.pr_tile - 1) / g.pr_tile;
     std::vector<int4> rx, ry;
-    pyramid_axis(nw, tx, g.pr_ntx, rx);
-    pyramid_axis(nh, ty, g.pr_nty, ry);
+    pyramid_axis(nw, tx, g.pr_ntx, g.pr_tile, rx);
+    pyramid_axis(nh, ty, g.pr_nty, g.pr_tile, ry);
     int64_t buf = 0;
     for (int l = 0; l < g.L; ++l) {
         int mw = 0, mh = 0;
@@ -889,8 +942,13 @@ static void pyramid_rects(OrbGeometry& g, std::vector<int4>& all) {
     for (int tx = 0; tx < g.pr_ntx; ++tx)
         for (int ty = 0; ty < g.pr_nty; ++ty)
             area0 = std::max<int64_t>(area0, (int64_t)(rx[tx * g.L].y - rx[tx * g.L].x) * (ry[ty * g.L].y - ry[ty * g.L].x));
-    // worst case 4 channels for the raw level-0 staging
-    if (((area0 * 4 + 15) & ~int64_t(15)) + 2 * buf + 4 * tabn > kPyLdsMax) return;  // level chain instead
+    int64_t w0 = 0, h0 = 0;
+    for (int tx = 0; tx < g.pr_ntx; ++tx) w0 = std::max<int64_t>(w0, rx[tx * g.L].y - rx[tx * g.L].x);
+    for (int ty = 0; ty < g.pr_nty; ++ty) h0 = std::max<int64_t>(h0, ry[ty * g.L].y - ry[ty * g.L].x);
+    g.pr_w0 = (int)w0;
+    g.pr_h0 = (int)h0;
+    // worst case 4 channels for the raw level-0 staging (dword rows, see k_pyramid)
+    if (pyr_raw_bytes(g, 4) + 2 * buf + 4 * tabn > kPyLdsMax) return;  // level chain instead
     g.pr_buf = (int)buf;
     g.pr_area0 = (int)area0;
     g.pr_tabn = (int)tabn;
@@ -1048,7 +1106,9 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
         g.ytab[l] = (int64_t)all.size();
         all.insert(all.end(), t.begin(), t.end());
     }
-    pyramid_rects(g, all);
+    int n_cu = 256;
+    (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+    pyramid_rects(g, all, std::max(1, n_cu));
     g.tab_entries = (int64_t)all.size();
     // FAST tiles / cells and selection staging
     int tiles = 0;
@@ -1100,8 +1160,9 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
     Slot& s = c->slots[slot];
     const int hist_n = g.L * 256;
     if (g.pyr_fused) {
-        const int raw = (g.pr_area0 * channels + 15) & ~15;
-        VX_HIP(c, launch(c, kStPyramid, k_pyramid, dim3(g.pr_ntx, g.pr_nty), dim3(kPyBlock),
+        const int raw = (int)((pyr_raw_bytes(g, channels) + 15) & ~int64_t(15));
+        VX_HIP(c, launch(c, kStPyramid, g.pr_block == 512 ? k_pyramid<512> : k_pyramid<1024>,
+                         dim3(g.pr_ntx, g.pr_nty), dim3(g.pr_block),
                          (uint32_t)(raw + 2 * g.pr_buf + 4 * g.pr_tabn), c->stream, d_img, channels,
                          (long long)stride, pyr, (const int4*)c->tabs.as<int4>(), a, c->hist.as<int>(), hist_n, raw));
     } else {

@@ -96,9 +96,11 @@ struct OrbGeometry {
     // {need_lo, need_hi, own_lo, own_hi} at tabs[pr_x] / tabs[pr_y], LDS bytes per ping-pong buffer
     bool pyr_fused = false;
     int pr_ntx = 0, pr_nty = 0;
+    int pr_tile = 64, pr_block = 1024;
     int64_t pr_x = 0, pr_y = 0;
     int pr_buf = 0;
     int pr_area0 = 0;               // max level-0 need area (pixels)
+    int pr_w0 = 0, pr_h0 = 0;       // max level-0 need width / height
     int pr_tabn = 0;                // max packed coefficient entries per tile
     // FAST tiles (64 x 16 pixels per workgroup) and output cells (row x tile column)
     int ntx[kMaxLevels], nty[kMaxLevels];

@@ -15,9 +15,10 @@ constexpr int kKtBlocks = 64, kKtSlots = 16;
 #define VX_KT(slot)                                                                        \
     do {                                                                                   \
         __builtin_amdgcn_s_waitcnt(0);                                                     \
-        if (threadIdx.x == 0 && blockIdx.x < vx::kKtBlocks) {                              \
-            g_ktrace[blockIdx.x * vx::kKtSlots + (slot)] = (long long)wall_clock64();      \
-            g_ktrace[(vx::kKtBlocks + blockIdx.x) * vx::kKtSlots + (slot)] =               \
+        const unsigned kt_b = blockIdx.x + blockIdx.y * gridDim.x; /* linear workgroup */  \
+        if (threadIdx.x == 0 && kt_b < (unsigned)vx::kKtBlocks) {                          \
+            g_ktrace[kt_b * vx::kKtSlots + (slot)] = (long long)wall_clock64();            \
+            g_ktrace[(vx::kKtBlocks + kt_b) * vx::kKtSlots + (slot)] =                     \
                 (long long)__builtin_amdgcn_s_memtime();                                   \
         }                                                                                  \
     } while (0)
