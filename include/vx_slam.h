@@ -201,6 +201,55 @@ int vx_ba_plan_inspect(const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
 /* Landmark -> shard assignment used by sharded plans (splitmix64(id) mod shard_count). */
 uint32_t vx_ba_shard_of(uint64_t lm_id, int shard_count);
 
+/* ---------------------------------------------------------------- Schur-complement joint BA
+ * NOT a reference entry point: the reference's LocalBA alternates per-keyframe and per-landmark
+ * steps (local_ba.cpp:116-238).  BASELINE.json's north_star (and configs C5) ask for the
+ * Schur-complement reduction of the landmark blocks into the dense 6N x 6N pose system and a
+ * dense pose solve; this is that solver, on the same window / landmark set / observations /
+ * residual / Jacobians / Huber weight / gates as LocalBA (local_ba.cpp:15-108, projection.h:11-31),
+ * as one damped Gauss-Newton (Levenberg-Marquardt) system with b = +J^T W e, the oldest
+ * `fixed_keyframes` window keyframes held fixed.  Same map snapshot and plan life cycle as
+ * vx_ba_plan_*; shard_count > 1 shards landmarks and all-reduces the reduced system over RCCL.
+ * Parity is against its CPU restatement (oracle/sba_oracle.cpp), see DESIGN.md §10. */
+typedef struct {
+    int32_t window_size;             /* keyframes in the window (SelectKeyFrames) */
+    int32_t max_iterations;          /* assemblies: initial + accepted + rejected steps, <= 64 */
+    int32_t min_point_observations;  /* landmark filter (local_ba.cpp:100-102) */
+    int32_t fixed_keyframes;         /* oldest window keyframes held fixed (gauge, 2: also the scale) */
+    double huber_delta;              /* 5.0 */
+    double max_reproj_error;         /* 5.0 */
+    double lambda_init;              /* Marquardt damping H_ii += lambda * H_ii (1e-4) */
+    double rel_tol;                  /* stop after an accepted step lowering the cost by < rel_tol */
+} vx_sba_options;
+
+typedef struct {
+    int32_t iterations;          /* assemblies executed */
+    int32_t accepted;            /* accepted steps */
+    int32_t n_window_kf, n_landmarks;
+    double cost[16];             /* Huber cost at each assembly */
+    int32_t obs[16];             /* valid observations at each assembly */
+    int32_t step[16];            /* 2 initial, 1 accepted, 0 rejected, 3 re-assembled after a reject */
+    double lambda;               /* damping after the last iteration */
+    double initial_cost, final_cost;
+    int32_t status;              /* 0 optimised, 1 early return (no KF pair / no landmark) */
+} vx_sba_stats;
+
+typedef struct vx_sba_plan vx_sba_plan;
+void vx_sba_default_options(vx_sba_options* o);
+int vx_sba_plan_create(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
+                       const vx_sba_options* opt, int shard_rank, int shard_count, vx_sba_plan** out);
+int vx_sba_plan_run_async(vx_ctx* ctx, vx_sba_plan* plan);
+int vx_sba_plan_fetch(vx_ctx* ctx, vx_sba_plan* plan, vx_map_view* map, vx_sba_stats* stats);
+void vx_sba_plan_destroy(vx_sba_plan* plan);
+/* out8 = {n_kf, n_opt (local landmarks), n_obs, n_pairs, n_blocks, n (= 6 n_kf), nonzero 16x16
+ * tiles of the Cholesky factors (symbolic factorisation, rhs row included), n_components} */
+int vx_sba_plan_info(const vx_sba_plan* plan, int64_t* out8);
+/* The reduced system of the LAST assembly of the last run (S row-major n x n, lower triangle
+ * meaningful, damping included; rhs n), for verification against the restatement. */
+int vx_sba_plan_system(vx_ctx* ctx, vx_sba_plan* plan, double* S, double* rhs, int n);
+int vx_sba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
+                        const vx_sba_options* opt, vx_sba_stats* stats);
+
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);
 int vx_comm_init(vx_ctx* ctx, const uint8_t* id_128, int nranks, int rank);

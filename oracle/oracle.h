@@ -111,6 +111,40 @@ typedef struct {
 int orc_ba_optimize_map(orc_map_view* map, uint64_t ref_kf_id, int has_ref,
                         const orc_ba_options* opt, orc_ba_stats* stats);
 
+/* ---- Schur-complement joint BA (NOT in the reference: SURVEY.md §8f rank 4, BASELINE.json
+ * north_star "Schur-complement marginalisation ... dense pose solve").  Restates the algorithm of
+ * visionx-slam_amd/csrc/sba.hip: the LocalBA window and landmark set
+ * (local_ba.cpp:42-108), the reference's residual / Jacobians / Huber weight / gates
+ * (local_ba.cpp:15-40, projection.h:11-31), but ONE joint Levenberg-Marquardt system over all free
+ * keyframe poses and optimised landmarks with the Gauss-Newton sign (b = +J^T W e), the landmarks
+ * eliminated by the Schur complement, a dense Cholesky pose solve and back-substitution. */
+typedef struct {
+    int32_t window_size, max_iterations, min_point_observations;
+    int32_t fixed_keyframes;     /* oldest window keyframes held fixed (gauge) */
+    double huber_delta, max_reproj_error;
+    double lambda_init;          /* Marquardt damping: H_ii += lambda * H_ii (+ 1e-6) */
+    double rel_tol;              /* stop after an accepted step with relative decrease < rel_tol */
+} orc_sba_options;
+
+typedef struct {
+    int32_t iterations;          /* assemblies (accepted, rejected and initial) */
+    int32_t accepted;
+    int32_t n_window_kf, n_landmarks;
+    double cost[16];             /* robust (Huber) cost at each assembly */
+    int32_t obs[16];             /* valid observations at each assembly */
+    int32_t step[16];            /* 2 initial, 1 accepted, 0 rejected, 3 re-assembled after a reject */
+    double lambda;               /* damping after the last iteration */
+    double initial_cost, final_cost;
+    int32_t status;              /* 0 ran, 1 early return */
+} orc_sba_stats;
+
+int orc_sba_optimize_map(orc_map_view* map, uint64_t ref_kf_id, int has_ref,
+                         const orc_sba_options* opt, orc_sba_stats* stats);
+/* Reduced pose system (Schur complement S, n x n row-major, lower triangle meaningful, and rhs)
+ * assembled at the map's current state with damping `lambda`; n = 6 * window keyframes. */
+int orc_sba_system(const orc_map_view* map, uint64_t ref_kf_id, int has_ref,
+                   const orc_sba_options* opt, double lambda, double* S, double* rhs, int n);
+
 #ifdef __cplusplus
 }
 #endif

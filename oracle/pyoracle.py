@@ -210,3 +210,57 @@ def ba_optimize(m, opts=None, ref_kf_id=None):
                                    C.byref(opts), C.byref(st))
     assert rc == 0
     return st
+
+
+# ---------------------------------------------------------------------------- Schur-complement BA
+class SBAOptions(C.Structure):
+    _fields_ = [("window_size", C.c_int32), ("max_iterations", C.c_int32),
+                ("min_point_observations", C.c_int32), ("fixed_keyframes", C.c_int32),
+                ("huber_delta", C.c_double), ("max_reproj_error", C.c_double),
+                ("lambda_init", C.c_double), ("rel_tol", C.c_double)]
+
+
+class SBAStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("accepted", C.c_int32), ("n_window_kf", C.c_int32),
+                ("n_landmarks", C.c_int32), ("cost", C.c_double * 16), ("obs", C.c_int32 * 16),
+                ("step", C.c_int32 * 16), ("lambda_", C.c_double), ("initial_cost", C.c_double),
+                ("final_cost", C.c_double), ("status", C.c_int32)]
+
+
+def sba_options(window=5, iters=10, min_point=2, fixed=2, huber=5.0, max_err=5.0, lam=1e-4,
+                rel_tol=1e-6):
+    return SBAOptions(window, iters, min_point, fixed, huber, max_err, lam, rel_tol)
+
+
+def _ref(m, ref_kf_id):
+    ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+    return C.c_uint64(0 if ref is None else int(ref)), (0 if ref is None else 1)
+
+
+def sba_optimize(m, opts=None, ref_kf_id=None):
+    """Runs the oracle Schur-complement BA on a synth.BAMap in place; returns SBAStats."""
+    if opts is None:
+        opts = sba_options(window=m.get("window", 5))
+    v = map_view(m)
+    st = SBAStats()
+    ref, has_ref = _ref(m, ref_kf_id)
+    assert lib().orc_sba_optimize_map(C.byref(v), ref, has_ref, C.byref(opts), C.byref(st)) == 0
+    return st
+
+
+def sba_system(m, opts=None, lam=None, ref_kf_id=None):
+    """Reduced pose system (S, rhs) at the map's current state (None on an early return)."""
+    if opts is None:
+        opts = sba_options(window=m.get("window", 5))
+    lam = opts.lambda_init if lam is None else lam
+    v = map_view(m)
+    ref, has_ref = _ref(m, ref_kf_id)
+    nk = min(int(opts.window_size), m.n_kf)
+    n = 6 * nk
+    S = np.zeros((n, n))
+    rhs = np.zeros(n)
+    rc = lib().orc_sba_system(C.byref(v), ref, has_ref, C.byref(opts), C.c_double(lam), _p(S), _p(rhs), n)
+    if rc == 1:
+        return None
+    assert rc == 0, rc
+    return S, rhs

@@ -1,0 +1,103 @@
+"""GPU parity of the Schur-complement joint BA (vx_sba_*) against its CPU restatement
+(oracle/sba_oracle.cpp, itself pinned by tests/test_sba_cpu.py).
+
+Bars: the reduced pose system S / rhs of an assembly within 1e-9 of max|S| (FP64 summation order
+differs: tree reductions on the GPU); identical Levenberg-Marquardt decisions (iteration count,
+accept / reject codes, observation counts), costs and final poses and landmarks within the north_star
+tolerance 1e-4 * max(|cpu|, 1e-3) per component (quaternion sign canonicalised)."""
+import numpy as np
+import pytest
+
+from vxslam import synth
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-4
+
+
+def _canon(q):
+    q = q.copy()
+    q[q[:, 3] < 0] *= -1
+    return q
+
+
+def _case(ctx, oracle, m, kw, ref=None):
+    import vxslam
+
+    mc, mg = m.copy(), m.copy()
+    st_c = oracle.sba_optimize(mc, oracle.sba_options(**kw), ref_kf_id=ref)
+    st_g = ctx.sba_optimize(mg, vxslam.default_sba_options(**kw), ref_kf_id=ref)
+    assert (st_g.status, st_g.n_window_kf, st_g.n_landmarks) == (st_c.status, st_c.n_window_kf, st_c.n_landmarks)
+    assert st_g.iterations == st_c.iterations, (st_g.iterations, st_c.iterations)
+    n = min(st_c.iterations, 16)
+    assert list(st_g.step[:n]) == list(st_c.step[:n])
+    assert list(st_g.obs[:n]) == list(st_c.obs[:n])
+    assert st_g.accepted == st_c.accepted
+    for i in range(n):
+        assert abs(st_g.cost[i] - st_c.cost[i]) <= RTOL * max(abs(st_c.cost[i]), 1.0)
+    pg, pc = mg["kf_pose"].copy(), mc["kf_pose"].copy()
+    pg[:, :4], pc[:, :4] = _canon(pg[:, :4]), _canon(pc[:, :4])
+    assert (np.abs(pg - pc) / np.maximum(np.abs(pc), 1e-3)).max() <= RTOL
+    assert (np.abs(mg["lm_pos"] - mc["lm_pos"]) / np.maximum(np.abs(mc["lm_pos"]), 1e-3)).max() <= RTOL
+    return st_g, st_c
+
+
+def test_sba_reduced_system_matches_restatement(ctx, oracle):
+    import vxslam
+
+    for (nk, nl, lam) in [(5, 400, 1e-3), (12, 2500, 1e-4), (50, 20000, 1e-4)]:
+        m = synth.make_ba_map(31 + nk, nk, nl, n_old_kf=0)
+        plan = ctx.sba_plan(m, vxslam.default_sba_options(window=nk, iters=1, lam=lam))
+        plan.run_async()
+        S_g, r_g = plan.system()
+        S_c, r_c = oracle.sba_system(m, oracle.sba_options(window=nk, iters=1, lam=lam))
+        lo = np.tril_indices(6 * nk)
+        scale = np.abs(S_c[lo]).max()
+        assert np.abs(S_g[lo] - S_c[lo]).max() <= 1e-9 * scale, (nk, np.abs(S_g[lo] - S_c[lo]).max() / scale)
+        assert np.abs(r_g - r_c).max() <= 1e-9 * max(np.abs(r_c).max(), 1.0)
+        plan.close()
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
+def test_sba_baseline_configs(ctx, oracle, cfg):
+    nk, nl, ns = synth.ba_config(cfg)
+    if cfg == "C5":  # 8 streams: 8 independent covisibility components (one dense solve each)
+        nk, nl = 8 * 12, 16000
+    m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=ns * 2)
+    st_g, st_c = _case(ctx, oracle, m, dict(window=nk, iters=8))
+    assert st_g.status == 0 and st_g.accepted >= 2
+    assert st_g.final_cost < 0.2 * st_g.initial_cost
+
+
+def test_sba_variants(ctx, oracle):
+    m = synth.make_ba_map(301, 12, 2500, n_old_kf=4, rot_deg=1.0, trans_m=0.03, lm_sigma=0.05)
+    _case(ctx, oracle, m, dict(window=8))                                         # window < keyframes
+    _case(ctx, oracle, m, dict(window=8), ref=int(m["kf_id"][-3]))               # older reference KF
+    _case(ctx, oracle, m, dict(window=12, huber=1.5, max_err=4.0))               # Huber weights active
+    _case(ctx, oracle, m, dict(window=12, fixed=3))                              # 3 gauge keyframes
+    _case(ctx, oracle, m, dict(window=12, fixed=0, lam=1e-2))                    # gauge-free, damped
+    _case(ctx, oracle, m, dict(window=12, iters=20, lam=1e-6))                   # long run, many accepts
+    _case(ctx, oracle, m, dict(window=12, iters=1))                              # assembly only
+    _case(ctx, oracle, m, dict(window=12, iters=0))                              # nothing runs
+    mm = m.copy()
+    mm["kf_has_cam"][-2] = 0                                                      # keyframe without camera
+    _case(ctx, oracle, mm, dict(window=12))
+    st, _ = _case(ctx, oracle, m, dict(window=12), ref=int(m["kf_id"][0]))       # < 2 keyframes
+    assert st.status == 1
+
+
+def test_sba_plan_is_repeatable(ctx):
+    import vxslam
+
+    m = synth.make_ba_map(77, 20, 6000)
+    plan = ctx.sba_plan(m, vxslam.default_sba_options(window=20))
+    outs = []
+    for _ in range(3):
+        plan.run_async()
+        mm = m.copy()
+        plan.fetch(mm)
+        outs.append(mm)
+    for o in outs[1:]:
+        assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
+    info = plan.info()
+    assert info["n_kf"] == 20 and info["n_comp"] == 1 and info["n_pairs"] > 0

@@ -1,0 +1,1421 @@
+// sba.hip — Schur-complement joint bundle adjustment on gfx950 (vx_sba_*).
+//
+// Not a reference entry point: the reference's LocalBA (core/backend/local_ba.cpp:66-249) alternates
+// per-keyframe and per-landmark steps (ba.hip reproduces that bit-for-bit semantics).  BASELINE.json's
+// north_star asks for the Schur-complement marginalisation of the landmark blocks into the dense
+// 6N x 6N pose system with a dense (MFMA) pose solve; SURVEY.md §8f rank 4.  This solver keeps the
+// reference's window / landmark set (local_ba.cpp:42-108), observation set (:126-138), residual,
+// Jacobians, Huber weight and gates (:15-40, projection.h:11-31) and the 1e-6 regulariser, and
+// solves ONE damped Gauss-Newton system per iteration (b = +J^T W e, Marquardt damping, accept /
+// reject on the Huber cost, oldest `fixed_keyframes` held fixed).  CPU restatement:
+// oracle/sba_oracle.cpp.  Per iteration (all launches early-exit once the stop rule fired):
+//
+//   k_sba_lm     one thread per observation of an optimised landmark, whole landmarks per
+//                workgroup: residual, gates, weight, J_T (2x6) and J_p (2x3); the landmark's owner
+//                thread sums V = sum w J_p^T J_p and g_p = sum w J_p^T e in CSR order, damps and
+//                inverts V (3x3 adjugate); every thread then writes W_o = w J_T^T J_p and
+//                Y_o = W_o V^-1 (6x3 each) for the Schur products.
+//   k_sba_blocks one workgroup per nonzero 6x6 block (i, j), i >= j, of the reduced system:
+//                diagonal blocks add every observation's w J_T^T J_T, g_T, Huber cost and count,
+//                minus Y_o g_p; every block subtracts sum Y_o1 W_o2^T over the co-observation
+//                pairs the host listed for it (fixed order: deterministic).  Blocks of a
+//                connected component of the covisibility graph land in that component's dense
+//                matrix; all blocks of a sharded run are all-reduced (one ncclAllReduce).
+//   k_sba_solve  one workgroup (16 waves) per connected component: Levenberg-Marquardt decision,
+//                then a right-looking tiled Cholesky of the damped component matrix with the
+//                right-hand side as an extra tile row (forward substitution for free): per 16 x 16
+//                diagonal tile, one wave factors it and forms L_kk^-1 from registers
+//                (v_readlane broadcasts); the panel L_ik = A_ik L_kk^-T and the trailing update
+//                A_ij -= L_ik L_jk^T are v_mfma_f64_16x16x4 tiles (panel staged in LDS); then the
+//                blocked back-substitution L^T x = y.
+//   k_sba_update landmark back-substitution dp = V^-1 (g_p - sum W_o^T dx) and T <- exp(dx) T into
+//                the trial buffers.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <unordered_map>
+#include <vector>
+
+#include "vx_internal.hpp"
+#include "vx_ktrace.hpp"
+#include "ba_common.hpp"
+
+namespace vx {
+namespace {
+
+using namespace vx::ba;
+
+constexpr int kSbaMaxIter = 64;
+constexpr int kLmThreads = 256;     // k_sba_lm: max observations (and landmarks) per workgroup
+constexpr int kBlkThreads = 256;    // k_sba_blocks
+constexpr int kSolveThreads = 256;  // k_sba_solve: 4 waves, one per SIMD (512 registers each: no spills)
+constexpr int kSolveWaves = kSolveThreads / 64;
+constexpr int kUpdThreads = 256;
+constexpr int kMaxCompKf = 128;     // keyframes of one connected component (dense n <= 768)
+constexpr int kWy = 36;             // doubles per optimised observation: W (6x3) | Y (6x3)
+constexpr int kLmSys = 12;          // doubles per optimised landmark: V^-1 (6) | g_p (3) | pad
+constexpr int kBlkTerms = 50;       // 36 block + 6 rhs + 6 D + cost + count
+constexpr int kPanelStride = 256;   // doubles per LDS panel tile (operand order)
+// smallest Marquardt damping after accepted steps (keeps gauge directions regularised)
+constexpr double kLambdaMin = 1e-6;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+VX_KT_TABLE();
+
+// Levenberg-Marquardt variables; k_sba_solve of iteration it reads lm[it & 1] and writes
+// lm[(it + 1) & 1] (so no workgroup of the launch reads what another writes).
+struct LMVars {
+    int sel;          // buffer with the best state: -1 = initial arrays, 0 / 1
+    int eval_trial;   // the next assembly evaluates the trial buffer
+    int do_solve;     // k_sba_update of this iteration applies a step
+    int accepted;
+    double lambda;    // damping of the next assembly
+    double best_cost;
+};
+
+struct SBAState {
+    int active[kSbaMaxIter + 1];
+    int fail[kSbaMaxIter];       // a component's Cholesky hit a non-positive pivot
+    LMVars lm[2];
+    int iterations;
+    int pad;
+    double initial_cost;
+    double cost[16];
+    int obs[16];
+    int step[16];
+};
+
+struct SBAArgs {
+    int nk, n_opt, n_lm, n_oo, n_obs;
+    int max_iter, min_point_obs;
+    double huber, max_err, lambda0, rel_tol;
+    double rho_gate;        // Huber cost of an observation at the gate (max_reproj_error)
+    const double* pose0;    // nk x 8
+    double* pose;           // 2 x nk x 8
+    const double* intr;     // nk x 4
+    const int* kf_flags;    // bit0 camera, bit1 fixed
+    const int* kf_comp;     // component of a free keyframe (-1 fixed)
+    const int* kf_local;    // keyframe index inside its component
+    const double* lm0;      // n_lm x 4
+    double* lm;             // 2 x n_opt x 4
+    const double2* obs_uv;
+    const int* obs_kf;
+    const int* obs_lm;
+    const int* lm_ptr;      // n_opt + 1
+    const int* lm_blk;      // k_sba_lm workgroup -> first landmark
+    const int* kf_ptr;      // nk + 1 into kf_obs
+    const int* kf_obs;
+    const int2* blk_ij;
+    const int* blk_ptr;
+    const int2* pairs;
+    const int* comp_kf_ptr; // component -> keyframe list (comp_kf)
+    const int* comp_kf;
+    const long long* comp_off;   // component -> offset of its dense matrix in red (ld = comp_np)
+    const long long* comp_loff;  // component -> offset of its factor in L ((np + 16) x np)
+    const int* comp_np;
+    const int* comp_hdr;    // component -> kHdrN ints (tile program offsets, nt)
+    const int* tl;          // tile programs
+    double* wy;             // n_oo x kWy
+    double* lm_sys;         // n_opt x kLmSys
+    double* red;            // local: S blocks | rhs (6 nk) | D (6 nk) | kf_cost (2 nk)
+    const double* red_sum;  // == red unless sharded
+    long long s_total;      // doubles of all component matrices
+    double* L;
+    double* Linv;           // per component: nt x 256, at the component's L offset
+    double* dx;             // 6 nk
+    SBAState* st;
+};
+
+// ------------------------------------------------------------------------- state selection
+__device__ __forceinline__ int trial_idx(int sel) { return sel == 0 ? 1 : 0; }
+
+// Pose / landmark tables the assembly of iteration it evaluates.
+__device__ __forceinline__ const double* eval_pose(const SBAArgs& a, int it) {
+    if (it == 0) return a.pose0;
+    const LMVars& v = a.st->lm[it & 1];
+    const int b = v.eval_trial ? trial_idx(v.sel) : v.sel;
+    return b < 0 ? a.pose0 : a.pose + (long long)b * a.nk * 8;
+}
+__device__ __forceinline__ const double* eval_lm(const SBAArgs& a, int it) {
+    if (it == 0) return a.lm0;
+    const LMVars& v = a.st->lm[it & 1];
+    const int b = v.eval_trial ? trial_idx(v.sel) : v.sel;
+    return b < 0 ? a.lm0 : a.lm + (long long)b * a.n_opt * 4;
+}
+
+// One observation at a state: residual, gates, IRLS weight, Huber cost and the Jacobians.
+struct ObsEval {
+    bool ok;
+    double w, rho, e0, e1;
+    double JT0[6], JT1[6];  // d(uv)/d(upsilon, omega), rows u and v (PoseJacobian, local_ba.cpp:26-33)
+    double JP0[3], JP1[3];  // d(uv)/dp = Jp R (local_ba.cpp:219-221)
+};
+
+__device__ __forceinline__ void eval_obs(const SBAArgs& a, const double* T, const double* C, D3 P, double2 uv,
+                                         bool need_jp, ObsEval& o) {
+    const D3 pc = se3_apply(T, P);
+    const bool front = pc.z > 1e-6;
+    const double inv_z = frcp(pc.z);
+    const double x = pc.x * inv_z, y = pc.y * inv_z;
+    const double fx = C[0], fy = C[1];
+    o.e0 = uv.x - (fx * x + C[2]);
+    o.e1 = uv.y - (fy * y + C[3]);
+    const double e2 = o.e0 * o.e0 + o.e1 * o.e1;
+    const double re = e2 > 0.0 ? frsq(e2) : 0.0;
+    const double en = e2 * re;
+    o.ok = front && !(en > a.max_err);
+    const double d = a.huber;
+    o.w = en <= d ? 1.0 : d * re;
+    o.rho = en <= d ? e2 : 2.0 * d * en - d * d;
+    const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+    o.JT0[0] = jp0; o.JT0[1] = 0.0; o.JT0[2] = jp2;
+    o.JT0[3] = jp2 * pc.y; o.JT0[4] = jp0 * pc.z - jp2 * pc.x; o.JT0[5] = -jp0 * pc.y;
+    o.JT1[0] = 0.0; o.JT1[1] = jp4; o.JT1[2] = jp5;
+    o.JT1[3] = jp5 * pc.y - jp4 * pc.z; o.JT1[4] = -jp5 * pc.x; o.JT1[5] = jp4 * pc.x;
+    if (need_jp) {
+        double R[9];
+        rot_from_quat(T, R);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            o.JP0[c] = jp0 * R[c] + jp2 * R[6 + c];
+            o.JP1[c] = jp4 * R[3 + c] + jp5 * R[6 + c];
+        }
+    }
+}
+
+// Inverse of the symmetric {a b c; b d e; c e f} by its adjugate (the restatement uses the same).
+__device__ __forceinline__ void sym3_inverse(const double* V, double* out) {
+    const double a = V[0], b = V[1], c = V[2], d = V[3], e = V[4], f = V[5];
+    const double A = d * f - e * e, B = c * e - b * f, C = b * e - c * d;
+    const double D = a * f - c * c, E = b * c - a * e, F = a * d - b * b;
+    const double det = a * A + b * B + c * C;
+    const double id = frcp(det);
+    out[0] = A * id; out[1] = B * id; out[2] = C * id; out[3] = D * id; out[4] = E * id; out[5] = F * id;
+}
+
+// ------------------------------------------------------------------------- k_sba_lm
+__global__ __launch_bounds__(kLmThreads) void k_sba_lm(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    __shared__ double terms[10][kLmThreads];
+    __shared__ double vinv[6][kLmThreads];
+    const int tid = threadIdx.x;
+    const int l0 = a.lm_blk[blockIdx.x], l1 = a.lm_blk[blockIdx.x + 1];
+    const int ob0 = a.lm_ptr[l0], ob1 = a.lm_ptr[l1];
+    const int o = ob0 + tid;
+    const bool has = o < ob1;
+    const double* Tb = eval_pose(a, it);
+    const double* Pb = eval_lm(a, it);
+    const double lambda = it == 0 ? a.lambda0 : a.st->lm[it & 1].lambda;
+    ObsEval e;
+    int s = l0;
+    if (has) {
+        const int k = a.obs_kf[o];
+        s = a.obs_lm[o];
+        const double* P = Pb + 4 * (long long)s;
+        double T[8], C[4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) T[j] = Tb[8 * k + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) C[j] = a.intr[4 * k + j];
+        eval_obs(a, T, C, {P[0], P[1], P[2]}, a.obs_uv[o], true, e);
+    } else {
+        e.ok = false;
+    }
+    {
+        const double w = e.ok ? e.w : 0.0;
+        const double* J0 = e.JP0;
+        const double* J1 = e.JP1;
+        terms[0][tid] = e.ok ? (w * J0[0]) * J0[0] + (w * J1[0]) * J1[0] : 0.0;
+        terms[1][tid] = e.ok ? (w * J0[0]) * J0[1] + (w * J1[0]) * J1[1] : 0.0;
+        terms[2][tid] = e.ok ? (w * J0[0]) * J0[2] + (w * J1[0]) * J1[2] : 0.0;
+        terms[3][tid] = e.ok ? (w * J0[1]) * J0[1] + (w * J1[1]) * J1[1] : 0.0;
+        terms[4][tid] = e.ok ? (w * J0[1]) * J0[2] + (w * J1[1]) * J1[2] : 0.0;
+        terms[5][tid] = e.ok ? (w * J0[2]) * J0[2] + (w * J1[2]) * J1[2] : 0.0;
+        terms[6][tid] = e.ok ? w * (J0[0] * e.e0 + J1[0] * e.e1) : 0.0;
+        terms[7][tid] = e.ok ? w * (J0[1] * e.e0 + J1[1] * e.e1) : 0.0;
+        terms[8][tid] = e.ok ? w * (J0[2] * e.e0 + J1[2] * e.e1) : 0.0;
+        terms[9][tid] = e.ok ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    const int l = l0 + tid;
+    if (l < l1) {
+        const int r0 = a.lm_ptr[l] - ob0, r1 = a.lm_ptr[l + 1] - ob0;
+        double h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int r = r0; r < r1; ++r)
+#pragma unroll
+            for (int j = 0; j < 10; ++j) h[j] += terms[j][r];
+        double Vd[6] = {h[0], h[1], h[2], h[3], h[4], h[5]};
+        Vd[0] += lambda * h[0] + 1e-6;
+        Vd[3] += lambda * h[3] + 1e-6;
+        Vd[5] += lambda * h[5] + 1e-6;
+        // fewer valid observations than min_point_observations: the landmark is held fixed in
+        // this iteration (V^-1 = 0, so no Schur term and dp = 0), as local_ba.cpp:228-229 skips it
+        double Vi[6] = {0, 0, 0, 0, 0, 0};
+        if (h[9] >= (double)a.min_point_obs) sym3_inverse(Vd, Vi);
+        double* out = a.lm_sys + (long long)l * kLmSys;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            vinv[j][tid] = Vi[j];
+            out[j] = Vi[j];
+        }
+        out[6] = h[6];
+        out[7] = h[7];
+        out[8] = h[8];
+    }
+    __syncthreads();
+    if (!has) return;
+    const int ls = s - l0;
+    const double Vi[6] = {vinv[0][ls], vinv[1][ls], vinv[2][ls], vinv[3][ls], vinv[4][ls], vinv[5][ls]};
+    const double w = e.ok ? e.w : 0.0;
+    double W[18], Y[18];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) W[3 * r + c] = e.ok ? w * (e.JT0[r] * e.JP0[c] + e.JT1[r] * e.JP1[c]) : 0.0;
+        Y[3 * r + 0] = Vi[0] * W[3 * r] + Vi[1] * W[3 * r + 1] + Vi[2] * W[3 * r + 2];
+        Y[3 * r + 1] = Vi[1] * W[3 * r] + Vi[3] * W[3 * r + 1] + Vi[4] * W[3 * r + 2];
+        Y[3 * r + 2] = Vi[2] * W[3 * r] + Vi[4] * W[3 * r + 1] + Vi[5] * W[3 * r + 2];
+    }
+    double2* dst = reinterpret_cast<double2*>(a.wy + (long long)o * kWy);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) dst[j] = make_double2(W[2 * j], W[2 * j + 1]);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) dst[9 + j] = make_double2(Y[2 * j], Y[2 * j + 1]);
+}
+
+// ------------------------------------------------------------------------- k_sba_blocks
+__device__ __forceinline__ void load18(const double* src, double* v) {
+    const double2* s2 = reinterpret_cast<const double2*>(src);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+        const double2 t = s2[j];
+        v[2 * j] = t.x;
+        v[2 * j + 1] = t.y;
+    }
+}
+
+__global__ __launch_bounds__(kBlkThreads) void k_sba_blocks(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    __shared__ double red[kBlkThreads / 64][64];
+    const int tid = threadIdx.x, b = blockIdx.x;
+    if (b == 0 && tid == 0) a.st->fail[it] = 0;
+    const int2 ij = a.blk_ij[b];
+    const int i = ij.x, j = ij.y;
+    const bool diag = i == j;
+    const bool fixed_i = (a.kf_flags[i] & 2) != 0;
+    double acc[kBlkTerms];
+#pragma unroll
+    for (int t = 0; t < kBlkTerms; ++t) acc[t] = 0.0;
+    if (diag) {
+        const double* Tb = eval_pose(a, it);
+        const double* Pb = eval_lm(a, it);
+        double T[8], C[4];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) T[q] = Tb[8 * i + q];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) C[q] = a.intr[4 * i + q];
+        for (int idx = a.kf_ptr[i] + tid; idx < a.kf_ptr[i + 1]; idx += kBlkThreads) {
+            const int o = a.kf_obs[idx];
+            const int s = a.obs_lm[o];
+            const double* P = (s < a.n_opt ? Pb : a.lm0) + 4 * (long long)s;
+            ObsEval e;
+            eval_obs(a, T, C, {P[0], P[1], P[2]}, a.obs_uv[o], false, e);
+            // a gated observation costs the constant rho(max_reproj_error) (truncated robust cost)
+            acc[48] += e.ok ? e.rho : a.rho_gate;
+            if (!e.ok) continue;
+            acc[49] += 1.0;
+            if (fixed_i) continue;
+            const double w = e.w;
+#pragma unroll
+            for (int r = 0; r < 6; ++r) {
+                const double wr0 = w * e.JT0[r], wr1 = w * e.JT1[r];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) acc[6 * r + c] += wr0 * e.JT0[c] + wr1 * e.JT1[c];
+                acc[36 + r] += wr0 * e.e0 + wr1 * e.e1;
+                acc[42 + r] += wr0 * e.JT0[r] + wr1 * e.JT1[r];
+            }
+            if (s < a.n_opt) {  // rhs -= Y_o g_p
+                double Y[18];
+                load18(a.wy + (long long)o * kWy + 18, Y);
+                const double* g = a.lm_sys + (long long)s * kLmSys + 6;
+                const double g0 = g[0], g1 = g[1], g2 = g[2];
+#pragma unroll
+                for (int r = 0; r < 6; ++r) acc[36 + r] -= Y[3 * r] * g0 + Y[3 * r + 1] * g1 + Y[3 * r + 2] * g2;
+            }
+        }
+    }
+    for (int p = a.blk_ptr[b] + tid; p < a.blk_ptr[b + 1]; p += kBlkThreads) {
+        const int2 pr = a.pairs[p];
+        double Y[18], W[18];
+        load18(a.wy + (long long)pr.x * kWy + 18, Y);
+        load18(a.wy + (long long)pr.y * kWy, W);
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = 0; c < 6; ++c)
+                acc[6 * r + c] -= Y[3 * r] * W[3 * c] + Y[3 * r + 1] * W[3 * c + 1] + Y[3 * r + 2] * W[3 * c + 2];
+    }
+    // workgroup reduction: two halving butterflies (terms 0-31, 32-49), then the 4 waves in order
+    const int wv = tid >> 6, lane = tid & 63;
+    {
+        double r[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) r[t] = acc[t];
+        const double tot = wave_sum32(r);
+        if ((lane & 1) == 0) red[wv][lane >> 1] = tot;
+    }
+    {
+        double r[32];
+#pragma unroll
+        for (int t = 0; t < 32; ++t) r[t] = t < kBlkTerms - 32 ? acc[32 + t] : 0.0;
+        const double tot = wave_sum32(r);
+        if ((lane & 1) == 0) red[wv][32 + (lane >> 1)] = tot;
+    }
+    __syncthreads();
+    if (tid >= kBlkTerms) return;
+    double v = red[0][tid];
+#pragma unroll
+    for (int w2 = 1; w2 < kBlkThreads / 64; ++w2) v += red[w2][tid];
+    const int n6 = 6 * a.nk;
+    double* rhs = a.red + a.s_total;
+    if (tid < 36) {
+        const int c = a.kf_comp[i];
+        if (c < 0) return;  // a fixed keyframe's block: its row is the identity (k_sba_solve)
+        const int np = a.comp_np[c];
+        const int li = a.kf_local[i], lj = a.kf_local[j];
+        const int r = tid / 6, cc = tid - 6 * r;
+        a.red[a.comp_loff[c] + (long long)(6 * li + r) * np + 6 * lj + cc] = v;
+    } else if (diag) {
+        if (tid < 42) rhs[6 * i + tid - 36] = v;
+        else if (tid < 48) rhs[n6 + 6 * i + tid - 42] = v;
+        else rhs[2 * n6 + 2 * i + tid - 48] = v;
+    }
+}
+
+// ------------------------------------------------------------------------- k_sba_solve
+__device__ __forceinline__ double rl(double v, int lane) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), lane),
+                            __builtin_amdgcn_readlane(__double2loint(v), lane));
+}
+
+// Levenberg-Marquardt decision of iteration it (identical in every workgroup): returns the step
+// code (2 initial, 1 accepted, 0 rejected, 3 re-assembled after a reject) and the next variables.
+__device__ int lm_decide(const SBAArgs& a, int it, double cost, int cnt, LMVars& nx, bool& active_next) {
+    LMVars pv;
+    if (it == 0) {
+        pv.sel = -1;
+        pv.eval_trial = 0;
+        pv.do_solve = 0;
+        pv.accepted = 0;
+        pv.lambda = a.lambda0;
+        pv.best_cost = cost;
+    } else {
+        pv = a.st->lm[it & 1];
+    }
+    nx = pv;
+    int step;
+    bool stop = false;
+    if (it == 0) {
+        step = 2;
+    } else if (pv.eval_trial) {
+        if (cost < pv.best_cost) {
+            const double rel = (pv.best_cost - cost) / pv.best_cost;
+            nx.sel = trial_idx(pv.sel);
+            nx.best_cost = cost;
+            nx.lambda = fmax(pv.lambda * 0.1, kLambdaMin);
+            nx.accepted = pv.accepted + 1;
+            step = 1;
+            stop = rel < a.rel_tol;
+        } else {
+            nx.lambda = pv.lambda * 10.0;
+            step = 0;
+            stop = nx.lambda > 1e12;
+        }
+    } else {
+        step = 3;
+    }
+    if (cnt == 0) stop = true;
+    const bool last = stop || it + 1 >= a.max_iter;
+    nx.do_solve = (!last && step != 0) ? 1 : 0;
+    nx.eval_trial = nx.do_solve;
+    active_next = !last;
+    return step;
+}
+
+// Operand-order LDS image of a 16x16 tile: lane l's MFMA operands (row l & 15, columns
+// 4 (l >> 4) .. + 3) are 4 consecutive doubles at 4 l: conflict-free 32-byte reads.
+__device__ __forceinline__ int opo(int row, int col) { return 4 * (row + 16 * (col >> 2)) + (col & 3); }
+
+// C += s * A B^T over one 16x16 tile pair given as operand-order LDS images.
+__device__ __forceinline__ d4 mfma_abt(const double* A, const double* B, d4 c, bool neg) {
+    const int lane = threadIdx.x & 63;
+    const double4 av = *reinterpret_cast<const double4*>(A + 4 * lane);
+    const double4 bv = *reinterpret_cast<const double4*>(B + 4 * lane);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(neg ? -av.x : av.x, bv.x, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(neg ? -av.y : av.y, bv.y, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(neg ? -av.z : av.z, bv.z, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(neg ? -av.w : av.w, bv.w, c, 0, 0, 0);
+    return c;
+}
+
+// Accumulator layout of v_mfma_f64_16x16x4: lane l, register r -> row (l >> 4) + 4 r, col l & 15.
+__device__ __forceinline__ d4 load_acc(const double* T, int ld) {
+    const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
+    d4 v;
+    v[0] = T[(long long)(r0) * ld + c];
+    v[1] = T[(long long)(r0 + 4) * ld + c];
+    v[2] = T[(long long)(r0 + 8) * ld + c];
+    v[3] = T[(long long)(r0 + 12) * ld + c];
+    return v;
+}
+__device__ __forceinline__ void store_acc(double* T, int ld, d4 v) {
+    const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
+    T[(long long)(r0) * ld + c] = v[0];
+    T[(long long)(r0 + 4) * ld + c] = v[1];
+    T[(long long)(r0 + 8) * ld + c] = v[2];
+    T[(long long)(r0 + 12) * ld + c] = v[3];
+}
+__device__ __forceinline__ void store_acc_opo(double* S, d4 v) {
+    const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) S[opo(r0 + 4 * r, c)] = v[r];
+}
+
+// One wave: Cholesky of the symmetric 16x16 tile at A (lower triangle read) and the inverse of its
+// factor.  Lane i holds row i in registers.  Per column j the pivot comes from lane j
+// (v_readlane), every lane scales its entry, writes it to the LDS column image `lcol` and reads the
+// column back with broadcast ds_reads for its rank-1 update; the next pivot is updated by its own
+// lane, so the chain per column is readlane -> rsq (+2 Newton) -> mul -> LDS round trip -> fma.
+// L^-1 (lane i = column i, right-looking forward substitution over the LDS columns) is written as
+// an operand-order LDS image and row-major to Lg.  Returns false on a non-positive pivot.
+__device__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
+    const int lane = threadIdx.x & 63, i = lane & 15;
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) a[c] = c <= i ? A[(long long)i * ld + c] : A[(long long)c * ld + i];
+    double srow = 0.0;  // lane i: 1 / L_ii
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const double d = rl(a[j], j);
+        ok = ok && d > 0.0 && d < 1e300;
+        const double r = frsq(d > 0.0 ? d : 1.0);
+        if (i == j) srow = r;
+        const double l = a[j] * r;  // L[i][j] for i >= j
+        a[j] = l;
+        if (lane < 16) lcol[16 * j + i] = l;
+#pragma unroll
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-l, lcol[16 * j + c], a[c]);
+    }
+    if (lane < 16) lcol[256 + i] = srow;
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = r == i ? 1.0 : 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        x[j] *= lcol[256 + j];
+#pragma unroll
+        for (int m = j + 1; m < 16; ++m) x[m] = fma(-lcol[16 * j + m], x[j], x[m]);
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            lds_inv[opo(r, i)] = x[r];
+            Lg[r * 16 + i] = x[r];
+        }
+    }
+    return ok;
+}
+
+// Per-component tile program (host symbolic factorisation, vx_sba_plan): int offsets into a.tl.
+enum {
+    kHdrCopy = 0,   // nonzero tiles of L + the rhs tile row (packed ti << 16 | tj)
+    kHdrNCopy,
+    kHdrPanel,      // nt + 1 pointers (absolute into tl), then per step the panel tile rows
+    kHdrTrail,      // nt + 1 pointers, then per step the trailing tiles
+    kHdrBack,       // nt + 1 pointers, then per step k the tile columns m < k of row k
+    kHdrNt,
+    kHdrN = 8
+};
+
+__global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    extern __shared__ __attribute__((aligned(32))) double smem[];
+    __shared__ int s_solve;
+    __shared__ double s_lambda;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int comp = blockIdx.x;
+    const int n6 = 6 * a.nk;
+    const double* rhs_g = a.red_sum + a.s_total;
+    // ---- decision (wave 0; fixed-order totals, identical in every workgroup)
+    if (wv == 0) {
+        double tot = 0.0, cnt = 0.0;
+        for (int q = lane; q < a.nk; q += 64) {
+            tot += rhs_g[2 * n6 + 2 * q];
+            cnt += rhs_g[2 * n6 + 2 * q + 1];
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            tot += __shfl_xor(tot, o, 64);
+            cnt += __shfl_xor(cnt, o, 64);
+        }
+        if (lane == 0) {
+            LMVars nx;
+            bool act;
+            const int step = lm_decide(a, it, tot, (int)cnt, nx, act);
+            s_solve = nx.do_solve;
+            s_lambda = it == 0 ? a.lambda0 : a.st->lm[it & 1].lambda;  // the damping S was assembled with
+            if (comp == 0) {
+                SBAState* st = a.st;
+                st->lm[(it + 1) & 1] = nx;
+                if (it == 0) {
+                    st->initial_cost = tot;
+                    for (int q = 1; q < 16; ++q) {
+                        st->cost[q] = 0;
+                        st->obs[q] = 0;
+                        st->step[q] = 0;
+                    }
+                }
+                if (it < 16) {
+                    st->cost[it] = tot;
+                    st->obs[it] = (int)cnt;
+                    st->step[it] = step;
+                }
+                st->iterations = it + 1;
+                if (act)
+                    st->active[it + 1] = 1;
+                else
+                    for (int q = it + 1; q <= a.max_iter; ++q) st->active[q] = 0;
+            }
+        }
+    }
+    __syncthreads();
+    if (!s_solve) return;
+    VX_KT(0);
+    const double lambda = s_lambda;
+    const int* hdr = a.comp_hdr + kHdrN * comp;
+    const int nt = hdr[kHdrNt], np = 16 * nt;
+    const int kq0 = a.comp_kf_ptr[comp], nkc = a.comp_kf_ptr[comp + 1] - kq0;
+    const int nc = 6 * nkc;
+    double* L = a.L + a.comp_loff[comp];
+    double* Linv = a.Linv + a.comp_loff[comp];  // same offsets as L (>= 16 np per component)
+    const int* tl = a.tl;
+    double* panel = smem;                                       // (nt + 1) operand-order tiles
+    double* dlds = smem + (long long)(nt + 1) * kPanelStride;   // L_kk^-1 of the current step
+    double* lcol = dlds + kPanelStride;                         // POTRF column images (272 doubles)
+    double* ys = lcol + 2 * kPanelStride;                       // np: y, then x
+    const int r0 = lane >> 4, cl = lane & 15;
+    // ---- k_sba_blocks wrote the component matrix straight into L (the all-reduce did, sharded);
+    // add the damping on the diagonal, the identity on padding rows and the rhs tile row
+    for (int e = tid; e < np; e += kSolveThreads) {
+        double* dg = L + (long long)e * np + e;
+        if (e < nc) {
+            const int g = 6 * a.comp_kf[kq0 + e / 6] + e % 6;
+            *dg += lambda * rhs_g[n6 + g] + 1e-6;
+            L[(long long)np * np + e] = rhs_g[g];
+        } else {
+            *dg = 1.0;
+            L[(long long)np * np + e] = 0.0;
+        }
+    }
+    __syncthreads();
+    VX_KT(1);
+    bool ok = true;
+    const int* pptr = tl + hdr[kHdrPanel];
+    const int* tptr = tl + hdr[kHdrTrail];
+    const int* bptr = tl + hdr[kHdrBack];
+    for (int k = 0; k < nt; ++k) {
+        // trace slots: steps 0, 1 and nt / 2 (factor | panel | trailing update)
+        const int kts = k == 0 ? 2 : (k == 1 ? 5 : (k == nt / 2 ? 8 : -1));
+        double* Lkk = L + (long long)(16 * k) * np + 16 * k;
+        if (wv == 0) ok = potrf_inv16(Lkk, np, lcol, dlds, Linv + 256 * k) && ok;
+        __syncthreads();
+        if (kts >= 0) VX_KT(kts);
+        // panel: L_ik = A_ik L_kk^-T over the nonzero tiles of column k (and the rhs row)
+        for (int q = pptr[k] + wv; q < pptr[k + 1]; q += kSolveWaves) {
+            const int i = tl[q];
+            double* Aik = L + (long long)(16 * i) * np + 16 * k;
+            // the A operand in operand order straight from global: row l & 15, columns 4 (l >> 4) ..
+            const double4 av = *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0);
+            const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
+            d4 c = {0.0, 0.0, 0.0, 0.0};
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.z, bv.z, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, c, 0, 0, 0);
+            store_acc(Aik, np, c);
+            store_acc_opo(panel + (long long)i * kPanelStride, c);
+        }
+        __syncthreads();
+        if (kts >= 0) VX_KT(kts + 1);
+        // trailing update A_ij -= L_ik L_jk^T over the tiles the symbolic factorisation lists,
+        // four tiles per wave in flight
+        const int t_beg = tptr[k], t_end = tptr[k + 1];
+        for (int t0 = t_beg + wv * 4; t0 < t_end; t0 += kSolveWaves * 4) {
+            d4 c[4];
+            int ti[4], tj[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int t = t0 + q;
+                ti[q] = -1;
+                if (t < t_end) {
+                    ti[q] = tl[t] >> 16;
+                    tj[q] = tl[t] & 0xffff;
+                    c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (ti[q] < 0) continue;
+                c[q] = mfma_abt(panel + (long long)ti[q] * kPanelStride, panel + (long long)tj[q] * kPanelStride, c[q],
+                                true);
+                store_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np, c[q]);
+            }
+        }
+        __syncthreads();
+        if (kts >= 0) VX_KT(kts + 2);
+    }
+    VX_KT(11);
+    if (wv == 0 && lane == 0 && !ok) atomicOr(&a.st->fail[it], 1);
+    // ---- back-substitution L^T x = y (y = row np of the factored rhs tile row)
+    for (int c = tid; c < np; c += kSolveThreads) ys[c] = L[(long long)np * np + c];
+    __syncthreads();
+    for (int k = nt - 1; k >= 0; --k) {
+        double xk = 0.0;
+        if (wv == 0) {  // x_k = L_kk^-T y_k
+            const double* Li = Linv + 256 * k;
+#pragma unroll
+            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) xk += Li[r * 16 + cl] * ys[16 * k + r];
+            xk += __shfl_xor(xk, 16, 64);
+            xk += __shfl_xor(xk, 32, 64);
+        }
+        __syncthreads();  // every lane has read y_k before it is overwritten with x_k
+        if (wv == 0 && r0 == 0) ys[16 * k + cl] = xk;
+        __syncthreads();
+        // y_m -= L_km^T x_k for the nonzero tiles of row k, one wave per tile
+        for (int q = bptr[k] + wv; q < bptr[k + 1]; q += kSolveWaves) {
+            const int mm = tl[q];
+            const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
+            double p = 0.0;
+#pragma unroll
+            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) p += Lkm[(long long)r * np + cl] * ys[16 * k + r];
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (r0 == 0) ys[16 * mm + cl] -= p;
+        }
+        __syncthreads();
+    }
+    VX_KT(12);
+    for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
+    // the next assembly writes only S's blocks into L: clear every tile the factorisation touched
+    {
+        const int* cp = tl + hdr[kHdrCopy];
+        const int ncp = hdr[kHdrNCopy];
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        for (int t = wv; t < ncp; t += kSolveWaves)
+            store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
+    }
+}
+
+// ------------------------------------------------------------------------- k_sba_update
+__global__ __launch_bounds__(kUpdThreads) void k_sba_update(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    const LMVars v = a.st->lm[(it + 1) & 1];
+    if (!v.do_solve) return;
+    const int t = blockIdx.x * kUpdThreads + threadIdx.x;
+    if (a.st->fail[it]) {  // a component's Cholesky failed: discard the step, damp harder
+        if (t == 0) {
+            LMVars& w = a.st->lm[(it + 1) & 1];
+            w.lambda *= 10.0;
+            w.eval_trial = 0;
+            w.do_solve = 0;
+        }
+        return;
+    }
+    const int best = v.sel, trial = trial_idx(v.sel);
+    if (t < a.nk) {
+        const double* Tb = best < 0 ? a.pose0 : a.pose + (long long)best * a.nk * 8;
+        double* Tt = a.pose + (long long)trial * a.nk * 8;
+        double T[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) T[j] = Tb[8 * t + j];
+        if (!(a.kf_flags[t] & 2)) {
+            double d[6];
+            bool fin = true;
+#pragma unroll
+            for (int j = 0; j < 6; ++j) {
+                d[j] = a.dx[6 * t + j];
+                fin = fin && isfinite(d[j]);
+            }
+            if (fin) se3_left_update(d, T);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Tt[8 * t + j] = T[j];
+    }
+    if (t < a.n_opt) {
+        const double* Pb = (best < 0 ? a.lm0 : a.lm + (long long)best * a.n_opt * 4) + 4 * (long long)t;
+        double* Pt = a.lm + (long long)trial * a.n_opt * 4 + 4 * (long long)t;
+        const double* sys = a.lm_sys + (long long)t * kLmSys;
+        double q[3] = {sys[6], sys[7], sys[8]};
+        for (int o = a.lm_ptr[t]; o < a.lm_ptr[t + 1]; ++o) {
+            const int k = a.obs_kf[o];
+            if (a.kf_flags[k] & 2) continue;
+            double W[18];
+            load18(a.wy + (long long)o * kWy, W);
+            const double* d = a.dx + 6 * k;
+            double dd[6];
+#pragma unroll
+            for (int r = 0; r < 6; ++r) dd[r] = d[r];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+#pragma unroll
+                for (int r = 0; r < 6; ++r) q[c] -= W[3 * r + c] * dd[r];
+        }
+        const double dp0 = sys[0] * q[0] + sys[1] * q[1] + sys[2] * q[2];
+        const double dp1 = sys[1] * q[0] + sys[3] * q[1] + sys[4] * q[2];
+        const double dp2 = sys[2] * q[0] + sys[4] * q[1] + sys[5] * q[2];
+        const bool fin = isfinite(dp0) && isfinite(dp1) && isfinite(dp2);
+        Pt[0] = Pb[0] + (fin ? dp0 : 0.0);
+        Pt[1] = Pb[1] + (fin ? dp1 : 0.0);
+        Pt[2] = Pb[2] + (fin ? dp2 : 0.0);
+        Pt[3] = 0.0;
+    }
+}
+
+template <class T>
+int upload(vx_ctx* c, DevBuf& d, const std::vector<T>& h) {
+    VX_HIP(c, d.ensure(std::max<size_t>(1, h.size()) * sizeof(T)));
+    if (!h.empty()) VX_HIP(c, hipMemcpy(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+    return VX_OK;
+}
+
+}  // namespace
+}  // namespace vx
+
+struct vx_sba_plan {
+    vx_ctx* c = nullptr;
+    vx_sba_options opt{};
+    int status = 1;
+    int shard_rank = 0, shard_count = 1;
+    int n_window_kf = 0, n_landmarks_global = 0;
+    int nk = 0, n_opt = 0, n_lm = 0, n_oo = 0, n_obs = 0;
+    int64_t n_pairs = 0;
+    int n_blocks = 0, n_lm_blocks = 0, n_comp = 0, max_np = 0;
+    long long s_total = 0, l_total = 0;
+    std::vector<int> kf_map_idx, lm_map_idx;
+    std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
+    std::vector<long long> comp_off_h, comp_loff_h;
+    int64_t n_lfactor_tiles = 0, n_trail_updates = 0;  // symbolic factorisation (all components)
+    vx::DevBuf pose0, pose, intr, kf_flags, kf_comp, kf_local, lm0, lm, obs_uv, obs_kf, obs_lm, lm_ptr, lm_blk,
+        kf_ptr, kf_obs, blk_ij, blk_ptr, pairs, comp_kf_ptr, comp_kf, comp_off, comp_loff, comp_np, comp_hdr, tl, wy,
+        lm_sys,
+        red, red_sum, L, Linv, dx, state;
+    bool ran = false;
+};
+
+namespace vx {
+namespace {
+
+SBAArgs make_args(vx_sba_plan* p) {
+    SBAArgs a{};
+    a.nk = p->nk;
+    a.n_opt = p->n_opt;
+    a.n_lm = p->n_lm;
+    a.n_oo = p->n_oo;
+    a.n_obs = p->n_obs;
+    a.max_iter = p->opt.max_iterations;
+    a.min_point_obs = p->opt.min_point_observations;
+    a.huber = p->opt.huber_delta;
+    a.max_err = p->opt.max_reproj_error;
+    a.lambda0 = p->opt.lambda_init;
+    a.rel_tol = p->opt.rel_tol;
+    {
+        const double d = p->opt.huber_delta, me = p->opt.max_reproj_error;
+        a.rho_gate = me <= d ? me * me : 2.0 * d * me - d * d;
+    }
+    a.pose0 = p->pose0.as<double>();
+    a.pose = p->pose.as<double>();
+    a.intr = p->intr.as<double>();
+    a.kf_flags = p->kf_flags.as<int>();
+    a.kf_comp = p->kf_comp.as<int>();
+    a.kf_local = p->kf_local.as<int>();
+    a.lm0 = p->lm0.as<double>();
+    a.lm = p->lm.as<double>();
+    a.obs_uv = p->obs_uv.as<double2>();
+    a.obs_kf = p->obs_kf.as<int>();
+    a.obs_lm = p->obs_lm.as<int>();
+    a.lm_ptr = p->lm_ptr.as<int>();
+    a.lm_blk = p->lm_blk.as<int>();
+    a.kf_ptr = p->kf_ptr.as<int>();
+    a.kf_obs = p->kf_obs.as<int>();
+    a.blk_ij = p->blk_ij.as<int2>();
+    a.blk_ptr = p->blk_ptr.as<int>();
+    a.pairs = p->pairs.as<int2>();
+    a.comp_kf_ptr = p->comp_kf_ptr.as<int>();
+    a.comp_kf = p->comp_kf.as<int>();
+    a.comp_off = p->comp_off.as<long long>();
+    a.comp_loff = p->comp_loff.as<long long>();
+    a.comp_np = p->comp_np.as<int>();
+    a.comp_hdr = p->comp_hdr.as<int>();
+    a.tl = p->tl.as<int>();
+    a.wy = p->wy.as<double>();
+    a.lm_sys = p->lm_sys.as<double>();
+    a.red = p->red.as<double>();
+    a.red_sum = p->shard_count > 1 ? p->red_sum.as<double>() : p->red.as<double>();
+    a.s_total = p->l_total;
+    a.L = const_cast<double*>(a.red_sum);  // component matrices are factored in place
+    a.Linv = p->Linv.as<double>();
+    a.dx = p->dx.as<double>();
+    a.st = p->state.as<SBAState>();
+    return a;
+}
+
+int find_root(std::vector<int>& par, int x) {
+    while (par[x] != x) {
+        par[x] = par[par[x]];
+        x = par[x];
+    }
+    return x;
+}
+
+int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_sba_plan* p) {
+    const vx_sba_options& o = p->opt;
+    p->status = 1;
+    Window W;
+    select_window(m, ref_kf_id, has_ref, o.window_size, o.min_point_observations, W);
+    p->n_window_kf = (int)W.win.size();
+    p->n_landmarks_global = (int)W.opt_all.size();
+    if (W.status != 0) return VX_OK;
+    p->status = 0;
+    const std::vector<int>& win = W.win;
+    const int nk = (int)win.size();
+    p->nk = nk;
+    p->kf_map_idx = win;
+    auto owned = [&](int l) {
+        return p->shard_count <= 1 ||
+               (int)(splitmix64(m->lm_id[l]) % (uint64_t)p->shard_count) == p->shard_rank;
+    };
+    std::vector<int> slot_of(m->n_lm, -1);
+    p->lm_map_idx.clear();
+    for (int l : W.opt_all)
+        if (owned(l)) {
+            slot_of[l] = (int)p->lm_map_idx.size();
+            p->lm_map_idx.push_back(l);
+        }
+    const int n_opt = (int)p->lm_map_idx.size();
+    p->n_opt = n_opt;
+
+    // ---- keyframes and observations (the pose stage's set, local_ba.cpp:126-138)
+    std::vector<double> pose0((size_t)nk * 8, 0.0), intr((size_t)nk * 4, 0.0);
+    std::vector<int> flags(nk, 0);
+    struct HObs { int kf, slot; double u, v; };
+    std::vector<std::vector<HObs>> per_slot(n_opt);
+    std::vector<HObs> fixed_obs;
+    for (int r = 0; r < nk; ++r) {
+        const int k = win[r];
+        for (int j = 0; j < 7; ++j) pose0[8 * r + j] = m->kf_pose[7 * k + j];
+        for (int j = 0; j < 4; ++j) intr[4 * r + j] = m->kf_intr[4 * k + j];
+        const bool cam = m->kf_has_cam[k] != 0;
+        flags[r] = (cam ? 1 : 0) | ((r < o.fixed_keyframes || !cam) ? 2 : 0);
+        if (!cam) continue;
+        for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) {
+            const uint8_t fl = m->feat_flags[f];
+            if (!(fl & 1) || (fl & 2)) continue;
+            auto it = W.lm_by_id.find(m->feat_lm_id[f]);
+            if (it == W.lm_by_id.end()) continue;
+            const int l = it->second;
+            if (m->lm_bad[l] || !owned(l)) continue;
+            if (slot_of[l] < 0) {  // a landmark the pose stage sees but BA does not optimise
+                slot_of[l] = (int)p->lm_map_idx.size();
+                p->lm_map_idx.push_back(l);
+            }
+            const HObs ob{r, slot_of[l], m->feat_uv[2 * f], m->feat_uv[2 * f + 1]};
+            if (ob.slot < n_opt)
+                per_slot[ob.slot].push_back(ob);
+            else
+                fixed_obs.push_back(ob);
+        }
+    }
+    p->n_lm = (int)p->lm_map_idx.size();
+    std::vector<double2> ouv;
+    std::vector<int> okf, olm, lptr(n_opt + 1, 0);
+    for (int s = 0; s < n_opt; ++s) {
+        if ((int)per_slot[s].size() > kLmThreads)
+            return set_error(c, VX_ERR_INVALID, "landmark with %d observations in the window (max %d)",
+                             (int)per_slot[s].size(), kLmThreads);
+        for (const HObs& ob : per_slot[s]) {
+            ouv.push_back(make_double2(ob.u, ob.v));
+            okf.push_back(ob.kf);
+            olm.push_back(ob.slot);
+        }
+        lptr[s + 1] = (int)okf.size();
+    }
+    p->n_oo = (int)okf.size();
+    for (const HObs& ob : fixed_obs) {
+        ouv.push_back(make_double2(ob.u, ob.v));
+        okf.push_back(ob.kf);
+        olm.push_back(ob.slot);
+    }
+    p->n_obs = (int)okf.size();
+    std::vector<double> lm0((size_t)std::max(p->n_lm, 1) * 4, 0.0);
+    for (int s = 0; s < p->n_lm; ++s)
+        for (int j = 0; j < 3; ++j) lm0[4 * s + j] = m->lm_pos[3 * p->lm_map_idx[s] + j];
+    // k_sba_lm workgroups: whole landmarks, <= kLmThreads observations and landmarks each
+    std::vector<int> blk{0};
+    {
+        int n_o = 0, n_l = 0;
+        for (int s = 0; s < n_opt; ++s) {
+            const int cnt = lptr[s + 1] - lptr[s];
+            if (n_l + 1 > kLmThreads || n_o + cnt > kLmThreads) {
+                blk.push_back(s);
+                n_o = n_l = 0;
+            }
+            n_o += cnt;
+            ++n_l;
+        }
+        blk.push_back(n_opt);
+    }
+    p->n_lm_blocks = (int)blk.size() - 1;
+    // keyframe-major observation lists
+    std::vector<int> kptr(nk + 1, 0), kobs(p->n_obs);
+    for (int ob = 0; ob < p->n_obs; ++ob) kptr[okf[ob] + 1]++;
+    for (int r = 0; r < nk; ++r) kptr[r + 1] += kptr[r];
+    {
+        std::vector<int> fill(kptr.begin(), kptr.end() - 1);
+        for (int ob = 0; ob < p->n_obs; ++ob) kobs[fill[okf[ob]]++] = ob;
+    }
+
+    // ---- connected components of the free keyframes' covisibility graph
+    std::vector<int> par(nk);
+    std::iota(par.begin(), par.end(), 0);
+    for (int s = 0; s < n_opt; ++s) {
+        int first = -1;
+        for (int ob = lptr[s]; ob < lptr[s + 1]; ++ob) {
+            if (flags[okf[ob]] & 2) continue;
+            if (first < 0)
+                first = okf[ob];
+            else
+                par[find_root(par, okf[ob])] = find_root(par, first);
+        }
+    }
+    std::vector<int> kcomp(nk, -1), klocal(nk, 0), root_comp(nk, -1);
+    p->comp_kf_ptr_h.assign(1, 0);
+    p->comp_kf_h.clear();
+    std::vector<std::vector<int>> comps;
+    for (int r = 0; r < nk; ++r) {
+        if (flags[r] & 2) continue;
+        const int rt = find_root(par, r);
+        if (root_comp[rt] < 0) {
+            root_comp[rt] = (int)comps.size();
+            comps.emplace_back();
+        }
+        kcomp[r] = root_comp[rt];
+        klocal[r] = (int)comps[kcomp[r]].size();
+        comps[kcomp[r]].push_back(r);
+    }
+    p->n_comp = (int)comps.size();
+    p->comp_np_h.clear();
+    p->comp_off_h.clear();
+    std::vector<long long> loff;
+    long long soff = 0, lo = 0;
+    p->max_np = 16;
+    for (const auto& cc : comps) {
+        if ((int)cc.size() > kMaxCompKf)
+            return set_error(c, VX_ERR_INVALID, "covisibility component of %d keyframes (dense solve max %d)",
+                             (int)cc.size(), kMaxCompKf);
+        const int np = std::max(16, (6 * (int)cc.size() + 15) / 16 * 16);
+        p->comp_np_h.push_back(np);
+        p->comp_off_h.push_back(soff);
+        loff.push_back(lo);
+        soff += (long long)np * np;
+        lo += (long long)(np + 16) * np;
+        p->max_np = std::max(p->max_np, np);
+        for (int r : cc) p->comp_kf_h.push_back(r);
+        p->comp_kf_ptr_h.push_back((int)p->comp_kf_h.size());
+    }
+    p->s_total = soff;
+    p->l_total = lo;
+    p->comp_loff_h = loff;
+
+    // ---- blocks of the reduced system: every keyframe's diagonal block, then the off-diagonal
+    // (i > j) blocks of co-observing free keyframes, each with its co-observation pairs
+    struct Quad { int64_t key; int o1, o2; };
+    std::vector<Quad> q;
+    for (int s = 0; s < n_opt; ++s)
+        for (int a1 = lptr[s]; a1 < lptr[s + 1]; ++a1) {
+            const int i = okf[a1];
+            if (flags[i] & 2) continue;
+            for (int a2 = lptr[s]; a2 < lptr[s + 1]; ++a2) {
+                const int j = okf[a2];
+                if ((flags[j] & 2) || j > i) continue;
+                q.push_back({(int64_t)i * nk + j, a1, a2});
+            }
+        }
+    std::sort(q.begin(), q.end(), [](const Quad& x, const Quad& y) {
+        if (x.key != y.key) return x.key < y.key;
+        if (x.o1 != y.o1) return x.o1 < y.o1;
+        return x.o2 < y.o2;
+    });
+    std::vector<int2> bij, prs;
+    std::vector<int> bptr{0};
+    {
+        // diagonal blocks first (block b = keyframe b), then off-diagonal blocks in key order
+        std::vector<std::vector<int2>> diag(nk);
+        std::vector<int64_t> keys;
+        std::vector<std::vector<int2>> off;
+        for (const Quad& x : q) {
+            const int i = (int)(x.key / nk), j = (int)(x.key % nk);
+            if (i == j) {
+                diag[i].push_back(make_int2(x.o1, x.o2));
+            } else {
+                if (keys.empty() || keys.back() != x.key) {
+                    keys.push_back(x.key);
+                    off.emplace_back();
+                }
+                off.back().push_back(make_int2(x.o1, x.o2));
+            }
+        }
+        for (int r = 0; r < nk; ++r) {
+            bij.push_back(make_int2(r, r));
+            prs.insert(prs.end(), diag[r].begin(), diag[r].end());
+            bptr.push_back((int)prs.size());
+        }
+        for (size_t b = 0; b < keys.size(); ++b) {
+            bij.push_back(make_int2((int)(keys[b] / nk), (int)(keys[b] % nk)));
+            prs.insert(prs.end(), off[b].begin(), off[b].end());
+            bptr.push_back((int)prs.size());
+        }
+    }
+    p->n_blocks = (int)bij.size();
+    p->n_pairs = (int64_t)prs.size();
+
+    // ---- symbolic tile factorisation per component: which 16 x 16 tiles of L are nonzero (the
+    // pattern of S's blocks plus Cholesky fill), and per step the panel / trailing-update / back-
+    // substitution tile lists k_sba_solve walks.  A sliding window's covisibility is banded, so
+    // most tiles of the dense matrix are never touched.
+    std::vector<int> hdr((size_t)kHdrN * std::max(p->n_comp, 1), 0), tlist;
+    p->n_lfactor_tiles = p->n_trail_updates = 0;
+    {
+        std::vector<std::vector<std::pair<int, int>>> cblk(p->n_comp);
+        for (const int2& b : bij) {
+            const int cc = kcomp[b.x];
+            if (cc >= 0 && kcomp[b.y] == cc) cblk[cc].push_back({klocal[b.x], klocal[b.y]});
+        }
+        for (int cc = 0; cc < p->n_comp; ++cc) {
+            const int nt = p->comp_np_h[cc] / 16;
+            std::vector<char> nz((size_t)nt * nt, 0);
+            auto NZ = [&](int i, int j) -> char& { return nz[(size_t)i * nt + j]; };
+            for (int t = 0; t < nt; ++t) NZ(t, t) = 1;
+            for (auto& b : cblk[cc])
+                for (int r = 6 * b.first; r < 6 * b.first + 6; r += 5)
+                    for (int q = 6 * b.second; q < 6 * b.second + 6; q += 5) {
+                        const int ti = std::max(r, q) / 16, tj = std::min(r, q) / 16;
+                        NZ(ti, tj) = 1;
+                    }
+            for (int k = 0; k < nt; ++k)
+                for (int i = k + 1; i < nt; ++i)
+                    if (NZ(i, k))
+                        for (int j = k + 1; j <= i; ++j)
+                            if (NZ(j, k)) NZ(i, j) = 1;
+            int* h = hdr.data() + (size_t)kHdrN * cc;
+            h[kHdrNt] = nt;
+            h[kHdrCopy] = (int)tlist.size();
+            for (int i = 0; i < nt; ++i)
+                for (int j = 0; j <= i; ++j)
+                    if (NZ(i, j)) tlist.push_back(i << 16 | j);
+            for (int j = 0; j < nt; ++j) tlist.push_back(nt << 16 | j);
+            h[kHdrNCopy] = (int)tlist.size() - h[kHdrCopy];
+            p->n_lfactor_tiles += h[kHdrNCopy];
+            // panel lists
+            h[kHdrPanel] = (int)tlist.size();
+            const int pp = (int)tlist.size();
+            tlist.resize(tlist.size() + nt + 1);
+            for (int k = 0; k < nt; ++k) {
+                tlist[pp + k] = (int)tlist.size();
+                for (int i = k + 1; i < nt; ++i)
+                    if (NZ(i, k)) tlist.push_back(i);
+                tlist.push_back(nt);
+            }
+            tlist[pp + nt] = (int)tlist.size();
+            // trailing-update lists
+            h[kHdrTrail] = (int)tlist.size();
+            const int tp = (int)tlist.size();
+            tlist.resize(tlist.size() + nt + 1);
+            for (int k = 0; k < nt; ++k) {
+                tlist[tp + k] = (int)tlist.size();
+                for (int i = k + 1; i < nt; ++i)
+                    if (NZ(i, k))
+                        for (int j = k + 1; j <= i; ++j)
+                            if (NZ(j, k)) tlist.push_back(i << 16 | j);
+                for (int j = k + 1; j < nt; ++j)
+                    if (NZ(j, k)) tlist.push_back(nt << 16 | j);
+                p->n_trail_updates += (int)tlist.size() - tlist[tp + k];
+            }
+            tlist[tp + nt] = (int)tlist.size();
+            // back-substitution lists: tile columns m < k of row k
+            h[kHdrBack] = (int)tlist.size();
+            const int bp = (int)tlist.size();
+            tlist.resize(tlist.size() + nt + 1);
+            for (int k = 0; k < nt; ++k) {
+                tlist[bp + k] = (int)tlist.size();
+                for (int m2 = 0; m2 < k; ++m2)
+                    if (NZ(k, m2)) tlist.push_back(m2);
+            }
+            tlist[bp + nt] = (int)tlist.size();
+        }
+    }
+
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = upload(c, p->pose0, pose0))) return rc;
+    if ((rc = upload(c, p->intr, intr))) return rc;
+    if ((rc = upload(c, p->kf_flags, flags))) return rc;
+    if ((rc = upload(c, p->kf_comp, kcomp))) return rc;
+    if ((rc = upload(c, p->kf_local, klocal))) return rc;
+    if ((rc = upload(c, p->lm0, lm0))) return rc;
+    if ((rc = upload(c, p->obs_uv, ouv))) return rc;
+    if ((rc = upload(c, p->obs_kf, okf))) return rc;
+    if ((rc = upload(c, p->obs_lm, olm))) return rc;
+    if ((rc = upload(c, p->lm_ptr, lptr))) return rc;
+    if ((rc = upload(c, p->lm_blk, blk))) return rc;
+    if ((rc = upload(c, p->kf_ptr, kptr))) return rc;
+    if ((rc = upload(c, p->kf_obs, kobs))) return rc;
+    if ((rc = upload(c, p->blk_ij, bij))) return rc;
+    if ((rc = upload(c, p->blk_ptr, bptr))) return rc;
+    if ((rc = upload(c, p->pairs, prs))) return rc;
+    if ((rc = upload(c, p->comp_kf_ptr, p->comp_kf_ptr_h))) return rc;
+    if ((rc = upload(c, p->comp_kf, p->comp_kf_h))) return rc;
+    if ((rc = upload(c, p->comp_off, p->comp_off_h))) return rc;
+    if ((rc = upload(c, p->comp_loff, loff))) return rc;
+    if ((rc = upload(c, p->comp_np, p->comp_np_h))) return rc;
+    if ((rc = upload(c, p->comp_hdr, hdr))) return rc;
+    if ((rc = upload(c, p->tl, tlist))) return rc;
+    VX_HIP(c, p->pose.ensure((size_t)nk * 2 * 8 * sizeof(double)));
+    VX_HIP(c, p->lm.ensure((size_t)std::max(n_opt, 1) * 2 * 4 * sizeof(double)));
+    VX_HIP(c, p->wy.ensure((size_t)std::max(p->n_oo, 1) * kWy * sizeof(double)));
+    VX_HIP(c, p->lm_sys.ensure((size_t)std::max(n_opt, 1) * kLmSys * sizeof(double)));
+    // reduction buffer = [component matrices in the factor layout ((np + 16) x np each) | rhs |
+    // D | kf_cost]; unsharded, k_sba_solve factors it in place, sharded it factors the all-reduced copy
+    const size_t red_n = (size_t)p->l_total + (size_t)nk * 14;
+    VX_HIP(c, p->red.ensure(red_n * sizeof(double)));
+    VX_HIP(c, hipMemset(p->red.p, 0, red_n * sizeof(double)));
+    if (p->shard_count > 1) {
+        VX_HIP(c, p->red_sum.ensure(red_n * sizeof(double)));
+        VX_HIP(c, hipMemset(p->red_sum.p, 0, red_n * sizeof(double)));
+    }
+    VX_HIP(c, p->Linv.ensure((size_t)std::max<long long>(p->l_total, 1) * sizeof(double)));
+    VX_HIP(c, p->dx.ensure((size_t)nk * 6 * sizeof(double)));
+    VX_HIP(c, hipMemset(p->dx.p, 0, (size_t)nk * 6 * sizeof(double)));
+    VX_HIP(c, p->state.ensure(sizeof(SBAState)));
+    VX_HIP(c, hipMemset(p->state.p, 0, sizeof(SBAState)));
+    return VX_OK;
+}
+
+size_t solve_lds_bytes(int np) {
+    const int nt = np / 16;  // panel (nt + 1 tiles) | L_kk^-1 | POTRF columns (2 tiles) | y
+    return ((size_t)(nt + 4) * kPanelStride + (size_t)np) * sizeof(double);
+}
+
+int sba_run(vx_ctx* c, vx_sba_plan* p) {
+    if (p->status != 0) {
+        p->ran = true;
+        return VX_OK;
+    }
+    const bool sharded = p->shard_count > 1;
+    if (sharded) {
+#ifndef VX_NO_RCCL
+        if (!c->comm || c->nranks != p->shard_count || c->rank != p->shard_rank)
+            return set_error(c, VX_ERR_STATE, "sharded plan needs vx_comm_init(%d ranks)", p->shard_count);
+#else
+        return set_error(c, VX_ERR_COMM, "built without RCCL");
+#endif
+    }
+    const SBAArgs a = make_args(p);
+    const size_t lds = solve_lds_bytes(p->max_np);
+    if (lds > 64 * 1024)
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_solve),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const int upd_blocks = (std::max(p->n_opt, p->nk) + kUpdThreads - 1) / kUpdThreads;
+    const size_t red_n = (size_t)p->l_total + (size_t)p->nk * 14;
+    for (int it = 0; it < p->opt.max_iterations; ++it) {
+        if (p->n_lm_blocks > 0)
+            VX_HIP(c, launch(c, kStSbaLandmark, k_sba_lm, dim3(p->n_lm_blocks), dim3(kLmThreads), 0, c->stream, a, it));
+        VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks, dim3(p->n_blocks), dim3(kBlkThreads), 0, c->stream, a, it));
+#ifndef VX_NO_RCCL
+        if (sharded) {
+            ProfScope ps(c, kStSbaAllreduce);
+            ncclResult_t r = ncclAllReduce(p->red.p, p->red_sum.p, red_n, ncclDouble, ncclSum, c->comm, c->stream);
+            if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+        }
+#endif
+        VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+                         (uint32_t)lds, c->stream, a, it));
+        VX_HIP(c, launch(c, kStSbaUpdate, k_sba_update, dim3(std::max(upd_blocks, 1)), dim3(kUpdThreads), 0,
+                         c->stream, a, it));
+    }
+    p->ran = true;
+    return VX_OK;
+}
+
+}  // namespace
+}  // namespace vx
+
+using namespace vx;
+
+VX_KT_EXPORT(vx_ktrace_read_sba);
+
+extern "C" {
+
+void vx_sba_default_options(vx_sba_options* o) {
+    if (!o) return;
+    o->window_size = 5;
+    o->max_iterations = 10;
+    o->min_point_observations = 2;
+    o->fixed_keyframes = 2;
+    o->huber_delta = 5.0;
+    o->max_reproj_error = 5.0;
+    o->lambda_init = 1e-4;
+    o->rel_tol = 1e-6;
+}
+
+int vx_sba_plan_create(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_ref, const vx_sba_options* opt,
+                       int shard_rank, int shard_count, vx_sba_plan** out) {
+    if (!c || !out || !opt) return VX_ERR_INVALID;
+    *out = nullptr;
+    if (opt->max_iterations < 0 || opt->max_iterations > kSbaMaxIter)
+        return set_error(c, VX_ERR_INVALID, "max_iterations must be in [0, %d]", kSbaMaxIter);
+    if (opt->fixed_keyframes < 0 || !(opt->lambda_init >= 0.0))
+        return set_error(c, VX_ERR_INVALID, "fixed_keyframes >= 0 and lambda_init >= 0 required");
+    if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count)
+        return set_error(c, VX_ERR_INVALID, "bad shard %d/%d", shard_rank, shard_count);
+    auto* p = new vx_sba_plan();
+    p->c = c;
+    p->opt = *opt;
+    p->shard_rank = shard_rank;
+    p->shard_count = shard_count;
+    const int rc = build_sba_plan(c, m, ref, has_ref, p);
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return VX_OK;
+}
+
+int vx_sba_plan_run_async(vx_ctx* c, vx_sba_plan* p) {
+    if (!c || !p || p->c != c) return VX_ERR_INVALID;
+    return sba_run(c, p);
+}
+
+int vx_sba_plan_fetch(vx_ctx* c, vx_sba_plan* p, vx_map_view* m, vx_sba_stats* st) {
+    if (!c || !p || p->c != c) return VX_ERR_INVALID;
+    if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
+    vx_sba_stats s{};
+    s.status = p->status;
+    s.n_window_kf = p->n_window_kf;
+    s.n_landmarks = p->n_landmarks_global;
+    if (p->status == 0 && p->opt.max_iterations > 0) {
+        SBAState hs;
+        VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+        const LMVars v = hs.lm[hs.iterations & 1];
+        std::vector<double> pose((size_t)p->nk * 8), lm((size_t)std::max(p->n_opt, 1) * 4);
+        const double* ps = v.sel < 0 ? p->pose0.as<double>() : p->pose.as<double>() + (size_t)v.sel * p->nk * 8;
+        const double* ls = v.sel < 0 ? p->lm0.as<double>() : p->lm.as<double>() + (size_t)v.sel * p->n_opt * 4;
+        VX_HIP(c, hipMemcpyAsync(pose.data(), ps, pose.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        if (p->n_opt > 0)
+            VX_HIP(c, hipMemcpyAsync(lm.data(), ls, (size_t)p->n_opt * 4 * sizeof(double), hipMemcpyDeviceToHost,
+                                     c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+        if (c->prof) prof_collect(c);
+        s.iterations = hs.iterations;
+        s.accepted = v.accepted;
+        s.lambda = v.lambda;
+        s.initial_cost = hs.initial_cost;
+        s.final_cost = v.best_cost;
+        for (int i = 0; i < 16; ++i) {
+            s.cost[i] = hs.cost[i];
+            s.obs[i] = hs.obs[i];
+            s.step[i] = hs.step[i];
+        }
+        if (m) {
+            for (int r = 0; r < p->nk; ++r)
+                for (int j = 0; j < 7; ++j) m->kf_pose[7 * p->kf_map_idx[r] + j] = pose[8 * r + j];
+            for (int sl = 0; sl < p->n_opt; ++sl)
+                for (int j = 0; j < 3; ++j) m->lm_pos[3 * p->lm_map_idx[sl] + j] = lm[4 * sl + j];
+        }
+    }
+    if (st) *st = s;
+    return VX_OK;
+}
+
+void vx_sba_plan_destroy(vx_sba_plan* p) { delete p; }
+
+int vx_sba_plan_info(const vx_sba_plan* p, int64_t* out8) {
+    if (!p || !out8) return VX_ERR_INVALID;
+    const int64_t v[8] = {p->nk, p->n_opt, p->n_obs, p->n_pairs, p->n_blocks, 6 * (int64_t)p->nk,
+                          p->n_lfactor_tiles, p->n_comp};
+    for (int i = 0; i < 8; ++i) out8[i] = v[i];
+    return VX_OK;
+}
+
+int vx_sba_plan_system(vx_ctx* c, vx_sba_plan* p, double* S, double* rhs, int n) {
+    if (!c || !p || p->c != c || !S || !rhs) return VX_ERR_INVALID;
+    if (p->status != 0) return set_error(c, VX_ERR_STATE, "empty plan");
+    if (n != 6 * p->nk) return set_error(c, VX_ERR_INVALID, "n must be %d", 6 * p->nk);
+    if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
+    const size_t red_n = (size_t)p->l_total + (size_t)p->nk * 14;
+    std::vector<double> h(red_n);
+    const void* src = p->shard_count > 1 ? p->red_sum.p : p->red.p;
+    VX_HIP(c, hipMemcpyAsync(h.data(), src, red_n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    SBAState hs;
+    VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    const int n6 = 6 * p->nk;
+    // the damping of the last assembly: lambda of lm[(iterations - 1) & 1] (lambda0 at iteration 0)
+    const double lambda = hs.iterations <= 1 ? p->opt.lambda_init : hs.lm[(hs.iterations - 1) & 1].lambda;
+    const double* rh = h.data() + p->l_total;
+    std::memset(S, 0, sizeof(double) * (size_t)n * n);
+    std::vector<int> comp_of(p->nk, -1), local(p->nk, 0);
+    for (int cc = 0; cc < p->n_comp; ++cc)
+        for (int q = p->comp_kf_ptr_h[cc]; q < p->comp_kf_ptr_h[cc + 1]; ++q) {
+            comp_of[p->comp_kf_h[q]] = cc;
+            local[p->comp_kf_h[q]] = q - p->comp_kf_ptr_h[cc];
+        }
+    for (int i = 0; i < p->nk; ++i) {
+        const int ci = comp_of[i];
+        for (int a2 = 0; a2 < 6; ++a2) rhs[6 * i + a2] = ci < 0 ? 0.0 : rh[6 * i + a2];
+        if (ci < 0) {
+            for (int a2 = 0; a2 < 6; ++a2) S[(size_t)(6 * i + a2) * (n + 1)] = 1.0;
+            continue;
+        }
+        for (int j = 0; j <= i; ++j) {
+            if (comp_of[j] != ci) continue;
+            const int np = p->comp_np_h[ci];
+            const double* B = h.data() + p->comp_loff_h[ci] + (size_t)(6 * local[i]) * np + 6 * local[j];
+            for (int r = 0; r < 6; ++r)
+                for (int cc = 0; cc < 6; ++cc) {
+                    double v = B[(size_t)r * np + cc];
+                    if (i == j && r == cc) v += lambda * rh[n6 + 6 * i + r] + 1e-6;
+                    S[(size_t)(6 * i + r) * n + 6 * j + cc] = v;
+                }
+        }
+    }
+    return VX_OK;
+}
+
+int vx_sba_optimize_map(vx_ctx* c, vx_map_view* m, uint64_t ref, int has_ref, const vx_sba_options* opt,
+                        vx_sba_stats* st) {
+    vx_sba_plan* p = nullptr;
+    int rc = vx_sba_plan_create(c, m, ref, has_ref, opt, 0, 1, &p);
+    if (rc) return rc;
+    rc = vx_sba_plan_run_async(c, p);
+    if (!rc) rc = vx_sba_plan_fetch(c, p, m, st);
+    (void)hipStreamSynchronize(c->stream);
+    vx_sba_plan_destroy(p);
+    return rc;
+}
+
+}  // extern "C"

@@ -37,6 +37,11 @@ enum Stage : int {
     kStBaSolve,
     kStBaLandmark,
     kStPyramid,
+    kStSbaLandmark,
+    kStSbaBlocks,
+    kStSbaSolve,
+    kStSbaUpdate,
+    kStSbaAllreduce,
     kStCount
 };
 

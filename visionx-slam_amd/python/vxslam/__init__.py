@@ -59,6 +59,20 @@ class BAStats(C.Structure):
                 ("status", C.c_int32)]
 
 
+class SBAOptions(C.Structure):
+    _fields_ = [("window_size", C.c_int32), ("max_iterations", C.c_int32),
+                ("min_point_observations", C.c_int32), ("fixed_keyframes", C.c_int32),
+                ("huber_delta", C.c_double), ("max_reproj_error", C.c_double),
+                ("lambda_init", C.c_double), ("rel_tol", C.c_double)]
+
+
+class SBAStats(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("accepted", C.c_int32), ("n_window_kf", C.c_int32),
+                ("n_landmarks", C.c_int32), ("cost", C.c_double * 16), ("obs", C.c_int32 * 16),
+                ("step", C.c_int32 * 16), ("lambda_", C.c_double), ("initial_cost", C.c_double),
+                ("final_cost", C.c_double), ("status", C.c_int32)]
+
+
 EXPORTS = [
     "vx_version", "vx_create", "vx_destroy", "vx_last_error", "vx_stream", "vx_synchronize",
     "vx_stream_wait_ctx", "vx_event_create", "vx_event_record", "vx_event_wait", "vx_event_destroy",
@@ -67,7 +81,9 @@ EXPORTS = [
     "vx_match_device_async", "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
     "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info",
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
-    "vx_prof_read",
+    "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
+    "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
+    "vx_sba_optimize_map",
 ]
 
 _lib = None
@@ -106,6 +122,9 @@ def lib():
         L.vx_ba_plan_destroy.restype = None
         L.vx_orb_default_params.restype = None
         L.vx_ba_default_options.restype = None
+        L.vx_sba_plan_destroy.argtypes = [C.c_void_p]
+        L.vx_sba_plan_destroy.restype = None
+        L.vx_sba_default_options.restype = None
         L.vx_ba_shard_of.restype = C.c_uint32
         L.vx_ba_shard_of.argtypes = [C.c_uint64, C.c_int]
         _lib = L
@@ -123,6 +142,11 @@ def default_orb_params(n_features=1000, scale_factor=1.2, n_levels=8, fast_thres
 
 def default_ba_options(window=5, iters=5, min_pose=20, min_point=2, huber=5.0, max_err=5.0):
     return BAOptions(window, iters, min_pose, min_point, huber, max_err)
+
+
+def default_sba_options(window=5, iters=10, min_point=2, fixed=2, huber=5.0, max_err=5.0, lam=1e-4,
+                        rel_tol=1e-6):
+    return SBAOptions(window, iters, min_point, fixed, huber, max_err, lam, rel_tol)
 
 
 def map_view(m) -> MapView:
@@ -312,6 +336,19 @@ class Context:
     def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1):
         return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
 
+    def sba_optimize(self, m, opts: SBAOptions | None = None, ref_kf_id=None) -> SBAStats:
+        """Schur-complement joint BA (vx_sba_optimize_map) on a synth.BAMap, in place."""
+        opts = opts or default_sba_options(window=m.get("window", 5))
+        ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+        v = map_view(m)
+        st = SBAStats()
+        self._check(lib().vx_sba_optimize_map(self._h, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
+                                              0 if ref is None else 1, C.byref(opts), C.byref(st)))
+        return st
+
+    def sba_plan(self, m, opts: SBAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1):
+        return SBAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
+
     # ---------------------------------------------------------------- multi-GPU
     @staticmethod
     def comm_unique_id() -> bytes:
@@ -381,6 +418,55 @@ class BAPlan:
     def close(self):
         if self._h:
             lib().vx_ba_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class SBAPlan:
+    """vx_sba_plan: Schur-complement joint BA plan (window, observation / block / pair tables)."""
+
+    def __init__(self, ctx: Context, m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1):
+        self.ctx = ctx
+        self.opts = opts or default_sba_options(window=m.get("window", 5))
+        ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
+        self._h = C.c_void_p()
+        v = map_view(m)
+        ctx._check(lib().vx_sba_plan_create(ctx.handle, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
+                                            0 if ref is None else 1, C.byref(self.opts), shard_rank,
+                                            shard_count, C.byref(self._h)))
+
+    def info(self):
+        out = np.zeros(8, np.int64)
+        assert lib().vx_sba_plan_info(self._h, _p(out)) == 0
+        keys = ["n_kf", "n_opt", "n_obs", "n_pairs", "n_blocks", "n", "n_tiles", "n_comp"]
+        return {k: int(v) for k, v in zip(keys, out)}
+
+    def run_async(self):
+        self.ctx._check(lib().vx_sba_plan_run_async(self.ctx.handle, self._h))
+
+    def fetch(self, m=None) -> SBAStats:
+        st = SBAStats()
+        v = map_view(m) if m is not None else None
+        self.ctx._check(lib().vx_sba_plan_fetch(self.ctx.handle, self._h, C.byref(v) if v is not None else None,
+                                                C.byref(st)))
+        return st
+
+    def system(self):
+        """(S, rhs) of the last assembly (lower triangle of S meaningful, damping included)."""
+        n = self.info()["n"]
+        S = np.zeros((n, n))
+        rhs = np.zeros(n)
+        self.ctx._check(lib().vx_sba_plan_system(self.ctx.handle, self._h, _p(S), _p(rhs), n))
+        return S, rhs
+
+    def close(self):
+        if self._h:
+            lib().vx_sba_plan_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):
