@@ -16,6 +16,10 @@
  *   vx_ba_optimize_map    <- LocalBA::Optimize(map, ref_kf)      core/backend/local_ba.h:23,
  *                                                                local_ba.cpp:66-249
  *                            LocalBA::Options                    core/backend/local_ba.h:12-19
+ *   vx_depth_landmarks    <- Tracking::CreateLandmarksFromDepth  core/frontend/tracking.cpp:586-650
+ *   vx_triangulate        <- Tracking::TriangulateWithLastKeyFrame + TriangulatePoint
+ *                                                                core/frontend/tracking.cpp:856-945
+ *   vx_sba_*              (no reference counterpart: north_star's Schur-complement dense solve)
  *
  * The host-side C++ adapters that keep the reference call surface (same class names and
  * signatures) are in visionx-slam_amd/host/; the bindings a reference maintainer adds are in
@@ -249,6 +253,36 @@ int vx_sba_plan_info(const vx_sba_plan* plan, int64_t* out8);
 int vx_sba_plan_system(vx_ctx* ctx, vx_sba_plan* plan, double* S, double* rhs, int n);
 int vx_sba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                         const vx_sba_options* opt, vx_sba_stats* stats);
+
+/* ---------------------------------------------------------------- landmark creation
+ * The two loops Tracking::CreateKeyFrame runs on every new keyframe right before LocalBA
+ * (core/frontend/tracking.cpp:577-580).  Both return the created landmarks in input order (the
+ * order landmark_id_++ numbers them): out_index[i] = rank of item i among the created ones or -1,
+ * out_pw[3 * rank ..] = its world position; *n_created = count.  The caller creates the Landmark
+ * objects, adds the observations and sets Feature::landmark_id_ / has_landmark / is_outlier
+ * exactly as the reference loop body does. */
+#define VX_DEPTH_U16 0   /* CV_16U, metres * 5000 (TUM; kDepthScale, tracking.cpp:601) */
+#define VX_DEPTH_F32 1   /* CV_32F metres */
+#define VX_DEPTH_F64 2   /* CV_64F metres */
+
+/* <- Tracking::CreateLandmarksFromDepth(frame) (tracking.cpp:586-650): features without a
+ * landmark, depth at (int)(x + 0.5), (int)(y + 0.5), 0.1 <= d <= 10 m, pw = T_cw^-1 * pixelToCamera.
+ * feat_uv: 2 per feature (Feature::position); intr4: fx fy cx cy; pose7: T_cw (qx qy qz qw tx ty tz).
+ * depth == NULL (Depth().empty()) creates nothing. */
+int vx_depth_landmarks(vx_ctx* ctx, const double* feat_uv, const uint8_t* feat_has_lm, int n_feat,
+                       const void* depth, int depth_type, int rows, int cols, int64_t row_stride,
+                       const double* intr4, const double* pose7, int32_t* out_index, double* out_pw,
+                       int* n_created);
+/* <- Tracking::TriangulateWithLastKeyFrame(last, curr) + TriangulatePoint (tracking.cpp:856-945)
+ * over the matches Match(last, curr) returned (query = last frame, train = current frame; query
+ * indices unique): parallax >= min_angle_deg, 4x4 DLT null vector, reprojection <= max_reproj_error
+ * in both views; a train feature triangulated by an earlier match is skipped (the reference sets
+ * has_landmark as it goes).  Options: Tracking::Options (tracking.h:43-44), 5.0 px / 1.0 deg. */
+int vx_triangulate(vx_ctx* ctx, const double* uv1, const uint8_t* has1, int n1, const double* intr1,
+                   const double* pose1, const double* uv2, const uint8_t* has2, int n2,
+                   const double* intr2, const double* pose2, const vx_match* matches, int n_matches,
+                   double min_angle_deg, double max_reproj_error, int32_t* out_index, double* out_pw,
+                   int* n_created);
 
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);

@@ -145,6 +145,16 @@ int orc_sba_optimize_map(orc_map_view* map, uint64_t ref_kf_id, int has_ref,
 int orc_sba_system(const orc_map_view* map, uint64_t ref_kf_id, int has_ref,
                    const orc_sba_options* opt, double lambda, double* S, double* rhs, int n);
 
+/* ---- keyframe-insertion landmark creation (landmark_oracle.cpp), same contract as vx_slam.h */
+int orc_depth_landmarks(const double* feat_uv, const uint8_t* feat_has_lm, int n_feat, const void* depth,
+                        int depth_type /* 0 u16, 1 f32, 2 f64 */, int rows, int cols, int64_t row_stride,
+                        const double* intr4, const double* pose7, int32_t* out_index, double* out_pw,
+                        int* n_created);
+int orc_triangulate(const double* uv1, const uint8_t* has1, int n1, const double* intr1, const double* pose1,
+                    const double* uv2, const uint8_t* has2, int n2, const double* intr2, const double* pose2,
+                    const orc_match* matches, int n_matches, double min_angle_deg, double max_reproj_error,
+                    int32_t* out_index, double* out_pw, int* n_created);
+
 #ifdef __cplusplus
 }
 #endif

@@ -264,3 +264,43 @@ def sba_system(m, opts=None, lam=None, ref_kf_id=None):
         return None
     assert rc == 0, rc
     return S, rhs
+
+
+# ---------------------------------------------------------------------------- landmark creation
+DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
+
+
+def depth_landmarks(uv, has, depth, intr, pose):
+    """CreateLandmarksFromDepth restated: (index per feature, created points)."""
+    uv = np.ascontiguousarray(uv, np.float64)
+    has = np.ascontiguousarray(has, np.uint8)
+    n = len(has)
+    idx = np.full(max(n, 1), -1, np.int32)
+    pw = np.zeros((max(n, 1), 3))
+    cnt = C.c_int(0)
+    if depth is None:
+        dptr, dt, rows, cols, stride = None, 0, 0, 0, 0
+    else:
+        depth = np.ascontiguousarray(depth)
+        dptr, dt, rows, cols, stride = _p(depth), DEPTH_TYPES[depth.dtype], depth.shape[0], depth.shape[1], depth.strides[0]
+    intr = np.ascontiguousarray(intr, np.float64)
+    pose = np.ascontiguousarray(pose, np.float64)
+    assert lib().orc_depth_landmarks(_p(uv), _p(has), n, dptr, dt, rows, cols, C.c_int64(stride), _p(intr),
+                                     _p(pose), _p(idx), _p(pw), C.byref(cnt)) == 0
+    return idx[:n].copy(), pw[:cnt.value].copy()
+
+
+def triangulate(d, min_angle_deg=1.0, max_err=5.0, intr1=None, intr2=None):
+    """TriangulateWithLastKeyFrame restated on a synth.make_keyframe_pair dict."""
+    m = np.ascontiguousarray(d["matches"])
+    nm = len(m)
+    idx = np.full(max(nm, 1), -1, np.int32)
+    pw = np.zeros((max(nm, 1), 3))
+    cnt = C.c_int(0)
+    i1 = np.ascontiguousarray(d["intr"] if intr1 is None else intr1, np.float64)
+    i2 = np.ascontiguousarray(d["intr"] if intr2 is None else intr2, np.float64)
+    rc = lib().orc_triangulate(_p(d["uv1"]), _p(d["has1"]), len(d["has1"]), _p(i1), _p(d["pose1"]),
+                               _p(d["uv2"]), _p(d["has2"]), len(d["has2"]), _p(i2), _p(d["pose2"]), _p(m), nm,
+                               C.c_double(min_angle_deg), C.c_double(max_err), _p(idx), _p(pw), C.byref(cnt))
+    assert rc == 0, rc
+    return idx[:nm].copy(), pw[:cnt.value].copy()

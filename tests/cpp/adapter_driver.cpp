@@ -5,14 +5,20 @@
 //   adapter_driver extract <img.bin> <h> <w> <c> <n_features> <out_prefix>
 //   adapter_driver match <q.bin> <nq> <t.bin> <nt> <out.bin>
 //   adapter_driver ba <dir> <window> <iters> <ref_id or -1> [flatten]
+//   adapter_driver depth <dir>                     (KeyFrameLandmarks::CreateLandmarksFromDepth)
+//   adapter_driver triangulate <dir> <min_deg> <max_err>   (TriangulateWithLastKeyFrame)
 #include <cstdio>
 #include <cstdlib>
+#include <climits>
+#include <cstdint>
 #include <fstream>
+#include <map>
 #include <iostream>
 #include <string>
 #include <vector>
 
 #include "visionx/feature.h"
+#include "visionx/mapping.h"
 
 using namespace visionx;
 
@@ -160,6 +166,99 @@ static int cmd_ba(int argc, char** a) {
     return 0;
 }
 
+// Frame with the features of <dir>/<pfx>uv.bin / <pfx>has.bin, the pose <pfx>pose.bin (7) and the
+// camera intr.bin (4)
+static Frame::Ptr frame_from(const std::string& dir, const std::string& pfx, uint64_t id) {
+    const auto uv = read_bin<double>(dir + "/" + pfx + "uv.bin");
+    const auto has = read_bin<uint8_t>(dir + "/" + pfx + "has.bin");
+    const auto pose = read_bin<double>(dir + "/" + pfx + "pose.bin");
+    const auto in = read_bin<double>(dir + "/intr.bin");
+    auto cam = std::make_shared<Camera>(in[0], in[1], in[2], in[3]);
+    DepthImage depth;
+    std::ifstream meta(dir + "/" + pfx + "depth_meta.txt");
+    if (meta) {
+        meta >> depth.rows >> depth.cols >> depth.type >> depth.step;
+        depth.data = read_bin<uint8_t>(dir + "/" + pfx + "depth.bin");
+    }
+    auto fr = std::make_shared<Frame>(id, 0.0, cam, ImageU8(), depth);
+    SE3d T;
+    T.qx = pose[0]; T.qy = pose[1]; T.qz = pose[2]; T.qw = pose[3];
+    T.tx = pose[4]; T.ty = pose[5]; T.tz = pose[6];
+    fr->SetPose(T);
+    for (size_t i = 0; i < has.size(); ++i) {
+        Feature f;
+        f.position = Vec2d(uv[2 * i], uv[2 * i + 1]);
+        f.has_landmark = has[i] != 0;
+        f.landmark_id_ = has[i] ? 999999999ull : 0;
+        fr->Features().push_back(f);
+    }
+    return fr;
+}
+
+// writes, per frame, every feature's landmark id (UINT64_MAX without) and the map's landmarks
+// (id, x, y, z) in id order
+static void dump_landmarks(const std::string& dir, const Map& map, const std::vector<Frame::Ptr>& frames) {
+    for (size_t k = 0; k < frames.size(); ++k) {
+        std::vector<uint64_t> ids;
+        for (const auto& f : frames[k]->Features()) ids.push_back(f.has_landmark ? f.landmark_id_ : UINT64_MAX);
+        write_bin(dir + "/feat_lm" + std::to_string(k) + ".out", ids);
+    }
+    std::map<uint64_t, Landmark::Ptr> by_id(map.Landmarks().begin(), map.Landmarks().end());
+    std::vector<double> out;
+    for (const auto& kv : by_id) {
+        const Vec3d p = kv.second->Position();
+        out.insert(out.end(), {(double)kv.first, p.x, p.y, p.z, (double)kv.second->ObservationCount()});
+    }
+    write_bin(dir + "/landmarks.out", out);
+    std::printf("%zu\n", by_id.size());
+}
+
+static int cmd_depth(char** a) {
+    const std::string dir = a[0];
+    auto map = std::make_shared<Map>();
+    auto fr = frame_from(dir, "", 7);
+    KeyFrameLandmarks kl(map, std::make_shared<ORBMatcher>(), KeyFrameLandmarks::Options());
+    kl.landmark_id_ = 100;
+    kl.CreateLandmarksFromDepth(fr);
+    dump_landmarks(dir, *map, {fr});
+    return 0;
+}
+
+// Match() replaced by the list in matches.bin (what ORBMatcher returned for the pair)
+class FixedMatcher : public FeatureMatcher {
+public:
+    explicit FixedMatcher(std::vector<DMatch> m) : m_(std::move(m)) {}
+    int Match(const Frame::Ptr&, const Frame::Ptr&, std::vector<DMatch>& matches) override {
+        matches = m_;
+        return (int)m_.size();
+    }
+
+private:
+    std::vector<DMatch> m_;
+};
+
+static int cmd_triangulate(char** a) {
+    const std::string dir = a[0];
+    const auto raw = read_bin<int32_t>(dir + "/matches.bin");  // (query, train, distance bits) triples
+    std::vector<DMatch> m;
+    for (size_t k = 0; k + 2 < raw.size(); k += 3) {
+        DMatch d;
+        d.queryIdx = raw[k];
+        d.trainIdx = raw[k + 1];
+        m.push_back(d);
+    }
+    auto map = std::make_shared<Map>();
+    auto f1 = frame_from(dir, "f1_", 3), f2 = frame_from(dir, "f2_", 5);
+    KeyFrameLandmarks::Options o;
+    o.triangulation_min_angle_deg = std::atof(a[1]);
+    o.triangulation_max_reproj_error = std::atof(a[2]);
+    KeyFrameLandmarks kl(map, std::make_shared<FixedMatcher>(m), o);
+    kl.landmark_id_ = 100;
+    kl.TriangulateWithLastKeyFrame(f1, f2);
+    dump_landmarks(dir, *map, {f1, f2});
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     const std::string cmd = argv[1];
@@ -167,6 +266,8 @@ int main(int argc, char** argv) {
         if (cmd == "extract" && argc >= 8) return cmd_extract(argv + 2);
         if (cmd == "match" && argc >= 7) return cmd_match(argv + 2);
         if (cmd == "ba" && argc >= 6) return cmd_ba(argc - 2, argv + 2);
+        if (cmd == "depth" && argc >= 3) return cmd_depth(argv + 2);
+        if (cmd == "triangulate" && argc >= 5) return cmd_triangulate(argv + 2);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;

@@ -106,3 +106,57 @@ def test_adapter_local_ba(driver, oracle, tmp_path):
             a[a[:, 3] < 0, :4] *= -1
             b[b[:, 3] < 0, :4] *= -1
         assert (np.abs(a - b) / np.maximum(np.abs(b), 1e-3)).max() <= 1e-4
+
+
+def _dump_frame(d, pfx, uv, has, pose):
+    np.ascontiguousarray(uv, np.float64).tofile(os.path.join(d, pfx + "uv.bin"))
+    np.ascontiguousarray(has, np.uint8).tofile(os.path.join(d, pfx + "has.bin"))
+    np.ascontiguousarray(pose, np.float64).tofile(os.path.join(d, pfx + "pose.bin"))
+
+
+def _read_landmarks(d, n_frames):
+    lm = np.fromfile(os.path.join(d, "landmarks.out"), np.float64).reshape(-1, 5)
+    feats = [np.fromfile(os.path.join(d, f"feat_lm{k}.out"), np.uint64) for k in range(n_frames)]
+    return lm, feats
+
+
+@pytest.mark.gpu
+def test_adapter_depth_landmarks(driver, oracle, tmp_path):
+    """KeyFrameLandmarks::CreateLandmarksFromDepth (tracking.cpp:586-650): ids 100.. in feature
+    order, one observation each, feature flags set; positions equal to the restatement."""
+    kp = synth.make_keyframe_pair(41, 1500)
+    d = str(tmp_path)
+    _dump_frame(d, "", kp["uv2"], kp["has2"], kp["pose2"])
+    kp["intr"].tofile(os.path.join(d, "intr.bin"))
+    kp["depth"].tofile(os.path.join(d, "depth.bin"))
+    open(os.path.join(d, "depth_meta.txt"), "w").write(f"480 640 0 {640 * 2}\n")
+    run(driver, "depth", d)
+    lm, (feat,) = _read_landmarks(d, 1)
+    idx, pw = oracle.depth_landmarks(kp["uv2"], kp["has2"], kp["depth"], kp["intr"], kp["pose2"])
+    made = np.nonzero(idx >= 0)[0]
+    assert len(lm) == len(made) == len(pw)
+    assert np.array_equal(lm[:, 0], 100 + np.arange(len(made)))
+    assert np.array_equal(lm[:, 1:4], pw) and (lm[:, 4] == 1).all()
+    assert np.array_equal(feat[made], (100 + idx[made]).astype(np.uint64))
+
+
+@pytest.mark.gpu
+def test_adapter_triangulate(driver, oracle, tmp_path):
+    """KeyFrameLandmarks::TriangulateWithLastKeyFrame (tracking.cpp:856-929) over a fixed match
+    list: ids in match order, two observations each, both features marked."""
+    kp = synth.make_keyframe_pair(42, 1500, frac_dup_train=0.1)
+    d = str(tmp_path)
+    _dump_frame(d, "f1_", kp["uv1"], kp["has1"], kp["pose1"])
+    _dump_frame(d, "f2_", kp["uv2"], kp["has2"], kp["pose2"])
+    kp["intr"].tofile(os.path.join(d, "intr.bin"))
+    m = kp["matches"]
+    np.stack([m["query_idx"], m["train_idx"], np.zeros(len(m), np.int32)], -1).astype(np.int32).tofile(
+        os.path.join(d, "matches.bin"))
+    run(driver, "triangulate", d, 1.0, 5.0)
+    lm, (f1, f2) = _read_landmarks(d, 2)
+    idx, pw = oracle.triangulate(kp, 1.0, 5.0)
+    made = np.nonzero(idx >= 0)[0]
+    assert len(lm) == len(made) and len(made) > 50
+    assert np.abs(lm[:, 1:4] - pw).max() <= 1e-9 * np.abs(pw).max() and (lm[:, 4] == 2).all()
+    assert np.array_equal(f1[m["query_idx"][made]], (100 + idx[made]).astype(np.uint64))
+    assert np.array_equal(f2[m["train_idx"][made]], (100 + idx[made]).astype(np.uint64))

@@ -78,7 +78,8 @@ static const char* kStageNames[vx::kStCount] = {
     "orb_gray",       "orb_resize",    "orb_fast_harris", "orb_select",  "orb_blur",
     "orb_describe",   "match_partial", "match_merge",     "ba_reset",    "ba_pose_partial",
     "ba_pose_sum",    "ba_allreduce",  "ba_pose_solve",   "ba_landmark",    "orb_pyramid",
-    "sba_landmark",   "sba_blocks",    "sba_solve",       "sba_update",     "sba_allreduce"};
+    "sba_landmark",   "sba_blocks",    "sba_solve",       "sba_update",     "sba_allreduce",
+    "lm_depth",       "lm_triangulate", "lm_compact"};
 
 extern "C" {
 

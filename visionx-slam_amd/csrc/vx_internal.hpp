@@ -42,6 +42,9 @@ enum Stage : int {
     kStSbaSolve,
     kStSbaUpdate,
     kStSbaAllreduce,
+    kStLmDepth,
+    kStLmTriangulate,
+    kStLmCompact,
     kStCount
 };
 
@@ -162,6 +165,9 @@ struct vx_ctx {
     vx::PinnedBuf host_stage;
     int match_cap = 0;
     bool match_valid = false;
+
+    // ---- landmark creation (landmarks.hip): inputs, per-item flags / points, compacted outputs
+    vx::DevBuf lm_in0, lm_in1, lm_in2, lm_in3, lm_in4, lm_depth, lm_valid, lm_pw, lm_index, lm_out, lm_count, lm_aux;
 
     // ---- profiling
     bool prof = false;

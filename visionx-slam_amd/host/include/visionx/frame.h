@@ -40,7 +40,7 @@ class Frame {  // frame.h:25-64
 public:
     using Ptr = std::shared_ptr<Frame>;
     Frame(uint64_t id, double timestamp, std::shared_ptr<Camera> camera, const ImageU8& image,
-          const ImageU8& depth = ImageU8())
+          const DepthImage& depth = DepthImage())
         : id_(id), timestamp_(timestamp), camera_(std::move(camera)), image_(image), depth_(depth) {}
 
     SE3d Pose() const {
@@ -54,7 +54,7 @@ public:
     uint64_t Id() const { return id_; }
     double Timestamp() const { return timestamp_; }
     const ImageU8& Image() const { return image_; }
-    const ImageU8& Depth() const { return depth_; }
+    const DepthImage& Depth() const { return depth_; }
     std::vector<Feature>& Features() { return features_; }
     const std::vector<Feature>& Features() const { return features_; }
     DescriptorMat& Descriptors() { return descriptors_; }
@@ -68,7 +68,7 @@ private:
     mutable std::mutex pose_mutex_;
     std::shared_ptr<Camera> camera_;
     ImageU8 image_;
-    ImageU8 depth_;
+    DepthImage depth_;
     std::vector<Feature> features_;
     DescriptorMat descriptors_;
 };

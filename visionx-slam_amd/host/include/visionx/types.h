@@ -3,6 +3,7 @@
 //   Vec2d / Vec3d      <- Eigen::Vector2d / Eigen::Vector3d   (frame.h:18, landmark.h:18)
 //   SE3d               <- Sophus::SE3d (unit quaternion x y z w + translation), T_cw
 //   ImageU8            <- cv::Mat 8UC1 / 8UC3 (frame.h:38), row-major, owned
+//   DepthImage         <- cv::Mat CV_16U / CV_32F / CV_64F depth (frame.h:39, tracking.cpp:610-623)
 //   DescriptorMat      <- cv::Mat N x 32 CV_8U (frame.h:43-44)
 //   DMatch             <- cv::DMatch (feature_matcher.h:12)
 #pragma once
@@ -45,6 +46,15 @@ struct ImageU8 {
     std::vector<uint8_t> data;  // rows * cols * channels, row-major
     bool empty() const { return data.empty(); }
     size_t step() const { return (size_t)cols * channels; }
+    const uint8_t* ptr() const { return data.data(); }
+};
+
+struct DepthImage {
+    int rows = 0, cols = 0;
+    int type = 0;                // 0 CV_16U (metres * 5000), 1 CV_32F, 2 CV_64F (vx_slam.h VX_DEPTH_*)
+    size_t step = 0;             // bytes per row
+    std::vector<uint8_t> data;   // rows * step
+    bool empty() const { return data.empty(); }
     const uint8_t* ptr() const { return data.data(); }
 };
 

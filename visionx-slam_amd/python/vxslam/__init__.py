@@ -83,8 +83,10 @@ EXPORTS = [
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
-    "vx_sba_optimize_map",
+    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate",
 ]
+
+DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
 
 _lib = None
 
@@ -335,6 +337,42 @@ class Context:
 
     def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1):
         return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
+
+    # ---------------------------------------------------------------- landmark creation
+    def depth_landmarks(self, uv, has, depth, intr, pose):
+        """Tracking::CreateLandmarksFromDepth on the GPU: (index per feature or -1, created points)."""
+        uv = np.ascontiguousarray(uv, np.float64)
+        has = np.ascontiguousarray(has, np.uint8)
+        n = len(has)
+        idx = np.full(max(n, 1), -1, np.int32)
+        pw = np.zeros((max(n, 1), 3))
+        cnt = C.c_int(0)
+        if depth is None:
+            dptr, dt, rows, cols, stride = None, 0, 0, 0, 0
+        else:
+            depth = np.ascontiguousarray(depth)
+            dptr, dt = _p(depth), DEPTH_TYPES[depth.dtype]
+            rows, cols, stride = depth.shape[0], depth.shape[1], depth.strides[0]
+        intr = np.ascontiguousarray(intr, np.float64)
+        pose = np.ascontiguousarray(pose, np.float64)
+        self._check(lib().vx_depth_landmarks(self._h, _p(uv), _p(has), n, dptr, dt, rows, cols, C.c_int64(stride),
+                                             _p(intr), _p(pose), _p(idx), _p(pw), C.byref(cnt)))
+        return idx[:n].copy(), pw[:cnt.value].copy()
+
+    def triangulate(self, d, min_angle_deg=1.0, max_err=5.0, intr1=None, intr2=None):
+        """Tracking::TriangulateWithLastKeyFrame on the GPU for a synth.make_keyframe_pair dict."""
+        m = np.ascontiguousarray(d["matches"])
+        nm = len(m)
+        idx = np.full(max(nm, 1), -1, np.int32)
+        pw = np.zeros((max(nm, 1), 3))
+        cnt = C.c_int(0)
+        i1 = np.ascontiguousarray(d["intr"] if intr1 is None else intr1, np.float64)
+        i2 = np.ascontiguousarray(d["intr"] if intr2 is None else intr2, np.float64)
+        self._check(lib().vx_triangulate(self._h, _p(d["uv1"]), _p(d["has1"]), len(d["has1"]), _p(i1),
+                                         _p(d["pose1"]), _p(d["uv2"]), _p(d["has2"]), len(d["has2"]), _p(i2),
+                                         _p(d["pose2"]), _p(m), nm, C.c_double(min_angle_deg), C.c_double(max_err),
+                                         _p(idx), _p(pw), C.byref(cnt)))
+        return idx[:nm].copy(), pw[:cnt.value].copy()
 
     def sba_optimize(self, m, opts: SBAOptions | None = None, ref_kf_id=None) -> SBAStats:
         """Schur-complement joint BA (vx_sba_optimize_map) on a synth.BAMap, in place."""

@@ -271,3 +271,72 @@ def ba_config(name: str):
     """(n_kf, n_lm, n_streams) of the BASELINE.json configs."""
     return {"C2": (10, 2000, 1), "C3": (50, 20000, 1), "C4": (100, 50000, 1),
             "C5": (200, 100000, 8)}[name]
+
+
+def make_keyframe_pair(seed: int, n: int = 2000, *, width: int = 640, height: int = 480, intr=(FX, FY, CX, CY),
+                       baseline_m: float = 0.08, yaw_deg: float = 1.5, noise_px: float = 0.3,
+                       frac_has: float = 0.1, frac_bad_match: float = 0.1, frac_dup_train: float = 0.03,
+                       depth_type: str = "u16"):
+    """Two keyframes seeing a common set of points, for Tracking::CreateKeyFrame's landmark
+    creation (tracking.cpp:577-580): per frame Feature positions and has_landmark flags, T_cw poses,
+    a depth image of the second frame (TUM u16 metres * 5000, with holes and out-of-range pixels)
+    and the match list Match(last, curr) would return (query = last frame, unique queries; some
+    wrong / duplicated train indices).  Returns a dict of numpy arrays."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = intr
+    # points in front of camera 1
+    u = rng.uniform(5, width - 5, n)
+    v = rng.uniform(5, height - 5, n)
+    z = rng.uniform(0.6, 6.0, n)
+    pc1 = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], -1)
+    q1 = quat_from_rotvec(rng.normal(0, 0.02, 3))
+    t1 = rng.normal(0, 0.1, 3)
+    R1 = quat_to_mat(q1)
+    pw = (pc1 - t1) @ R1  # R1^T (pc - t)
+    q12 = quat_from_rotvec(np.array([0.0, np.deg2rad(yaw_deg), 0.0]))
+    q2 = quat_mul(q12, q1)
+    q2 /= np.linalg.norm(q2)
+    R2 = quat_to_mat(q2)
+    c1w = -R1.T @ t1
+    c2w = c1w + np.array([baseline_m, 0.01, 0.005])
+    t2 = -R2 @ c2w
+    pc2 = pw @ R2.T + t2
+    uv1 = np.stack([fx * pc1[:, 0] / pc1[:, 2] + cx, fy * pc1[:, 1] / pc1[:, 2] + cy], -1)
+    uv2 = np.stack([fx * pc2[:, 0] / pc2[:, 2] + cx, fy * pc2[:, 1] / pc2[:, 2] + cy], -1)
+    uv1 += rng.normal(0, noise_px, uv1.shape)
+    uv2 += rng.normal(0, noise_px, uv2.shape)
+    # frame 2 feature order is a permutation of frame 1's
+    perm = rng.permutation(n)
+    uv2 = uv2[perm]
+    inv = np.empty(n, np.int64)
+    inv[perm] = np.arange(n)  # point i is feature inv[i] of frame 2
+    has1 = (rng.random(n) < frac_has).astype(np.uint8)
+    has2 = (rng.random(n) < frac_has).astype(np.uint8)
+    q_idx = np.sort(rng.choice(n, size=int(0.8 * n), replace=False))
+    t_idx = inv[q_idx].copy()
+    bad = rng.random(q_idx.size) < frac_bad_match
+    t_idx[bad] = rng.integers(0, n, bad.sum())
+    dup = rng.random(q_idx.size) < frac_dup_train
+    dup_src = rng.integers(0, q_idx.size, dup.sum())
+    t_idx[dup] = t_idx[dup_src]
+    matches = np.zeros(q_idx.size, np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("distance", "<f4")]))
+    matches["query_idx"] = q_idx
+    matches["train_idx"] = t_idx
+    matches["distance"] = rng.integers(0, 64, q_idx.size)
+    # depth image of frame 2: smooth field, holes (0) and out-of-range pixels
+    yy, xx = np.mgrid[0:height, 0:width]
+    dm = 2.5 + 1.5 * np.sin(xx / 57.0) * np.cos(yy / 43.0) + 0.002 * xx
+    dm[rng.random(dm.shape) < 0.05] = 0.0
+    dm[rng.random(dm.shape) < 0.02] = 0.05
+    dm[rng.random(dm.shape) < 0.02] = 12.0
+    if depth_type == "u16":
+        depth = np.round(dm * 5000.0).clip(0, 65535).astype(np.uint16)
+    elif depth_type == "f32":
+        depth = dm.astype(np.float32)
+    else:
+        depth = dm.astype(np.float64)
+    pose1 = np.concatenate([q1, t1])
+    pose2 = np.concatenate([q2, t2])
+    return {"uv1": np.ascontiguousarray(uv1), "has1": has1, "uv2": np.ascontiguousarray(uv2), "has2": has2,
+            "intr": np.array(intr, np.float64), "pose1": pose1, "pose2": pose2, "matches": matches,
+            "depth": np.ascontiguousarray(depth), "pw_true": pw, "inv": inv}
