@@ -96,6 +96,12 @@ int vx_event_create(vx_ctx* ctx, vx_event** out);
 int vx_event_record(vx_ctx* ctx, vx_event* ev); /* marks everything enqueued on ctx so far */
 int vx_event_wait(vx_ctx* ctx, vx_event* ev);   /* later work on ctx waits for the marked work */
 void vx_event_destroy(vx_event* ev);
+/* hipGraph replay: the *_async entry points (and vx_ba_plan_run_async / vx_sba_plan_run_async) run
+ * eagerly the first time a launch configuration is seen, capture it into a hipGraph the second
+ * time and replay it with one hipGraphLaunch afterwards ($VX_GRAPHS=0 or enable = 0 disables;
+ * profiling bypasses it).  Counts of captured graphs and graph launches so far. */
+int vx_graph_enable(vx_ctx* ctx, int enable);
+int vx_graph_counts(const vx_ctx* ctx, int* captured, int* launched);
 void vx_orb_default_params(vx_orb_params* p);
 /* Copies the compiled-in rBRIEF pattern (bit_pattern_31_, 256 x {x1,y1,x2,y2}). */
 int vx_orb_pattern(int32_t* out_1024);

@@ -310,3 +310,42 @@ def test_frontend_backend_contexts_overlap(ctx, oracle):
             e.close()
         bctx.close()
         mctx.close()
+
+
+def test_graph_replay_matches_eager(ctx, oracle):
+    """The async entry points replay hipGraphs after their second identical call: results of
+    replayed extraction / matching / LocalBA runs equal the eager path and the restatement."""
+    import torch
+    import vxslam
+
+    c = vxslam.Context(0)
+    try:
+        frames = synth.make_frames(0x5EED0077, 2, 480, 640)
+        d = torch.from_numpy(frames).cuda()
+        p = vxslam.default_orb_params(n_features=2000)
+        kc = [oracle.orb_extract(frames[i], 2000, order=oracle.ORDER_RASTER) for i in range(2)]
+        nk, nl, _ = synth.ba_config("C2")
+        m = synth.make_ba_map(91, nk, nl)
+        plan = c.ba_plan(m, vxslam.default_ba_options(window=nk))
+        outs = []
+        for rep in range(4):  # rep 0 eager, rep 1 captured, reps 2-3 replayed
+            for s in range(2):
+                c.orb_extract_async(d[s].data_ptr(), 640, 480, 3, 640 * 3, s, p)
+            c.match_slots_async(0, 1)
+            sl = [c.slot_device(s) for s in range(2)]
+            c.match_device_async(sl[0], sl[1])
+            plan.run_async()
+            c.synchronize()
+            for s in range(2):
+                _assert_orb_equal(*c.orb_fetch(s), *kc[s])
+            assert np.array_equal(c.match_fetch(), oracle.match(kc[0][1], kc[1][1]))
+            mm = m.copy()
+            plan.fetch(mm)
+            outs.append(mm)
+        for o in outs[1:]:
+            assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
+        captured, launched = c.graph_counts()
+        assert captured >= 4 and launched >= 8, (captured, launched)
+        plan.close()
+    finally:
+        c.close()

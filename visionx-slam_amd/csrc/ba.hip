@@ -537,6 +537,7 @@ struct vx_ba_plan {
         pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_lm, lm_blk, lobs_uv, state;
     int n_lm_blocks = 1;
     bool ran = false;
+    vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
 };
 
 namespace vx {
@@ -824,7 +825,9 @@ int vx_ba_plan_create(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_ref
 
 int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
-    return plan_run(c, p);
+    if (p->shard_count > 1 || p->status != 0) return plan_run(c, p);  // (RCCL calls stay outside graphs)
+    p->ran = true;
+    return graph_run_owned(c, p->graph, [](vx_ctx* cc, void* v) { return plan_run(cc, static_cast<vx_ba_plan*>(v)); }, p);
 }
 
 int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) {
@@ -865,7 +868,9 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
     return VX_OK;
 }
 
-void vx_ba_plan_destroy(vx_ba_plan* p) { delete p; }
+void vx_ba_plan_destroy(vx_ba_plan* p) {
+    delete p;
+}
 
 int vx_ba_plan_inspect(const vx_map_view* m, uint64_t ref, int has_ref, const vx_ba_options* opt, int shard_rank,
                        int shard_count, int64_t* out8, int32_t* lm_map_idx, int cap_lm, int32_t* kf_map_idx,

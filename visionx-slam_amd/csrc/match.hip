@@ -13,6 +13,8 @@
 //                  v_med3: VALU-popcount bound.
 //   k_knn_merge    one block: merge chunk partials, ratio test, ordered compaction (ascending
 //                  query index) by block scan.
+#include <cstring>
+
 #include "vx_internal.hpp"
 
 namespace vx {
@@ -182,7 +184,24 @@ int vx_match_device_async(vx_ctx* c, const uint8_t* dq, const int32_t* dnq, int 
         return set_error(c, VX_ERR_INVALID, "vx_match_device_async: null buffers or negative capacity");
     if (t_cap > (1 << 22)) return set_error(c, VX_ERR_INVALID, "train set larger than 2^22 rows");
     VX_HIP(c, hipSetDevice(c->device));
-    return match_enqueue(c, dq, dnq, q_cap, dt, dnt, t_cap, q_cap, t_cap, ratio);
+    struct A {
+        const uint8_t *dq, *dt;
+        const int32_t *dnq, *dnt;
+        int q_cap, t_cap;
+        float ratio;
+    } a{dq, dt, dnq, dnt, q_cap, t_cap, ratio};
+    uint32_t rbits;
+    std::memcpy(&rbits, &ratio, 4);
+    // the buffers match_enqueue bakes into the graph are part of the key (they grow on demand)
+    return graph_run(c, {2, (uint64_t)(uintptr_t)dq, (uint64_t)(uintptr_t)dnq, (uint64_t)q_cap, (uint64_t)(uintptr_t)dt,
+                         (uint64_t)(uintptr_t)dnt, (uint64_t)t_cap, rbits, (uint64_t)(uintptr_t)c->partial.p,
+                         (uint64_t)(uintptr_t)c->matches.p, (uint64_t)(uintptr_t)c->match_count.p},
+                     [](vx_ctx* cc, void* v) {
+                         const A* x = static_cast<const A*>(v);
+                         return match_enqueue(cc, x->dq, x->dnq, x->q_cap, x->dt, x->dnt, x->t_cap, x->q_cap, x->t_cap,
+                                              x->ratio);
+                     },
+                     &a);
 }
 
 int vx_match_fetch(vx_ctx* c, vx_match* out, int cap, int* n_out) {

@@ -1150,6 +1150,7 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
     }
     c->geo = g;
     c->geo_valid = true;
+    ++c->geo_gen;
     return VX_OK;
 }
 
@@ -1243,7 +1244,18 @@ int vx_orb_extract_async(vx_ctx* c, const vx_orb_params* p, const uint8_t* d_img
     if (stride < (int64_t)w * channels) return set_error(c, VX_ERR_INVALID, "row stride too small");
     int rc = orb_prepare(c, p, w, h);
     if (rc) return rc;
-    return orb_enqueue(c, d_img, channels, stride, slot);
+    struct A {
+        const uint8_t* img;
+        int channels;
+        int64_t stride;
+        int slot;
+    } a{d_img, channels, stride, slot};
+    return graph_run(c, {1, (uint64_t)(uintptr_t)d_img, (uint64_t)channels, (uint64_t)stride, (uint64_t)slot, c->geo_gen},
+                     [](vx_ctx* cc, void* v) {
+                         const A* x = static_cast<const A*>(v);
+                         return orb_enqueue(cc, x->img, x->channels, x->stride, x->slot);
+                     },
+                     &a);
 }
 
 int vx_orb_fetch(vx_ctx* c, int slot, vx_keypoint* out_kp, uint8_t* out_desc, int cap, int* n_out) {

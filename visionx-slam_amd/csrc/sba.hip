@@ -808,6 +808,7 @@ struct vx_sba_plan {
     std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
     std::vector<long long> comp_off_h, comp_loff_h;
     int64_t n_lfactor_tiles = 0, n_trail_updates = 0;  // symbolic factorisation (all components)
+    vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
     vx::DevBuf pose0, pose, intr, kf_flags, kf_comp, kf_local, lm0, lm, obs_uv, obs_kf, obs_lm, lm_ptr, lm_blk,
         kf_ptr, kf_obs, blk_ij, blk_ptr, pairs, comp_kf_ptr, comp_kf, comp_off, comp_loff, comp_np, comp_hdr, tl, wy,
         lm_sys,
@@ -1306,7 +1307,9 @@ int vx_sba_plan_create(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_re
 
 int vx_sba_plan_run_async(vx_ctx* c, vx_sba_plan* p) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
-    return sba_run(c, p);
+    if (p->shard_count > 1 || p->status != 0) return sba_run(c, p);  // (RCCL calls stay outside graphs)
+    p->ran = true;
+    return graph_run_owned(c, p->graph, [](vx_ctx* cc, void* v) { return sba_run(cc, static_cast<vx_sba_plan*>(v)); }, p);
 }
 
 int vx_sba_plan_fetch(vx_ctx* c, vx_sba_plan* p, vx_map_view* m, vx_sba_stats* st) {
@@ -1351,7 +1354,9 @@ int vx_sba_plan_fetch(vx_ctx* c, vx_sba_plan* p, vx_map_view* m, vx_sba_stats* s
     return VX_OK;
 }
 
-void vx_sba_plan_destroy(vx_sba_plan* p) { delete p; }
+void vx_sba_plan_destroy(vx_sba_plan* p) {
+    delete p;
+}
 
 int vx_sba_plan_info(const vx_sba_plan* p, int64_t* out8) {
     if (!p || !out8) return VX_ERR_INVALID;

@@ -1,4 +1,6 @@
 // vx_ctx.cpp — context lifetime, error reporting, stage profiling and the RCCL communicator.
+#include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstring>
@@ -72,6 +74,80 @@ void prof_collect(vx_ctx* c) {
     c->pending.clear();
 }
 
+uint64_t next_serial() {
+    static std::atomic<uint64_t> n{1};
+    return n++;
+}
+
+// Capture-or-replay of one graph slot: exec == nullptr && !seen -> eager run (and remember);
+// seen once -> capture + instantiate + launch; exec set -> launch.
+static int graph_slot_run(vx_ctx* c, hipGraphExec_t& exec, bool& seen, int (*enqueue)(vx_ctx*, void*), void* arg) {
+    if (exec) {
+        ++c->graphs.launched;
+        VX_HIP(c, hipGraphLaunch(exec, c->stream));
+        return VX_OK;
+    }
+    if (!seen) {  // first sighting: eager (allocations happen outside any capture)
+        seen = true;
+        return enqueue(c, arg);
+    }
+    VX_HIP(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed));
+    const int rc = enqueue(c, arg);
+    hipGraph_t g = nullptr;
+    const hipError_t ce = hipStreamEndCapture(c->stream, &g);
+    hipGraphExec_t x = nullptr;
+    hipError_t ie = hipErrorUnknown;
+    if (rc == VX_OK && ce == hipSuccess && g) ie = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (rc != VX_OK) return rc;
+    if (ie != hipSuccess) {  // not capturable here: stay eager from now on
+        c->use_graphs = false;
+        return enqueue(c, arg);
+    }
+    exec = x;
+    ++c->graphs.captured;
+    ++c->graphs.launched;
+    VX_HIP(c, hipGraphLaunch(exec, c->stream));
+    return VX_OK;
+}
+
+int graph_run(vx_ctx* c, const std::vector<uint64_t>& key, int (*enqueue)(vx_ctx*, void*), void* arg) {
+    if (!c->use_graphs || c->prof || c->orb_fork) return enqueue(c, arg);
+    GraphCache& gc = c->graphs;
+    const uint64_t now = ++gc.tick;
+    GraphCache::Entry* e = nullptr;
+    for (auto& x : gc.entries)
+        if (x.key == key) {
+            e = &x;
+            break;
+        }
+    if (!e) {
+        constexpr size_t kMaxGraphs = 64;
+        if (gc.entries.size() >= kMaxGraphs) {
+            auto lru = std::min_element(gc.entries.begin(), gc.entries.end(),
+                                        [](const GraphCache::Entry& a, const GraphCache::Entry& b) { return a.last < b.last; });
+            if (lru->exec) (void)hipGraphExecDestroy(lru->exec);
+            gc.entries.erase(lru);
+        }
+        gc.entries.push_back({key, nullptr, now});
+        e = &gc.entries.back();
+        bool seen = false;
+        return graph_slot_run(c, e->exec, seen, enqueue, arg);
+    }
+    e->last = now;
+    bool seen = true;
+    return graph_slot_run(c, e->exec, seen, enqueue, arg);
+}
+
+int graph_run_owned(vx_ctx* c, OwnedGraph& g, int (*enqueue)(vx_ctx*, void*), void* arg) {
+    if (!c->use_graphs || c->prof) return enqueue(c, arg);
+    return graph_slot_run(c, g.exec, g.seen, enqueue, arg);
+}
+
+OwnedGraph::~OwnedGraph() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+}
+
 }  // namespace vx
 
 static const char* kStageNames[vx::kStCount] = {
@@ -95,6 +171,7 @@ int vx_create(int device, vx_ctx** out) {
     auto* c = new vx_ctx();
     c->device = device;
     if (const char* f = std::getenv("VX_ORB_FORK")) c->orb_fork = std::atoi(f) != 0;
+    if (const char* f = std::getenv("VX_GRAPHS")) c->use_graphs = std::atoi(f) != 0;
     // one HIP stream per context (HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues, 4 by
     // default: streams beyond that share queues and serialise); the fork stream only on request
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -113,6 +190,8 @@ void vx_destroy(vx_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto& e : c->graphs.entries)
+        if (e.exec) (void)hipGraphExecDestroy(e.exec);
     vx::prof_collect(c);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     for (auto e : {c->order_event, c->fork_ev, c->join_ev})
@@ -126,6 +205,19 @@ void vx_destroy(vx_ctx* c) {
 }
 
 const char* vx_last_error(const vx_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int vx_graph_enable(vx_ctx* c, int enable) {
+    if (!c) return VX_ERR_INVALID;
+    c->use_graphs = enable != 0;
+    return VX_OK;
+}
+
+int vx_graph_counts(const vx_ctx* c, int* captured, int* launched) {
+    if (!c) return VX_ERR_INVALID;
+    if (captured) *captured = c->graphs.captured;
+    if (launched) *launched = c->graphs.launched;
+    return VX_OK;
+}
 
 void* vx_stream(vx_ctx* c) { return c ? (void*)c->stream : nullptr; }
 

@@ -134,6 +134,21 @@ struct ProfEvent {
     int stage;
 };
 
+// Launch sequences of the async entry points captured into hipGraphs and replayed with one
+// hipGraphLaunch (the per-frame pipeline is otherwise bound by host-side launch cost: ~18 kernel
+// launches per frame).  Keyed by everything the captured sequence bakes in (device pointers,
+// sizes, a geometry / plan serial); least-recently-used entries are evicted.
+struct GraphCache {
+    struct Entry {
+        std::vector<uint64_t> key;
+        hipGraphExec_t exec = nullptr;
+        uint64_t last = 0;
+    };
+    std::vector<Entry> entries;
+    uint64_t tick = 0;
+    int captured = 0, launched = 0;
+};
+
 }  // namespace vx
 
 struct vx_ba_plan;
@@ -168,6 +183,11 @@ struct vx_ctx {
 
     // ---- landmark creation (landmarks.hip): inputs, per-item flags / points, compacted outputs
     vx::DevBuf lm_in0, lm_in1, lm_in2, lm_in3, lm_in4, lm_depth, lm_valid, lm_pw, lm_index, lm_out, lm_count, lm_aux;
+
+    // ---- hipGraph replay of the async entry points ($VX_GRAPHS=0 disables)
+    vx::GraphCache graphs;
+    bool use_graphs = true;
+    uint64_t geo_gen = 0;  // bumped whenever the ORB geometry (and its buffers) is rebuilt
 
     // ---- profiling
     bool prof = false;
@@ -223,6 +243,23 @@ inline hipError_t launch(vx_ctx* c, int stage, F kernel, dim3 grid, dim3 block, 
 }
 
 int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h);
+
+// Runs `enqueue` (which only enqueues work on c->stream) through the context's graph cache: the
+// first call with a key runs eagerly (so every buffer it needs gets allocated outside a capture),
+// the second captures the sequence into a hipGraph, later ones replay it.  Profiling (events
+// around launches) and the intra-frame fork bypass the cache.
+int graph_run(vx_ctx* c, const std::vector<uint64_t>& key, int (*enqueue)(vx_ctx*, void*), void* arg);
+// A graph owned by a long-lived object (a BA plan): captured on its second run, replayed after,
+// destroyed with its owner (independently of the context's cache).
+struct OwnedGraph {
+    hipGraphExec_t exec = nullptr;
+    bool seen = false;
+    OwnedGraph() = default;
+    OwnedGraph(const OwnedGraph&) = delete;
+    OwnedGraph& operator=(const OwnedGraph&) = delete;
+    ~OwnedGraph();
+};
+int graph_run_owned(vx_ctx* c, OwnedGraph& g, int (*enqueue)(vx_ctx*, void*), void* arg);
 
 }  // namespace vx
 

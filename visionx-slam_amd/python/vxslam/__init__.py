@@ -83,7 +83,7 @@ EXPORTS = [
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
-    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate",
+    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
@@ -337,6 +337,15 @@ class Context:
 
     def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1):
         return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
+
+    def graph_enable(self, on=True):
+        self._check(lib().vx_graph_enable(self._h, 1 if on else 0))
+
+    def graph_counts(self):
+        """(graphs captured, graph launches) of this context's hipGraph replay."""
+        cap, lau = C.c_int(0), C.c_int(0)
+        self._check(lib().vx_graph_counts(self._h, C.byref(cap), C.byref(lau)))
+        return cap.value, lau.value
 
     # ---------------------------------------------------------------- landmark creation
     def depth_landmarks(self, uv, has, depth, intr, pose):
