@@ -63,10 +63,8 @@ def stage_bytes(stage, geo, counts):
         return W * H * C + sum(px)
     if stage == "orb_resize":       # average over the L-1 launches
         return sum(px[l - 1] + px[l] for l in range(1, len(px))) / (len(px) - 1)
-    if stage == "orb_fast_harris":
-        return sum(px) + 16 * counts["n_cand"]
-    if stage == "orb_blur":
-        return 2 * sum(px)
+    if stage == "orb_fast_harris":  # every level read, blurred levels written, candidate records
+        return 2 * sum(px) + 16 * counts["n_cand"]
     if stage == "orb_select":
         return 16 * counts["n_cand"] + 16 * N
     if stage == "orb_describe":
@@ -194,6 +192,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=30, help="frames timed for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
+    ap.add_argument("--ba-cus", type=float, default=0.0,
+                    help="fraction of the CUs reserved for the LocalBA context (disjoint CU masks; 0: shared)")
     ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
                     help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
     args = ap.parse_args()
@@ -205,10 +205,17 @@ def main():
     from vxslam import synth
 
     torch.cuda.set_device(dist.local_rank)
-    # one context (HIP stream) per pipeline stage; see Pipeline
-    ectx = vxslam.Context(dist.local_rank)
-    mctx = ectx if args.streams < 3 else vxslam.Context(dist.local_rank)
-    bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank)
+    # one context (HIP stream) per pipeline stage; see Pipeline.  --ba-cus > 0 gives LocalBA its own
+    # compute units (every k-th CU, spread over the XCDs) and extraction / matching the rest
+    fe_mask = ba_mask = None
+    if args.ba_cus > 0 and args.streams > 1:
+        ncu = vxslam.lib().vx_device_cus(dist.local_rank)
+        k = max(1, int(round(1.0 / args.ba_cus)))
+        ba_mask = [i for i in range(ncu) if i % k == k - 1]
+        fe_mask = [i for i in range(ncu) if i % k != k - 1]
+    ectx = vxslam.Context(dist.local_rank, cu_mask=fe_mask)
+    mctx = ectx if args.streams < 3 else vxslam.Context(dist.local_rank, cu_mask=fe_mask)
+    bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank, cu_mask=ba_mask)
     ctxs = list({id(c): c for c in (ectx, mctx, bctx)}.values())
     cfg = CONFIGS[args.config]
     h, w, nf, nk, nl = cfg

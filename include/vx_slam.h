@@ -79,6 +79,13 @@ typedef struct {
 /* ---------------------------------------------------------------- context */
 int vx_version(void);
 int vx_create(int device, vx_ctx** out);
+/* vx_create with a stream priority (0 normal, 1 the device's greatest) and an optional CU mask
+ * (bit i = compute unit i may run this context's workgroups; mask_words 32-bit words, NULL / 0 =
+ * every CU).  Disjoint masks keep a latency-critical chain (the LocalBA context of a pipeline)
+ * from queueing behind concurrently running bulk work (extraction) — see bench.py --ba-cus. */
+int vx_create_ex(int device, int priority, const uint32_t* cu_mask, int mask_words, vx_ctx** out);
+/* compute units of a device (the width of a CU mask) */
+int vx_device_cus(int device);
 void vx_destroy(vx_ctx* ctx);
 const char* vx_last_error(const vx_ctx* ctx);
 void* vx_stream(vx_ctx* ctx);          /* the context's hipStream_t */

@@ -1,0 +1,70 @@
+"""Where does the 3-stream pipeline lose time?  Per-frame time of Extract / Match / LocalBA alone,
+of independent pairs on separate contexts (no events), and of the event-ordered pipeline."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
+import torch  # noqa: E402
+import vxslam  # noqa: E402
+from vxslam import synth  # noqa: E402
+
+h, w, nf, nk, nl = 480, 640, 2000, 50, 20000
+e, m, b = vxslam.Context(0), vxslam.Context(0), vxslam.Context(0)
+frames = torch.from_numpy(synth.make_frames(7, 8, h, w)).cuda()
+params = vxslam.default_orb_params(n_features=nf)
+plan = b.ba_plan(synth.make_ba_map(0x5EED0003, nk, nl), vxslam.default_ba_options(window=nk))
+for i in range(3):
+    e.orb_extract_async(frames[i].data_ptr(), w, h, 3, w * 3, i, params)
+e.synchronize()
+slot = [e.slot_device(s) for s in range(3)]
+ev_e = e.event()
+ev_m = [m.event() for _ in range(3)]
+
+
+def E(i):
+    e.orb_extract_async(frames[i % 8].data_ptr(), w, h, 3, w * 3, i % 3, params)
+
+
+def M(i):
+    m.match_device_async(slot[(i - 1) % 3], slot[i % 3])
+
+
+def B(i):
+    plan.run_async()
+
+
+def piped(i):
+    e.wait_event(ev_m[(i + 1) % 3])
+    E(i)
+    e.record(ev_e)
+    m.wait_event(ev_e)
+    M(i)
+    m.record(ev_m[i % 3])
+    b.wait_event(ev_m[i % 3])
+    B(i)
+
+
+def run(name, fns, K=200):
+    for i in range(10):
+        for f in fns:
+            f(i)
+    for c in (e, m, b):
+        c.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        for f in fns:
+            f(10 + i)
+    for c in (e, m, b):
+        c.synchronize()
+    print(f"{name:28s} {1e3 * (time.perf_counter() - t0) / K:.4f} ms/frame", flush=True)
+
+
+run("extract alone", [E])
+run("match alone", [M])
+run("localBA alone", [B])
+run("extract | localBA (no deps)", [E, B])
+run("extract | match (no deps)", [E, M])
+run("extract | match | BA (no deps)", [E, M, B])
+run("pipeline (events)", [piped])

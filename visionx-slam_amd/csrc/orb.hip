@@ -384,14 +384,31 @@ constexpr int kTX = 64, kTY = 16, kCellCap = 32;
 constexpr int kTW = kTX + 8, kTH = kTY + 8;   // staged tile
 constexpr int kSW = kTX + 2, kSH = kTY + 2;   // score tile
 
+// The GaussianBlur of the same 64 x 16 output tile (k_blur's arithmetic, reflect-101 halo of 3)
+// is computed here too: the tile is already being read, and the separate blur launch was a
+// dependent step of its own on the extraction chain.
+constexpr int kBW = kTX + 6, kBH = kTY + 6;   // blur input tile (3 px reflect-101 halo)
+
+__device__ __forceinline__ int refl101(int p, int n) {
+    if (n == 1) return 0;
+    while (p < 0 || p >= n) {
+        if (p < 0) p = -p;
+        if (p >= n) p = 2 * n - 2 - p;
+    }
+    return p;
+}
+
 __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr, LevelArgs a,
                                                  CandRec* __restrict__ cand,
                                                  int* __restrict__ cell_count,
-                                                 int* __restrict__ hist) {
+                                                 int* __restrict__ hist,
+                                                 uint8_t* __restrict__ blur) {
     __shared__ uint8_t tile[kTH * kTW];
     __shared__ uint8_t sc[kSH * kSW];
     __shared__ int s_list[kTY * kCellCap];   // (cell slot << 16) | (row << 8) | local x
     __shared__ int s_n;
+    __shared__ uint8_t bin_[kBH * kBW];
+    __shared__ float brow[kBH * kTX];
     const int b = blockIdx.x;
     int l = 0;
     while (l + 1 < a.L && b >= a.tile_base[l + 1]) ++l;
@@ -410,6 +427,10 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
         const int gx = min(max(x0 - 4 + c, 0), W - 1);
         return img[(long long)gy * W + gx];
     });
+    stage_lds<kBlock, (kBH * kBW + kBlock - 1) / kBlock>(bin_, kBH * kBW, [&](int i) {
+        const int r = i / kBW, c = i - r * kBW;
+        return img[(long long)refl101(y0 - 3 + r, H) * W + refl101(x0 - 3 + c, W)];
+    });
     __syncthreads();
     VX_KT(5);
     const int thr = a.fast_threshold;
@@ -420,8 +441,37 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
         if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) s = fast_score(tile + (r + 3) * kTW + c + 3, kTW, thr);
         sc[i] = (uint8_t)s;
     }
+    // blur row pass 8U -> 32F (float separable GaussianBlur)
+    const float k0 = a.gk[0], k1 = a.gk[1], k2 = a.gk[2], k3 = a.gk[3], k4 = a.gk[4], k5 = a.gk[5], k6 = a.gk[6];
+    for (int i = tid; i < kBH * kTX; i += kBlock) {
+        const int r = i / kTX, c = i - r * kTX;
+        const uint8_t* p = bin_ + r * kBW + c;
+        float s = k0 * (float)p[0];
+        s += k1 * (float)p[1];
+        s += k2 * (float)p[2];
+        s += k3 * (float)p[3];
+        s += k4 * (float)p[4];
+        s += k5 * (float)p[5];
+        s += k6 * (float)p[6];
+        brow[i] = s;
+    }
     __syncthreads();
     VX_KT(6);
+    {  // blur column pass 32F -> 8U (symmetric form, round half to even)
+        uint8_t* out = blur + a.off[l];
+        for (int i = tid; i < kTY * kTX; i += kBlock) {
+            const int r = i / kTX, c = i - r * kTX;
+            const int x = x0 + c, y = y0 + r;
+            if (x >= W || y >= H) continue;
+            const float* q = brow + (r + 3) * kTX + c;
+            float s = k3 * q[0] + 0.0f;
+            s += k4 * (q[kTX] + q[-kTX]);
+            s += k5 * (q[2 * kTX] + q[-2 * kTX]);
+            s += k6 * (q[3 * kTX] + q[-3 * kTX]);
+            const int v = __float2int_rn(s);
+            out[(long long)y * W + x] = (uint8_t)min(255, max(0, v));
+        }
+    }
     const int e = a.edge;
     for (int r = wv; r < kTY; r += kBlock / 64) {
         const int y = y0 + r, x = x0 + lane;
@@ -478,66 +528,6 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
         }
     }
     VX_KT(8);
-}
-
-// ------------------------------------------------------------------------------ blur
-__global__ __launch_bounds__(kBlock) void k_blur(const uint8_t* __restrict__ pyr,
-                                                 uint8_t* __restrict__ blur, LevelArgs a) {
-    constexpr int TXo = 64, TYo = 16;
-    __shared__ uint8_t sin_[(TYo + 6) * (TXo + 6)];
-    __shared__ float srow[(TYo + 6) * TXo];
-    const int b = blockIdx.x;
-    VX_KT(9);
-    int l = 0;
-    while (l + 1 < a.L && b >= a.bbase[l + 1]) ++l;
-    const int W = a.lw[l], H = a.lh[l];
-    const int t = b - a.bbase[l];
-    const int tx = t % a.btx[l], ty = t / a.btx[l];
-    const int x0 = tx * TXo, y0 = ty * TYo;
-    const uint8_t* img = pyr + a.off[l];
-    auto refl = [](int p, int n) {
-        if (n == 1) return 0;
-        while (p < 0 || p >= n) {
-            if (p < 0) p = -p;
-            if (p >= n) p = 2 * n - 2 - p;
-        }
-        return p;
-    };
-    stage_lds<kBlock, ((TYo + 6) * (TXo + 6) + kBlock - 1) / kBlock>(sin_, (TYo + 6) * (TXo + 6), [&](int i) {
-        const int r = i / (TXo + 6), c = i - r * (TXo + 6);
-        return img[(long long)refl(y0 - 3 + r, H) * W + refl(x0 - 3 + c, W)];
-    });
-    __syncthreads();
-    VX_KT(10);
-    const float k0 = a.gk[0], k1 = a.gk[1], k2 = a.gk[2], k3 = a.gk[3], k4 = a.gk[4],
-                k5 = a.gk[5], k6 = a.gk[6];
-    for (int i = threadIdx.x; i < (TYo + 6) * TXo; i += kBlock) {
-        const int r = i / TXo, c = i - r * TXo;
-        const uint8_t* p = sin_ + r * (TXo + 6) + c;
-        float s = k0 * (float)p[0];
-        s += k1 * (float)p[1];
-        s += k2 * (float)p[2];
-        s += k3 * (float)p[3];
-        s += k4 * (float)p[4];
-        s += k5 * (float)p[5];
-        s += k6 * (float)p[6];
-        srow[i] = s;
-    }
-    __syncthreads();
-    uint8_t* out = blur + a.off[l];
-    for (int i = threadIdx.x; i < TYo * TXo; i += kBlock) {
-        const int r = i / TXo, c = i - r * TXo;
-        const int x = x0 + c, y = y0 + r;
-        if (x >= W || y >= H) continue;
-        const float* q = srow + (r + 3) * TXo + c;
-        float s = k3 * q[0] + 0.0f;
-        s += k4 * (q[TXo] + q[-TXo]);
-        s += k5 * (q[2 * TXo] + q[-2 * TXo]);
-        s += k6 * (q[3 * TXo] + q[-3 * TXo]);
-        const int v = __float2int_rn(s);
-        out[(long long)y * W + x] = (uint8_t)min(255, max(0, v));
-    }
-    VX_KT(11);
 }
 
 // ------------------------------------------------------------------------------ select
@@ -1030,11 +1020,6 @@ LevelArgs level_args(const OrbGeometry& g) {
     return a;
 }
 
-int blur_blocks(const LevelArgs& a) {
-    int n = 0;
-    for (int l = 0; l < a.L; ++l) n += a.btx[l] * a.bty[l];
-    return n;
-}
 
 bool same_params(const vx_orb_params& x, const vx_orb_params& y) {
     return x.n_features == y.n_features && x.scale_factor == y.scale_factor &&
@@ -1182,22 +1167,12 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
             VX_LAUNCH_CHECK(c, "k_resize");
         }
     }
-    // blur depends only on the pyramid: fork it onto the side stream, join before describe
-    hipStream_t bs = c->stream;
-    if (c->orb_fork) {
-        VX_HIP(c, hipEventRecord(c->fork_ev, c->stream));
-        VX_HIP(c, hipStreamWaitEvent(c->side, c->fork_ev, 0));
-        bs = c->side;
-    }
-    VX_HIP(c, launch(c, kStBlur, k_blur, dim3(blur_blocks(a)), dim3(kBlock), 0, bs, (const uint8_t*)pyr,
-                     c->blur.as<uint8_t>(), a));
-    if (c->orb_fork) VX_HIP(c, hipEventRecord(c->join_ev, c->side));
+    // FAST + NMS + Harris and the GaussianBlur of every level, one launch over 64 x 16 tiles
     VX_HIP(c, launch(c, kStFast, k_fast, dim3(g.total_tiles), dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, a,
-                     c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>()));
+                     c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>(), c->blur.as<uint8_t>()));
     VX_HIP(c, launch(c, kStSelect, k_select, dim3(g.L), dim3(kSelBlock), 0, c->stream,
                      (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(),
                      (const int*)c->hist.as<int>(), a, c->stage.as<CandRec>(), c->level_count.as<int>()));
-    if (c->orb_fork) VX_HIP(c, hipStreamWaitEvent(c->stream, c->join_ev, 0));
     {
         const int waves_per_block = kBlock / 64;
         VX_HIP(c, launch(c, kStDescribe, k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block),

@@ -112,7 +112,7 @@ static int graph_slot_run(vx_ctx* c, hipGraphExec_t& exec, bool& seen, int (*enq
 }
 
 int graph_run(vx_ctx* c, const std::vector<uint64_t>& key, int (*enqueue)(vx_ctx*, void*), void* arg) {
-    if (!c->use_graphs || c->prof || c->orb_fork) return enqueue(c, arg);
+    if (!c->use_graphs || c->prof) return enqueue(c, arg);
     GraphCache& gc = c->graphs;
     const uint64_t now = ++gc.tick;
     GraphCache::Entry* e = nullptr;
@@ -161,7 +161,15 @@ extern "C" {
 
 int vx_version(void) { return 100; }
 
-int vx_create(int device, vx_ctx** out) {
+int vx_create(int device, vx_ctx** out) { return vx_create_ex(device, 0, nullptr, 0, out); }
+
+int vx_device_cus(int device) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return -1;
+    return n;
+}
+
+int vx_create_ex(int device, int priority, const uint32_t* cu_mask, int mask_words, vx_ctx** out) {
     if (!out) return VX_ERR_INVALID;
     *out = nullptr;
     int n = 0;
@@ -170,14 +178,16 @@ int vx_create(int device, vx_ctx** out) {
     if (hipSetDevice(device) != hipSuccess) return VX_ERR_HIP;
     auto* c = new vx_ctx();
     c->device = device;
-    if (const char* f = std::getenv("VX_ORB_FORK")) c->orb_fork = std::atoi(f) != 0;
     if (const char* f = std::getenv("VX_GRAPHS")) c->use_graphs = std::atoi(f) != 0;
     // one HIP stream per context (HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues, 4 by
-    // default: streams beyond that share queues and serialise); the fork stream only on request
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        (c->orb_fork && (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-                         hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
-                         hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess))) {
+    // default: streams beyond that share queues and serialise)
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    const hipError_t se =
+        (cu_mask && mask_words > 0)
+            ? hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask_words, cu_mask)
+            : hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, priority > 0 ? greatest : least);
+    if (se != hipSuccess) {
         vx_destroy(c);
         return VX_ERR_HIP;
     }
@@ -188,18 +198,16 @@ int vx_create(int device, vx_ctx** out) {
 void vx_destroy(vx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->side) (void)hipStreamSynchronize(c->side);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (auto& e : c->graphs.entries)
         if (e.exec) (void)hipGraphExecDestroy(e.exec);
     vx::prof_collect(c);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
-    for (auto e : {c->order_event, c->fork_ev, c->join_ev})
+    for (auto e : {c->order_event})
         if (e) (void)hipEventDestroy(e);
 #ifndef VX_NO_RCCL
     if (c->comm) ncclCommDestroy(c->comm);
 #endif
-    if (c->side) (void)hipStreamDestroy(c->side);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }

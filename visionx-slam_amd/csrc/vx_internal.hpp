@@ -26,7 +26,7 @@ enum Stage : int {
     kStResize,
     kStFast,
     kStSelect,
-    kStBlur,
+    kStBlur,          // (unused: the blur is computed inside k_fast)
     kStDescribe,
     kStMatchPartial,
     kStMatchMerge,
@@ -162,11 +162,6 @@ struct vx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t order_event = nullptr;  // vx_stream_wait_ctx: recorded on this stream
-    // intra-frame fork/join: k_blur runs on `side` concurrently with FAST + selection
-    hipStream_t side = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-    // off by default: with LocalBA on a second context the fork measured 4 % slower (v6)
-    bool orb_fork = false;  // $VX_ORB_FORK=1 enables it
     std::string err;
 
     // ---- ORB

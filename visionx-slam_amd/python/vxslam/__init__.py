@@ -83,7 +83,7 @@ EXPORTS = [
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
-    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts",
+    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts", "vx_create_ex", "vx_device_cus",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
@@ -219,9 +219,17 @@ class Context:
     """One vx_ctx = one device + one HIP stream (not thread-safe, like the reference's tracking
     thread owning the hot path, core/system/system.cpp:39-52)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, priority: int = 0, cu_mask=None):
+        """cu_mask: iterable of compute-unit indices this context may use (None: all)."""
         self._h = C.c_void_p()
-        rc = lib().vx_create(int(device), C.byref(self._h))
+        words, nw = None, 0
+        if cu_mask is not None:
+            n = lib().vx_device_cus(int(device))
+            nw = (n + 31) // 32
+            words = (C.c_uint32 * nw)()
+            for i in cu_mask:
+                words[i // 32] |= 1 << (i % 32)
+        rc = lib().vx_create_ex(int(device), int(priority), words, nw, C.byref(self._h))
         if rc != VX_OK:
             raise VxError(rc, f"vx_create(device={device}) failed")
 
