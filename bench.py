@@ -232,6 +232,14 @@ def main():
         bctx.comm_init(uid, N, dist.rank)
     plan = bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N)
     info = plan.info()
+    # what a drop-in LocalBA::Optimize() adds per call on top of the solve: the window / CSR
+    # build from the map snapshot (device build), reported beside `value`
+    plan_ms = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N).close()
+        plan_ms.append(1e3 * (time.perf_counter() - t0))
+    plan_build_ms = float(np.median(plan_ms))
     torch.cuda.synchronize()
 
     # Pipeline.  Frame t: Extract(t) on ectx into slot t % 3, Match(t - 1, t) on mctx, LocalBA(t) on
@@ -375,6 +383,10 @@ def main():
             # one frame alone through the same dependency chain (host enqueue to completion, median
             # of 20): the per-frame latency; `value` is the pipelined throughput
             "latency_ms_per_frame": round(latency_ms, 4),
+            # the LocalBA plan (SelectKeyFrames + landmark set + CSRs) built on the device from the
+            # map snapshot, incl. upload: paid once per LocalBA::Optimize() call of a drop-in
+            # (a new keyframe, tracking.cpp:76-84); the timed steps replay a resident plan
+            "ba_plan_build_ms": round(plan_build_ms, 3),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_us": {k: round(v[0] * 1e3, 2) for k, v in stages.items()},

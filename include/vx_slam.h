@@ -203,6 +203,13 @@ typedef struct vx_ba_plan vx_ba_plan;
 int vx_ba_plan_create(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                       const vx_ba_options* opt, int shard_rank, int shard_count,
                       vx_ba_plan** out);
+/* flags: VX_PLAN_HOST_BUILD builds the plan with the host reference restatement of
+ * local_ba.cpp:42-108 (hash maps, one core) instead of the device build (default: window join,
+ * slot assignment and both CSRs as HIP kernels).  Both give the same plan. */
+#define VX_PLAN_HOST_BUILD 1
+int vx_ba_plan_create_ex(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
+                         const vx_ba_options* opt, int shard_rank, int shard_count, int flags,
+                         vx_ba_plan** out);
 int vx_ba_plan_run_async(vx_ctx* ctx, vx_ba_plan* plan);
 int vx_ba_plan_fetch(vx_ctx* ctx, vx_ba_plan* plan, vx_map_view* map, vx_ba_stats* stats);
 void vx_ba_plan_destroy(vx_ba_plan* plan);

@@ -349,3 +349,53 @@ def test_graph_replay_matches_eager(ctx, oracle):
         plan.close()
     finally:
         c.close()
+
+
+def _plan_result(ctx, m, opts, ref, rank, count, host_build):
+    plan = ctx.ba_plan(m, opts, ref_kf_id=ref, shard_rank=rank, shard_count=count, host_build=host_build)
+    info = plan.info()
+    mm = m.copy()
+    if count == 1:
+        plan.run_async()
+        st = plan.fetch(mm)
+        out = (info, st.status, st.iterations, list(st.obs[:16]), list(st.cost[:16]), st.n_window_kf, st.n_landmarks)
+    else:  # sharded plans are only built here (running them needs the RCCL communicator)
+        out = (info,)
+    plan.close()
+    return out, mm
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
+def test_device_plan_build_equals_host_build(ctx, cfg):
+    """vx_ba_plan_create builds the window / landmark set / CSRs on the GPU (ba_window.hip); the
+    host restatement (VX_PLAN_HOST_BUILD) gives the same plan: identical counts and bitwise
+    identical LocalBA results."""
+    import vxslam
+
+    nk, nl, ns = synth.ba_config(cfg)
+    m = synth.make_ba_map(0x5EED0100 + nk, nk + 4, nl, n_old_kf=2)
+    cases = [(dict(window=nk), None, 0, 1), (dict(window=nk // 2), None, 0, 1),
+             (dict(window=nk), int(m["kf_id"][-4]), 0, 1), (dict(window=nk, min_point=3), None, 0, 1),
+             (dict(window=nk), None, 0, 2), (dict(window=nk), None, 1, 2), (dict(window=nk), None, 2, 3)]
+    mm = m.copy()
+    mm["kf_has_cam"][-3] = 0
+    for kw, ref, rank, count in cases:
+        for mp in (m, mm):
+            opts = vxslam.default_ba_options(**kw)
+            (rd, md) = _plan_result(ctx, mp, opts, ref, rank, count, False)
+            (rh, mh) = _plan_result(ctx, mp, opts, ref, rank, count, True)
+            assert rd == rh, (kw, ref, rank, count)
+            assert np.array_equal(md["kf_pose"], mh["kf_pose"]) and np.array_equal(md["lm_pos"], mh["lm_pos"])
+
+
+def test_device_plan_build_edges(ctx):
+    import vxslam
+
+    m = synth.make_ba_map(5, 6, 300, n_old_kf=0)
+    for kw, ref in [(dict(window=1), None), (dict(window=6), int(m["kf_id"][0]))]:  # < 2 keyframes
+        (rd, _), (rh, _) = (_plan_result(ctx, m, vxslam.default_ba_options(**kw), ref, 0, 1, hb) for hb in (False, True))
+        assert rd == rh and rd[1] == 1
+    mm = m.copy()
+    mm["lm_bad"][:] = 1  # no optimisable landmark
+    (rd, _), (rh, _) = (_plan_result(ctx, mm, vxslam.default_ba_options(window=6), None, 0, 1, hb) for hb in (False, True))
+    assert rd == rh and rd[1] == 1

@@ -39,13 +39,14 @@
 #include "vx_internal.hpp"
 #include "vx_ktrace.hpp"
 #include "ba_common.hpp"
+#include "ba_plan.hpp"
 
 namespace vx {
 namespace {
 
 using namespace vx::ba;
 
-constexpr int kPoseBlock = 512;  // threads per pose-stage workgroup
+constexpr int kPoseBlock = kBaPoseBlock;  // threads per pose-stage workgroup
 constexpr int kNTerms = 29;      // 21 H (upper) + 6 b + cost + count
 constexpr int kStride = 32;      // doubles per keyframe block in global memory
 // LDS slot stride of k_landmark_solve: 33, not 32 doubles — a 256-B stride is one full turn of the
@@ -53,9 +54,9 @@ constexpr int kStride = 32;      // doubles per keyframe block in global memory
 constexpr int kLdsStride = 33;
 constexpr int kMaxIter = 64;
 constexpr int kMaxKfLds = 256;   // keyframes whose LDS slots fit k_landmark_solve
-constexpr int kMaxSplit = 4;     // pose-stage workgroups per keyframe
+constexpr int kMaxSplit = kBaMaxSplit;    // pose-stage workgroups per keyframe
 constexpr int kCombine = 6;      // (keyframe, term) pairs per thread per combine pass
-constexpr int kLmBlock = 512;    // k_landmark_solve: threads = max observations = max landmarks
+constexpr int kLmBlock = kBaLmBlock;      // k_landmark_solve: threads = max observations = max landmarks
 
 VX_KT_TABLE();
 
@@ -523,22 +524,6 @@ __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
 }  // namespace
 }  // namespace vx
 
-struct vx_ba_plan {
-    vx_ctx* c = nullptr;
-    vx_ba_options opt{};
-    int status = 1;
-    int shard_rank = 0, shard_count = 1;
-    int n_window_kf = 0, n_landmarks_global = 0;
-    int n_kf = 0, n_opt = 0, n_lm = 0;
-    int64_t n_pose_obs = 0, n_lm_obs = 0;
-    std::vector<int> kf_map_idx, lm_map_idx;
-    int n_split = 1;
-    vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags, kf_obs_ptr, kf_part, kf_cost, lm_pos0, lm_pos,
-        pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_lm, lm_blk, lobs_uv, state;
-    int n_lm_blocks = 1;
-    bool ran = false;
-    vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
-};
 
 namespace vx {
 namespace {
@@ -581,6 +566,41 @@ int upload(vx_ctx* c, DevBuf& d, const std::vector<T>& h) {
     if (!h.empty()) VX_HIP(c, hipMemcpy(d.p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
     return VX_OK;
 }
+
+}  // namespace
+
+// k_landmark_solve workgroups: whole landmarks, at most kLmBlock landmarks and observations each
+// (a window of <= kMaxKfLds keyframes gives a landmark <= kMaxKfLds < kLmBlock of them)
+std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt) {
+    std::vector<int> blk{0};
+    int n_o = 0, n_l = 0;
+    for (int s = 0; s < n_opt; ++s) {
+        const int cnt = lptr[s + 1] - lptr[s];
+        if (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock) {
+            blk.push_back(s);
+            n_o = n_l = 0;
+        }
+        n_o += cnt;
+        ++n_l;
+    }
+    blk.push_back(n_opt);
+    return blk;
+}
+
+// Work buffers of a run (both plan builders end here): ping-pong poses, rotations, pose-stage
+// partial blocks, costs, landmark positions and the iteration state.
+int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
+    const size_t nk = (size_t)p->n_kf;
+    VX_HIP(c, p->kf_pose.ensure(nk * 2 * 8 * sizeof(double)));
+    VX_HIP(c, p->kf_rot.ensure(nk * 9 * sizeof(double)));
+    VX_HIP(c, p->kf_part.ensure(nk * p->n_split * kStride * sizeof(double)));
+    VX_HIP(c, p->kf_cost.ensure(nk * 2 * sizeof(double)));
+    VX_HIP(c, p->lm_pos.ensure((size_t)std::max(p->n_lm, 1) * 4 * sizeof(double)));
+    VX_HIP(c, p->state.ensure(sizeof(BAState)));
+    return VX_OK;
+}
+
+namespace {
 
 int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p,
                bool device = true) {
@@ -686,22 +706,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
         lptr[s + 1] = (int)lkf.size();
     }
     p->n_lm_obs = (int64_t)lkf.size();
-    // k_landmark_solve workgroups: whole landmarks, at most kLmBlock landmarks and observations
-    // each (a window of <= kMaxKfLds keyframes gives a landmark <= kMaxKfLds < kLmBlock of them)
-    std::vector<int> blk{0};
-    {
-        int n_o = 0, n_l = 0;
-        for (int s = 0; s < p->n_opt; ++s) {
-            const int cnt = lptr[s + 1] - lptr[s];
-            if (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock) {
-                blk.push_back(s);
-                n_o = n_l = 0;
-            }
-            n_o += cnt;
-            ++n_l;
-        }
-        blk.push_back(p->n_opt);
-    }
+    const std::vector<int> blk = pack_lm_blocks(lptr, p->n_opt);
     p->n_lm_blocks = (int)blk.size() - 1;
     if (!device) return VX_OK;
 
@@ -719,13 +724,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     if ((rc = upload(c, p->lobs_lm, llm))) return rc;
     if ((rc = upload(c, p->lm_blk, blk))) return rc;
     if ((rc = upload(c, p->lobs_uv, luv))) return rc;
-    VX_HIP(c, p->kf_pose.ensure((size_t)nk * 2 * 8 * sizeof(double)));
-    VX_HIP(c, p->kf_rot.ensure((size_t)nk * 9 * sizeof(double)));
-    VX_HIP(c, p->kf_part.ensure((size_t)nk * p->n_split * kStride * sizeof(double)));
-    VX_HIP(c, p->kf_cost.ensure((size_t)nk * 2 * sizeof(double)));
-    VX_HIP(c, p->lm_pos.ensure(lm0.size() * sizeof(double)));
-    VX_HIP(c, p->state.ensure(sizeof(BAState)));
-    return VX_OK;
+    return alloc_run_buffers(c, p);
 }
 
 int plan_run(vx_ctx* c, vx_ba_plan* p) {
@@ -803,6 +802,11 @@ void vx_ba_default_options(vx_ba_options* o) {
 
 int vx_ba_plan_create(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_ref, const vx_ba_options* opt,
                       int shard_rank, int shard_count, vx_ba_plan** out) {
+    return vx_ba_plan_create_ex(c, m, ref, has_ref, opt, shard_rank, shard_count, 0, out);
+}
+
+int vx_ba_plan_create_ex(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_ref, const vx_ba_options* opt,
+                         int shard_rank, int shard_count, int flags, vx_ba_plan** out) {
     if (!c || !out || !opt) return VX_ERR_INVALID;
     *out = nullptr;
     if (opt->max_iterations < 0 || opt->max_iterations > kMaxIter)
@@ -814,7 +818,7 @@ int vx_ba_plan_create(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_ref
     p->opt = *opt;
     p->shard_rank = shard_rank;
     p->shard_count = shard_count;
-    const int rc = build_plan(c, m, ref, has_ref, p);
+    const int rc = (flags & VX_PLAN_HOST_BUILD) ? build_plan(c, m, ref, has_ref, p) : build_plan_device(c, m, ref, has_ref, p);
     if (rc) {
         delete p;
         return rc;

@@ -1,0 +1,36 @@
+// ba_plan.hpp — the LocalBA plan (vx_ba_plan) shared by its two builders: the host reference
+// build (ba.hip, build_plan) and the device build (ba_window.hip, build_plan_device).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "vx_internal.hpp"
+
+struct vx_ba_plan {
+    vx_ctx* c = nullptr;
+    vx_ba_options opt{};
+    int status = 1;
+    int shard_rank = 0, shard_count = 1;
+    int n_window_kf = 0, n_landmarks_global = 0;
+    int n_kf = 0, n_opt = 0, n_lm = 0;
+    int64_t n_pose_obs = 0, n_lm_obs = 0;
+    std::vector<int> kf_map_idx, lm_map_idx;
+    int n_split = 1;
+    vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags, kf_obs_ptr, kf_part, kf_cost, lm_pos0, lm_pos,
+        pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_lm, lm_blk, lobs_uv, state;
+    int n_lm_blocks = 1;
+    bool ran = false;
+    vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
+};
+
+namespace vx {
+constexpr int kBaPoseBlock = 512;  // k_pose_kf threads per workgroup (ba.hip kPoseBlock)
+constexpr int kBaLmBlock = 512;    // k_landmark_solve observations / landmarks per workgroup
+constexpr int kBaMaxSplit = 4;     // pose-stage workgroups per keyframe
+
+int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p);
+// SelectKeyFrames + landmark set + both CSRs built on the device from the map snapshot (§8f rank 2)
+int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
+// greedy k_landmark_solve workgroup packing over the landmark-stage CSR pointers
+std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt);
+}  // namespace vx

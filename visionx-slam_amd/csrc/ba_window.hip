@@ -1,0 +1,451 @@
+// ba_window.hip — LocalBA window / landmark set / CSR build on the device.
+//
+// The host build of a vx_ba_plan (ba.hip, build_plan) restates local_ba.cpp:42-108 and the
+// per-observation checks of :126-138 and :186-204 with hash maps over the snapshot: 7.4 ms at C3,
+// 24 ms at C4 on one core — two orders of magnitude above the GPU frame.  Here the host only
+// sorts the keyframe ids (SelectKeyFrames) and gathers the window keyframes' feature ranges; the
+// landmark join, the optimised-landmark filter, the slot assignment and both CSRs are device
+// kernels over the snapshot:
+//   k_ht_insert    landmark id -> map index, open-addressing hash table (ids are unique)
+//   k_feat_scan    per window feature: its landmark (hash probe), referenced-by-window mark,
+//                  pose-stage validity (has_landmark, !is_outlier, exists, !bad, owned, camera)
+//   k_lm_flags     per landmark: optimised = referenced && !bad && total observations >= min,
+//                  owned by this shard (splitmix64(id) mod N)
+//   (scan)         optimised owned landmarks -> slots 0.. in map-index order (std::sort order)
+//   k_first_occ    first pose observation of each non-optimised landmark (atomicMin)
+//   (scan)         those landmarks -> slots n_opt.. in first-occurrence order (the host build
+//                  numbers them as its keyframe-major pose scan meets them)
+//   (scan)         pose-stage CSR positions; k_pose_fill writes (uv, slot) and kf_obs_ptr
+//   k_lobs_count / (scan) / k_lobs_fill   landmark-stage CSR: each optimised landmark's
+//                  observations whose keyframe is in the window (binary search over the sorted
+//                  window ids), with a camera, a feature index in range and a feature that is a
+//                  non-outlier observation of this landmark — in observation order
+//   k_lm_gather    initial positions by slot
+// The result is the same plan, array for array, as the host build (tests compare the runs
+// bitwise).  Scans are rocPRIM's device exclusive scan.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include <rocprim/rocprim.hpp>
+
+#include "vx_internal.hpp"
+#include "ba_common.hpp"
+#include "ba_plan.hpp"
+
+namespace vx {
+namespace {
+
+constexpr int kT = 256;
+constexpr uint64_t kEmpty = ~0ull;
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {  // splitmix64 (the shard hash as well)
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+struct WinArgs {
+    // window features (keyframe rows in ascending id order, features concatenated)
+    int nk, nf;
+    const int* wptr;          // nk + 1
+    const uint64_t* wlm;      // nf
+    const uint8_t* wfl;       // nf
+    const uint8_t* cam;       // nk
+    const uint64_t* wid;      // nk: window keyframe ids, ascending
+    // snapshot landmarks
+    int nl;
+    const uint64_t* lid;
+    const uint8_t* bad;
+    const int64_t* optr;      // nl + 1
+    const uint64_t* okf;
+    const uint64_t* ofi;
+    // hash table
+    uint64_t* hkey;
+    int* hval;
+    unsigned hmask;
+    int min_point, shard_rank, shard_count;
+    // per feature / per landmark scratch
+    int* f_lm;                // landmark map index or -1
+    int* f_pv;                // pose-stage valid (0/1)
+    int* f_first;             // first pose observation of a non-optimised landmark (0/1)
+    int* l_ref;
+    int* l_opt;               // optimised and owned (0/1)
+    int* l_slot;
+    int* l_first;             // first pose observation index (or INT_MAX)
+    unsigned* counts;         // [0] optimised landmarks over all shards
+};
+
+__device__ __forceinline__ int ht_find(const WinArgs& a, uint64_t key) {
+    unsigned h = (unsigned)mix(key) & a.hmask;
+    for (unsigned probe = 0; probe <= a.hmask; ++probe) {
+        const uint64_t k = a.hkey[h];
+        if (k == key) return a.hval[h];
+        if (k == kEmpty) return -1;
+        h = (h + 1) & a.hmask;
+    }
+    return -1;
+}
+
+__global__ __launch_bounds__(kT) void k_ht_insert(WinArgs a) {
+    const int l = blockIdx.x * kT + threadIdx.x;
+    if (l >= a.nl) return;
+    const uint64_t key = a.lid[l];
+    unsigned h = (unsigned)mix(key) & a.hmask;
+    for (;;) {
+        const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(&a.hkey[h]),
+                                                  (unsigned long long)kEmpty, (unsigned long long)key);
+        if (prev == kEmpty || prev == key) {
+            a.hval[h] = l;
+            return;
+        }
+        h = (h + 1) & a.hmask;
+    }
+}
+
+__device__ __forceinline__ int row_of_feature(const WinArgs& a, int f) {
+    int lo = 0, hi = a.nk - 1;  // last row with wptr[row] <= f
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.wptr[mid] <= f) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ bool owned(const WinArgs& a, uint64_t id) {
+    return a.shard_count <= 1 || (int)(mix(id) % (uint64_t)a.shard_count) == a.shard_rank;
+}
+
+__global__ __launch_bounds__(kT) void k_feat_scan(WinArgs a) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f >= a.nf) return;
+    const uint8_t fl = a.wfl[f];
+    int l = -1;
+    if (fl & 1) {
+        l = ht_find(a, a.wlm[f]);
+        if (l >= 0) a.l_ref[l] = 1;  // the window references it (local_ba.cpp:83-92)
+    }
+    a.f_lm[f] = l;
+    const int r = row_of_feature(a, f);
+    // pose-stage observation (local_ba.cpp:126-138)
+    a.f_pv[f] = (a.cam[r] && (fl & 1) && !(fl & 2) && l >= 0 && !a.bad[l] && owned(a, a.lid[l])) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kT) void k_lm_flags(WinArgs a) {
+    const int l = blockIdx.x * kT + threadIdx.x;
+    if (l >= a.nl) return;
+    const bool opt = a.l_ref[l] && !a.bad[l] && (a.optr[l + 1] - a.optr[l]) >= (int64_t)a.min_point;
+    if (opt) atomicAdd(&a.counts[0], 1u);
+    a.l_opt[l] = (opt && owned(a, a.lid[l])) ? 1 : 0;
+    a.l_first[l] = 0x7fffffff;
+}
+
+__global__ __launch_bounds__(kT) void k_opt_slots(WinArgs a, const int* scan, int* inv) {
+    const int l = blockIdx.x * kT + threadIdx.x;
+    if (l >= a.nl) return;
+    a.l_slot[l] = -1;
+    if (a.l_opt[l]) {
+        a.l_slot[l] = scan[l];
+        inv[scan[l]] = l;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_first_occ(WinArgs a) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f >= a.nf || !a.f_pv[f]) return;
+    const int l = a.f_lm[f];
+    if (!a.l_opt[l]) atomicMin(&a.l_first[l], f);
+}
+
+__global__ __launch_bounds__(kT) void k_is_first(WinArgs a) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f >= a.nf) return;
+    const int l = a.f_lm[f];
+    a.f_first[f] = (a.f_pv[f] && !a.l_opt[l] && a.l_first[l] == f) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(kT) void k_fixed_slots(WinArgs a, const int* scan, int n_opt, int* inv) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f >= a.nf || !a.f_first[f]) return;
+    const int l = a.f_lm[f];
+    a.l_slot[l] = n_opt + scan[f];
+    inv[n_opt + scan[f]] = l;
+}
+
+__global__ __launch_bounds__(kT) void k_pose_fill(WinArgs a, const int* pscan, const double* wuv, double2* puv,
+                                                  int* plm, int* kf_obs_ptr, int n_pose) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f < a.nf && a.f_pv[f]) {
+        const int o = pscan[f];
+        puv[o] = make_double2(wuv[2 * f], wuv[2 * f + 1]);
+        plm[o] = a.l_slot[a.f_lm[f]];
+    }
+    if (f <= a.nk) kf_obs_ptr[f] = f < a.nk ? pscan[a.wptr[f]] : n_pose;  // (wptr[nk] == nf)
+}
+
+// landmark-stage observation check (local_ba.cpp:186-204); returns the window feature or -1
+__device__ __forceinline__ int lobs_feature(const WinArgs& a, int l, int64_t o, int& row) {
+    const uint64_t kid = a.okf[o];
+    int lo = 0, hi = a.nk - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a.wid[mid] < kid) lo = mid + 1;
+        else hi = mid;
+    }
+    if (a.wid[lo] != kid) return -1;
+    row = lo;
+    if (!a.cam[lo]) return -1;
+    const uint64_t fi = a.ofi[o];
+    const int nfk = a.wptr[lo + 1] - a.wptr[lo];
+    if (fi >= (uint64_t)nfk) return -1;
+    const int f = a.wptr[lo] + (int)fi;
+    const uint8_t fl = a.wfl[f];
+    if (!(fl & 1) || (fl & 2) || a.wlm[f] != a.lid[l]) return -1;
+    return f;
+}
+
+__global__ __launch_bounds__(kT) void k_lobs_count(WinArgs a, const int* inv, int n_opt, int* cnt) {
+    const int s = blockIdx.x * kT + threadIdx.x;
+    if (s >= n_opt) return;
+    const int l = inv[s];
+    int c = 0, row;
+    for (int64_t o = a.optr[l]; o < a.optr[l + 1]; ++o) c += lobs_feature(a, l, o, row) >= 0 ? 1 : 0;
+    cnt[s] = c;
+}
+
+__global__ __launch_bounds__(kT) void k_lobs_fill(WinArgs a, const int* inv, int n_opt, const int* lptr,
+                                                  const double* wuv, int* lkf, int* llm, double2* luv) {
+    const int s = blockIdx.x * kT + threadIdx.x;
+    if (s >= n_opt) return;
+    const int l = inv[s];
+    int w = lptr[s], row = 0;
+    for (int64_t o = a.optr[l]; o < a.optr[l + 1]; ++o) {
+        const int f = lobs_feature(a, l, o, row);
+        if (f < 0) continue;
+        lkf[w] = row;
+        llm[w] = s;
+        luv[w] = make_double2(wuv[2 * f], wuv[2 * f + 1]);
+        ++w;
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_lm_gather(const int* inv, int n, const double* pos, double* lm0) {
+    const int s = blockIdx.x * kT + threadIdx.x;
+    if (s >= n) return;
+    const int l = inv[s];
+    lm0[4 * s] = pos[3 * l];
+    lm0[4 * s + 1] = pos[3 * l + 1];
+    lm0[4 * s + 2] = pos[3 * l + 2];
+    lm0[4 * s + 3] = 0.0;
+}
+
+inline unsigned grid(long long n) { return (unsigned)std::max(1ll, (n + kT - 1) / kT); }
+
+template <class T>
+int up(vx_ctx* c, DevBuf& d, const T* h, size_t n) {
+    VX_HIP(c, d.ensure(std::max<size_t>(1, n) * sizeof(T)));
+    if (n) VX_HIP(c, hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return VX_OK;
+}
+
+// exclusive scan of n ints (n + 1 outputs: the total at [n])
+int scan(vx_ctx* c, DevBuf& tmp, const int* in, int* out, int n) {
+    size_t bytes = 0;
+    VX_HIP(c, rocprim::exclusive_scan(nullptr, bytes, in, out, 0, (size_t)n + 1, rocprim::plus<int>(), c->stream));
+    VX_HIP(c, tmp.ensure(std::max<size_t>(bytes, 16)));
+    VX_HIP(c, rocprim::exclusive_scan(tmp.p, bytes, in, out, 0, (size_t)n + 1, rocprim::plus<int>(), c->stream));
+    return VX_OK;
+}
+
+}  // namespace
+
+int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p) {
+    const vx_ba_options& o = p->opt;
+    p->status = 1;
+    p->n_window_kf = 0;
+    p->n_landmarks_global = 0;
+    if (!m || m->n_kf <= 0) return VX_OK;
+    // ---- SelectKeyFrames (local_ba.cpp:42-62): host, over the keyframe ids only
+    std::vector<int> order(m->n_kf);
+    for (int i = 0; i < m->n_kf; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int x, int y) { return m->kf_id[x] < m->kf_id[y]; });
+    const int window = std::max(1, (int)o.window_size);
+    const uint64_t max_id = has_ref ? ref_kf_id : m->kf_id[order.back()];
+    std::vector<int> win;
+    for (int i = m->n_kf - 1; i >= 0 && (int)win.size() < window; --i)
+        if (m->kf_id[order[i]] <= max_id) win.push_back(order[i]);
+    std::reverse(win.begin(), win.end());
+    const int nk = (int)win.size();
+    p->n_window_kf = nk;
+    if (nk < 2) return VX_OK;
+    // ---- window feature gather + keyframe tables (host: contiguous copies per keyframe)
+    std::vector<int> wptr(nk + 1, 0);
+    for (int r = 0; r < nk; ++r) wptr[r + 1] = wptr[r] + (int)(m->kf_feat_ptr[win[r] + 1] - m->kf_feat_ptr[win[r]]);
+    const int nf = wptr[nk];
+    std::vector<double> wuv((size_t)nf * 2);
+    std::vector<uint64_t> wlm(nf), wid(nk);
+    std::vector<uint8_t> wfl(nf), cam(nk);
+    std::vector<double> pose0((size_t)nk * 8, 0.0), intr((size_t)nk * 4, 0.0);
+    std::vector<int> kf_flags(nk);
+    int64_t mx = 0;
+    for (int r = 0; r < nk; ++r) {
+        const int k = win[r];
+        const int64_t f0 = m->kf_feat_ptr[k], n = m->kf_feat_ptr[k + 1] - f0;
+        std::memcpy(&wuv[2 * (size_t)wptr[r]], m->feat_uv + 2 * f0, (size_t)n * 2 * sizeof(double));
+        std::memcpy(&wlm[wptr[r]], m->feat_lm_id + f0, (size_t)n * sizeof(uint64_t));
+        std::memcpy(&wfl[wptr[r]], m->feat_flags + f0, (size_t)n);
+        wid[r] = m->kf_id[k];
+        cam[r] = m->kf_has_cam[k] ? 1 : 0;
+        kf_flags[r] = cam[r];
+        for (int j = 0; j < 7; ++j) pose0[8 * r + j] = m->kf_pose[7 * k + j];
+        for (int j = 0; j < 4; ++j) intr[4 * r + j] = m->kf_intr[4 * k + j];
+        if (cam[r]) {
+            int64_t cnt = 0;
+            for (int64_t f = 0; f < n; ++f) cnt += wfl[wptr[r] + f] & 1;
+            mx = std::max(mx, cnt);
+        }
+    }
+    p->n_split = (int)std::min<int64_t>(kBaMaxSplit, std::max<int64_t>(1, (mx + kBaPoseBlock - 1) / kBaPoseBlock));
+    const int nl = m->n_lm;
+    const int64_t nobs = nl > 0 ? m->lm_obs_ptr[nl] : 0;
+    unsigned hcap = 1024;
+    while (hcap < 2u * (unsigned)std::max(nl, 1)) hcap <<= 1;
+
+    VX_HIP(c, hipSetDevice(c->device));
+    vx_ctx::PlanScratch& B = c->plan_scratch;  // reused across this context's plan builds
+    int rc;
+    if ((rc = up(c, B.wptr, wptr.data(), wptr.size()))) return rc;
+    if ((rc = up(c, B.wlm, wlm.data(), wlm.size()))) return rc;
+    if ((rc = up(c, B.wfl, wfl.data(), wfl.size()))) return rc;
+    if ((rc = up(c, B.cam, cam.data(), cam.size()))) return rc;
+    if ((rc = up(c, B.wid, wid.data(), wid.size()))) return rc;
+    if ((rc = up(c, B.wuv, wuv.data(), wuv.size()))) return rc;
+    if ((rc = up(c, B.lid, m->lm_id, (size_t)nl))) return rc;
+    if ((rc = up(c, B.bad, m->lm_bad, (size_t)nl))) return rc;
+    if ((rc = up(c, B.optr, m->lm_obs_ptr, (size_t)nl + 1))) return rc;
+    if ((rc = up(c, B.okf, m->obs_kf_id, (size_t)nobs))) return rc;
+    if ((rc = up(c, B.ofi, m->obs_feat_idx, (size_t)nobs))) return rc;
+    if ((rc = up(c, B.pos, m->lm_pos, (size_t)nl * 3))) return rc;
+    VX_HIP(c, B.hkey.ensure((size_t)hcap * 8));
+    VX_HIP(c, B.hval.ensure((size_t)hcap * 4));
+    VX_HIP(c, hipMemsetAsync(B.hkey.p, 0xff, (size_t)hcap * 8, c->stream));
+    const size_t fN = (size_t)std::max(nf, 1) + 1, lN = (size_t)std::max(nl, 1) + 1;
+    for (DevBuf* d : {&B.f_lm, &B.f_pv, &B.f_first, &B.scan_b}) VX_HIP(c, d->ensure(fN * 4));
+    for (DevBuf* d : {&B.l_ref, &B.l_opt, &B.l_slot, &B.l_first, &B.scan_a, &B.inv, &B.cnt, &B.scan_c})
+        VX_HIP(c, d->ensure(lN * 4));
+    VX_HIP(c, B.counts.ensure(64));
+    VX_HIP(c, hipMemsetAsync(B.l_ref.p, 0, lN * 4, c->stream));
+    VX_HIP(c, hipMemsetAsync(B.counts.p, 0, 64, c->stream));
+    VX_HIP(c, hipMemsetAsync(B.f_pv.p, 0, fN * 4, c->stream));      // [nf] = 0 for the scans
+    VX_HIP(c, hipMemsetAsync(B.f_first.p, 0, fN * 4, c->stream));
+    VX_HIP(c, hipMemsetAsync(B.l_opt.p, 0, lN * 4, c->stream));
+
+    WinArgs a{};
+    a.nk = nk;
+    a.nf = nf;
+    a.wptr = B.wptr.as<int>();
+    a.wlm = B.wlm.as<uint64_t>();
+    a.wfl = B.wfl.as<uint8_t>();
+    a.cam = B.cam.as<uint8_t>();
+    a.wid = B.wid.as<uint64_t>();
+    a.nl = nl;
+    a.lid = B.lid.as<uint64_t>();
+    a.bad = B.bad.as<uint8_t>();
+    a.optr = B.optr.as<int64_t>();
+    a.okf = B.okf.as<uint64_t>();
+    a.ofi = B.ofi.as<uint64_t>();
+    a.hkey = B.hkey.as<uint64_t>();
+    a.hval = B.hval.as<int>();
+    a.hmask = hcap - 1;
+    a.min_point = o.min_point_observations;
+    a.shard_rank = p->shard_rank;
+    a.shard_count = p->shard_count;
+    a.f_lm = B.f_lm.as<int>();
+    a.f_pv = B.f_pv.as<int>();
+    a.f_first = B.f_first.as<int>();
+    a.l_ref = B.l_ref.as<int>();
+    a.l_opt = B.l_opt.as<int>();
+    a.l_slot = B.l_slot.as<int>();
+    a.l_first = B.l_first.as<int>();
+    a.counts = B.counts.as<unsigned>();
+    hipStream_t s = c->stream;
+    hipLaunchKernelGGL(k_ht_insert, dim3(grid(nl)), dim3(kT), 0, s, a);
+    hipLaunchKernelGGL(k_feat_scan, dim3(grid(nf)), dim3(kT), 0, s, a);
+    hipLaunchKernelGGL(k_lm_flags, dim3(grid(nl)), dim3(kT), 0, s, a);
+    VX_LAUNCH_CHECK(c, "plan build kernels");
+    // optimised owned landmarks -> slots 0.. (map-index order)
+    int* opt_scan = B.scan_a.as<int>();
+    if ((rc = scan(c, B.tmp, a.l_opt, opt_scan, nl))) return rc;
+    int* inv = B.inv.as<int>();
+    hipLaunchKernelGGL(k_opt_slots, dim3(grid(nl)), dim3(kT), 0, s, a, opt_scan, inv);
+    hipLaunchKernelGGL(k_first_occ, dim3(grid(nf)), dim3(kT), 0, s, a);
+    hipLaunchKernelGGL(k_is_first, dim3(grid(nf)), dim3(kT), 0, s, a);
+    VX_LAUNCH_CHECK(c, "plan slot kernels");
+    int* first_scan = B.scan_b.as<int>();
+    if ((rc = scan(c, B.tmp, a.f_first, first_scan, nf))) return rc;
+    int hc[3] = {0, 0, 0};  // n_opt, n_fixed, n_landmarks_global
+    VX_HIP(c, hipMemcpyAsync(&hc[0], opt_scan + nl, 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(&hc[1], first_scan + nf, 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(&hc[2], B.counts.p, 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipStreamSynchronize(s));
+    p->n_landmarks_global = hc[2];
+    if (hc[2] == 0) return VX_OK;  // no optimised landmark anywhere (local_ba.cpp:106-108)
+    p->status = 0;
+    p->n_kf = nk;
+    p->kf_map_idx = win;
+    const int n_opt = hc[0], n_lm = hc[0] + hc[1];
+    p->n_opt = n_opt;
+    p->n_lm = n_lm;
+    hipLaunchKernelGGL(k_fixed_slots, dim3(grid(nf)), dim3(kT), 0, s, a, first_scan, n_opt, inv);
+    // pose-stage CSR
+    int* pscan = B.scan_b.as<int>();  // (first_scan consumed by k_fixed_slots above, stream-ordered)
+    if ((rc = scan(c, B.tmp, a.f_pv, pscan, nf))) return rc;
+    int n_pose = 0;
+    VX_HIP(c, hipMemcpyAsync(&n_pose, pscan + nf, 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipStreamSynchronize(s));
+    p->n_pose_obs = n_pose;
+    VX_HIP(c, p->pobs_uv.ensure((size_t)std::max(n_pose, 1) * sizeof(double2)));
+    VX_HIP(c, p->pobs_lm.ensure((size_t)std::max(n_pose, 1) * 4));
+    VX_HIP(c, p->kf_obs_ptr.ensure((size_t)(nk + 1) * 4));
+    hipLaunchKernelGGL(k_pose_fill, dim3(grid(std::max(nf, nk + 1))), dim3(kT), 0, s, a, pscan,
+                       (const double*)B.wuv.as<double>(), p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(),
+                       p->kf_obs_ptr.as<int>(), n_pose);
+    // landmark-stage CSR
+    int* cnt = B.cnt.as<int>();
+    VX_HIP(c, hipMemsetAsync(cnt + n_opt, 0, 4, s));
+    hipLaunchKernelGGL(k_lobs_count, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, cnt);
+    VX_LAUNCH_CHECK(c, "plan CSR kernels");
+    VX_HIP(c, p->lobs_ptr.ensure((size_t)(n_opt + 1) * 4));
+    if ((rc = scan(c, B.tmp, cnt, p->lobs_ptr.as<int>(), n_opt))) return rc;
+    std::vector<int> lptr(n_opt + 1);
+    std::vector<int> inv_h(std::max(n_lm, 1));
+    VX_HIP(c, hipMemcpyAsync(lptr.data(), p->lobs_ptr.p, (size_t)(n_opt + 1) * 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(inv_h.data(), inv, (size_t)n_lm * 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipStreamSynchronize(s));
+    const int n_lobs = lptr[n_opt];
+    p->n_lm_obs = n_lobs;
+    p->lm_map_idx.assign(inv_h.begin(), inv_h.begin() + n_lm);
+    VX_HIP(c, p->lobs_kf.ensure((size_t)std::max(n_lobs, 1) * 4));
+    VX_HIP(c, p->lobs_lm.ensure((size_t)std::max(n_lobs, 1) * 4));
+    VX_HIP(c, p->lobs_uv.ensure((size_t)std::max(n_lobs, 1) * sizeof(double2)));
+    hipLaunchKernelGGL(k_lobs_fill, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, p->lobs_ptr.as<int>(),
+                       (const double*)B.wuv.as<double>(), p->lobs_kf.as<int>(), p->lobs_lm.as<int>(),
+                       p->lobs_uv.as<double2>());
+    VX_HIP(c, p->lm_pos0.ensure((size_t)std::max(n_lm, 1) * 4 * sizeof(double)));
+    hipLaunchKernelGGL(k_lm_gather, dim3(grid(n_lm)), dim3(kT), 0, s, (const int*)inv, n_lm,
+                       (const double*)B.pos.as<double>(), p->lm_pos0.as<double>());
+    VX_LAUNCH_CHECK(c, "plan fill kernels");
+    const std::vector<int> blk = pack_lm_blocks(lptr, n_opt);
+    p->n_lm_blocks = (int)blk.size() - 1;
+    if ((rc = up(c, p->lm_blk, blk.data(), blk.size()))) return rc;
+    if ((rc = up(c, p->kf_pose0, pose0.data(), pose0.size()))) return rc;
+    if ((rc = up(c, p->kf_intr, intr.data(), intr.size()))) return rc;
+    if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
+    if ((rc = alloc_run_buffers(c, p))) return rc;
+    VX_HIP(c, hipStreamSynchronize(s));  // the host vectors above must outlive their async copies
+    return VX_OK;
+}
+
+}  // namespace vx

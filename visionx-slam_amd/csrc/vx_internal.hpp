@@ -179,6 +179,12 @@ struct vx_ctx {
     // ---- landmark creation (landmarks.hip): inputs, per-item flags / points, compacted outputs
     vx::DevBuf lm_in0, lm_in1, lm_in2, lm_in3, lm_in4, lm_depth, lm_valid, lm_pw, lm_index, lm_out, lm_count, lm_aux;
 
+    // ---- device-side LocalBA plan build scratch (ba_window.hip)
+    struct PlanScratch {
+        vx::DevBuf wptr, wlm, wfl, cam, wid, wuv, lid, bad, optr, okf, ofi, pos, hkey, hval, f_lm, f_pv, f_first,
+            l_ref, l_opt, l_slot, l_first, counts, scan_a, scan_b, scan_c, inv, cnt, tmp;
+    } plan_scratch;
+
     // ---- hipGraph replay of the async entry points ($VX_GRAPHS=0 disables)
     vx::GraphCache graphs;
     bool use_graphs = true;

@@ -83,7 +83,7 @@ EXPORTS = [
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
-    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts", "vx_create_ex", "vx_device_cus",
+    "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts", "vx_create_ex", "vx_device_cus", "vx_ba_plan_create_ex",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
@@ -343,8 +343,9 @@ class Context:
                                              0 if ref is None else 1, C.byref(opts), C.byref(st)))
         return st
 
-    def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1):
-        return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
+    def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1,
+                host_build=False):
+        return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count, host_build)
 
     def graph_enable(self, on=True):
         self._check(lib().vx_graph_enable(self._h, 1 if on else 0))
@@ -442,16 +443,18 @@ class Context:
 class BAPlan:
     """vx_ba_plan: host window selection + device CSR upload, repeatable device runs."""
 
-    def __init__(self, ctx: Context, m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1):
+    def __init__(self, ctx: Context, m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1, host_build=False):
+        """host_build: the host reference build of the plan (VX_PLAN_HOST_BUILD) instead of the
+        device build."""
         self.ctx = ctx
         self.m = m
         self.opts = opts or default_ba_options(window=m.get("window", 5))
         ref = m.get("ref_kf_id") if ref_kf_id is None else ref_kf_id
         self._h = C.c_void_p()
         v = map_view(m)
-        ctx._check(lib().vx_ba_plan_create(ctx.handle, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
-                                           0 if ref is None else 1, C.byref(self.opts), shard_rank,
-                                           shard_count, C.byref(self._h)))
+        ctx._check(lib().vx_ba_plan_create_ex(ctx.handle, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
+                                              0 if ref is None else 1, C.byref(self.opts), shard_rank,
+                                              shard_count, 1 if host_build else 0, C.byref(self._h)))
 
     def info(self):
         out = np.zeros(8, np.int64)
