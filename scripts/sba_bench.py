@@ -1,0 +1,45 @@
+"""Schur-complement joint BA (vx_sba_*) on one MI355X: C3 window (50 KF / 20k landmarks) and the C5
+global window (8 camera streams x 25 KF = 200 KF, 100k landmarks: 8 covisibility components, one
+dense MFMA solve each).  Prints one JSON line per config: ms per optimisation (K replays of the
+resident plan, 8 Levenberg-Marquardt iterations max), iterations, cost, per-kernel us (HIP events,
+separate pass), plan-build ms (host)."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
+import vxslam  # noqa: E402
+from vxslam import synth  # noqa: E402
+
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+ctx = vxslam.Context(0)
+for cfg, (nk, nl, ns) in [("C3", synth.ba_config("C3")), ("C5", synth.ba_config("C5"))]:
+    m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
+    opts = vxslam.default_sba_options(window=nk, iters=8)
+    t0 = time.perf_counter()
+    plan = ctx.sba_plan(m, opts)
+    build_ms = 1e3 * (time.perf_counter() - t0)
+    for _ in range(3):
+        plan.run_async()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        plan.run_async()
+    ctx.synchronize()
+    ms = 1e3 * (time.perf_counter() - t0) / K
+    st = plan.fetch()
+    ctx.prof_enable(True)
+    plan.run_async()
+    plan.fetch()
+    prof = ctx.prof_read()
+    ctx.prof_enable(False)
+    print(json.dumps({"config": cfg, "window_kf": nk, "landmarks": nl, "streams": ns, "plan": plan.info(),
+                      "ms_per_optimize": round(ms, 4), "iterations": st.iterations, "accepted": st.accepted,
+                      "cost": [round(st.initial_cost, 1), round(st.final_cost, 1)],
+                      "plan_build_ms_host": round(build_ms, 2),
+                      "kernel_us_per_launch": {k: round(v[0] * 1e3 / v[1], 2) for k, v in prof.items()
+                                               if k.startswith("sba") and v[1]}}), flush=True)
+    plan.close()
+ctx.close()
