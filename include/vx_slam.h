@@ -19,6 +19,8 @@
  *   vx_depth_landmarks    <- Tracking::CreateLandmarksFromDepth  core/frontend/tracking.cpp:586-650
  *   vx_triangulate        <- Tracking::TriangulateWithLastKeyFrame + TriangulatePoint
  *                                                                core/frontend/tracking.cpp:856-945
+ *   vx_pnp_ransac         <- cv::solvePnPRansac in Tracking::TrackWithPnP
+ *                                                                core/frontend/tracking.cpp:414-423
  *   vx_sba_*              (no reference counterpart: north_star's Schur-complement dense solve)
  *
  * The host-side C++ adapters that keep the reference call surface (same class names and
@@ -303,6 +305,48 @@ int vx_triangulate(vx_ctx* ctx, const double* uv1, const uint8_t* has1, int n1, 
                    const double* intr2, const double* pose2, const vx_match* matches, int n_matches,
                    double min_angle_deg, double max_reproj_error, int32_t* out_index, double* out_pw,
                    int* n_created);
+
+/* ---------------------------------------------------------------- geometry RANSAC (ransac.hip)
+ * <- cv::solvePnPRansac(pts_3d, pts_2d, K, noArray(), rvec, tvec, false, iterations,
+ *    max_reproj_error, 0.99, inliers) in Tracking::TrackWithPnP (tracking.cpp:414-423).
+ * All hypotheses are generated and scored at once on the device; the sequential RANSAC loop's
+ * adaptive stop rule (RANSACUpdateNumIters) is then replayed over them in order, so the selected
+ * model is the one a sequential run over the same hypothesis stream keeps.  Minimal solver: P3P
+ * (Grunert) on 3 points, the 4th of the sample picks among its up to 4 solutions; hypotheses come
+ * from a counter-based splitmix64 stream (OpenCV's cv::RNG stream and its EPnP kernel are not
+ * reproduced: parity against OpenCV is unpinned).  Inliers: point in front of the
+ * camera and squared reprojection error <= reproj_error^2.  The kept model is refined on its
+ * inliers by Levenberg-Marquardt (the SOLVEPNP_ITERATIVE refinement solvePnPRansac runs). */
+typedef struct {
+    int32_t max_iterations;    /* iterationsCount (tracking.cpp:420: min(100, 2 * n)), <= 4096 */
+    int32_t refine_iterations; /* LM iterations on the inliers (0: keep the RANSAC model) */
+    double reproj_error;       /* reprojectionError, px (Tracking::Options::max_reproj_error 2.0) */
+    double confidence;         /* 0.99 (tracking.cpp:423) */
+    uint64_t seed;             /* hypothesis stream */
+} vx_pnp_options;
+typedef struct {
+    int32_t ok;                /* solvePnPRansac's return value */
+    int32_t n_inliers;         /* inliers.rows */
+    int32_t best_hypothesis;   /* index of the kept hypothesis, -1 when !ok */
+    int32_t hypotheses_run;    /* hypotheses the adaptive stop rule let the loop evaluate */
+    int32_t refine_iterations; /* LM iterations performed */
+    int32_t reserved;
+    double rvec[3], tvec[3];   /* T_cw as cv::Rodrigues vector + translation */
+    double pose[7];            /* the same T_cw as Sophus storage: qx qy qz qw tx ty tz */
+    double cost0, cost;        /* sum of squared reprojection errors over the inliers, before / after LM */
+} vx_pnp_result;
+/* tracking.cpp:420-423 defaults for n correspondences: min(100, 2n) iterations, 2.0 px, 0.99, 20 LM */
+void vx_pnp_default_options(int n_points, vx_pnp_options* out);
+/* obj_pts: 3 floats per correspondence (cv::Point3f), img_pts: 2 floats (cv::Point2f), intr4: fx fy
+ * cx cy (no distortion, as the reference passes cv::Mat()).  inlier_mask (n bytes) may be NULL. */
+int vx_pnp_ransac(vx_ctx* ctx, const float* obj_pts, const float* img_pts, int n, const double* intr4,
+                  const vx_pnp_options* opt, uint8_t* inlier_mask, vx_pnp_result* out);
+/* Independent problems in one pass (e.g. the C5 rig's 8 camera streams): problem p owns
+ * correspondences [offsets[p], offsets[p+1]), intrinsics intr4[4p..], options opt[p]; inlier_mask
+ * covers all offsets[n_problems] correspondences; out[p] per problem. */
+int vx_pnp_ransac_batch(vx_ctx* ctx, int n_problems, const int32_t* offsets, const float* obj_pts,
+                        const float* img_pts, const double* intr4, const vx_pnp_options* opt,
+                        uint8_t* inlier_mask, vx_pnp_result* out);
 
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);

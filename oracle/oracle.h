@@ -155,6 +155,27 @@ int orc_triangulate(const double* uv1, const uint8_t* has1, int n1, const double
                     const orc_match* matches, int n_matches, double min_angle_deg, double max_reproj_error,
                     int32_t* out_index, double* out_pw, int* n_created);
 
+/* ---- PnP RANSAC (ransac_oracle.cpp), same contract and struct layout as vx_slam.h's vx_pnp_* */
+#define ORC_PNP_MAX_HYP 4096
+typedef struct {
+    int32_t max_iterations, refine_iterations;
+    double reproj_error, confidence;
+    uint64_t seed;
+} orc_pnp_options;
+typedef struct {
+    int32_t ok, n_inliers, best_hypothesis, hypotheses_run, refine_iterations, reserved;
+    double rvec[3], tvec[3], pose[7], cost0, cost;
+} orc_pnp_result;
+int orc_pnp_ransac_batch(int n_problems, const int32_t* offsets, const float* obj, const float* img,
+                         const double* intr4, const orc_pnp_options* opt, uint8_t* mask, orc_pnp_result* out);
+/* pieces, for the numpy pins: hypothesis h's model (1 = valid), P3P on 3 world points + unit
+ * bearings (up to 4 solutions), real roots of a degree <= 4 polynomial, RANSACUpdateNumIters */
+int orc_pnp_hypothesis(const float* obj, const float* img, int n, const double* intr4, uint64_t seed, int h,
+                       double* R9, double* t3);
+int orc_p3p(const double* P9, const double* f9, double* R72, double* t24);  /* up to 8 candidates */
+int orc_poly_roots(const double* c, int d, double* out);
+int orc_pnp_update_iters(double p, double ep, int max_iters);
+
 #ifdef __cplusplus
 }
 #endif

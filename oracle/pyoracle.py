@@ -304,3 +304,72 @@ def triangulate(d, min_angle_deg=1.0, max_err=5.0, intr1=None, intr2=None):
                                C.c_double(min_angle_deg), C.c_double(max_err), _p(idx), _p(pw), C.byref(cnt))
     assert rc == 0, rc
     return idx[:nm].copy(), pw[:cnt.value].copy()
+
+
+# ---------------------------------------------------------------------------- PnP RANSAC
+PNP_OPTIONS_DTYPE = np.dtype([("max_iterations", "<i4"), ("refine_iterations", "<i4"), ("reproj_error", "<f8"),
+                              ("confidence", "<f8"), ("seed", "<u8")])
+PNP_RESULT_DTYPE = np.dtype([("ok", "<i4"), ("n_inliers", "<i4"), ("best_hypothesis", "<i4"),
+                             ("hypotheses_run", "<i4"), ("refine_iterations", "<i4"), ("reserved", "<i4"),
+                             ("rvec", "<f8", 3), ("tvec", "<f8", 3), ("pose", "<f8", 7), ("cost0", "<f8"),
+                             ("cost", "<f8")])
+
+
+def pnp_options(n, max_iterations=None, reproj_error=2.0, confidence=0.99, seed=0x5EED, refine_iterations=20):
+    """Tracking::TrackWithPnP's solvePnPRansac arguments (tracking.cpp:420-423)."""
+    o = np.zeros((), PNP_OPTIONS_DTYPE)
+    o["max_iterations"] = min(100, 2 * n) if max_iterations is None else max_iterations
+    o["refine_iterations"] = refine_iterations
+    o["reproj_error"] = reproj_error
+    o["confidence"] = confidence
+    o["seed"] = seed
+    return o
+
+
+def pnp_ransac_batch(offsets, obj, img, intr, opts):
+    """Restated PnP RANSAC over independent problems: (results[P], mask[N])."""
+    offsets = np.ascontiguousarray(offsets, np.int32)
+    obj = np.ascontiguousarray(obj, np.float32)
+    img = np.ascontiguousarray(img, np.float32)
+    intr = np.ascontiguousarray(intr, np.float64)
+    opts = np.ascontiguousarray(opts, PNP_OPTIONS_DTYPE)
+    P = len(offsets) - 1
+    out = np.zeros(P, PNP_RESULT_DTYPE)
+    mask = np.zeros(max(int(offsets[-1]), 1), np.uint8)
+    assert lib().orc_pnp_ransac_batch(P, _p(offsets), _p(obj), _p(img), _p(intr), _p(opts), _p(mask), _p(out)) == 0
+    return out, mask[:offsets[-1]].copy()
+
+
+def pnp_ransac(obj, img, intr, opt):
+    out, mask = pnp_ransac_batch(np.array([0, len(obj)]), obj, img, intr, np.atleast_1d(opt))
+    return out[0], mask
+
+
+def pnp_hypothesis(obj, img, intr, seed, h):
+    obj = np.ascontiguousarray(obj, np.float32)
+    img = np.ascontiguousarray(img, np.float32)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    ok = lib().orc_pnp_hypothesis(_p(obj), _p(img), len(obj), _p(np.ascontiguousarray(intr, np.float64)),
+                                  C.c_uint64(seed), h, _p(R), _p(t))
+    return (R.reshape(3, 3), t) if ok else None
+
+
+def p3p(P, f):
+    P = np.ascontiguousarray(P, np.float64)
+    f = np.ascontiguousarray(f, np.float64)
+    R = np.zeros(72)
+    t = np.zeros(24)
+    ns = lib().orc_p3p(_p(P), _p(f), _p(R), _p(t))
+    return [(R[9 * s:9 * s + 9].reshape(3, 3), t[3 * s:3 * s + 3].copy()) for s in range(ns)]
+
+
+def poly_roots(c):
+    c = np.ascontiguousarray(c, np.float64)
+    out = np.zeros(4)
+    n = lib().orc_poly_roots(_p(c), len(c) - 1, _p(out))
+    return out[:n].copy()
+
+
+def pnp_update_iters(p, ep, max_iters):
+    return lib().orc_pnp_update_iters(C.c_double(p), C.c_double(ep), max_iters)

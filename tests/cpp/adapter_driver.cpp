@@ -7,6 +7,7 @@
 //   adapter_driver ba <dir> <window> <iters> <ref_id or -1> [flatten]
 //   adapter_driver depth <dir>                     (KeyFrameLandmarks::CreateLandmarksFromDepth)
 //   adapter_driver triangulate <dir> <min_deg> <max_err>   (TriangulateWithLastKeyFrame)
+//   adapter_driver pnp <dir> <iterations> <reproj_err>    (solvePnPRansac as TrackWithPnP calls it)
 #include <cstdio>
 #include <cstdlib>
 #include <climits>
@@ -18,6 +19,7 @@
 #include <vector>
 
 #include "visionx/feature.h"
+#include "visionx/geometry.h"
 #include "visionx/mapping.h"
 
 using namespace visionx;
@@ -259,6 +261,30 @@ static int cmd_triangulate(char** a) {
     return 0;
 }
 
+// obj.bin (float x3), img.bin (float x2), intr.bin (fx fy cx cy) -> prints ok and the inlier count,
+// writes pose.out (rvec, tvec, then the SE3d qx qy qz qw tx ty tz) and inliers.out (int32 indices)
+static int cmd_pnp(char** a) {
+    const std::string dir = a[0];
+    const auto obj = read_bin<float>(dir + "/obj.bin");
+    const auto img = read_bin<float>(dir + "/img.bin");
+    const auto intr = read_bin<double>(dir + "/intr.bin");
+    std::vector<Point3f> pts_3d;
+    std::vector<Point2f> pts_2d;
+    for (size_t i = 0; i + 2 < obj.size(); i += 3) pts_3d.emplace_back(obj[i], obj[i + 1], obj[i + 2]);
+    for (size_t i = 0; i + 1 < img.size(); i += 2) pts_2d.emplace_back(img[i], img[i + 1]);
+    Camera cam(intr[0], intr[1], intr[2], intr[3]);
+    Vec3d rvec, tvec;
+    std::vector<int> inliers;
+    const bool ok = SolvePnPRansac(pts_3d, pts_2d, cam, rvec, tvec, false, std::atoi(a[1]), (float)std::atof(a[2]),
+                                   0.99, &inliers);
+    const SE3d T = PoseFromRvecTvec(rvec, tvec);
+    write_bin(dir + "/pose.out", std::vector<double>{rvec.x, rvec.y, rvec.z, tvec.x, tvec.y, tvec.z, T.qx, T.qy,
+                                                     T.qz, T.qw, T.tx, T.ty, T.tz});
+    write_bin(dir + "/inliers.out", std::vector<int32_t>(inliers.begin(), inliers.end()));
+    std::printf("%d %zu\n", ok ? 1 : 0, inliers.size());
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     const std::string cmd = argv[1];
@@ -268,6 +294,7 @@ int main(int argc, char** argv) {
         if (cmd == "ba" && argc >= 6) return cmd_ba(argc - 2, argv + 2);
         if (cmd == "depth" && argc >= 3) return cmd_depth(argv + 2);
         if (cmd == "triangulate" && argc >= 5) return cmd_triangulate(argv + 2);
+        if (cmd == "pnp" && argc >= 5) return cmd_pnp(argv + 2);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;

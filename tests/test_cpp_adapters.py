@@ -160,3 +160,24 @@ def test_adapter_triangulate(driver, oracle, tmp_path):
     assert np.abs(lm[:, 1:4] - pw).max() <= 1e-9 * np.abs(pw).max() and (lm[:, 4] == 2).all()
     assert np.array_equal(f1[m["query_idx"][made]], (100 + idx[made]).astype(np.uint64))
     assert np.array_equal(f2[m["train_idx"][made]], (100 + idx[made]).astype(np.uint64))
+
+
+@pytest.mark.gpu
+def test_adapter_pnp_ransac(driver, oracle, tmp_path):
+    """SolvePnPRansac as Tracking::TrackWithPnP calls cv::solvePnPRansac (tracking.cpp:414-447):
+    min(100, 2n) iterations, 2 px, 0.99; inliers ascending; pose via Rodrigues -> SE3d."""
+    d = synth.make_pnp_problem(77, 800, outlier_frac=0.35)
+    p = str(tmp_path)
+    d["obj"].tofile(os.path.join(p, "obj.bin"))
+    d["img"].tofile(os.path.join(p, "img.bin"))
+    d["intr"].tofile(os.path.join(p, "intr.bin"))
+    ok, n_in = map(int, run(driver, "pnp", p, 100, 2.0))
+    o = oracle.pnp_options(800, max_iterations=100, reproj_error=2.0)
+    o["seed"] = 0x5EED  # vx_pnp_default_options
+    r, mask = oracle.pnp_ransac(d["obj"], d["img"], d["intr"], o)
+    assert ok == r["ok"] == 1 and n_in == r["n_inliers"]
+    inl = np.fromfile(os.path.join(p, "inliers.out"), np.int32)
+    assert np.array_equal(inl, np.nonzero(mask)[0])
+    pose = np.fromfile(os.path.join(p, "pose.out"), np.float64)
+    assert np.abs(pose[:3] - r["rvec"]).max() < 1e-9 and np.abs(pose[3:6] - r["tvec"]).max() < 1e-9
+    assert np.abs(pose[6:] - r["pose"]).max() < 1e-9

@@ -45,6 +45,8 @@ enum Stage : int {
     kStLmDepth,
     kStLmTriangulate,
     kStLmCompact,
+    kStPnpHyp,
+    kStPnpRefine,
     kStCount
 };
 
@@ -178,6 +180,11 @@ struct vx_ctx {
 
     // ---- landmark creation (landmarks.hip): inputs, per-item flags / points, compacted outputs
     vx::DevBuf lm_in0, lm_in1, lm_in2, lm_in3, lm_in4, lm_depth, lm_valid, lm_pw, lm_index, lm_out, lm_count, lm_aux;
+
+    // ---- PnP RANSAC (ransac.hip): packed inputs (pinned staging + device), hypothesis records,
+    // packed outputs (results + inlier mask)
+    vx::PinnedBuf rs_host, rs_host_out;
+    vx::DevBuf rs_in, rs_hyp, rs_out;
 
     // ---- device-side LocalBA plan build scratch (ba_window.hip)
     struct PlanScratch {

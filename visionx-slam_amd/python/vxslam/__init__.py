@@ -127,6 +127,7 @@ def lib():
         L.vx_sba_plan_destroy.argtypes = [C.c_void_p]
         L.vx_sba_plan_destroy.restype = None
         L.vx_sba_default_options.restype = None
+        L.vx_pnp_default_options.restype = None
         L.vx_ba_shard_of.restype = C.c_uint32
         L.vx_ba_shard_of.argtypes = [C.c_uint64, C.c_int]
         _lib = L
@@ -135,6 +136,28 @@ def lib():
 
 def _p(a):
     return C.c_void_p(a.ctypes.data)
+
+
+# vx_pnp_options / vx_pnp_result (include/vx_slam.h) as numpy records
+PNP_OPTIONS_DTYPE = np.dtype([("max_iterations", "<i4"), ("refine_iterations", "<i4"), ("reproj_error", "<f8"),
+                              ("confidence", "<f8"), ("seed", "<u8")])
+PNP_RESULT_DTYPE = np.dtype([("ok", "<i4"), ("n_inliers", "<i4"), ("best_hypothesis", "<i4"),
+                             ("hypotheses_run", "<i4"), ("refine_iterations", "<i4"), ("reserved", "<i4"),
+                             ("rvec", "<f8", 3), ("tvec", "<f8", 3), ("pose", "<f8", 7), ("cost0", "<f8"),
+                             ("cost", "<f8")])
+
+
+def pnp_options(n, max_iterations=None, reproj_error=2.0, confidence=0.99, seed=0x5EED, refine_iterations=20):
+    """solvePnPRansac's arguments in Tracking::TrackWithPnP (tracking.cpp:420-423) for n pairs."""
+    o = np.zeros((), PNP_OPTIONS_DTYPE)
+    lib().vx_pnp_default_options(int(n), _p(o))
+    if max_iterations is not None:
+        o["max_iterations"] = max_iterations
+    o["refine_iterations"] = refine_iterations
+    o["reproj_error"] = reproj_error
+    o["confidence"] = confidence
+    o["seed"] = seed
+    return o
 
 
 def default_orb_params(n_features=1000, scale_factor=1.2, n_levels=8, fast_threshold=20,
@@ -391,6 +414,35 @@ class Context:
                                          _p(d["pose2"]), _p(m), nm, C.c_double(min_angle_deg), C.c_double(max_err),
                                          _p(idx), _p(pw), C.byref(cnt)))
         return idx[:nm].copy(), pw[:cnt.value].copy()
+
+    def pnp_ransac_batch(self, offsets, obj, img, intr, opts):
+        """cv::solvePnPRansac (Tracking::TrackWithPnP, tracking.cpp:414-423) on the GPU for independent
+        problems: problem p owns rows offsets[p]:offsets[p+1] of obj (float32 x3) / img (float32 x2),
+        intr[p] = fx fy cx cy, opts[p] a PNP_OPTIONS_DTYPE record.  Returns (results[P], mask[N])."""
+        offsets = np.ascontiguousarray(offsets, np.int32)
+        obj = np.ascontiguousarray(obj, np.float32).reshape(-1, 3)
+        img = np.ascontiguousarray(img, np.float32).reshape(-1, 2)
+        intr = np.ascontiguousarray(intr, np.float64).reshape(-1, 4)
+        opts = np.ascontiguousarray(np.atleast_1d(opts), PNP_OPTIONS_DTYPE)
+        P = len(offsets) - 1
+        n = int(offsets[-1])
+        assert len(obj) == n and len(img) == n and len(intr) == P and len(opts) == P
+        out = np.zeros(max(P, 1), PNP_RESULT_DTYPE)
+        mask = np.zeros(max(n, 1), np.uint8)
+        self._check(lib().vx_pnp_ransac_batch(self._h, P, _p(offsets), _p(obj), _p(img), _p(intr), _p(opts),
+                                              _p(mask), _p(out)))
+        return out[:P].copy(), mask[:n].copy()
+
+    def pnp_ransac(self, obj, img, intr, opt):
+        """One solvePnPRansac call: (result record, inlier mask)."""
+        obj = np.ascontiguousarray(obj, np.float32).reshape(-1, 3)
+        img = np.ascontiguousarray(img, np.float32).reshape(-1, 2)
+        intr = np.ascontiguousarray(intr, np.float64)
+        opt = np.ascontiguousarray(opt, PNP_OPTIONS_DTYPE)
+        out = np.zeros(1, PNP_RESULT_DTYPE)
+        mask = np.zeros(max(len(obj), 1), np.uint8)
+        self._check(lib().vx_pnp_ransac(self._h, _p(obj), _p(img), len(obj), _p(intr), _p(opt), _p(mask), _p(out)))
+        return out[0], mask[:len(obj)].copy()
 
     def sba_optimize(self, m, opts: SBAOptions | None = None, ref_kf_id=None) -> SBAStats:
         """Schur-complement joint BA (vx_sba_optimize_map) on a synth.BAMap, in place."""

@@ -340,3 +340,29 @@ def make_keyframe_pair(seed: int, n: int = 2000, *, width: int = 640, height: in
     return {"uv1": np.ascontiguousarray(uv1), "has1": has1, "uv2": np.ascontiguousarray(uv2), "has2": has2,
             "intr": np.array(intr, np.float64), "pose1": pose1, "pose2": pose2, "matches": matches,
             "depth": np.ascontiguousarray(depth), "pw_true": pw, "inv": inv}
+
+
+def make_pnp_problem(seed: int, n: int = 1000, *, outlier_frac: float = 0.3, noise_px: float = 0.5,
+                     width: int = 640, height: int = 480, intr=(FX, FY, CX, CY), z_range=(1.0, 6.0)):
+    """3D-2D correspondences as Tracking::TrackWithPnP builds them (tracking.cpp:364-401:
+    cv::Point3f landmark positions, cv::Point2f current-frame feature positions): points seen by a
+    camera at a random T_cw, pixel noise, a fraction of wrong matches (random pixels).  Returns a
+    dict: obj (n x 3 float32), img (n x 2 float32), intr, pose (T_cw qx qy qz qw tx ty tz),
+    R, t, outlier (bool per correspondence)."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = intr
+    u = rng.uniform(0, width, n)
+    v = rng.uniform(0, height, n)
+    z = rng.uniform(z_range[0], z_range[1], n)
+    pc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], -1)
+    q = quat_from_rotvec(rng.normal(0, 0.3, 3))
+    R = quat_to_mat(q)
+    t = rng.normal(0, 0.5, 3)
+    pw = (pc - t) @ R  # R^T (pc - t)
+    uv = np.stack([u, v], -1) + rng.normal(0, noise_px, (n, 2))
+    out = rng.random(n) < outlier_frac
+    uv[out] = np.stack([rng.uniform(0, width, out.sum()), rng.uniform(0, height, out.sum())], -1)
+    if q[3] < 0:
+        q = -q
+    return {"obj": pw.astype(np.float32), "img": uv.astype(np.float32), "intr": np.array(intr, np.float64),
+            "pose": np.concatenate([q, t]), "R": R, "t": t, "outlier": out}
