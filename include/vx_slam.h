@@ -21,6 +21,8 @@
  *                                                                core/frontend/tracking.cpp:856-945
  *   vx_pnp_ransac         <- cv::solvePnPRansac in Tracking::TrackWithPnP
  *                                                                core/frontend/tracking.cpp:414-423
+ *   vx_essential_ransac   <- cv::findEssentialMat + cv::recoverPose in
+ *                            Tracking::EstimatePoseByEssential   core/frontend/tracking.cpp:503-547
  *   vx_sba_*              (no reference counterpart: north_star's Schur-complement dense solve)
  *
  * The host-side C++ adapters that keep the reference call surface (same class names and
@@ -347,6 +349,42 @@ int vx_pnp_ransac(vx_ctx* ctx, const float* obj_pts, const float* img_pts, int n
 int vx_pnp_ransac_batch(vx_ctx* ctx, int n_problems, const int32_t* offsets, const float* obj_pts,
                         const float* img_pts, const double* intr4, const vx_pnp_options* opt,
                         uint8_t* inlier_mask, vx_pnp_result* out);
+
+/* <- E = cv::findEssentialMat(pts_last, pts_curr, K, cv::RANSAC, 0.999, 1.0, mask);
+ *    inliers = cv::recoverPose(E, pts_last, pts_curr, K, R, t, mask)
+ *    in Tracking::EstimatePoseByEssential (tracking.cpp:503-547).
+ * Same device strategy as vx_pnp_ransac: every hypothesis (5 correspondences from a splitmix64
+ * stream) is solved by the five-point method (up to 10 E, all scored by Sampson error) at once, and
+ * the sequential RANSAC loop is replayed over the per-model inlier counts; the kept E is decomposed
+ * (E = U diag V^T; R1 = U W V^T, R2 = U W^T V^T, t = U e3) and the four (R, +-t) are scored by DLT
+ * triangulation of the RANSAC inliers (positive depth below distance_thresh in both views), OpenCV's
+ * tie order.  Parity against OpenCV is unpinned (its cv::RNG stream); DESIGN.md §14. */
+typedef struct {
+    int32_t max_iterations;    /* findEssentialMat maxIters (OpenCV default 1000), <= 4096 */
+    int32_t reserved;
+    double threshold;          /* px (tracking.cpp:521: 1.0); divided by (fx + fy) / 2 */
+    double confidence;         /* prob (0.999) */
+    double distance_thresh;    /* recoverPose's triangulated-depth limit (50) */
+    uint64_t seed;             /* hypothesis stream */
+} vx_essential_options;
+typedef struct {
+    int32_t ok;                /* !E.empty() */
+    int32_t n_inliers;         /* recoverPose's return value: RANSAC inliers in front of both views */
+    int32_t n_ransac_inliers;  /* findEssentialMat's mask count */
+    int32_t best_hypothesis, best_model, hypotheses_run;
+    int32_t pose_candidate;    /* 0: (R1, t) 1: (R2, t) 2: (R1, -t) 3: (R2, -t) */
+    int32_t reserved;
+    double E[9];               /* row-major, unit Frobenius norm, x_curr^T E x_last = 0 (normalised) */
+    double R[9], t[3];         /* T_cl: x_curr = R x_last + t, |t| = 1 (recoverPose's R, t) */
+} vx_essential_result;
+void vx_essential_default_options(vx_essential_options* out);
+/* pts_last / pts_curr: 2 floats per match (cv::Point2f, tracking.cpp:506-514); mask (n bytes, may
+ * be NULL) = recoverPose's output mask. */
+int vx_essential_ransac(vx_ctx* ctx, const float* pts_last, const float* pts_curr, int n, const double* intr4,
+                        const vx_essential_options* opt, uint8_t* mask, vx_essential_result* out);
+int vx_essential_ransac_batch(vx_ctx* ctx, int n_problems, const int32_t* offsets, const float* pts_last,
+                              const float* pts_curr, const double* intr4, const vx_essential_options* opt,
+                              uint8_t* mask, vx_essential_result* out);
 
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);

@@ -176,6 +176,23 @@ int orc_p3p(const double* P9, const double* f9, double* R72, double* t24);  /* u
 int orc_poly_roots(const double* c, int d, double* out);
 int orc_pnp_update_iters(double p, double ep, int max_iters);
 
+/* ---- essential-matrix RANSAC + recoverPose (essential_oracle.cpp), layout = vx_essential_* */
+#define ORC_EM_MAX_HYP 4096
+typedef struct {
+    int32_t max_iterations, reserved;
+    double threshold, confidence, distance_thresh;
+    uint64_t seed;
+} orc_essential_options;
+typedef struct {
+    int32_t ok, n_inliers, n_ransac_inliers, best_hypothesis, best_model, hypotheses_run, pose_candidate, reserved;
+    double E[9], R[9], t[3];
+} orc_essential_result;
+int orc_essential_ransac_batch(int n_problems, const int32_t* offsets, const float* pts1, const float* pts2,
+                               const double* intr4, const orc_essential_options* opt, uint8_t* mask,
+                               orc_essential_result* out);
+/* five-point solver on 5 normalised correspondences: up to 10 unit-norm E (row-major) */
+int orc_five_point(const double* x1, const double* x2, double* Es);
+
 #ifdef __cplusplus
 }
 #endif

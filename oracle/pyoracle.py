@@ -373,3 +373,50 @@ def poly_roots(c):
 
 def pnp_update_iters(p, ep, max_iters):
     return lib().orc_pnp_update_iters(C.c_double(p), C.c_double(ep), max_iters)
+
+
+# ---------------------------------------------------------------------------- essential RANSAC
+EM_OPTIONS_DTYPE = np.dtype([("max_iterations", "<i4"), ("reserved", "<i4"), ("threshold", "<f8"),
+                             ("confidence", "<f8"), ("distance_thresh", "<f8"), ("seed", "<u8")])
+EM_RESULT_DTYPE = np.dtype([("ok", "<i4"), ("n_inliers", "<i4"), ("n_ransac_inliers", "<i4"),
+                            ("best_hypothesis", "<i4"), ("best_model", "<i4"), ("hypotheses_run", "<i4"),
+                            ("pose_candidate", "<i4"), ("reserved", "<i4"), ("E", "<f8", 9), ("R", "<f8", 9),
+                            ("t", "<f8", 3)])
+
+
+def essential_options(max_iterations=1000, threshold=1.0, confidence=0.999, distance_thresh=50.0, seed=0x5EED):
+    """findEssentialMat(.., RANSAC, 0.999, 1.0, mask) + recoverPose (tracking.cpp:521-528)."""
+    o = np.zeros((), EM_OPTIONS_DTYPE)
+    o["max_iterations"] = max_iterations
+    o["threshold"] = threshold
+    o["confidence"] = confidence
+    o["distance_thresh"] = distance_thresh
+    o["seed"] = seed
+    return o
+
+
+def essential_ransac_batch(offsets, pts1, pts2, intr, opts):
+    offsets = np.ascontiguousarray(offsets, np.int32)
+    pts1 = np.ascontiguousarray(pts1, np.float32)
+    pts2 = np.ascontiguousarray(pts2, np.float32)
+    intr = np.ascontiguousarray(intr, np.float64)
+    opts = np.ascontiguousarray(opts, EM_OPTIONS_DTYPE)
+    P = len(offsets) - 1
+    out = np.zeros(P, EM_RESULT_DTYPE)
+    mask = np.zeros(max(int(offsets[-1]), 1), np.uint8)
+    assert lib().orc_essential_ransac_batch(P, _p(offsets), _p(pts1), _p(pts2), _p(intr), _p(opts), _p(mask),
+                                            _p(out)) == 0
+    return out, mask[:offsets[-1]].copy()
+
+
+def essential_ransac(pts1, pts2, intr, opt):
+    out, mask = essential_ransac_batch(np.array([0, len(pts1)]), pts1, pts2, intr, np.atleast_1d(opt))
+    return out[0], mask
+
+
+def five_point(x1, x2):
+    x1 = np.ascontiguousarray(x1, np.float64)
+    x2 = np.ascontiguousarray(x2, np.float64)
+    Es = np.zeros(90)
+    n = lib().orc_five_point(_p(x1), _p(x2), _p(Es))
+    return Es[:9 * n].reshape(n, 3, 3)

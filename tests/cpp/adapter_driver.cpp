@@ -8,6 +8,7 @@
 //   adapter_driver depth <dir>                     (KeyFrameLandmarks::CreateLandmarksFromDepth)
 //   adapter_driver triangulate <dir> <min_deg> <max_err>   (TriangulateWithLastKeyFrame)
 //   adapter_driver pnp <dir> <iterations> <reproj_err>    (solvePnPRansac as TrackWithPnP calls it)
+//   adapter_driver essential <dir>                         (EstimatePoseByEssential's two calls)
 #include <cstdio>
 #include <cstdlib>
 #include <climits>
@@ -285,6 +286,32 @@ static int cmd_pnp(char** a) {
     return 0;
 }
 
+// p1.bin / p2.bin (float x2), intr.bin -> prints findEssentialMat/recoverPose's inlier count (-1: no
+// E); writes pose.out (R row-major, t, then T_cl as SE3d) and mask.out (uint8 per match)
+static int cmd_essential(char** a) {
+    const std::string dir = a[0];
+    const auto p1 = read_bin<float>(dir + "/p1.bin");
+    const auto p2 = read_bin<float>(dir + "/p2.bin");
+    const auto intr = read_bin<double>(dir + "/intr.bin");
+    std::vector<Point2f> last, curr;
+    for (size_t i = 0; i + 1 < p1.size(); i += 2) {
+        last.emplace_back(p1[i], p1[i + 1]);
+        curr.emplace_back(p2[i], p2[i + 1]);
+    }
+    Camera cam(intr[0], intr[1], intr[2], intr[3]);
+    double R[9];
+    Vec3d t;
+    std::vector<uint8_t> mask;
+    const int inliers = FindEssentialMatRecoverPose(last, curr, cam, R, t, &mask, 0.999, 1.0);
+    std::vector<double> out(R, R + 9);
+    const SE3d T = PoseFromRt(R, t);
+    out.insert(out.end(), {t.x, t.y, t.z, T.qx, T.qy, T.qz, T.qw, T.tx, T.ty, T.tz});
+    write_bin(dir + "/pose.out", out);
+    write_bin(dir + "/mask.out", mask);
+    std::printf("%d\n", inliers);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 2) return 2;
     const std::string cmd = argv[1];
@@ -295,6 +322,7 @@ int main(int argc, char** argv) {
         if (cmd == "depth" && argc >= 3) return cmd_depth(argv + 2);
         if (cmd == "triangulate" && argc >= 5) return cmd_triangulate(argv + 2);
         if (cmd == "pnp" && argc >= 5) return cmd_pnp(argv + 2);
+        if (cmd == "essential" && argc >= 3) return cmd_essential(argv + 2);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;

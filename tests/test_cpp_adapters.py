@@ -181,3 +181,23 @@ def test_adapter_pnp_ransac(driver, oracle, tmp_path):
     pose = np.fromfile(os.path.join(p, "pose.out"), np.float64)
     assert np.abs(pose[:3] - r["rvec"]).max() < 1e-9 and np.abs(pose[3:6] - r["tvec"]).max() < 1e-9
     assert np.abs(pose[6:] - r["pose"]).max() < 1e-9
+
+
+@pytest.mark.gpu
+def test_adapter_essential(driver, oracle, tmp_path):
+    """FindEssentialMatRecoverPose as Tracking::EstimatePoseByEssential calls findEssentialMat +
+    recoverPose (tracking.cpp:503-547): RANSAC 0.999 / 1 px, 1000 iterations; R, t, mask."""
+    d = synth.make_two_view(78, 900, outlier_frac=0.3)
+    p = str(tmp_path)
+    d["pts_last"].tofile(os.path.join(p, "p1.bin"))
+    d["pts_curr"].tofile(os.path.join(p, "p2.bin"))
+    d["intr"].tofile(os.path.join(p, "intr.bin"))
+    (n_in,) = map(int, run(driver, "essential", p))
+    r, mask = oracle.essential_ransac(d["pts_last"], d["pts_curr"], d["intr"], oracle.essential_options())
+    assert r["ok"] == 1 and n_in == r["n_inliers"]
+    assert np.array_equal(np.fromfile(os.path.join(p, "mask.out"), np.uint8), mask)
+    pose = np.fromfile(os.path.join(p, "pose.out"), np.float64)
+    assert np.array_equal(pose[:9], r["R"]) and np.array_equal(pose[9:12], r["t"])
+    q = pose[12:16]
+    R = synth.quat_to_mat(q)
+    assert np.abs(R - r["R"].reshape(3, 3)).max() < 1e-12

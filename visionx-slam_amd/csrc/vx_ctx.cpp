@@ -155,7 +155,8 @@ static const char* kStageNames[vx::kStCount] = {
     "orb_describe",   "match_partial", "match_merge",     "ba_reset",    "ba_pose_partial",
     "ba_pose_sum",    "ba_allreduce",  "ba_pose_solve",   "ba_landmark",    "orb_pyramid",
     "sba_landmark",   "sba_blocks",    "sba_solve",       "sba_update",     "sba_allreduce",
-    "lm_depth",       "lm_triangulate", "lm_compact",  "pnp_hypotheses", "pnp_refine"};
+    "lm_depth",       "lm_triangulate", "lm_compact",  "pnp_hypotheses", "pnp_refine",
+    "em_hypotheses",  "em_select"};
 
 extern "C" {
 

@@ -47,6 +47,8 @@ enum Stage : int {
     kStLmCompact,
     kStPnpHyp,
     kStPnpRefine,
+    kStEmHyp,
+    kStEmSelect,
     kStCount
 };
 
@@ -162,6 +164,7 @@ struct vx_event {
 
 struct vx_ctx {
     int device = 0;
+    int n_cus = 0;  // compute units of the device (lazily queried)
     hipStream_t stream = nullptr;
     hipEvent_t order_event = nullptr;  // vx_stream_wait_ctx: recorded on this stream
     std::string err;
@@ -184,7 +187,7 @@ struct vx_ctx {
     // ---- PnP RANSAC (ransac.hip): packed inputs (pinned staging + device), hypothesis records,
     // packed outputs (results + inlier mask)
     vx::PinnedBuf rs_host, rs_host_out;
-    vx::DevBuf rs_in, rs_hyp, rs_out;
+    vx::DevBuf rs_in, rs_hyp, rs_out;  // (shared by vx_essential_ransac, essential.hip)
 
     // ---- device-side LocalBA plan build scratch (ba_window.hip)
     struct PlanScratch {

@@ -38,4 +38,16 @@ bool SolvePnPRansac(const std::vector<Point3f>& objectPoints, const std::vector<
 // cv::Rodrigues + Sophus::SE3d(R, t) (tracking.cpp:429-447): the unit quaternion of rvec
 SE3d PoseFromRvecTvec(const Vec3d& rvec, const Vec3d& tvec);
 
+// E = cv::findEssentialMat(pts_last, pts_curr, K, cv::RANSAC, prob, threshold, mask);
+// inliers = cv::recoverPose(E, pts_last, pts_curr, K, R, t, mask)   (tracking.cpp:521-528)
+// in one call: returns -1 when findEssentialMat finds no E (E.empty()), else recoverPose's inlier
+// count; R (row-major) and t give T_cl (x_curr = R x_last + t, |t| = 1); mask (optional) is
+// recoverPose's output mask, E (optional) the row-major essential matrix.
+int FindEssentialMatRecoverPose(const std::vector<Point2f>& pts_last, const std::vector<Point2f>& pts_curr,
+                                const Camera& K, double R[9], Vec3d& t, std::vector<uint8_t>* mask = nullptr,
+                                double prob = 0.999, double threshold = 1.0, double E[9] = nullptr);
+
+// Sophus::SE3d T_cl(R, t) of a rotation matrix (row-major) and translation
+SE3d PoseFromRt(const double R[9], const Vec3d& t);
+
 }  // namespace visionx

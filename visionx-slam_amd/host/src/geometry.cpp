@@ -56,4 +56,55 @@ SE3d PoseFromRvecTvec(const Vec3d& rvec, const Vec3d& tvec) {
     return T;
 }
 
+int FindEssentialMatRecoverPose(const std::vector<Point2f>& pts_last, const std::vector<Point2f>& pts_curr,
+                                const Camera& K, double R[9], Vec3d& t, std::vector<uint8_t>* mask, double prob,
+                                double threshold, double E[9]) {
+    if (pts_last.size() != pts_curr.size())
+        throw std::invalid_argument("FindEssentialMatRecoverPose: point list size mismatch");
+    const int n = (int)pts_last.size();
+    vx_essential_options o;
+    vx_essential_default_options(&o);
+    o.confidence = prob;
+    o.threshold = threshold;
+    const double intr[4] = {K.fx(), K.fy(), K.cx(), K.cy()};
+    std::vector<uint8_t> m(n > 0 ? n : 1);
+    vx_essential_result r;
+    vx_ctx* c = vxhost::ThreadContext();
+    const int rc = vx_essential_ransac(c, reinterpret_cast<const float*>(pts_last.data()),
+                                       reinterpret_cast<const float*>(pts_curr.data()), n, intr, &o, m.data(), &r);
+    if (rc != VX_OK) throw std::runtime_error(std::string("vx_essential_ransac: ") + vx_last_error(c));
+    if (mask) mask->assign(m.begin(), m.begin() + n);
+    if (!r.ok) return -1;
+    for (int k = 0; k < 9; ++k) {
+        R[k] = r.R[k];
+        if (E) E[k] = r.E[k];
+    }
+    t = Vec3d(r.t[0], r.t[1], r.t[2]);
+    return r.n_inliers;
+}
+
+// Shepperd's method (largest of trace / diagonal), as Eigen::Quaterniond(Matrix3d)
+SE3d PoseFromRt(const double* R, const Vec3d& t) {
+    double x, y, z, w;
+    const double tr = R[0] + R[4] + R[8];
+    if (tr > 0.0) {
+        const double s = std::sqrt(tr + 1.0) * 2.0;
+        w = 0.25 * s; x = (R[7] - R[5]) / s; y = (R[2] - R[6]) / s; z = (R[3] - R[1]) / s;
+    } else if (R[0] > R[4] && R[0] > R[8]) {
+        const double s = std::sqrt(1.0 + R[0] - R[4] - R[8]) * 2.0;
+        w = (R[7] - R[5]) / s; x = 0.25 * s; y = (R[1] + R[3]) / s; z = (R[2] + R[6]) / s;
+    } else if (R[4] > R[8]) {
+        const double s = std::sqrt(1.0 + R[4] - R[0] - R[8]) * 2.0;
+        w = (R[2] - R[6]) / s; x = (R[1] + R[3]) / s; y = 0.25 * s; z = (R[5] + R[7]) / s;
+    } else {
+        const double s = std::sqrt(1.0 + R[8] - R[0] - R[4]) * 2.0;
+        w = (R[3] - R[1]) / s; x = (R[2] + R[6]) / s; y = (R[5] + R[7]) / s; z = 0.25 * s;
+    }
+    const double inv = 1.0 / std::sqrt(x * x + y * y + z * z + w * w);
+    SE3d T;
+    T.qx = x * inv; T.qy = y * inv; T.qz = z * inv; T.qw = w * inv;
+    T.tx = t.x; T.ty = t.y; T.tz = t.z;
+    return T;
+}
+
 }  // namespace visionx

@@ -128,6 +128,7 @@ def lib():
         L.vx_sba_plan_destroy.restype = None
         L.vx_sba_default_options.restype = None
         L.vx_pnp_default_options.restype = None
+        L.vx_essential_default_options.restype = None
         L.vx_ba_shard_of.restype = C.c_uint32
         L.vx_ba_shard_of.argtypes = [C.c_uint64, C.c_int]
         _lib = L
@@ -145,6 +146,26 @@ PNP_RESULT_DTYPE = np.dtype([("ok", "<i4"), ("n_inliers", "<i4"), ("best_hypothe
                              ("hypotheses_run", "<i4"), ("refine_iterations", "<i4"), ("reserved", "<i4"),
                              ("rvec", "<f8", 3), ("tvec", "<f8", 3), ("pose", "<f8", 7), ("cost0", "<f8"),
                              ("cost", "<f8")])
+
+
+EM_OPTIONS_DTYPE = np.dtype([("max_iterations", "<i4"), ("reserved", "<i4"), ("threshold", "<f8"),
+                             ("confidence", "<f8"), ("distance_thresh", "<f8"), ("seed", "<u8")])
+EM_RESULT_DTYPE = np.dtype([("ok", "<i4"), ("n_inliers", "<i4"), ("n_ransac_inliers", "<i4"),
+                            ("best_hypothesis", "<i4"), ("best_model", "<i4"), ("hypotheses_run", "<i4"),
+                            ("pose_candidate", "<i4"), ("reserved", "<i4"), ("E", "<f8", 9), ("R", "<f8", 9),
+                            ("t", "<f8", 3)])
+
+
+def essential_options(max_iterations=None, threshold=None, confidence=None, distance_thresh=None, seed=None):
+    """findEssentialMat(.., RANSAC, 0.999, 1.0, mask) + recoverPose (tracking.cpp:521-528) defaults,
+    any field overridable."""
+    o = np.zeros((), EM_OPTIONS_DTYPE)
+    lib().vx_essential_default_options(_p(o))
+    for k, v in (("max_iterations", max_iterations), ("threshold", threshold), ("confidence", confidence),
+                 ("distance_thresh", distance_thresh), ("seed", seed)):
+        if v is not None:
+            o[k] = v
+    return o
 
 
 def pnp_options(n, max_iterations=None, reproj_error=2.0, confidence=0.99, seed=0x5EED, refine_iterations=20):
@@ -443,6 +464,35 @@ class Context:
         mask = np.zeros(max(len(obj), 1), np.uint8)
         self._check(lib().vx_pnp_ransac(self._h, _p(obj), _p(img), len(obj), _p(intr), _p(opt), _p(mask), _p(out)))
         return out[0], mask[:len(obj)].copy()
+
+    def essential_ransac_batch(self, offsets, pts_last, pts_curr, intr, opts):
+        """cv::findEssentialMat + cv::recoverPose (Tracking::EstimatePoseByEssential,
+        tracking.cpp:503-547) on the GPU for independent problems: (results[P], mask[N])."""
+        offsets = np.ascontiguousarray(offsets, np.int32)
+        p1 = np.ascontiguousarray(pts_last, np.float32).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts_curr, np.float32).reshape(-1, 2)
+        intr = np.ascontiguousarray(intr, np.float64).reshape(-1, 4)
+        opts = np.ascontiguousarray(np.atleast_1d(opts), EM_OPTIONS_DTYPE)
+        P = len(offsets) - 1
+        n = int(offsets[-1])
+        assert len(p1) == n and len(p2) == n and len(intr) == P and len(opts) == P
+        out = np.zeros(max(P, 1), EM_RESULT_DTYPE)
+        mask = np.zeros(max(n, 1), np.uint8)
+        self._check(lib().vx_essential_ransac_batch(self._h, P, _p(offsets), _p(p1), _p(p2), _p(intr), _p(opts),
+                                                    _p(mask), _p(out)))
+        return out[:P].copy(), mask[:n].copy()
+
+    def essential_ransac(self, pts_last, pts_curr, intr, opt):
+        """One findEssentialMat + recoverPose: (result record, recoverPose mask)."""
+        p1 = np.ascontiguousarray(pts_last, np.float32).reshape(-1, 2)
+        p2 = np.ascontiguousarray(pts_curr, np.float32).reshape(-1, 2)
+        intr = np.ascontiguousarray(intr, np.float64)
+        opt = np.ascontiguousarray(opt, EM_OPTIONS_DTYPE)
+        out = np.zeros(1, EM_RESULT_DTYPE)
+        mask = np.zeros(max(len(p1), 1), np.uint8)
+        self._check(lib().vx_essential_ransac(self._h, _p(p1), _p(p2), len(p1), _p(intr), _p(opt), _p(mask),
+                                              _p(out)))
+        return out[0], mask[:len(p1)].copy()
 
     def sba_optimize(self, m, opts: SBAOptions | None = None, ref_kf_id=None) -> SBAStats:
         """Schur-complement joint BA (vx_sba_optimize_map) on a synth.BAMap, in place."""

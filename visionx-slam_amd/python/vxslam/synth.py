@@ -366,3 +366,37 @@ def make_pnp_problem(seed: int, n: int = 1000, *, outlier_frac: float = 0.3, noi
         q = -q
     return {"obj": pw.astype(np.float32), "img": uv.astype(np.float32), "intr": np.array(intr, np.float64),
             "pose": np.concatenate([q, t]), "R": R, "t": t, "outlier": out}
+
+
+def make_two_view(seed: int, n: int = 1000, *, outlier_frac: float = 0.3, noise_px: float = 0.5,
+                  width: int = 640, height: int = 480, intr=(FX, FY, CX, CY), baseline_m: float = 0.15,
+                  rot_deg: float = 3.0, z_range=(1.0, 6.0)):
+    """Matched pixel pairs as Tracking::EstimatePoseByEssential builds them (tracking.cpp:506-514:
+    cv::Point2f of the last and the current frame's features): points seen by both cameras, pixel
+    noise, a fraction of wrong matches.  Returns pts_last, pts_curr (n x 2 float32), intr, the true
+    T_cl (R, t with x_curr = R x_last + t; t unit-normalised copy in t_dir) and the outlier flags."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = intr
+    q = quat_from_rotvec(rng.normal(0, 1, 3) * np.deg2rad(rot_deg) / np.sqrt(3))
+    R = quat_to_mat(q)
+    d = rng.normal(0, 1, 3)
+    d[2] *= 0.3
+    t = baseline_m * d / np.linalg.norm(d)
+    pts_last, pts_curr = [], []
+    while not pts_last or sum(len(a) for a in pts_last) < n:
+        u = rng.uniform(0, width, 2 * n)
+        v = rng.uniform(0, height, 2 * n)
+        z = rng.uniform(z_range[0], z_range[1], 2 * n)
+        p1 = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], -1)
+        p2 = p1 @ R.T + t
+        u2 = fx * p2[:, 0] / p2[:, 2] + cx
+        v2 = fy * p2[:, 1] / p2[:, 2] + cy
+        ok = (p2[:, 2] > 0.1) & (u2 >= 0) & (u2 < width) & (v2 >= 0) & (v2 < height)
+        pts_last.append(np.stack([u, v], -1)[ok])
+        pts_curr.append(np.stack([u2, v2], -1)[ok])
+    a = np.concatenate(pts_last)[:n] + rng.normal(0, noise_px, (n, 2))
+    b = np.concatenate(pts_curr)[:n] + rng.normal(0, noise_px, (n, 2))
+    out = rng.random(n) < outlier_frac
+    b[out] = np.stack([rng.uniform(0, width, out.sum()), rng.uniform(0, height, out.sum())], -1)
+    return {"pts_last": a.astype(np.float32), "pts_curr": b.astype(np.float32), "intr": np.array(intr, np.float64),
+            "R": R, "t": t, "t_dir": t / np.linalg.norm(t), "outlier": out}
