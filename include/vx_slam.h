@@ -23,6 +23,9 @@
  *                                                                core/frontend/tracking.cpp:414-423
  *   vx_essential_ransac   <- cv::findEssentialMat + cv::recoverPose in
  *                            Tracking::EstimatePoseByEssential   core/frontend/tracking.cpp:503-547
+ *   vx_dmap_*             <- visionx::Map (map.h:13-35) kept resident on the device, updated like
+ *                            Map::InsertKeyFrame / InsertLandmark / Landmark::AddObservation
+ *   vx_ba_plan_create_dmap <- the gather of local_ba.cpp:42-108 from the resident map
  *   vx_sba_*              (no reference counterpart: north_star's Schur-complement dense solve)
  *
  * The host-side C++ adapters that keep the reference call surface (same class names and
@@ -228,6 +231,44 @@ int vx_ba_plan_inspect(const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                        int32_t* lm_map_idx, int cap_lm, int32_t* kf_map_idx, int cap_kf);
 /* Landmark -> shard assignment used by sharded plans (splitmix64(id) mod shard_count). */
 uint32_t vx_ba_shard_of(uint64_t lm_id, int shard_count);
+
+/* ---------------------------------------------------------------- device-resident map
+ * A persistent mirror of visionx::Map on the device: keyframes with their
+ * features, landmarks, observations, updated incrementally as Tracking / the Map change them
+ * (Map::InsertKeyFrame, Map::InsertLandmark, Landmark::AddObservation, Feature::landmark_id_,
+ * Landmark::SetBad, Frame::SetPose), so a LocalBA plan is built from device memory — no map
+ * snapshot crosses PCIe per keyframe — and its result is scattered back into the device map
+ * without a host round trip.  Keyframes / landmarks keep their insertion order (the map index
+ * order of an equivalent vx_map_view); a landmark's observations keep their insertion order.
+ * Capacities grow on demand. */
+typedef struct vx_dmap vx_dmap;
+int vx_dmap_create(vx_ctx* ctx, vx_dmap** out);
+void vx_dmap_destroy(vx_dmap* map);
+/* Map::InsertKeyFrame: kf_id unique; pose7 T_cw; intr4 fx fy cx cy (ignored unless has_cam);
+ * features as in vx_map_view (uv 2 each, landmark ids, flags bit0 has_landmark bit1 is_outlier) */
+int vx_dmap_add_keyframe(vx_dmap* map, uint64_t kf_id, const double* pose7, const double* intr4, int has_cam,
+                         int n_feat, const double* feat_uv, const uint64_t* feat_lm_id, const uint8_t* feat_flags);
+/* Map::InsertLandmark: ids unique; pos 3 each; bad may be NULL (all good) */
+int vx_dmap_add_landmarks(vx_dmap* map, int n, const uint64_t* lm_id, const double* pos3, const uint8_t* bad);
+/* Landmark::AddObservation(kf_id, feat_idx) on existing landmarks (VX_ERR_INVALID for unknown ids) */
+int vx_dmap_add_observations(vx_dmap* map, int n, const uint64_t* lm_id, const uint64_t* kf_id,
+                             const uint64_t* feat_idx);
+/* Feature::landmark_id_ / has_landmark / is_outlier of features of keyframe kf_id */
+int vx_dmap_set_features(vx_dmap* map, uint64_t kf_id, int n, const int32_t* feat_idx, const uint64_t* lm_id,
+                         const uint8_t* flags);
+int vx_dmap_set_landmark_bad(vx_dmap* map, int n, const uint64_t* lm_id, const uint8_t* bad);
+int vx_dmap_set_poses(vx_dmap* map, int n, const uint64_t* kf_id, const double* pose7);
+/* out4 = {keyframes, features, landmarks, observations} */
+int vx_dmap_counts(const vx_dmap* map, int64_t* out4);
+/* current poses (7 per keyframe) / positions (3 per landmark) in insertion order; either may be NULL */
+int vx_dmap_download(vx_dmap* map, double* kf_pose, double* lm_pos);
+/* LocalBA plan from the resident map (the plan vx_ba_plan_create builds from the equivalent
+ * vx_map_view snapshot); run with vx_ba_plan_run_async as usual */
+int vx_ba_plan_create_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_ref, const vx_ba_options* opt,
+                           int shard_rank, int shard_count, vx_ba_plan** out);
+/* enqueue the scatter of a run's window poses and optimised landmark positions into the map (stream
+ * ordered after the run; no host synchronisation) */
+int vx_ba_plan_apply_dmap(vx_ctx* ctx, vx_ba_plan* plan, vx_dmap* map);
 
 /* ---------------------------------------------------------------- Schur-complement joint BA
  * NOT a reference entry point: the reference's LocalBA alternates per-keyframe and per-landmark

@@ -3,6 +3,15 @@ import sys
 
 import pytest
 
+# PyTorch bundles its own HIP runtime (ROCm 7.0) while libvxslam.so links the system one (7.2);
+# both carry the soname libamdhip64.so.7, so whichever a process loads first serves both.  torch only
+# initialises on its own copy: load it before any test loads libvxslam (a full-suite run does this
+# anyway when collecting the modules that import torch; a narrower selection might not).
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "visionx-slam_amd", "python"), os.path.join(ROOT, "oracle"), ROOT):
     if p not in sys.path:

@@ -1,0 +1,156 @@
+"""Device-resident map (vx_dmap_*, csrc/dmap.hip) and the LocalBA plan built from it
+(vx_ba_plan_create_dmap / vx_ba_plan_apply_dmap).
+
+The map is filled the way a running system fills it (keyframe by keyframe: features, newly seen
+landmarks, that keyframe's observations) and must give the plan the snapshot device build gives on
+the equivalent vx_map_view (same rows in the same order): the runs are compared bitwise, and the
+result scattered into the resident map must equal the snapshot fetch."""
+import numpy as np
+import pytest
+
+import vxslam
+from vxslam import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _stats_equal(a, b):
+    assert (a.status, a.iterations, a.n_window_kf, a.n_landmarks) == (b.status, b.iterations, b.n_window_kf,
+                                                                        b.n_landmarks)
+    assert list(a.cost) == list(b.cost) and list(a.obs) == list(b.obs)
+
+
+def _run(plan):
+    plan.run_async()
+    return plan.fetch()
+
+
+@pytest.mark.parametrize("cfg", [("C2", 10, 2000, 1), ("C3", 50, 20000, 1), ("C5s", 40, 8000, 4)])
+def test_dmap_plan_equals_snapshot_plan(ctx, cfg):
+    name, nk, nl, ns = cfg
+    m = synth.make_ba_map(0xD0 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
+    dm = vxslam.DMap(ctx)
+    kf_order, lm_order = vxslam.dmap_load(dm, m)
+    c = dm.counts()
+    assert c == {"kf": len(m["kf_id"]), "feat": len(m["feat_lm_id"]), "lm": len(m["lm_id"]),
+                 "obs": len(m["obs_kf_id"])}
+    m2 = vxslam.map_reorder(m, kf_order, lm_order)
+    opts = vxslam.default_ba_options(window=nk, iters=5)
+    pd = dm.plan(opts, ref_kf_id=m["ref_kf_id"])
+    ps = ctx.ba_plan(m2, opts, ref_kf_id=m["ref_kf_id"])
+    assert pd.info() == ps.info()
+    sd, ss = _run(pd), _run(ps)
+    _stats_equal(sd, ss)
+    # scatter: resident map vs snapshot fetch
+    pd.apply(dm)
+    ps.fetch(m2)
+    pose, pos = dm.download()
+    assert np.array_equal(pose, m2["kf_pose"].reshape(-1, 7))
+    assert np.array_equal(pos, m2["lm_pos"].reshape(-1, 3))
+    # a second plan on the updated resident map == a plan on the updated snapshot
+    pd2 = dm.plan(opts, ref_kf_id=m["ref_kf_id"])
+    ps2 = ctx.ba_plan(m2, opts, ref_kf_id=m["ref_kf_id"])
+    _stats_equal(_run(pd2), _run(ps2))
+    pd2.close(), ps2.close(), pd.close(), ps.close(), dm.close()
+
+
+class _Mirror:
+    """Feeds snapshot keyframe rows into a DMap one at a time and keeps the equivalent snapshot."""
+
+    def __init__(self, m, dm):
+        self.m, self.dm = m, dm
+        self.kf_rows, self.lm_rows, self.obs_rows = [], [], []
+        self.seen = set()
+        self.obs_lm = np.repeat(np.arange(len(m["lm_id"])), np.diff(m["lm_obs_ptr"]))
+
+    def add(self, k):
+        m = self.m
+        f0, f1 = m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]
+        self.dm.add_keyframe(m["kf_id"][k], m["kf_pose"].reshape(-1, 7)[k], m["kf_intr"].reshape(-1, 4)[k],
+                             m["kf_has_cam"][k], m["feat_uv"].reshape(-1, 2)[f0:f1], m["feat_lm_id"][f0:f1],
+                             m["feat_flags"][f0:f1])
+        sel = np.nonzero(m["obs_kf_id"] == m["kf_id"][k])[0]
+        new = [int(l) for l in np.unique(self.obs_lm[sel]) if int(l) not in self.seen]
+        if new:
+            self.dm.add_landmarks(m["lm_id"][new], m["lm_pos"].reshape(-1, 3)[new], m["lm_bad"][new])
+            self.seen.update(new)
+            self.lm_rows.extend(new)
+        if len(sel):
+            self.dm.add_observations(m["lm_id"][self.obs_lm[sel]], m["obs_kf_id"][sel], m["obs_feat_idx"][sel])
+        self.kf_rows.append(k)
+        self.obs_rows.extend(sel.tolist())
+
+    def snapshot(self):
+        m = self.m
+        sub = vxslam.map_reorder(m, np.asarray(self.kf_rows), np.asarray(self.lm_rows, np.int64))
+        obs = np.asarray(self.obs_rows, np.int64)
+        lm_of = self.obs_lm[obs]
+        per = [obs[lm_of == l] for l in self.lm_rows]  # insertion (= keyframe) order per landmark
+        cnt = np.array([len(x) for x in per], np.int64)
+        sub["lm_obs_ptr"] = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        allo = np.concatenate(per) if per else np.zeros(0, np.int64)
+        sub["obs_kf_id"] = m["obs_kf_id"][allo].copy()
+        sub["obs_feat_idx"] = m["obs_feat_idx"][allo].copy()
+        return sub
+
+
+def test_dmap_incremental_updates(ctx):
+    """Keyframes arrive one by one with plans in between; feature / bad-flag / pose edits go to
+    both representations; every plan equals the snapshot plan of the map as it stands."""
+    m = synth.make_ba_map(0xD7, 12, 3000, n_old_kf=2)
+    dm = vxslam.DMap(ctx)
+    mir = _Mirror(m, dm)
+    opts = vxslam.default_ba_options(window=6, iters=3)
+    rng = np.random.default_rng(5)
+    for step, k in enumerate(np.argsort(m["kf_id"], kind="stable")):
+        mir.add(k)
+        if step < 3:
+            continue
+        kid = int(m["kf_id"][k])
+        f0, f1 = m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]
+        fi = rng.choice(f1 - f0, 5, replace=False).astype(np.int32)
+        fl = m["feat_flags"][f0 + fi] ^ 2  # toggle is_outlier
+        m["feat_flags"][f0 + fi] = fl
+        dm.set_features(kid, fi, m["feat_lm_id"][f0 + fi], fl)
+        bad = rng.choice(np.asarray(mir.lm_rows), 3, replace=False)
+        m["lm_bad"][bad] = 1
+        dm.set_landmark_bad(m["lm_id"][bad], np.ones(3, np.uint8))
+        pose = m["kf_pose"].reshape(-1, 7)[k].copy()
+        pose[4] += 0.01
+        m["kf_pose"].reshape(-1, 7)[k] = pose
+        dm.set_poses([kid], pose[None])
+        m2 = mir.snapshot()
+        pd = dm.plan(opts, ref_kf_id=kid)
+        ps = ctx.ba_plan(m2, opts, ref_kf_id=kid)
+        assert pd.info() == ps.info()
+        _stats_equal(_run(pd), _run(ps))
+        # the run lands in both maps identically
+        pd.apply(dm)
+        ps.fetch(m2)
+        pose_d, pos_d = dm.download()
+        assert np.array_equal(pose_d, m2["kf_pose"].reshape(-1, 7))
+        assert np.array_equal(pos_d, m2["lm_pos"].reshape(-1, 3))
+        # carry the optimised state back into the source map rows for the next step
+        m["kf_pose"].reshape(-1, 7)[np.asarray(mir.kf_rows)] = pose_d
+        m["lm_pos"].reshape(-1, 3)[np.asarray(mir.lm_rows)] = pos_d
+        pd.close(), ps.close()
+    dm.close()
+
+
+def test_dmap_errors(ctx):
+    dm = vxslam.DMap(ctx)
+    dm.add_keyframe(1, [0, 0, 0, 1, 0, 0, 0], [500, 500, 320, 240], 1, np.zeros((3, 2)), np.zeros(3, np.uint64),
+                    np.zeros(3, np.uint8))
+    with pytest.raises(vxslam.VxError):
+        dm.add_keyframe(1, [0, 0, 0, 1, 0, 0, 0], [500, 500, 320, 240], 1, np.zeros((1, 2)), np.zeros(1, np.uint64),
+                        np.zeros(1, np.uint8))
+    with pytest.raises(vxslam.VxError):
+        dm.add_observations([7], [1], [0])  # unknown landmark
+    with pytest.raises(vxslam.VxError):
+        dm.set_features(2, [0], [0], [0])  # unknown keyframe
+    with pytest.raises(vxslam.VxError):
+        dm.set_features(1, [5], [0], [0])  # feature index out of range
+    # a map with one keyframe: plan status 1 (local_ba.cpp:67-75)
+    p = dm.plan(vxslam.default_ba_options(window=5, iters=2))
+    assert p.info()["n_kf"] == 0
+    dm.close()

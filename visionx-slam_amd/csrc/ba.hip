@@ -40,6 +40,7 @@
 #include "vx_ktrace.hpp"
 #include "ba_common.hpp"
 #include "ba_plan.hpp"
+#include "dmap.hpp"
 
 namespace vx {
 namespace {
@@ -589,6 +590,21 @@ std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt) {
 
 // Work buffers of a run (both plan builders end here): ping-pong poses, rotations, pose-stage
 // partial blocks, costs, landmark positions and the iteration state.
+namespace {
+// a finished run's window poses (ping-pong buffer of the last iteration) and optimised landmark
+// positions into the resident map's rows
+__global__ void k_apply_dmap(const BAState* st, const double* kf_pose, int n_kf, const double* lm_pos, int n_opt,
+                             const int* kf_map, const int* lm_map, double* map_pose, double* map_pos) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_kf) {
+        const double* src = kf_pose + (size_t)(st->iterations & 1) * n_kf * 8 + (size_t)8 * i;
+        for (int j = 0; j < 7; ++j) map_pose[(size_t)7 * kf_map[i] + j] = src[j];
+    }
+    if (i < n_opt)
+        for (int j = 0; j < 3; ++j) map_pos[(size_t)3 * lm_map[i] + j] = lm_pos[(size_t)4 * i + j];
+}
+}  // namespace
+
 int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
     const size_t nk = (size_t)p->n_kf;
     VX_HIP(c, p->kf_pose.ensure(nk * 2 * 8 * sizeof(double)));
@@ -827,6 +843,43 @@ int vx_ba_plan_create_ex(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_
     return VX_OK;
 }
 
+int vx_ba_plan_create_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_options* opt, int shard_rank,
+                           int shard_count, vx_ba_plan** out) {
+    if (!c || !out || !opt || !m || m->c != c) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_plan_create_dmap: bad arguments") : VX_ERR_INVALID;
+    *out = nullptr;
+    if (opt->max_iterations < 0 || opt->max_iterations > kMaxIter)
+        return set_error(c, VX_ERR_INVALID, "max_iterations must be in [0, %d]", kMaxIter);
+    if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count)
+        return set_error(c, VX_ERR_INVALID, "bad shard %d/%d", shard_rank, shard_count);
+    auto* p = new vx_ba_plan();
+    p->c = c;
+    p->opt = *opt;
+    p->shard_rank = shard_rank;
+    p->shard_count = shard_count;
+    p->from_dmap = true;
+    const int rc = build_plan_dmap(c, m, ref, has_ref, p);
+    if (rc) {
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return VX_OK;
+}
+
+int vx_ba_plan_apply_dmap(vx_ctx* c, vx_ba_plan* p, vx_dmap* m) {
+    if (!c || !p || !m || p->c != c || m->c != c) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_plan_apply_dmap: bad arguments") : VX_ERR_INVALID;
+    if (!p->from_dmap) return set_error(c, VX_ERR_STATE, "plan was not built from a vx_dmap");
+    if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
+    if (p->status != 0) return VX_OK;
+    const int n = std::max(p->n_kf, p->n_opt);
+    hipLaunchKernelGGL(k_apply_dmap, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const BAState*)p->state.as<BAState>(),
+                       (const double*)p->kf_pose.as<double>(), p->n_kf, (const double*)p->lm_pos.as<double>(), p->n_opt,
+                       (const int*)p->kf_map_dev.as<int>(), (const int*)p->lm_map_dev.as<int>(), m->kf_pose.as<double>(),
+                       m->lm_pos.as<double>());
+    VX_LAUNCH_CHECK(c, "k_apply_dmap");
+    return VX_OK;
+}
+
 int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
     if (p->shard_count > 1 || p->status != 0) return plan_run(c, p);  // (RCCL calls stay outside graphs)
@@ -837,6 +890,7 @@ int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
 int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
     if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
+    if (m && p->from_dmap) return set_error(c, VX_ERR_STATE, "dmap plan: scatter with vx_ba_plan_apply_dmap");
     vx_ba_stats s{};
     s.gate_margin = -1.0;
     s.status = p->status;

@@ -21,7 +21,11 @@ struct vx_ba_plan {
     int n_lm_blocks = 1;
     bool ran = false;
     vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
+    vx::DevBuf kf_map_dev, lm_map_dev;  // plans built from a vx_dmap: window row / slot -> map index
+    bool from_dmap = false;
 };
+
+struct vx_dmap;
 
 namespace vx {
 constexpr int kBaPoseBlock = 512;  // k_pose_kf threads per workgroup (ba.hip kPoseBlock)
@@ -31,6 +35,8 @@ constexpr int kBaMaxSplit = 4;     // pose-stage workgroups per keyframe
 int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p);
 // SelectKeyFrames + landmark set + both CSRs built on the device from the map snapshot (§8f rank 2)
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
+// the same plan from a device-resident map (vx_dmap; its CSR rebuilt first if stale)
+int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
 // greedy k_landmark_solve workgroup packing over the landmark-stage CSR pointers
 std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt);
 }  // namespace vx

@@ -32,6 +32,7 @@
 #include "vx_internal.hpp"
 #include "ba_common.hpp"
 #include "ba_plan.hpp"
+#include "dmap.hpp"
 
 namespace vx {
 namespace {
@@ -261,6 +262,44 @@ int scan(vx_ctx* c, DevBuf& tmp, const int* in, int* out, int n) {
 
 }  // namespace
 
+// device inputs of the build: the window's features (keyframe rows in ascending id order) and the
+// map's landmarks with their landmark-major observation CSR
+struct BuildInputs {
+    int nk, nf, nl;
+    const int* wptr;
+    const uint64_t* wlm;
+    const uint8_t* wfl;
+    const uint8_t* cam;
+    const uint64_t* wid;
+    const double* wuv;
+    const uint64_t* lid;
+    const uint8_t* bad;
+    const int64_t* optr;
+    const uint64_t* okf;
+    const uint64_t* ofi;
+    const double* pos;
+};
+
+namespace {
+int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, const std::vector<int>& kf_flags,
+               vx_ba_plan* p);
+
+// SelectKeyFrames (local_ba.cpp:42-62) over keyframe ids: newest `window` with id <= max_id, in
+// ascending id order (as indices into `ids`)
+std::vector<int> select_ids(const uint64_t* ids, int n, uint64_t ref_kf_id, int has_ref, int window_size) {
+    std::vector<int> order(n);
+    for (int i = 0; i < n; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int x, int y) { return ids[x] < ids[y]; });
+    const int window = std::max(1, window_size);
+    const uint64_t max_id = has_ref ? ref_kf_id : ids[order.back()];
+    std::vector<int> win;
+    for (int i = n - 1; i >= 0 && (int)win.size() < window; --i)
+        if (ids[order[i]] <= max_id) win.push_back(order[i]);
+    std::reverse(win.begin(), win.end());
+    return win;
+}
+}  // namespace
+
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p) {
     const vx_ba_options& o = p->opt;
     p->status = 1;
@@ -268,15 +307,7 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     p->n_landmarks_global = 0;
     if (!m || m->n_kf <= 0) return VX_OK;
     // ---- SelectKeyFrames (local_ba.cpp:42-62): host, over the keyframe ids only
-    std::vector<int> order(m->n_kf);
-    for (int i = 0; i < m->n_kf; ++i) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](int x, int y) { return m->kf_id[x] < m->kf_id[y]; });
-    const int window = std::max(1, (int)o.window_size);
-    const uint64_t max_id = has_ref ? ref_kf_id : m->kf_id[order.back()];
-    std::vector<int> win;
-    for (int i = m->n_kf - 1; i >= 0 && (int)win.size() < window; --i)
-        if (m->kf_id[order[i]] <= max_id) win.push_back(order[i]);
-    std::reverse(win.begin(), win.end());
+    const std::vector<int> win = select_ids(m->kf_id, m->n_kf, ref_kf_id, has_ref, o.window_size);
     const int nk = (int)win.size();
     p->n_window_kf = nk;
     if (nk < 2) return VX_OK;
@@ -310,9 +341,6 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     p->n_split = (int)std::min<int64_t>(kBaMaxSplit, std::max<int64_t>(1, (mx + kBaPoseBlock - 1) / kBaPoseBlock));
     const int nl = m->n_lm;
     const int64_t nobs = nl > 0 ? m->lm_obs_ptr[nl] : 0;
-    unsigned hcap = 1024;
-    while (hcap < 2u * (unsigned)std::max(nl, 1)) hcap <<= 1;
-
     VX_HIP(c, hipSetDevice(c->device));
     vx_ctx::PlanScratch& B = c->plan_scratch;  // reused across this context's plan builds
     int rc;
@@ -328,6 +356,26 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     if ((rc = up(c, B.okf, m->obs_kf_id, (size_t)nobs))) return rc;
     if ((rc = up(c, B.ofi, m->obs_feat_idx, (size_t)nobs))) return rc;
     if ((rc = up(c, B.pos, m->lm_pos, (size_t)nl * 3))) return rc;
+    if ((rc = up(c, p->kf_pose0, pose0.data(), pose0.size()))) return rc;
+    if ((rc = up(c, p->kf_intr, intr.data(), intr.size()))) return rc;
+    BuildInputs in{nk, nf, nl, B.wptr.as<int>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(), B.cam.as<uint8_t>(),
+                   B.wid.as<uint64_t>(), B.wuv.as<double>(), B.lid.as<uint64_t>(), B.bad.as<uint8_t>(),
+                   B.optr.as<int64_t>(), B.okf.as<uint64_t>(), B.ofi.as<uint64_t>(), B.pos.as<double>()};
+    rc = build_core(c, in, win, kf_flags, p);
+    VX_HIP(c, hipStreamSynchronize(c->stream));  // the host vectors above must outlive their async copies
+    return rc;
+}
+
+namespace {
+int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, const std::vector<int>& kf_flags,
+               vx_ba_plan* p) {
+    const vx_ba_options& o = p->opt;
+    const int nk = in.nk, nf = in.nf, nl = in.nl;
+    vx_ctx::PlanScratch& B = c->plan_scratch;
+    int rc;
+    unsigned hcap = 1024;
+    while (hcap < 2u * (unsigned)std::max(nl, 1)) hcap <<= 1;
+
     VX_HIP(c, B.hkey.ensure((size_t)hcap * 8));
     VX_HIP(c, B.hval.ensure((size_t)hcap * 4));
     VX_HIP(c, hipMemsetAsync(B.hkey.p, 0xff, (size_t)hcap * 8, c->stream));
@@ -345,17 +393,17 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     WinArgs a{};
     a.nk = nk;
     a.nf = nf;
-    a.wptr = B.wptr.as<int>();
-    a.wlm = B.wlm.as<uint64_t>();
-    a.wfl = B.wfl.as<uint8_t>();
-    a.cam = B.cam.as<uint8_t>();
-    a.wid = B.wid.as<uint64_t>();
+    a.wptr = in.wptr;
+    a.wlm = in.wlm;
+    a.wfl = in.wfl;
+    a.cam = in.cam;
+    a.wid = in.wid;
     a.nl = nl;
-    a.lid = B.lid.as<uint64_t>();
-    a.bad = B.bad.as<uint8_t>();
-    a.optr = B.optr.as<int64_t>();
-    a.okf = B.okf.as<uint64_t>();
-    a.ofi = B.ofi.as<uint64_t>();
+    a.lid = in.lid;
+    a.bad = in.bad;
+    a.optr = in.optr;
+    a.okf = in.okf;
+    a.ofi = in.ofi;
     a.hkey = B.hkey.as<uint64_t>();
     a.hval = B.hval.as<int>();
     a.hmask = hcap - 1;
@@ -410,7 +458,7 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     VX_HIP(c, p->pobs_lm.ensure((size_t)std::max(n_pose, 1) * 4));
     VX_HIP(c, p->kf_obs_ptr.ensure((size_t)(nk + 1) * 4));
     hipLaunchKernelGGL(k_pose_fill, dim3(grid(std::max(nf, nk + 1))), dim3(kT), 0, s, a, pscan,
-                       (const double*)B.wuv.as<double>(), p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(),
+                       in.wuv, p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(),
                        p->kf_obs_ptr.as<int>(), n_pose);
     // landmark-stage CSR
     int* cnt = B.cnt.as<int>();
@@ -431,20 +479,122 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     VX_HIP(c, p->lobs_lm.ensure((size_t)std::max(n_lobs, 1) * 4));
     VX_HIP(c, p->lobs_uv.ensure((size_t)std::max(n_lobs, 1) * sizeof(double2)));
     hipLaunchKernelGGL(k_lobs_fill, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, p->lobs_ptr.as<int>(),
-                       (const double*)B.wuv.as<double>(), p->lobs_kf.as<int>(), p->lobs_lm.as<int>(),
+                       in.wuv, p->lobs_kf.as<int>(), p->lobs_lm.as<int>(),
                        p->lobs_uv.as<double2>());
     VX_HIP(c, p->lm_pos0.ensure((size_t)std::max(n_lm, 1) * 4 * sizeof(double)));
     hipLaunchKernelGGL(k_lm_gather, dim3(grid(n_lm)), dim3(kT), 0, s, (const int*)inv, n_lm,
-                       (const double*)B.pos.as<double>(), p->lm_pos0.as<double>());
+                       in.pos, p->lm_pos0.as<double>());
     VX_LAUNCH_CHECK(c, "plan fill kernels");
     const std::vector<int> blk = pack_lm_blocks(lptr, n_opt);
     p->n_lm_blocks = (int)blk.size() - 1;
     if ((rc = up(c, p->lm_blk, blk.data(), blk.size()))) return rc;
-    if ((rc = up(c, p->kf_pose0, pose0.data(), pose0.size()))) return rc;
-    if ((rc = up(c, p->kf_intr, intr.data(), intr.size()))) return rc;
     if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
     if ((rc = alloc_run_buffers(c, p))) return rc;
     VX_HIP(c, hipStreamSynchronize(s));  // the host vectors above must outlive their async copies
+    return VX_OK;
+}
+}  // namespace
+
+
+
+// ---------------------------------------------------------------- plan from the resident map
+namespace {
+// window features out of the resident feature arrays: output feature f of window row r (found by
+// binary search over wptr) is resident feature src[r] + (f - wptr[r])
+__global__ __launch_bounds__(kT) void k_gather_window(int nk, int nf, const int* wptr, const int64_t* src,
+                                                      const double* uv, const uint64_t* lm, const uint8_t* fl,
+                                                      double* wuv, uint64_t* wlm, uint8_t* wfl) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f >= nf) return;
+    int lo = 0, hi = nk;  // largest r with wptr[r] <= f
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (wptr[mid] <= f) lo = mid;
+        else hi = mid;
+    }
+    const int64_t g = src[lo] + (f - wptr[lo]);
+    wuv[2 * f] = uv[2 * g];
+    wuv[2 * f + 1] = uv[2 * g + 1];
+    wlm[f] = lm[g];
+    wfl[f] = fl[g];
+}
+// window keyframes' poses (8-double rows, last 0) and intrinsics
+__global__ void k_gather_kf(int nk, const int* win, const double* pose, const double* intr, double* pose0,
+                            double* intr0) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nk) return;
+    const int k = win[r];
+    for (int j = 0; j < 7; ++j) pose0[8 * r + j] = pose[7 * k + j];
+    pose0[8 * r + 7] = 0.0;
+    for (int j = 0; j < 4; ++j) intr0[4 * r + j] = intr[4 * k + j];
+}
+}  // namespace
+
+int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p) {
+    const vx_ba_options& o = p->opt;
+    p->status = 1;
+    p->n_window_kf = 0;
+    p->n_landmarks_global = 0;
+    const int n_kf = (int)m->kf_id.size();
+    if (n_kf <= 0) return VX_OK;
+    const std::vector<int> win = select_ids(m->kf_id.data(), n_kf, ref_kf_id, has_ref, o.window_size);
+    const int nk = (int)win.size();
+    p->n_window_kf = nk;
+    if (nk < 2) return VX_OK;
+    // host: the window's feature ranges and keyframe tables (keyframe-sized, from the mirrors)
+    std::vector<int> wptr(nk + 1, 0), kf_flags(nk);
+    std::vector<int64_t> src(nk);
+    std::vector<uint64_t> wid(nk);
+    std::vector<uint8_t> cam(nk);
+    int64_t mx = 0;
+    for (int r = 0; r < nk; ++r) {
+        const int k = win[r];
+        src[r] = m->kf_feat_ptr[k];
+        wptr[r + 1] = wptr[r] + (int)(m->kf_feat_ptr[k + 1] - m->kf_feat_ptr[k]);
+        wid[r] = m->kf_id[k];
+        cam[r] = m->kf_has_cam[k];
+        kf_flags[r] = cam[r];
+        if (cam[r]) mx = std::max<int64_t>(mx, m->kf_valid_cnt[k]);
+    }
+    p->n_split = (int)std::min<int64_t>(kBaMaxSplit, std::max<int64_t>(1, (mx + kBaPoseBlock - 1) / kBaPoseBlock));
+    const int nf = wptr[nk];
+    VX_HIP(c, hipSetDevice(c->device));
+    vx_ctx::PlanScratch& B = c->plan_scratch;
+    int rc;
+    if ((rc = up(c, B.wptr, wptr.data(), wptr.size()))) return rc;
+    if ((rc = up(c, B.cam, cam.data(), cam.size()))) return rc;
+    if ((rc = up(c, B.wid, wid.data(), wid.size()))) return rc;
+    if ((rc = up(c, B.optr /* staging: source offsets, then window rows */, src.data(), src.size()))) return rc;
+    VX_HIP(c, B.wlm.ensure((size_t)std::max(nf, 1) * 8));
+    VX_HIP(c, B.wfl.ensure((size_t)std::max(nf, 1)));
+    VX_HIP(c, B.wuv.ensure((size_t)std::max(nf, 1) * 16));
+    hipLaunchKernelGGL(k_gather_window, dim3(grid(nf)), dim3(kT), 0, c->stream, nk, nf, (const int*)B.wptr.as<int>(),
+                       (const int64_t*)B.optr.as<int64_t>(), (const double*)m->feat_uv.as<double>(),
+                       (const uint64_t*)m->feat_lm.as<uint64_t>(), (const uint8_t*)m->feat_fl.as<uint8_t>(),
+                       B.wuv.as<double>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>());
+    VX_LAUNCH_CHECK(c, "k_gather_window");
+    std::vector<int> win_i(win.begin(), win.end());
+    if ((rc = up(c, B.okf /* staging: window keyframe indices */, win_i.data(), win_i.size()))) return rc;
+    VX_HIP(c, p->kf_pose0.ensure((size_t)nk * 8 * sizeof(double)));
+    VX_HIP(c, p->kf_intr.ensure((size_t)nk * 4 * sizeof(double)));
+    hipLaunchKernelGGL(k_gather_kf, dim3(grid(nk)), dim3(kT), 0, c->stream, nk, (const int*)B.okf.as<int>(),
+                       (const double*)m->kf_pose.as<double>(), (const double*)m->kf_intr.as<double>(),
+                       p->kf_pose0.as<double>(), p->kf_intr.as<double>());
+    VX_LAUNCH_CHECK(c, "k_gather_kf");
+    if ((rc = dmap_build_csr(c, m))) return rc;
+    const int nl = (int)m->n_lm;
+    BuildInputs in{nk, nf, nl, B.wptr.as<int>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(), B.cam.as<uint8_t>(),
+                   B.wid.as<uint64_t>(), B.wuv.as<double>(), m->lm_id.as<uint64_t>(), m->lm_bad.as<uint8_t>(),
+                   m->optr.as<int64_t>(), m->okf.as<uint64_t>(), m->ofi.as<uint64_t>(), m->lm_pos.as<double>()};
+    rc = build_core(c, in, win, kf_flags, p);
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (rc) return rc;
+    // device copies of the slot -> map index tables for vx_ba_plan_apply_dmap
+    if (p->status == 0) {
+        if ((rc = up(c, p->kf_map_dev, p->kf_map_idx.data(), p->kf_map_idx.size()))) return rc;
+        if ((rc = up(c, p->lm_map_dev, p->lm_map_idx.data(), p->lm_map_idx.size()))) return rc;
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+    }
     return VX_OK;
 }
 

@@ -1,0 +1,296 @@
+// dmap.hip — the device-resident map (vx_dmap_*).
+//
+// The reference rebuilds LocalBA's input from visionx::Map on every keyframe
+// (local_ba.cpp:42-108: std::map / unordered_map walks under mutexes), and a snapshot-based drop-in
+// still ships the whole map over PCIe per plan.  Here the map lives on the device and is updated by
+// the same events that change the reference's Map (Map::InsertKeyFrame, Map::InsertLandmark,
+// Landmark::AddObservation, Feature::landmark_id_, Landmark::SetBad, Frame::SetPose): each update
+// is one small host-to-device copy of the new rows, appended (or scattered) into arrays grown by
+// doubling.  Landmarks' observation lists are an append-only list; the landmark-major CSR the plan
+// build reads is rebuilt lazily by a stable radix sort (rocPRIM) when it changed, which keeps each
+// landmark's observations in insertion order.
+#include <algorithm>
+#include <cstring>
+
+#include <rocprim/rocprim.hpp>
+
+#include "dmap.hpp"
+
+namespace vx {
+namespace {
+
+constexpr int kT = 256;
+inline unsigned grid(long long n) { return (unsigned)std::max(1ll, (n + kT - 1) / kT); }
+
+// make room for `want` bytes keeping the first `used` bytes (doubling; device-to-device copy)
+int grow(vx_ctx* c, DevBuf& d, size_t used, size_t want) {
+    if (want <= d.bytes) return VX_OK;
+    size_t cap = std::max<size_t>(d.bytes * 2, 4096);
+    while (cap < want) cap *= 2;
+    void* np = nullptr;
+    VX_HIP(c, hipMalloc(&np, cap));
+    if (used) VX_HIP(c, hipMemcpyAsync(np, d.p, used, hipMemcpyDeviceToDevice, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    d.release();
+    d.p = np;
+    d.bytes = cap;
+    return VX_OK;
+}
+
+// append n elements of T (host) at element offset `at` of a device array
+template <class T>
+int append(vx_ctx* c, DevBuf& d, int64_t at, const T* h, int64_t n) {
+    int rc;
+    if ((rc = grow(c, d, (size_t)at * sizeof(T), (size_t)(at + n) * sizeof(T)))) return rc;
+    if (n) {
+        VX_HIP(c, hipMemcpyAsync(d.as<T>() + at, h, (size_t)n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));  // the caller's host rows may go away on return
+    }
+    return VX_OK;
+}
+
+// scatter rows of `width` elements: dst[idx[i] * width + j] = src[i * width + j]
+template <class T>
+__global__ void k_scatter_rows(T* dst, const int64_t* idx, const T* src, int n, int width) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)n * width) return;
+    const int64_t i = e / width, j = e - i * width;
+    dst[idx[i] * width + j] = src[e];
+}
+
+template <class T>
+int scatter(vx_ctx* c, DevBuf& dst, const std::vector<int64_t>& idx, const T* src, int width) {
+    const int n = (int)idx.size();
+    if (!n) return VX_OK;
+    // one staging allocation: indices then values
+    const size_t ib = (size_t)n * sizeof(int64_t), vb = (size_t)n * width * sizeof(T);
+    DevBuf tmp;
+    VX_HIP(c, tmp.ensure(ib + vb));
+    VX_HIP(c, hipMemcpyAsync(tmp.p, idx.data(), ib, hipMemcpyHostToDevice, c->stream));
+    VX_HIP(c, hipMemcpyAsync(tmp.as<uint8_t>() + ib, src, vb, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_scatter_rows<T>, dim3(grid((long long)n * width)), dim3(kT), 0, c->stream, dst.as<T>(),
+                       tmp.as<int64_t>(), reinterpret_cast<const T*>(tmp.as<uint8_t>() + ib), n, width);
+    VX_LAUNCH_CHECK(c, "k_scatter_rows");
+    VX_HIP(c, hipStreamSynchronize(c->stream));  // tmp is freed on return
+    return VX_OK;
+}
+
+__global__ void k_iota(int* v, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (int)i;
+}
+__global__ void k_count(const int* keys, int64_t n, int* cnt) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&cnt[keys[i]], 1);
+}
+// sorted order -> CSR payload; int32 prefix -> int64 pointers
+__global__ void k_csr_fill(const int* perm, int64_t n, const uint64_t* okf_in, const uint64_t* ofi_in,
+                           uint64_t* okf, uint64_t* ofi, const int* scan, int64_t n_lm, int64_t* optr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const int j = perm[i];
+        okf[i] = okf_in[j];
+        ofi[i] = ofi_in[j];
+    }
+    if (i <= n_lm) optr[i] = scan[i];
+}
+
+}  // namespace
+
+int dmap_build_csr(vx_ctx* c, vx_dmap* m) {
+    if (!m->csr_dirty) return VX_OK;
+    const int64_t n = m->n_obs, nl = m->n_lm;
+    hipStream_t s = c->stream;
+    VX_HIP(c, m->optr.ensure((size_t)(nl + 1) * sizeof(int64_t)));
+    VX_HIP(c, m->okf.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+    VX_HIP(c, m->ofi.ensure((size_t)std::max<int64_t>(n, 1) * 8));
+    VX_HIP(c, m->cnt.ensure((size_t)(nl + 1) * 4 * 2));
+    int* cnt = m->cnt.as<int>();
+    int* scn = cnt + (nl + 1);
+    VX_HIP(c, hipMemsetAsync(cnt, 0, (size_t)(nl + 1) * 4, s));
+    if (n > 0) {
+        for (DevBuf* d : {&m->sort_keys, &m->sort_keys2, &m->sort_vals, &m->sort_vals2})
+            VX_HIP(c, d->ensure((size_t)n * 4));
+        hipLaunchKernelGGL(k_iota, dim3(grid(n)), dim3(kT), 0, s, m->sort_vals.as<int>(), n);
+        hipLaunchKernelGGL(k_count, dim3(grid(n)), dim3(kT), 0, s, m->obs_lm.as<int>(), n, cnt);
+        VX_LAUNCH_CHECK(c, "dmap csr count");
+        unsigned bits = 1;
+        while ((1ll << bits) <= nl) ++bits;
+        size_t bytes = 0;
+        VX_HIP(c, rocprim::radix_sort_pairs(nullptr, bytes, m->obs_lm.as<int>(), m->sort_keys2.as<int>(),
+                                            m->sort_vals.as<int>(), m->sort_vals2.as<int>(), (size_t)n, 0, bits, s));
+        VX_HIP(c, m->tmp.ensure(std::max<size_t>(bytes, 16)));
+        VX_HIP(c, rocprim::radix_sort_pairs(m->tmp.p, bytes, m->obs_lm.as<int>(), m->sort_keys2.as<int>(),
+                                            m->sort_vals.as<int>(), m->sort_vals2.as<int>(), (size_t)n, 0, bits, s));
+    }
+    size_t bytes = 0;
+    VX_HIP(c, rocprim::exclusive_scan(nullptr, bytes, cnt, scn, 0, (size_t)nl + 1, rocprim::plus<int>(), s));
+    VX_HIP(c, m->tmp.ensure(std::max<size_t>(bytes, 16)));
+    VX_HIP(c, rocprim::exclusive_scan(m->tmp.p, bytes, cnt, scn, 0, (size_t)nl + 1, rocprim::plus<int>(), s));
+    hipLaunchKernelGGL(k_csr_fill, dim3(grid(std::max<int64_t>(n, nl + 1))), dim3(kT), 0, s,
+                       (const int*)m->sort_vals2.as<int>(), n, (const uint64_t*)m->obs_kf.as<uint64_t>(),
+                       (const uint64_t*)m->obs_fi.as<uint64_t>(), m->okf.as<uint64_t>(), m->ofi.as<uint64_t>(),
+                       (const int*)scn, nl, m->optr.as<int64_t>());
+    VX_LAUNCH_CHECK(c, "dmap csr fill");
+    m->csr_dirty = false;
+    return VX_OK;
+}
+
+}  // namespace vx
+
+using namespace vx;
+
+extern "C" {
+
+int vx_dmap_create(vx_ctx* c, vx_dmap** out) {
+    if (!c || !out) return c ? set_error(c, VX_ERR_INVALID, "vx_dmap_create: bad arguments") : VX_ERR_INVALID;
+    *out = new vx_dmap();
+    (*out)->c = c;
+    return VX_OK;
+}
+
+void vx_dmap_destroy(vx_dmap* m) { delete m; }
+
+int vx_dmap_add_keyframe(vx_dmap* m, uint64_t kf_id, const double* pose7, const double* intr4, int has_cam,
+                         int n_feat, const double* uv, const uint64_t* lm, const uint8_t* fl) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (!pose7 || n_feat < 0 || (n_feat > 0 && (!uv || !lm || !fl)) || (has_cam && !intr4))
+        return set_error(c, VX_ERR_INVALID, "vx_dmap_add_keyframe: bad arguments");
+    if (m->kf_index.count(kf_id)) return set_error(c, VX_ERR_INVALID, "keyframe %llu already in the map",
+                                                   (unsigned long long)kf_id);
+    VX_HIP(c, hipSetDevice(c->device));
+    const int64_t k = (int64_t)m->kf_id.size(), f0 = m->kf_feat_ptr.back();
+    const double zero4[4] = {0, 0, 0, 0};
+    int rc;
+    if ((rc = append(c, m->kf_pose, 7 * k, pose7, 7))) return rc;
+    if ((rc = append(c, m->kf_intr, 4 * k, has_cam ? intr4 : zero4, 4))) return rc;
+    if ((rc = append(c, m->feat_uv, 2 * f0, uv, 2 * (int64_t)n_feat))) return rc;
+    if ((rc = append(c, m->feat_lm, f0, lm, n_feat))) return rc;
+    if ((rc = append(c, m->feat_fl, f0, fl, n_feat))) return rc;
+    int valid = 0;
+    for (int i = 0; i < n_feat; ++i) valid += fl[i] & 1;
+    m->kf_index[kf_id] = (int)k;
+    m->kf_id.push_back(kf_id);
+    m->kf_feat_ptr.push_back(f0 + n_feat);
+    m->kf_has_cam.push_back(has_cam ? 1 : 0);
+    m->kf_valid_cnt.push_back(valid);
+    m->feat_flags.insert(m->feat_flags.end(), fl, fl + n_feat);
+    return VX_OK;
+}
+
+int vx_dmap_add_landmarks(vx_dmap* m, int n, const uint64_t* id, const double* pos3, const uint8_t* bad) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && (!id || !pos3))) return set_error(c, VX_ERR_INVALID, "vx_dmap_add_landmarks: bad arguments");
+    for (int i = 0; i < n; ++i)
+        if (m->lm_index.count(id[i]))
+            return set_error(c, VX_ERR_INVALID, "landmark %llu already in the map", (unsigned long long)id[i]);
+    VX_HIP(c, hipSetDevice(c->device));
+    std::vector<uint8_t> b(bad ? bad : nullptr, bad ? bad + n : nullptr);
+    if (!bad) b.assign(n, 0);
+    int rc;
+    if ((rc = append(c, m->lm_id, m->n_lm, id, n))) return rc;
+    if ((rc = append(c, m->lm_pos, 3 * m->n_lm, pos3, 3 * (int64_t)n))) return rc;
+    if ((rc = append(c, m->lm_bad, m->n_lm, b.data(), n))) return rc;
+    for (int i = 0; i < n; ++i) m->lm_index[id[i]] = (int)(m->n_lm + i);
+    m->n_lm += n;
+    m->csr_dirty = true;
+    return VX_OK;
+}
+
+int vx_dmap_add_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uint64_t* kf_id, const uint64_t* fi) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && (!lm_id || !kf_id || !fi)))
+        return set_error(c, VX_ERR_INVALID, "vx_dmap_add_observations: bad arguments");
+    std::vector<int> li(n);
+    for (int i = 0; i < n; ++i) {
+        auto it = m->lm_index.find(lm_id[i]);
+        if (it == m->lm_index.end())
+            return set_error(c, VX_ERR_INVALID, "observation of unknown landmark %llu", (unsigned long long)lm_id[i]);
+        li[i] = it->second;
+    }
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = append(c, m->obs_lm, m->n_obs, li.data(), n))) return rc;
+    if ((rc = append(c, m->obs_kf, m->n_obs, kf_id, n))) return rc;
+    if ((rc = append(c, m->obs_fi, m->n_obs, fi, n))) return rc;
+    m->n_obs += n;
+    m->csr_dirty = true;
+    return VX_OK;
+}
+
+int vx_dmap_set_features(vx_dmap* m, uint64_t kf_id, int n, const int32_t* idx, const uint64_t* lm,
+                         const uint8_t* fl) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && (!idx || !lm || !fl))) return set_error(c, VX_ERR_INVALID, "vx_dmap_set_features: bad arguments");
+    auto it = m->kf_index.find(kf_id);
+    if (it == m->kf_index.end()) return set_error(c, VX_ERR_INVALID, "unknown keyframe %llu", (unsigned long long)kf_id);
+    const int k = it->second;
+    const int64_t f0 = m->kf_feat_ptr[k], nf = m->kf_feat_ptr[k + 1] - f0;
+    std::vector<int64_t> g(n);
+    for (int i = 0; i < n; ++i) {
+        if (idx[i] < 0 || idx[i] >= nf) return set_error(c, VX_ERR_INVALID, "feature index %d out of range", idx[i]);
+        g[i] = f0 + idx[i];
+        m->kf_valid_cnt[k] += (fl[i] & 1) - (m->feat_flags[g[i]] & 1);
+        m->feat_flags[g[i]] = fl[i];
+    }
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = scatter(c, m->feat_lm, g, lm, 1))) return rc;
+    if ((rc = scatter(c, m->feat_fl, g, fl, 1))) return rc;
+    return VX_OK;
+}
+
+int vx_dmap_set_landmark_bad(vx_dmap* m, int n, const uint64_t* id, const uint8_t* bad) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && (!id || !bad))) return set_error(c, VX_ERR_INVALID, "vx_dmap_set_landmark_bad: bad arguments");
+    std::vector<int64_t> g(n);
+    for (int i = 0; i < n; ++i) {
+        auto it = m->lm_index.find(id[i]);
+        if (it == m->lm_index.end()) return set_error(c, VX_ERR_INVALID, "unknown landmark %llu", (unsigned long long)id[i]);
+        g[i] = it->second;
+    }
+    VX_HIP(c, hipSetDevice(c->device));
+    return scatter(c, m->lm_bad, g, bad, 1);
+}
+
+int vx_dmap_set_poses(vx_dmap* m, int n, const uint64_t* id, const double* pose7) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && (!id || !pose7))) return set_error(c, VX_ERR_INVALID, "vx_dmap_set_poses: bad arguments");
+    std::vector<int64_t> g(n);
+    for (int i = 0; i < n; ++i) {
+        auto it = m->kf_index.find(id[i]);
+        if (it == m->kf_index.end()) return set_error(c, VX_ERR_INVALID, "unknown keyframe %llu", (unsigned long long)id[i]);
+        g[i] = it->second;
+    }
+    VX_HIP(c, hipSetDevice(c->device));
+    return scatter(c, m->kf_pose, g, pose7, 7);
+}
+
+int vx_dmap_counts(const vx_dmap* m, int64_t* out4) {
+    if (!m || !out4) return VX_ERR_INVALID;
+    out4[0] = (int64_t)m->kf_id.size();
+    out4[1] = m->kf_feat_ptr.back();
+    out4[2] = m->n_lm;
+    out4[3] = m->n_obs;
+    return VX_OK;
+}
+
+int vx_dmap_download(vx_dmap* m, double* kf_pose, double* lm_pos) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    VX_HIP(c, hipSetDevice(c->device));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    const size_t nk = m->kf_id.size();
+    if (kf_pose && nk) VX_HIP(c, hipMemcpy(kf_pose, m->kf_pose.p, nk * 7 * sizeof(double), hipMemcpyDeviceToHost));
+    if (lm_pos && m->n_lm)
+        VX_HIP(c, hipMemcpy(lm_pos, m->lm_pos.p, (size_t)m->n_lm * 3 * sizeof(double), hipMemcpyDeviceToHost));
+    return VX_OK;
+}
+
+}  // extern "C"

@@ -121,6 +121,8 @@ def lib():
                                             C.c_int, C.c_float]
         L.vx_prof_name.restype = C.c_char_p
         L.vx_ba_plan_destroy.argtypes = [C.c_void_p]
+        L.vx_dmap_destroy.argtypes = [C.c_void_p]
+        L.vx_dmap_destroy.restype = None
         L.vx_ba_plan_destroy.restype = None
         L.vx_orb_default_params.restype = None
         L.vx_ba_default_options.restype = None
@@ -575,9 +577,98 @@ class BAPlan:
                                                C.byref(st)))
         return st
 
+    def apply(self, dmap: "DMap"):
+        """vx_ba_plan_apply_dmap: scatter the run's poses / positions into the resident map."""
+        self.ctx._check(lib().vx_ba_plan_apply_dmap(self.ctx.handle, self._h, dmap.handle))
+
     def close(self):
         if self._h:
             lib().vx_ba_plan_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DMap:
+    """vx_dmap: visionx::Map resident on the device, updated incrementally (include/vx_slam.h)."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+        self._h = C.c_void_p()
+        ctx._check(lib().vx_dmap_create(ctx.handle, C.byref(self._h)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def add_keyframe(self, kf_id, pose7, intr4, has_cam, feat_uv, feat_lm_id, feat_flags):
+        uv = np.ascontiguousarray(feat_uv, np.float64).reshape(-1, 2)
+        lm = np.ascontiguousarray(feat_lm_id, np.uint64)
+        fl = np.ascontiguousarray(feat_flags, np.uint8)
+        pose = np.ascontiguousarray(pose7, np.float64)
+        intr = np.ascontiguousarray(intr4, np.float64)
+        self.ctx._check(lib().vx_dmap_add_keyframe(self._h, C.c_uint64(int(kf_id)), _p(pose), _p(intr),
+                                                   1 if has_cam else 0, len(fl), _p(uv), _p(lm), _p(fl)))
+
+    def add_landmarks(self, ids, pos, bad=None):
+        ids = np.ascontiguousarray(ids, np.uint64)
+        pos = np.ascontiguousarray(pos, np.float64).reshape(-1, 3)
+        b = None if bad is None else np.ascontiguousarray(bad, np.uint8)
+        self.ctx._check(lib().vx_dmap_add_landmarks(self._h, len(ids), _p(ids), _p(pos),
+                                                    None if b is None else _p(b)))
+
+    def add_observations(self, lm_ids, kf_ids, feat_idx):
+        a = np.ascontiguousarray(lm_ids, np.uint64)
+        k = np.ascontiguousarray(kf_ids, np.uint64)
+        f = np.ascontiguousarray(feat_idx, np.uint64)
+        self.ctx._check(lib().vx_dmap_add_observations(self._h, len(a), _p(a), _p(k), _p(f)))
+
+    def set_features(self, kf_id, feat_idx, lm_ids, flags):
+        i = np.ascontiguousarray(feat_idx, np.int32)
+        lm = np.ascontiguousarray(lm_ids, np.uint64)
+        fl = np.ascontiguousarray(flags, np.uint8)
+        self.ctx._check(lib().vx_dmap_set_features(self._h, C.c_uint64(int(kf_id)), len(i), _p(i), _p(lm), _p(fl)))
+
+    def set_landmark_bad(self, ids, bad):
+        ids = np.ascontiguousarray(ids, np.uint64)
+        b = np.ascontiguousarray(bad, np.uint8)
+        self.ctx._check(lib().vx_dmap_set_landmark_bad(self._h, len(ids), _p(ids), _p(b)))
+
+    def set_poses(self, kf_ids, poses):
+        ids = np.ascontiguousarray(kf_ids, np.uint64)
+        ps = np.ascontiguousarray(poses, np.float64).reshape(-1, 7)
+        self.ctx._check(lib().vx_dmap_set_poses(self._h, len(ids), _p(ids), _p(ps)))
+
+    def counts(self):
+        out = np.zeros(4, np.int64)
+        self.ctx._check(lib().vx_dmap_counts(self._h, _p(out)))
+        return dict(zip(["kf", "feat", "lm", "obs"], map(int, out)))
+
+    def download(self):
+        c = self.counts()
+        pose = np.zeros((max(c["kf"], 1), 7))
+        pos = np.zeros((max(c["lm"], 1), 3))
+        self.ctx._check(lib().vx_dmap_download(self._h, _p(pose), _p(pos)))
+        return pose[:c["kf"]], pos[:c["lm"]]
+
+    def plan(self, opts, ref_kf_id=None, shard_rank=0, shard_count=1) -> "BAPlan":
+        """vx_ba_plan_create_dmap: the LocalBA plan from the resident map."""
+        plan = BAPlan.__new__(BAPlan)
+        plan.ctx, plan.m, plan.opts = self.ctx, None, opts
+        plan._h = C.c_void_p()
+        self.ctx._check(lib().vx_ba_plan_create_dmap(self.ctx.handle, self._h,
+                                                     C.c_uint64(0 if ref_kf_id is None else int(ref_kf_id)),
+                                                     0 if ref_kf_id is None else 1, C.byref(opts), shard_rank,
+                                                     shard_count, C.byref(plan._h)))
+        return plan
+
+    def close(self):
+        if self._h:
+            lib().vx_dmap_destroy(self._h)
             self._h = C.c_void_p()
 
     def __del__(self):
@@ -634,3 +725,62 @@ class SBAPlan:
             self.close()
         except Exception:
             pass
+
+
+def dmap_load(dmap: DMap, m, kf_rows=None):
+    """Insert a synth.BAMap into a DMap the way a running system builds its map: keyframes in
+    ascending id order (``kf_rows`` limits it to those snapshot rows, in that order), each with its
+    features; the landmarks first observed by that keyframe; then that keyframe's observations
+    (Landmark::AddObservation, in landmark order).  Returns (kf_order, lm_order): the snapshot
+    keyframe / landmark rows in the DMap's insertion order (landmarks never observed go last)."""
+    ids = m["kf_id"]
+    kf_order = np.argsort(ids, kind="stable") if kf_rows is None else np.asarray(kf_rows)
+    optr = m["lm_obs_ptr"]
+    obs_lm = np.repeat(np.arange(len(m["lm_id"])), np.diff(optr))
+    obs_kf = m["obs_kf_id"]
+    seen = np.zeros(len(m["lm_id"]), bool)
+    lm_order = []
+    for k in kf_order:
+        f0, f1 = m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]
+        dmap.add_keyframe(ids[k], m["kf_pose"].reshape(-1, 7)[k], m["kf_intr"].reshape(-1, 4)[k], m["kf_has_cam"][k],
+                          m["feat_uv"].reshape(-1, 2)[f0:f1], m["feat_lm_id"][f0:f1], m["feat_flags"][f0:f1])
+        sel = np.nonzero(obs_kf == ids[k])[0]  # observation rows of this keyframe, landmark order
+        new = np.unique(obs_lm[sel][~seen[obs_lm[sel]]])
+        if len(new):
+            dmap.add_landmarks(m["lm_id"][new], m["lm_pos"].reshape(-1, 3)[new], m["lm_bad"][new])
+            seen[new] = True
+            lm_order.extend(new.tolist())
+        if len(sel):
+            dmap.add_observations(m["lm_id"][obs_lm[sel]], obs_kf[sel], m["obs_feat_idx"][sel])
+    if kf_rows is None:
+        rest = np.nonzero(~seen)[0]
+        if len(rest):
+            dmap.add_landmarks(m["lm_id"][rest], m["lm_pos"].reshape(-1, 3)[rest], m["lm_bad"][rest])
+            lm_order.extend(rest.tolist())
+    return np.asarray(kf_order), np.asarray(lm_order, np.int64)
+
+
+def map_reorder(m, kf_order, lm_order):
+    """The snapshot with its keyframe / landmark rows permuted (per-landmark observation lists kept)."""
+    out = dict(m)
+    fp = m["kf_feat_ptr"]
+    cnt = np.diff(fp)[kf_order]
+    out["kf_id"] = m["kf_id"][kf_order].copy()
+    out["kf_pose"] = m["kf_pose"].reshape(-1, 7)[kf_order].copy()
+    out["kf_intr"] = m["kf_intr"].reshape(-1, 4)[kf_order].copy()
+    out["kf_has_cam"] = m["kf_has_cam"][kf_order].copy()
+    out["kf_feat_ptr"] = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    fidx = np.concatenate([np.arange(fp[k], fp[k + 1]) for k in kf_order]) if len(kf_order) else np.zeros(0, int)
+    out["feat_uv"] = m["feat_uv"].reshape(-1, 2)[fidx].copy()
+    out["feat_lm_id"] = m["feat_lm_id"][fidx].copy()
+    out["feat_flags"] = m["feat_flags"][fidx].copy()
+    optr = m["lm_obs_ptr"]
+    out["lm_id"] = m["lm_id"][lm_order].copy()
+    out["lm_pos"] = m["lm_pos"].reshape(-1, 3)[lm_order].copy()
+    out["lm_bad"] = m["lm_bad"][lm_order].copy()
+    ocnt = np.diff(optr)[lm_order]
+    out["lm_obs_ptr"] = np.concatenate([[0], np.cumsum(ocnt)]).astype(np.int64)
+    oidx = np.concatenate([np.arange(optr[l], optr[l + 1]) for l in lm_order]) if len(lm_order) else np.zeros(0, int)
+    out["obs_kf_id"] = m["obs_kf_id"][oidx].copy()
+    out["obs_feat_idx"] = m["obs_feat_idx"][oidx].copy()
+    return out
