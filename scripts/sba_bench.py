@@ -18,9 +18,14 @@ ctx = vxslam.Context(0)
 for cfg, (nk, nl, ns) in [("C3", synth.ba_config("C3")), ("C5", synth.ba_config("C5"))]:
     m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
     opts = vxslam.default_sba_options(window=nk, iters=8)
-    t0 = time.perf_counter()
-    plan = ctx.sba_plan(m, opts)
-    build_ms = 1e3 * (time.perf_counter() - t0)
+    builds = []
+    for rep in range(3):  # the first build also allocates the plan's device buffers
+        t0 = time.perf_counter()
+        plan = ctx.sba_plan(m, opts)
+        builds.append(1e3 * (time.perf_counter() - t0))
+        if rep < 2:
+            plan.close()
+    build_ms = min(builds)
     for _ in range(3):
         plan.run_async()
     ctx.synchronize()
@@ -38,7 +43,7 @@ for cfg, (nk, nl, ns) in [("C3", synth.ba_config("C3")), ("C5", synth.ba_config(
     print(json.dumps({"config": cfg, "window_kf": nk, "landmarks": nl, "streams": ns, "plan": plan.info(),
                       "ms_per_optimize": round(ms, 4), "iterations": st.iterations, "accepted": st.accepted,
                       "cost": [round(st.initial_cost, 1), round(st.final_cost, 1)],
-                      "plan_build_ms_host": round(build_ms, 2),
+                      "plan_build_ms_host": round(build_ms, 2), "plan_build_ms_host_first": round(builds[0], 2),
                       "kernel_us_per_launch": {k: round(v[0] * 1e3 / v[1], 2) for k, v in prof.items()
                                                if k.startswith("sba") and v[1]}}), flush=True)
     plan.close()

@@ -666,9 +666,9 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
         for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) {
             const uint8_t fl = m->feat_flags[f];
             if (!(fl & 1) || (fl & 2)) continue;
-            auto it = lm_by_id.find(m->feat_lm_id[f]);
-            if (it == lm_by_id.end()) continue;
-            const int l = it->second;
+            const int l_found = lm_by_id.get(m->feat_lm_id[f]);
+            if (l_found < 0) continue;
+            const int l = l_found;
             if (m->lm_bad[l] || !owned(l)) continue;
             if (slot_of[l] < 0) {
                 slot_of[l] = (int)p->lm_map_idx.size();

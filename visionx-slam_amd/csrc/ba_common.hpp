@@ -266,6 +266,37 @@ inline uint64_t splitmix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
+// landmark id -> map index: open addressing over a power-of-two table (splitmix64 probe start,
+// linear probing); ids are unique in a map.  Several times faster than std::unordered_map for the
+// 10^5-landmark maps of C4 / C5, where the host plan builds spend most of their time here.
+struct FlatIdMap {
+    std::vector<uint64_t> key;
+    std::vector<int> val;
+    uint64_t mask = 0;
+    void build(const uint64_t* ids, int n) {
+        size_t cap = 16;
+        while (cap < 2 * (size_t)std::max(n, 1)) cap <<= 1;
+        key.assign(cap, 0);
+        val.assign(cap, -1);
+        mask = cap - 1;
+        for (int i = 0; i < n; ++i) {
+            uint64_t h = splitmix64(ids[i]) & mask;
+            while (val[h] >= 0 && key[h] != ids[i]) h = (h + 1) & mask;
+            key[h] = ids[i];
+            val[h] = i;
+        }
+    }
+    int get(uint64_t id) const {  // map index or -1
+        if (val.empty()) return -1;
+        uint64_t h = splitmix64(id) & mask;
+        while (val[h] >= 0) {
+            if (key[h] == id) return val[h];
+            h = (h + 1) & mask;
+        }
+        return -1;
+    }
+};
+
 // SelectKeyFrames (local_ba.cpp:42-62) and the optimised landmark set (:77-108) of a map snapshot:
 // `win` = map keyframe indices of the window in ascending id order (the reference's std::map
 // order), `opt_all` = map indices of the landmarks that pass !IsBad and the total observation
@@ -274,7 +305,7 @@ struct Window {
     int status = 1;
     std::vector<int> win;
     std::unordered_map<uint64_t, int> win_row;  // keyframe id -> window row
-    std::unordered_map<uint64_t, int> lm_by_id; // landmark id -> map index
+    FlatIdMap lm_by_id;                         // landmark id -> map index
     std::vector<int> opt_all;
 };
 
@@ -294,21 +325,21 @@ inline void select_window(const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     std::reverse(w.win.begin(), w.win.end());
     if (w.win.size() < 2) return;
     for (int r = 0; r < (int)w.win.size(); ++r) w.win_row[m->kf_id[w.win[r]]] = r;
-    w.lm_by_id.reserve((size_t)m->n_lm * 2);
-    for (int i = 0; i < m->n_lm; ++i) w.lm_by_id[m->lm_id[i]] = i;
-    std::unordered_set<uint64_t> lm_ids;
+    w.lm_by_id.build(m->lm_id, m->n_lm);
+    // landmarks referenced by a window feature (the reference's unordered_set of ids), then the
+    // filter, in map-index order
+    std::vector<uint8_t> ref((size_t)std::max(m->n_lm, 1), 0);
     for (int k : w.win)
         for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f)
-            if (m->feat_flags[f] & 1) lm_ids.insert(m->feat_lm_id[f]);
-    for (uint64_t id : lm_ids) {
-        auto it = w.lm_by_id.find(id);
-        if (it == w.lm_by_id.end()) continue;
-        const int l = it->second;
-        if (m->lm_bad[l]) continue;
+            if (m->feat_flags[f] & 1) {
+                const int l = w.lm_by_id.get(m->feat_lm_id[f]);
+                if (l >= 0) ref[l] = 1;
+            }
+    for (int l = 0; l < m->n_lm; ++l) {
+        if (!ref[l] || m->lm_bad[l]) continue;
         if (m->lm_obs_ptr[l + 1] - m->lm_obs_ptr[l] < (int64_t)min_point_observations) continue;
         w.opt_all.push_back(l);
     }
-    std::sort(w.opt_all.begin(), w.opt_all.end());
     if (!w.opt_all.empty()) w.status = 0;
 }
 

@@ -34,6 +34,9 @@
 #include <cmath>
 #include <cstring>
 #include <numeric>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <unordered_map>
 #include <vector>
 
@@ -883,12 +886,21 @@ int find_root(std::vector<int>& par, int x) {
 
 int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_sba_plan* p) {
     const vx_sba_options& o = p->opt;
+    static const bool timing = std::getenv("VX_SBA_PLAN_TIMING") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!timing) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "sba plan %-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     p->status = 1;
     Window W;
     select_window(m, ref_kf_id, has_ref, o.window_size, o.min_point_observations, W);
     p->n_window_kf = (int)W.win.size();
     p->n_landmarks_global = (int)W.opt_all.size();
     if (W.status != 0) return VX_OK;
+    lap("window");
     p->status = 0;
     const std::vector<int>& win = W.win;
     const int nk = (int)win.size();
@@ -911,9 +923,10 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     // ---- keyframes and observations (the pose stage's set, local_ba.cpp:126-138)
     std::vector<double> pose0((size_t)nk * 8, 0.0), intr((size_t)nk * 4, 0.0);
     std::vector<int> flags(nk, 0);
+    // pass 1: the pose-stage observations in keyframe-major order, slots assigned as met
     struct HObs { int kf, slot; double u, v; };
-    std::vector<std::vector<HObs>> per_slot(n_opt);
-    std::vector<HObs> fixed_obs;
+    std::vector<HObs> all;
+    all.reserve(4096);
     for (int r = 0; r < nk; ++r) {
         const int k = win[r];
         for (int j = 0; j < 7; ++j) pose0[8 * r + j] = m->kf_pose[7 * k + j];
@@ -924,41 +937,42 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
         for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) {
             const uint8_t fl = m->feat_flags[f];
             if (!(fl & 1) || (fl & 2)) continue;
-            auto it = W.lm_by_id.find(m->feat_lm_id[f]);
-            if (it == W.lm_by_id.end()) continue;
-            const int l = it->second;
+            const int l = W.lm_by_id.get(m->feat_lm_id[f]);
+            if (l < 0) continue;
             if (m->lm_bad[l] || !owned(l)) continue;
             if (slot_of[l] < 0) {  // a landmark the pose stage sees but BA does not optimise
                 slot_of[l] = (int)p->lm_map_idx.size();
                 p->lm_map_idx.push_back(l);
             }
-            const HObs ob{r, slot_of[l], m->feat_uv[2 * f], m->feat_uv[2 * f + 1]};
-            if (ob.slot < n_opt)
-                per_slot[ob.slot].push_back(ob);
-            else
-                fixed_obs.push_back(ob);
+            all.push_back(HObs{r, slot_of[l], m->feat_uv[2 * f], m->feat_uv[2 * f + 1]});
         }
     }
     p->n_lm = (int)p->lm_map_idx.size();
-    std::vector<double2> ouv;
-    std::vector<int> okf, olm, lptr(n_opt + 1, 0);
-    for (int s = 0; s < n_opt; ++s) {
-        if ((int)per_slot[s].size() > kLmThreads)
-            return set_error(c, VX_ERR_INVALID, "landmark with %d observations in the window (max %d)",
-                             (int)per_slot[s].size(), kLmThreads);
-        for (const HObs& ob : per_slot[s]) {
-            ouv.push_back(make_double2(ob.u, ob.v));
-            okf.push_back(ob.kf);
-            olm.push_back(ob.slot);
+    // pass 2: stable counting sort into landmark-major order for the optimised slots (keyframe
+    // order within a landmark), then the fixed landmarks' observations in keyframe-major order
+    std::vector<int> lptr(n_opt + 1, 0);
+    for (const HObs& ob : all)
+        if (ob.slot < n_opt) ++lptr[ob.slot + 1];
+    for (int sl = 0; sl < n_opt; ++sl) {
+        if (lptr[sl + 1] > kLmThreads)
+            return set_error(c, VX_ERR_INVALID, "landmark with %d observations in the window (max %d)", lptr[sl + 1],
+                             kLmThreads);
+        lptr[sl + 1] += lptr[sl];
+    }
+    const int n_oo = lptr[n_opt];
+    std::vector<double2> ouv(all.size());
+    std::vector<int> okf(all.size()), olm(all.size());
+    {
+        std::vector<int> fill(lptr.begin(), lptr.end() - 1);
+        int fo = n_oo;
+        for (const HObs& ob : all) {
+            const int at = ob.slot < n_opt ? fill[ob.slot]++ : fo++;
+            ouv[at] = make_double2(ob.u, ob.v);
+            okf[at] = ob.kf;
+            olm[at] = ob.slot;
         }
-        lptr[s + 1] = (int)okf.size();
     }
-    p->n_oo = (int)okf.size();
-    for (const HObs& ob : fixed_obs) {
-        ouv.push_back(make_double2(ob.u, ob.v));
-        okf.push_back(ob.kf);
-        olm.push_back(ob.slot);
-    }
+    p->n_oo = n_oo;
     p->n_obs = (int)okf.size();
     std::vector<double> lm0((size_t)std::max(p->n_lm, 1) * 4, 0.0);
     for (int s = 0; s < p->n_lm; ++s)
@@ -988,6 +1002,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
         for (int ob = 0; ob < p->n_obs; ++ob) kobs[fill[okf[ob]]++] = ob;
     }
 
+    lap("observations");
     // ---- connected components of the free keyframes' covisibility graph
     std::vector<int> par(nk);
     std::iota(par.begin(), par.end(), 0);
@@ -1040,57 +1055,52 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     p->l_total = lo;
     p->comp_loff_h = loff;
 
+    lap("components");
     // ---- blocks of the reduced system: every keyframe's diagonal block, then the off-diagonal
     // (i > j) blocks of co-observing free keyframes, each with its co-observation pairs
-    struct Quad { int64_t key; int o1, o2; };
-    std::vector<Quad> q;
-    for (int s = 0; s < n_opt; ++s)
-        for (int a1 = lptr[s]; a1 < lptr[s + 1]; ++a1) {
-            const int i = okf[a1];
-            if (flags[i] & 2) continue;
-            for (int a2 = lptr[s]; a2 < lptr[s + 1]; ++a2) {
-                const int j = okf[a2];
-                if ((flags[j] & 2) || j > i) continue;
-                q.push_back({(int64_t)i * nk + j, a1, a2});
-            }
-        }
-    std::sort(q.begin(), q.end(), [](const Quad& x, const Quad& y) {
-        if (x.key != y.key) return x.key < y.key;
-        if (x.o1 != y.o1) return x.o1 < y.o1;
-        return x.o2 < y.o2;
-    });
-    std::vector<int2> bij, prs;
-    std::vector<int> bptr{0};
-    {
-        // diagonal blocks first (block b = keyframe b), then off-diagonal blocks in key order
-        std::vector<std::vector<int2>> diag(nk);
-        std::vector<int64_t> keys;
-        std::vector<std::vector<int2>> off;
-        for (const Quad& x : q) {
-            const int i = (int)(x.key / nk), j = (int)(x.key % nk);
-            if (i == j) {
-                diag[i].push_back(make_int2(x.o1, x.o2));
-            } else {
-                if (keys.empty() || keys.back() != x.key) {
-                    keys.push_back(x.key);
-                    off.emplace_back();
+    // Every (i >= j) pair of free keyframes co-observing a landmark contributes the pair of its two
+    // observations to block (i, j).  Blocks: the nk diagonal blocks in keyframe order, then the
+    // non-empty off-diagonal blocks by (i, j); pairs inside a block by (o1, o2).  The pairs are
+    // generated in (o1, o2) order, so a two-pass counting sort by block key keeps that order.
+    const int64_t nkey = (int64_t)nk * nk;
+    std::vector<int> kcnt((size_t)nkey, 0);
+    auto for_pairs = [&](auto&& emit) {
+        for (int sl = 0; sl < n_opt; ++sl)
+            for (int a1 = lptr[sl]; a1 < lptr[sl + 1]; ++a1) {
+                const int i = okf[a1];
+                if (flags[i] & 2) continue;
+                for (int a2 = lptr[sl]; a2 < lptr[sl + 1]; ++a2) {
+                    const int j = okf[a2];
+                    if ((flags[j] & 2) || j > i) continue;
+                    emit((int64_t)i * nk + j, a1, a2);
                 }
-                off.back().push_back(make_int2(x.o1, x.o2));
             }
-        }
-        for (int r = 0; r < nk; ++r) {
-            bij.push_back(make_int2(r, r));
-            prs.insert(prs.end(), diag[r].begin(), diag[r].end());
-            bptr.push_back((int)prs.size());
-        }
-        for (size_t b = 0; b < keys.size(); ++b) {
-            bij.push_back(make_int2((int)(keys[b] / nk), (int)(keys[b] % nk)));
-            prs.insert(prs.end(), off[b].begin(), off[b].end());
-            bptr.push_back((int)prs.size());
-        }
+    };
+    for_pairs([&](int64_t key, int, int) { ++kcnt[key]; });
+    std::vector<int2> bij;
+    std::vector<int> bptr{0};
+    std::vector<int> kpos((size_t)nkey, -1);  // output offset of each block key
+    int64_t total = 0;
+    for (int r = 0; r < nk; ++r) {
+        const int64_t key = (int64_t)r * nk + r;
+        bij.push_back(make_int2(r, r));
+        kpos[key] = (int)total;
+        total += kcnt[key];
+        bptr.push_back((int)total);
     }
+    for (int64_t key = 0; key < nkey; ++key) {
+        const int i = (int)(key / nk), j = (int)(key % nk);
+        if (i == j || kcnt[key] == 0) continue;
+        bij.push_back(make_int2(i, j));
+        kpos[key] = (int)total;
+        total += kcnt[key];
+        bptr.push_back((int)total);
+    }
+    std::vector<int2> prs((size_t)total);
+    for_pairs([&](int64_t key, int a1, int a2) { prs[kpos[key]++] = make_int2(a1, a2); });
     p->n_blocks = (int)bij.size();
     p->n_pairs = (int64_t)prs.size();
+    lap("blocks");
 
     // ---- symbolic tile factorisation per component: which 16 x 16 tiles of L are nonzero (the
     // pattern of S's blocks plus Cholesky fill), and per step the panel / trailing-update / back-
@@ -1168,6 +1178,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
         }
     }
 
+    lap("symbolic");
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
     if ((rc = upload(c, p->pose0, pose0))) return rc;
@@ -1211,6 +1222,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     VX_HIP(c, hipMemset(p->dx.p, 0, (size_t)nk * 6 * sizeof(double)));
     VX_HIP(c, p->state.ensure(sizeof(SBAState)));
     VX_HIP(c, hipMemset(p->state.p, 0, sizeof(SBAState)));
+    lap("upload");
     return VX_OK;
 }
 
