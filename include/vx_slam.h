@@ -214,6 +214,10 @@ int vx_ba_plan_create(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, i
  * local_ba.cpp:42-108 (hash maps, one core) instead of the device build (default: window join,
  * slot assignment and both CSRs as HIP kernels).  Both give the same plan. */
 #define VX_PLAN_HOST_BUILD 1
+/* VX_PLAN_GLOBAL_POSES runs the large-window kernels (poses solved once into global memory, one
+ * thread per landmark) at any window size; by default they run only beyond 448 keyframes, where
+ * the per-workgroup LDS copy of every keyframe's pose no longer fits.  Same results. */
+#define VX_PLAN_GLOBAL_POSES 2
 int vx_ba_plan_create_ex(vx_ctx* ctx, const vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                          const vx_ba_options* opt, int shard_rank, int shard_count, int flags,
                          vx_ba_plan** out);

@@ -235,6 +235,29 @@ def test_ba_variants(ctx, oracle):
     assert st.status == 1
 
 
+@pytest.mark.parametrize("nk,nl,ns,global_poses", [(50, 20000, 1, True),      # C3 on the large-window kernels
+                                                    (440, 22000, 8, False),    # LDS-pose kernels near their limit
+                                                    (480, 24000, 8, False)])   # beyond it: large-window kernels
+def test_ba_large_windows(ctx, oracle, nk, nl, ns, global_poses):
+    """Both LocalBA kernel sets (k_landmark_solve with every keyframe's pose in LDS up to 448
+    keyframes; k_pose_solve_g + k_landmark beyond, or forced by VX_PLAN_GLOBAL_POSES) against the
+    restatement: the N-GPU bench's global windows are N x 50 keyframes."""
+    import vxslam
+
+    m = synth.make_ba_map(0x5EED0100 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
+    mc = m.copy()
+    st_c = oracle.ba_optimize(mc, oracle.ba_options(window=nk))
+    if st_c.gate_margin < 1e-8:
+        pytest.skip(f"gate margin {st_c.gate_margin} too small for a stable comparison")
+    plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk), global_poses=global_poses)
+    plan.run_async()
+    mg = m.copy()
+    st_g = plan.fetch(mg)
+    plan.close()
+    assert st_g.n_window_kf == nk
+    _assert_ba_close(mg, mc, st_g, st_c)
+
+
 def test_ba_plan_is_repeatable(ctx, oracle):
     import vxslam
 

@@ -54,10 +54,15 @@ constexpr int kStride = 32;      // doubles per keyframe block in global memory
 // 64 four-byte LDS banks, so lanes reading different keyframes' slots would all hit one bank
 constexpr int kLdsStride = 33;
 constexpr int kMaxIter = 64;
-constexpr int kMaxKfLds = 256;   // keyframes whose LDS slots fit k_landmark_solve
+// keyframes whose LDS slots fit k_landmark_solve: 448 * 33 * 8 B + kLmBlock * (9 * 8 + 4) B =
+// 157,184 B of gfx950's 160 KB per workgroup
+constexpr int kMaxKfLds = 448;
 constexpr int kMaxSplit = kBaMaxSplit;    // pose-stage workgroups per keyframe
 constexpr int kCombine = 6;      // (keyframe, term) pairs per thread per combine pass
 constexpr int kLmBlock = kBaLmBlock;      // k_landmark_solve: threads = max observations = max landmarks
+static_assert(kLmBlock >= kMaxKfLds, "k_landmark_solve solves one keyframe per thread");
+static_assert((size_t)kMaxKfLds * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int)) <=
+                  160 * 1024, "k_landmark_solve LDS exceeds gfx950's 160 KB per workgroup");
 
 VX_KT_TABLE();
 
@@ -764,9 +769,13 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
         hipLaunchKernelGGL(k_ba_reset, dim3((n + 255) / 256), dim3(256), 0, c->stream, a);
         VX_LAUNCH_CHECK(c, "k_ba_reset");
     }
-    const bool lds_poses = p->n_kf <= kMaxKfLds;
+    // Every k_landmark_solve workgroup re-solves all window poses, so that redundancy grows as
+    // n_kf x workgroups: beyond the measured crossover (scripts/ba_window_sweep.py) the
+    // large-window kernels (poses solved once, one extra launch per iteration) are faster
+    const bool lds_poses = p->n_kf <= kMaxKfLds && !p->global_poses && (int64_t)p->n_kf * p->n_lm_blocks <= 80000 &&
+                           p->n_lm_blocks <= 480;
     const size_t lds = (size_t)p->n_kf * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
-    if (lds_poses && lds > 64 * 1024) {  // up to ~103 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
+    if (lds_poses && lds > 64 * 1024) {  // up to ~154 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
         static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
                                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         VX_HIP(c, attr);
@@ -834,6 +843,7 @@ int vx_ba_plan_create_ex(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_
     p->opt = *opt;
     p->shard_rank = shard_rank;
     p->shard_count = shard_count;
+    p->global_poses = (flags & VX_PLAN_GLOBAL_POSES) != 0;
     const int rc = (flags & VX_PLAN_HOST_BUILD) ? build_plan(c, m, ref, has_ref, p) : build_plan_device(c, m, ref, has_ref, p);
     if (rc) {
         delete p;

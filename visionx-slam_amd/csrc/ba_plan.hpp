@@ -23,6 +23,7 @@ struct vx_ba_plan {
     vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
     vx::DevBuf kf_map_dev, lm_map_dev;  // plans built from a vx_dmap: window row / slot -> map index
     bool from_dmap = false;
+    bool global_poses = false;  // VX_PLAN_GLOBAL_POSES
 };
 
 struct vx_dmap;

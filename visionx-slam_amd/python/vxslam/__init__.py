@@ -390,8 +390,8 @@ class Context:
         return st
 
     def ba_plan(self, m, opts: BAOptions | None = None, ref_kf_id=None, shard_rank=0, shard_count=1,
-                host_build=False):
-        return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count, host_build)
+                host_build=False, global_poses=False):
+        return BAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count, host_build, global_poses)
 
     def graph_enable(self, on=True):
         self._check(lib().vx_graph_enable(self._h, 1 if on else 0))
@@ -547,9 +547,11 @@ class Context:
 class BAPlan:
     """vx_ba_plan: host window selection + device CSR upload, repeatable device runs."""
 
-    def __init__(self, ctx: Context, m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1, host_build=False):
+    def __init__(self, ctx: Context, m, opts=None, ref_kf_id=None, shard_rank=0, shard_count=1, host_build=False,
+                 global_poses=False):
         """host_build: the host reference build of the plan (VX_PLAN_HOST_BUILD) instead of the
-        device build."""
+        device build; global_poses: the large-window kernels at any window size
+        (VX_PLAN_GLOBAL_POSES)."""
         self.ctx = ctx
         self.m = m
         self.opts = opts or default_ba_options(window=m.get("window", 5))
@@ -558,7 +560,8 @@ class BAPlan:
         v = map_view(m)
         ctx._check(lib().vx_ba_plan_create_ex(ctx.handle, C.byref(v), C.c_uint64(0 if ref is None else int(ref)),
                                               0 if ref is None else 1, C.byref(self.opts), shard_rank,
-                                              shard_count, 1 if host_build else 0, C.byref(self._h)))
+                                              shard_count, (1 if host_build else 0) | (2 if global_poses else 0),
+                                              C.byref(self._h)))
 
     def info(self):
         out = np.zeros(8, np.int64)
