@@ -36,6 +36,9 @@ namespace vx {
 namespace {
 
 constexpr int kBlock = 256;
+// FAST score histograms: one replica per XCD slot (blockIdx mod 8) so that k_fast's atomics from
+// different XCDs never meet on one address; k_select sums the replicas
+constexpr int kHistRep = 8;
 
 VX_KT_TABLE();
 
@@ -380,14 +383,27 @@ __device__ __forceinline__ int block_scan_excl(int v, int* sh, int& total) {
 // Block = 64 x 16 output tile (4 px halo staged in LDS).  Output is written per cell = (row,
 // tile column) with a fixed capacity of 32 (strict NMS keeps at most every other pixel of a
 // 64 px row segment), so cell order == raster order and the per-row compaction is one ballot.
+//
+// LDS is read a dword (4 pixels) at a time wherever a lane works on a pixel quad: the FAST ring
+// test, the blur's row pass (3 dwords per 4 outputs) and its column pass (float4 rows), instead of
+// one ds_read_u8 per tap — the byte-read version was LDS-issue bound (SQ_WAIT_INST_LDS, 234 LDS
+// instructions per wave).  cornerScore<16> runs only for the compacted corner list (3-7 % of the
+// pixels), not under a divergent branch that nearly every wave takes.
 constexpr int kTX = 64, kTY = 16, kCellCap = 32;
-constexpr int kTW = kTX + 8, kTH = kTY + 8;   // staged tile
-constexpr int kSW = kTX + 2, kSH = kTY + 2;   // score tile
+constexpr int kTW = kTX + 12, kTH = kTY + 8;  // staged tile: x0-4 .. x0+71 (quad reads up to x0+71)
+constexpr int kSW = kTX + 4, kSH = kTY + 2;   // score tile (66 used + 2 pad: dword rows)
+constexpr int kSQ = 17;                       // score quads per row (68 columns)
 
 // The GaussianBlur of the same 64 x 16 output tile (k_blur's arithmetic, reflect-101 halo of 3)
 // is computed here too: the tile is already being read, and the separate blur launch was a
 // dependent step of its own on the extraction chain.
-constexpr int kBW = kTX + 6, kBH = kTY + 6;   // blur input tile (3 px reflect-101 halo)
+constexpr int kBW = kTX + 8, kBH = kTY + 6;   // blur input tile x0-4 .. x0+67 (reflect-101), 3 row halo
+static_assert(kTW % 4 == 0 && kSW % 4 == 0 && kBW % 4 == 0, "quad rows must be dword aligned");
+
+// byte b (0..11) of a 12-byte window held as three dwords
+__device__ __forceinline__ int win_byte(const uint32_t (&w)[3], int b) {
+    return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u);
+}
 
 __device__ __forceinline__ int refl101(int p, int n) {
     if (n == 1) return 0;
@@ -403,12 +419,14 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
                                                  int* __restrict__ cell_count,
                                                  int* __restrict__ hist,
                                                  uint8_t* __restrict__ blur) {
-    __shared__ uint8_t tile[kTH * kTW];
-    __shared__ uint8_t sc[kSH * kSW];
+    __shared__ __attribute__((aligned(16))) uint8_t tile[kTH * kTW];
+    __shared__ __attribute__((aligned(16))) uint8_t sc[kSH * kSW];
     __shared__ int s_list[kTY * kCellCap];   // (cell slot << 16) | (row << 8) | local x
-    __shared__ int s_n;
-    __shared__ uint8_t bin_[kBH * kBW];
-    __shared__ float brow[kBH * kTX];
+    __shared__ int s_n, s_nc;
+    __shared__ uint16_t s_corner[kSH * kSW];  // FAST corners of the score tile: (row << 8) | col
+    __shared__ int s_hist[256];               // this tile's NMS corners by FAST score
+    __shared__ __attribute__((aligned(16))) uint8_t bin_[kBH * kBW];
+    __shared__ __attribute__((aligned(16))) float brow[kBH * kTX];
     const int b = blockIdx.x;
     int l = 0;
     while (l + 1 < a.L && b >= a.tile_base[l + 1]) ++l;
@@ -420,7 +438,9 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     const int x0 = tx * kTX, y0 = ty * kTY;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     VX_KT(4);
-    if (tid == 0) s_n = 0;
+    if (tid == 0) s_n = s_nc = 0;
+    s_hist[tid] = 0;
+    static_assert(kBlock == 256, "one histogram bin per thread");
     stage_lds<kBlock, (kTH * kTW + kBlock - 1) / kBlock>(tile, kTH * kTW, [&](int i) {
         const int r = i / kTW, c = i - r * kTW;
         const int gy = min(max(y0 - 4 + r, 0), H - 1);
@@ -429,49 +449,109 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     });
     stage_lds<kBlock, (kBH * kBW + kBlock - 1) / kBlock>(bin_, kBH * kBW, [&](int i) {
         const int r = i / kBW, c = i - r * kBW;
-        return img[(long long)refl101(y0 - 3 + r, H) * W + refl101(x0 - 3 + c, W)];
+        return img[(long long)refl101(y0 - 3 + r, H) * W + refl101(x0 - 4 + c, W)];
     });
     __syncthreads();
     VX_KT(5);
     const int thr = a.fast_threshold;
-    for (int i = tid; i < kSH * kSW; i += kBlock) {
-        const int r = i / kSW, c = i - r * kSW;
-        const int y = y0 - 1 + r, x = x0 - 1 + c;
-        int s = 0;
-        if (y >= 3 && y < H - 3 && x >= 3 && x < W - 3) s = fast_score(tile + (r + 3) * kTW + c + 3, kTW, thr);
-        sc[i] = (uint8_t)s;
+    // FAST ring test per pixel quad: score-tile pixel (r, c) is (x0 - 1 + c, y0 - 1 + r), tile
+    // (r + 3, c + 3); its 7 ring rows are tile rows r .. r + 6 and the quad's ring columns lie in
+    // the 12 bytes from tile column 4g.  Corners go to a list; the score tile is zeroed.
+    for (int i = tid; i < kSH * kSQ; i += kBlock) {
+        const int r = i / kSQ, g = i - r * kSQ;
+        const uint32_t* rp = reinterpret_cast<const uint32_t*>(tile + r * kTW) + g;
+        uint32_t w[7][3];
+#pragma unroll
+        for (int d = 0; d < 7; ++d)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) w[d][k] = rp[d * (kTW / 4) + k];
+        const int y = y0 - 1 + r;
+        unsigned cm = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int x = x0 - 1 + 4 * g + j;
+            const int v = win_byte(w[3], j + 3);
+            uint32_t bright = 0, dark = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int pk = win_byte(w[3 + ring_dy(k)], j + 3 + ring_dx(k));
+                bright |= (uint32_t)(pk > v + thr) << k;
+                dark |= (uint32_t)(pk < v - thr) << k;
+            }
+            const bool ok = 4 * g + j < kSW - 2 && y >= 3 && y < H - 3 && x >= 3 && x < W - 3;
+            cm |= (unsigned)(ok && (has_run9(bright) || has_run9(dark))) << j;
+        }
+        *reinterpret_cast<uint32_t*>(sc + r * kSW + 4 * g) = 0u;
+        if (cm) {
+            int k = atomicAdd(&s_nc, __popc(cm));
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (cm & (1u << j)) s_corner[k++] = (uint16_t)((r << 8) | (4 * g + j));
+        }
     }
-    // blur row pass 8U -> 32F (float separable GaussianBlur)
+    // blur row pass 8U -> 32F (float separable GaussianBlur): output columns 4q .. 4q+3
+    // of blur row r take bin_ bytes 4q + j + 1 .. 4q + j + 7 (bin_ column 0 is x0 - 4)
     const float k0 = a.gk[0], k1 = a.gk[1], k2 = a.gk[2], k3 = a.gk[3], k4 = a.gk[4], k5 = a.gk[5], k6 = a.gk[6];
-    for (int i = tid; i < kBH * kTX; i += kBlock) {
-        const int r = i / kTX, c = i - r * kTX;
-        const uint8_t* p = bin_ + r * kBW + c;
-        float s = k0 * (float)p[0];
-        s += k1 * (float)p[1];
-        s += k2 * (float)p[2];
-        s += k3 * (float)p[3];
-        s += k4 * (float)p[4];
-        s += k5 * (float)p[5];
-        s += k6 * (float)p[6];
-        brow[i] = s;
+    for (int i = tid; i < kBH * (kTX / 4); i += kBlock) {
+        const int r = i / (kTX / 4), q = i - r * (kTX / 4);
+        const uint32_t* bp = reinterpret_cast<const uint32_t*>(bin_ + r * kBW) + q;
+        const uint32_t w[3] = {bp[0], bp[1], bp[2]};
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float s = k0 * (float)win_byte(w, j + 1);
+            s += k1 * (float)win_byte(w, j + 2);
+            s += k2 * (float)win_byte(w, j + 3);
+            s += k3 * (float)win_byte(w, j + 4);
+            s += k4 * (float)win_byte(w, j + 5);
+            s += k5 * (float)win_byte(w, j + 6);
+            s += k6 * (float)win_byte(w, j + 7);
+            o[j] = s;
+        }
+        *reinterpret_cast<float4*>(brow + r * kTX + 4 * q) = make_float4(o[0], o[1], o[2], o[3]);
     }
     __syncthreads();
     VX_KT(6);
-    {  // blur column pass 32F -> 8U (symmetric form, round half to even)
-        uint8_t* out = blur + a.off[l];
-        for (int i = tid; i < kTY * kTX; i += kBlock) {
-            const int r = i / kTX, c = i - r * kTX;
-            const int x = x0 + c, y = y0 + r;
-            if (x >= W || y >= H) continue;
-            const float* q = brow + (r + 3) * kTX + c;
-            float s = k3 * q[0] + 0.0f;
-            s += k4 * (q[kTX] + q[-kTX]);
-            s += k5 * (q[2 * kTX] + q[-2 * kTX]);
-            s += k6 * (q[3 * kTX] + q[-3 * kTX]);
-            const int v = __float2int_rn(s);
-            out[(long long)y * W + x] = (uint8_t)min(255, max(0, v));
+    // cornerScore<16> for the listed corners only
+    {
+        const int nc = s_nc;
+        for (int i = tid; i < nc; i += kBlock) {
+            const int v = s_corner[i], r = v >> 8, c = v & 255;
+            sc[r * kSW + c] = (uint8_t)fast_score(tile + (r + 3) * kTW + c + 3, kTW, thr);
         }
     }
+    {  // blur column pass 32F -> 8U (symmetric form, round half to even), one output quad per thread
+        uint8_t* out = blur + a.off[l];
+        const float4* b4 = reinterpret_cast<const float4*>(brow);
+        for (int i = tid; i < kTY * (kTX / 4); i += kBlock) {
+            const int r = i / (kTX / 4), q = i - r * (kTX / 4);
+            const int y = y0 + r, xq = x0 + 4 * q;
+            if (y >= H || xq >= W) continue;
+            float4 m[7];
+#pragma unroll
+            for (int d = 0; d < 7; ++d) m[d] = b4[(r + d) * (kTX / 4) + q];
+            int v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                auto at = [&](int d) { return j == 0 ? m[d].x : j == 1 ? m[d].y : j == 2 ? m[d].z : m[d].w; };
+                float s = k3 * at(3) + 0.0f;
+                s += k4 * (at(4) + at(2));
+                s += k5 * (at(5) + at(1));
+                s += k6 * (at(6) + at(0));
+                v[j] = min(255, max(0, __float2int_rn(s)));
+            }
+            uint8_t* dst = out + (long long)y * W + xq;
+            if (xq + 3 < W && ((reinterpret_cast<uintptr_t>(dst) & 3u) == 0)) {
+                *reinterpret_cast<uint32_t*>(dst) = (uint32_t)v[0] | ((uint32_t)v[1] << 8) | ((uint32_t)v[2] << 16) |
+                                                    ((uint32_t)v[3] << 24);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    if (xq + j < W) dst[j] = (uint8_t)v[j];
+            }
+        }
+    }
+    __syncthreads();
     const int e = a.edge;
     for (int r = wv; r < kTY; r += kBlock / 64) {
         const int y = y0 + r, x = x0 + lane;
@@ -524,8 +604,13 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
             c.harris = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
             c.pad = 0;
             cand[(long long)(a.cell_base[l] + (y0 + r) * ntx + tx) * kCellCap + rank] = c;
-            atomicAdd(&hist[l * 256 + s], 1);
+            atomicAdd(&s_hist[s], 1);
         }
+    }
+    __syncthreads();
+    {
+        const int hc = s_hist[tid];
+        if (hc) atomicAdd(&hist[(l * kHistRep + (int)(blockIdx.x % kHistRep)) * 256 + tid], hc);
     }
     VX_KT(8);
 }
@@ -579,7 +664,11 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     const int q = a.quota[l];
     const int k1 = 2 * q;
     // ---- level histogram of FAST scores (border-passing NMS corners) -> n and thr1
-    const int hv = tid < 256 ? hist[l * 256 + 255 - tid] : 0;
+    int hv = 0;
+    if (tid < 256) {
+#pragma unroll
+        for (int r = 0; r < kHistRep; ++r) hv += hist[(l * kHistRep + r) * 256 + 255 - tid];
+    }
     int n;
     {
         int ex = block_scan_excl<kSelBlock>(hv, sw, n);
@@ -1124,7 +1213,7 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
     VX_HIP(c, c->cand.ensure(g.cells_total * kCellCap * sizeof(CandRec)));
     VX_HIP(c, c->stage.ensure(g.stage_total * sizeof(CandRec)));
     VX_HIP(c, c->band_count.ensure(g.cells_total * sizeof(int)));
-    VX_HIP(c, c->hist.ensure(g.L * 256 * sizeof(int)));
+    VX_HIP(c, c->hist.ensure(g.L * kHistRep * 256 * sizeof(int)));
     VX_HIP(c, c->level_count.ensure(kMaxLevels * sizeof(int)));
     for (auto& s : c->slots) {
         s.valid = false;
@@ -1144,7 +1233,7 @@ static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t st
     const LevelArgs a = level_args(g);
     uint8_t* pyr = c->pyr.as<uint8_t>();
     Slot& s = c->slots[slot];
-    const int hist_n = g.L * 256;
+    const int hist_n = g.L * kHistRep * 256;
     if (g.pyr_fused) {
         const int raw = (int)((pyr_raw_bytes(g, channels) + 15) & ~int64_t(15));
         VX_HIP(c, launch(c, kStPyramid, g.pr_block == 512 ? k_pyramid<512> : k_pyramid<1024>,
