@@ -23,6 +23,8 @@ namespace {
 constexpr int kQB = 256;      // queries per block (one per thread)
 constexpr int kTC = 64;       // train rows per chunk
 constexpr int kMergeBlock = 1024;
+constexpr int kMergeBatch = 32;   // chunk partials in flight per thread in k_knn_merge
+constexpr int kMergeQB = 64;      // queries per k_knn_merge workgroup (one wave: more CUs, same loads)
 constexpr unsigned kNone = 0xffffffffu;
 
 __global__ __launch_bounds__(kQB) void k_knn_partial(const uint8_t* __restrict__ q,
@@ -46,6 +48,7 @@ __global__ __launch_bounds__(kQB) void k_knn_partial(const uint8_t* __restrict__
     const uint4 a0 = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[0];
     const uint4 a1 = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[1];
     unsigned k1 = kNone, k2 = kNone;
+#pragma unroll 8
     for (int j = 0; j < tn; ++j) {
         const uint4 b0 = st[2 * j], b1 = st[2 * j + 1];
         unsigned d = __builtin_popcount(a0.x ^ b0.x);
@@ -64,42 +67,58 @@ __global__ __launch_bounds__(kQB) void k_knn_partial(const uint8_t* __restrict__
     (void)n_chunks_cap;
 }
 
+// Exclusive block scan: wave prefix by __shfl_up, then the NT/64 wave totals from LDS (two
+// barriers per call instead of a Hillis-Steele pass per doubling step).
 template <int NT>
 __device__ __forceinline__ int scan_excl(int v, int* sh, int& total) {
-    const int t = threadIdx.x;
-    sh[t] = v;
-    __syncthreads();
-    for (int o = 1; o < NT; o <<= 1) {
-        const int x = t >= o ? sh[t - o] : 0;
-        __syncthreads();
-        sh[t] += x;
-        __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    total = sh[NT - 1];
-    const int incl = sh[t];
+    if (lane == 63) sh[w] = x;
     __syncthreads();
-    return incl - v;
+    int pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) {
+        const int t = sh[i];
+        tot += t;
+        pre += i < w ? t : 0;
+    }
+    total = tot;
+    __syncthreads();
+    return pre + x - v;
 }
 
 // Per-query merge of the chunk partials + ratio test, one thread per query over many blocks.
 // best[qi] = winning key when the query passes the ratio test, kNone otherwise.
-__global__ __launch_bounds__(256) void k_knn_merge(const uint2* __restrict__ partial,
+__global__ __launch_bounds__(kMergeQB) void k_knn_merge(const uint2* __restrict__ partial,
                                                    const int* __restrict__ nq_p, int nq_host,
                                                    const int* __restrict__ nt_p, int nt_host,
                                                    int q_stride, float ratio,
                                                    unsigned* __restrict__ best) {
     const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
     const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
-    const int qi = blockIdx.x * 256 + threadIdx.x;
+    const int qi = blockIdx.x * kMergeQB + threadIdx.x;
     if (qi >= nq) return;
     const int nchunks = (nt + kTC - 1) / kTC;
     unsigned k1 = kNone, k2 = kNone;
-    for (int c = 0; c < nchunks; ++c) {
-        const uint2 p = partial[(long long)c * q_stride + qi];
-        k2 = max(min(k1, p.x), min(k2, max(k1, p.x)));
-        k1 = min(k1, p.x);
-        k2 = max(min(k1, p.y), min(k2, max(k1, p.y)));
-        k1 = min(k1, p.y);
+    // the chunk partials of a batch are loaded together (one exposed L2 latency per kMergeBatch
+    // chunks, not per chunk); the merge order is the chunk order either way
+    for (int c0 = 0; c0 < nchunks; c0 += kMergeBatch) {
+        uint2 p[kMergeBatch];
+#pragma unroll
+        for (int j = 0; j < kMergeBatch; ++j)
+            p[j] = c0 + j < nchunks ? partial[(long long)(c0 + j) * q_stride + qi] : make_uint2(kNone, kNone);
+#pragma unroll
+        for (int j = 0; j < kMergeBatch; ++j) {
+            k2 = max(min(k1, p[j].x), min(k2, max(k1, p[j].x)));
+            k1 = min(k1, p[j].x);
+            k2 = max(min(k1, p[j].y), min(k2, max(k1, p[j].y)));
+            k1 = min(k1, p[j].y);
+        }
     }
     bool keep = false;
     if (k2 != kNone) {  // knn.size() == 2 (orb_matcher.cpp:28)
@@ -114,7 +133,7 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __r
                                                              const int* __restrict__ nq_p, int nq_host,
                                                              vx_match* __restrict__ out,
                                                              int* __restrict__ out_count) {
-    __shared__ int sh[kMergeBlock];
+    __shared__ int sh[kMergeBlock / 64];
     const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
     int written = 0;
     for (int base = 0; base < nq; base += kMergeBlock) {
@@ -148,7 +167,7 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
     {
         ProfScope ps(c, kStMatchMerge);
         unsigned* best = reinterpret_cast<unsigned*>(c->partial.as<uint2>() + (size_t)n_chunks * q_stride);
-        hipLaunchKernelGGL(k_knn_merge, dim3((q_cap + 255) / 256), dim3(256), 0, c->stream, c->partial.as<uint2>(),
+        hipLaunchKernelGGL(k_knn_merge, dim3((q_cap + kMergeQB - 1) / kMergeQB), dim3(kMergeQB), 0, c->stream, c->partial.as<uint2>(),
                            dnq, nq_host, dnt, nt_host, q_stride, ratio, best);
         VX_LAUNCH_CHECK(c, "k_knn_merge");
         hipLaunchKernelGGL(k_knn_compact, dim3(1), dim3(kMergeBlock), 0, c->stream, best, dnq, nq_host,
