@@ -194,6 +194,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--ba-cus", type=float, default=0.0,
                     help="fraction of the CUs reserved for the LocalBA context (disjoint CU masks; 0: shared)")
+    ap.add_argument("--grid-share", type=float, default=None,
+                    help="share of the CUs the extraction context's one-round grids are sized for "
+                         "(vx_set_grid_share; default 1/3 with more than one stream, 1 otherwise)")
     ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
                     help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
     args = ap.parse_args()
@@ -217,6 +220,9 @@ def main():
     mctx = ectx if args.streams < 3 else vxslam.Context(dist.local_rank, cu_mask=fe_mask)
     bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank, cu_mask=ba_mask)
     ctxs = list({id(c): c for c in (ectx, mctx, bctx)}.values())
+    # extraction runs beside the previous frame's LocalBA: its pyramid grid leaves CUs free for it
+    grid_share = args.grid_share if args.grid_share else (1.0 / 3.0 if args.streams > 1 else 1.0)
+    ectx.set_grid_share(grid_share)
     cfg = CONFIGS[args.config]
     h, w, nf, nk, nl = cfg
     N = dist.world
@@ -338,9 +344,12 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if roofline and os.path.exists(pmc):
         try:
-            tr = json.load(open(pmc)).get(dominant)
-            if tr:
-                roofline["traffic"] = int(tr)
+            d = json.load(open(pmc))
+            if d.get("config") == args.config and d.get("n_gpus") == N:  # counters of this very workload
+                tr = d["bytes_per_launch"].get(dominant)
+                if tr:
+                    roofline["traffic"] = int(tr)
+                    roofline["traffic_source"] = "profiles/pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE, WRITE_SIZE)"
         except Exception:
             pass
 

@@ -85,6 +85,25 @@ def test_orb_edge_inputs(ctx, oracle):
     _assert_orb_equal(k, d, kc, dc)
 
 
+@pytest.mark.parametrize("share", [1.0 / 3.0, 0.05])
+def test_orb_grid_share(oracle, share):
+    """vx_set_grid_share changes only the pyramid's grid: results stay bit-exact."""
+    import vxslam
+
+    c = vxslam.Context(0)
+    try:
+        c.set_grid_share(share)
+        for seed, h, w, n in [(31, 480, 640, 2000), (32, 960, 1280, 4000)]:
+            f = synth.make_frames(seed, 1, h, w)[0]
+            k, d = c.orb_extract(f, vxslam.default_orb_params(n_features=n))
+            kc, dc = oracle.orb_extract(f, n, order=oracle.ORDER_RASTER)
+            assert np.array_equal(k, kc) and np.array_equal(d, dc)
+        with pytest.raises(Exception):
+            c.set_grid_share(0.0)
+    finally:
+        c.close()
+
+
 def test_orb_repeatable_and_params_switch(ctx):
     import vxslam
 

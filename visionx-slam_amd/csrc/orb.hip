@@ -123,7 +123,11 @@ __global__ void k_gray(const uint8_t* __restrict__ img, int W, int ch, long long
 // parallelism against redundant halo work.  A 1024-thread workgroup occupies a whole CU, so the
 // tile is the smallest edge (>= 32, step 4) whose grid fits the device's CUs in one round
 // (640x480 on 256 CUs: 36 -> 18 x 14 workgroups; measured 13.9 us at 40 vs 17.3 us at 64 and
-// 22.9 us at 32, which needs two rounds).  $VX_PYR_TILE / $VX_PYR_BLOCK override for sweeps.
+// 22.9 us at 32, which needs two rounds).  A context sharing the device with concurrent ones
+// (vx_set_grid_share) sizes the grid for its share of the CUs instead: in the 3-context pipeline
+// (share 1/3: tile 64, 80 workgroups) the LocalBA kernels find free CUs and the pipelined frame
+// is ~5 % faster than with the one-round grid (scripts/sweep_pyr_pipe.sh).
+// $VX_PYR_TILE / $VX_PYR_BLOCK override for sweeps.
 constexpr int kPyBlockDef = 1024;
 constexpr int kPyLdsMax = 64 * 1024;
 
@@ -1182,7 +1186,7 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
     }
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
-    pyramid_rects(g, all, std::max(1, n_cu));
+    pyramid_rects(g, all, std::max(1, (int)(n_cu * c->grid_share)));
     g.tab_entries = (int64_t)all.size();
     // FAST tiles / cells and selection staging
     int tiles = 0;

@@ -221,6 +221,21 @@ int vx_graph_enable(vx_ctx* c, int enable) {
     return VX_OK;
 }
 
+int vx_set_grid_share(vx_ctx* c, float share) {
+    if (!c) return VX_ERR_INVALID;
+    if (!(share > 0.0f && share <= 1.0f)) return vx::set_error(c, VX_ERR_INVALID, "grid share must be in (0, 1]");
+    if (share == c->grid_share) return VX_OK;
+    VX_HIP(c, hipSetDevice(c->device));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    // captured launch sequences bake the old grids in: drop them with the cached geometry
+    for (auto& e : c->graphs.entries)
+        if (e.exec) (void)hipGraphExecDestroy(e.exec);
+    c->graphs.entries.clear();
+    c->grid_share = share;
+    c->geo_valid = false;
+    return VX_OK;
+}
+
 int vx_graph_counts(const vx_ctx* c, int* captured, int* launched) {
     if (!c) return VX_ERR_INVALID;
     if (captured) *captured = c->graphs.captured;

@@ -165,6 +165,7 @@ struct vx_event {
 struct vx_ctx {
     int device = 0;
     int n_cus = 0;  // compute units of the device (lazily queried)
+    float grid_share = 1.0f;  // vx_set_grid_share: CUs the single-round grids (k_pyramid) size for
     hipStream_t stream = nullptr;
     hipEvent_t order_event = nullptr;  // vx_stream_wait_ctx: recorded on this stream
     std::string err;

@@ -109,6 +109,7 @@ def lib():
         L.vx_stream.restype = C.c_void_p
         L.vx_stream.argtypes = [C.c_void_p]
         L.vx_synchronize.argtypes = [C.c_void_p]
+        L.vx_set_grid_share.argtypes = [C.c_void_p, C.c_float]
         L.vx_stream_wait_ctx.argtypes = [C.c_void_p, C.c_void_p]
         L.vx_event_create.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
         L.vx_event_record.argtypes = [C.c_void_p, C.c_void_p]
@@ -395,6 +396,10 @@ class Context:
 
     def graph_enable(self, on=True):
         self._check(lib().vx_graph_enable(self._h, 1 if on else 0))
+
+    def set_grid_share(self, share: float):
+        """vx_set_grid_share: size one-round grids for this share of the CUs (concurrent contexts)."""
+        self._check(lib().vx_set_grid_share(self._h, C.c_float(share)))
 
     def graph_counts(self):
         """(graphs captured, graph launches) of this context's hipGraph replay."""
