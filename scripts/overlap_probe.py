@@ -46,6 +46,24 @@ def piped(i):
     B(i)
 
 
+def em_only(i):  # Match(t) after Extract(t); LocalBA unordered
+    e.wait_event(ev_m[(i + 1) % 3])
+    E(i)
+    e.record(ev_e)
+    m.wait_event(ev_e)
+    M(i)
+    m.record(ev_m[i % 3])
+    B(i)
+
+
+def mb_only(i):  # LocalBA(t) after Match(t); Match unordered after Extract
+    E(i)
+    M(i)
+    m.record(ev_m[i % 3])
+    b.wait_event(ev_m[i % 3])
+    B(i)
+
+
 def run(name, fns, K=200):
     for i in range(10):
         for f in fns:
@@ -67,4 +85,6 @@ run("localBA alone", [B])
 run("extract | localBA (no deps)", [E, B])
 run("extract | match (no deps)", [E, M])
 run("extract | match | BA (no deps)", [E, M, B])
+run("events E->M only", [em_only])
+run("events M->B only", [mb_only])
 run("pipeline (events)", [piped])
