@@ -12,6 +12,7 @@ from vxslam import synth  # noqa: E402
 
 h, w, nf, nk, nl = 480, 640, 2000, 50, 20000
 e, m, b = vxslam.Context(0), vxslam.Context(0), vxslam.Context(0)
+e.set_grid_share(float(os.environ.get("VX_GRID_SHARE", 1.0 / 3.0)))  # as bench.py
 frames = torch.from_numpy(synth.make_frames(7, 8, h, w)).cuda()
 params = vxslam.default_orb_params(n_features=nf)
 plan = b.ba_plan(synth.make_ba_map(0x5EED0003, nk, nl), vxslam.default_ba_options(window=nk))

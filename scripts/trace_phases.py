@@ -12,7 +12,7 @@ import sys
 import numpy as np
 
 path, kernel, per = sys.argv[1], sys.argv[2], int(sys.argv[3])
-steps = int(sys.argv[4]) if len(sys.argv) > 4 else 50
+steps = int(sys.argv[4]) if len(sys.argv) > 4 else 300
 warmup = int(sys.argv[5]) if len(sys.argv) > 5 else 5
 rows = [r for r in csv.DictReader(open(path)) if kernel + "(" in r["Kernel_Name"] or kernel + "<" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))

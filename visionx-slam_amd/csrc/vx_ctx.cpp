@@ -25,14 +25,23 @@ int hip_fail(vx_ctx* c, hipError_t e, const char* what) {
     return set_error(c, VX_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
+// Cross-context ordering events order work of one device: a device-scope release / acquire is
+// all they need ($VX_EVENT_SYSTEM_FENCE=1 restores the default system-scope fences).
+static const unsigned kSyncEventFlags = [] {
+    const char* e = std::getenv("VX_EVENT_SYSTEM_FENCE");
+    return (e && std::atoi(e) != 0) ? 0u : (unsigned)hipEventDisableSystemFence;
+}();
+
 static hipEvent_t get_event(vx_ctx* c) {
     if (!c->event_pool.empty()) {
         hipEvent_t e = c->event_pool.back();
         c->event_pool.pop_back();
         return e;
     }
+    // timing only: no system-scope fences (nothing here needs host visibility of device memory;
+    // the fences made every bracketed dispatch ~2 us longer than rocprofv3 sees it)
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
     return e;
 }
 
@@ -258,7 +267,8 @@ int vx_stream_wait_ctx(vx_ctx* c, vx_ctx* after) {
     if (c->device != after->device)
         return vx::set_error(c, VX_ERR_INVALID, "vx_stream_wait_ctx: contexts on devices %d and %d", c->device,
                              after->device);
-    if (!after->order_event) VX_HIP(c, hipEventCreateWithFlags(&after->order_event, hipEventDisableTiming));
+    if (!after->order_event)
+        VX_HIP(c, hipEventCreateWithFlags(&after->order_event, hipEventDisableTiming | vx::kSyncEventFlags));
     VX_HIP(c, hipEventRecord(after->order_event, after->stream));
     VX_HIP(c, hipStreamWaitEvent(c->stream, after->order_event, 0));
     return VX_OK;
@@ -270,7 +280,7 @@ int vx_event_create(vx_ctx* c, vx_event** out) {
     VX_HIP(c, hipSetDevice(c->device));
     auto* e = new vx_event();
     e->device = c->device;
-    const hipError_t r = hipEventCreateWithFlags(&e->ev, hipEventDisableTiming);
+    const hipError_t r = hipEventCreateWithFlags(&e->ev, hipEventDisableTiming | vx::kSyncEventFlags);
     if (r != hipSuccess) {
         delete e;
         return vx::hip_fail(c, r, "hipEventCreateWithFlags");
