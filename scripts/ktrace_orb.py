@@ -25,7 +25,9 @@ def main():
     tr = read("vx_ktrace_read_orb")
     report(tr, [0, 1, 2, 3], "k_pyramid (1 tables + BGR staged, 2 gray level 0, 3 levels 1..L-1)")
     report(tr, [4, 5, 6, 7, 8], "k_fast (5 tiles staged, 6 FAST scores + blur row pass, 7 blur column pass + NMS + cells, 8 Harris + stores)")
-    report(tr, [12, 13, 14, 15], "k_select (13 gather, 14 radix select, 15 compaction)")
+    report(tr, [12, 9, 10, 11, 13, 14, 15],
+           "k_select (9 histogram -> thr1, 10 first pass counts + records, 11 its scan, 13 gather done, "
+           "14 radix select, 15 compaction)")
     ctx.close()
 
 

@@ -667,6 +667,15 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     CandRec* fin = stage + a.stage_base[l] + a.level_cap[l];      // retainBest(q) result
     const int q = a.quota[l];
     const int k1 = 2 * q;
+    // the first gather pass's cell counts do not depend on thr1: their loads are issued before the
+    // histogram scan so that their latency passes during it
+    const int cpt = min(kCellsPer, (ncell + kSelBlock - 1) / kSelBlock);
+    int cnt0[kCellsPer];
+#pragma unroll
+    for (int j = 0; j < kCellsPer; ++j) {
+        const int c = tid * cpt + j;
+        cnt0[j] = (k1 > 0 && j < cpt && c < ncell) ? cell_count[cbase + c] : 0;
+    }
     // ---- level histogram of FAST scores (border-passing NMS corners) -> n and thr1
     int hv = 0;
     if (tid < 256) {
@@ -684,20 +693,20 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
         find_digit(hv, k1, sw, s_out);
         thr1 = s_out[0];
     }
+    VX_KT(9);
     // ---- gather kept candidates (score >= thr1) in raster order.  Each thread owns cpt
     // consecutive cells: their counts are loaded in one batch, then up to kRecBatch of their
     // records in one batch (a per-record loop would expose one memory latency per record).
     // Survivors go to LDS (when they fit) and to the global staging list.
     int K1 = 0;
     if (k1 > 0) {
-        const int cpt = min(kCellsPer, (ncell + kSelBlock - 1) / kSelBlock);
         for (int base = 0; base < ncell; base += kSelBlock * cpt) {
             const int c0 = base + tid * cpt;
             int cnts[kCellsPer];
             int tot = 0;
 #pragma unroll
             for (int j = 0; j < kCellsPer; ++j) {
-                cnts[j] = (j < cpt && c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
+                cnts[j] = base == 0 ? cnt0[j] : (j < cpt && c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
             }
 #pragma unroll
             for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
@@ -719,8 +728,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 #pragma unroll
             for (int k = 0; k < kRecBatch; ++k) kc += (k < tot && rr[k].score >= thr1) ? 1 : 0;
             for (int k = kRecBatch; k < tot; ++k) kc += cand[rec_index(k)].score >= thr1 ? 1 : 0;
+            if (base == 0) VX_KT(10);
             int btot;
             int pos = K1 + block_scan_excl<kSelBlock>(kc, sw, btot);
+            if (base == 0) VX_KT(11);
             auto put = [&](const CandRec& r) {
                 if (pos < kSelRecLds) srec[pos] = r;
                 kept[pos] = r;
