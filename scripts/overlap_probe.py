@@ -11,7 +11,9 @@ import vxslam  # noqa: E402
 from vxslam import synth  # noqa: E402
 
 h, w, nf, nk, nl = 480, 640, 2000, 50, 20000
-e, m, b = vxslam.Context(0), vxslam.Context(0), vxslam.Context(0)
+# $VX_PRIO = "E M B" stream priorities (> 0: high) of the three contexts
+pe, pm, pb = (int(x) for x in os.environ.get("VX_PRIO", "0 0 0").split())
+e, m, b = vxslam.Context(0, priority=pe), vxslam.Context(0, priority=pm), vxslam.Context(0, priority=pb)
 e.set_grid_share(float(os.environ.get("VX_GRID_SHARE", 1.0 / 3.0)))  # as bench.py
 frames = torch.from_numpy(synth.make_frames(7, 8, h, w)).cuda()
 params = vxslam.default_orb_params(n_features=nf)
