@@ -867,11 +867,16 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
         const int v = lane - 15;
         const int d = c_umax[v < 0 ? -v : v];
         const uint8_t* row = img + (long long)(yl + v) * W + xl;
+        // all 31 taps of the row issued before the first is used (|u| <= d predicated): one
+        // exposed load latency per row instead of one per tap
+        int px[31];
+#pragma unroll
+        for (int u = -15; u <= 15; ++u) px[u + 15] = (u >= -d && u <= d) ? (int)row[u] : 0;
         int s = 0, su = 0;
-        for (int u = -d; u <= d; ++u) {
-            const int p = row[u];
-            s += p;
-            su += u * p;
+#pragma unroll
+        for (int u = -15; u <= 15; ++u) {
+            s += px[u + 15];
+            su += u * px[u + 15];
         }
         m10 = su;
         m01 = v * s;
