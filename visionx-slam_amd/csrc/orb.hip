@@ -576,39 +576,50 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     }
     __syncthreads();
     VX_KT(7);
-    // Harris 7x7 (HarrisResponses): one wave per candidate, lane < 49 takes one window pixel.
+    // Harris 7x7 (HarrisResponses): four candidates per wave, 16 lanes each; lane s of a group
+    // takes window pixels s, s + 16, s + 32 (and 48) and the integer sums are reduced over the 16
+    // lanes (exact in any order).
     const int n = s_n;
-    const int dy = lane / 7 - 3, dx = lane % 7 - 3;
-    for (int j = wv; j < n; j += kBlock / 64) {
-        const int v = s_list[j];
+    const int grp = lane >> 4, sl = lane & 15;
+    for (int j0 = wv * 4; j0 < n; j0 += (kBlock / 64) * 4) {
+        const int j = j0 + grp;
+        const bool valid = j < n;
+        const int v = valid ? s_list[j] : 0;
         const int xl = v & 255, r = (v >> 8) & 255, rank = v >> 16;
         int ia = 0, ib = 0, ic = 0;
-        if (lane < 49) {
-            const uint8_t* p = tile + (r + 4 + dy) * kTW + xl + 4 + dx;
-            const int Ix = (p[1] - p[-1]) * 2 + (p[-kTW + 1] - p[-kTW - 1]) + (p[kTW + 1] - p[kTW - 1]);
-            const int Iy = (p[kTW] - p[-kTW]) * 2 + (p[kTW - 1] - p[-kTW - 1]) + (p[kTW + 1] - p[-kTW + 1]);
-            ia = Ix * Ix;
-            ib = Iy * Iy;
-            ic = Ix * Iy;
+        if (valid) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int e = sl + 16 * q;
+                if (e < 49) {
+                    const int dy = e / 7 - 3, dx = e % 7 - 3;
+                    const uint8_t* p = tile + (r + 4 + dy) * kTW + xl + 4 + dx;
+                    const int Ix = (p[1] - p[-1]) * 2 + (p[-kTW + 1] - p[-kTW - 1]) + (p[kTW + 1] - p[kTW - 1]);
+                    const int Iy = (p[kTW] - p[-kTW]) * 2 + (p[kTW - 1] - p[-kTW - 1]) + (p[kTW + 1] - p[-kTW + 1]);
+                    ia += Ix * Ix;
+                    ib += Iy * Iy;
+                    ic += Ix * Iy;
+                }
+            }
         }
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
+        for (int o = 8; o > 0; o >>= 1) {
             ia += __shfl_xor(ia, o, 64);
             ib += __shfl_xor(ib, o, 64);
             ic += __shfl_xor(ic, o, 64);
         }
-        if (lane == 0) {
+        if (valid && sl == 0) {
             const float scale = 1.f / ((1 << 2) * 7 * 255.f);
             const float s4 = scale * scale * scale * scale;
             const float fa = (float)ia, fb = (float)ib, fc = (float)ic;
-            const int s = sc[(r + 1) * kSW + xl + 1];
+            const int sco = sc[(r + 1) * kSW + xl + 1];
             CandRec c;
             c.xy = (unsigned)(x0 + xl) | ((unsigned)(y0 + r) << 16);
-            c.score = s;
+            c.score = sco;
             c.harris = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
             c.pad = 0;
             cand[(long long)(a.cell_base[l] + (y0 + r) * ntx + tx) * kCellCap + rank] = c;
-            atomicAdd(&s_hist[s], 1);
+            atomicAdd(&s_hist[sco], 1);
         }
     }
     __syncthreads();
