@@ -94,7 +94,7 @@ struct BAArgs {
     const int* lobs_ptr;     // n_opt + 1
     const int* lobs_kf;
     const int* lobs_lm;      // landmark slot of each landmark-stage observation
-    const int* lm_blk;       // k_landmark_solve workgroup -> first landmark (n_blocks + 1)
+    const int* lm_blk;       // k_landmark_solve workgroup -> {first landmark, first observation} (n_blocks + 1)
     const double2* lobs_uv;
     BAState* state;
 };
@@ -374,8 +374,9 @@ __global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
     double* terms = kf_lds + (long long)a.n_kf * kLdsStride;  // [9][kLmBlock]
     const int tid = threadIdx.x;
     VX_KT(8);
-    const int l0 = a.lm_blk[blockIdx.x], l1 = a.lm_blk[blockIdx.x + 1];
-    const int ob0 = a.lobs_ptr[l0], ob1 = a.lobs_ptr[l1];
+    const int2 b0 = reinterpret_cast<const int2*>(a.lm_blk)[blockIdx.x];
+    const int2 b1 = reinterpret_cast<const int2*>(a.lm_blk)[blockIdx.x + 1];
+    const int l0 = b0.x, l1 = b1.x, ob0 = b0.y, ob1 = b1.y;
     // this thread's observation ...
     const int o = ob0 + tid;
     const bool has_o = o < ob1;
@@ -577,19 +578,23 @@ int upload(vx_ctx* c, DevBuf& d, const std::vector<T>& h) {
 
 // k_landmark_solve workgroups: whole landmarks, at most kLmBlock landmarks and observations each
 // (a window of <= kMaxKfLds keyframes gives a landmark <= kMaxKfLds < kLmBlock of them)
+// Returned as {first landmark, its first observation} per workgroup (n_blocks + 1 pairs), so a
+// workgroup reads both in one load instead of a dependent lobs_ptr load after lm_blk.
 std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt) {
-    std::vector<int> blk{0};
+    std::vector<int> blk{0, lptr[0]};
     int n_o = 0, n_l = 0;
     for (int s = 0; s < n_opt; ++s) {
         const int cnt = lptr[s + 1] - lptr[s];
         if (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock) {
             blk.push_back(s);
+            blk.push_back(lptr[s]);
             n_o = n_l = 0;
         }
         n_o += cnt;
         ++n_l;
     }
     blk.push_back(n_opt);
+    blk.push_back(lptr[n_opt]);
     return blk;
 }
 
@@ -728,7 +733,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     }
     p->n_lm_obs = (int64_t)lkf.size();
     const std::vector<int> blk = pack_lm_blocks(lptr, p->n_opt);
-    p->n_lm_blocks = (int)blk.size() - 1;
+    p->n_lm_blocks = (int)blk.size() / 2 - 1;
     if (!device) return VX_OK;
 
     VX_HIP(c, hipSetDevice(c->device));

@@ -38,6 +38,7 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p);
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
 // the same plan from a device-resident map (vx_dmap; its CSR rebuilt first if stale)
 int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
-// greedy k_landmark_solve workgroup packing over the landmark-stage CSR pointers
+// greedy k_landmark_solve workgroup packing over the landmark-stage CSR pointers: {first landmark,
+// first observation} per workgroup, n_blocks + 1 pairs
 std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt);
 }  // namespace vx

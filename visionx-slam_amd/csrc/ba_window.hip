@@ -486,7 +486,7 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
                        in.pos, p->lm_pos0.as<double>());
     VX_LAUNCH_CHECK(c, "plan fill kernels");
     const std::vector<int> blk = pack_lm_blocks(lptr, n_opt);
-    p->n_lm_blocks = (int)blk.size() - 1;
+    p->n_lm_blocks = (int)blk.size() / 2 - 1;
     if ((rc = up(c, p->lm_blk, blk.data(), blk.size()))) return rc;
     if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
     if ((rc = alloc_run_buffers(c, p))) return rc;
