@@ -687,23 +687,65 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
         const int c = tid * cpt + j;
         cnt0[j] = (k1 > 0 && j < cpt && c < ncell) ? cell_count[cbase + c] : 0;
     }
-    // ---- level histogram of FAST scores (border-passing NMS corners) -> n and thr1
-    int hv = 0;
-    if (tid < 256) {
+    // the first pass's records depend only on the counts, not on thr1: they are requested now, so
+    // their latency passes while wave 0 derives thr1 from the histogram (no block barrier there:
+    // a barrier would wait for these loads)
+    int tot0 = 0;
 #pragma unroll
-        for (int r = 0; r < kHistRep; ++r) hv += hist[(l * kHistRep + r) * 256 + 255 - tid];
+    for (int j = 0; j < kCellsPer; ++j) tot0 += cnt0[j];
+    auto rec_index_of = [&](const int (&cn)[kCellsPer], int c0, int k) {
+        int j = 0, i = k;
+#pragma unroll
+        for (int jj = 0; jj < kCellsPer; ++jj)
+            if (j == jj && i >= cn[jj]) {
+                i -= cn[jj];
+                j = jj + 1;
+            }
+        return (cbase + c0 + j) * kCellCap + i;
+    };
+    CandRec rr0[kRecBatch];
+#pragma unroll
+    for (int k = 0; k < kRecBatch; ++k) rr0[k] = k < tot0 ? cand[rec_index_of(cnt0, tid * cpt, k)] : CandRec{};
+    // ---- level histogram of FAST scores (border-passing NMS corners) -> thr1, on wave 0: lane L
+    // holds the bins 255 - 4L .. 252 - 4L (descending), an inclusive wave scan gives the count of
+    // candidates at or above each bin; thr1 = the largest score whose count reaches 2q (A.3)
+    if ((tid >> 6) == 0) {
+        const int lane = tid & 63;
+        int c[4], ls = 0;
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) {
+            int h = 0;
+#pragma unroll
+            for (int r = 0; r < kHistRep; ++r) h += hist[(l * kHistRep + r) * 256 + 255 - (4 * lane + q2)];
+            c[q2] = h;
+            ls += h;
+        }
+        int incl = ls;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        const int n = __shfl(incl, 63, 64);
+        int t1 = 0;
+        if (n > k1 && k1 > 0) {
+            const unsigned long long m = __ballot(incl >= k1);
+            const int first = __ffsll((long long)m) - 1;
+            int cand_t = 0;
+            if (lane == first) {
+                int cum = incl - ls;
+#pragma unroll
+                for (int q2 = 0; q2 < 4; ++q2) {
+                    cum += c[q2];
+                    if (cum >= k1 && cand_t == 0 && c[q2] > 0) cand_t = 256 - (4 * lane + q2);  // score + 1
+                }
+            }
+            t1 = __shfl(cand_t, first, 64) - 1;
+        }
+        if (lane == 0) s_out[0] = t1;
     }
-    int n;
-    {
-        int ex = block_scan_excl<kSelBlock>(hv, sw, n);
-        (void)ex;
-    }
-    int thr1 = 0;
-    if (n > k1 && k1 > 0) {
-        if (tid == 0) s_out[0] = 0;
-        find_digit(hv, k1, sw, s_out);
-        thr1 = s_out[0];
-    }
+    __syncthreads();
+    const int thr1 = s_out[0];
     VX_KT(9);
     // ---- gather kept candidates (score >= thr1) in raster order.  Each thread owns cpt
     // consecutive cells: their counts are loaded in one batch, then up to kRecBatch of their
@@ -722,19 +764,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 #pragma unroll
             for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
             // k-th record of this thread -> cand index
-            auto rec_index = [&](int k) {
-                int j = 0, i = k;
-#pragma unroll
-                for (int jj = 0; jj < kCellsPer; ++jj)
-                    if (j == jj && i >= cnts[jj]) {
-                        i -= cnts[jj];
-                        j = jj + 1;
-                    }
-                return (cbase + c0 + j) * kCellCap + i;
-            };
+            auto rec_index = [&](int k) { return rec_index_of(cnts, c0, k); };
             CandRec rr[kRecBatch];
 #pragma unroll
-            for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? cand[rec_index(k)] : CandRec{};
+            for (int k = 0; k < kRecBatch; ++k) rr[k] = base == 0 ? rr0[k] : k < tot ? cand[rec_index(k)] : CandRec{};
             int kc = 0;
 #pragma unroll
             for (int k = 0; k < kRecBatch; ++k) kc += (k < tot && rr[k].score >= thr1) ? 1 : 0;
