@@ -1,0 +1,65 @@
+"""bench.py's output contract (the driver parses its one JSON line) and the PMC traffic summary
+that feeds `roofline.traffic`."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _write_counters(path, counter, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Counter_Name", "Counter_Value"])
+        w.writeheader()
+        for name, value in rows:
+            w.writerow({"Kernel_Name": name, "Counter_Name": counter, "Counter_Value": value})
+
+
+def test_pmc_summary_tags_workload_and_doubles_fetch(tmp_path):
+    """FETCH_SIZE is doubled (gfx950 correction), WRITE_SIZE taken as is, both KB -> bytes per
+    launch averaged over dispatches, and the output names the workload it was measured on."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import pmc_summary
+
+    k = "void vx::(anonymous namespace)::k_landmark_solve(vx::BAArgs, int)"
+    _write_counters(tmp_path / "f.csv", "FETCH_SIZE", [(k, 100.0), (k, 300.0)])
+    _write_counters(tmp_path / "w.csv", "WRITE_SIZE", [(k, 10.0), (k, 30.0)])
+    out = tmp_path / "t.json"
+    pmc_summary.main(str(tmp_path / "f.csv"), str(tmp_path / "w.csv"), str(out), "C4", "2")
+    d = json.load(open(out))
+    assert d["config"] == "C4" and d["n_gpus"] == 2
+    assert d["bytes_per_launch"]["ba_landmark"] == int(2 * 200.0 * 1024 + 20.0 * 1024)
+
+
+def test_committed_traffic_is_tagged():
+    d = json.load(open(os.path.join(ROOT, "profiles", "pmc_traffic.json")))
+    assert d["config"] == "C3" and d["n_gpus"] == 1 and d["bytes_per_launch"]["ba_landmark"] > 0
+
+
+def test_bench_help_runs_without_gpu():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "--steps" in r.stdout and "--grid-share" in r.stdout
+
+
+@pytest.mark.gpu
+def test_bench_json_line():
+    """A short bench run prints exactly one JSON line with the fields the driver reads."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
+                        "--no-cpu-baseline"], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert key in d, key
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 2 and d["higher_is_better"] is False
+    assert d["value"] > 0 and d["unit"] == "ms/frame" and d["config"]["workload"].startswith("C3")
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] < 1
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-4
