@@ -430,6 +430,45 @@ def test_device_plan_build_equals_host_build(ctx, cfg):
             assert np.array_equal(md["kf_pose"], mh["kf_pose"]) and np.array_equal(md["lm_pos"], mh["lm_pos"])
 
 
+def test_sharded_plan_split(ctx):
+    """Pose-stage slices per keyframe (ba_plan.hpp ba_split): from the pre-shard feature count
+    (1914 at the 8-GPU rig's window), divided by the shard count, so every rank builds the same
+    all-reduced layout and an 8-way shard all-reduces 400 x 1 x 32 doubles instead of 400 x 4 x 32."""
+    import vxslam
+
+    m = synth.make_ba_map(0x5EED0003, 400, 160000, n_streams=8, n_old_kf=16)
+    opts = vxslam.default_ba_options(window=400)
+    want = {1: 4, 2: 2, 4: 1, 8: 1}
+    for n in (1, 2, 4, 8):
+        for host_build in (False, True):
+            splits = {ctx.ba_plan(m, opts, shard_rank=r, shard_count=n, host_build=host_build).info()["n_split"]
+                      for r in sorted({0, n - 1})}
+            assert splits == {want[n]}, (n, host_build, splits)
+
+
+def test_comm_init_single_rank():
+    """The RCCL communicator the multi-GPU bench creates (vx_comm_unique_id, vx_comm_init) comes up
+    on this box; a 2-shard plan on a 1-rank communicator refuses to run (no half-summed solve)."""
+    import vxslam
+
+    c = vxslam.Context(0)
+    try:
+        uid = vxslam.Context.comm_unique_id()
+        assert len(uid) == 128
+        c.comm_init(uid, 1, 0)
+        m = synth.make_ba_map(7, 12, 2000, n_old_kf=2)
+        plan = c.ba_plan(m, vxslam.default_ba_options(window=12), shard_rank=0, shard_count=2)
+        with pytest.raises(vxslam.VxError):
+            plan.run_async()
+        plan.close()
+        one = c.ba_plan(m, vxslam.default_ba_options(window=12))
+        one.run_async()
+        assert one.fetch(m.copy()).status == 0
+        one.close()
+    finally:
+        c.close()
+
+
 def test_device_plan_build_edges(ctx):
     import vxslam
 

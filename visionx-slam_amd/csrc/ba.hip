@@ -700,7 +700,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
                 for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) n += m->feat_flags[f] & 1;
                 mx = std::max(mx, n);
             }
-        p->n_split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (mx + kPoseBlock - 1) / kPoseBlock));
+        p->n_split = ba_split(mx, p->shard_count);
     }
     p->n_lm = (int)p->lm_map_idx.size();
     p->n_pose_obs = (int64_t)puv.size();

@@ -33,6 +33,17 @@ constexpr int kBaPoseBlock = 512;  // k_pose_kf threads per workgroup (ba.hip kP
 constexpr int kBaLmBlock = 512;    // k_landmark_solve observations / landmarks per workgroup
 constexpr int kBaMaxSplit = 4;     // pose-stage workgroups per keyframe
 
+// Pose-stage workgroups per keyframe: about one observation per thread.  mx is the largest window
+// keyframe's landmark-feature count before sharding (a count every rank sees alike, so the
+// all-reduced partial layout is the same on every rank); a shard holds ~1/shard_count of those
+// observations, so sharded plans use fewer slices — which also shrinks the per-iteration
+// all-reduce (n_kf x n_split x 32 doubles) up to kBaMaxSplit times.  Any n_split >= 1 is correct.
+inline int ba_split(int64_t mx, int shard_count) {
+    const int64_t per = (int64_t)kBaPoseBlock * (shard_count > 1 ? shard_count : 1);
+    const int64_t s = (mx + per - 1) / per;
+    return (int)(s < 1 ? 1 : (s > kBaMaxSplit ? kBaMaxSplit : s));
+}
+
 int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p);
 // SelectKeyFrames + landmark set + both CSRs built on the device from the map snapshot (§8f rank 2)
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);

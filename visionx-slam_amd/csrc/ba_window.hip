@@ -338,7 +338,7 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
             mx = std::max(mx, cnt);
         }
     }
-    p->n_split = (int)std::min<int64_t>(kBaMaxSplit, std::max<int64_t>(1, (mx + kBaPoseBlock - 1) / kBaPoseBlock));
+    p->n_split = ba_split(mx, p->shard_count);
     const int nl = m->n_lm;
     const int64_t nobs = nl > 0 ? m->lm_obs_ptr[nl] : 0;
     VX_HIP(c, hipSetDevice(c->device));
@@ -556,7 +556,7 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
         kf_flags[r] = cam[r];
         if (cam[r]) mx = std::max<int64_t>(mx, m->kf_valid_cnt[k]);
     }
-    p->n_split = (int)std::min<int64_t>(kBaMaxSplit, std::max<int64_t>(1, (mx + kBaPoseBlock - 1) / kBaPoseBlock));
+    p->n_split = ba_split(mx, p->shard_count);
     const int nf = wptr[nk];
     VX_HIP(c, hipSetDevice(c->device));
     vx_ctx::PlanScratch& B = c->plan_scratch;
