@@ -119,17 +119,15 @@ __device__ __forceinline__ const double* lm_in(const BAArgs& a, int it, int s) {
 __device__ __forceinline__ void solve_pose(const BAArgs& a, int flags, const double* S, double* T, double* R) {
     const int obs = (int)S[28];
     if (obs >= a.min_pose_obs && (flags & 1)) {
-        double H[36], b[6], dx[6];
+        double U[21], b[6], dx[6];
 #pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = 0; c < 6; ++c) H[6 * r + c] = r <= c ? S[hidx(r, c)] : S[hidx(c, r)];
+        for (int t = 0; t < 21; ++t) U[t] = S[t];
 #pragma unroll
         for (int r = 0; r < 6; ++r) {
-            H[7 * r] += 1e-6;
+            U[hidx(r, r)] += 1e-6;
             b[r] = S[21 + r];
         }
-        ldlt_spd_solve<6>(H, b, dx);
+        spd6_block_solve(U, b, dx);
         bool fin = true;
 #pragma unroll
         for (int r = 0; r < 6; ++r) fin = fin && isfinite(dx[r]);

@@ -192,6 +192,61 @@ __device__ __forceinline__ void ldlt_spd_solve(const double* A, const double* b,
     });
 }
 
+// Symmetric 3x3 inverse by cofactors: m = {m00 m01 m02 m11 m12 m22}, out the same layout.
+// Dependent depth ~11 FP64 ops (2 cofactor, 3 determinant, 5 reciprocal, 1 scale).
+__device__ __forceinline__ void sym3_inv(const double* m, double* out) {
+    const double c00 = m[3] * m[5] - m[4] * m[4];
+    const double c01 = m[2] * m[4] - m[1] * m[5];
+    const double c02 = m[1] * m[4] - m[2] * m[3];
+    const double c11 = m[0] * m[5] - m[2] * m[2];
+    const double c12 = m[1] * m[2] - m[0] * m[4];
+    const double c22 = m[0] * m[3] - m[1] * m[1];
+    const double id = frcp(m[0] * c00 + (m[1] * c01 + m[2] * c02));
+    out[0] = c00 * id;
+    out[1] = c01 * id;
+    out[2] = c02 * id;
+    out[3] = c11 * id;
+    out[4] = c12 * id;
+    out[5] = c22 * id;
+}
+
+// x = H^-1 b for the damped SPD 6x6 pose system given as its upper triangle (hidx layout), by 3x3
+// blocks: H = [A B; B^T C], W = A^-1 B, S = C - B^T W, x2 = S^-1 (b2 - B^T A^-1 b1), x1 = A^-1 b1 -
+// W x2.  Same solution as an LDLT up to rounding, with a dependent chain of ~35 FP64 ops instead
+// of ~100 (the one-thread-per-keyframe pose solve of k_landmark_solve sits on the LocalBA
+// critical path).  A singular block gives a non-finite x, which the caller rejects.
+__device__ __forceinline__ void spd6_block_solve(const double* U, const double* b, double* x) {
+    const double A[6] = {U[0], U[1], U[2], U[6], U[7], U[11]};  // (00 01 02 11 12 22)
+    const double B[3][3] = {{U[3], U[4], U[5]}, {U[8], U[9], U[10]}, {U[12], U[13], U[14]}};
+    double Ai[6];
+    sym3_inv(A, Ai);
+    const double Ai3[3][3] = {{Ai[0], Ai[1], Ai[2]}, {Ai[1], Ai[3], Ai[4]}, {Ai[2], Ai[4], Ai[5]}};
+    double W[3][3], y1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) W[i][j] = Ai3[i][0] * B[0][j] + (Ai3[i][1] * B[1][j] + Ai3[i][2] * B[2][j]);
+        y1[i] = Ai3[i][0] * b[0] + (Ai3[i][1] * b[1] + Ai3[i][2] * b[2]);
+    }
+    const int cu[6][2] = {{0, 0}, {0, 1}, {0, 2}, {1, 1}, {1, 2}, {2, 2}};
+    const double Cu[6] = {U[15], U[16], U[17], U[18], U[19], U[20]};
+    double S[6], Si[6];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) {
+        const int i = cu[e][0], j = cu[e][1];
+        S[e] = Cu[e] - (B[0][i] * W[0][j] + (B[1][i] * W[1][j] + B[2][i] * W[2][j]));
+    }
+    sym3_inv(S, Si);
+    double r2[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r2[i] = b[3 + i] - (B[0][i] * y1[0] + (B[1][i] * y1[1] + B[2][i] * y1[2]));
+    const double Si3[3][3] = {{Si[0], Si[1], Si[2]}, {Si[1], Si[3], Si[4]}, {Si[2], Si[4], Si[5]}};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[3 + i] = Si3[i][0] * r2[0] + (Si3[i][1] * r2[1] + Si3[i][2] * r2[2]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = y1[i] - (W[i][0] * x[3] + (W[i][1] * x[4] + W[i][2] * x[5]));
+}
+
 // upper-triangle index of the 6x6 pose Hessian
 __device__ __forceinline__ int hidx(int i, int j) {  // i <= j
     return i * 6 - (i * (i - 1)) / 2 + (j - i);
