@@ -29,9 +29,15 @@ struct vx_ba_plan {
 struct vx_dmap;
 
 namespace vx {
-constexpr int kBaPoseBlock = 512;  // k_pose_kf threads per workgroup (ba.hip kPoseBlock)
+#ifndef VX_BA_POSE_BLOCK  // build-time overrides for sweeps only (scripts/ba_variants.sh)
+#define VX_BA_POSE_BLOCK 512
+#endif
+#ifndef VX_BA_MAX_SPLIT
+#define VX_BA_MAX_SPLIT 4
+#endif
+constexpr int kBaPoseBlock = VX_BA_POSE_BLOCK;  // k_pose_kf threads per workgroup (ba.hip kPoseBlock)
 constexpr int kBaLmBlock = 512;    // k_landmark_solve observations / landmarks per workgroup
-constexpr int kBaMaxSplit = 4;     // pose-stage workgroups per keyframe
+constexpr int kBaMaxSplit = VX_BA_MAX_SPLIT;     // pose-stage workgroups per keyframe
 
 // Pose-stage workgroups per keyframe: about one observation per thread.  mx is the largest window
 // keyframe's landmark-feature count before sharding (a count every rank sees alike, so the
