@@ -231,8 +231,15 @@ int vx_ba_plan_run_async(vx_ctx* ctx, vx_ba_plan* plan);
 int vx_ba_plan_fetch(vx_ctx* ctx, vx_ba_plan* plan, vx_map_view* map, vx_ba_stats* stats);
 void vx_ba_plan_destroy(vx_ba_plan* plan);
 /* sizes of the device problem: out8 = {n_kf, n_lm (local shard), n_pose_obs, n_lm_obs, n_opt,
- * n_split (pose-stage workgroups per keyframe), n_lm_blocks (landmark-stage workgroups), 0} */
+ * n_split (pose-stage workgroups per keyframe), n_lm_blocks (landmark-stage workgroups),
+ * max_lm_obs (most landmark-stage observations of one landmark)} */
 int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out8);
+/* Test hook: runs the n shard plans plans[r] (shard r of n, built from one window, all on ctx) the
+ * way n ranks would run them, on one device: per iteration every shard's pose stage, then the
+ * element-wise sum of their partial blocks in rank order written back to every shard in place of
+ * the ncclAllReduce, then every shard's landmark stage (the kernel set chosen from the maxima over
+ * the shards, as the all-reduced choice of a real sharded run).  Fetch each plan afterwards. */
+int vx_ba_shard_emulate_run(vx_ctx* ctx, vx_ba_plan* const* plans, int n);
 /* Host-only dry run of vx_ba_plan_create (needs no device): out8 = {status, n_window_kf,
  * n_landmarks (all shards), n_kf, n_opt (local optimisable), n_lm (local table), n_pose_obs,
  * n_lm_obs}; lm_map_idx / kf_map_idx (optional) receive the local tables as map indices. */
@@ -260,17 +267,37 @@ int vx_dmap_add_keyframe(vx_dmap* map, uint64_t kf_id, const double* pose7, cons
                          int n_feat, const double* feat_uv, const uint64_t* feat_lm_id, const uint8_t* feat_flags);
 /* Map::InsertLandmark: ids unique; pos 3 each; bad may be NULL (all good) */
 int vx_dmap_add_landmarks(vx_dmap* map, int n, const uint64_t* lm_id, const double* pos3, const uint8_t* bad);
-/* Landmark::AddObservation(kf_id, feat_idx) on existing landmarks (VX_ERR_INVALID for unknown ids) */
+/* Landmark::AddObservation(kf_id, feat_idx) on existing landmarks (VX_ERR_INVALID for unknown ids).
+ * Like observations_[keyframe_id] = feature_idx (landmark.h:32-35), a (landmark, keyframe) pair
+ * already present keeps its place and takes the new feature index; a landmark never holds two
+ * observations from one keyframe. */
 int vx_dmap_add_observations(vx_dmap* map, int n, const uint64_t* lm_id, const uint64_t* kf_id,
                              const uint64_t* feat_idx);
+/* Landmark::RemoveObservation(kf_id) (landmark.h:37-40): the pair stops counting towards
+ * ObservationCount and leaves the landmark's list; an absent pair is a no-op (unordered_map::erase).
+ * VX_ERR_INVALID for an unknown landmark id. */
+int vx_dmap_remove_observations(vx_dmap* map, int n, const uint64_t* lm_id, const uint64_t* kf_id);
+/* Map::RemoveKeyFrame(id) (map.cpp:15-18): the keyframe leaves the map (SelectKeyFrames no longer
+ * sees it; observations naming it fail the window check like GetFrame() == nullptr).  Its feature
+ * rows stay as dead storage.  The id may be inserted again later.  VX_ERR_INVALID if absent.
+ * Tracking::RemoveKeyFrame (tracking.cpp:752-773) = vx_dmap_remove_observations for the frame's
+ * landmark features + vx_dmap_set_features (0, no landmark, outlier) + this call. */
+int vx_dmap_remove_keyframe(vx_dmap* map, uint64_t kf_id);
+/* Map::RemoveLandmark(id) (map.cpp:20-23): GetLandmark() == nullptr afterwards (pose stage and
+ * landmark set skip it).  Absent ids are a no-op, as std::unordered_map::erase. */
+int vx_dmap_remove_landmarks(vx_dmap* map, int n, const uint64_t* lm_id);
 /* Feature::landmark_id_ / has_landmark / is_outlier of features of keyframe kf_id */
 int vx_dmap_set_features(vx_dmap* map, uint64_t kf_id, int n, const int32_t* feat_idx, const uint64_t* lm_id,
                          const uint8_t* flags);
 int vx_dmap_set_landmark_bad(vx_dmap* map, int n, const uint64_t* lm_id, const uint8_t* bad);
 int vx_dmap_set_poses(vx_dmap* map, int n, const uint64_t* kf_id, const double* pose7);
-/* out4 = {keyframes, features, landmarks, observations} */
+/* out4 = {keyframe rows, feature rows, landmark rows, observation rows}: storage rows in insertion
+ * order, removed ones included (vx_dmap_download returns that many) */
 int vx_dmap_counts(const vx_dmap* map, int64_t* out4);
-/* current poses (7 per keyframe) / positions (3 per landmark) in insertion order; either may be NULL */
+/* out4 = {keyframes, landmarks, observations, 0} currently in the map (removed ones excluded) */
+int vx_dmap_live_counts(const vx_dmap* map, int64_t* out4);
+/* current poses (7 per keyframe row) / positions (3 per landmark row) in insertion order (rows of
+ * removed keyframes / landmarks included); either may be NULL */
 int vx_dmap_download(vx_dmap* map, double* kf_pose, double* lm_pos);
 /* LocalBA plan from the resident map (the plan vx_ba_plan_create builds from the equivalent
  * vx_map_view snapshot); run with vx_ba_plan_run_async as usual */

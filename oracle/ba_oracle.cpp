@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <chrono>
 #include <cmath>
 #include <limits>
 #include <map>
@@ -27,8 +28,21 @@
 
 using namespace orc_ba;
 
+// wall time of the last call's two parts (bench.py's CPU baseline reports them apart): the window /
+// landmark-set selection (local_ba.cpp:66-108, what a GPU plan build replaces) and the iterations
+// (local_ba.cpp:110-248, what a GPU plan run replaces)
+static double g_setup_s = 0.0, g_iter_s = 0.0;
+
+extern "C" void orc_ba_last_timing(double* out2) {
+    out2[0] = g_setup_s;
+    out2[1] = g_iter_s;
+}
+
 extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_ref,
                                    const orc_ba_options* opt, orc_ba_stats* st) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    g_setup_s = g_iter_s = 0.0;
     orc_ba_stats local{};
     if (!st) st = &local;
     *st = orc_ba_stats{};
@@ -93,6 +107,12 @@ extern "C" int orc_ba_optimize_map(orc_map_view* m, uint64_t ref_kf_id, int has_
         st->gate_margin = std::min(st->gate_margin, std::fabs(e - opt->max_reproj_error));
     };
 
+    const auto t1 = clk::now();
+    g_setup_s = std::chrono::duration<double>(t1 - t0).count();
+    struct IterTimer {  // stops at every return below
+        clk::time_point t;
+        ~IterTimer() { g_iter_s = std::chrono::duration<double>(clk::now() - t).count(); }
+    } iter_timer{t1};
     double last_cost = std::numeric_limits<double>::max();
     for (int iter = 0; iter < opt->max_iterations; ++iter) {
         double total_cost = 0.0;

@@ -110,6 +110,8 @@ typedef struct {
 
 int orc_ba_optimize_map(orc_map_view* map, uint64_t ref_kf_id, int has_ref,
                         const orc_ba_options* opt, orc_ba_stats* stats);
+/* wall seconds of the last orc_ba_optimize_map: {window + landmark-set selection, iterations} */
+void orc_ba_last_timing(double* out2);
 
 /* ---- Schur-complement joint BA (NOT in the reference: SURVEY.md §8f rank 4, BASELINE.json
  * north_star "Schur-complement marginalisation ... dense pose solve").  Restates the algorithm of

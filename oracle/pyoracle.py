@@ -212,6 +212,14 @@ def ba_optimize(m, opts=None, ref_kf_id=None):
     return st
 
 
+def ba_last_timing():
+    """(setup_s, iterations_s) of the last ba_optimize: window / landmark-set selection
+    (local_ba.cpp:66-108) and the alternating iterations (:110-248)."""
+    out = (C.c_double * 2)()
+    lib().orc_ba_last_timing(out)
+    return out[0], out[1]
+
+
 # ---------------------------------------------------------------------------- Schur-complement BA
 class SBAOptions(C.Structure):
     _fields_ = [("window_size", C.c_int32), ("max_iterations", C.c_int32),

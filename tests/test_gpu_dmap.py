@@ -154,3 +154,124 @@ def test_dmap_errors(ctx):
     p = dm.plan(vxslam.default_ba_options(window=5, iters=2))
     assert p.info()["n_kf"] == 0
     dm.close()
+
+
+def test_dmap_culling_and_reobservation(ctx):
+    """The map edits of culling and re-association (tracking.cpp:652-773, landmark.h:32-40,
+    map.cpp:15-23) on the resident map: Tracking::RemoveKeyFrame of a window keyframe
+    (RemoveObservation of each of its landmarks + feature reset + Map::RemoveKeyFrame),
+    CullLandmarks (SetBad + feature reset + Map::RemoveLandmark), AddObservation of a pair that is
+    already present (the entry keeps its place, takes the new feature index: observations_[kf] = i)
+    and of a new pair twice in one batch.  Every plan afterwards equals the snapshot plan of the
+    map as it then stands (ObservationCount, window and landmark table all follow the removals)."""
+    m = synth.make_ba_map(0xD9, 14, 3000, n_old_kf=2)
+    for key in ("obs_kf_id", "obs_feat_idx", "feat_lm_id", "feat_flags", "lm_bad"):
+        m[key] = m[key].copy()
+    dm = vxslam.DMap(ctx)
+    mir = _Mirror(m, dm)
+    order = np.argsort(m["kf_id"], kind="stable")
+    for k in order:
+        mir.add(k)
+    opts = vxslam.default_ba_options(window=8, iters=3)
+    rng = np.random.default_rng(11)
+
+    def check():
+        m2 = mir.snapshot()
+        pd = dm.plan(opts)
+        ps = ctx.ba_plan(m2, opts)
+        assert pd.info() == ps.info()
+        _stats_equal(_run(pd), _run(ps))
+        pd.apply(dm)
+        ps.fetch(m2)
+        pose_d, pos_d = dm.download()
+        kr, lr = np.asarray(mir.kf_rows), np.asarray(mir.lm_rows, np.int64)
+        assert np.array_equal(pose_d[[mir.row_of_kf[k] for k in kr]], m2["kf_pose"].reshape(-1, 7))
+        assert np.array_equal(pos_d[[mir.row_of_lm[l] for l in lr]], m2["lm_pos"].reshape(-1, 3))
+        m["kf_pose"].reshape(-1, 7)[kr] = m2["kf_pose"].reshape(-1, 7)
+        m["lm_pos"].reshape(-1, 3)[lr] = m2["lm_pos"].reshape(-1, 3)
+        live = dm.live_counts()
+        assert live == {"kf": len(kr), "lm": len(lr),
+                        "obs": int(sum(mir.obs_lm[r] in mir.lm_set() for r in mir.obs_rows))}
+        pd.close(), ps.close()
+        return m2
+
+    mir.row_of_kf = {int(k): i for i, k in enumerate(mir.kf_rows)}
+    mir.row_of_lm = {int(l): i for i, l in enumerate(mir.lm_rows)}
+    mir.lm_set = lambda: set(mir.lm_rows)
+    check()
+
+    def clear_features(k, fidx):
+        f0 = m["kf_feat_ptr"][k]
+        m["feat_lm_id"][f0 + fidx] = 0
+        m["feat_flags"][f0 + fidx] = 2  # has_landmark false, is_outlier true
+        dm.set_features(int(m["kf_id"][k]), fidx.astype(np.int32), np.zeros(len(fidx), np.uint64),
+                        np.full(len(fidx), 2, np.uint8))
+
+    # --- Tracking::RemoveKeyFrame of a keyframe inside the window (tracking.cpp:752-773)
+    k = int(order[-4])
+    kid = int(m["kf_id"][k])
+    f0, f1 = m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]
+    fidx = np.nonzero(m["feat_flags"][f0:f1] & 1)[0]
+    lms = m["feat_lm_id"][f0 + fidx]
+    known = np.isin(lms, m["lm_id"][np.asarray(mir.lm_rows)])
+    dm.remove_observations(lms[known], np.full(int(known.sum()), kid, np.uint64))
+    lm_row = {int(i): r for r, i in enumerate(m["lm_id"])}
+    drop = {(lm_row[int(i)], kid) for i in lms[known]}
+    mir.obs_rows = [r for r in mir.obs_rows if (int(mir.obs_lm[r]), int(m["obs_kf_id"][r])) not in drop]
+    clear_features(k, fidx)
+    dm.remove_keyframe(kid)
+    mir.kf_rows.remove(k)
+    with pytest.raises(vxslam.VxError):
+        dm.remove_keyframe(kid)  # already gone
+    dm.remove_observations(lms[known][:3], np.full(3, kid, np.uint64))  # absent pairs: no-op
+    check()
+
+    # --- CullLandmarks (tracking.cpp:652-750): SetBad, features reset, Map::RemoveLandmark
+    cull = rng.choice(np.asarray(mir.lm_rows), 40, replace=False)
+    for k2 in mir.kf_rows:
+        g0, g1 = m["kf_feat_ptr"][k2], m["kf_feat_ptr"][k2 + 1]
+        hit = np.nonzero(np.isin(m["feat_lm_id"][g0:g1], m["lm_id"][cull]) & (m["feat_flags"][g0:g1] & 1 > 0))[0]
+        if len(hit):
+            clear_features(k2, hit)
+    dm.set_landmark_bad(m["lm_id"][cull], np.ones(len(cull), np.uint8))
+    dm.remove_landmarks(m["lm_id"][cull])
+    dm.remove_landmarks(m["lm_id"][cull[:2]])  # absent ids: no-op
+    for l in cull:
+        mir.lm_rows.remove(int(l))
+    with pytest.raises(vxslam.VxError):
+        dm.add_observations(m["lm_id"][cull[:1]], [kid], [0])  # a removed landmark is unknown
+    check()
+
+    # --- AddObservation of a present pair: re-associate landmark l from feature fi to feature fj
+    #     of the same keyframe (the pair keeps its place in the landmark's list)
+    live = set(mir.lm_rows)
+    cand = [r for r in mir.obs_rows if int(mir.obs_lm[r]) in live and int(m["obs_kf_id"][r]) in
+            {int(m["kf_id"][q]) for q in mir.kf_rows[-6:]}]
+    for r in rng.choice(np.asarray(cand), 25, replace=False):
+        l, kq = int(mir.obs_lm[r]), int(m["obs_kf_id"][r])
+        q = int(np.nonzero(m["kf_id"] == kq)[0][0])
+        g0, g1 = m["kf_feat_ptr"][q], m["kf_feat_ptr"][q + 1]
+        free = np.nonzero((m["feat_flags"][g0:g1] & 1) == 0)[0]
+        fi, fj = int(m["obs_feat_idx"][r]), int(free[0])
+        m["feat_lm_id"][g0 + fj], m["feat_flags"][g0 + fj] = m["lm_id"][l], 1
+        dm.set_features(kq, np.array([fj], np.int32), m["lm_id"][[l]], np.array([1], np.uint8))
+        if fi < g1 - g0 and m["feat_lm_id"][g0 + fi] == m["lm_id"][l]:
+            clear_features(q, np.array([fi]))
+        m["obs_feat_idx"][r] = fj
+        dm.add_observations(m["lm_id"][[l]], [kq], [fj])
+    # a new pair added twice in one batch: one entry, the later feature index
+    q = mir.kf_rows[-1]
+    kq = int(m["kf_id"][q])
+    seen_in_q = {int(mir.obs_lm[r]) for r in mir.obs_rows if int(m["obs_kf_id"][r]) == kq}
+    l = next(int(x) for x in mir.lm_rows[5:] if int(x) not in seen_in_q)
+    g0, g1 = m["kf_feat_ptr"][q], m["kf_feat_ptr"][q + 1]
+    fa, fb = np.nonzero((m["feat_flags"][g0:g1] & 1) == 0)[0][:2]
+    m["feat_lm_id"][g0 + fb], m["feat_flags"][g0 + fb] = m["lm_id"][l], 1
+    dm.set_features(kq, np.array([fb], np.int32), m["lm_id"][[l]], np.array([1], np.uint8))
+    dm.add_observations(m["lm_id"][[l, l]], [kq, kq], [fa, fb])
+    m["obs_kf_id"] = np.append(m["obs_kf_id"], np.uint64(kq))
+    m["obs_feat_idx"] = np.append(m["obs_feat_idx"], np.uint64(fb))
+    mir.obs_lm = np.append(mir.obs_lm, l)
+    mir.obs_rows.append(len(m["obs_kf_id"]) - 1)
+    check()
+    dm.close()

@@ -1,0 +1,141 @@
+"""Landmark-sharded LocalBA on one GPU (vx_ba_shard_emulate_run).
+
+The sharded path of bench.py at N GPUs — N shard plans of one global window (landmarks split by
+splitmix64(id) mod N, each with all its observations), per iteration every shard's pose stage, the
+sum of the per-(keyframe, slice) partial blocks over the shards (ncclAllReduce on a real rig),
+every shard's landmark stage — run on one device with the all-reduce replaced by a rank-order sum.
+Every shard must end with bitwise-identical poses and stop decisions, the union of the shards'
+landmarks must be the unsharded result (≤ 1e-4, no gate flips), and both must match the CPU
+restatement.  The windows are the ones bench.py builds at N = 2, 4, 8 (N x 50 KF / N x 20k)."""
+import numpy as np
+import pytest
+
+import vxslam
+from vxslam import synth
+
+from test_gpu_parity import _assert_ba_close, _canon
+
+pytestmark = pytest.mark.gpu
+
+
+def _shard_run(ctx, m, opts, n):
+    plans = [ctx.ba_plan(m, opts, shard_rank=r, shard_count=n) for r in range(n)]
+    infos = [p.info() for p in plans]
+    ctx.ba_shard_emulate(plans)
+    outs, stats = [], []
+    for p in plans:
+        mm = m.copy()
+        stats.append(p.fetch(mm))
+        outs.append(mm)
+        p.close()
+    return infos, outs, stats
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_sharded_localba_bench_windows(ctx, oracle, n):
+    nk, nl = 50 * n, 20000 * n
+    m = synth.make_ba_map(0x5EED0003, nk, nl, n_streams=n, n_old_kf=2 * n)  # bench.py's rig window
+    opts = vxslam.default_ba_options(window=nk)
+    infos, outs, stats = _shard_run(ctx, m, opts, n)
+    assert len({i["n_split"] for i in infos}) == 1 and len({i["n_kf"] for i in infos}) == 1
+    assert sum(i["n_opt"] for i in infos) == stats[0].n_landmarks  # the shards partition the landmark set
+    # every rank: the same poses (bitwise) and the same stop decisions
+    for o, s in zip(outs[1:], stats[1:]):
+        assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"])
+        assert (s.iterations, list(s.obs[:16]), list(s.cost[:16])) == \
+               (stats[0].iterations, list(stats[0].obs[:16]), list(stats[0].cost[:16]))
+    # union of the shards' landmarks
+    shard = np.array([vxslam.lib().vx_ba_shard_of(int(i), n) for i in m["lm_id"]])
+    got = m.copy()
+    got["kf_pose"] = outs[0]["kf_pose"]
+    lp = got["lm_pos"].reshape(-1, 3).copy()
+    for r in range(n):
+        sel = shard == r
+        lp[sel] = outs[r]["lm_pos"].reshape(-1, 3)[sel]
+    got["lm_pos"] = lp.reshape(m["lm_pos"].shape)
+    # vs the unsharded GPU run and the CPU restatement
+    one = m.copy()
+    st1 = ctx.ba_optimize(one, opts)
+    _assert_ba_close(got, one, stats[0], st1)
+    mc = m.copy()
+    stc = oracle.ba_optimize(mc, oracle.ba_options(window=nk))
+    if stc.gate_margin < 1e-8:
+        pytest.skip(f"gate margin {stc.gate_margin} too small for a stable comparison")
+    _assert_ba_close(got, mc, stats[0], stc)
+
+
+def test_sharded_kernel_choice_is_shared(ctx, oracle):
+    """A window near the kernel-choice threshold (workgroups x keyframes = 80,000 at 200
+    keyframes): the unsharded window runs the large-window kernels, its 2- and 3-way shards the
+    LDS-pose kernel, chosen from the maximum workgroup count over the shards so every rank runs the
+    same kernels; poses are bitwise equal across ranks and match the unsharded run."""
+    nk, nl = 200, 125000
+    m = synth.make_ba_map(0x5EED0200, nk, nl, n_streams=8, n_old_kf=16)
+    opts = vxslam.default_ba_options(window=nk)
+    one = m.copy()
+    ctx.ba_optimize(one, opts)
+    pc = one["kf_pose"].copy()
+    pc[:, :4] = _canon(pc[:, :4])
+    for n in (2, 3):
+        infos, outs, stats = _shard_run(ctx, m, opts, n)
+        for o in outs[1:]:
+            assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"])
+        pg = outs[0]["kf_pose"].copy()
+        pg[:, :4] = _canon(pg[:, :4])
+        assert (np.abs(pg - pc) / np.maximum(np.abs(pc), 1e-3)).max() <= 1e-4
+
+
+def test_shard_emulation_rejects_mismatched_plans(ctx):
+    m = synth.make_ba_map(7, 12, 2000, n_old_kf=2)
+    opts = vxslam.default_ba_options(window=12)
+    a = ctx.ba_plan(m, opts, shard_rank=0, shard_count=2)
+    b = ctx.ba_plan(m, opts, shard_rank=0, shard_count=2)  # rank 0 twice
+    with pytest.raises(vxslam.VxError):
+        ctx.ba_shard_emulate([a, b])
+    c = ctx.ba_plan(m, vxslam.default_ba_options(window=6), shard_rank=1, shard_count=2)  # another window
+    with pytest.raises(vxslam.VxError):
+        ctx.ba_shard_emulate([a, c])
+    a.close(), b.close(), c.close()
+
+
+def test_landmark_with_more_observations_than_a_workgroup(ctx, oracle):
+    """A snapshot that lists a landmark's (keyframe, feature) pairs over and over (600+ entries,
+    more than the 512 observations of a k_landmark_solve workgroup; a Landmark's unordered_map
+    cannot hold that, a hand-built snapshot can): the plan reports it (max_lm_obs) and runs the
+    one-thread-per-landmark kernels; the result equals the restatement, which walks the same list.
+    (The whole list is repeated, not one pair: 600 copies of one ray leave the 3x3 system nearly
+    singular along it, where both sides only agree to rounding amplified by the conditioning.)"""
+    m = synth.make_ba_map(0x5EED0300, 10, 2000, n_old_kf=2)
+    optr = m["lm_obs_ptr"]
+    # a landmark observation in the newest keyframe whose feature is a valid observation of it
+    k = int(np.argmax(m["kf_id"]))
+    f0 = m["kf_feat_ptr"][k]
+    ok = False
+    for l in range(len(m["lm_id"])):
+        if optr[l + 1] - optr[l] < 3:  # a well-conditioned landmark (three rays or more)
+            continue
+        for o in range(optr[l], optr[l + 1]):
+            f = f0 + int(m["obs_feat_idx"][o])
+            if (m["obs_kf_id"][o] == m["kf_id"][k] and f < m["kf_feat_ptr"][k + 1] and m["feat_flags"][f] == 1
+                    and m["feat_lm_id"][f] == m["lm_id"][l]):
+                ok = True
+                break
+        if ok:
+            break
+    assert ok
+    a, b = int(optr[l]), int(optr[l + 1])
+    reps = -(-600 // (b - a))
+    extra = (reps - 1) * (b - a)
+    for key in ("obs_kf_id", "obs_feat_idx"):
+        m[key] = np.concatenate([m[key][:a], np.tile(m[key][a:b], reps), m[key][b:]])
+    m["lm_obs_ptr"] = optr + np.concatenate([np.zeros(l + 1, np.int64), np.full(len(optr) - l - 1, extra)])
+    opts = vxslam.default_ba_options(window=10)
+    plan = ctx.ba_plan(m, opts)
+    assert plan.info()["max_lm_obs"] >= 512
+    plan.run_async()
+    mg = m.copy()
+    stg = plan.fetch(mg)
+    plan.close()
+    mc = m.copy()
+    stc = oracle.ba_optimize(mc, oracle.ba_options(window=10))
+    _assert_ba_close(mg, mc, stg, stc)

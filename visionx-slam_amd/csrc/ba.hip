@@ -578,11 +578,15 @@ int upload(vx_ctx* c, DevBuf& d, const std::vector<T>& h) {
 // (a window of <= kMaxKfLds keyframes gives a landmark <= kMaxKfLds < kLmBlock of them)
 // Returned as {first landmark, its first observation} per workgroup (n_blocks + 1 pairs), so a
 // workgroup reads both in one load instead of a dependent lobs_ptr load after lm_blk.
-std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt) {
+// A landmark with more than kLmBlock observations (possible only if a snapshot lists one keyframe
+// twice for it) gets a workgroup of its own and *max_cnt reports it: plan_run then takes the
+// one-thread-per-landmark kernels, which have no such limit.
+std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt, int* max_cnt) {
     std::vector<int> blk{0, lptr[0]};
-    int n_o = 0, n_l = 0;
+    int n_o = 0, n_l = 0, mx = 0;
     for (int s = 0; s < n_opt; ++s) {
         const int cnt = lptr[s + 1] - lptr[s];
+        mx = std::max(mx, cnt);
         if (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock) {
             blk.push_back(s);
             blk.push_back(lptr[s]);
@@ -593,6 +597,7 @@ std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt) {
     }
     blk.push_back(n_opt);
     blk.push_back(lptr[n_opt]);
+    if (max_cnt) *max_cnt = mx;
     return blk;
 }
 
@@ -730,7 +735,7 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
         lptr[s + 1] = (int)lkf.size();
     }
     p->n_lm_obs = (int64_t)lkf.size();
-    const std::vector<int> blk = pack_lm_blocks(lptr, p->n_opt);
+    const std::vector<int> blk = pack_lm_blocks(lptr, p->n_opt, &p->max_lm_obs);
     p->n_lm_blocks = (int)blk.size() / 2 - 1;
     if (!device) return VX_OK;
 
@@ -751,41 +756,98 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     return alloc_run_buffers(c, p);
 }
 
+// Kernel set of a run.  Every k_landmark_solve workgroup re-solves all window poses, so that
+// redundancy grows as n_kf x workgroups: beyond the measured crossover (scripts/ba_window_sweep.py,
+// DESIGN.md §6) the large-window kernels (poses solved once, one extra launch per iteration) are
+// faster; they are also the only ones for windows beyond kMaxKfLds keyframes and for a landmark
+// with more than kLmBlock observations.  `blocks` / `max_obs` are maxima over every shard of the
+// window (all-reduced once for a sharded plan), so all ranks take the same kernels.
+bool choose_lds_poses(const vx_ba_plan* p, int blocks, int max_obs) {
+    return p->n_kf <= kMaxKfLds && !p->global_poses && (int64_t)p->n_kf * blocks <= 80000 && blocks <= 480 &&
+           max_obs <= kLmBlock;
+}
+
+size_t landmark_solve_lds(const vx_ba_plan* p) {
+    return (size_t)p->n_kf * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
+}
+
+int pose_stage(vx_ctx* c, const vx_ba_plan* p, const BAArgs& a, int it) {
+    VX_HIP(c, launch(c, kStBaPose, k_pose_kf, dim3(p->n_kf * p->n_split), dim3(kPoseBlock), 0, c->stream, a, it));
+    return VX_OK;
+}
+
+int landmark_stage(vx_ctx* c, const vx_ba_plan* p, const BAArgs& a, int it, bool lds_poses) {
+    if (lds_poses) {
+        const size_t lds = landmark_solve_lds(p);
+        if (lds > 64 * 1024) {  // up to ~154 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
+            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            VX_HIP(c, attr);
+        }
+        VX_HIP(c, launch(c, kStBaLandmark, k_landmark_solve, dim3(p->n_lm_blocks), dim3(kLmBlock), (uint32_t)lds,
+                         c->stream, a, it));
+    } else {
+        ProfScope ps(c, kStBaLandmark);
+        hipLaunchKernelGGL(k_pose_solve_g, dim3((p->n_kf + 255) / 256), dim3(256), 0, c->stream, a, it);
+        VX_LAUNCH_CHECK(c, "k_pose_solve_g");
+        hipLaunchKernelGGL(k_landmark, dim3(std::max(1, (p->n_opt + 255) / 256)), dim3(256), 0, c->stream, a, it);
+        VX_LAUNCH_CHECK(c, "k_landmark");
+    }
+    return VX_OK;
+}
+
+int reset_if_no_iterations(vx_ctx* c, const vx_ba_plan* p, const BAArgs& a) {
+    if (p->opt.max_iterations != 0) return VX_OK;
+    ProfScope ps(c, kStBaReset);
+    const int n = std::max(p->n_kf * 8, std::max(p->n_lm, 1) * 4);
+    hipLaunchKernelGGL(k_ba_reset, dim3((n + 255) / 256), dim3(256), 0, c->stream, a);
+    VX_LAUNCH_CHECK(c, "k_ba_reset");
+    return VX_OK;
+}
+
+#ifndef VX_NO_RCCL
+// a sharded plan's kernel choice from the maxima over all ranks (once per plan: one small
+// all-reduce and a host synchronisation at its first run)
+int shard_kernel_choice(vx_ctx* c, vx_ba_plan* p) {
+    if (p->choice_made) return VX_OK;
+    const int32_t mine[2] = {p->n_lm_blocks, p->max_lm_obs};
+    DevBuf d;
+    VX_HIP(c, d.ensure(sizeof mine));
+    VX_HIP(c, hipMemcpyAsync(d.p, mine, sizeof mine, hipMemcpyHostToDevice, c->stream));
+    ncclResult_t r = ncclAllReduce(d.p, d.p, 2, ncclInt32, ncclMax, c->comm, c->stream);
+    if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+    int32_t all[2];
+    VX_HIP(c, hipMemcpyAsync(all, d.p, sizeof all, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    p->lds_poses = choose_lds_poses(p, all[0], all[1]);
+    p->choice_made = true;
+    return VX_OK;
+}
+#endif
+
 int plan_run(vx_ctx* c, vx_ba_plan* p) {
     if (p->status != 0) {
         p->ran = true;
         return VX_OK;
     }
     const bool sharded = p->shard_count > 1;
+    int rc;
     if (sharded) {
 #ifndef VX_NO_RCCL
         if (!c->comm || c->nranks != p->shard_count || c->rank != p->shard_rank)
             return set_error(c, VX_ERR_STATE, "sharded plan needs vx_comm_init(%d ranks)", p->shard_count);
+        if ((rc = shard_kernel_choice(c, p))) return rc;
 #else
         return set_error(c, VX_ERR_COMM, "built without RCCL");
 #endif
+    } else if (!p->choice_made) {
+        p->lds_poses = choose_lds_poses(p, p->n_lm_blocks, p->max_lm_obs);
+        p->choice_made = true;
     }
     const BAArgs a = make_args(p);
-    if (p->opt.max_iterations == 0) {
-        ProfScope ps(c, kStBaReset);
-        const int n = std::max(p->n_kf * 8, std::max(p->n_lm, 1) * 4);
-        hipLaunchKernelGGL(k_ba_reset, dim3((n + 255) / 256), dim3(256), 0, c->stream, a);
-        VX_LAUNCH_CHECK(c, "k_ba_reset");
-    }
-    // Every k_landmark_solve workgroup re-solves all window poses, so that redundancy grows as
-    // n_kf x workgroups: beyond the measured crossover (scripts/ba_window_sweep.py) the
-    // large-window kernels (poses solved once, one extra launch per iteration) are faster
-    const bool lds_poses = p->n_kf <= kMaxKfLds && !p->global_poses && (int64_t)p->n_kf * p->n_lm_blocks <= 80000 &&
-                           p->n_lm_blocks <= 480;
-    const size_t lds = (size_t)p->n_kf * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
-    if (lds_poses && lds > 64 * 1024) {  // up to ~154 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        VX_HIP(c, attr);
-    }
-    const int lm_blocks = std::max(1, (p->n_opt + 255) / 256);
+    if ((rc = reset_if_no_iterations(c, p, a))) return rc;
     for (int it = 0; it < p->opt.max_iterations; ++it) {
-        VX_HIP(c, launch(c, kStBaPose, k_pose_kf, dim3(p->n_kf * p->n_split), dim3(kPoseBlock), 0, c->stream, a, it));
+        if ((rc = pose_stage(c, p, a, it))) return rc;
 #ifndef VX_NO_RCCL
         if (sharded) {
             ProfScope ps(c, kStBaAllreduce);
@@ -794,19 +856,24 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
             if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
         }
 #endif
-        if (lds_poses) {
-            VX_HIP(c, launch(c, kStBaLandmark, k_landmark_solve, dim3(p->n_lm_blocks), dim3(kLmBlock), (uint32_t)lds,
-                             c->stream, a, it));
-        } else {
-            ProfScope ps(c, kStBaLandmark);
-            hipLaunchKernelGGL(k_pose_solve_g, dim3((p->n_kf + 255) / 256), dim3(256), 0, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_pose_solve_g");
-            hipLaunchKernelGGL(k_landmark, dim3(lm_blocks), dim3(256), 0, c->stream, a, it);
-            VX_LAUNCH_CHECK(c, "k_landmark");
-        }
+        if ((rc = landmark_stage(c, p, a, it, p->lds_poses))) return rc;
     }
     p->ran = true;
     return VX_OK;
+}
+
+// Test hook for the sharded path on one device: the element-wise sum of the shards' partial blocks
+// (in rank order) written back to every shard, in place of the per-iteration ncclAllReduce.
+constexpr int kMaxEmuShards = 16;
+struct PartPtrs {
+    double* p[kMaxEmuShards];
+};
+__global__ void k_sum_parts(PartPtrs parts, int n, long long len) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    double s = parts.p[0][i];
+    for (int r = 1; r < n; ++r) s += parts.p[r][i];
+    for (int r = 0; r < n; ++r) parts.p[r][i] = s;
 }
 
 }  // namespace
@@ -900,6 +967,51 @@ int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
     return graph_run_owned(c, p->graph, [](vx_ctx* cc, void* v) { return plan_run(cc, static_cast<vx_ba_plan*>(v)); }, p);
 }
 
+int vx_ba_shard_emulate_run(vx_ctx* c, vx_ba_plan* const* plans, int n) {
+    if (!c || !plans || n < 1 || n > kMaxEmuShards) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_shard_emulate_run: bad arguments") : VX_ERR_INVALID;
+    vx_ba_plan* p0 = plans[0];
+    for (int r = 0; r < n; ++r) {
+        const vx_ba_plan* p = plans[r];
+        if (!p || p->c != c || p->shard_count != n || p->shard_rank != r)
+            return set_error(c, VX_ERR_INVALID, "shard %d: plan of another context or shard layout", r);
+        if (p->status != p0->status || p->n_kf != p0->n_kf || p->n_split != p0->n_split ||
+            p->opt.max_iterations != p0->opt.max_iterations)
+            return set_error(c, VX_ERR_INVALID, "shard %d: plan built from another window", r);
+    }
+    if (p0->status != 0) {
+        for (int r = 0; r < n; ++r) plans[r]->ran = true;
+        return VX_OK;
+    }
+    // the kernel choice every rank would make from the all-reduced maxima
+    int blocks = 0, max_obs = 0;
+    for (int r = 0; r < n; ++r) {
+        blocks = std::max(blocks, plans[r]->n_lm_blocks);
+        max_obs = std::max(max_obs, plans[r]->max_lm_obs);
+    }
+    PartPtrs parts{};
+    std::vector<BAArgs> args(n);
+    for (int r = 0; r < n; ++r) {
+        plans[r]->lds_poses = choose_lds_poses(plans[r], blocks, max_obs);
+        plans[r]->choice_made = true;
+        parts.p[r] = plans[r]->kf_part.as<double>();
+        args[r] = make_args(plans[r]);
+    }
+    const long long len = (long long)p0->n_kf * p0->n_split * kStride;
+    int rc;
+    for (int r = 0; r < n; ++r)
+        if ((rc = reset_if_no_iterations(c, plans[r], args[r]))) return rc;
+    for (int it = 0; it < p0->opt.max_iterations; ++it) {
+        for (int r = 0; r < n; ++r)
+            if ((rc = pose_stage(c, plans[r], args[r], it))) return rc;
+        hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, c->stream, parts, n, len);
+        VX_LAUNCH_CHECK(c, "k_sum_parts");
+        for (int r = 0; r < n; ++r)
+            if ((rc = landmark_stage(c, plans[r], args[r], it, plans[r]->lds_poses))) return rc;
+    }
+    for (int r = 0; r < n; ++r) plans[r]->ran = true;
+    return VX_OK;
+}
+
 int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
     if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
@@ -973,7 +1085,8 @@ uint32_t vx_ba_shard_of(uint64_t lm_id, int shard_count) {
 
 int vx_ba_plan_info(const vx_ba_plan* p, int64_t* out8) {
     if (!p || !out8) return VX_ERR_INVALID;
-    const int64_t v[8] = {p->n_kf, p->n_lm, p->n_pose_obs, p->n_lm_obs, p->n_opt, p->n_split, p->n_lm_blocks, 0};
+    const int64_t v[8] = {p->n_kf, p->n_lm, p->n_pose_obs, p->n_lm_obs, p->n_opt, p->n_split, p->n_lm_blocks,
+                          p->max_lm_obs};
     for (int i = 0; i < 8; ++i) out8[i] = v[i];
     return VX_OK;
 }

@@ -19,6 +19,9 @@ struct vx_ba_plan {
     vx::DevBuf kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags, kf_obs_ptr, kf_part, kf_cost, lm_pos0, lm_pos,
         pobs_uv, pobs_lm, lobs_ptr, lobs_kf, lobs_lm, lm_blk, lobs_uv, state;
     int n_lm_blocks = 1;
+    int max_lm_obs = 0;         // most landmark-stage observations of one landmark
+    bool choice_made = false;   // kernel set decided (ba.hip choose_lds_poses; sharded: over all ranks)
+    bool lds_poses = true;
     bool ran = false;
     vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
     vx::DevBuf kf_map_dev, lm_map_dev;  // plans built from a vx_dmap: window row / slot -> map index
@@ -56,6 +59,6 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
 // the same plan from a device-resident map (vx_dmap; its CSR rebuilt first if stale)
 int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
 // greedy k_landmark_solve workgroup packing over the landmark-stage CSR pointers: {first landmark,
-// first observation} per workgroup, n_blocks + 1 pairs
-std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt);
+// first observation} per workgroup, n_blocks + 1 pairs; *max_cnt = most observations of one landmark
+std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt, int* max_cnt);
 }  // namespace vx

@@ -91,7 +91,7 @@ __device__ __forceinline__ int ht_find(const WinArgs& a, uint64_t key) {
 
 __global__ __launch_bounds__(kT) void k_ht_insert(WinArgs a) {
     const int l = blockIdx.x * kT + threadIdx.x;
-    if (l >= a.nl) return;
+    if (l >= a.nl || a.bad[l] == kLmRemoved) return;  // Map::RemoveLandmark: GetLandmark() == nullptr
     const uint64_t key = a.lid[l];
     unsigned h = (unsigned)mix(key) & a.hmask;
     for (;;) {
@@ -285,11 +285,16 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
                vx_ba_plan* p);
 
 // SelectKeyFrames (local_ba.cpp:42-62) over keyframe ids: newest `window` with id <= max_id, in
-// ascending id order (as indices into `ids`)
-std::vector<int> select_ids(const uint64_t* ids, int n, uint64_t ref_kf_id, int has_ref, int window_size) {
-    std::vector<int> order(n);
-    for (int i = 0; i < n; ++i) order[i] = i;
+// ascending id order (as indices into `ids`); `alive` (may be null) masks out removed keyframes
+std::vector<int> select_ids(const uint64_t* ids, int n, uint64_t ref_kf_id, int has_ref, int window_size,
+                            const uint8_t* alive = nullptr) {
+    std::vector<int> order;
+    order.reserve(n);
+    for (int i = 0; i < n; ++i)
+        if (!alive || alive[i]) order.push_back(i);
+    if (order.empty()) return {};
     std::sort(order.begin(), order.end(), [&](int x, int y) { return ids[x] < ids[y]; });
+    n = (int)order.size();
     const int window = std::max(1, window_size);
     const uint64_t max_id = has_ref ? ref_kf_id : ids[order.back()];
     std::vector<int> win;
@@ -485,7 +490,7 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     hipLaunchKernelGGL(k_lm_gather, dim3(grid(n_lm)), dim3(kT), 0, s, (const int*)inv, n_lm,
                        in.pos, p->lm_pos0.as<double>());
     VX_LAUNCH_CHECK(c, "plan fill kernels");
-    const std::vector<int> blk = pack_lm_blocks(lptr, n_opt);
+    const std::vector<int> blk = pack_lm_blocks(lptr, n_opt, &p->max_lm_obs);
     p->n_lm_blocks = (int)blk.size() / 2 - 1;
     if ((rc = up(c, p->lm_blk, blk.data(), blk.size()))) return rc;
     if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
@@ -537,7 +542,7 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
     p->n_landmarks_global = 0;
     const int n_kf = (int)m->kf_id.size();
     if (n_kf <= 0) return VX_OK;
-    const std::vector<int> win = select_ids(m->kf_id.data(), n_kf, ref_kf_id, has_ref, o.window_size);
+    const std::vector<int> win = select_ids(m->kf_id.data(), n_kf, ref_kf_id, has_ref, o.window_size, m->kf_alive.data());
     const int nk = (int)win.size();
     p->n_window_kf = nk;
     if (nk < 2) return VX_OK;

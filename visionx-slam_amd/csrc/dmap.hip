@@ -79,9 +79,10 @@ __global__ void k_iota(int* v, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) v[i] = (int)i;
 }
-__global__ void k_count(const int* keys, int64_t n, int* cnt) {
+// observations per landmark row; removed observations (kDeadObs) are not counted
+__global__ void k_count(const int* keys, int64_t n, int64_t nl, int* cnt) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&cnt[keys[i]], 1);
+    if (i < n && (unsigned)keys[i] < (unsigned long long)nl) atomicAdd(&cnt[keys[i]], 1);
 }
 // sorted order -> CSR payload; int32 prefix -> int64 pointers
 __global__ void k_csr_fill(const int* perm, int64_t n, const uint64_t* okf_in, const uint64_t* ofi_in,
@@ -112,8 +113,10 @@ int dmap_build_csr(vx_ctx* c, vx_dmap* m) {
         for (DevBuf* d : {&m->sort_keys, &m->sort_keys2, &m->sort_vals, &m->sort_vals2})
             VX_HIP(c, d->ensure((size_t)n * 4));
         hipLaunchKernelGGL(k_iota, dim3(grid(n)), dim3(kT), 0, s, m->sort_vals.as<int>(), n);
-        hipLaunchKernelGGL(k_count, dim3(grid(n)), dim3(kT), 0, s, m->obs_lm.as<int>(), n, cnt);
+        hipLaunchKernelGGL(k_count, dim3(grid(n)), dim3(kT), 0, s, m->obs_lm.as<int>(), n, nl, cnt);
         VX_LAUNCH_CHECK(c, "dmap csr count");
+        // (1 << bits) > nl: a removed observation's key (kDeadObs, all bits set) sorts after every
+        // live landmark row, so the CSR's first optr[nl] entries are exactly the live observations
         unsigned bits = 1;
         while ((1ll << bits) <= nl) ++bits;
         size_t bytes = 0;
@@ -174,6 +177,8 @@ int vx_dmap_add_keyframe(vx_dmap* m, uint64_t kf_id, const double* pose7, const 
     m->kf_id.push_back(kf_id);
     m->kf_feat_ptr.push_back(f0 + n_feat);
     m->kf_has_cam.push_back(has_cam ? 1 : 0);
+    m->kf_alive.push_back(1);
+    ++m->n_kf_live;
     m->kf_valid_cnt.push_back(valid);
     m->feat_flags.insert(m->feat_flags.end(), fl, fl + n_feat);
     return VX_OK;
@@ -183,9 +188,12 @@ int vx_dmap_add_landmarks(vx_dmap* m, int n, const uint64_t* id, const double* p
     if (!m) return VX_ERR_INVALID;
     vx_ctx* c = m->c;
     if (n < 0 || (n > 0 && (!id || !pos3))) return set_error(c, VX_ERR_INVALID, "vx_dmap_add_landmarks: bad arguments");
-    for (int i = 0; i < n; ++i)
-        if (m->lm_index.count(id[i]))
-            return set_error(c, VX_ERR_INVALID, "landmark %llu already in the map", (unsigned long long)id[i]);
+    {
+        std::unordered_map<uint64_t, int> batch;
+        for (int i = 0; i < n; ++i)
+            if (m->lm_index.count(id[i]) || !batch.emplace(id[i], i).second)
+                return set_error(c, VX_ERR_INVALID, "landmark %llu already in the map", (unsigned long long)id[i]);
+    }
     VX_HIP(c, hipSetDevice(c->device));
     std::vector<uint8_t> b(bad ? bad : nullptr, bad ? bad + n : nullptr);
     if (!bad) b.assign(n, 0);
@@ -195,6 +203,8 @@ int vx_dmap_add_landmarks(vx_dmap* m, int n, const uint64_t* id, const double* p
     if ((rc = append(c, m->lm_bad, m->n_lm, b.data(), n))) return rc;
     for (int i = 0; i < n; ++i) m->lm_index[id[i]] = (int)(m->n_lm + i);
     m->n_lm += n;
+    m->n_lm_live += n;
+    m->lm_obs_live.resize(m->n_lm, 0);
     m->csr_dirty = true;
     return VX_OK;
 }
@@ -211,14 +221,99 @@ int vx_dmap_add_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uin
             return set_error(c, VX_ERR_INVALID, "observation of unknown landmark %llu", (unsigned long long)lm_id[i]);
         li[i] = it->second;
     }
+    // observations_[keyframe_id] = feature_idx (landmark.h:32-35): a new pair is appended (in
+    // call order), a present one -- from an earlier call or earlier in this batch -- keeps its row
+    // and takes the new feature index
+    std::vector<int> a_lm;
+    std::vector<uint64_t> a_kf, a_fi;
+    std::vector<int64_t> w_row;
+    std::vector<uint64_t> w_fi;
+    for (int i = 0; i < n; ++i) {
+        const auto key = std::make_pair(li[i], kf_id[i]);
+        auto it = m->obs_index.find(key);
+        if (it == m->obs_index.end()) {
+            m->obs_index.emplace(key, m->n_obs + (int64_t)a_lm.size());
+            ++m->lm_obs_live[li[i]];
+            ++m->n_obs_live;
+            a_lm.push_back(li[i]);
+            a_kf.push_back(kf_id[i]);
+            a_fi.push_back(fi[i]);
+        } else if (it->second >= m->n_obs) {
+            a_fi[it->second - m->n_obs] = fi[i];
+        } else {
+            w_row.push_back(it->second);
+            w_fi.push_back(fi[i]);
+        }
+    }
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
-    if ((rc = append(c, m->obs_lm, m->n_obs, li.data(), n))) return rc;
-    if ((rc = append(c, m->obs_kf, m->n_obs, kf_id, n))) return rc;
-    if ((rc = append(c, m->obs_fi, m->n_obs, fi, n))) return rc;
-    m->n_obs += n;
+    const int64_t na = (int64_t)a_lm.size();
+    if ((rc = append(c, m->obs_lm, m->n_obs, a_lm.data(), na))) return rc;
+    if ((rc = append(c, m->obs_kf, m->n_obs, a_kf.data(), na))) return rc;
+    if ((rc = append(c, m->obs_fi, m->n_obs, a_fi.data(), na))) return rc;
+    if ((rc = scatter(c, m->obs_fi, w_row, w_fi.data(), 1))) return rc;
+    m->n_obs += na;
+    if (na || !w_row.empty()) m->csr_dirty = true;
+    return VX_OK;
+}
+
+int vx_dmap_remove_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uint64_t* kf_id) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && (!lm_id || !kf_id)))
+        return set_error(c, VX_ERR_INVALID, "vx_dmap_remove_observations: bad arguments");
+    std::vector<int> li(n);
+    for (int i = 0; i < n; ++i) {
+        auto it = m->lm_index.find(lm_id[i]);
+        if (it == m->lm_index.end())
+            return set_error(c, VX_ERR_INVALID, "unknown landmark %llu", (unsigned long long)lm_id[i]);
+        li[i] = it->second;
+    }
+    std::vector<int64_t> rows;
+    for (int i = 0; i < n; ++i) {
+        auto it = m->obs_index.find(std::make_pair(li[i], kf_id[i]));
+        if (it == m->obs_index.end()) continue;  // unordered_map::erase of an absent key
+        rows.push_back(it->second);
+        m->obs_index.erase(it);
+        --m->lm_obs_live[li[i]];
+        --m->n_obs_live;
+    }
+    if (rows.empty()) return VX_OK;
+    const std::vector<int> dead(rows.size(), kDeadObs);
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = scatter(c, m->obs_lm, rows, dead.data(), 1))) return rc;
     m->csr_dirty = true;
     return VX_OK;
+}
+
+int vx_dmap_remove_keyframe(vx_dmap* m, uint64_t kf_id) {
+    if (!m) return VX_ERR_INVALID;
+    auto it = m->kf_index.find(kf_id);
+    if (it == m->kf_index.end()) return set_error(m->c, VX_ERR_INVALID, "unknown keyframe %llu", (unsigned long long)kf_id);
+    m->kf_alive[it->second] = 0;
+    m->kf_index.erase(it);
+    --m->n_kf_live;
+    return VX_OK;
+}
+
+int vx_dmap_remove_landmarks(vx_dmap* m, int n, const uint64_t* lm_id) {
+    if (!m) return VX_ERR_INVALID;
+    vx_ctx* c = m->c;
+    if (n < 0 || (n > 0 && !lm_id)) return set_error(c, VX_ERR_INVALID, "vx_dmap_remove_landmarks: bad arguments");
+    std::vector<int64_t> rows;
+    for (int i = 0; i < n; ++i) {
+        auto it = m->lm_index.find(lm_id[i]);
+        if (it == m->lm_index.end()) continue;  // unordered_map::erase of an absent key
+        rows.push_back(it->second);
+        m->n_obs_live -= m->lm_obs_live[it->second];  // (its pairs can no longer be named: lm_index)
+        m->lm_index.erase(it);
+    }
+    if (rows.empty()) return VX_OK;
+    m->n_lm_live -= (int64_t)rows.size();
+    const std::vector<uint8_t> removed(rows.size(), kLmRemoved);
+    VX_HIP(c, hipSetDevice(c->device));
+    return scatter(c, m->lm_bad, rows, removed.data(), 1);
 }
 
 int vx_dmap_set_features(vx_dmap* m, uint64_t kf_id, int n, const int32_t* idx, const uint64_t* lm,
@@ -278,6 +373,15 @@ int vx_dmap_counts(const vx_dmap* m, int64_t* out4) {
     out4[1] = m->kf_feat_ptr.back();
     out4[2] = m->n_lm;
     out4[3] = m->n_obs;
+    return VX_OK;
+}
+
+int vx_dmap_live_counts(const vx_dmap* m, int64_t* out4) {
+    if (!m || !out4) return VX_ERR_INVALID;
+    out4[0] = m->n_kf_live;
+    out4[1] = m->n_lm_live;
+    out4[2] = m->n_obs_live;
+    out4[3] = 0;
     return VX_OK;
 }
 

@@ -16,10 +16,23 @@ struct vx_dmap {
     std::vector<uint64_t> kf_id;
     std::vector<int64_t> kf_feat_ptr{0};
     std::vector<uint8_t> kf_has_cam;
+    std::vector<uint8_t> kf_alive;               // 0 after Map::RemoveKeyFrame (row kept as dead storage)
     std::vector<int> kf_valid_cnt;
     std::vector<uint8_t> feat_flags;
-    std::unordered_map<uint64_t, int> kf_index, lm_index;
-    int64_t n_lm = 0, n_obs = 0;
+    std::unordered_map<uint64_t, int> kf_index, lm_index;  // live keyframes / landmarks only
+    // (landmark row, keyframe id) -> observation row of the live pair: Landmark::observations_ is
+    // keyed by keyframe id, so AddObservation of a present pair overwrites it in place and
+    // RemoveObservation tombstones it (obs_lm = kDeadObs: skipped by the CSR rebuild)
+    struct PairHash {
+        size_t operator()(const std::pair<int, uint64_t>& k) const {
+            uint64_t x = k.second * 0x9e3779b97f4a7c15ull ^ ((uint64_t)(uint32_t)k.first << 1);
+            return (size_t)(x ^ (x >> 29));
+        }
+    };
+    std::unordered_map<std::pair<int, uint64_t>, int64_t, PairHash> obs_index;
+    int64_t n_lm = 0, n_obs = 0;                 // rows (removed ones included)
+    int64_t n_kf_live = 0, n_lm_live = 0, n_obs_live = 0;
+    std::vector<int> lm_obs_live;                // live observations per landmark row
     // device arrays, insertion order, grown by doubling (used sizes from the counts above)
     vx::DevBuf kf_pose, kf_intr;                 // 7 / 4 doubles per keyframe
     vx::DevBuf feat_uv, feat_lm, feat_fl;        // 2 doubles / u64 / u8 per feature
@@ -32,6 +45,10 @@ struct vx_dmap {
 };
 
 namespace vx {
+// obs_lm of a removed observation: sorts after every live landmark row under the CSR's radix bits
+constexpr int kDeadObs = 0x7fffffff;
+// lm_bad value of a removed landmark (Map::RemoveLandmark): the plan build's landmark table skips it
+constexpr uint8_t kLmRemoved = 2;
 // stable landmark-major CSR of the observation list into m->optr / okf / ofi
 int dmap_build_csr(vx_ctx* c, vx_dmap* m);
 }  // namespace vx

@@ -84,6 +84,10 @@ EXPORTS = [
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
     "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts", "vx_create_ex", "vx_device_cus", "vx_ba_plan_create_ex",
+    "vx_dmap_create", "vx_dmap_add_keyframe", "vx_dmap_add_landmarks", "vx_dmap_add_observations",
+    "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
+    "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
+    "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
@@ -515,6 +519,12 @@ class Context:
         return SBAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
 
     # ---------------------------------------------------------------- multi-GPU
+    def ba_shard_emulate(self, plans):
+        """vx_ba_shard_emulate_run: the shard plans (rank r of len(plans)) run on this one device
+        as the ranks of a sharded LocalBA would, the all-reduce replaced by a rank-order sum."""
+        arr = (C.c_void_p * len(plans))(*[pl._h.value for pl in plans])
+        self._check(lib().vx_ba_shard_emulate_run(self._h, arr, len(plans)))
+
     @staticmethod
     def comm_unique_id() -> bytes:
         buf = (C.c_uint8 * 128)()
@@ -572,7 +582,7 @@ class BAPlan:
         out = np.zeros(8, np.int64)
         rc = lib().vx_ba_plan_info(self._h, _p(out))
         assert rc == 0
-        keys = ["n_kf", "n_lm", "n_pose_obs", "n_lm_obs", "n_opt", "n_split", "n_lm_blocks"]
+        keys = ["n_kf", "n_lm", "n_pose_obs", "n_lm_obs", "n_opt", "n_split", "n_lm_blocks", "max_lm_obs"]
         return {k: int(v) for k, v in zip(keys, out)}
 
     def run_async(self):
@@ -634,6 +644,26 @@ class DMap:
         k = np.ascontiguousarray(kf_ids, np.uint64)
         f = np.ascontiguousarray(feat_idx, np.uint64)
         self.ctx._check(lib().vx_dmap_add_observations(self._h, len(a), _p(a), _p(k), _p(f)))
+
+    def remove_observations(self, lm_ids, kf_ids):
+        """Landmark::RemoveObservation(kf_id) for each (landmark, keyframe) pair."""
+        a = np.ascontiguousarray(lm_ids, np.uint64)
+        k = np.ascontiguousarray(kf_ids, np.uint64)
+        self.ctx._check(lib().vx_dmap_remove_observations(self._h, len(a), _p(a), _p(k)))
+
+    def remove_keyframe(self, kf_id):
+        """Map::RemoveKeyFrame(id)."""
+        self.ctx._check(lib().vx_dmap_remove_keyframe(self._h, C.c_uint64(int(kf_id))))
+
+    def remove_landmarks(self, lm_ids):
+        """Map::RemoveLandmark(id) for each id."""
+        a = np.ascontiguousarray(lm_ids, np.uint64)
+        self.ctx._check(lib().vx_dmap_remove_landmarks(self._h, len(a), _p(a)))
+
+    def live_counts(self):
+        out = np.zeros(4, np.int64)
+        self.ctx._check(lib().vx_dmap_live_counts(self._h, _p(out)))
+        return dict(zip(["kf", "lm", "obs"], map(int, out[:3])))
 
     def set_features(self, kf_id, feat_idx, lm_ids, flags):
         i = np.ascontiguousarray(feat_idx, np.int32)
