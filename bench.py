@@ -37,7 +37,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HIP_KERNEL = {"orb_pyramid": "k_pyramid", "orb_fast_harris": "k_fast", "orb_select": "k_select",
               "orb_blur": "k_blur", "orb_describe": "k_describe", "match_partial": "k_knn_partial",
               "match_merge": "k_knn_merge+k_knn_compact", "ba_pose_partial": "k_pose_kf",
-              "ba_landmark": "k_landmark_solve"}
+              "ba_landmark": "k_landmark_solve", "ba_iter": "k_ba_iter", "ba_prologue": "k_ba_iter"}
 
 CONFIGS = {
     # name: (height, width, n_features, n_kf, n_lm)
@@ -83,6 +83,15 @@ def stage_bytes(stage, geo, counts):
         # 32 read, pose 64 + rotation 72 + cost 16 written (by workgroup 0)
         return (counts["n_lm_obs"] * 24 + counts["n_opt"] * 52 +
                 counts["n_kf"] * (counts["n_split"] * 232 + 96 + 152))
+    if stage == "ba_iter":
+        # one fused launch = one iteration: SURVEY §8(d)'s per-iteration bytes (pose stage: uv 16 +
+        # landmark slot 4 + landmark position 24 per observation; landmark stage: uv 16 + keyframe 4
+        # per observation; landmark position read + written; per keyframe pose 56, intrinsics 32,
+        # the 29-double normal-equation block) — 64 O + 48 LM + 320 KF with O split by stage
+        return (counts["n_pose_obs"] * 44 + counts["n_lm_obs"] * 20 + counts["n_opt"] * 48 +
+                counts["n_kf"] * 320)
+    if stage == "ba_prologue":  # iteration 0's pose stage
+        return counts["n_pose_obs"] * 44 + counts["n_kf"] * (56 + 32 + 232)
     return None
 
 

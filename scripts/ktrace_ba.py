@@ -44,6 +44,18 @@ def main():
     nk, nl, ns = synth.ba_config("C3")
     m = synth.make_ba_map(0x5EED0003, nk, nl)
     ctx = vxslam.Context(0)
+    # fused path (default): the traced launch is k_ba_iter(it = 1) of a 5-iteration run
+    plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk, iters=5))
+    print("plan", plan.info())
+    for _ in range(30):
+        plan.run_async()
+    ctx.synchronize()
+    report(read(), [0, 1, 2, 3, 4, 6, 7, 5],
+           "k_ba_iter (1 loads, 2 combine + totals + barrier, 3 pose solve + barrier, 4 landmark stage + barrier, "
+           "6 pose-stage entry, 7 its rounds, 5 pose stage of it + 1 done)")
+    plan.close()
+    # the two-kernel path (sharded plans, windows the fused layout does not fit)
+    os.environ["VX_BA_FUSED"] = "0"
     plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk, iters=1))
     print("plan", plan.info())
     for _ in range(30):

@@ -190,6 +190,46 @@ __global__ void k_ba_reset(BAArgs a) {
     }
 }
 
+// One pose-stage observation (local_ba.cpp:131-159) against pose T / intrinsics C, added to the 29
+// running terms v (21 H upper, 6 b, cost, count): projection with the z > 1e-6 check, the gate,
+// the Huber weight and the 2x6 PoseJacobian.
+__device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T, const double* C, D3 Pw, double2 uv,
+                                               double* v) {
+    const double fx = C[0], fy = C[1];
+    const D3 pc = se3_apply(T, Pw);
+    if (!(pc.z > 1e-6)) return;
+    const double inv_z = frcp(pc.z);
+    const double x = pc.x * inv_z, y = pc.y * inv_z;
+    const double e0 = uv.x - (fx * x + C[2]);
+    const double e1 = uv.y - (fy * y + C[3]);
+    const double e2 = e0 * e0 + e1 * e1;
+    const double re = e2 > 0.0 ? frsq(e2) : 0.0;
+    const double en = e2 * re;  // |e| without a sqrt + division on the chain
+    if (en > a.max_err) return;
+    const double w = en <= a.huber ? 1.0 : a.huber * re;
+    // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
+    // written out without its structural zeros (J0[1] = J1[0] = 0)
+    const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+    const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, jp0 * pc.z - jp2 * pc.x, -jp0 * pc.y};
+    const double J1[6] = {0.0, jp4, jp5, jp5 * pc.y - jp4 * pc.z, -jp5 * pc.x, jp4 * pc.x};
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) {
+            const bool u0 = r != 1 && c != 1, u1 = r != 0 && c != 0;  // compile-time after unroll
+            const double t0 = u0 ? (w * J0[r]) * J0[c] : 0.0;
+            const double t1 = u1 ? (w * J1[r]) * J1[c] : 0.0;
+            v[hidx(r, c)] += (u0 && u1) ? t0 + t1 : (u0 ? t0 : t1);
+        }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        const double g = r == 0 ? J0[0] * e0 : (r == 1 ? J1[1] * e1 : J0[r] * e0 + J1[r] * e1);
+        v[21 + r] -= w * g;
+    }
+    v[27] += w * (e0 * e0 + e1 * e1);
+    v[28] += 1.0;
+}
+
 // Pose stage (local_ba.cpp:116-161): n_split workgroups per keyframe, each over a contiguous
 // slice of the keyframe's observations.  Each thread accumulates the 29 terms of its observations
 // (strided) in registers; a fixed-order wave butterfly + LDS tree reduces them into the slice's
@@ -219,7 +259,6 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
     for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) C[j] = a.kf_intr[4 * k + j];
-    const double fx = C[0], fy = C[1];
     VX_KT(1);
     double v[kNTerms];
 #pragma unroll
@@ -232,38 +271,7 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
             const double* P = lm_in(a, it, a.pobs_lm[i]);
             Pw = {P[0], P[1], P[2]};
         }
-        const D3 pc = se3_apply(T, Pw);
-        if (!(pc.z > 1e-6)) continue;
-        const double inv_z = frcp(pc.z);
-        const double x = pc.x * inv_z, y = pc.y * inv_z;
-        const double e0 = uv.x - (fx * x + C[2]);
-        const double e1 = uv.y - (fy * y + C[3]);
-        const double e2 = e0 * e0 + e1 * e1;
-        const double re = e2 > 0.0 ? frsq(e2) : 0.0;
-        const double en = e2 * re;  // |e| without a sqrt + division on the chain
-        if (en > a.max_err) continue;
-        const double w = en <= a.huber ? 1.0 : a.huber * re;
-        // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
-        // written out without its structural zeros (J0[1] = J1[0] = 0)
-        const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
-        const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, jp0 * pc.z - jp2 * pc.x, -jp0 * pc.y};
-        const double J1[6] = {0.0, jp4, jp5, jp5 * pc.y - jp4 * pc.z, -jp5 * pc.x, jp4 * pc.x};
-#pragma unroll
-        for (int r = 0; r < 6; ++r)
-#pragma unroll
-            for (int c = r; c < 6; ++c) {
-                const bool u0 = r != 1 && c != 1, u1 = r != 0 && c != 0;  // compile-time after unroll
-                const double t0 = u0 ? (w * J0[r]) * J0[c] : 0.0;
-                const double t1 = u1 ? (w * J1[r]) * J1[c] : 0.0;
-                v[hidx(r, c)] += (u0 && u1) ? t0 + t1 : (u0 ? t0 : t1);
-            }
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-            const double g = r == 0 ? J0[0] * e0 : (r == 1 ? J1[1] * e1 : J0[r] * e0 + J1[r] * e1);
-            v[21 + r] -= w * g;
-        }
-        v[27] += w * (e0 * e0 + e1 * e1);
-        v[28] += 1.0;
+        pose_obs_accum(a, T, C, Pw, uv, v);
     }
     VX_KT(2);
     // wave reduction of the 29 terms (halving butterfly, wave_sum32)
@@ -343,7 +351,7 @@ __device__ __forceinline__ bool obs_terms(const BAArgs& a, D3 P, int k, double2 
 
 // Landmark update from its summed terms (local_ba.cpp:228-237): skipped below min_point_obs or
 // for a non-finite step; the position is written either way (iteration 0 reads lm_pos0).
-__device__ __forceinline__ void lm_update(const BAArgs& a, int l, D3 P, const double* h, int obs) {
+__device__ __forceinline__ D3 lm_update(const BAArgs& a, int l, D3 P, const double* h, int obs) {
     D3 out = P;
     if (obs >= a.min_point_obs) {
         double H[9] = {h[0] + 1e-6, h[1], h[2], h[1], h[3] + 1e-6, h[4], h[2], h[4], h[5] + 1e-6};
@@ -356,6 +364,7 @@ __device__ __forceinline__ void lm_update(const BAArgs& a, int l, D3 P, const do
     Pp[0] = out.x;
     Pp[1] = out.y;
     Pp[2] = out.z;
+    return out;
 }
 
 // Pose solve of every window keyframe (redundantly in each workgroup) + landmark stage, one launch.
@@ -525,6 +534,287 @@ __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
     lm_update(a, l, P, h, obs);
 }
 
+// ------------------------------------------------------------------ fused path: one launch per iteration
+// k_ba_iter(it) = combine + pose solve of iteration it, landmark stage of it, pose stage of it + 1.
+// Workgroups own whole landmarks in keyframe-locality order (plan: build_fused), so each needs the
+// poses of only the few keyframes its observations touch (kent: at most kFK entries).  After its
+// landmark stage a workgroup holds the iteration's poses (LDS) and its landmarks' new positions
+// (LDS), which is everything the next iteration's pose stage needs for the pose observations of
+// those landmarks (local_ba.cpp:131-159 at it + 1): it forms their 29 terms per keyframe (one wave
+// per keyframe entry, halving butterfly) into that keyframe's partial slot.  The next launch sums a
+// keyframe's slots in slot order — the same sum in every workgroup that needs the pose, so the
+// redundant solves agree bitwise — and every keyframe's pose is published by exactly one owner.
+// Pose observations of fixed landmarks (not optimised: positions constant) go to the owner of their
+// keyframe.  The prologue launch (kPro) forms iteration 0's pose stage from the initial state.
+constexpr int kFK = kBaFusedK;
+constexpr int kFT = kLmBlock;  // threads per fused workgroup
+constexpr int kFW = kFT / 64;  // waves per fused workgroup
+
+// Fused layout (ba.hip build_fused).  Per workgroup b: landmarks and landmark-stage observations at
+// the fixed bases b * kFT (padded), so their loads do not wait for the workgroup table; keyframe
+// entries at b * kFK; pose-stage observations in wave-major order — wave w takes entries w, w + kFW,
+// ..., each entry's observations start on a 64-aligned index (lane l of round r reads wstart + 64 r
+// + l), with fixed landmarks' positions stored in the observation record.
+struct FusedArgs {
+    const int4* blk;        // 1 + kFW / 2 per workgroup: {landmarks, landmark-stage observations,
+                            // keyframe entries, 0}, then {wstart, rounds} per wave
+    const int* lm_slot;     // [b * kFT + t] landmark slot (padding: slot 0)
+    const int2* lm_run;     // [b * kFT + t] its landmark-stage observations [r0, r1) (workgroup-local)
+    const double2* lobs_uv; // [b * kFT + t]
+    const int4* lobs_rec;   // [b * kFT + t] {keyframe entry, workgroup-local landmark, slot, 0}
+    const int4* kent;       // 2 per entry, kFK entries per workgroup: {row | owner << 30, or -1; slots of
+                            // the row; pose observations [start, end)}, {partial slot or -1, 0, 0, 0}
+    const double2* pobs_uv;
+    const double4* pobs_p;  // {x, y, z, code}: code >= 0 workgroup-local landmark (position from LDS),
+                            // code < 0 a fixed landmark at (x, y, z)
+    double* part;           // 2 x n_kf x maxl partial blocks of 32 doubles (row-major by keyframe): the
+                            // pose stage of iteration i fills buffer i & 1 (a launch reads one buffer
+                            // and writes the other, so no workgroup reads what another overwrites)
+    int maxl, n_part;
+};
+
+// LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), 9 x kFT
+// observation terms, kFT counted flags, 3 x kFT landmark positions, the block-0 totals
+constexpr size_t kFusedLds = (size_t)kFK * kLdsStride * sizeof(double) + (size_t)9 * kFT * sizeof(double) +
+                             (size_t)kFT * sizeof(int) + (size_t)3 * kFT * sizeof(double) +
+                             (size_t)2 * kFW * sizeof(double);
+static_assert(kFusedLds <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's 160 KB per workgroup");
+
+// trace build: phases of the it == 1 launch only (the last launch of a run has no pose stage)
+#define FKT(slot)                              \
+    do {                                       \
+        if (!kPro && it == 1) VX_KT(slot);     \
+    } while (0)
+
+template <bool kPro>
+__global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) {
+    if (!kPro && it > 0 && !a.state->active[it]) return;
+    extern __shared__ __attribute__((aligned(16))) double fl[];
+    double* kslot = fl;                                  // [kFK][kLdsStride]
+    double* terms = kslot + kFK * kLdsStride;            // [9][kFT]
+    int* tcount = reinterpret_cast<int*>(terms + 9 * kFT);
+    double* lpos = terms + 9 * kFT + kFT / 2;            // [kFT][3] (after kFT ints)
+    double* red = lpos + 3 * kFT;                        // [2][kFW]
+    const int tid = threadIdx.x, b = blockIdx.x, wv = tid >> 6, lane = tid & 63;
+    const size_t base = (size_t)b * kFT;
+    const int4* KE = f.kent + (size_t)b * kFK * 2;
+    const double* part_in = f.part + (size_t)(it & 1) * f.n_part * kStride;  // (unused by kPro)
+    double* part_out = f.part + (size_t)((it + 1) & 1) * f.n_part * kStride;
+    FKT(0);
+    // ---- every load the launch needs, issued up front (at most two dependent levels)
+    const int4 B = f.blk[(size_t)b * (1 + kFW / 2)];
+    const int4 WB = f.blk[(size_t)b * (1 + kFW / 2) + 1 + (wv >> 1)];
+    const int wstart = (wv & 1) ? WB.z : WB.x, wrounds = (wv & 1) ? WB.w : WB.y;
+    // (a) this thread's landmark-stage observation (padding rows are valid memory)
+    int4 orec = make_int4(0, 0, 0, 0);
+    double2 ouv = make_double2(1e300, 1e300);
+    D3 PO{0, 0, 0};
+    if (!kPro) {
+        orec = f.lobs_rec[base + tid];
+        ouv = f.lobs_uv[base + tid];
+        const double* P = lm_in(a, it, orec.z);
+        PO = {P[0], P[1], P[2]};
+    }
+    // (b) the landmark it owns
+    const int lslot = f.lm_slot[base + tid];
+    int2 run = make_int2(0, 0);
+    if (!kPro) run = f.lm_run[base + tid];
+    D3 PL;
+    {
+        const double* P = kPro ? a.lm_pos0 + 4 * (size_t)lslot : lm_in(a, it, lslot);
+        PL = {P[0], P[1], P[2]};
+    }
+    // (c) the keyframe entry it solves
+    int4 ke = make_int4(-1, 0, 0, 0);
+    double kT[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kC[4] = {0, 0, 0, 0};
+    int kflg = 0;
+    if (tid < kFK) {
+        ke = KE[2 * tid];
+        if (ke.x >= 0) {
+            const int row = ke.x & 0x3fffffff;
+            const double* Tin = kPro ? a.kf_pose0 : pose_in(a, it);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) kT[j] = Tin[8 * row + j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) kC[j] = a.kf_intr[4 * row + j];
+            kflg = a.kf_flags[row];
+        }
+    }
+    // (d) this wave's first two pose-stage rounds (rolling prefetch: round r + 2 is requested when
+    // round r is consumed)
+    const bool pose_next = kPro || it + 1 < a.max_iter;
+    const int4 pe = KE[2 * wv];
+    const int pdst = KE[2 * wv + 1].x;
+    double2 u0 = make_double2(0, 0), u1 = make_double2(0, 0);
+    double4 p0 = make_double4(0, 0, 0, 0), p1 = make_double4(0, 0, 0, 0);
+    if (pose_next && wrounds > 0) {
+        u0 = f.pobs_uv[wstart + lane];
+        p0 = f.pobs_p[wstart + lane];
+        if (wrounds > 1) {
+            u1 = f.pobs_uv[wstart + 64 + lane];
+            p1 = f.pobs_p[wstart + 64 + lane];
+        }
+    }
+    const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
+    const bool has_o = !kPro && tid < n_ob, own = tid < n_lm;
+    FKT(1);
+    if (!kPro) {
+        // ---- combine: S of entry j, term t = the row's partial slots summed in slot order
+        for (int pr = tid; pr < n_ent * kNTerms; pr += kFT) {
+            const int j = pr / kNTerms, t = pr - j * kNTerms;
+            const int4 e = KE[2 * j];
+            const double* src = part_in + ((size_t)(e.x & 0x3fffffff) * f.maxl) * kStride + t;
+            double acc = 0.0;
+            for (int i0 = 0; i0 < e.y; i0 += 16) {
+                double v[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) v[q] = i0 + q < e.y ? src[(size_t)(i0 + q) * kStride] : 0.0;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) acc += v[q];  // (+0.0 past the end: exact)
+            }
+            kslot[j * kLdsStride + t] = acc;
+        }
+        // ---- stop rule of iteration it (workgroup 0): totals over every partial slot
+        if (b == 0) {
+            double tot = 0.0, cnt = 0.0;
+            for (int q = tid; q < f.n_part; q += kFT) {
+                tot += part_in[(size_t)q * kStride + 27];
+                cnt += part_in[(size_t)q * kStride + 28];
+            }
+#pragma unroll
+            for (int m = 32; m > 0; m >>= 1) {
+                tot += __shfl_xor(tot, m, 64);
+                cnt += __shfl_xor(cnt, m, 64);
+            }
+            if (lane == 0) {
+                red[wv] = tot;
+                red[kFW + wv] = cnt;
+            }
+        }
+    }
+    __syncthreads();
+    FKT(2);
+    // ---- pose solve of the entries (local_ba.cpp:163-173); owners publish
+    if (ke.x >= 0) {
+        double* sl = kslot + tid * kLdsStride;
+        double T[8], R[9];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) T[j] = kT[j];
+        if (!kPro) {
+            double S[kNTerms];
+#pragma unroll
+            for (int t = 0; t < kNTerms; ++t) S[t] = sl[t];
+            solve_pose(a, kflg, S, T, R);
+            if (ke.x & (1 << 30)) {
+                double* Tout = pose_out(a, it) + 8 * (size_t)(ke.x & 0x3fffffff);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) Tout[j] = T[j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 9; ++j) R[j] = 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sl[j] = T[j];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) sl[8 + j] = R[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sl[17 + j] = kC[j];
+    }
+    if (!kPro && b == 0 && tid == 0) {
+        double tot = 0.0, cnt = 0.0;
+        for (int w2 = 0; w2 < kFW; ++w2) {
+            tot += red[w2];
+            cnt += red[kFW + w2];
+        }
+        stop_rule(a, it, tot, (int)cnt);
+    }
+    __syncthreads();
+    FKT(3);
+    // ---- landmark stage of iteration it (local_ba.cpp:176-238)
+    if (!kPro) {
+        double h[9];
+        const bool ok = obs_terms(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride, kslot + 17, kLdsStride, h);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) terms[j * kFT + tid] = h[j];
+        tcount[tid] = (has_o && ok) ? 1 : 0;
+        __syncthreads();
+        if (own) {
+            double hs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            int obs = 0;
+            for (int r = run.x; r < run.y; ++r) {
+#pragma unroll
+                for (int j = 0; j < 9; ++j) hs[j] += terms[j * kFT + r];
+                obs += tcount[r];
+            }
+            PL = lm_update(a, lslot, PL, hs, obs);
+        }
+    }
+    if (own) {
+        lpos[3 * tid] = PL.x;
+        lpos[3 * tid + 1] = PL.y;
+        lpos[3 * tid + 2] = PL.z;
+    }
+    __syncthreads();
+    FKT(4);
+    // ---- pose stage of iteration it + 1: wave wv takes entries wv, wv + kFW, ...
+    if (!pose_next) return;
+    int r = 0;
+    FKT(6);
+    for (int j = wv; j < n_ent; j += kFW) {
+        const int4 e = j == wv ? pe : KE[2 * j];
+        const int dst = j == wv ? pdst : KE[2 * j + 1].x;
+        const int nr = (e.w - e.z + 63) >> 6;
+        if (nr == 0) continue;
+        const double* T = kslot + j * kLdsStride;
+        const double* C = T + 17;
+        double v[kStride];
+#pragma unroll
+        for (int t = 0; t < kStride; ++t) v[t] = 0.0;
+        for (int q = 0; q < nr; ++q, ++r) {
+            const double2 uv = u0;
+            const double4 P4 = p0;
+            u0 = u1;
+            p0 = p1;
+            if (r + 2 < wrounds) {
+                u1 = f.pobs_uv[wstart + 64 * (r + 2) + lane];
+                p1 = f.pobs_p[wstart + 64 * (r + 2) + lane];
+            }
+            if (e.z + 64 * q + lane < e.w) {
+                const int code = (int)P4.w;
+                const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]}
+                                       : D3{P4.x, P4.y, P4.z};
+                pose_obs_accum(a, T, C, P, uv, v);
+            }
+        }
+        if (j == wv) FKT(7);
+        const double tot = wave_sum32(v);
+        if ((lane & 1) == 0) part_out[(size_t)dst * kStride + (lane >> 1)] = (lane >> 1) < kNTerms ? tot : 0.0;
+    }
+    FKT(5);
+}
+
+// fused-order observation payloads: uv by plan index (-1: padding), pose records with the fixed
+// landmarks' positions
+__global__ void k_fused_gather(const int* lsrc, int nl, const double2* luv, double2* out_luv, const int* psrc,
+                               const int* pcode, int np, const double2* puv, const double* lm_pos0, double2* out_puv,
+                               double4* out_pp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nl) out_luv[i] = lsrc[i] >= 0 ? luv[lsrc[i]] : make_double2(1e300, 1e300);
+    if (i < np) {
+        const int sidx = psrc[i], c = pcode[i];
+        out_puv[i] = sidx >= 0 ? puv[sidx] : make_double2(0.0, 0.0);
+        double4 P = make_double4(0.0, 0.0, 0.0, (double)c);
+        if (c < 0) {
+            const double* q = lm_pos0 + 4 * (size_t)(-1 - c);
+            P.x = q[0];
+            P.y = q[1];
+            P.z = q[2];
+        }
+        out_pp[i] = P;
+    }
+}
+
 
 }  // namespace
 }  // namespace vx
@@ -626,6 +916,224 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
     VX_HIP(c, p->kf_cost.ensure(nk * 2 * sizeof(double)));
     VX_HIP(c, p->lm_pos.ensure((size_t)std::max(p->n_lm, 1) * 4 * sizeof(double)));
     VX_HIP(c, p->state.ensure(sizeof(BAState)));
+    return VX_OK;
+}
+
+// The fused layout (k_ba_iter) from the plan's CSRs, on the host: both plan builders end here with
+// the same arrays, so the layout — and every run — is the same for both.
+//   1. optimised landmarks ordered by the first window keyframe that observes them (stable), so a
+//      workgroup's landmarks share few keyframes;
+//   2. greedy workgroups: at most kLmBlock landmarks, kLmBlock landmark-stage observations and kFK
+//      keyframes (those of its landmark-stage and pose-stage observations);
+//   3. each window keyframe owned by the first workgroup that touches it (untouched ones by
+//      workgroup 0): the owner publishes its pose and takes the pose observations of fixed
+//      landmarks in it;
+//   4. a workgroup's pose observations grouped by keyframe (ascending observation index inside,
+//      i.e. the plan's keyframe-major order), one partial slot per non-empty (workgroup, keyframe)
+//      group, numbered per keyframe in workgroup order.
+int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const std::vector<int>& plm,
+                const std::vector<int>& lptr, const std::vector<int>& lkf) {
+    p->fused = false;
+    if (p->status != 0 || p->shard_count > 1 || p->global_poses || p->n_kf > kMaxKfLds || p->n_opt <= 0) return VX_OK;
+    if (const char* e = getenv("VX_BA_FUSED"))
+        if (e[0] == '0') return VX_OK;
+    const int nk = p->n_kf, n_opt = p->n_opt, n_pose = kptr[nk];
+    std::vector<int> pkf(n_pose);
+    for (int k = 0; k < nk; ++k)
+        for (int o = kptr[k]; o < kptr[k + 1]; ++o) pkf[o] = k;
+    // pose observations per optimised slot (ascending)
+    std::vector<int> pp(n_opt + 1, 0), pidx;
+    for (int o = 0; o < n_pose; ++o)
+        if (plm[o] < n_opt) ++pp[plm[o] + 1];
+    for (int q = 0; q < n_opt; ++q) pp[q + 1] += pp[q];
+    pidx.resize(pp[n_opt]);
+    {
+        std::vector<int> w(pp.begin(), pp.end() - 1);
+        for (int o = 0; o < n_pose; ++o)
+            if (plm[o] < n_opt) pidx[w[plm[o]]++] = o;
+    }
+    // 1. keyframe-locality order (counting sort by first keyframe, stable)
+    std::vector<int> key(n_opt, nk), order(n_opt);
+    for (int q = 0; q < n_opt; ++q) {
+        int k0 = nk;
+        for (int o = lptr[q]; o < lptr[q + 1]; ++o) k0 = std::min(k0, lkf[o]);
+        for (int i = pp[q]; i < pp[q + 1]; ++i) k0 = std::min(k0, pkf[pidx[i]]);
+        key[q] = k0;
+    }
+    {
+        std::vector<int> kc(nk + 2, 0);
+        for (int q = 0; q < n_opt; ++q) ++kc[key[q] + 1];
+        for (int k = 0; k <= nk; ++k) kc[k + 1] += kc[k];
+        for (int q = 0; q < n_opt; ++q) order[kc[key[q]]++] = q;
+    }
+    // 2. greedy workgroups
+    std::vector<int> stamp(nk, -1), mark(nk, -1);
+    std::vector<std::vector<int>> K(1), LM(1);
+    int n_l = 0, n_o = 0, token = 0;
+    auto fresh = [&](int q, int blk) {  // keyframes of landmark q not yet in workgroup blk
+        ++token;
+        int n = 0;
+        auto see = [&](int k) {
+            if (stamp[k] != blk && mark[k] != token) {
+                mark[k] = token;
+                ++n;
+            }
+        };
+        for (int o = lptr[q]; o < lptr[q + 1]; ++o) see(lkf[o]);
+        for (int i = pp[q]; i < pp[q + 1]; ++i) see(pkf[pidx[i]]);
+        return n;
+    };
+    for (int idx = 0; idx < n_opt; ++idx) {
+        const int q = order[idx], cnt = lptr[q + 1] - lptr[q];
+        if (cnt > kLmBlock) return VX_OK;
+        int cur = (int)K.size() - 1;
+        int nn = fresh(q, cur);
+        if (n_l > 0 && (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock || (int)K[cur].size() + nn > kFK)) {
+            K.emplace_back();
+            LM.emplace_back();
+            ++cur;
+            n_l = n_o = 0;
+            nn = fresh(q, cur);
+        }
+        if (nn > kFK) return VX_OK;
+        auto add = [&](int k) {
+            if (stamp[k] != cur) {
+                stamp[k] = cur;
+                K[cur].push_back(k);
+            }
+        };
+        for (int o = lptr[q]; o < lptr[q + 1]; ++o) add(lkf[o]);
+        for (int i = pp[q]; i < pp[q + 1]; ++i) add(pkf[pidx[i]]);
+        LM[cur].push_back(q);
+        ++n_l;
+        n_o += cnt;
+    }
+    const int nb = (int)K.size();
+    // 3. owners
+    std::vector<int> owner(nk, -1);
+    for (int b = 0; b < nb; ++b)
+        for (int k : K[b])
+            if (owner[k] < 0) owner[k] = b;
+    for (int k = 0; k < nk; ++k)
+        if (owner[k] < 0) {
+            owner[k] = 0;
+            K[0].push_back(k);
+        }
+    if ((int)K[0].size() > kFK) return VX_OK;
+    for (auto& v : K) std::sort(v.begin(), v.end());
+    // 4. pose observations per workgroup (ascending observation index = keyframe-major)
+    std::vector<int> lm_blk(n_opt), lm_loc(n_opt);
+    for (int b = 0; b < nb; ++b)
+        for (int i = 0; i < (int)LM[b].size(); ++i) {
+            lm_blk[LM[b][i]] = b;
+            lm_loc[LM[b][i]] = i;
+        }
+    std::vector<std::vector<int>> PO(nb);
+    for (int o = 0; o < n_pose; ++o) PO[plm[o] < n_opt ? lm_blk[plm[o]] : owner[pkf[o]]].push_back(o);
+    // tables: landmarks / landmark-stage observations at b * kFT, keyframe entries at b * kFK,
+    // pose observations wave-major with 64-aligned entries
+    constexpr int kBlkInts = 4 * (1 + kFW / 2);
+    std::vector<int> blk((size_t)nb * kBlkInts, 0), lm_slot((size_t)nb * kFT, 0), lobs_src((size_t)nb * kFT, -1);
+    std::vector<int2> lm_run((size_t)nb * kFT, make_int2(0, 0));
+    std::vector<int4> lobs_rec((size_t)nb * kFT, make_int4(0, 0, 0, 0));
+    std::vector<int> kent((size_t)nb * kFK * 8, 0), loc(nk, -1), rank(nk, 0), pobs_src, pobs_code;
+    std::vector<int> ent_rank((size_t)nb * kFK, -1);  // per (workgroup, entry): its slot's rank in the row
+    pobs_src.reserve((size_t)n_pose + (size_t)nb * kFK * 64);
+    pobs_code.reserve(pobs_src.capacity());
+    std::vector<int> ent_beg(kFK), ent_end(kFK);
+    for (int b = 0; b < nb; ++b) {
+        for (int j = 0; j < (int)K[b].size(); ++j) loc[K[b][j]] = j;
+        int* B = &blk[(size_t)b * kBlkInts];
+        const size_t base = (size_t)b * kFT;
+        int ob = 0;
+        for (int t = 0; t < (int)LM[b].size(); ++t) {
+            const int q = LM[b][t];
+            lm_slot[base + t] = q;
+            lm_run[base + t].x = ob;
+            for (int o = lptr[q]; o < lptr[q + 1]; ++o, ++ob) {
+                lobs_src[base + ob] = o;
+                lobs_rec[base + ob] = make_int4(loc[lkf[o]], t, q, 0);
+            }
+            lm_run[base + t].y = ob;
+        }
+        B[0] = (int)LM[b].size();
+        B[1] = ob;
+        B[2] = (int)K[b].size();
+        // pose observations of each entry (PO[b] is keyframe-major: ascending observation index)
+        size_t i = 0;
+        for (int j = 0; j < (int)K[b].size(); ++j) {
+            ent_beg[j] = (int)i;
+            while (i < PO[b].size() && pkf[PO[b][i]] == K[b][j]) ++i;
+            ent_end[j] = (int)i;
+        }
+        if (i != PO[b].size()) return set_error(c, VX_ERR_STATE, "fused layout: pose observations out of keyframe order");
+        int* E = &kent[(size_t)b * kFK * 8];
+        for (int j = 0; j < kFK; ++j) {
+            E[8 * j] = -1;
+            E[8 * j + 4] = -1;
+        }
+        for (int w = 0; w < kFW; ++w) {
+            const int wstart = (int)pobs_src.size();
+            for (int j = w; j < (int)K[b].size(); j += kFW) {
+                const int k = K[b][j];
+                const int n = ent_end[j] - ent_beg[j];
+                E[8 * j] = k | (owner[k] == b ? (1 << 30) : 0);
+                E[8 * j + 2] = (int)pobs_src.size();
+                E[8 * j + 3] = (int)pobs_src.size() + n;
+                for (int x = ent_beg[j]; x < ent_end[j]; ++x) {
+                    const int o = PO[b][x];
+                    pobs_src.push_back(o);
+                    pobs_code.push_back(plm[o] < n_opt ? lm_loc[plm[o]] : -1 - plm[o]);
+                }
+                while (pobs_src.size() % 64) {  // pad to the next round
+                    pobs_src.push_back(-1);
+                    pobs_code.push_back(0);
+                }
+                if (n > 0) ent_rank[(size_t)b * kFK + j] = rank[k]++;
+            }
+            B[4 + 2 * w] = wstart;
+            B[4 + 2 * w + 1] = ((int)pobs_src.size() - wstart) / 64;
+        }
+        for (int k : K[b]) loc[k] = -1;
+    }
+    int maxl = 1;
+    for (int k = 0; k < nk; ++k) maxl = std::max(maxl, rank[k]);
+    for (int b = 0; b < nb; ++b)
+        for (int j = 0; j < (int)K[b].size(); ++j) {
+            int* E = &kent[((size_t)b * kFK + j) * 8];
+            const int k = K[b][j];
+            E[1] = rank[k];
+            const int r = ent_rank[(size_t)b * kFK + j];
+            E[4] = r >= 0 ? k * maxl + r : -1;
+        }
+    // upload + gather the observation payloads into the fused order
+    const int n_pp = (int)pobs_src.size(), n_lp = nb * kFT;
+    int rc;
+    if ((rc = upload(c, p->f_blk, blk))) return rc;
+    if ((rc = upload(c, p->f_lm_slot, lm_slot))) return rc;
+    if ((rc = upload(c, p->f_lm_run, lm_run))) return rc;
+    if ((rc = upload(c, p->f_lobs_rec, lobs_rec))) return rc;
+    if ((rc = upload(c, p->f_kent, kent))) return rc;
+    std::vector<int> idx(lobs_src);
+    idx.insert(idx.end(), pobs_src.begin(), pobs_src.end());
+    idx.insert(idx.end(), pobs_code.begin(), pobs_code.end());
+    if ((rc = upload(c, p->f_idx, idx))) return rc;
+    VX_HIP(c, p->f_lobs_uv.ensure((size_t)n_lp * sizeof(double2)));
+    VX_HIP(c, p->f_pobs_uv.ensure((size_t)std::max(n_pp, 1) * sizeof(double2)));
+    VX_HIP(c, p->f_pobs_p.ensure((size_t)std::max(n_pp, 1) * sizeof(double4)));
+    const int* d_idx = p->f_idx.as<int>();
+    hipLaunchKernelGGL(k_fused_gather, dim3((std::max(n_lp, n_pp) + 255) / 256), dim3(256), 0, c->stream, d_idx, n_lp,
+                       (const double2*)p->lobs_uv.as<double2>(), p->f_lobs_uv.as<double2>(), d_idx + n_lp,
+                       d_idx + n_lp + n_pp, n_pp, (const double2*)p->pobs_uv.as<double2>(),
+                       (const double*)p->lm_pos0.as<double>(), p->f_pobs_uv.as<double2>(), p->f_pobs_p.as<double4>());
+    VX_LAUNCH_CHECK(c, "k_fused_gather");
+    const size_t part_bytes = 2 * (size_t)nk * maxl * kStride * sizeof(double);
+    VX_HIP(c, p->f_part.ensure(part_bytes));
+    VX_HIP(c, hipMemsetAsync(p->f_part.p, 0, part_bytes, c->stream));  // slots no group writes stay 0
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    p->f_blocks = nb;
+    p->f_maxl = maxl;
+    p->fused = true;
     return VX_OK;
 }
 
@@ -753,7 +1261,8 @@ int build_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref,
     if ((rc = upload(c, p->lobs_lm, llm))) return rc;
     if ((rc = upload(c, p->lm_blk, blk))) return rc;
     if ((rc = upload(c, p->lobs_uv, luv))) return rc;
-    return alloc_run_buffers(c, p);
+    if ((rc = alloc_run_buffers(c, p))) return rc;
+    return build_fused(c, p, kf_obs_ptr, plm, lptr, lkf);
 }
 
 // Kernel set of a run.  Every k_landmark_solve workgroup re-solves all window poses, so that
@@ -825,10 +1334,52 @@ int shard_kernel_choice(vx_ctx* c, vx_ba_plan* p) {
 }
 #endif
 
+FusedArgs make_fused_args(vx_ba_plan* p) {
+    FusedArgs f{};
+    f.blk = p->f_blk.as<int4>();
+    f.lm_slot = p->f_lm_slot.as<int>();
+    f.lm_run = p->f_lm_run.as<int2>();
+    f.lobs_uv = p->f_lobs_uv.as<double2>();
+    f.lobs_rec = p->f_lobs_rec.as<int4>();
+    f.kent = p->f_kent.as<int4>();
+    f.pobs_uv = p->f_pobs_uv.as<double2>();
+    f.pobs_p = p->f_pobs_p.as<double4>();
+    f.part = p->f_part.as<double>();
+    f.maxl = p->f_maxl;
+    f.n_part = p->n_kf * p->f_maxl;
+    return f;
+}
+
+// the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration
+int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
+    static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<true>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLds);
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLds);
+    VX_HIP(c, a0);
+    VX_HIP(c, a1);
+    const BAArgs a = make_args(p);
+    const FusedArgs f = make_fused_args(p);
+    int rc;
+    if ((rc = reset_if_no_iterations(c, p, a))) return rc;
+    if (p->opt.max_iterations == 0) return VX_OK;
+    VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true>, dim3(p->f_blocks), dim3(kFT), (uint32_t)kFusedLds, c->stream,
+                     a, f, -1));
+    for (int it = 0; it < p->opt.max_iterations; ++it)
+        VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false>, dim3(p->f_blocks), dim3(kFT), (uint32_t)kFusedLds, c->stream,
+                         a, f, it));
+    return VX_OK;
+}
+
 int plan_run(vx_ctx* c, vx_ba_plan* p) {
     if (p->status != 0) {
         p->ran = true;
         return VX_OK;
+    }
+    if (p->fused && p->shard_count == 1) {
+        const int rc = plan_run_fused(c, p);
+        if (!rc) p->ran = true;
+        return rc;
     }
     const bool sharded = p->shard_count > 1;
     int rc;

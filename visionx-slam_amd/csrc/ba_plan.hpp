@@ -27,6 +27,13 @@ struct vx_ba_plan {
     vx::DevBuf kf_map_dev, lm_map_dev;  // plans built from a vx_dmap: window row / slot -> map index
     bool from_dmap = false;
     bool global_poses = false;  // VX_PLAN_GLOBAL_POSES
+    // fused path (one k_ba_iter launch per iteration, ba.hip build_fused): landmark workgroups in
+    // keyframe-locality order, each with its keyframe table (kent), its landmark-stage observations
+    // and the pose-stage observations of its landmarks grouped by keyframe; per-keyframe partial
+    // slots (n_kf x f_maxl x 32 doubles) summed in slot order by every workgroup that needs the pose
+    bool fused = false;
+    int f_blocks = 0, f_maxl = 0;
+    vx::DevBuf f_blk, f_lm_slot, f_lm_run, f_lobs_uv, f_lobs_rec, f_kent, f_pobs_uv, f_pobs_p, f_part, f_idx;
 };
 
 struct vx_dmap;
@@ -54,6 +61,12 @@ inline int ba_split(int64_t mx, int shard_count) {
 }
 
 int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p);
+// the fused layout from the plan's CSRs (host copies: kf_obs_ptr n_kf + 1, pose-observation landmark
+// slots, landmark-stage pointers n_opt + 1 and keyframe rows); p->fused stays false when a window
+// does not fit it (sharded plans, a workgroup needing more than kBaFusedK keyframes)
+int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kf_obs_ptr, const std::vector<int>& plm,
+                const std::vector<int>& lptr, const std::vector<int>& lkf);
+constexpr int kBaFusedK = 64;      // keyframes per fused workgroup
 // SelectKeyFrames + landmark set + both CSRs built on the device from the map snapshot (§8f rank 2)
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
 // the same plan from a device-resident map (vx_dmap; its CSR rebuilt first if stale)

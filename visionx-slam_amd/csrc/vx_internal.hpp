@@ -49,6 +49,8 @@ enum Stage : int {
     kStPnpRefine,
     kStEmHyp,
     kStEmSelect,
+    kStBaIter,        // fused LocalBA iteration (k_ba_iter)
+    kStBaPrologue,    // iteration 0's pose stage of the fused path
     kStCount
 };
 
