@@ -215,6 +215,9 @@ def main():
                          "(vx_set_grid_share; default 1/3 with more than one stream, 1 otherwise)")
     ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
                     help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
+    ap.add_argument("--extract-ctx", type=int, default=2, choices=(1, 2),
+                    help="extraction contexts (with --streams 3): frames alternate between them, so the "
+                         "extraction of frame t+1 overlaps frame t's; Match and LocalBA stay in frame order")
     args = ap.parse_args()
 
     dist = Dist(args.gpus)
@@ -232,13 +235,16 @@ def main():
         k = max(1, int(round(1.0 / args.ba_cus)))
         ba_mask = [i for i in range(ncu) if i % k == k - 1]
         fe_mask = [i for i in range(ncu) if i % k != k - 1]
-    ectx = vxslam.Context(dist.local_rank, cu_mask=fe_mask)
+    n_ex = args.extract_ctx if args.streams == 3 else 1
+    ectxs = [vxslam.Context(dist.local_rank, cu_mask=fe_mask) for _ in range(n_ex)]
+    ectx = ectxs[0]
     mctx = ectx if args.streams < 3 else vxslam.Context(dist.local_rank, cu_mask=fe_mask)
     bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank, cu_mask=ba_mask)
-    ctxs = list({id(c): c for c in (ectx, mctx, bctx)}.values())
+    ctxs = list({id(c): c for c in ectxs + [mctx, bctx]}.values())
     # extraction runs beside the previous frame's LocalBA: its pyramid grid leaves CUs free for it
     grid_share = args.grid_share if args.grid_share else (1.0 / 3.0 if args.streams > 1 else 1.0)
-    ectx.set_grid_share(grid_share)
+    for c in ectxs:
+        c.set_grid_share(grid_share)
     cfg = CONFIGS[args.config]
     h, w, nf, nk, nl = cfg
     N = dist.world
@@ -264,30 +270,39 @@ def main():
     plan_build_ms = float(np.median(plan_ms))
     torch.cuda.synchronize()
 
-    # Pipeline.  Frame t: Extract(t) on ectx into slot t % 3, Match(t - 1, t) on mctx, LocalBA(t) on
-    # bctx, ordered on the device by events: Match(t) after Extract(t), LocalBA(t) after Match(t),
-    # and Extract(t) after Match(t - 2) (the last reader of the slot it overwrites).  Nothing of
-    # frame t + 1 depends on Match(t) or LocalBA(t), so consecutive frames' stages overlap; with
-    # --streams 1 the same calls run back to back on one stream.
-    ev_e = ectx.event()
-    ev_m = [mctx.event() for _ in range(3)]
+    # Pipeline.  Frame t: Extract(t) on extraction context t % E (E = --extract-ctx) into that
+    # context's slot (t // E) % 3, Match(t - 1, t) on mctx, LocalBA(t) on bctx, ordered on the device
+    # by events: Match(t) after Extract(t), LocalBA(t) after Match(t) (so Match and LocalBA run in
+    # frame order), and Extract(t) after Match(t - 3E + 1) (the last reader of the slot it
+    # overwrites).  Nothing of frame t + 1 depends on Match(t) or LocalBA(t), so consecutive frames'
+    # stages overlap, and with E = 2 so do two frames' extractions (frames are independent there);
+    # with --streams 1 the same calls run back to back on one stream.
+    E = n_ex
+    ev_e = [c.event() for c in ectxs]
+    ev_m = [mctx.event() for _ in range(4 * E)]
+
+    def loc(i):  # (extraction context, slot) of frame i
+        return i % E, (i // E) % 3
 
     def extract(i):
         f = frames_dev[i % args.frames]
-        ectx.orb_extract_async(f.data_ptr(), w, h, 3, w * 3, i % 3, params)
+        ci, si = loc(i)
+        ectxs[ci].orb_extract_async(f.data_ptr(), w, h, 3, w * 3, si, params)
 
-    for i in (-3, -2, -1):  # fill the three slots (frame -1 is step 0's previous frame)
+    for i in range(-3 * E, 0):  # fill every slot (frame -1 is step 0's previous frame)
         extract(i)
-    slot = [ectx.slot_device(s) for s in range(3)]
+    slot = {(ci, si): ectxs[ci].slot_device(si) for ci in range(E) for si in range(3)}
 
     def step(i):
-        ectx.wait_event(ev_m[(i + 1) % 3])  # (an event not yet recorded is an immediate no-op)   # Match(i - 2) done with slot i % 3
+        ci, si = loc(i)
+        ex = ectxs[ci]
+        ex.wait_event(ev_m[(i - 3 * E + 1) % (4 * E)])  # (an event not yet recorded is an immediate no-op)
         extract(i)
-        ectx.record(ev_e)
-        mctx.wait_event(ev_e)
-        mctx.match_device_async(slot[(i - 1) % 3], slot[i % 3])
-        mctx.record(ev_m[i % 3])
-        bctx.wait_event(ev_m[i % 3])
+        ex.record(ev_e[ci])
+        mctx.wait_event(ev_e[ci])
+        mctx.match_device_async(slot[loc(i - 1)], slot[loc(i)])
+        mctx.record(ev_m[i % (4 * E)])
+        bctx.wait_event(ev_m[i % (4 * E)])
         plan.run_async()
 
     def sync():
@@ -332,7 +347,8 @@ def main():
     latency_ms = 1e3 * float(np.median(lat))
 
     # counts for the byte formulas
-    kps, _ = ectx.orb_fetch((args.warmup + args.steps + 19) % 3)
+    last = args.warmup + args.steps + 19
+    kps, _ = ectxs[loc(last)[0]].orb_fetch(loc(last)[1])
     matches = mctx.match_fetch()
     st = plan.fetch(None)
     lw = [int(round(w / 1.2 ** l)) for l in range(8)]
@@ -399,8 +415,9 @@ def main():
                 "parallelism": f"frames: 1 per rank; BA: landmark shards x{N}" + (" + RCCL all-reduce" if N > 1 else ""),
                 "streams": {1: "1: Extract, Match, LocalBA back to back",
                             2: "2: Extract+Match | LocalBA (LocalBA(t) after Match(t))",
-                            3: "3: Extract | Match | LocalBA, device events (Match(t) after Extract(t), "
-                               "LocalBA(t) after Match(t), Extract(t) after Match(t-2))"}[args.streams],
+                            3: f"{2 + E}: Extract x{E} (frames alternate) | Match | LocalBA, device events "
+                               f"(Match(t) after Extract(t), LocalBA(t) after Match(t): Match and LocalBA in "
+                               f"frame order; Extract(t) after the last Match reading its slot)"}[args.streams],
                 "ba_window_kf": nk * N,
                 "ba_landmarks": nl * N,
                 "orb_features": nf,
@@ -418,7 +435,7 @@ def main():
         }
         print(json.dumps(out), flush=True)
     plan.close()
-    for e in [ev_e] + ev_m:
+    for e in ev_e + ev_m:
         e.close()
     for c in reversed(ctxs):
         c.close()

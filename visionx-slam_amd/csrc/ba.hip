@@ -547,8 +547,10 @@ __global__ __launch_bounds__(256) void k_landmark(BAArgs a, int it) {
 // Pose observations of fixed landmarks (not optimised: positions constant) go to the owner of their
 // keyframe.  The prologue launch (kPro) forms iteration 0's pose stage from the initial state.
 constexpr int kFK = kBaFusedK;
-constexpr int kFT = kLmBlock;  // threads per fused workgroup
-constexpr int kFW = kFT / 64;  // waves per fused workgroup
+// Threads per fused workgroup (= its landmark-stage observation / landmark capacity): 512, or 1024
+// for windows whose 512-thread packing needs more workgroups than the device has CUs (fewer,
+// larger workgroups: shorter per-keyframe slot lists; measured).
+constexpr int kFTSmall = 512, kFTLarge = 1024;
 
 // Fused layout (ba.hip build_fused).  Per workgroup b: landmarks and landmark-stage observations at
 // the fixed bases b * kFT (padded), so their loads do not wait for the workgroup table; keyframe
@@ -573,12 +575,15 @@ struct FusedArgs {
     int maxl, n_part;
 };
 
-// LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), 9 x kFT
-// observation terms, kFT counted flags, 3 x kFT landmark positions, the block-0 totals
-constexpr size_t kFusedLds = (size_t)kFK * kLdsStride * sizeof(double) + (size_t)9 * kFT * sizeof(double) +
-                             (size_t)kFT * sizeof(int) + (size_t)3 * kFT * sizeof(double) +
-                             (size_t)2 * kFW * sizeof(double);
-static_assert(kFusedLds <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's 160 KB per workgroup");
+// LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), kFK loaded
+// entry states (T 8 | C 4 | flags), 9 x kFT observation terms, kFT counted flags, 3 x kFT landmark
+// positions, the block-0 totals
+constexpr int kTStride = 13;
+constexpr size_t fused_lds(int ft) {
+    return (size_t)kFK * (kLdsStride + kTStride) * sizeof(double) + (size_t)9 * ft * sizeof(double) +
+           (size_t)ft * sizeof(int) + (size_t)3 * ft * sizeof(double) + (size_t)2 * (ft / 64) * sizeof(double);
+}
+static_assert(fused_lds(kFTLarge) <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's 160 KB per workgroup");
 
 // trace build: phases of the it == 1 launch only (the last launch of a run has no pose stage)
 #define FKT(slot)                              \
@@ -586,12 +591,14 @@ static_assert(kFusedLds <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's 160 KB pe
         if (!kPro && it == 1) VX_KT(slot);     \
     } while (0)
 
-template <bool kPro>
+template <bool kPro, int kFT>
 __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) {
+    constexpr int kFW = kFT / 64;  // waves per workgroup
     if (!kPro && it > 0 && !a.state->active[it]) return;
     extern __shared__ __attribute__((aligned(16))) double fl[];
     double* kslot = fl;                                  // [kFK][kLdsStride]
-    double* terms = kslot + kFK * kLdsStride;            // [9][kFT]
+    double* tslot = kslot + kFK * kLdsStride;            // [kFK][kTStride]
+    double* terms = tslot + kFK * kTStride;              // [9][kFT]
     int* tcount = reinterpret_cast<int*>(terms + 9 * kFT);
     double* lpos = terms + 9 * kFT + kFT / 2;            // [kFT][3] (after kFT ints)
     double* red = lpos + 3 * kFT;                        // [2][kFW]
@@ -601,21 +608,19 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     const double* part_in = f.part + (size_t)(it & 1) * f.n_part * kStride;  // (unused by kPro)
     double* part_out = f.part + (size_t)((it + 1) & 1) * f.n_part * kStride;
     FKT(0);
-    // ---- every load the launch needs, issued up front (at most two dependent levels)
+    // ---- every load the launch needs, issued up front (at most two dependent levels); values
+    // needed only after the first barrier are parked in LDS, not held in registers
     const int4 B = f.blk[(size_t)b * (1 + kFW / 2)];
     const int4 WB = f.blk[(size_t)b * (1 + kFW / 2) + 1 + (wv >> 1)];
     const int wstart = (wv & 1) ? WB.z : WB.x, wrounds = (wv & 1) ? WB.w : WB.y;
     // (a) this thread's landmark-stage observation (padding rows are valid memory)
     int4 orec = make_int4(0, 0, 0, 0);
     double2 ouv = make_double2(1e300, 1e300);
-    D3 PO{0, 0, 0};
     if (!kPro) {
         orec = f.lobs_rec[base + tid];
         ouv = f.lobs_uv[base + tid];
-        const double* P = lm_in(a, it, orec.z);
-        PO = {P[0], P[1], P[2]};
     }
-    // (b) the landmark it owns
+    // (b) the landmark it owns (its position goes to LDS for the observations of the landmark)
     const int lslot = f.lm_slot[base + tid];
     int2 run = make_int2(0, 0);
     if (!kPro) run = f.lm_run[base + tid];
@@ -624,39 +629,38 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         const double* P = kPro ? a.lm_pos0 + 4 * (size_t)lslot : lm_in(a, it, lslot);
         PL = {P[0], P[1], P[2]};
     }
-    // (c) the keyframe entry it solves
+    // (c) the keyframe entry it solves: previous pose, intrinsics, flags -> tslot
     int4 ke = make_int4(-1, 0, 0, 0);
-    double kT[8] = {0, 0, 0, 0, 0, 0, 0, 0}, kC[4] = {0, 0, 0, 0};
-    int kflg = 0;
     if (tid < kFK) {
         ke = KE[2 * tid];
         if (ke.x >= 0) {
             const int row = ke.x & 0x3fffffff;
-            const double* Tin = kPro ? a.kf_pose0 : pose_in(a, it);
+            const double* Tin = (kPro ? a.kf_pose0 : pose_in(a, it)) + 8 * (size_t)row;
+            double* ts = tslot + tid * kTStride;
+            double v[12];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) kT[j] = Tin[8 * row + j];
+            for (int j = 0; j < 8; ++j) v[j] = Tin[j];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) kC[j] = a.kf_intr[4 * row + j];
-            kflg = a.kf_flags[row];
+            for (int j = 0; j < 4; ++j) v[8 + j] = a.kf_intr[4 * row + j];
+            const int flg = a.kf_flags[row];
+#pragma unroll
+            for (int j = 0; j < 12; ++j) ts[j] = v[j];
+            ts[12] = (double)flg;
         }
     }
-    // (d) this wave's first two pose-stage rounds (rolling prefetch: round r + 2 is requested when
-    // round r is consumed)
+    // (d) this wave's first pose-stage round (round r + 1 is requested when round r is consumed)
     const bool pose_next = kPro || it + 1 < a.max_iter;
-    const int4 pe = KE[2 * wv];
-    const int pdst = KE[2 * wv + 1].x;
-    double2 u0 = make_double2(0, 0), u1 = make_double2(0, 0);
-    double4 p0 = make_double4(0, 0, 0, 0), p1 = make_double4(0, 0, 0, 0);
+    double2 u0 = make_double2(0, 0);
+    double4 p0 = make_double4(0, 0, 0, 0);
     if (pose_next && wrounds > 0) {
         u0 = f.pobs_uv[wstart + lane];
         p0 = f.pobs_p[wstart + lane];
-        if (wrounds > 1) {
-            u1 = f.pobs_uv[wstart + 64 + lane];
-            p1 = f.pobs_p[wstart + 64 + lane];
-        }
     }
     const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
     const bool has_o = !kPro && tid < n_ob, own = tid < n_lm;
+    lpos[3 * tid] = PL.x;
+    lpos[3 * tid + 1] = PL.y;
+    lpos[3 * tid + 2] = PL.z;
     FKT(1);
     if (!kPro) {
         // ---- combine: S of entry j, term t = the row's partial slots summed in slot order
@@ -697,14 +701,17 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // ---- pose solve of the entries (local_ba.cpp:163-173); owners publish
     if (ke.x >= 0) {
         double* sl = kslot + tid * kLdsStride;
-        double T[8], R[9];
+        const double* ts = tslot + tid * kTStride;
+        double T[8], R[9], C[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) T[j] = kT[j];
+        for (int j = 0; j < 8; ++j) T[j] = ts[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) C[j] = ts[8 + j];
         if (!kPro) {
             double S[kNTerms];
 #pragma unroll
             for (int t = 0; t < kNTerms; ++t) S[t] = sl[t];
-            solve_pose(a, kflg, S, T, R);
+            solve_pose(a, (int)ts[12], S, T, R);
             if (ke.x & (1 << 30)) {
                 double* Tout = pose_out(a, it) + 8 * (size_t)(ke.x & 0x3fffffff);
 #pragma unroll
@@ -719,7 +726,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
 #pragma unroll
         for (int j = 0; j < 9; ++j) sl[8 + j] = R[j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sl[17 + j] = kC[j];
+        for (int j = 0; j < 4; ++j) sl[17 + j] = C[j];
     }
     if (!kPro && b == 0 && tid == 0) {
         double tot = 0.0, cnt = 0.0;
@@ -734,6 +741,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // ---- landmark stage of iteration it (local_ba.cpp:176-238)
     if (!kPro) {
         double h[9];
+        const D3 PO{lpos[3 * orec.y], lpos[3 * orec.y + 1], lpos[3 * orec.y + 2]};
         const bool ok = obs_terms(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride, kslot + 17, kLdsStride, h);
 #pragma unroll
         for (int j = 0; j < 9; ++j) terms[j * kFT + tid] = h[j];
@@ -748,22 +756,20 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 obs += tcount[r];
             }
             PL = lm_update(a, lslot, PL, hs, obs);
+            lpos[3 * tid] = PL.x;
+            lpos[3 * tid + 1] = PL.y;
+            lpos[3 * tid + 2] = PL.z;
         }
+        __syncthreads();
     }
-    if (own) {
-        lpos[3 * tid] = PL.x;
-        lpos[3 * tid + 1] = PL.y;
-        lpos[3 * tid + 2] = PL.z;
-    }
-    __syncthreads();
     FKT(4);
     // ---- pose stage of iteration it + 1: wave wv takes entries wv, wv + kFW, ...
     if (!pose_next) return;
     int r = 0;
     FKT(6);
     for (int j = wv; j < n_ent; j += kFW) {
-        const int4 e = j == wv ? pe : KE[2 * j];
-        const int dst = j == wv ? pdst : KE[2 * j + 1].x;
+        const int4 e = KE[2 * j];
+        const int dst = KE[2 * j + 1].x;
         const int nr = (e.w - e.z + 63) >> 6;
         if (nr == 0) continue;
         const double* T = kslot + j * kLdsStride;
@@ -774,11 +780,9 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         for (int q = 0; q < nr; ++q, ++r) {
             const double2 uv = u0;
             const double4 P4 = p0;
-            u0 = u1;
-            p0 = p1;
-            if (r + 2 < wrounds) {
-                u1 = f.pobs_uv[wstart + 64 * (r + 2) + lane];
-                p1 = f.pobs_p[wstart + 64 * (r + 2) + lane];
+            if (r + 1 < wrounds) {
+                u0 = f.pobs_uv[wstart + 64 * (r + 1) + lane];
+                p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
             }
             if (e.z + 64 * q + lane < e.w) {
                 const int code = (int)P4.w;
@@ -923,7 +927,7 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
 // the same arrays, so the layout — and every run — is the same for both.
 //   1. optimised landmarks ordered by the first window keyframe that observes them (stable), so a
 //      workgroup's landmarks share few keyframes;
-//   2. greedy workgroups: at most kLmBlock landmarks, kLmBlock landmark-stage observations and kFK
+//   2. greedy workgroups: at most ft landmarks, ft landmark-stage observations and kFK
 //      keyframes (those of its landmark-stage and pose-stage observations);
 //   3. each window keyframe owned by the first workgroup that touches it (untouched ones by
 //      workgroup 0): the owner publishes its pose and takes the pose observations of fixed
@@ -966,49 +970,66 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         for (int k = 0; k <= nk; ++k) kc[k + 1] += kc[k];
         for (int q = 0; q < n_opt; ++q) order[kc[key[q]]++] = q;
     }
-    // 2. greedy workgroups
+    // 2. greedy workgroups of ft threads (cap: landmark-stage observations and landmarks per
+    // workgroup; VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps)
+    if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
+    std::vector<std::vector<int>> K, LM;
+    int ft = kFTSmall;
+    int token = 0;
     std::vector<int> stamp(nk, -1), mark(nk, -1);
-    std::vector<std::vector<int>> K(1), LM(1);
-    int n_l = 0, n_o = 0, token = 0;
-    auto fresh = [&](int q, int blk) {  // keyframes of landmark q not yet in workgroup blk
-        ++token;
-        int n = 0;
-        auto see = [&](int k) {
-            if (stamp[k] != blk && mark[k] != token) {
-                mark[k] = token;
-                ++n;
-            }
+    const char* env_ft = getenv("VX_BA_FUSED_THREADS");
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        if (env_ft) ft = atoi(env_ft) == kFTLarge ? kFTLarge : kFTSmall;
+        else if (attempt == 1) ft = kFTLarge;
+        int cap = ft;
+        if (const char* e = getenv("VX_BA_FUSED_CAP")) cap = std::min(ft, std::max(64, atoi(e)));
+        std::fill(stamp.begin(), stamp.end(), -1);
+        K.assign(1, {});
+        LM.assign(1, {});
+        int n_l = 0, n_o = 0;
+        auto fresh = [&](int q, int blk) {  // keyframes of landmark q not yet in workgroup blk
+            ++token;
+            int n = 0;
+            auto see = [&](int k) {
+                if (stamp[k] != blk && mark[k] != token) {
+                    mark[k] = token;
+                    ++n;
+                }
+            };
+            for (int o = lptr[q]; o < lptr[q + 1]; ++o) see(lkf[o]);
+            for (int i = pp[q]; i < pp[q + 1]; ++i) see(pkf[pidx[i]]);
+            return n;
         };
-        for (int o = lptr[q]; o < lptr[q + 1]; ++o) see(lkf[o]);
-        for (int i = pp[q]; i < pp[q + 1]; ++i) see(pkf[pidx[i]]);
-        return n;
-    };
-    for (int idx = 0; idx < n_opt; ++idx) {
-        const int q = order[idx], cnt = lptr[q + 1] - lptr[q];
-        if (cnt > kLmBlock) return VX_OK;
-        int cur = (int)K.size() - 1;
-        int nn = fresh(q, cur);
-        if (n_l > 0 && (n_l + 1 > kLmBlock || n_o + cnt > kLmBlock || (int)K[cur].size() + nn > kFK)) {
-            K.emplace_back();
-            LM.emplace_back();
-            ++cur;
-            n_l = n_o = 0;
-            nn = fresh(q, cur);
+        for (int idx = 0; idx < n_opt; ++idx) {
+            const int q = order[idx], cnt = lptr[q + 1] - lptr[q];
+            if (cnt > ft) return VX_OK;
+            int cur = (int)K.size() - 1;
+            int nn = fresh(q, cur);
+            if (n_l > 0 && (n_l + 1 > cap || n_o + cnt > cap || (int)K[cur].size() + nn > kFK)) {
+                K.emplace_back();
+                LM.emplace_back();
+                ++cur;
+                n_l = n_o = 0;
+                nn = fresh(q, cur);
+            }
+            if (nn > kFK) return VX_OK;
+            auto add = [&](int k) {
+                if (stamp[k] != cur) {
+                    stamp[k] = cur;
+                    K[cur].push_back(k);
+                }
+            };
+            for (int o = lptr[q]; o < lptr[q + 1]; ++o) add(lkf[o]);
+            for (int i = pp[q]; i < pp[q + 1]; ++i) add(pkf[pidx[i]]);
+            LM[cur].push_back(q);
+            ++n_l;
+            n_o += cnt;
         }
-        if (nn > kFK) return VX_OK;
-        auto add = [&](int k) {
-            if (stamp[k] != cur) {
-                stamp[k] = cur;
-                K[cur].push_back(k);
-            }
-        };
-        for (int o = lptr[q]; o < lptr[q + 1]; ++o) add(lkf[o]);
-        for (int i = pp[q]; i < pp[q + 1]; ++i) add(pkf[pidx[i]]);
-        LM[cur].push_back(q);
-        ++n_l;
-        n_o += cnt;
+        // more 512-thread workgroups than compute units: repack into 1024-thread ones
+        if (env_ft || ft == kFTLarge || (int)K.size() <= c->n_cus) break;
     }
     const int nb = (int)K.size();
+    const int fw = ft / 64;
     // 3. owners
     std::vector<int> owner(nk, -1);
     for (int b = 0; b < nb; ++b)
@@ -1030,12 +1051,12 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         }
     std::vector<std::vector<int>> PO(nb);
     for (int o = 0; o < n_pose; ++o) PO[plm[o] < n_opt ? lm_blk[plm[o]] : owner[pkf[o]]].push_back(o);
-    // tables: landmarks / landmark-stage observations at b * kFT, keyframe entries at b * kFK,
+    // tables: landmarks / landmark-stage observations at b * ft, keyframe entries at b * kFK,
     // pose observations wave-major with 64-aligned entries
-    constexpr int kBlkInts = 4 * (1 + kFW / 2);
-    std::vector<int> blk((size_t)nb * kBlkInts, 0), lm_slot((size_t)nb * kFT, 0), lobs_src((size_t)nb * kFT, -1);
-    std::vector<int2> lm_run((size_t)nb * kFT, make_int2(0, 0));
-    std::vector<int4> lobs_rec((size_t)nb * kFT, make_int4(0, 0, 0, 0));
+    const int kBlkInts = 4 * (1 + fw / 2);
+    std::vector<int> blk((size_t)nb * kBlkInts, 0), lm_slot((size_t)nb * ft, 0), lobs_src((size_t)nb * ft, -1);
+    std::vector<int2> lm_run((size_t)nb * ft, make_int2(0, 0));
+    std::vector<int4> lobs_rec((size_t)nb * ft, make_int4(0, 0, 0, 0));
     std::vector<int> kent((size_t)nb * kFK * 8, 0), loc(nk, -1), rank(nk, 0), pobs_src, pobs_code;
     std::vector<int> ent_rank((size_t)nb * kFK, -1);  // per (workgroup, entry): its slot's rank in the row
     pobs_src.reserve((size_t)n_pose + (size_t)nb * kFK * 64);
@@ -1044,7 +1065,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     for (int b = 0; b < nb; ++b) {
         for (int j = 0; j < (int)K[b].size(); ++j) loc[K[b][j]] = j;
         int* B = &blk[(size_t)b * kBlkInts];
-        const size_t base = (size_t)b * kFT;
+        const size_t base = (size_t)b * ft;
         int ob = 0;
         for (int t = 0; t < (int)LM[b].size(); ++t) {
             const int q = LM[b][t];
@@ -1072,9 +1093,9 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             E[8 * j] = -1;
             E[8 * j + 4] = -1;
         }
-        for (int w = 0; w < kFW; ++w) {
+        for (int w = 0; w < fw; ++w) {
             const int wstart = (int)pobs_src.size();
-            for (int j = w; j < (int)K[b].size(); j += kFW) {
+            for (int j = w; j < (int)K[b].size(); j += fw) {
                 const int k = K[b][j];
                 const int n = ent_end[j] - ent_beg[j];
                 E[8 * j] = k | (owner[k] == b ? (1 << 30) : 0);
@@ -1107,7 +1128,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             E[4] = r >= 0 ? k * maxl + r : -1;
         }
     // upload + gather the observation payloads into the fused order
-    const int n_pp = (int)pobs_src.size(), n_lp = nb * kFT;
+    const int n_pp = (int)pobs_src.size(), n_lp = nb * ft;
     int rc;
     if ((rc = upload(c, p->f_blk, blk))) return rc;
     if ((rc = upload(c, p->f_lm_slot, lm_slot))) return rc;
@@ -1133,6 +1154,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     VX_HIP(c, hipStreamSynchronize(c->stream));
     p->f_blocks = nb;
     p->f_maxl = maxl;
+    p->f_threads = ft;
     p->fused = true;
     return VX_OK;
 }
@@ -1351,11 +1373,13 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
 }
 
 // the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration
-int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
-    static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<true>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLds);
-    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFusedLds);
+template <int kFT>
+int plan_run_fused_t(vx_ctx* c, vx_ba_plan* p) {
+    constexpr int lds = (int)fused_lds(kFT);
+    static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<true, kFT>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false, kFT>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     VX_HIP(c, a0);
     VX_HIP(c, a1);
     const BAArgs a = make_args(p);
@@ -1363,12 +1387,17 @@ int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
     int rc;
     if ((rc = reset_if_no_iterations(c, p, a))) return rc;
     if (p->opt.max_iterations == 0) return VX_OK;
-    VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true>, dim3(p->f_blocks), dim3(kFT), (uint32_t)kFusedLds, c->stream,
+    VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
                      a, f, -1));
     for (int it = 0; it < p->opt.max_iterations; ++it)
-        VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false>, dim3(p->f_blocks), dim3(kFT), (uint32_t)kFusedLds, c->stream,
+        VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
                          a, f, it));
     return VX_OK;
+}
+
+// the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration
+int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
+    return p->f_threads == kFTLarge ? plan_run_fused_t<kFTLarge>(c, p) : plan_run_fused_t<kFTSmall>(c, p);
 }
 
 int plan_run(vx_ctx* c, vx_ba_plan* p) {

@@ -32,7 +32,7 @@ struct vx_ba_plan {
     // and the pose-stage observations of its landmarks grouped by keyframe; per-keyframe partial
     // slots (n_kf x f_maxl x 32 doubles) summed in slot order by every workgroup that needs the pose
     bool fused = false;
-    int f_blocks = 0, f_maxl = 0;
+    int f_blocks = 0, f_maxl = 0, f_threads = 512;
     vx::DevBuf f_blk, f_lm_slot, f_lm_run, f_lobs_uv, f_lobs_rec, f_kent, f_pobs_uv, f_pobs_p, f_part, f_idx;
 };
 
