@@ -79,6 +79,7 @@ struct BAArgs {
     int n_kf, n_opt, n_lm, pad0;
     int min_pose_obs, min_point_obs, max_iter, n_split;
     double huber, max_err;
+    double huber2, max_err2;     // squared thresholds (gates on |e|^2)
     const double* kf_pose0;  // 8 per KF: qx qy qz qw tx ty tz 0
     double* kf_pose;         // 2 x n_kf x 8: ping-pong by iteration parity (see pose_in / pose_out)
     const double* kf_intr;   // 4 per KF
@@ -190,43 +191,92 @@ __global__ void k_ba_reset(BAArgs a) {
     }
 }
 
-// One pose-stage observation (local_ba.cpp:131-159) against pose T / intrinsics C, added to the 29
-// running terms v (21 H upper, 6 b, cost, count): projection with the z > 1e-6 check, the gate,
-// the Huber weight and the 2x6 PoseJacobian.
-__device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T, const double* C, D3 Pw, double2 uv,
-                                               double* v) {
+// Camera-frame point of pose (R, t) (T_cw * p, projection.h:16): R p + t as three FMA chains (the
+// rotation matrix of the pose's quaternion, Eigen toRotationMatrix, instead of Eigen's quaternion
+// _transformVector: the same map up to rounding, a third of the dependent depth).
+__device__ __forceinline__ D3 rt_apply(const double* R, const double* t, D3 p) {
+    return {fma(R[2], p.z, fma(R[1], p.y, fma(R[0], p.x, t[0]))), fma(R[5], p.z, fma(R[4], p.y, fma(R[3], p.x, t[1]))),
+            fma(R[8], p.z, fma(R[7], p.y, fma(R[6], p.x, t[2])))};
+}
+
+// One pose-stage observation (local_ba.cpp:131-159) against pose T (rotation R) / intrinsics C,
+// added to the 29 running terms v (21 H upper, 6 b, cost, count): projection with the z > 1e-6
+// check, the gate, the Huber weight and the 2x6 PoseJacobian.  The gate and the Huber switch compare
+// |e|^2 with max_reproj_error^2 / huber_delta^2, so 1 / |e| (v_rsq) is only evaluated for
+// observations beyond huber_delta; |e| > max_err <=> |e|^2 > max_err^2 up to rounding at the
+// boundary (the parity tests keep inputs away from it).
+template <bool kFma = true>
+__device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T, const double* R, const double* C,
+                                               D3 Pw, double2 uv, double* v) {
     const double fx = C[0], fy = C[1];
-    const D3 pc = se3_apply(T, Pw);
+    // (!kFma: the quaternion form, 7 live doubles instead of 12 — the 1024-thread kernel's budget)
+    const D3 pc = kFma ? rt_apply(R, T + 4, Pw) : se3_apply(T, Pw);
     if (!(pc.z > 1e-6)) return;
     const double inv_z = frcp(pc.z);
     const double x = pc.x * inv_z, y = pc.y * inv_z;
     const double e0 = uv.x - (fx * x + C[2]);
     const double e1 = uv.y - (fy * y + C[3]);
     const double e2 = e0 * e0 + e1 * e1;
-    const double re = e2 > 0.0 ? frsq(e2) : 0.0;
-    const double en = e2 * re;  // |e| without a sqrt + division on the chain
-    if (en > a.max_err) return;
-    const double w = en <= a.huber ? 1.0 : a.huber * re;
+    double w = 1.0;
+    if constexpr (kFma) {
+        if (e2 > a.max_err2) return;
+        if (e2 > a.huber2) w = a.huber * frsq(e2);
+    } else {  // (the round-1 form: |e| by v_rsq, branch-free weight)
+        const double re = e2 > 0.0 ? frsq(e2) : 0.0;
+        const double en = e2 * re;
+        if (en > a.max_err) return;
+        w = en <= a.huber ? 1.0 : a.huber * re;
+    }
     // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
     // written out without its structural zeros (J0[1] = J1[0] = 0)
     const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
-    const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, jp0 * pc.z - jp2 * pc.x, -jp0 * pc.y};
-    const double J1[6] = {0.0, jp4, jp5, jp5 * pc.y - jp4 * pc.z, -jp5 * pc.x, jp4 * pc.x};
+    const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, fma(jp0, pc.z, -jp2 * pc.x), -jp0 * pc.y};
+    const double J1[6] = {0.0, jp4, jp5, fma(jp5, pc.y, -jp4 * pc.z), -jp5 * pc.x, jp4 * pc.x};
+    if constexpr (!kFma) {  // products then sums: fewer live registers (the 1024-thread kernel's budget)
+#pragma unroll
+        for (int r = 0; r < 6; ++r)
+#pragma unroll
+            for (int c = r; c < 6; ++c) {
+                const bool u0 = r != 1 && c != 1, u1 = r != 0 && c != 0;  // compile-time after unroll
+                const double t0 = u0 ? (w * J0[r]) * J0[c] : 0.0;
+                const double t1 = u1 ? (w * J1[r]) * J1[c] : 0.0;
+                v[hidx(r, c)] += (u0 && u1) ? t0 + t1 : (u0 ? t0 : t1);
+            }
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const double g = r == 0 ? J0[0] * e0 : (r == 1 ? J1[1] * e1 : J0[r] * e0 + J1[r] * e1);
+            v[21 + r] -= w * g;
+        }
+        v[27] += w * e2;
+        v[28] += 1.0;
+        return;
+    }
+    // w J^T J, -w J^T e and w |e|^2 accumulated as FMA chains (the FP64 issue rate bounds this loop,
+    // ~2 FMAs per term instead of 2 products and 2 sums)
+    double wJ0[6], wJ1[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        wJ0[r] = w * J0[r];
+        wJ1[r] = w * J1[r];
+    }
 #pragma unroll
     for (int r = 0; r < 6; ++r)
 #pragma unroll
         for (int c = r; c < 6; ++c) {
             const bool u0 = r != 1 && c != 1, u1 = r != 0 && c != 0;  // compile-time after unroll
-            const double t0 = u0 ? (w * J0[r]) * J0[c] : 0.0;
-            const double t1 = u1 ? (w * J1[r]) * J1[c] : 0.0;
-            v[hidx(r, c)] += (u0 && u1) ? t0 + t1 : (u0 ? t0 : t1);
+            double acc = v[hidx(r, c)];
+            if (u0) acc = fma(wJ0[r], J0[c], acc);
+            if (u1) acc = fma(wJ1[r], J1[c], acc);
+            v[hidx(r, c)] = acc;
         }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        const double g = r == 0 ? J0[0] * e0 : (r == 1 ? J1[1] * e1 : J0[r] * e0 + J1[r] * e1);
-        v[21 + r] -= w * g;
+        double acc = v[21 + r];
+        if (r != 1) acc = fma(-wJ0[r], e0, acc);
+        if (r != 0) acc = fma(-wJ1[r], e1, acc);
+        v[21 + r] = acc;
     }
-    v[27] += w * (e0 * e0 + e1 * e1);
+    v[27] = fma(w, e2, v[27]);
     v[28] += 1.0;
 }
 
@@ -254,11 +304,12 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
         P0 = {P[0], P[1], P[2]};
     }
     const double* Tin = pose_in(a, it);
-    double T[8], C[4];
+    double T[8], C[4], R[9];
 #pragma unroll
     for (int j = 0; j < 8; ++j) T[j] = Tin[8 * k + j];
 #pragma unroll
     for (int j = 0; j < 4; ++j) C[j] = a.kf_intr[4 * k + j];
+    rot_from_quat(T, R);
     VX_KT(1);
     double v[kNTerms];
 #pragma unroll
@@ -271,7 +322,7 @@ __global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
             const double* P = lm_in(a, it, a.pobs_lm[i]);
             Pw = {P[0], P[1], P[2]};
         }
-        pose_obs_accum(a, T, C, Pw, uv, v);
+        pose_obs_accum(a, T, R, C, Pw, uv, v);
     }
     VX_KT(2);
     // wave reduction of the 29 terms (halving butterfly, wave_sum32)
@@ -312,11 +363,13 @@ __device__ __forceinline__ double combine_term(const BAArgs& a, int k, int t) {
 // (local_ba.cpp:206-224) against keyframe k of tables T/R/C (strides in doubles), branch-free:
 // returns false for a gated-out observation (behind the camera or beyond max_reproj_error),
 // whose terms are then exactly +0.0.
+template <bool kFma = true>
 __device__ __forceinline__ bool obs_terms(const BAArgs& a, D3 P, int k, double2 uv, const double* T0, int tst,
                                           const double* R0, int rst, const double* C0, int cst, double* h) {
     const double* T = T0 + (long long)tst * k;
     const double* C = C0 + (long long)cst * k;
-    const D3 pc = se3_apply(T, P);
+    const double* R = R0 + (long long)rst * k;
+    const D3 pc = kFma ? rt_apply(R, T + 4, P) : se3_apply(T, P);
     const bool front = pc.z > 1e-6;
     const double inv_z = frcp(pc.z);
     const double x = pc.x * inv_z, y = pc.y * inv_z;
@@ -324,28 +377,51 @@ __device__ __forceinline__ bool obs_terms(const BAArgs& a, D3 P, int k, double2 
     const double e0 = uv.x - (fx * x + C[2]);
     const double e1 = uv.y - (fy * y + C[3]);
     const double e2 = e0 * e0 + e1 * e1;
-    const double re = e2 > 0.0 ? frsq(e2) : 0.0;
-    const double en = e2 * re;
-    const bool ok = front && !(en > a.max_err);
-    const double w = en <= a.huber ? 1.0 : a.huber * re;
+    const bool ok = front && !(e2 > a.max_err2);  // (squared gate, see pose_obs_accum)
+    double w = 1.0;
+    if (e2 > a.huber2) w = a.huber * frsq(e2);
     const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
-    const double* R = R0 + (long long)rst * k;
-    // J = Jp * R with Jp's structural zeros dropped (local_ba.cpp:219-221)
-    double J0[3], J1[3];
+    // J = Jp * R with Jp's structural zeros dropped (local_ba.cpp:219-221); the 9 terms as FMAs with
+    // w folded into one factor (a gated-out observation gets w = 0: its terms are exactly +0.0 as
+    // long as J and e are finite, and they are selected to 0 below regardless)
+    if constexpr (!kFma) {
+        double J0[3], J1[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            J0[c] = jp0 * R[c] + jp2 * R[6 + c];
+            J1[c] = jp4 * R[3 + c] + jp5 * R[6 + c];
+        }
+        h[0] = ok ? (w * J0[0]) * J0[0] + (w * J1[0]) * J1[0] : 0.0;
+        h[1] = ok ? (w * J0[0]) * J0[1] + (w * J1[0]) * J1[1] : 0.0;
+        h[2] = ok ? (w * J0[0]) * J0[2] + (w * J1[0]) * J1[2] : 0.0;
+        h[3] = ok ? (w * J0[1]) * J0[1] + (w * J1[1]) * J1[1] : 0.0;
+        h[4] = ok ? (w * J0[1]) * J0[2] + (w * J1[1]) * J1[2] : 0.0;
+        h[5] = ok ? (w * J0[2]) * J0[2] + (w * J1[2]) * J1[2] : 0.0;
+        h[6] = ok ? w * ((-J0[0]) * e0 + (-J1[0]) * e1) : 0.0;
+        h[7] = ok ? w * ((-J0[1]) * e0 + (-J1[1]) * e1) : 0.0;
+        h[8] = ok ? w * ((-J0[2]) * e0 + (-J1[2]) * e1) : 0.0;
+        return ok;
+    }
+    double J0[3], J1[3], wJ0[3], wJ1[3];
+    const double wv = ok ? w : 0.0;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        J0[c] = jp0 * R[c] + jp2 * R[6 + c];
-        J1[c] = jp4 * R[3 + c] + jp5 * R[6 + c];
+        J0[c] = fma(jp0, R[c], jp2 * R[6 + c]);
+        J1[c] = fma(jp4, R[3 + c], jp5 * R[6 + c]);
+        wJ0[c] = wv * J0[c];
+        wJ1[c] = wv * J1[c];
     }
-    h[0] = ok ? (w * J0[0]) * J0[0] + (w * J1[0]) * J1[0] : 0.0;
-    h[1] = ok ? (w * J0[0]) * J0[1] + (w * J1[0]) * J1[1] : 0.0;
-    h[2] = ok ? (w * J0[0]) * J0[2] + (w * J1[0]) * J1[2] : 0.0;
-    h[3] = ok ? (w * J0[1]) * J0[1] + (w * J1[1]) * J1[1] : 0.0;
-    h[4] = ok ? (w * J0[1]) * J0[2] + (w * J1[1]) * J1[2] : 0.0;
-    h[5] = ok ? (w * J0[2]) * J0[2] + (w * J1[2]) * J1[2] : 0.0;
-    h[6] = ok ? w * ((-J0[0]) * e0 + (-J1[0]) * e1) : 0.0;
-    h[7] = ok ? w * ((-J0[1]) * e0 + (-J1[1]) * e1) : 0.0;
-    h[8] = ok ? w * ((-J0[2]) * e0 + (-J1[2]) * e1) : 0.0;
+    h[0] = fma(wJ0[0], J0[0], wJ1[0] * J1[0]);
+    h[1] = fma(wJ0[0], J0[1], wJ1[0] * J1[1]);
+    h[2] = fma(wJ0[0], J0[2], wJ1[0] * J1[2]);
+    h[3] = fma(wJ0[1], J0[1], wJ1[1] * J1[1]);
+    h[4] = fma(wJ0[1], J0[2], wJ1[1] * J1[2]);
+    h[5] = fma(wJ0[2], J0[2], wJ1[2] * J1[2]);
+    h[6] = fma(-wJ0[0], e0, -wJ1[0] * e1);
+    h[7] = fma(-wJ0[1], e0, -wJ1[1] * e1);
+    h[8] = fma(-wJ0[2], e0, -wJ1[2] * e1);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) h[j] = ok ? h[j] : 0.0;
     return ok;
 }
 
@@ -718,8 +794,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 for (int j = 0; j < 8; ++j) Tout[j] = T[j];
             }
         } else {
-#pragma unroll
-            for (int j = 0; j < 9; ++j) R[j] = 0.0;
+            rot_from_quat(T, R);
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) sl[j] = T[j];
@@ -742,7 +817,8 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     if (!kPro) {
         double h[9];
         const D3 PO{lpos[3 * orec.y], lpos[3 * orec.y + 1], lpos[3 * orec.y + 2]};
-        const bool ok = obs_terms(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride, kslot + 17, kLdsStride, h);
+        const bool ok = obs_terms<kFT == kFTSmall>(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride,
+                                                   kslot + 17, kLdsStride, h);
 #pragma unroll
         for (int j = 0; j < 9; ++j) terms[j * kFT + tid] = h[j];
         tcount[tid] = (has_o && ok) ? 1 : 0;
@@ -773,6 +849,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         const int nr = (e.w - e.z + 63) >> 6;
         if (nr == 0) continue;
         const double* T = kslot + j * kLdsStride;
+        const double* R = T + 8;
         const double* C = T + 17;
         double v[kStride];
 #pragma unroll
@@ -788,7 +865,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 const int code = (int)P4.w;
                 const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]}
                                        : D3{P4.x, P4.y, P4.z};
-                pose_obs_accum(a, T, C, P, uv, v);
+                pose_obs_accum<kFT == kFTSmall>(a, T, R, C, P, uv, v);
             }
         }
         if (j == wv) FKT(7);
@@ -837,6 +914,8 @@ BAArgs make_args(vx_ba_plan* p) {
     a.max_iter = p->opt.max_iterations;
     a.huber = p->opt.huber_delta;
     a.max_err = p->opt.max_reproj_error;
+    a.huber2 = a.huber * a.huber;
+    a.max_err2 = a.max_err * a.max_err;
     a.kf_pose0 = p->kf_pose0.as<double>();
     a.kf_pose = p->kf_pose.as<double>();
     a.kf_intr = p->kf_intr.as<double>();
