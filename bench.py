@@ -210,6 +210,10 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--ba-cus", type=float, default=0.0,
                     help="fraction of the CUs reserved for the LocalBA context (disjoint CU masks; 0: shared)")
+    ap.add_argument("--diag-skip", default="", choices=("", "ba", "match", "extract"),
+                    help="diagnostics only (the JSON line is marked invalid): leave one stage out of every step")
+    ap.add_argument("--ba-priority", type=int, default=0, choices=(0, 1),
+                    help="stream priority of the LocalBA context (1: the device's greatest)")
     ap.add_argument("--grid-share", type=float, default=None,
                     help="share of the CUs the extraction context's one-round grids are sized for "
                          "(vx_set_grid_share; default 1/3 with more than one stream, 1 otherwise)")
@@ -239,7 +243,7 @@ def main():
     ectxs = [vxslam.Context(dist.local_rank, cu_mask=fe_mask) for _ in range(n_ex)]
     ectx = ectxs[0]
     mctx = ectx if args.streams < 3 else vxslam.Context(dist.local_rank, cu_mask=fe_mask)
-    bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank, cu_mask=ba_mask)
+    bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank, priority=args.ba_priority, cu_mask=ba_mask)
     ctxs = list({id(c): c for c in ectxs + [mctx, bctx]}.values())
     # extraction runs beside the previous frame's LocalBA: its pyramid grid leaves CUs free for it
     grid_share = args.grid_share if args.grid_share else (1.0 / 3.0 if args.streams > 1 else 1.0)
@@ -293,17 +297,26 @@ def main():
         extract(i)
     slot = {(ci, si): ectxs[ci].slot_device(si) for ci in range(E) for si in range(3)}
 
+    skip = args.diag_skip
+    if skip == "ba":
+        plan.run_async()  # (so the statistics fetched at the end exist)
+    if skip == "match":
+        mctx.match_device_async(slot[loc(-2)], slot[loc(-1)])
+
     def step(i):
         ci, si = loc(i)
         ex = ectxs[ci]
         ex.wait_event(ev_m[(i - 3 * E + 1) % (4 * E)])  # (an event not yet recorded is an immediate no-op)
-        extract(i)
+        if skip != "extract":
+            extract(i)
         ex.record(ev_e[ci])
         mctx.wait_event(ev_e[ci])
-        mctx.match_device_async(slot[loc(i - 1)], slot[loc(i)])
+        if skip != "match":
+            mctx.match_device_async(slot[loc(i - 1)], slot[loc(i)])
         mctx.record(ev_m[i % (4 * E)])
         bctx.wait_event(ev_m[i % (4 * E)])
-        plan.run_async()
+        if skip != "ba":
+            plan.run_async()
 
     def sync():
         for c in ctxs:
@@ -394,8 +407,10 @@ def main():
             f"obs/iter {list(st.obs[:st.iterations])} plan {info}")
         for k, (ms, n) in sorted(stages.items(), key=lambda kv: -kv[1][0] * kv[1][1]):
             log(f"[bench] stage {k:18s} {ms * 1e3:9.2f} us/launch x {n:5.2f} launches/step")
+        if skip:
+            log(f"[bench] --diag-skip {skip}: diagnostic run, not the metric")
         out = {
-            "metric": METRIC,
+            "metric": METRIC if not skip else f"DIAGNOSTIC (stage {skip} skipped)",
             "value": round(value, 4),
             "unit": "ms/frame",
             "n_gpus": N,

@@ -91,3 +91,36 @@ run("extract | match | BA (no deps)", [E, M, B])
 run("events E->M only", [em_only])
 run("events M->B only", [mb_only])
 run("pipeline (events)", [piped])
+
+# two extraction contexts (bench.py --extract-ctx 2): frames alternate between them
+e2 = vxslam.Context(0, priority=pe)
+e2.set_grid_share(float(os.environ.get("VX_GRID_SHARE", 1.0 / 3.0)))
+for i in range(3):
+    e2.orb_extract_async(frames[i].data_ptr(), w, h, 3, w * 3, i, params)
+e2.synchronize()
+
+
+def E2(i):
+    (e if i % 2 == 0 else e2).orb_extract_async(frames[i % 8].data_ptr(), w, h, 3, w * 3, (i // 2) % 3, params)
+
+
+def run2(name, fns, K=200):
+    for i in range(10):
+        for f in fns:
+            f(i)
+    for c in (e, e2, m, b):
+        c.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        for f in fns:
+            f(10 + i)
+    for c in (e, e2, m, b):
+        c.synchronize()
+    print(f"{name:28s} {1e3 * (time.perf_counter() - t0) / K:.4f} ms/frame", flush=True)
+
+
+run2("extract x2 alone", [E2])
+run2("extract x2 | localBA", [E2, B])
+run2("match | localBA", [M, B])
+run2("extract x2 | match", [E2, M])
+run2("extract x2 | match | BA", [E2, M, B])

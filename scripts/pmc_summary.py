@@ -16,7 +16,7 @@ STAGE = {"k_gray": "orb_gray", "k_resize": "orb_resize", "k_pyramid": "orb_pyram
          "k_select": "orb_select", "k_blur": "orb_blur", "k_describe": "orb_describe",
          "k_knn_partial": "match_partial", "k_knn_merge": "match_merge", "k_ba_reset": "ba_reset",
          "k_pose_kf": "ba_pose_partial", "k_landmark_solve": "ba_landmark", "k_pose_solve_g": "ba_landmark",
-         "k_landmark": "ba_landmark"}
+         "k_landmark": "ba_landmark", "k_ba_iter": "ba_iter", "k_ba_prologue": "ba_prologue"}
 
 
 def agg(path, counter):
@@ -24,9 +24,12 @@ def agg(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"\b(k_[a-z0-9_]+)(?:<[^>(]*>)?\(", r["Kernel_Name"])
+        m = re.search(r"\b(k_[a-z0-9_]+)(<[^>(]*>)?\(", r["Kernel_Name"])
         if m:
-            d[m.group(1)].append(float(r["Counter_Value"]))
+            name = m.group(1)
+            if name == "k_ba_iter":  # the fused LocalBA: prologue (<true, ...>) vs iterations
+                name = "k_ba_prologue" if "true" in (m.group(2) or "") else "k_ba_iter"
+            d[name].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in d.items()}
 
 

@@ -29,6 +29,7 @@
 // iteration 0 reads the initial poses / positions directly, so a run needs no reset launch.
 // The step keeps the reference's sign (b = -J^T e, :156 and :224): this is a drop-in, not a fix.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <type_traits>
 #include <cstring>
@@ -1021,6 +1022,12 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     if (const char* e = getenv("VX_BA_FUSED"))
         if (e[0] == '0') return VX_OK;
     const int nk = p->n_kf, n_opt = p->n_opt, n_pose = kptr[nk];
+    // $VX_PLAN_TIMING=1: phase times of this build on stderr (scripts/plan_build_time.py)
+    static const bool timing = getenv("VX_PLAN_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    double t_ph[4] = {0, 0, 0, 0};
+    auto lap = [&](int i) { t_ph[i] = std::chrono::duration<double, std::milli>(clk::now() - t_start).count(); };
     std::vector<int> pkf(n_pose);
     for (int k = 0; k < nk; ++k)
         for (int o = kptr[k]; o < kptr[k + 1]; ++o) pkf[o] = k;
@@ -1049,66 +1056,63 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         for (int k = 0; k <= nk; ++k) kc[k + 1] += kc[k];
         for (int q = 0; q < n_opt; ++q) order[kc[key[q]]++] = q;
     }
-    // 2. greedy workgroups of ft threads (cap: landmark-stage observations and landmarks per
-    // workgroup; VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps)
-    if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
-    std::vector<std::vector<int>> K, LM;
-    int ft = kFTSmall;
-    int token = 0;
-    std::vector<int> stamp(nk, -1), mark(nk, -1);
-    const char* env_ft = getenv("VX_BA_FUSED_THREADS");
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        if (env_ft) ft = atoi(env_ft) == kFTLarge ? kFTLarge : kFTSmall;
-        else if (attempt == 1) ft = kFTLarge;
-        int cap = ft;
-        if (const char* e = getenv("VX_BA_FUSED_CAP")) cap = std::min(ft, std::max(64, atoi(e)));
-        std::fill(stamp.begin(), stamp.end(), -1);
-        K.assign(1, {});
-        LM.assign(1, {});
-        int n_l = 0, n_o = 0;
-        auto fresh = [&](int q, int blk) {  // keyframes of landmark q not yet in workgroup blk
-            ++token;
-            int n = 0;
-            auto see = [&](int k) {
-                if (stamp[k] != blk && mark[k] != token) {
-                    mark[k] = token;
-                    ++n;
+    // each optimised landmark's distinct keyframes (landmark-stage and pose-stage observations)
+    std::vector<int> uk_ptr(n_opt + 1, 0), uk;
+    uk.reserve((size_t)lptr[n_opt] + pidx.size());
+    {
+        std::vector<int> seen(nk, -1);
+        for (int q = 0; q < n_opt; ++q) {
+            for (int o = lptr[q]; o < lptr[q + 1]; ++o)
+                if (seen[lkf[o]] != q) {
+                    seen[lkf[o]] = q;
+                    uk.push_back(lkf[o]);
                 }
-            };
-            for (int o = lptr[q]; o < lptr[q + 1]; ++o) see(lkf[o]);
-            for (int i = pp[q]; i < pp[q + 1]; ++i) see(pkf[pidx[i]]);
-            return n;
-        };
-        for (int idx = 0; idx < n_opt; ++idx) {
-            const int q = order[idx], cnt = lptr[q + 1] - lptr[q];
-            if (cnt > ft) return VX_OK;
-            int cur = (int)K.size() - 1;
-            int nn = fresh(q, cur);
-            if (n_l > 0 && (n_l + 1 > cap || n_o + cnt > cap || (int)K[cur].size() + nn > kFK)) {
-                K.emplace_back();
-                LM.emplace_back();
-                ++cur;
-                n_l = n_o = 0;
-                nn = fresh(q, cur);
-            }
-            if (nn > kFK) return VX_OK;
-            auto add = [&](int k) {
-                if (stamp[k] != cur) {
-                    stamp[k] = cur;
-                    K[cur].push_back(k);
+            for (int i = pp[q]; i < pp[q + 1]; ++i)
+                if (seen[pkf[pidx[i]]] != q) {
+                    seen[pkf[pidx[i]]] = q;
+                    uk.push_back(pkf[pidx[i]]);
                 }
-            };
-            for (int o = lptr[q]; o < lptr[q + 1]; ++o) add(lkf[o]);
-            for (int i = pp[q]; i < pp[q + 1]; ++i) add(pkf[pidx[i]]);
-            LM[cur].push_back(q);
-            ++n_l;
-            n_o += cnt;
+            uk_ptr[q + 1] = (int)uk.size();
         }
-        // more 512-thread workgroups than compute units: repack into 1024-thread ones
-        if (env_ft || ft == kFTLarge || (int)K.size() <= c->n_cus) break;
+    }
+    // 2. greedy workgroups of ft threads (cap: landmark-stage observations and landmarks per
+    // workgroup; VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps).  1024
+    // threads when 512-thread workgroups would outnumber the compute units (their count is within a
+    // few percent of the landmark-stage observations / 512: whole landmarks of <= 5 observations)
+    if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
+    int ft = (int64_t)lptr[n_opt] > (int64_t)c->n_cus * (kFTSmall - 16) ? kFTLarge : kFTSmall;
+    if (const char* e = getenv("VX_BA_FUSED_THREADS")) ft = atoi(e) == kFTLarge ? kFTLarge : kFTSmall;
+    int cap = ft;
+    if (const char* e = getenv("VX_BA_FUSED_CAP")) cap = std::min(ft, std::max(64, atoi(e)));
+    std::vector<std::vector<int>> K(1), LM(1);
+    std::vector<int> stamp(nk, -1);
+    int n_l = 0, n_o = 0;
+    for (int idx = 0; idx < n_opt; ++idx) {
+        const int q = order[idx], cnt = lptr[q + 1] - lptr[q];
+        if (cnt > ft) return VX_OK;
+        int cur = (int)K.size() - 1;
+        int nn = 0;
+        for (int u = uk_ptr[q]; u < uk_ptr[q + 1]; ++u) nn += stamp[uk[u]] != cur;
+        if (n_l > 0 && (n_l + 1 > cap || n_o + cnt > cap || (int)K[cur].size() + nn > kFK)) {
+            K.emplace_back();
+            LM.emplace_back();
+            ++cur;
+            n_l = n_o = 0;
+            nn = uk_ptr[q + 1] - uk_ptr[q];
+        }
+        if (nn > kFK) return VX_OK;
+        for (int u = uk_ptr[q]; u < uk_ptr[q + 1]; ++u)
+            if (stamp[uk[u]] != cur) {
+                stamp[uk[u]] = cur;
+                K[cur].push_back(uk[u]);
+            }
+        LM[cur].push_back(q);
+        ++n_l;
+        n_o += cnt;
     }
     const int nb = (int)K.size();
     const int fw = ft / 64;
+    lap(0);
     // 3. owners
     std::vector<int> owner(nk, -1);
     for (int b = 0; b < nb; ++b)
@@ -1128,22 +1132,66 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             lm_blk[LM[b][i]] = b;
             lm_loc[LM[b][i]] = i;
         }
-    std::vector<std::vector<int>> PO(nb);
-    for (int o = 0; o < n_pose; ++o) PO[plm[o] < n_opt ? lm_blk[plm[o]] : owner[pkf[o]]].push_back(o);
+    // (CSR by workgroup, ascending observation index inside)
+    std::vector<int> po_ptr(nb + 1, 0), po(n_pose), po_blk(n_pose);
+    for (int o = 0; o < n_pose; ++o) {
+        po_blk[o] = plm[o] < n_opt ? lm_blk[plm[o]] : owner[pkf[o]];
+        ++po_ptr[po_blk[o] + 1];
+    }
+    for (int b = 0; b < nb; ++b) po_ptr[b + 1] += po_ptr[b];
+    {
+        std::vector<int> w(po_ptr.begin(), po_ptr.end() - 1);
+        for (int o = 0; o < n_pose; ++o) po[w[po_blk[o]]++] = o;
+    }
     // tables: landmarks / landmark-stage observations at b * ft, keyframe entries at b * kFK,
-    // pose observations wave-major with 64-aligned entries
+    // pose observations wave-major with 64-aligned entries.  Written straight into one pinned
+    // staging block and uploaded with one copy (the build is paid per LocalBA::Optimize call).
     const int kBlkInts = 4 * (1 + fw / 2);
-    std::vector<int> blk((size_t)nb * kBlkInts, 0), lm_slot((size_t)nb * ft, 0), lobs_src((size_t)nb * ft, -1);
-    std::vector<int2> lm_run((size_t)nb * ft, make_int2(0, 0));
-    std::vector<int4> lobs_rec((size_t)nb * ft, make_int4(0, 0, 0, 0));
-    std::vector<int> kent((size_t)nb * kFK * 8, 0), loc(nk, -1), rank(nk, 0), pobs_src, pobs_code;
-    std::vector<int> ent_rank((size_t)nb * kFK, -1);  // per (workgroup, entry): its slot's rank in the row
-    pobs_src.reserve((size_t)n_pose + (size_t)nb * kFK * 64);
-    pobs_code.reserve(pobs_src.capacity());
-    std::vector<int> ent_beg(kFK), ent_end(kFK);
+    // pass 1: each entry's pose observations, the waves' rounds
+    std::vector<int> ent_beg((size_t)nb * kFK, 0), ent_end((size_t)nb * kFK, 0);
+    size_t n_pp = 0;
+    for (int b = 0; b < nb; ++b) {
+        int i = po_ptr[b];
+        for (int j = 0; j < (int)K[b].size(); ++j) {
+            ent_beg[(size_t)b * kFK + j] = i;
+            while (i < po_ptr[b + 1] && pkf[po[i]] == K[b][j]) ++i;
+            ent_end[(size_t)b * kFK + j] = i;
+            n_pp += (size_t)(i - ent_beg[(size_t)b * kFK + j] + 63) / 64 * 64;
+        }
+        if (i != po_ptr[b + 1]) return set_error(c, VX_ERR_STATE, "fused layout: pose observations out of keyframe order");
+    }
+    const size_t n_lp = (size_t)nb * ft;
+    FusedOffsets& F = p->f_off;
+    size_t at = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = at;
+        at += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    F.blk = take((size_t)nb * kBlkInts * 4);
+    F.lm_slot = take(n_lp * 4);
+    F.lm_run = take(n_lp * 8);
+    F.lobs_rec = take(n_lp * 16);
+    F.kent = take((size_t)nb * kFK * 32);
+    F.lobs_src = take(n_lp * 4);
+    F.pobs_src = take(std::max<size_t>(n_pp, 1) * 4);
+    F.pobs_code = take(std::max<size_t>(n_pp, 1) * 4);
+    VX_HIP(c, p->f_stage.ensure(at, true));
+    uint8_t* S = static_cast<uint8_t*>(p->f_stage.p);
+    int* blk = reinterpret_cast<int*>(S + F.blk);
+    int* lm_slot = reinterpret_cast<int*>(S + F.lm_slot);
+    int2* lm_run = reinterpret_cast<int2*>(S + F.lm_run);
+    int4* lobs_rec = reinterpret_cast<int4*>(S + F.lobs_rec);
+    int* kent = reinterpret_cast<int*>(S + F.kent);
+    int* lobs_src = reinterpret_cast<int*>(S + F.lobs_src);
+    int* pobs_src = reinterpret_cast<int*>(S + F.pobs_src);
+    int* pobs_code = reinterpret_cast<int*>(S + F.pobs_code);
+    std::memset(blk, 0, (size_t)nb * kBlkInts * 4);
+    std::vector<int> loc(nk, -1), rank(nk, 0), ent_rank((size_t)nb * kFK, -1);
+    size_t pw = 0;
     for (int b = 0; b < nb; ++b) {
         for (int j = 0; j < (int)K[b].size(); ++j) loc[K[b][j]] = j;
-        int* B = &blk[(size_t)b * kBlkInts];
+        int* B = blk + (size_t)b * kBlkInts;
         const size_t base = (size_t)b * ft;
         int ob = 0;
         for (int t = 0; t < (int)LM[b].size(); ++t) {
@@ -1156,43 +1204,44 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             }
             lm_run[base + t].y = ob;
         }
+        // padding rows (valid loads: slot 0, empty runs, no observation)
+        for (int t = (int)LM[b].size(); t < ft; ++t) {
+            lm_slot[base + t] = 0;
+            lm_run[base + t] = make_int2(0, 0);
+        }
+        for (int t = ob; t < ft; ++t) {
+            lobs_src[base + t] = -1;
+            lobs_rec[base + t] = make_int4(0, 0, 0, 0);
+        }
         B[0] = (int)LM[b].size();
         B[1] = ob;
         B[2] = (int)K[b].size();
-        // pose observations of each entry (PO[b] is keyframe-major: ascending observation index)
-        size_t i = 0;
-        for (int j = 0; j < (int)K[b].size(); ++j) {
-            ent_beg[j] = (int)i;
-            while (i < PO[b].size() && pkf[PO[b][i]] == K[b][j]) ++i;
-            ent_end[j] = (int)i;
-        }
-        if (i != PO[b].size()) return set_error(c, VX_ERR_STATE, "fused layout: pose observations out of keyframe order");
-        int* E = &kent[(size_t)b * kFK * 8];
-        for (int j = 0; j < kFK; ++j) {
-            E[8 * j] = -1;
-            E[8 * j + 4] = -1;
-        }
+        int* E = kent + (size_t)b * kFK * 8;
+        for (int j = 0; j < kFK; ++j)
+            for (int x = 0; x < 8; ++x) E[8 * j + x] = (x == 0 || x == 4) ? -1 : 0;
         for (int w = 0; w < fw; ++w) {
-            const int wstart = (int)pobs_src.size();
+            const size_t wstart = pw;
             for (int j = w; j < (int)K[b].size(); j += fw) {
                 const int k = K[b][j];
-                const int n = ent_end[j] - ent_beg[j];
+                const int e0 = ent_beg[(size_t)b * kFK + j], e1 = ent_end[(size_t)b * kFK + j], n = e1 - e0;
                 E[8 * j] = k | (owner[k] == b ? (1 << 30) : 0);
-                E[8 * j + 2] = (int)pobs_src.size();
-                E[8 * j + 3] = (int)pobs_src.size() + n;
-                for (int x = ent_beg[j]; x < ent_end[j]; ++x) {
-                    const int o = PO[b][x];
-                    pobs_src.push_back(o);
-                    pobs_code.push_back(plm[o] < n_opt ? lm_loc[plm[o]] : -1 - plm[o]);
+                E[8 * j + 2] = (int)pw;
+                E[8 * j + 3] = (int)pw + n;
+                for (int x = e0; x < e1; ++x) {
+                    const int o = po[x];
+                    pobs_src[pw + (x - e0)] = o;
+                    pobs_code[pw + (x - e0)] = plm[o] < n_opt ? lm_loc[plm[o]] : -1 - plm[o];
                 }
-                while (pobs_src.size() % 64) {  // pad to the next round
-                    pobs_src.push_back(-1);
-                    pobs_code.push_back(0);
+                const size_t padded = (size_t)(n + 63) / 64 * 64;  // pad to the next round
+                for (size_t x = n; x < padded; ++x) {
+                    pobs_src[pw + x] = -1;
+                    pobs_code[pw + x] = 0;
                 }
+                pw += padded;
                 if (n > 0) ent_rank[(size_t)b * kFK + j] = rank[k]++;
             }
-            B[4 + 2 * w] = wstart;
-            B[4 + 2 * w + 1] = ((int)pobs_src.size() - wstart) / 64;
+            B[4 + 2 * w] = (int)wstart;
+            B[4 + 2 * w + 1] = (int)((pw - wstart) / 64);
         }
         for (int k : K[b]) loc[k] = -1;
     }
@@ -1200,41 +1249,38 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     for (int k = 0; k < nk; ++k) maxl = std::max(maxl, rank[k]);
     for (int b = 0; b < nb; ++b)
         for (int j = 0; j < (int)K[b].size(); ++j) {
-            int* E = &kent[((size_t)b * kFK + j) * 8];
+            int* E = kent + ((size_t)b * kFK + j) * 8;
             const int k = K[b][j];
             E[1] = rank[k];
             const int r = ent_rank[(size_t)b * kFK + j];
             E[4] = r >= 0 ? k * maxl + r : -1;
         }
-    // upload + gather the observation payloads into the fused order
-    const int n_pp = (int)pobs_src.size(), n_lp = nb * ft;
-    int rc;
-    if ((rc = upload(c, p->f_blk, blk))) return rc;
-    if ((rc = upload(c, p->f_lm_slot, lm_slot))) return rc;
-    if ((rc = upload(c, p->f_lm_run, lm_run))) return rc;
-    if ((rc = upload(c, p->f_lobs_rec, lobs_rec))) return rc;
-    if ((rc = upload(c, p->f_kent, kent))) return rc;
-    std::vector<int> idx(lobs_src);
-    idx.insert(idx.end(), pobs_src.begin(), pobs_src.end());
-    idx.insert(idx.end(), pobs_code.begin(), pobs_code.end());
-    if ((rc = upload(c, p->f_idx, idx))) return rc;
-    VX_HIP(c, p->f_lobs_uv.ensure((size_t)n_lp * sizeof(double2)));
-    VX_HIP(c, p->f_pobs_uv.ensure((size_t)std::max(n_pp, 1) * sizeof(double2)));
-    VX_HIP(c, p->f_pobs_p.ensure((size_t)std::max(n_pp, 1) * sizeof(double4)));
-    const int* d_idx = p->f_idx.as<int>();
-    hipLaunchKernelGGL(k_fused_gather, dim3((std::max(n_lp, n_pp) + 255) / 256), dim3(256), 0, c->stream, d_idx, n_lp,
-                       (const double2*)p->lobs_uv.as<double2>(), p->f_lobs_uv.as<double2>(), d_idx + n_lp,
-                       d_idx + n_lp + n_pp, n_pp, (const double2*)p->pobs_uv.as<double2>(),
+    lap(1);
+    // one upload, then the observation payloads gathered into the fused order
+    VX_HIP(c, p->f_tab.ensure(at));
+    VX_HIP(c, hipMemcpyAsync(p->f_tab.p, S, at, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* T = p->f_tab.as<uint8_t>();
+    VX_HIP(c, p->f_lobs_uv.ensure(n_lp * sizeof(double2)));
+    VX_HIP(c, p->f_pobs_uv.ensure(std::max<size_t>(n_pp, 1) * sizeof(double2)));
+    VX_HIP(c, p->f_pobs_p.ensure(std::max<size_t>(n_pp, 1) * sizeof(double4)));
+    hipLaunchKernelGGL(k_fused_gather, dim3((unsigned)((std::max(n_lp, n_pp) + 255) / 256)), dim3(256), 0, c->stream,
+                       reinterpret_cast<const int*>(T + F.lobs_src), (int)n_lp, (const double2*)p->lobs_uv.as<double2>(),
+                       p->f_lobs_uv.as<double2>(), reinterpret_cast<const int*>(T + F.pobs_src),
+                       reinterpret_cast<const int*>(T + F.pobs_code), (int)n_pp, (const double2*)p->pobs_uv.as<double2>(),
                        (const double*)p->lm_pos0.as<double>(), p->f_pobs_uv.as<double2>(), p->f_pobs_p.as<double4>());
     VX_LAUNCH_CHECK(c, "k_fused_gather");
     const size_t part_bytes = 2 * (size_t)nk * maxl * kStride * sizeof(double);
     VX_HIP(c, p->f_part.ensure(part_bytes));
     VX_HIP(c, hipMemsetAsync(p->f_part.p, 0, part_bytes, c->stream));  // slots no group writes stay 0
-    VX_HIP(c, hipStreamSynchronize(c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));  // (the staging block is reused by the next build)
     p->f_blocks = nb;
     p->f_maxl = maxl;
     p->f_threads = ft;
     p->fused = true;
+    lap(2);
+    if (timing)
+        fprintf(stderr, "[vx plan] fused layout: pack %.3f ms, tables %.3f ms, upload + gather %.3f ms (%d workgroups x %d)\n",
+                t_ph[0], t_ph[1] - t_ph[0], t_ph[2] - t_ph[1], nb, ft);
     return VX_OK;
 }
 
@@ -1437,12 +1483,13 @@ int shard_kernel_choice(vx_ctx* c, vx_ba_plan* p) {
 
 FusedArgs make_fused_args(vx_ba_plan* p) {
     FusedArgs f{};
-    f.blk = p->f_blk.as<int4>();
-    f.lm_slot = p->f_lm_slot.as<int>();
-    f.lm_run = p->f_lm_run.as<int2>();
+    const uint8_t* T = p->f_tab.as<uint8_t>();
+    f.blk = reinterpret_cast<const int4*>(T + p->f_off.blk);
+    f.lm_slot = reinterpret_cast<const int*>(T + p->f_off.lm_slot);
+    f.lm_run = reinterpret_cast<const int2*>(T + p->f_off.lm_run);
     f.lobs_uv = p->f_lobs_uv.as<double2>();
-    f.lobs_rec = p->f_lobs_rec.as<int4>();
-    f.kent = p->f_kent.as<int4>();
+    f.lobs_rec = reinterpret_cast<const int4*>(T + p->f_off.lobs_rec);
+    f.kent = reinterpret_cast<const int4*>(T + p->f_off.kent);
     f.pobs_uv = p->f_pobs_uv.as<double2>();
     f.pobs_p = p->f_pobs_p.as<double4>();
     f.part = p->f_part.as<double>();

@@ -6,6 +6,11 @@
 
 #include "vx_internal.hpp"
 
+// byte offsets of the fused layout's index tables inside one device block (ba.hip build_fused)
+struct FusedOffsets {
+    size_t blk = 0, lm_slot = 0, lm_run = 0, lobs_rec = 0, kent = 0, lobs_src = 0, pobs_src = 0, pobs_code = 0;
+};
+
 struct vx_ba_plan {
     vx_ctx* c = nullptr;
     vx_ba_options opt{};
@@ -33,7 +38,9 @@ struct vx_ba_plan {
     // slots (n_kf x f_maxl x 32 doubles) summed in slot order by every workgroup that needs the pose
     bool fused = false;
     int f_blocks = 0, f_maxl = 0, f_threads = 512;
-    vx::DevBuf f_blk, f_lm_slot, f_lm_run, f_lobs_uv, f_lobs_rec, f_kent, f_pobs_uv, f_pobs_p, f_part, f_idx;
+    vx::DevBuf f_tab, f_lobs_uv, f_pobs_uv, f_pobs_p, f_part;  // f_tab: the index tables, one upload
+    vx::PinnedBuf f_stage;                                        // their host staging block
+    FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
 };
 
 struct vx_dmap;

@@ -24,6 +24,8 @@
 // The result is the same plan, array for array, as the host build (tests compare the runs
 // bitwise).  Scans are rocPRIM's device exclusive scan.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -497,6 +499,8 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     if ((rc = alloc_run_buffers(c, p))) return rc;
     VX_HIP(c, hipStreamSynchronize(s));  // the host vectors above must outlive their async copies
     if (p->shard_count == 1) {
+        static const bool timing = getenv("VX_PLAN_TIMING") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         // host copies of the CSR index arrays for the fused layout (ba.hip build_fused)
         std::vector<int> kptr(nk + 1), plm(std::max(n_pose, 1)), lkf(std::max(n_lobs, 1));
         VX_HIP(c, hipMemcpyAsync(kptr.data(), p->kf_obs_ptr.p, (size_t)(nk + 1) * 4, hipMemcpyDeviceToHost, s));
@@ -505,6 +509,9 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
         VX_HIP(c, hipStreamSynchronize(s));
         plm.resize(n_pose);
         lkf.resize(n_lobs);
+        if (timing)
+            fprintf(stderr, "[vx plan] CSR download for the fused layout %.3f ms\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         if ((rc = build_fused(c, p, kptr, plm, lptr, lkf))) return rc;
     }
     return VX_OK;

@@ -81,12 +81,14 @@ struct PinnedBuf {
     ~PinnedBuf() {
         if (p) (void)hipHostFree(p);
     }
-    hipError_t ensure(size_t want) {
+    // cached = true: host-cached (non-coherent) pages for a staging block the CPU fills with many
+    // scattered writes; the default (coherent) pages are uncached on the host side
+    hipError_t ensure(size_t want, bool cached = false) {
         if (want <= bytes) return hipSuccess;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         bytes = 0;
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, cached ? hipHostMallocNonCoherent : hipHostMallocDefault);
         if (e == hipSuccess) bytes = want;
         return e;
     }
