@@ -18,6 +18,17 @@ from test_gpu_parity import _assert_ba_close, _canon
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["fused", "two-kernel"])
+def ba_path(request, monkeypatch):
+    """Both sharded LocalBA paths: the fused one (k_ba_iter + per-row sums + one all-reduce per
+    iteration) and the two-kernel one (k_pose_kf + all-reduce + k_landmark_solve, VX_BA_FUSED=0)."""
+    if request.param == "two-kernel":
+        monkeypatch.setenv("VX_BA_FUSED", "0")
+    else:
+        monkeypatch.delenv("VX_BA_FUSED", raising=False)
+    return request.param
+
+
 def _shard_run(ctx, m, opts, n):
     plans = [ctx.ba_plan(m, opts, shard_rank=r, shard_count=n) for r in range(n)]
     infos = [p.info() for p in plans]
@@ -32,7 +43,7 @@ def _shard_run(ctx, m, opts, n):
 
 
 @pytest.mark.parametrize("n", [2, 4, 8])
-def test_sharded_localba_bench_windows(ctx, oracle, n):
+def test_sharded_localba_bench_windows(ctx, oracle, n, ba_path):
     nk, nl = 50 * n, 20000 * n
     m = synth.make_ba_map(0x5EED0003, nk, nl, n_streams=n, n_old_kf=2 * n)  # bench.py's rig window
     opts = vxslam.default_ba_options(window=nk)
@@ -64,7 +75,7 @@ def test_sharded_localba_bench_windows(ctx, oracle, n):
     _assert_ba_close(got, mc, stats[0], stc)
 
 
-def test_sharded_kernel_choice_is_shared(ctx, oracle):
+def test_sharded_kernel_choice_is_shared(ctx, oracle, ba_path):
     """A window near the kernel-choice threshold (workgroups x keyframes = 80,000 at 200
     keyframes): the unsharded window runs the large-window kernels, its 2- and 3-way shards the
     LDS-pose kernel, chosen from the maximum workgroup count over the shards so every rank runs the

@@ -650,6 +650,8 @@ struct FusedArgs {
                             // pose stage of iteration i fills buffer i & 1 (a launch reads one buffer
                             // and writes the other, so no workgroup reads what another overwrites)
     int maxl, n_part;
+    const double* rowpart;  // sharded plans: per keyframe row the partial slots summed (k_row_sum) and
+                            // all-reduced over the ranks; the combine and the stop rule read it instead
 };
 
 // LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), kFK loaded
@@ -744,6 +746,10 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         for (int pr = tid; pr < n_ent * kNTerms; pr += kFT) {
             const int j = pr / kNTerms, t = pr - j * kNTerms;
             const int4 e = KE[2 * j];
+            if (f.rowpart) {  // sharded: the all-reduced row (identical on every rank)
+                kslot[j * kLdsStride + t] = f.rowpart[(size_t)(e.x & 0x3fffffff) * kStride + t];
+                continue;
+            }
             const double* src = part_in + ((size_t)(e.x & 0x3fffffff) * f.maxl) * kStride + t;
             double acc = 0.0;
             for (int i0 = 0; i0 < e.y; i0 += 16) {
@@ -758,9 +764,11 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         // ---- stop rule of iteration it (workgroup 0): totals over every partial slot
         if (b == 0) {
             double tot = 0.0, cnt = 0.0;
-            for (int q = tid; q < f.n_part; q += kFT) {
-                tot += part_in[(size_t)q * kStride + 27];
-                cnt += part_in[(size_t)q * kStride + 28];
+            const double* tp = f.rowpart ? f.rowpart : part_in;
+            const int n_tp = f.rowpart ? a.n_kf : f.n_part;
+            for (int q = tid; q < n_tp; q += kFT) {
+                tot += tp[(size_t)q * kStride + 27];
+                cnt += tp[(size_t)q * kStride + 28];
             }
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) {
@@ -874,6 +882,18 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         if ((lane & 1) == 0) part_out[(size_t)dst * kStride + (lane >> 1)] = (lane >> 1) < kNTerms ? tot : 0.0;
     }
     FKT(5);
+}
+
+// sharded plans: each keyframe row's partial slots summed in slot order (the slots of a row no group
+// fills are 0) -> rowpart, which the per-iteration all-reduce then sums over the ranks
+__global__ void k_row_sum(const double* part, int n_kf, int maxl, double* rowpart) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_kf * kStride) return;
+    const int row = i / kStride, t = i - row * kStride;
+    const double* src = part + (size_t)row * maxl * kStride + t;
+    double s = 0.0;
+    for (int q = 0; q < maxl; ++q) s += src[(size_t)q * kStride];
+    rowpart[i] = s;
 }
 
 // fused-order observation payloads: uv by plan index (-1: padding), pose records with the fixed
@@ -1018,7 +1038,7 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
 int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const std::vector<int>& plm,
                 const std::vector<int>& lptr, const std::vector<int>& lkf) {
     p->fused = false;
-    if (p->status != 0 || p->shard_count > 1 || p->global_poses || p->n_kf > kMaxKfLds || p->n_opt <= 0) return VX_OK;
+    if (p->status != 0 || p->global_poses || p->n_kf > kMaxKfLds || p->n_opt <= 0) return VX_OK;
     if (const char* e = getenv("VX_BA_FUSED"))
         if (e[0] == '0') return VX_OK;
     const int nk = p->n_kf, n_opt = p->n_opt, n_pose = kptr[nk];
@@ -1271,6 +1291,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     VX_LAUNCH_CHECK(c, "k_fused_gather");
     const size_t part_bytes = 2 * (size_t)nk * maxl * kStride * sizeof(double);
     VX_HIP(c, p->f_part.ensure(part_bytes));
+    if (p->shard_count > 1) VX_HIP(c, p->f_rowpart.ensure((size_t)nk * kStride * sizeof(double)));
     VX_HIP(c, hipMemsetAsync(p->f_part.p, 0, part_bytes, c->stream));  // slots no group writes stay 0
     VX_HIP(c, hipStreamSynchronize(c->stream));  // (the staging block is reused by the next build)
     p->f_blocks = nb;
@@ -1466,16 +1487,19 @@ int reset_if_no_iterations(vx_ctx* c, const vx_ba_plan* p, const BAArgs& a) {
 // all-reduce and a host synchronisation at its first run)
 int shard_kernel_choice(vx_ctx* c, vx_ba_plan* p) {
     if (p->choice_made) return VX_OK;
-    const int32_t mine[2] = {p->n_lm_blocks, p->max_lm_obs};
+    // {workgroups, most observations of a landmark, 1 if this rank has no fused layout}: the fused
+    // path runs only when every rank has one (their collectives must match)
+    const int32_t mine[3] = {p->n_lm_blocks, p->max_lm_obs, p->fused ? 0 : 1};
     DevBuf d;
     VX_HIP(c, d.ensure(sizeof mine));
     VX_HIP(c, hipMemcpyAsync(d.p, mine, sizeof mine, hipMemcpyHostToDevice, c->stream));
-    ncclResult_t r = ncclAllReduce(d.p, d.p, 2, ncclInt32, ncclMax, c->comm, c->stream);
+    ncclResult_t r = ncclAllReduce(d.p, d.p, 3, ncclInt32, ncclMax, c->comm, c->stream);
     if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
-    int32_t all[2];
+    int32_t all[3];
     VX_HIP(c, hipMemcpyAsync(all, d.p, sizeof all, hipMemcpyDeviceToHost, c->stream));
     VX_HIP(c, hipStreamSynchronize(c->stream));
     p->lds_poses = choose_lds_poses(p, all[0], all[1]);
+    p->fused_all = all[2] == 0;
     p->choice_made = true;
     return VX_OK;
 }
@@ -1495,12 +1519,13 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
     f.part = p->f_part.as<double>();
     f.maxl = p->f_maxl;
     f.n_part = p->n_kf * p->f_maxl;
+    f.rowpart = p->shard_count > 1 ? p->f_rowpart.as<double>() : nullptr;
     return f;
 }
 
-// the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration
+// the fused path's launches: prologue (iteration 0's pose stage, it = -1) or k_ba_iter(it)
 template <int kFT>
-int plan_run_fused_t(vx_ctx* c, vx_ba_plan* p) {
+int fused_launch_t(vx_ctx* c, vx_ba_plan* p, const BAArgs& a, const FusedArgs& f, int it) {
     constexpr int lds = (int)fused_lds(kFT);
     static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<true, kFT>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -1508,33 +1533,58 @@ int plan_run_fused_t(vx_ctx* c, vx_ba_plan* p) {
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     VX_HIP(c, a0);
     VX_HIP(c, a1);
+    if (it < 0)
+        VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
+                         a, f, -1));
+    else
+        VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
+                         a, f, it));
+    return VX_OK;
+}
+int fused_launch(vx_ctx* c, vx_ba_plan* p, const BAArgs& a, const FusedArgs& f, int it) {
+    return p->f_threads == kFTLarge ? fused_launch_t<kFTLarge>(c, p, a, f, it) : fused_launch_t<kFTSmall>(c, p, a, f, it);
+}
+// sharded fused path: the rows of the partial buffer iteration it reads (parity it & 1) -> f_rowpart
+int fused_row_sum(vx_ctx* c, vx_ba_plan* p, int it) {
+    const int n = p->n_kf * kStride;
+    ProfScope ps(c, kStBaPoseSum);
+    hipLaunchKernelGGL(k_row_sum, dim3((n + 255) / 256), dim3(256), 0, c->stream,
+                       (const double*)(p->f_part.as<double>() + (size_t)(it & 1) * p->n_kf * p->f_maxl * kStride),
+                       p->n_kf, p->f_maxl, p->f_rowpart.as<double>());
+    VX_LAUNCH_CHECK(c, "k_row_sum");
+    return VX_OK;
+}
+
+// the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration (sharded: each
+// preceded by the row sums and their all-reduce)
+int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
     const BAArgs a = make_args(p);
     const FusedArgs f = make_fused_args(p);
     int rc;
     if ((rc = reset_if_no_iterations(c, p, a))) return rc;
     if (p->opt.max_iterations == 0) return VX_OK;
-    VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
-                     a, f, -1));
-    for (int it = 0; it < p->opt.max_iterations; ++it)
-        VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
-                         a, f, it));
+    if ((rc = fused_launch(c, p, a, f, -1))) return rc;
+    for (int it = 0; it < p->opt.max_iterations; ++it) {
+        if (p->shard_count > 1) {
+#ifndef VX_NO_RCCL
+            if ((rc = fused_row_sum(c, p, it))) return rc;
+            ProfScope ps(c, kStBaAllreduce);
+            ncclResult_t r = ncclAllReduce(p->f_rowpart.p, p->f_rowpart.p, (size_t)p->n_kf * kStride, ncclDouble, ncclSum,
+                                           c->comm, c->stream);
+            if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+#else
+            return set_error(c, VX_ERR_COMM, "built without RCCL");
+#endif
+        }
+        if ((rc = fused_launch(c, p, a, f, it))) return rc;
+    }
     return VX_OK;
-}
-
-// the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration
-int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
-    return p->f_threads == kFTLarge ? plan_run_fused_t<kFTLarge>(c, p) : plan_run_fused_t<kFTSmall>(c, p);
 }
 
 int plan_run(vx_ctx* c, vx_ba_plan* p) {
     if (p->status != 0) {
         p->ran = true;
         return VX_OK;
-    }
-    if (p->fused && p->shard_count == 1) {
-        const int rc = plan_run_fused(c, p);
-        if (!rc) p->ran = true;
-        return rc;
     }
     const bool sharded = p->shard_count > 1;
     int rc;
@@ -1546,7 +1596,13 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
 #else
         return set_error(c, VX_ERR_COMM, "built without RCCL");
 #endif
-    } else if (!p->choice_made) {
+    }
+    if (p->fused && (!sharded || p->fused_all)) {
+        rc = plan_run_fused(c, p);
+        if (!rc) p->ran = true;
+        return rc;
+    }
+    if (!sharded && !p->choice_made) {
         p->lds_poses = choose_lds_poses(p, p->n_lm_blocks, p->max_lm_obs);
         p->choice_made = true;
     }
@@ -1690,9 +1746,39 @@ int vx_ba_shard_emulate_run(vx_ctx* c, vx_ba_plan* const* plans, int n) {
     }
     // the kernel choice every rank would make from the all-reduced maxima
     int blocks = 0, max_obs = 0;
+    bool all_fused = true;
     for (int r = 0; r < n; ++r) {
         blocks = std::max(blocks, plans[r]->n_lm_blocks);
         max_obs = std::max(max_obs, plans[r]->max_lm_obs);
+        all_fused = all_fused && plans[r]->fused;
+    }
+    int rc;
+    if (all_fused) {  // fused path: row sums of every shard summed in rank order in place of the all-reduce
+        PartPtrs rows{};
+        std::vector<BAArgs> args(n);
+        std::vector<FusedArgs> fargs(n);
+        for (int r = 0; r < n; ++r) {
+            plans[r]->fused_all = true;
+            plans[r]->choice_made = true;
+            rows.p[r] = plans[r]->f_rowpart.as<double>();
+            args[r] = make_args(plans[r]);
+            fargs[r] = make_fused_args(plans[r]);
+            if ((rc = reset_if_no_iterations(c, plans[r], args[r]))) return rc;
+        }
+        const long long len = (long long)p0->n_kf * kStride;
+        if (p0->opt.max_iterations > 0)
+            for (int r = 0; r < n; ++r)
+                if ((rc = fused_launch(c, plans[r], args[r], fargs[r], -1))) return rc;
+        for (int it = 0; it < p0->opt.max_iterations; ++it) {
+            for (int r = 0; r < n; ++r)
+                if ((rc = fused_row_sum(c, plans[r], it))) return rc;
+            hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, c->stream, rows, n, len);
+            VX_LAUNCH_CHECK(c, "k_sum_parts");
+            for (int r = 0; r < n; ++r)
+                if ((rc = fused_launch(c, plans[r], args[r], fargs[r], it))) return rc;
+        }
+        for (int r = 0; r < n; ++r) plans[r]->ran = true;
+        return VX_OK;
     }
     PartPtrs parts{};
     std::vector<BAArgs> args(n);
@@ -1703,7 +1789,6 @@ int vx_ba_shard_emulate_run(vx_ctx* c, vx_ba_plan* const* plans, int n) {
         args[r] = make_args(plans[r]);
     }
     const long long len = (long long)p0->n_kf * p0->n_split * kStride;
-    int rc;
     for (int r = 0; r < n; ++r)
         if ((rc = reset_if_no_iterations(c, plans[r], args[r]))) return rc;
     for (int it = 0; it < p0->opt.max_iterations; ++it) {

@@ -37,8 +37,10 @@ struct vx_ba_plan {
     // and the pose-stage observations of its landmarks grouped by keyframe; per-keyframe partial
     // slots (n_kf x f_maxl x 32 doubles) summed in slot order by every workgroup that needs the pose
     bool fused = false;
+    bool fused_all = false;  // sharded: every rank has a fused layout (decided at the first run)
     int f_blocks = 0, f_maxl = 0, f_threads = 512;
     vx::DevBuf f_tab, f_lobs_uv, f_pobs_uv, f_pobs_p, f_part;  // f_tab: the index tables, one upload
+    vx::DevBuf f_rowpart;                                         // sharded: all-reduced per-row partials
     vx::PinnedBuf f_stage;                                        // their host staging block
     FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
 };
