@@ -234,6 +234,11 @@ void vx_ba_plan_destroy(vx_ba_plan* plan);
  * n_split (pose-stage workgroups per keyframe), n_lm_blocks (landmark-stage workgroups),
  * max_lm_obs (most landmark-stage observations of one landmark)} */
 int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out8);
+/* kernel layout of the plan: out4 = {1 if it has the fused one-launch-per-iteration layout
+ * (k_ba_iter) else 0, threads per fused workgroup, fused workgroups, most partial slots of one
+ * keyframe}.  A sharded plan runs the fused kernel only when every rank has the layout (decided by
+ * one all-reduce on its first run). */
+int vx_ba_plan_layout(const vx_ba_plan* plan, int64_t* out4);
 /* Test hook: runs the n shard plans plans[r] (shard r of n, built from one window, all on ctx) the
  * way n ranks would run them, on one device: per iteration every shard's pose stage, then the
  * element-wise sum of their partial blocks in rank order written back to every shard in place of

@@ -29,9 +29,11 @@ def ba_path(request, monkeypatch):
     return request.param
 
 
-def _shard_run(ctx, m, opts, n):
+def _shard_run(ctx, m, opts, n, path=None):
     plans = [ctx.ba_plan(m, opts, shard_rank=r, shard_count=n) for r in range(n)]
     infos = [p.info() for p in plans]
+    if path is not None:  # the shard plans carry the fused layout exactly when that path is enabled
+        assert [p.layout()["fused"] for p in plans] == [int(path == "fused")] * n
     ctx.ba_shard_emulate(plans)
     outs, stats = [], []
     for p in plans:
@@ -47,7 +49,7 @@ def test_sharded_localba_bench_windows(ctx, oracle, n, ba_path):
     nk, nl = 50 * n, 20000 * n
     m = synth.make_ba_map(0x5EED0003, nk, nl, n_streams=n, n_old_kf=2 * n)  # bench.py's rig window
     opts = vxslam.default_ba_options(window=nk)
-    infos, outs, stats = _shard_run(ctx, m, opts, n)
+    infos, outs, stats = _shard_run(ctx, m, opts, n, ba_path)
     assert len({i["n_split"] for i in infos}) == 1 and len({i["n_kf"] for i in infos}) == 1
     assert sum(i["n_opt"] for i in infos) == stats[0].n_landmarks  # the shards partition the landmark set
     # every rank: the same poses (bitwise) and the same stop decisions
@@ -88,7 +90,7 @@ def test_sharded_kernel_choice_is_shared(ctx, oracle, ba_path):
     pc = one["kf_pose"].copy()
     pc[:, :4] = _canon(pc[:, :4])
     for n in (2, 3):
-        infos, outs, stats = _shard_run(ctx, m, opts, n)
+        infos, outs, stats = _shard_run(ctx, m, opts, n, ba_path)
         for o in outs[1:]:
             assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"])
         pg = outs[0]["kf_pose"].copy()

@@ -1882,6 +1882,15 @@ int vx_ba_plan_info(const vx_ba_plan* p, int64_t* out8) {
     return VX_OK;
 }
 
+int vx_ba_plan_layout(const vx_ba_plan* p, int64_t* out4) {
+    if (!p || !out4) return VX_ERR_INVALID;
+    out4[0] = p->fused ? 1 : 0;
+    out4[1] = p->fused ? p->f_threads : 0;
+    out4[2] = p->fused ? p->f_blocks : 0;
+    out4[3] = p->fused ? p->f_maxl : 0;
+    return VX_OK;
+}
+
 int vx_ba_optimize_map(vx_ctx* c, vx_map_view* m, uint64_t ref, int has_ref, const vx_ba_options* opt,
                        vx_ba_stats* st) {
     vx_ba_plan* p = nullptr;

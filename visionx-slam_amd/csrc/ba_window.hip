@@ -498,7 +498,7 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
     if ((rc = alloc_run_buffers(c, p))) return rc;
     VX_HIP(c, hipStreamSynchronize(s));  // the host vectors above must outlive their async copies
-    if (p->shard_count == 1) {
+    {  // every plan, sharded ones included (their ranks all-reduce the fused layout's row sums)
         static const bool timing = getenv("VX_PLAN_TIMING") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         // host copies of the CSR index arrays for the fused layout (ba.hip build_fused)
