@@ -1023,6 +1023,42 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
     return VX_OK;
 }
 
+namespace {
+template <class B>
+void swap_buf(B& a, B& b) {
+    std::swap(a.p, b.p);
+    std::swap(a.bytes, b.bytes);
+}
+// dst takes src's buffers (and src dst's); nothing else of either plan moves
+void adopt_buffers(vx_ba_plan* dst, vx_ba_plan* src) {
+#define VX_SWAP_BUF(b) swap_buf(dst->b, src->b);
+    VX_PLAN_BUFFERS(VX_SWAP_BUF)
+#undef VX_SWAP_BUF
+}
+constexpr size_t kMaxPlanHusks = 4;  // parked buffer sets per context
+}  // namespace
+
+vx_ba_plan* plan_new(vx_ctx* c) {
+    auto* p = new vx_ba_plan();
+    p->c = c;
+    if (!c) return p;
+    if (!c->plan_husks.empty()) {
+        vx_ba_plan* h = c->plan_husks.back();
+        c->plan_husks.pop_back();
+        adopt_buffers(p, h);
+        delete h;
+    }
+    c->plan_live.push_back(p);
+    return p;
+}
+
+void plan_pool_release(vx_ctx* c) {
+    for (vx_ba_plan* h : c->plan_husks) delete h;
+    c->plan_husks.clear();
+    for (vx_ba_plan* p : c->plan_live) p->c = nullptr;  // their destroy then just frees
+    c->plan_live.clear();
+}
+
 // The fused layout (k_ba_iter) from the plan's CSRs, on the host: both plan builders end here with
 // the same arrays, so the layout — and every run — is the same for both.
 //   1. optimised landmarks ordered by the first window keyframe that observes them (stable), so a
@@ -1046,7 +1082,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     static const bool timing = getenv("VX_PLAN_TIMING") != nullptr;
     using clk = std::chrono::steady_clock;
     const auto t_start = clk::now();
-    double t_ph[4] = {0, 0, 0, 0};
+    double t_ph[16] = {0};
     auto lap = [&](int i) { t_ph[i] = std::chrono::duration<double, std::milli>(clk::now() - t_start).count(); };
     std::vector<int> pkf(n_pose);
     for (int k = 0; k < nk; ++k)
@@ -1062,6 +1098,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         for (int o = 0; o < n_pose; ++o)
             if (plm[o] < n_opt) pidx[w[plm[o]]++] = o;
     }
+    lap(3);
     // 1. keyframe-locality order (counting sort by first keyframe, stable)
     std::vector<int> key(n_opt, nk), order(n_opt);
     for (int q = 0; q < n_opt; ++q) {
@@ -1076,6 +1113,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         for (int k = 0; k <= nk; ++k) kc[k + 1] += kc[k];
         for (int q = 0; q < n_opt; ++q) order[kc[key[q]]++] = q;
     }
+    lap(4);
     // each optimised landmark's distinct keyframes (landmark-stage and pose-stage observations)
     std::vector<int> uk_ptr(n_opt + 1, 0), uk;
     uk.reserve((size_t)lptr[n_opt] + pidx.size());
@@ -1095,6 +1133,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             uk_ptr[q + 1] = (int)uk.size();
         }
     }
+    lap(5);
     // 2. greedy workgroups of ft threads (cap: landmark-stage observations and landmarks per
     // workgroup; VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps).  1024
     // threads when 512-thread workgroups would outnumber the compute units (their count is within a
@@ -1145,6 +1184,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         }
     if ((int)K[0].size() > kFK) return VX_OK;
     for (auto& v : K) std::sort(v.begin(), v.end());
+    lap(6);
     // 4. pose observations per workgroup (ascending observation index = keyframe-major)
     std::vector<int> lm_blk(n_opt), lm_loc(n_opt);
     for (int b = 0; b < nb; ++b)
@@ -1167,6 +1207,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     // pose observations wave-major with 64-aligned entries.  Written straight into one pinned
     // staging block and uploaded with one copy (the build is paid per LocalBA::Optimize call).
     const int kBlkInts = 4 * (1 + fw / 2);
+    lap(7);
     // pass 1: each entry's pose observations, the waves' rounds
     std::vector<int> ent_beg((size_t)nb * kFK, 0), ent_end((size_t)nb * kFK, 0);
     size_t n_pp = 0;
@@ -1196,7 +1237,9 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     F.lobs_src = take(n_lp * 4);
     F.pobs_src = take(std::max<size_t>(n_pp, 1) * 4);
     F.pobs_code = take(std::max<size_t>(n_pp, 1) * 4);
+    lap(8);
     VX_HIP(c, p->f_stage.ensure(at, true));
+    lap(9);
     uint8_t* S = static_cast<uint8_t*>(p->f_stage.p);
     int* blk = reinterpret_cast<int*>(S + F.blk);
     int* lm_slot = reinterpret_cast<int*>(S + F.lm_slot);
@@ -1265,6 +1308,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         }
         for (int k : K[b]) loc[k] = -1;
     }
+    lap(10);
     int maxl = 1;
     for (int k = 0; k < nk; ++k) maxl = std::max(maxl, rank[k]);
     for (int b = 0; b < nb; ++b)
@@ -1300,8 +1344,13 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     p->fused = true;
     lap(2);
     if (timing)
+    {
         fprintf(stderr, "[vx plan] fused layout: pack %.3f ms, tables %.3f ms, upload + gather %.3f ms (%d workgroups x %d)\n",
                 t_ph[0], t_ph[1] - t_ph[0], t_ph[2] - t_ph[1], nb, ft);
+        fprintf(stderr, "[vx plan]   laps: pp %.3f order %.3f uk %.3f greedy %.3f owners %.3f po %.3f pass1 %.3f pinned %.3f tables %.3f ranks %.3f\n",
+                t_ph[3], t_ph[4] - t_ph[3], t_ph[5] - t_ph[4], t_ph[0] - t_ph[5], t_ph[6] - t_ph[0], t_ph[7] - t_ph[6],
+                t_ph[8] - t_ph[7], t_ph[9] - t_ph[8], t_ph[10] - t_ph[9], t_ph[1] - t_ph[10]);
+    }
     return VX_OK;
 }
 
@@ -1670,8 +1719,7 @@ int vx_ba_plan_create_ex(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_
         return set_error(c, VX_ERR_INVALID, "max_iterations must be in [0, %d]", kMaxIter);
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count)
         return set_error(c, VX_ERR_INVALID, "bad shard %d/%d", shard_rank, shard_count);
-    auto* p = new vx_ba_plan();
-    p->c = c;
+    auto* p = plan_new(c);
     p->opt = *opt;
     p->shard_rank = shard_rank;
     p->shard_count = shard_count;
@@ -1693,8 +1741,7 @@ int vx_ba_plan_create_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, con
         return set_error(c, VX_ERR_INVALID, "max_iterations must be in [0, %d]", kMaxIter);
     if (shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count)
         return set_error(c, VX_ERR_INVALID, "bad shard %d/%d", shard_rank, shard_count);
-    auto* p = new vx_ba_plan();
-    p->c = c;
+    auto* p = plan_new(c);
     p->opt = *opt;
     p->shard_rank = shard_rank;
     p->shard_count = shard_count;
@@ -1843,6 +1890,17 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
 }
 
 void vx_ba_plan_destroy(vx_ba_plan* p) {
+    if (!p) return;
+    vx_ctx* c = p->c;
+    if (c) {
+        auto& live = c->plan_live;
+        live.erase(std::remove(live.begin(), live.end(), p), live.end());
+        if (c->plan_husks.size() < kMaxPlanHusks) {  // park the buffers (no hipFree)
+            auto* h = new vx_ba_plan();
+            adopt_buffers(h, p);
+            c->plan_husks.push_back(h);
+        }
+    }
     delete p;
 }
 

@@ -47,7 +47,18 @@ struct vx_ba_plan {
 
 struct vx_dmap;
 
+// every buffer of a plan: vx_ba_plan_destroy parks them in the context (vx_ctx::plan_husks) and the
+// next plan of that context adopts them, so a LocalBA::Optimize per keyframe allocates and frees
+// nothing once the buffers have grown to the window's size (hipFree synchronises the device)
+#define VX_PLAN_BUFFERS(X)                                                                              \
+    X(kf_pose0) X(kf_pose) X(kf_intr) X(kf_rot) X(kf_flags) X(kf_obs_ptr) X(kf_part) X(kf_cost) X(lm_pos0) \
+    X(lm_pos) X(pobs_uv) X(pobs_lm) X(lobs_ptr) X(lobs_kf) X(lobs_lm) X(lm_blk) X(lobs_uv) X(state)       \
+    X(kf_map_dev) X(lm_map_dev) X(f_tab) X(f_lobs_uv) X(f_pobs_uv) X(f_pobs_p) X(f_part) X(f_rowpart)    \
+    X(f_stage)
+
 namespace vx {
+// a new plan of context c (buffers adopted from a parked plan when there is one)
+vx_ba_plan* plan_new(vx_ctx* c);
 #ifndef VX_BA_POSE_BLOCK  // build-time overrides for sweeps only (scripts/ba_variants.sh)
 #define VX_BA_POSE_BLOCK 512
 #endif

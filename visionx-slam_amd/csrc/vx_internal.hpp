@@ -199,6 +199,9 @@ struct vx_ctx {
         vx::DevBuf wptr, wlm, wfl, cam, wid, wuv, lid, bad, optr, okf, ofi, pos, hkey, hval, f_lm, f_pv, f_first,
             l_ref, l_opt, l_slot, l_first, counts, scan_a, scan_b, scan_c, inv, cnt, tmp;
     } plan_scratch;
+    // LocalBA plans of this context: parked buffer sets of destroyed plans (adopted by the next
+    // vx_ba_plan_create) and the live plans (detached when the context goes first)
+    std::vector<vx_ba_plan*> plan_husks, plan_live;
 
     // ---- hipGraph replay of the async entry points ($VX_GRAPHS=0 disables)
     vx::GraphCache graphs;
@@ -223,6 +226,8 @@ struct vx_ctx {
 namespace vx {
 
 int set_error(vx_ctx* c, int code, const char* fmt, ...);
+// frees the parked plan buffers and detaches the live plans of c (vx_destroy; ba.hip)
+void plan_pool_release(vx_ctx* c);
 int hip_fail(vx_ctx* c, hipError_t e, const char* what);
 
 // Event bracket around launches of one stage (no-op when profiling is off).
