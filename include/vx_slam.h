@@ -239,6 +239,11 @@ int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out8);
  * keyframe}.  A sharded plan runs the fused kernel only when every rank has the layout (decided by
  * one all-reduce on its first run). */
 int vx_ba_plan_layout(const vx_ba_plan* plan, int64_t* out4);
+/* Test hook: the fused layout's index tables (workgroup headers, landmark slots and runs,
+ * landmark-stage records, keyframe entries, landmark- and pose-stage observation sources, pose
+ * codes) copied back to back into dst; *bytes = their total size (dst NULL: the size only).  The
+ * device build of the layout must equal the host packing (VX_PLAN_HOST_BUILD) byte for byte. */
+int vx_ba_plan_fused_tables(vx_ctx* ctx, const vx_ba_plan* plan, void* dst, size_t cap, size_t* bytes);
 /* Test hook: runs the n shard plans plans[r] (shard r of n, built from one window, all on ctx) the
  * way n ranks would run them, on one device: per iteration every shard's pose stage, then the
  * element-wise sum of their partial blocks in rank order written back to every shard in place of

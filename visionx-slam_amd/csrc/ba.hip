@@ -50,14 +50,14 @@ using namespace vx::ba;
 
 constexpr int kPoseBlock = kBaPoseBlock;  // threads per pose-stage workgroup
 constexpr int kNTerms = 29;      // 21 H (upper) + 6 b + cost + count
-constexpr int kStride = 32;      // doubles per keyframe block in global memory
+constexpr int kStride = kBaStride;  // doubles per keyframe block in global memory
 // LDS slot stride of k_landmark_solve: 33, not 32 doubles — a 256-B stride is one full turn of the
 // 64 four-byte LDS banks, so lanes reading different keyframes' slots would all hit one bank
 constexpr int kLdsStride = 33;
 constexpr int kMaxIter = 64;
 // keyframes whose LDS slots fit k_landmark_solve: 448 * 33 * 8 B + kLmBlock * (9 * 8 + 4) B =
 // 157,184 B of gfx950's 160 KB per workgroup
-constexpr int kMaxKfLds = 448;
+constexpr int kMaxKfLds = kBaMaxKfLds;
 constexpr int kMaxSplit = kBaMaxSplit;    // pose-stage workgroups per keyframe
 constexpr int kCombine = 6;      // (keyframe, term) pairs per thread per combine pass
 constexpr int kLmBlock = kBaLmBlock;      // k_landmark_solve: threads = max observations = max landmarks
@@ -627,7 +627,7 @@ constexpr int kFK = kBaFusedK;
 // Threads per fused workgroup (= its landmark-stage observation / landmark capacity): 512, or 1024
 // for windows whose 512-thread packing needs more workgroups than the device has CUs (fewer,
 // larger workgroups: shorter per-keyframe slot lists; measured).
-constexpr int kFTSmall = 512, kFTLarge = 1024;
+constexpr int kFTSmall = kBaFTSmall, kFTLarge = kBaFTLarge;
 
 // Fused layout (ba.hip build_fused).  Per workgroup b: landmarks and landmark-stage observations at
 // the fixed bases b * kFT (padded), so their loads do not wait for the workgroup table; keyframe
@@ -1059,6 +1059,69 @@ void plan_pool_release(vx_ctx* c) {
     c->plan_live.clear();
 }
 
+bool fused_eligible(const vx_ba_plan* p) {
+    if (p->status != 0 || p->global_poses || p->n_kf > kMaxKfLds || p->n_opt <= 0) return false;
+    if (const char* e = getenv("VX_BA_FUSED"))
+        if (e[0] == '0') return false;
+    return true;
+}
+
+// 1024 threads when 512-thread workgroups would outnumber the compute units (their count is within a
+// few percent of the landmark-stage observations / 512: whole landmarks of <= 5 observations);
+// VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps
+int fused_threads(vx_ctx* c, int64_t n_lobs, int* cap) {
+    if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
+    int ft = n_lobs > (int64_t)c->n_cus * (kFTSmall - 16) ? kFTLarge : kFTSmall;
+    if (const char* e = getenv("VX_BA_FUSED_THREADS")) ft = atoi(e) == kFTLarge ? kFTLarge : kFTSmall;
+    *cap = ft;
+    if (const char* e = getenv("VX_BA_FUSED_CAP")) *cap = std::min(ft, std::max(64, atoi(e)));
+    return ft;
+}
+
+size_t fused_offsets(int nb, int ft, size_t n_pp, FusedOffsets& F) {
+    const size_t n_lp = (size_t)nb * ft;
+    size_t at = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = at;
+        at += (bytes + 255) & ~(size_t)255;
+        return o;
+    };
+    F.blk = take((size_t)nb * fused_blk_ints(ft) * 4);
+    F.lm_slot = take(n_lp * 4);
+    F.lm_run = take(n_lp * 8);
+    F.lobs_rec = take(n_lp * 16);
+    F.kent = take((size_t)nb * kFK * 32);
+    F.lobs_src = take(n_lp * 4);
+    F.pobs_src = take(std::max<size_t>(n_pp, 1) * 4);
+    F.pobs_code = take(std::max<size_t>(n_pp, 1) * 4);
+    return at;
+}
+
+int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp) {
+    const FusedOffsets& F = p->f_off;
+    const size_t n_lp = (size_t)nb * ft;
+    const uint8_t* T = p->f_tab.as<uint8_t>();
+    VX_HIP(c, p->f_lobs_uv.ensure(n_lp * sizeof(double2)));
+    VX_HIP(c, p->f_pobs_uv.ensure(std::max<size_t>(n_pp, 1) * sizeof(double2)));
+    VX_HIP(c, p->f_pobs_p.ensure(std::max<size_t>(n_pp, 1) * sizeof(double4)));
+    hipLaunchKernelGGL(k_fused_gather, dim3((unsigned)((std::max(n_lp, n_pp) + 255) / 256)), dim3(256), 0, c->stream,
+                       reinterpret_cast<const int*>(T + F.lobs_src), (int)n_lp, (const double2*)p->lobs_uv.as<double2>(),
+                       p->f_lobs_uv.as<double2>(), reinterpret_cast<const int*>(T + F.pobs_src),
+                       reinterpret_cast<const int*>(T + F.pobs_code), (int)n_pp, (const double2*)p->pobs_uv.as<double2>(),
+                       (const double*)p->lm_pos0.as<double>(), p->f_pobs_uv.as<double2>(), p->f_pobs_p.as<double4>());
+    VX_LAUNCH_CHECK(c, "k_fused_gather");
+    const size_t part_bytes = 2 * (size_t)p->n_kf * maxl * kStride * sizeof(double);
+    VX_HIP(c, p->f_part.ensure(part_bytes));
+    if (p->shard_count > 1) VX_HIP(c, p->f_rowpart.ensure((size_t)p->n_kf * kStride * sizeof(double)));
+    VX_HIP(c, hipMemsetAsync(p->f_part.p, 0, part_bytes, c->stream));  // slots no group writes stay 0
+    p->f_blocks = nb;
+    p->f_maxl = maxl;
+    p->f_threads = ft;
+    p->f_npp = n_pp;
+    p->fused = true;
+    return VX_OK;
+}
+
 // The fused layout (k_ba_iter) from the plan's CSRs, on the host: both plan builders end here with
 // the same arrays, so the layout — and every run — is the same for both.
 //   1. optimised landmarks ordered by the first window keyframe that observes them (stable), so a
@@ -1074,9 +1137,7 @@ void plan_pool_release(vx_ctx* c) {
 int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const std::vector<int>& plm,
                 const std::vector<int>& lptr, const std::vector<int>& lkf) {
     p->fused = false;
-    if (p->status != 0 || p->global_poses || p->n_kf > kMaxKfLds || p->n_opt <= 0) return VX_OK;
-    if (const char* e = getenv("VX_BA_FUSED"))
-        if (e[0] == '0') return VX_OK;
+    if (!fused_eligible(p)) return VX_OK;
     const int nk = p->n_kf, n_opt = p->n_opt, n_pose = kptr[nk];
     // $VX_PLAN_TIMING=1: phase times of this build on stderr (scripts/plan_build_time.py)
     static const bool timing = getenv("VX_PLAN_TIMING") != nullptr;
@@ -1138,11 +1199,8 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     // workgroup; VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps).  1024
     // threads when 512-thread workgroups would outnumber the compute units (their count is within a
     // few percent of the landmark-stage observations / 512: whole landmarks of <= 5 observations)
-    if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
-    int ft = (int64_t)lptr[n_opt] > (int64_t)c->n_cus * (kFTSmall - 16) ? kFTLarge : kFTSmall;
-    if (const char* e = getenv("VX_BA_FUSED_THREADS")) ft = atoi(e) == kFTLarge ? kFTLarge : kFTSmall;
-    int cap = ft;
-    if (const char* e = getenv("VX_BA_FUSED_CAP")) cap = std::min(ft, std::max(64, atoi(e)));
+    int cap = 0;
+    const int ft = fused_threads(c, lptr[n_opt], &cap);
     std::vector<std::vector<int>> K(1), LM(1);
     std::vector<int> stamp(nk, -1);
     int n_l = 0, n_o = 0;
@@ -1206,7 +1264,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     // tables: landmarks / landmark-stage observations at b * ft, keyframe entries at b * kFK,
     // pose observations wave-major with 64-aligned entries.  Written straight into one pinned
     // staging block and uploaded with one copy (the build is paid per LocalBA::Optimize call).
-    const int kBlkInts = 4 * (1 + fw / 2);
+    const int kBlkInts = fused_blk_ints(ft);
     lap(7);
     // pass 1: each entry's pose observations, the waves' rounds
     std::vector<int> ent_beg((size_t)nb * kFK, 0), ent_end((size_t)nb * kFK, 0);
@@ -1221,22 +1279,8 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         }
         if (i != po_ptr[b + 1]) return set_error(c, VX_ERR_STATE, "fused layout: pose observations out of keyframe order");
     }
-    const size_t n_lp = (size_t)nb * ft;
     FusedOffsets& F = p->f_off;
-    size_t at = 0;
-    auto take = [&](size_t bytes) {
-        const size_t o = at;
-        at += (bytes + 255) & ~(size_t)255;
-        return o;
-    };
-    F.blk = take((size_t)nb * kBlkInts * 4);
-    F.lm_slot = take(n_lp * 4);
-    F.lm_run = take(n_lp * 8);
-    F.lobs_rec = take(n_lp * 16);
-    F.kent = take((size_t)nb * kFK * 32);
-    F.lobs_src = take(n_lp * 4);
-    F.pobs_src = take(std::max<size_t>(n_pp, 1) * 4);
-    F.pobs_code = take(std::max<size_t>(n_pp, 1) * 4);
+    const size_t at = fused_offsets(nb, ft, n_pp, F);
     lap(8);
     VX_HIP(c, p->f_stage.ensure(at, true));
     lap(9);
@@ -1323,25 +1367,9 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     // one upload, then the observation payloads gathered into the fused order
     VX_HIP(c, p->f_tab.ensure(at));
     VX_HIP(c, hipMemcpyAsync(p->f_tab.p, S, at, hipMemcpyHostToDevice, c->stream));
-    const uint8_t* T = p->f_tab.as<uint8_t>();
-    VX_HIP(c, p->f_lobs_uv.ensure(n_lp * sizeof(double2)));
-    VX_HIP(c, p->f_pobs_uv.ensure(std::max<size_t>(n_pp, 1) * sizeof(double2)));
-    VX_HIP(c, p->f_pobs_p.ensure(std::max<size_t>(n_pp, 1) * sizeof(double4)));
-    hipLaunchKernelGGL(k_fused_gather, dim3((unsigned)((std::max(n_lp, n_pp) + 255) / 256)), dim3(256), 0, c->stream,
-                       reinterpret_cast<const int*>(T + F.lobs_src), (int)n_lp, (const double2*)p->lobs_uv.as<double2>(),
-                       p->f_lobs_uv.as<double2>(), reinterpret_cast<const int*>(T + F.pobs_src),
-                       reinterpret_cast<const int*>(T + F.pobs_code), (int)n_pp, (const double2*)p->pobs_uv.as<double2>(),
-                       (const double*)p->lm_pos0.as<double>(), p->f_pobs_uv.as<double2>(), p->f_pobs_p.as<double4>());
-    VX_LAUNCH_CHECK(c, "k_fused_gather");
-    const size_t part_bytes = 2 * (size_t)nk * maxl * kStride * sizeof(double);
-    VX_HIP(c, p->f_part.ensure(part_bytes));
-    if (p->shard_count > 1) VX_HIP(c, p->f_rowpart.ensure((size_t)nk * kStride * sizeof(double)));
-    VX_HIP(c, hipMemsetAsync(p->f_part.p, 0, part_bytes, c->stream));  // slots no group writes stay 0
+    int rc;
+    if ((rc = fused_finish(c, p, nb, ft, maxl, n_pp))) return rc;
     VX_HIP(c, hipStreamSynchronize(c->stream));  // (the staging block is reused by the next build)
-    p->f_blocks = nb;
-    p->f_maxl = maxl;
-    p->f_threads = ft;
-    p->fused = true;
     lap(2);
     if (timing)
     {
@@ -1946,6 +1974,37 @@ int vx_ba_plan_layout(const vx_ba_plan* p, int64_t* out4) {
     out4[1] = p->fused ? p->f_threads : 0;
     out4[2] = p->fused ? p->f_blocks : 0;
     out4[3] = p->fused ? p->f_maxl : 0;
+    return VX_OK;
+}
+
+int vx_ba_plan_fused_tables(vx_ctx* c, const vx_ba_plan* p, void* dst, size_t cap, size_t* bytes) {
+    if (!c || !p || !bytes || p->c != c) return VX_ERR_INVALID;
+    if (!p->fused) return set_error(c, VX_ERR_STATE, "plan has no fused layout");
+    const FusedOffsets& F = p->f_off;
+    const size_t n_lp = (size_t)p->f_blocks * p->f_threads;
+    const std::pair<size_t, size_t> part[] = {
+        {F.blk, (size_t)p->f_blocks * fused_blk_ints(p->f_threads) * 4},
+        {F.lm_slot, n_lp * 4},
+        {F.lm_run, n_lp * 8},
+        {F.lobs_rec, n_lp * 16},
+        {F.kent, (size_t)p->f_blocks * kFK * 32},
+        {F.lobs_src, n_lp * 4},
+        {F.pobs_src, p->f_npp * 4},
+        {F.pobs_code, p->f_npp * 4}};
+    size_t total = 0;
+    for (const auto& x : part) total += x.second;
+    *bytes = total;
+    if (!dst) return VX_OK;
+    if (cap < total) return VX_ERR_CAPACITY;
+    VX_HIP(c, hipSetDevice(c->device));
+    size_t at = 0;
+    for (const auto& x : part) {
+        if (x.second)
+            VX_HIP(c, hipMemcpyAsync(static_cast<uint8_t*>(dst) + at, p->f_tab.as<uint8_t>() + x.first, x.second,
+                                     hipMemcpyDeviceToHost, c->stream));
+        at += x.second;
+    }
+    VX_HIP(c, hipStreamSynchronize(c->stream));
     return VX_OK;
 }
 

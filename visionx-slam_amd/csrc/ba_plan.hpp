@@ -43,6 +43,7 @@ struct vx_ba_plan {
     vx::DevBuf f_rowpart;                                         // sharded: all-reduced per-row partials
     vx::PinnedBuf f_stage;                                        // their host staging block
     FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
+    size_t f_npp = 0;                                             // pose-observation positions (padded)
 };
 
 struct vx_dmap;
@@ -86,7 +87,24 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p);
 // does not fit it (sharded plans, a workgroup needing more than kBaFusedK keyframes)
 int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kf_obs_ptr, const std::vector<int>& plm,
                 const std::vector<int>& lptr, const std::vector<int>& lkf);
+// the same layout built on the device from the plan's device CSRs (ba_fused_build.hip): same tables,
+// byte for byte (tests/test_gpu_fused_build.py), without the CSR download or host packing
+int build_fused_device(vx_ctx* c, vx_ba_plan* p);
 constexpr int kBaFusedK = 64;      // keyframes per fused workgroup
+constexpr int kBaFTSmall = 512, kBaFTLarge = 1024;  // threads per fused workgroup
+constexpr int kBaStride = 32;      // doubles per partial block
+constexpr int kBaMaxKfLds = 448;   // most window keyframes of the LDS-pose / fused kernels
+// whether the plan can take the fused layout at all (window size, options, $VX_BA_FUSED)
+bool fused_eligible(const vx_ba_plan* p);
+// threads per fused workgroup for n_lobs landmark-stage observations (and the packing cap)
+int fused_threads(vx_ctx* c, int64_t n_lobs, int* cap);
+// table offsets in f_tab for nb workgroups of ft threads and n_pp pose-observation positions; returns
+// the block's bytes
+size_t fused_offsets(int nb, int ft, size_t n_pp, FusedOffsets& F);
+inline int fused_blk_ints(int ft) { return 4 * (1 + ft / 64 / 2); }
+// after the tables are in f_tab: the observation payloads gathered into the fused order, the
+// partial buffers cleared, the layout enabled
+int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp);
 // SelectKeyFrames + landmark set + both CSRs built on the device from the map snapshot (§8f rank 2)
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
 // the same plan from a device-resident map (vx_dmap; its CSR rebuilt first if stale)

@@ -498,22 +498,8 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
     if ((rc = alloc_run_buffers(c, p))) return rc;
     VX_HIP(c, hipStreamSynchronize(s));  // the host vectors above must outlive their async copies
-    {  // every plan, sharded ones included (their ranks all-reduce the fused layout's row sums)
-        static const bool timing = getenv("VX_PLAN_TIMING") != nullptr;
-        const auto t0 = std::chrono::steady_clock::now();
-        // host copies of the CSR index arrays for the fused layout (ba.hip build_fused)
-        std::vector<int> kptr(nk + 1), plm(std::max(n_pose, 1)), lkf(std::max(n_lobs, 1));
-        VX_HIP(c, hipMemcpyAsync(kptr.data(), p->kf_obs_ptr.p, (size_t)(nk + 1) * 4, hipMemcpyDeviceToHost, s));
-        if (n_pose) VX_HIP(c, hipMemcpyAsync(plm.data(), p->pobs_lm.p, (size_t)n_pose * 4, hipMemcpyDeviceToHost, s));
-        if (n_lobs) VX_HIP(c, hipMemcpyAsync(lkf.data(), p->lobs_kf.p, (size_t)n_lobs * 4, hipMemcpyDeviceToHost, s));
-        VX_HIP(c, hipStreamSynchronize(s));
-        plm.resize(n_pose);
-        lkf.resize(n_lobs);
-        if (timing)
-            fprintf(stderr, "[vx plan] CSR download for the fused layout %.3f ms\n",
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-        if ((rc = build_fused(c, p, kptr, plm, lptr, lkf))) return rc;
-    }
+    // the fused layout, on the device from the CSRs just built (every plan, sharded ones included)
+    if ((rc = build_fused_device(c, p))) return rc;
     return VX_OK;
 }
 }  // namespace

@@ -79,7 +79,7 @@ EXPORTS = [
     "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
     "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
     "vx_match_device_async", "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
-    "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info", "vx_ba_plan_layout",
+    "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info", "vx_ba_plan_layout", "vx_ba_plan_fused_tables",
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
@@ -590,6 +590,14 @@ class BAPlan:
         out = np.zeros(4, np.int64)
         self.ctx._check(lib().vx_ba_plan_layout(self._h, _p(out)))
         return {k: int(v) for k, v in zip(["fused", "threads", "workgroups", "max_slots"], out)}
+
+    def fused_tables(self) -> bytes:
+        """vx_ba_plan_fused_tables: the fused layout's index tables, back to back (test hook)."""
+        n = C.c_size_t(0)
+        self.ctx._check(lib().vx_ba_plan_fused_tables(self.ctx.handle, self._h, None, C.c_size_t(0), C.byref(n)))
+        buf = np.zeros(n.value, np.uint8)
+        self.ctx._check(lib().vx_ba_plan_fused_tables(self.ctx.handle, self._h, _p(buf), n, C.byref(n)))
+        return buf.tobytes()
 
     def run_async(self):
         self.ctx._check(lib().vx_ba_plan_run_async(self.ctx.handle, self._h))
