@@ -37,7 +37,7 @@ constexpr int kT = 256;
 constexpr int kFK = kBaFusedK;
 constexpr int kMaxW = (kBaMaxKfLds + 63) / 64;  // 64-bit words of a keyframe set
 constexpr int kChainWin = 12288;                 // next[] window of the chain walk (ints of LDS)
-constexpr int kMaxGroupsRank = 16384;            // workgroup counters per keyframe wave (LDS)
+constexpr int kMaxGroupsRank = 8192;             // workgroup counters of k_fb_pose_rank (LDS)
 constexpr int kMaxWaves = kBaFTLarge / 64;
 static_assert(kBaFTLarge <= kChainWin / 2, "the chain walk advances at most cap landmarks per step");
 
@@ -57,8 +57,9 @@ __device__ __forceinline__ int popc_below(const u64* m, int W, int k) {
     return r;
 }
 
-__global__ void k_fb_init(int n_opt, int nk, int W, int* key, int* iota, u64* mask, int* owner) {
+__global__ void k_fb_init(int n_opt, int nk, int W, int* key, int* iota, u64* mask, int* owner, int* counters) {
     const int i = blockIdx.x * kT + threadIdx.x;
+    if (i < 16) counters[i] = 0;
     if (i < n_opt) {
         key[i] = nk;
         iota[i] = i;
@@ -99,52 +100,74 @@ __global__ void k_fb_mask(int n_lobs, const int* llm, const int* lkf, int n_pose
 
 // sorted-order copies of the observation counts and keyframe sets; the landmarks that can never
 // fit a workgroup (more observations than threads, more keyframes than entries)
-__global__ void k_fb_sorted(const int* order, int n_opt, const int* lptr, const u64* mask, int W, int ft,
-                            int* cntS, u64* maskS, int* counters) {
+__global__ void k_fb_sorted(const int* order, const int* firstS, int n_opt, const int* lptr, const u64* mask, int W,
+                            int ft, int* cntS, u64* maskS, int* counters) {
     const int i = blockIdx.x * kT + threadIdx.x;
     if (i == 0) cntS[n_opt] = 0;
     if (i >= n_opt) return;
     const int q = order[i];
     const int c = lptr[q + 1] - lptr[q];
     cntS[i] = c;
-    int pc = 0;
+    int pc = 0, last = -1;
     for (int w = 0; w < W; ++w) {
         const u64 m = mask[(size_t)q * W + w];
         maskS[(size_t)i * W + w] = m;
         pc += __popcll(m);
+        if (m) last = 64 * w + 63 - __clzll((long long)m);
     }
     int f = 0;
     if (c > ft) f |= kFailObs;
     if (pc > kFK) f |= kFailLmKf;
     if (f) atomicOr(&counters[1], f);
+    if (last >= 0) atomicMax(&counters[3], last - firstS[i]);  // widest keyframe span of a landmark
 }
 
 // next[i]: the end of the greedy workgroup that starts at sorted landmark i (build_fused step 2:
 // break before a landmark when the group is non-empty and one more landmark, its observations or its
 // new keyframes would exceed cap, cap, kFK).  The landmarks i .. i + cap - 1 of the block's threads
-// are staged in LDS: counts, then the W words of their keyframe sets.
-__global__ __launch_bounds__(kT) void k_fb_next(const int* cntS, const u64* maskS, int n_opt, int W, int cap,
-                                               int* next) {
+// are staged in LDS (observation prefix sums, first keyframes, keyframe sets).  The landmark and
+// observation caps alone give an end j1 by binary search over the prefix sums; the keyframe cap
+// cannot bind before j1 when every keyframe of [i, j1) lies in [first(i), first(j1 - 1) + span]
+// (landmarks sorted by first keyframe; span = the widest landmark, counters[3]) spans at most kFK
+// rows — otherwise the thread replays the greedy over the staged sets.
+__global__ __launch_bounds__(kT) void k_fb_next(const int* cntScan, const int* firstS, const u64* maskS, int n_opt,
+                                               int W, int cap, const int* counters, int* next) {
     extern __shared__ u64 fb_lds[];
     const int span_cap = kT + cap;
-    u64* mL = fb_lds;                                            // [W][span_cap]
-    int* cL = reinterpret_cast<int*>(fb_lds + (size_t)W * span_cap);  // [span_cap]
+    u64* mL = fb_lds;                                                 // [W][span_cap]
+    int* cs = reinterpret_cast<int*>(fb_lds + (size_t)W * span_cap);  // [span_cap + 1]
+    int* fs = cs + span_cap + 1;                                      // [span_cap]
     const int base = blockIdx.x * kT;
     const int span = min(n_opt - base, span_cap);
-    for (int i = threadIdx.x; i < span; i += kT) {
-        cL[i] = cntS[base + i];
-        for (int w = 0; w < W; ++w) mL[(size_t)w * span_cap + i] = maskS[(size_t)(base + i) * W + w];
+    for (int i = threadIdx.x; i <= span; i += kT) {
+        cs[i] = cntScan[base + i];
+        if (i < span) {
+            fs[i] = firstS[base + i];
+            for (int w = 0; w < W; ++w) mL[(size_t)w * span_cap + i] = maskS[(size_t)(base + i) * W + w];
+        }
     }
     __syncthreads();
     const int t = threadIdx.x;
     if (base + t >= n_opt) return;
+    const int hi = min(t + cap, span);
+    int lo = t + 1, h = hi;  // smallest j in (t, hi) whose observations overflow the group, else hi
+    while (lo < h) {
+        const int mid = (lo + h) >> 1;
+        if (cs[mid + 1] - cs[t] > cap) h = mid;
+        else lo = mid + 1;
+    }
+    const int j1 = lo;
+    if (fs[j1 - 1] + counters[3] - fs[t] + 1 <= kFK) {
+        next[base + t] = base + j1;
+        return;
+    }
     u64 cur[kMaxW];
 #pragma unroll
     for (int w = 0; w < kMaxW; ++w) cur[w] = 0;
     int nl = 0, no = 0, kc = 0, i = t;
     for (; i < span; ++i) {
         if (nl >= cap) break;
-        const int c = cL[i];
+        const int c = cs[i + 1] - cs[i];
         u64 m[kMaxW];
         int nn = 0;
 #pragma unroll
@@ -194,10 +217,15 @@ __global__ __launch_bounds__(1024) void k_fb_chain(const int* next, int n, int* 
 
 // per workgroup: its landmarks' workgroup / local index, its keyframe set, keyframe owners
 __global__ __launch_bounds__(kT) void k_fb_group(const int* starts, const int* order, const u64* maskS, int W,
-                                                int nk, int* lm_blk, int* lm_loc, u64* gmask, int* owner) {
+                                                int nk, int* lm_blk, int* lm_loc, u64* gmask, int* owner, int* cntE,
+                                                int* erank) {
     __shared__ u64 gm[kMaxW];
     const int b = blockIdx.x;
     if (threadIdx.x < kMaxW) gm[threadIdx.x] = 0;
+    if (threadIdx.x < kFK) {  // entry sizes and slot ranks, filled by k_fb_pose_rank
+        cntE[(size_t)b * kFK + threadIdx.x] = 0;
+        erank[(size_t)b * kFK + threadIdx.x] = -1;
+    }
     __syncthreads();
     const int s = starts[b], e = starts[b + 1];
     u64 loc[kMaxW];
@@ -239,47 +267,73 @@ __global__ __launch_bounds__(kT) void k_fb_owner0(int nk, int W, int* owner, u64
     }
 }
 
-// one wave per keyframe row k: its pose observations (ascending index) split by workgroup — an
+// one workgroup per keyframe row k: its pose observations (ascending index) split by workgroup — an
 // optimised landmark's observation goes to the landmark's workgroup, a fixed landmark's to the
-// keyframe's owner — with their rank inside the (workgroup, keyframe) entry; then the entry sizes
-// and each entry's partial-slot rank among the keyframe's non-empty entries (workgroup order)
-__global__ __launch_bounds__(64) void k_fb_pose_rank(const int* kptr, const int* plm, int n_opt, const int* lm_blk,
-                                                    const int* owner, int nb, const u64* gmask, int W, int* pblk,
-                                                    int* prank, int* cntE, int* erank, int* rankk, int* counters) {
-    extern __shared__ int cb[];  // [nb] observations so far per workgroup
-    const int k = blockIdx.x, lane = threadIdx.x;
-    for (int i = lane; i < nb; i += 64) cb[i] = 0;
-    __syncthreads();
+// keyframe's owner — with their rank inside the (workgroup, keyframe) entry; then the entry sizes and
+// each entry's partial-slot rank among the keyframe's non-empty entries (workgroup order).  The S
+// waves take consecutive segments: per wave counts by workgroup (a ballot per distinct workgroup of
+// a 64-observation chunk), their exclusive prefix over the waves, then the ranks.
+__device__ __forceinline__ void rank_chunk(int b, bool valid, int lane, int* cnt, int* prank, int* pblk, int o) {
     const u64 lt = (1ull << lane) - 1;
-    const int o0 = kptr[k], o1 = kptr[k + 1], own = owner[k];
-    for (int base = o0; base < o1; base += 64) {
-        const int o = base + lane;
-        const bool valid = o < o1;
-        int b = -1;
-        if (valid) {
-            const int q = plm[o];
-            b = q < n_opt ? lm_blk[q] : own;
+    u64 act = __ballot(valid);
+    while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int bl = __shfl(b, leader);
+        const u64 m = __ballot(valid && b == bl);
+        const int c0 = cnt[bl];
+        if (prank && valid && b == bl) {
+            prank[o] = c0 + __popcll(m & lt);
+            pblk[o] = bl;
         }
-        u64 act = __ballot(valid);
-        while (act) {
-            const int leader = __ffsll((long long)act) - 1;
-            const int bl = __shfl(b, leader);
-            const u64 m = __ballot(valid && b == bl);
-            const int c0 = cb[bl];
-            if (valid && b == bl) {
-                prank[o] = c0 + __popcll(m & lt);
-                pblk[o] = bl;
+        if (lane == leader) cnt[bl] = c0 + __popcll(m);  // (one wave: LDS accesses in program order)
+        act &= ~m;
+    }
+}
+
+__global__ __launch_bounds__(512) void k_fb_pose_rank(const int* kptr, const int* plm, int n_opt, const int* lm_blk,
+                                                     const int* owner, int nb, const u64* gmask, int W, int* pblk,
+                                                     int* prank, int* cntE, int* erank, int* rankk, int* counters) {
+    extern __shared__ int cb[];  // [S][nb] per-wave counts, then [nb] totals
+    const int S = blockDim.x >> 6;
+    const int k = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int* tot = cb + (size_t)S * nb;
+    for (int i = threadIdx.x; i < (S + 1) * nb; i += blockDim.x) cb[i] = 0;
+    __syncthreads();
+    const int o0 = kptr[k], o1 = kptr[k + 1], own = owner[k];
+    const int seg = ((o1 - o0 + S - 1) / S + 63) & ~63;
+    const int s0 = min(o1, o0 + wv * seg), s1 = min(o1, s0 + seg);
+    int* mine = cb + (size_t)wv * nb;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int base = s0; base < s1; base += 64) {
+            const int o = base + lane;
+            const bool valid = o < s1;
+            int b = -1;
+            if (valid) {
+                const int q = plm[o];
+                b = q < n_opt ? lm_blk[q] : own;
             }
-            __syncthreads();  // (one wave: orders the read above before the update)
-            if (lane == leader) cb[bl] = c0 + __popcll(m);
+            rank_chunk(b, valid, lane, mine, pass ? prank : nullptr, pblk, o);
+        }
+        __syncthreads();
+        if (pass == 0) {  // counts -> exclusive prefix over the waves; totals
+            for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+                int run = 0;
+                for (int w = 0; w < S; ++w) {
+                    const int c = cb[(size_t)w * nb + b];
+                    cb[(size_t)w * nb + b] = run;
+                    run += c;
+                }
+                tot[b] = run;
+            }
             __syncthreads();
-            act &= ~m;
         }
     }
+    if (wv != 0) return;
+    const u64 lt = (1ull << lane) - 1;
     int run = 0;
     for (int bb = 0; bb < nb; bb += 64) {
         const int b = bb + lane;
-        const int c = b < nb ? cb[b] : 0;
+        const int c = b < nb ? tot[b] : 0;
         const u64 m = __ballot(c > 0);
         if (c > 0) {
             const int j = popc_below(gmask + (size_t)b * W, W, k);
@@ -472,7 +526,7 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
 
     // ---- per-landmark / per-observation scratch
     const size_t no = (size_t)n_opt, np = (size_t)std::max(n_pose, 1);
-    size_t need = carve_bytes<int>(np) * 3 + carve_bytes<int>(no) * 6 + carve_bytes<u64>(no * W) * 2 +
+    size_t need = carve_bytes<int>(np) * 3 + carve_bytes<int>(no) * 7 + carve_bytes<u64>(no * W) * 2 +
                   carve_bytes<int>(no + 1) * 3 + carve_bytes<int>(nk) * 2 + carve_bytes<int>(16);
     VX_HIP(c, S.fb.ensure(need));
     Carve cv{S.fb.as<uint8_t>()};
@@ -493,10 +547,10 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     int* owner = cv.take<int>(nk);
     int* rankk = cv.take<int>(nk);
     int* counters = cv.take<int>(16);
-    int* next = keys2;  // (the sorted keys are not needed after the sort)
+    int* next = cv.take<int>(no);
 
-    VX_HIP(c, hipMemsetAsync(counters, 0, 16 * sizeof(int), s));
-    hipLaunchKernelGGL(k_fb_init, dim3(grid(std::max(n_opt, nk))), dim3(kT), 0, s, n_opt, nk, W, key, iota, mask, owner);
+    hipLaunchKernelGGL(k_fb_init, dim3(grid(std::max(std::max(n_opt, nk), 16))), dim3(kT), 0, s, n_opt, nk, W, key, iota,
+                       mask, owner, counters);
     hipLaunchKernelGGL(k_fb_pkf, dim3(grid(n_pose)), dim3(kT), 0, s, kptr, nk, n_pose, pkf);
     hipLaunchKernelGGL(k_fb_mask, dim3(grid(std::max(n_lobs, n_pose))), dim3(kT), 0, s, n_lobs, llm, lkf, n_pose, plm,
                        (const int*)pkf, n_opt, W, key, mask);
@@ -509,17 +563,17 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     VX_HIP(c, rocprim::exclusive_scan(nullptr, tb2, cntS, cntScan, 0, no + 1, rocprim::plus<int>(), s));
     VX_HIP(c, S.fb_tmp.ensure(std::max<size_t>(std::max(tb, tb2), 16)));
     VX_HIP(c, rocprim::radix_sort_pairs(S.fb_tmp.p, tb, key, keys2, iota, order, no, 0, bits, s));
-    hipLaunchKernelGGL(k_fb_sorted, dim3(grid(n_opt)), dim3(kT), 0, s, (const int*)order, n_opt, lptr,
-                       (const u64*)mask, W, ft, cntS, maskS, counters);
+    hipLaunchKernelGGL(k_fb_sorted, dim3(grid(n_opt)), dim3(kT), 0, s, (const int*)order, (const int*)keys2, n_opt,
+                       lptr, (const u64*)mask, W, ft, cntS, maskS, counters);
     VX_LAUNCH_CHECK(c, "fused build: sorted order");
     VX_HIP(c, rocprim::exclusive_scan(S.fb_tmp.p, tb2, cntS, cntScan, 0, no + 1, rocprim::plus<int>(), s));
-    const size_t next_lds = (size_t)(kT + cap) * (W * sizeof(u64) + sizeof(int));
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_fb_next),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)((kT + kBaFTLarge) * (kMaxW * sizeof(u64) + sizeof(int))));
+    const size_t next_lds = (size_t)(kT + cap) * (W * sizeof(u64) + 2 * sizeof(int)) + sizeof(int);
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&k_fb_next), hipFuncAttributeMaxDynamicSharedMemorySize,
+        (int)((kT + kBaFTLarge) * (kMaxW * sizeof(u64) + 2 * sizeof(int)) + sizeof(int)));
     VX_HIP(c, attr);
-    hipLaunchKernelGGL(k_fb_next, dim3(grid(n_opt)), dim3(kT), (uint32_t)next_lds, s, (const int*)cntS,
-                       (const u64*)maskS, n_opt, W, cap, next);
+    hipLaunchKernelGGL(k_fb_next, dim3(grid(n_opt)), dim3(kT), (uint32_t)next_lds, s, (const int*)cntScan,
+                       (const int*)keys2, (const u64*)maskS, n_opt, W, cap, (const int*)counters, next);
     hipLaunchKernelGGL(k_fb_chain, dim3(1), dim3(1024), 0, s, (const int*)next, n_opt, starts, counters);
     VX_LAUNCH_CHECK(c, "fused build: packing");
     VX_HIP(c, S.fb_host.ensure(64));
@@ -544,12 +598,11 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     int* wrd = cg.take<int>(nbs * kMaxWaves);
     int* G = cg.take<int>(nbs + 1);
     int* gbase = cg.take<int>(nbs + 1);
-    VX_HIP(c, hipMemsetAsync(cntE, 0, nbs * kFK * sizeof(int), s));
-    VX_HIP(c, hipMemsetAsync(erank, 0xff, nbs * kFK * sizeof(int), s));
     hipLaunchKernelGGL(k_fb_group, dim3(nb), dim3(kT), 0, s, (const int*)starts, (const int*)order, (const u64*)maskS,
-                       W, nk, lm_blk, lm_loc, gmask, owner);
+                       W, nk, lm_blk, lm_loc, gmask, owner, cntE, erank);
     hipLaunchKernelGGL(k_fb_owner0, dim3(1), dim3(kT), 0, s, nk, W, owner, gmask, counters);
-    hipLaunchKernelGGL(k_fb_pose_rank, dim3(nk), dim3(64), (uint32_t)(nbs * sizeof(int)), s, kptr, plm, n_opt,
+    const int nw = std::max(1, std::min(8, kMaxGroupsRank * 2 / nb - 1));  // waves per keyframe: (nw + 1) x nb ints of LDS
+    hipLaunchKernelGGL(k_fb_pose_rank, dim3(nk), dim3(64 * nw), (uint32_t)((nw + 1) * nbs * sizeof(int)), s, kptr, plm, n_opt,
                        (const int*)lm_blk, (const int*)owner, nb, (const u64*)gmask, W, pblk, prank, cntE, erank,
                        rankk, counters);
     hipLaunchKernelGGL(k_fb_entries, dim3(nb), dim3(64), 0, s, (const u64*)gmask, W, fw, (const int*)cntE, eoff, wst,

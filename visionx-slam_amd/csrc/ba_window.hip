@@ -211,11 +211,29 @@ __device__ __forceinline__ int lobs_feature(const WinArgs& a, int l, int64_t o, 
 
 __global__ __launch_bounds__(kT) void k_lobs_count(WinArgs a, const int* inv, int n_opt, int* cnt) {
     const int s = blockIdx.x * kT + threadIdx.x;
+    if (s == 0) cnt[n_opt] = 0;  // (the scan's extra element)
     if (s >= n_opt) return;
     const int l = inv[s];
     int c = 0, row;
     for (int64_t o = a.optr[l]; o < a.optr[l + 1]; ++o) c += lobs_feature(a, l, o, row) >= 0 ? 1 : 0;
     cnt[s] = c;
+}
+
+// the build's scratch state in one launch: empty hash slots, zeroed per-landmark / per-feature
+// flags (the scans' extra elements included) and counters
+__global__ __launch_bounds__(kT) void k_build_init(uint64_t* hkey, size_t hcap, int* l_ref, int* l_opt, size_t lN,
+                                                   int* f_pv, int* f_first, size_t fN, unsigned* counts) {
+    const size_t i = (size_t)blockIdx.x * kT + threadIdx.x;
+    if (i < hcap) hkey[i] = ~0ull;
+    if (i < lN) {
+        l_ref[i] = 0;
+        l_opt[i] = 0;
+    }
+    if (i < fN) {
+        f_pv[i] = 0;
+        f_first[i] = 0;
+    }
+    if (i < 16) counts[i] = 0;
 }
 
 __global__ __launch_bounds__(kT) void k_lobs_fill(WinArgs a, const int* inv, int n_opt, const int* lptr,
@@ -385,17 +403,14 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
 
     VX_HIP(c, B.hkey.ensure((size_t)hcap * 8));
     VX_HIP(c, B.hval.ensure((size_t)hcap * 4));
-    VX_HIP(c, hipMemsetAsync(B.hkey.p, 0xff, (size_t)hcap * 8, c->stream));
     const size_t fN = (size_t)std::max(nf, 1) + 1, lN = (size_t)std::max(nl, 1) + 1;
     for (DevBuf* d : {&B.f_lm, &B.f_pv, &B.f_first, &B.scan_b}) VX_HIP(c, d->ensure(fN * 4));
     for (DevBuf* d : {&B.l_ref, &B.l_opt, &B.l_slot, &B.l_first, &B.scan_a, &B.inv, &B.cnt, &B.scan_c})
         VX_HIP(c, d->ensure(lN * 4));
     VX_HIP(c, B.counts.ensure(64));
-    VX_HIP(c, hipMemsetAsync(B.l_ref.p, 0, lN * 4, c->stream));
-    VX_HIP(c, hipMemsetAsync(B.counts.p, 0, 64, c->stream));
-    VX_HIP(c, hipMemsetAsync(B.f_pv.p, 0, fN * 4, c->stream));      // [nf] = 0 for the scans
-    VX_HIP(c, hipMemsetAsync(B.f_first.p, 0, fN * 4, c->stream));
-    VX_HIP(c, hipMemsetAsync(B.l_opt.p, 0, lN * 4, c->stream));
+    hipLaunchKernelGGL(k_build_init, dim3(grid((int)std::max<size_t>(std::max<size_t>(hcap, lN), fN))), dim3(kT), 0,
+                       c->stream, B.hkey.as<uint64_t>(), (size_t)hcap, B.l_ref.as<int>(), B.l_opt.as<int>(), lN,
+                       B.f_pv.as<int>(), B.f_first.as<int>(), fN, B.counts.as<unsigned>());  // ([nf] = 0 for the scans)
 
     WinArgs a{};
     a.nk = nk;
@@ -469,7 +484,6 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
                        p->kf_obs_ptr.as<int>(), n_pose);
     // landmark-stage CSR
     int* cnt = B.cnt.as<int>();
-    VX_HIP(c, hipMemsetAsync(cnt + n_opt, 0, 4, s));
     hipLaunchKernelGGL(k_lobs_count, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, cnt);
     VX_LAUNCH_CHECK(c, "plan CSR kernels");
     VX_HIP(c, p->lobs_ptr.ensure((size_t)(n_opt + 1) * 4));
