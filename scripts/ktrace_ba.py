@@ -50,9 +50,21 @@ def main():
     for _ in range(30):
         plan.run_async()
     ctx.synchronize()
-    report(read(), [0, 1, 2, 3, 4, 6, 7, 5],
+    tr2 = read()
+    report(tr2, [0, 1, 2, 3, 4, 6, 7, 5],
            "k_ba_iter (1 loads, 2 combine + totals + barrier, 3 pose solve + barrier, 4 landmark stage + barrier, "
            "6 pose-stage entry, 7 its rounds, 5 pose stage of it + 1 done)")
+    # the slowest workgroups (and workgroup 0, which also runs the stop rule's totals): phase deltas
+    tr = tr2[0]
+    ok = tr[:, 0] > 0
+    d = (tr[:, [1, 2, 3, 4, 5]] - tr[:, [0, 1, 2, 3, 4]]) / 100.0
+    end = (tr[:, 5] - tr[:, 0]) / 100.0
+    order = [b for b in np.argsort(-end) if ok[b]][:6]
+    if 0 not in order and ok[0]:
+        order.append(0)
+    print("  slowest workgroups: wg  loads combine solve landmark pose-stage  total (us)")
+    for b in order:
+        print(f"    {b:3d}  " + "  ".join(f"{x:6.2f}" for x in d[b]) + f"  {end[b]:6.2f}")
     plan.close()
     # the two-kernel path (sharded plans, windows the fused layout does not fit)
     os.environ["VX_BA_FUSED"] = "0"

@@ -652,6 +652,14 @@ struct FusedArgs {
     int maxl, n_part;
     const double* rowpart;  // sharded plans: per keyframe row the partial slots summed (k_row_sum) and
                             // all-reduced over the ranks; the combine and the stop rule read it instead
+    double4* lpos;          // [b * kFT + t] the workgroup's landmark positions in fused order (each read
+                            // and rewritten by its owning thread only; the prologue fills them)
+    double2* costpart;      // 2 x n_part: each partial slot's {cost, observations} (terms 27, 28) again,
+                            // compact, for the stop rule's totals (parity as part)
+    int stop_b;             // the workgroup that runs the stop rule (the lightest pose stage, plan time)
+    double* epose;          // [(b * kFK + j) * 16] the workgroup's copy of entry j's pose T 8 | C 4 | flags:
+                            // every workgroup solving the entry computes the same pose, so each keeps
+                            // its own and reads it back at a fixed address (no keyframe-row indirection)
 };
 
 // LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), kFK loaded
@@ -673,7 +681,16 @@ static_assert(fused_lds(kFTLarge) <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's
 template <bool kPro, int kFT>
 __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) {
     constexpr int kFW = kFT / 64;  // waves per workgroup
-    if (!kPro && it > 0 && !a.state->active[it]) return;
+    // per-entry pose copies (f.epose) and fused-order landmark positions (f.lpos) in the 512-thread
+    // kernel; the 1024-thread one (128 VGPRs) keeps the indirect reads of the published poses and
+    // positions, whose longer live ranges it cannot afford
+    constexpr bool kEcopy = kFT == kFTSmall;
+    // (an iteration after the stop returns before its first write, below: its loads are issued
+    // first so the flag's latency overlaps theirs)
+    if (!kEcopy && !kPro && it > 0 && !a.state->active[it]) return;
+    // (a relaxed atomic load is issued here with the other loads — a plain one was sunk to its use —
+    // and waited for only at its use below)
+    const int act = kPro ? 1 : __hip_atomic_load(&a.state->active[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     extern __shared__ __attribute__((aligned(16))) double fl[];
     double* kslot = fl;                                  // [kFK][kLdsStride]
     double* tslot = kslot + kFK * kLdsStride;            // [kFK][kTStride]
@@ -699,32 +716,52 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         orec = f.lobs_rec[base + tid];
         ouv = f.lobs_uv[base + tid];
     }
-    // (b) the landmark it owns (its position goes to LDS for the observations of the landmark)
+    // (b) the landmark it owns (its position goes to LDS for the observations of the landmark):
+    // fused-order copy at a fixed address (the prologue reads the slot's initial position)
     const int lslot = f.lm_slot[base + tid];
     int2 run = make_int2(0, 0);
     if (!kPro) run = f.lm_run[base + tid];
     D3 PL;
-    {
+    if (kPro || !kEcopy) {
         const double* P = kPro ? a.lm_pos0 + 4 * (size_t)lslot : lm_in(a, it, lslot);
         PL = {P[0], P[1], P[2]};
+    } else {
+        const double* P = reinterpret_cast<const double*>(f.lpos + base + tid);
+        PL = {P[0], P[1], P[2]};
     }
-    // (c) the keyframe entry it solves: previous pose, intrinsics, flags -> tslot
+    // (c) the keyframe entry it solves: previous pose, intrinsics, flags -> tslot (the prologue
+    // gathers them by keyframe row into the workgroup's entry copy; later launches read the copy)
     int4 ke = make_int4(-1, 0, 0, 0);
+    double ev[13];
     if (tid < kFK) {
         ke = KE[2 * tid];
-        if (ke.x >= 0) {
-            const int row = ke.x & 0x3fffffff;
-            const double* Tin = (kPro ? a.kf_pose0 : pose_in(a, it)) + 8 * (size_t)row;
-            double* ts = tslot + tid * kTStride;
-            double v[12];
+        // (the copy is read whether or not the entry exists — unused entries are valid memory — so
+        // the load does not wait for the entry table)
+        if (ke.x >= 0 || (!kPro && kEcopy)) {
+            if (kPro || !kEcopy) {
+                const int row = ke.x & 0x3fffffff;
+                const double* Tin = (kPro ? a.kf_pose0 : pose_in(a, it)) + 8 * (size_t)row;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = Tin[j];
+                for (int j = 0; j < 8; ++j) ev[j] = Tin[j];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) v[8 + j] = a.kf_intr[4 * row + j];
-            const int flg = a.kf_flags[row];
+                for (int j = 0; j < 4; ++j) ev[8 + j] = a.kf_intr[4 * row + j];
+                ev[12] = (double)a.kf_flags[row];
+            } else {
+                const double4* E4 = reinterpret_cast<const double4*>(f.epose + ((size_t)b * kFK + tid) * 16);
+                const double4 e0 = E4[0], e1 = E4[1], e2 = E4[2];
+                ev[0] = e0.x, ev[1] = e0.y, ev[2] = e0.z, ev[3] = e0.w;
+                ev[4] = e1.x, ev[5] = e1.y, ev[6] = e1.z, ev[7] = e1.w;
+                ev[8] = e2.x, ev[9] = e2.y, ev[10] = e2.z, ev[11] = e2.w;
+                ev[12] = reinterpret_cast<const double*>(E4 + 3)[0];
+            }
+            double* ts = tslot + tid * kTStride;  // (LDS: harmless if the iteration is not live)
 #pragma unroll
-            for (int j = 0; j < 12; ++j) ts[j] = v[j];
-            ts[12] = (double)flg;
+            for (int j = 0; j < 13; ++j) ts[j] = ev[j];
+            if (kPro && kEcopy) {
+                double* E = f.epose + ((size_t)b * kFK + tid) * 16;
+#pragma unroll
+                for (int j = 0; j < 13; ++j) E[j] = ev[j];
+            }
         }
     }
     // (d) this wave's first pose-stage round (round r + 1 is requested when round r is consumed)
@@ -737,6 +774,8 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     }
     const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
     const bool has_o = !kPro && tid < n_ob, own = tid < n_lm;
+    if (!kPro && it > 0 && !act) return;  // iteration after the stop: no global write
+    if (kPro && kEcopy) f.lpos[base + tid] = make_double4(PL.x, PL.y, PL.z, 0.0);
     lpos[3 * tid] = PL.x;
     lpos[3 * tid + 1] = PL.y;
     lpos[3 * tid + 2] = PL.z;
@@ -751,24 +790,36 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 continue;
             }
             const double* src = part_in + ((size_t)(e.x & 0x3fffffff) * f.maxl) * kStride + t;
+            constexpr int kCB = kFT == kFTSmall ? 32 : 16;  // slots per batch of loads (one round at C3)
             double acc = 0.0;
-            for (int i0 = 0; i0 < e.y; i0 += 16) {
-                double v[16];
+            for (int i0 = 0; i0 < e.y; i0 += kCB) {
+                double v[kCB];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) v[q] = i0 + q < e.y ? src[(size_t)(i0 + q) * kStride] : 0.0;
+                for (int q = 0; q < kCB; ++q) v[q] = i0 + q < e.y ? src[(size_t)(i0 + q) * kStride] : 0.0;
 #pragma unroll
-                for (int q = 0; q < 16; ++q) acc += v[q];  // (+0.0 past the end: exact)
+                for (int q = 0; q < kCB; ++q) acc += v[q];  // (+0.0 past the end: exact)
             }
             kslot[j * kLdsStride + t] = acc;
         }
         // ---- stop rule of iteration it (workgroup 0): totals over every partial slot
-        if (b == 0) {
+        if (b == f.stop_b) {
             double tot = 0.0, cnt = 0.0;
-            const double* tp = f.rowpart ? f.rowpart : part_in;
-            const int n_tp = f.rowpart ? a.n_kf : f.n_part;
-            for (int q = tid; q < n_tp; q += kFT) {
-                tot += tp[(size_t)q * kStride + 27];
-                cnt += tp[(size_t)q * kStride + 28];
+            if (f.rowpart) {
+                for (int q = tid; q < a.n_kf; q += kFT) {
+                    tot += f.rowpart[(size_t)q * kStride + 27];
+                    cnt += f.rowpart[(size_t)q * kStride + 28];
+                }
+            } else {
+                const double2* cp = f.costpart + (size_t)(it & 1) * f.n_part;
+                for (int q0 = 0; q0 < f.n_part; q0 += 2 * kFT) {  // (two loads in flight per thread)
+                    const int q1 = q0 + tid, q2 = q0 + kFT + tid;
+                    const double2 c1 = q1 < f.n_part ? cp[q1] : make_double2(0.0, 0.0);
+                    const double2 c2 = q2 < f.n_part ? cp[q2] : make_double2(0.0, 0.0);
+                    tot += c1.x;
+                    cnt += c1.y;
+                    tot += c2.x;
+                    cnt += c2.y;
+                }
             }
 #pragma unroll
             for (int m = 32; m > 0; m >>= 1) {
@@ -802,6 +853,11 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
 #pragma unroll
                 for (int j = 0; j < 8; ++j) Tout[j] = T[j];
             }
+            if (kEcopy) {
+                double4* E4 = reinterpret_cast<double4*>(f.epose + ((size_t)b * kFK + tid) * 16);
+                E4[0] = make_double4(T[0], T[1], T[2], T[3]);
+                E4[1] = make_double4(T[4], T[5], T[6], T[7]);
+            }
         } else {
             rot_from_quat(T, R);
         }
@@ -812,7 +868,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
 #pragma unroll
         for (int j = 0; j < 4; ++j) sl[17 + j] = C[j];
     }
-    if (!kPro && b == 0 && tid == 0) {
+    if (!kPro && b == f.stop_b && tid == 0) {
         double tot = 0.0, cnt = 0.0;
         for (int w2 = 0; w2 < kFW; ++w2) {
             tot += red[w2];
@@ -841,6 +897,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 obs += tcount[r];
             }
             PL = lm_update(a, lslot, PL, hs, obs);
+            if (kEcopy) f.lpos[base + tid] = make_double4(PL.x, PL.y, PL.z, 0.0);
             lpos[3 * tid] = PL.x;
             lpos[3 * tid + 1] = PL.y;
             lpos[3 * tid + 2] = PL.z;
@@ -880,6 +937,8 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         if (j == wv) FKT(7);
         const double tot = wave_sum32(v);
         if ((lane & 1) == 0) part_out[(size_t)dst * kStride + (lane >> 1)] = (lane >> 1) < kNTerms ? tot : 0.0;
+        if (lane == 54 || lane == 56)  // terms 27 (cost) and 28 (observations)
+            reinterpret_cast<double*>(f.costpart + (size_t)((it + 1) & 1) * f.n_part + dst)[(lane - 54) >> 1] = tot;
     }
     FKT(5);
 }
@@ -1097,7 +1156,7 @@ size_t fused_offsets(int nb, int ft, size_t n_pp, FusedOffsets& F) {
     return at;
 }
 
-int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp) {
+int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp, int stop_b) {
     const FusedOffsets& F = p->f_off;
     const size_t n_lp = (size_t)nb * ft;
     const uint8_t* T = p->f_tab.as<uint8_t>();
@@ -1110,10 +1169,16 @@ int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp
                        reinterpret_cast<const int*>(T + F.pobs_code), (int)n_pp, (const double2*)p->pobs_uv.as<double2>(),
                        (const double*)p->lm_pos0.as<double>(), p->f_pobs_uv.as<double2>(), p->f_pobs_p.as<double4>());
     VX_LAUNCH_CHECK(c, "k_fused_gather");
+    VX_HIP(c, p->f_lpos.ensure(n_lp * sizeof(double4)));
+    VX_HIP(c, p->f_epose.ensure((size_t)nb * kFK * 16 * sizeof(double)));
     const size_t part_bytes = 2 * (size_t)p->n_kf * maxl * kStride * sizeof(double);
     VX_HIP(c, p->f_part.ensure(part_bytes));
     if (p->shard_count > 1) VX_HIP(c, p->f_rowpart.ensure((size_t)p->n_kf * kStride * sizeof(double)));
     VX_HIP(c, hipMemsetAsync(p->f_part.p, 0, part_bytes, c->stream));  // slots no group writes stay 0
+    const size_t cost_bytes = 2 * (size_t)p->n_kf * maxl * sizeof(double2);
+    VX_HIP(c, p->f_costpart.ensure(cost_bytes));
+    VX_HIP(c, hipMemsetAsync(p->f_costpart.p, 0, cost_bytes, c->stream));
+    p->f_stop_b = stop_b;
     p->f_blocks = nb;
     p->f_maxl = maxl;
     p->f_threads = ft;
@@ -1296,7 +1361,9 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     std::memset(blk, 0, (size_t)nb * kBlkInts * 4);
     std::vector<int> loc(nk, -1), rank(nk, 0), ent_rank((size_t)nb * kFK, -1);
     size_t pw = 0;
+    long long stop_key = -1;
     for (int b = 0; b < nb; ++b) {
+        int max_rounds = 0;
         for (int j = 0; j < (int)K[b].size(); ++j) loc[K[b][j]] = j;
         int* B = blk + (size_t)b * kBlkInts;
         const size_t base = (size_t)b * ft;
@@ -1349,7 +1416,10 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             }
             B[4 + 2 * w] = (int)wstart;
             B[4 + 2 * w + 1] = (int)((pw - wstart) / 64);
+            max_rounds = std::max(max_rounds, B[4 + 2 * w + 1]);
         }
+        const long long key = fused_stop_key(max_rounds, (int)K[b].size(), b);
+        if (stop_key < 0 || key < stop_key) stop_key = key;
         for (int k : K[b]) loc[k] = -1;
     }
     lap(10);
@@ -1368,7 +1438,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     VX_HIP(c, p->f_tab.ensure(at));
     VX_HIP(c, hipMemcpyAsync(p->f_tab.p, S, at, hipMemcpyHostToDevice, c->stream));
     int rc;
-    if ((rc = fused_finish(c, p, nb, ft, maxl, n_pp))) return rc;
+    if ((rc = fused_finish(c, p, nb, ft, maxl, n_pp, (int)(stop_key & 0xffffffff)))) return rc;
     VX_HIP(c, hipStreamSynchronize(c->stream));  // (the staging block is reused by the next build)
     lap(2);
     if (timing)
@@ -1597,6 +1667,10 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
     f.maxl = p->f_maxl;
     f.n_part = p->n_kf * p->f_maxl;
     f.rowpart = p->shard_count > 1 ? p->f_rowpart.as<double>() : nullptr;
+    f.costpart = p->f_costpart.as<double2>();
+    f.stop_b = p->f_stop_b;
+    f.lpos = p->f_lpos.as<double4>();
+    f.epose = p->f_epose.as<double>();
     return f;
 }
 

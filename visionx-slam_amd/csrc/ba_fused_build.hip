@@ -59,7 +59,7 @@ __device__ __forceinline__ int popc_below(const u64* m, int W, int k) {
 
 __global__ void k_fb_init(int n_opt, int nk, int W, int* key, int* iota, u64* mask, int* owner, int* counters) {
     const int i = blockIdx.x * kT + threadIdx.x;
-    if (i < 16) counters[i] = 0;
+    if (i < 16) counters[i] = i < 4 ? 0 : -1;  // ([4..5]: the stop-rule workgroup's key, atomicMin)
     if (i < n_opt) {
         key[i] = nk;
         iota[i] = i;
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(512) void k_fb_pose_rank(const int* kptr, const int
 // per workgroup (lane = keyframe entry j): padded entry sizes, their offsets in wave-major order
 // (wave w takes entries w, w + fw, ...), each wave's start and rounds, the workgroup's total
 __global__ __launch_bounds__(64) void k_fb_entries(const u64* gmask, int W, int fw, const int* cntE, int* eoff,
-                                                  int* wst, int* wrd, int* G, int nb) {
+                                                  int* wst, int* wrd, int* G, int nb, int* counters) {
     __shared__ int pad[kFK], key[kFK];
     const int b = blockIdx.x, j = threadIdx.x;
     int nent = 0;
@@ -378,6 +378,12 @@ __global__ __launch_bounds__(64) void k_fb_entries(const u64* gmask, int W, int 
         G[b] = tot;
         if (b == 0) G[nb] = 0;
     }
+    // the lightest pose stage runs the stop rule (ba.hip fused_stop_key; lanes < fw hold the waves)
+    int mr = j < fw ? wr / 64 : 0;
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) mr = max(mr, __shfl_xor(mr, m, 64));
+    if (j == 0)
+        atomicMin(reinterpret_cast<unsigned long long*>(counters + 4), (unsigned long long)fused_stop_key(mr, nent, b));
 }
 
 struct FusedTabs {
@@ -606,18 +612,19 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
                        (const int*)lm_blk, (const int*)owner, nb, (const u64*)gmask, W, pblk, prank, cntE, erank,
                        rankk, counters);
     hipLaunchKernelGGL(k_fb_entries, dim3(nb), dim3(64), 0, s, (const u64*)gmask, W, fw, (const int*)cntE, eoff, wst,
-                       wrd, G, nb);
+                       wrd, G, nb, counters);
     VX_LAUNCH_CHECK(c, "fused build: entries");
     VX_HIP(c, rocprim::exclusive_scan(nullptr, tb, G, gbase, 0, nbs + 1, rocprim::plus<int>(), s));
     VX_HIP(c, S.fb_tmp.ensure(std::max<size_t>(tb, 16)));
     VX_HIP(c, rocprim::exclusive_scan(S.fb_tmp.p, tb, G, gbase, 0, nbs + 1, rocprim::plus<int>(), s));
-    VX_HIP(c, hipMemcpyAsync(H, counters, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipMemcpyAsync(H + 4, gbase + nb, sizeof(int), hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(H, counters, 6 * sizeof(int), hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(H + 8, gbase + nb, sizeof(int), hipMemcpyDeviceToHost, s));
     VX_HIP(c, hipStreamSynchronize(s));
     const double t_entries = ms();
     if (H[1] != 0) return VX_OK;
     const int maxl = std::max(1, H[2]);
-    const size_t n_pp = (size_t)H[4];
+    const size_t n_pp = (size_t)H[8];
+    const int stop_b = H[4];  // (low word of the minimal key)
 
     // ---- the tables, straight into f_tab
     FusedOffsets& F = p->f_off;
@@ -637,7 +644,7 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
                        (const int*)gbase);
     VX_LAUNCH_CHECK(c, "fused build: tables");
     int rc;
-    if ((rc = fused_finish(c, p, nb, ft, maxl, n_pp))) return rc;
+    if ((rc = fused_finish(c, p, nb, ft, maxl, n_pp, stop_b))) return rc;
     if (timing) {
         VX_HIP(c, hipStreamSynchronize(s));
         fprintf(stderr, "[vx plan] fused layout on the device: packing %.3f ms, entries %.3f ms, tables %.3f ms (%d workgroups x %d)\n",

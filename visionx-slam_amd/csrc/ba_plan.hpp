@@ -41,6 +41,9 @@ struct vx_ba_plan {
     int f_blocks = 0, f_maxl = 0, f_threads = 512;
     vx::DevBuf f_tab, f_lobs_uv, f_pobs_uv, f_pobs_p, f_part;  // f_tab: the index tables, one upload
     vx::DevBuf f_rowpart;                                         // sharded: all-reduced per-row partials
+    vx::DevBuf f_lpos, f_epose;  // k_ba_iter's fused-order landmark positions and per-entry pose copies
+    vx::DevBuf f_costpart;       // compact {cost, observations} of every partial slot (stop rule)
+    int f_stop_b = 0;            // workgroup running the stop rule
     vx::PinnedBuf f_stage;                                        // their host staging block
     FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
     size_t f_npp = 0;                                             // pose-observation positions (padded)
@@ -55,7 +58,7 @@ struct vx_dmap;
     X(kf_pose0) X(kf_pose) X(kf_intr) X(kf_rot) X(kf_flags) X(kf_obs_ptr) X(kf_part) X(kf_cost) X(lm_pos0) \
     X(lm_pos) X(pobs_uv) X(pobs_lm) X(lobs_ptr) X(lobs_kf) X(lobs_lm) X(lm_blk) X(lobs_uv) X(state)       \
     X(kf_map_dev) X(lm_map_dev) X(f_tab) X(f_lobs_uv) X(f_pobs_uv) X(f_pobs_p) X(f_part) X(f_rowpart)    \
-    X(f_stage)
+    X(f_stage) X(f_lpos) X(f_epose) X(f_costpart)
 
 namespace vx {
 // a new plan of context c (buffers adopted from a parked plan when there is one)
@@ -104,7 +107,12 @@ size_t fused_offsets(int nb, int ft, size_t n_pp, FusedOffsets& F);
 inline int fused_blk_ints(int ft) { return 4 * (1 + ft / 64 / 2); }
 // after the tables are in f_tab: the observation payloads gathered into the fused order, the
 // partial buffers cleared, the layout enabled
-int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp);
+// (stop_b: the workgroup that evaluates the stop rule — the one with the lightest pose stage)
+int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp, int stop_b);
+// the stop-rule workgroup's key: lower = lighter pose stage (most rounds of a wave, then entries)
+__host__ __device__ inline long long fused_stop_key(int max_wave_rounds, int n_ent, int b) {
+    return ((long long)(max_wave_rounds * 64 + n_ent) << 32) | (unsigned)b;
+}
 // SelectKeyFrames + landmark set + both CSRs built on the device from the map snapshot (§8f rank 2)
 int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p);
 // the same plan from a device-resident map (vx_dmap; its CSR rebuilt first if stale)
