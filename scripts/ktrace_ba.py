@@ -62,6 +62,17 @@ def main():
     order = [b for b in np.argsort(-end) if ok[b]][:6]
     if 0 not in order and ok[0]:
         order.append(0)
+    # per wave: end of its pose stage (slots 8..15) after the landmark stage's barrier (slot 4), beside
+    # the wave's rounds from the layout
+    lay = plan.layout()
+    fw = lay["threads"] // 64
+    bi = 4 * (1 + fw // 2)
+    blk = np.frombuffer(plan.fused_tables(), np.int32)[: lay["workgroups"] * bi].reshape(-1, bi)
+    print("  per-wave pose stage done after slot 4 (us) [rounds]:")
+    for b in list(range(4)):
+        if ok[b]:
+            w = (tr[b, 8:8 + min(fw, 8)] - tr[b, 4]) / 100.0
+            print(f"    wg {b}: " + "  ".join(f"{x:5.2f}[{blk[b, 5 + 2 * i]}]" for i, x in enumerate(w)))
     print("  slowest workgroups: wg  loads combine solve landmark pose-stage  total (us)")
     for b in order:
         print(f"    {b:3d}  " + "  ".join(f"{x:6.2f}" for x in d[b]) + f"  {end[b]:6.2f}")

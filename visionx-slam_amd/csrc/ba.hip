@@ -785,6 +785,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         for (int pr = tid; pr < n_ent * kNTerms; pr += kFT) {
             const int j = pr / kNTerms, t = pr - j * kNTerms;
             const int4 e = KE[2 * j];
+            if (e.x < 0) continue;  // a hole in the entry positions
             if (f.rowpart) {  // sharded: the all-reduced row (identical on every rank)
                 kslot[j * kLdsStride + t] = f.rowpart[(size_t)(e.x & 0x3fffffff) * kStride + t];
                 continue;
@@ -940,6 +941,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         if (lane == 54 || lane == 56)  // terms 27 (cost) and 28 (observations)
             reinterpret_cast<double*>(f.costpart + (size_t)((it + 1) & 1) * f.n_part + dst)[(lane - 54) >> 1] = tot;
     }
+    if (!kPro && it == 1) VX_KTW(8, 8);  // (trace build: each wave's pose stage done)
     FKT(5);
 }
 
@@ -1344,6 +1346,15 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         }
         if (i != po_ptr[b + 1]) return set_error(c, VX_ERR_STATE, "fused layout: pose observations out of keyframe order");
     }
+    // entry positions: SIMD-aware LPT over the entries' pose-stage rounds (fused_place_entries)
+    std::vector<int> epos((size_t)nb * kFK, -1), n_pos(nb, 0);
+    for (int b = 0; b < nb; ++b) {
+        int rounds[kFK];
+        const int ne = (int)K[b].size();
+        for (int j = 0; j < ne; ++j)
+            rounds[j] = (ent_end[(size_t)b * kFK + j] - ent_beg[(size_t)b * kFK + j] + 63) / 64;
+        n_pos[b] = fused_place_entries(rounds, ne, &epos[(size_t)b * kFK]);
+    }
     FusedOffsets& F = p->f_off;
     const size_t at = fused_offsets(nb, ft, n_pp, F);
     lap(8);
@@ -1359,12 +1370,15 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     int* pobs_src = reinterpret_cast<int*>(S + F.pobs_src);
     int* pobs_code = reinterpret_cast<int*>(S + F.pobs_code);
     std::memset(blk, 0, (size_t)nb * kBlkInts * 4);
-    std::vector<int> loc(nk, -1), rank(nk, 0), ent_rank((size_t)nb * kFK, -1);
+    std::vector<int> loc(nk, -1), rank(nk, 0), ent_rank((size_t)nb * kFK, -1), at_pos(kFK);
     size_t pw = 0;
     long long stop_key = -1;
     for (int b = 0; b < nb; ++b) {
         int max_rounds = 0;
-        for (int j = 0; j < (int)K[b].size(); ++j) loc[K[b][j]] = j;
+        const int* EP = &epos[(size_t)b * kFK];
+        for (int j = 0; j < (int)K[b].size(); ++j) loc[K[b][j]] = EP[j];
+        std::fill(at_pos.begin(), at_pos.end(), -1);
+        for (int j = 0; j < (int)K[b].size(); ++j) at_pos[EP[j]] = j;
         int* B = blk + (size_t)b * kBlkInts;
         const size_t base = (size_t)b * ft;
         int ob = 0;
@@ -1389,18 +1403,20 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         }
         B[0] = (int)LM[b].size();
         B[1] = ob;
-        B[2] = (int)K[b].size();
+        B[2] = n_pos[b];  // (positions: entries and holes)
         int* E = kent + (size_t)b * kFK * 8;
         for (int j = 0; j < kFK; ++j)
             for (int x = 0; x < 8; ++x) E[8 * j + x] = (x == 0 || x == 4) ? -1 : 0;
         for (int w = 0; w < fw; ++w) {
             const size_t wstart = pw;
-            for (int j = w; j < (int)K[b].size(); j += fw) {
+            for (int P = w; P < n_pos[b]; P += fw) {
+                const int j = at_pos[P];
+                if (j < 0) continue;  // a hole
                 const int k = K[b][j];
                 const int e0 = ent_beg[(size_t)b * kFK + j], e1 = ent_end[(size_t)b * kFK + j], n = e1 - e0;
-                E[8 * j] = k | (owner[k] == b ? (1 << 30) : 0);
-                E[8 * j + 2] = (int)pw;
-                E[8 * j + 3] = (int)pw + n;
+                E[8 * P] = k | (owner[k] == b ? (1 << 30) : 0);
+                E[8 * P + 2] = (int)pw;
+                E[8 * P + 3] = (int)pw + n;
                 for (int x = e0; x < e1; ++x) {
                     const int o = po[x];
                     pobs_src[pw + (x - e0)] = o;
@@ -1418,7 +1434,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
             B[4 + 2 * w + 1] = (int)((pw - wstart) / 64);
             max_rounds = std::max(max_rounds, B[4 + 2 * w + 1]);
         }
-        const long long key = fused_stop_key(max_rounds, (int)K[b].size(), b);
+        const long long key = fused_stop_key(max_rounds, n_pos[b], b);
         if (stop_key < 0 || key < stop_key) stop_key = key;
         for (int k : K[b]) loc[k] = -1;
     }
@@ -1427,7 +1443,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
     for (int k = 0; k < nk; ++k) maxl = std::max(maxl, rank[k]);
     for (int b = 0; b < nb; ++b)
         for (int j = 0; j < (int)K[b].size(); ++j) {
-            int* E = kent + ((size_t)b * kFK + j) * 8;
+            int* E = kent + ((size_t)b * kFK + epos[(size_t)b * kFK + j]) * 8;
             const int k = K[b][j];
             E[1] = rank[k];
             const int r = ent_rank[(size_t)b * kFK + j];

@@ -351,31 +351,39 @@ __global__ __launch_bounds__(512) void k_fb_pose_rank(const int* kptr, const int
 // per workgroup (lane = keyframe entry j): padded entry sizes, their offsets in wave-major order
 // (wave w takes entries w, w + fw, ...), each wave's start and rounds, the workgroup's total
 __global__ __launch_bounds__(64) void k_fb_entries(const u64* gmask, int W, int fw, const int* cntE, int* eoff,
-                                                  int* wst, int* wrd, int* G, int nb, int* counters) {
-    __shared__ int pad[kFK], key[kFK];
+                                                  int* wst, int* wrd, int* G, int nb, int* counters, int* epos,
+                                                  int* npos) {
+    __shared__ int pad[kFK], rnd[kFK], pos[kFK], sh_npos;
     const int b = blockIdx.x, j = threadIdx.x;
     int nent = 0;
     for (int w = 0; w < W; ++w) nent += __popcll(gmask[(size_t)b * W + w]);
     const int n = j < nent ? cntE[(size_t)b * kFK + j] : 0;
     pad[j] = j < nent ? (n + 63) / 64 * 64 : 0;
-    key[j] = j < nent ? (j % fw) * kFK + j / fw : INT_MAX;
+    rnd[j] = (n + 63) / 64;
     __syncthreads();
+    if (j == 0) sh_npos = fused_place_entries(rnd, nent, pos);  // (SIMD-aware LPT, ba_plan.hpp)
+    __syncthreads();
+    const int P = j < nent ? pos[j] : INT_MAX;
+    const int key = j < nent ? (P % fw) * kFK + P / fw : INT_MAX;  // wave-major over positions
     int off = 0, tot = 0, ws = 0, wr = 0;
     for (int i = 0; i < nent; ++i) {
-        if (key[i] < key[j]) off += pad[i];
+        const int pi = pos[i], ki = (pi % fw) * kFK + pi / fw;
+        if (ki < key) off += pad[i];
         tot += pad[i];
         if (j < fw) {
-            if (i % fw < j) ws += pad[i];
-            if (i % fw == j) wr += pad[i];
+            if (pi % fw < j) ws += pad[i];
+            if (pi % fw == j) wr += pad[i];
         }
     }
     eoff[(size_t)b * kFK + j] = off;
+    epos[(size_t)b * kFK + j] = j < nent ? P : -1;
     if (j < fw) {
         wst[(size_t)b * kMaxWaves + j] = ws;
         wrd[(size_t)b * kMaxWaves + j] = wr / 64;
     }
     if (j == 0) {
         G[b] = tot;
+        npos[b] = sh_npos;
         if (b == 0) G[nb] = 0;
     }
     // the lightest pose stage runs the stop rule (ba.hip fused_stop_key; lanes < fw hold the waves)
@@ -383,7 +391,8 @@ __global__ __launch_bounds__(64) void k_fb_entries(const u64* gmask, int W, int 
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) mr = max(mr, __shfl_xor(mr, m, 64));
     if (j == 0)
-        atomicMin(reinterpret_cast<unsigned long long*>(counters + 4), (unsigned long long)fused_stop_key(mr, nent, b));
+        atomicMin(reinterpret_cast<unsigned long long*>(counters + 4),
+                  (unsigned long long)fused_stop_key(mr, sh_npos, b));
 }
 
 struct FusedTabs {
@@ -403,17 +412,22 @@ __global__ void k_fb_fill_group(FusedTabs T, int ft, int fw, int blk_ints, int m
                                 const int* starts, const int* order, const int* cntS, const int* cntScan,
                                 const int* lptr, const int* lkf, const u64* gmask, const int* owner,
                                 const int* rankk, const int* cntE, const int* erank, const int* eoff, const int* wst,
-                                const int* wrd, const int* gbase) {
-    __shared__ int jl[kBaMaxKfLds], kof[kFK];
+                                const int* wrd, const int* gbase, const int* epos, const int* npos) {
+    __shared__ int jl[kBaMaxKfLds], kof[kFK], jof[kFK];
     __shared__ u64 gm[kMaxW];
     const int b = blockIdx.x, t = threadIdx.x;
     if (t < W) gm[t] = gmask[(size_t)b * W + t];
+    if (t < kFK) jof[t] = -1;
     __syncthreads();
-    for (int k = t; k < nk; k += ft) {
+    for (int k = t; k < nk; k += ft) {  // keyframe -> entry position; position -> keyframe, sorted index
         const bool in = (gm[k >> 6] >> (k & 63)) & 1;
         const int j = in ? popc_below(gm, W, k) : -1;
-        jl[k] = j;
-        if (in) kof[j] = k;
+        const int P = in ? epos[(size_t)b * kFK + j] : -1;
+        jl[k] = P;
+        if (in) {
+            kof[P] = k;
+            jof[P] = j;
+        }
     }
     __syncthreads();
     int nent = 0;
@@ -444,18 +458,18 @@ __global__ void k_fb_fill_group(FusedTabs T, int ft, int fw, int blk_ints, int m
         int v = 0;
         if (t == 0) v = nl;
         else if (t == 1) v = ob_total;
-        else if (t == 2) v = nent;
+        else if (t == 2) v = npos[b];
         else if (t >= 4) {
             const int w = (t - 4) >> 1;
             v = (t & 1) ? wrd[(size_t)b * kMaxWaves + w] : gb + wst[(size_t)b * kMaxWaves + w];
         }
         T.blk[(size_t)b * blk_ints + t] = v;
     }
-    for (int x = t; x < kFK * 8; x += ft) {
-        const int j = x >> 3, f = x & 7;
+    for (int x = t; x < kFK * 8; x += ft) {  // entries by position (holes keep the defaults)
+        const int P = x >> 3, f = x & 7, j = jof[P];
         int v = (f == 0 || f == 4) ? -1 : 0;
-        if (j < nent) {
-            const int k = kof[j];
+        if (j >= 0) {
+            const int k = kof[P];
             const size_t ej = (size_t)b * kFK + j;
             const int st = gb + eoff[ej];
             if (f == 0) v = k | (owner[k] == b ? (1 << 30) : 0);
@@ -592,8 +606,8 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
 
     // ---- per-workgroup scratch
     const size_t nbs = (size_t)nb;
-    need = carve_bytes<u64>(nbs * W) + carve_bytes<int>(nbs * kFK) * 3 + carve_bytes<int>(nbs * kMaxWaves) * 2 +
-           carve_bytes<int>(nbs + 1) * 2;
+    need = carve_bytes<u64>(nbs * W) + carve_bytes<int>(nbs * kFK) * 4 + carve_bytes<int>(nbs * kMaxWaves) * 2 +
+           carve_bytes<int>(nbs + 1) * 3;
     VX_HIP(c, S.fb_groups.ensure(need));
     Carve cg{S.fb_groups.as<uint8_t>()};
     u64* gmask = cg.take<u64>(nbs * W);
@@ -604,6 +618,8 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     int* wrd = cg.take<int>(nbs * kMaxWaves);
     int* G = cg.take<int>(nbs + 1);
     int* gbase = cg.take<int>(nbs + 1);
+    int* epos = cg.take<int>(nbs * kFK);  // entry (sorted index) -> position
+    int* npos = cg.take<int>(nbs + 1);    // positions per workgroup
     hipLaunchKernelGGL(k_fb_group, dim3(nb), dim3(kT), 0, s, (const int*)starts, (const int*)order, (const u64*)maskS,
                        W, nk, lm_blk, lm_loc, gmask, owner, cntE, erank);
     hipLaunchKernelGGL(k_fb_owner0, dim3(1), dim3(kT), 0, s, nk, W, owner, gmask, counters);
@@ -612,7 +628,7 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
                        (const int*)lm_blk, (const int*)owner, nb, (const u64*)gmask, W, pblk, prank, cntE, erank,
                        rankk, counters);
     hipLaunchKernelGGL(k_fb_entries, dim3(nb), dim3(64), 0, s, (const u64*)gmask, W, fw, (const int*)cntE, eoff, wst,
-                       wrd, G, nb, counters);
+                       wrd, G, nb, counters, epos, npos);
     VX_LAUNCH_CHECK(c, "fused build: entries");
     VX_HIP(c, rocprim::exclusive_scan(nullptr, tb, G, gbase, 0, nbs + 1, rocprim::plus<int>(), s));
     VX_HIP(c, S.fb_tmp.ensure(std::max<size_t>(tb, 16)));
@@ -638,7 +654,8 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     hipLaunchKernelGGL(k_fb_fill_group, dim3(nb), dim3(ft), 0, s, T, ft, fw, fused_blk_ints(ft), maxl, nk, W,
                        (const int*)starts, (const int*)order, (const int*)cntS, (const int*)cntScan, lptr, lkf,
                        (const u64*)gmask, (const int*)owner, (const int*)rankk, (const int*)cntE, (const int*)erank,
-                       (const int*)eoff, (const int*)wst, (const int*)wrd, (const int*)gbase);
+                       (const int*)eoff, (const int*)wst, (const int*)wrd, (const int*)gbase, (const int*)epos,
+                       (const int*)npos);
     hipLaunchKernelGGL(k_fb_fill_pose, dim3(grid(n_pose)), dim3(kT), 0, s, T, n_pose, n_opt, W, plm, (const int*)pkf,
                        (const int*)pblk, (const int*)prank, (const int*)lm_loc, (const u64*)gmask, (const int*)eoff,
                        (const int*)gbase);

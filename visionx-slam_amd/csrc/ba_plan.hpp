@@ -109,6 +109,30 @@ inline int fused_blk_ints(int ft) { return 4 * (1 + ft / 64 / 2); }
 // partial buffers cleared, the layout enabled
 // (stop_b: the workgroup that evaluates the stop rule — the one with the lightest pose stage)
 int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp, int stop_b);
+// Positions of a fused workgroup's entries (k_ba_iter: position P is taken by wave P % waves, i.e.
+// by SIMD P % 4): LPT over the SIMDs — entries by pose-stage rounds, most first (ties: lower index),
+// each to the SIMD with the fewest rounds so far (ties: fewer entries, lower SIMD) that has fewer
+// than 16 entries, at position SIMD + 4 x (its entries so far).  pos[j] for the n entries; returns
+// the number of positions (highest + 1; unused positions are holes).  Both layout builders use it.
+__host__ __device__ inline int fused_place_entries(const int* rounds, int n, int* pos) {
+    int load[4] = {0, 0, 0, 0}, cnt[4] = {0, 0, 0, 0}, n_pos = 0;
+    unsigned long long done = 0;
+    for (int it = 0; it < n; ++it) {
+        int j = -1;
+        for (int i = 0; i < n; ++i)  // next entry: most rounds, then lowest index
+            if (!((done >> i) & 1) && (j < 0 || rounds[i] > rounds[j])) j = i;
+        done |= 1ull << j;
+        int s = -1;
+        for (int q = 0; q < 4; ++q)
+            if (cnt[q] < 16 && (s < 0 || load[q] < load[s] || (load[q] == load[s] && cnt[q] < cnt[s]))) s = q;
+        pos[j] = s + 4 * cnt[s];
+        ++cnt[s];
+        load[s] += rounds[j];
+        n_pos = pos[j] + 1 > n_pos ? pos[j] + 1 : n_pos;
+    }
+    return n_pos;
+}
+
 // the stop-rule workgroup's key: lower = lighter pose stage (most rounds of a wave, then entries)
 __host__ __device__ inline long long fused_stop_key(int max_wave_rounds, int n_ent, int b) {
     return ((long long)(max_wave_rounds * 64 + n_ent) << 32) | (unsigned)b;

@@ -22,6 +22,15 @@ constexpr int kKtBlocks = 64, kKtSlots = 16;
                 (long long)__builtin_amdgcn_s_memtime();                                   \
         }                                                                                  \
     } while (0)
+// per wave: lane 0 of wave w records slot (base + w), for w < nw
+#define VX_KTW(base, nw)                                                                   \
+    do {                                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                                     \
+        const unsigned kt_b = blockIdx.x + blockIdx.y * gridDim.x;                         \
+        const unsigned kt_w = threadIdx.x >> 6;                                            \
+        if ((threadIdx.x & 63) == 0 && kt_w < (unsigned)(nw) && kt_b < (unsigned)vx::kKtBlocks) \
+            g_ktrace[kt_b * vx::kKtSlots + (base) + kt_w] = (long long)wall_clock64();     \
+    } while (0)
 #define VX_KT_EXPORT(name)                                                                 \
     extern "C" int name(long long* out) {                                                  \
         return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ktrace), sizeof(g_ktrace)) == hipSuccess ? 0 : -1; \
@@ -30,6 +39,9 @@ constexpr int kKtBlocks = 64, kKtSlots = 16;
 #define VX_KT_TABLE() static_assert(true, "")
 #define VX_KT(slot) \
     do {            \
+    } while (0)
+#define VX_KTW(base, nw) \
+    do {                 \
     } while (0)
 #define VX_KT_EXPORT(name) static_assert(true, "")
 #endif
