@@ -30,6 +30,12 @@ def load(kind, i):
     if kind == "copy":
         with torch.cuda.stream(side):
             dst.copy_(src)
+    elif kind == "write":  # streaming writes only: dirty lines in the L2s
+        with torch.cuda.stream(side):
+            dst.zero_()
+    elif kind == "read":  # streaming reads only
+        with torch.cuda.stream(side):
+            src.sum()
     elif kind == "matmul":
         with torch.cuda.stream(side):
             for _ in range(4):
@@ -39,7 +45,7 @@ def load(kind, i):
         c.orb_extract_async(frames[i % 8].data_ptr(), 640, 480, 3, 640 * 3, (i // 2) % 3, params)
 
 
-for kind in ("none", "copy", "matmul", "extract"):
+for kind in ("none", "copy", "write", "read", "matmul", "extract"):
     for i in range(5):
         plan.run_async()
         load(kind, i)

@@ -208,32 +208,30 @@ __device__ __forceinline__ D3 rt_apply(const double* R, const double* t, D3 p) {
 // boundary (the parity tests keep inputs away from it).
 template <bool kFma = true>
 __device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T, const double* R, const double* C,
-                                               D3 Pw, double2 uv, double* v) {
+                                               D3 Pw, double2 uv, double* v, bool valid = true) {
+    // kFma: branch-free — a rejected observation (invalid lane, behind the camera, beyond the gate)
+    // gets weight 0 with finite stand-ins (z = 1), so its terms are exactly +0.0 and the count is not
+    // raised (early returns made the running terms a control-flow merge: 27 register moves per
+    // observation in the pose-stage loop)
     const double fx = C[0], fy = C[1];
-    // (!kFma: the quaternion form, 7 live doubles instead of 12 — the 1024-thread kernel's budget)
-    const D3 pc = kFma ? rt_apply(R, T + 4, Pw) : se3_apply(T, Pw);
-    if (!(pc.z > 1e-6)) return;
-    const double inv_z = frcp(pc.z);
-    const double x = pc.x * inv_z, y = pc.y * inv_z;
-    const double e0 = uv.x - (fx * x + C[2]);
-    const double e1 = uv.y - (fy * y + C[3]);
-    const double e2 = e0 * e0 + e1 * e1;
-    double w = 1.0;
-    if constexpr (kFma) {
-        if (e2 > a.max_err2) return;
-        if (e2 > a.huber2) w = a.huber * frsq(e2);
-    } else {  // (the round-1 form: |e| by v_rsq, branch-free weight)
+    if constexpr (!kFma) {
+        // the round-1 form with early returns, the quaternion rotation, |e| by v_rsq and products
+        // then sums: fewer live registers (the 1024-thread kernel's 128-VGPR budget)
+        if (!valid) return;
+        const D3 pc = se3_apply(T, Pw);
+        if (!(pc.z > 1e-6)) return;
+        const double inv_z = frcp(pc.z);
+        const double x = pc.x * inv_z, y = pc.y * inv_z;
+        const double e0 = uv.x - (fx * x + C[2]);
+        const double e1 = uv.y - (fy * y + C[3]);
+        const double e2 = e0 * e0 + e1 * e1;
         const double re = e2 > 0.0 ? frsq(e2) : 0.0;
         const double en = e2 * re;
         if (en > a.max_err) return;
-        w = en <= a.huber ? 1.0 : a.huber * re;
-    }
-    // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
-    // written out without its structural zeros (J0[1] = J1[0] = 0)
-    const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
-    const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, fma(jp0, pc.z, -jp2 * pc.x), -jp0 * pc.y};
-    const double J1[6] = {0.0, jp4, jp5, fma(jp5, pc.y, -jp4 * pc.z), -jp5 * pc.x, jp4 * pc.x};
-    if constexpr (!kFma) {  // products then sums: fewer live registers (the 1024-thread kernel's budget)
+        const double w = en <= a.huber ? 1.0 : a.huber * re;
+        const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+        const double J0[6] = {jp0, 0.0, jp2, jp2 * pc.y, fma(jp0, pc.z, -jp2 * pc.x), -jp0 * pc.y};
+        const double J1[6] = {0.0, jp4, jp5, fma(jp5, pc.y, -jp4 * pc.z), -jp5 * pc.x, jp4 * pc.x};
 #pragma unroll
         for (int r = 0; r < 6; ++r)
 #pragma unroll
@@ -252,6 +250,21 @@ __device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T,
         v[28] += 1.0;
         return;
     }
+    const D3 pc = rt_apply(R, T + 4, Pw);
+    const bool front = pc.z > 1e-6;
+    const double inv_z = frcp(front ? pc.z : 1.0);
+    const double x = pc.x * inv_z, y = pc.y * inv_z;
+    const double e0 = uv.x - (fx * x + C[2]);
+    const double e1 = uv.y - (fy * y + C[3]);
+    const double e2 = e0 * e0 + e1 * e1;
+    const bool ok = valid && front && !(e2 > a.max_err2);
+    const double w = ok ? (e2 > a.huber2 ? a.huber * frsq(e2) : 1.0) : 0.0;
+    const double zz = front ? pc.z : 1.0, xx = front ? pc.x : 0.0, yy = front ? pc.y : 0.0;
+    // J = Jp * [I | -hat(pc)] (local_ba.cpp:15-33) with Jp = [[jp0, 0, jp2], [0, jp4, jp5]],
+    // written out without its structural zeros (J0[1] = J1[0] = 0)
+    const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+    const double J0[6] = {jp0, 0.0, jp2, jp2 * yy, fma(jp0, zz, -jp2 * xx), -jp0 * yy};
+    const double J1[6] = {0.0, jp4, jp5, fma(jp5, yy, -jp4 * zz), -jp5 * xx, jp4 * xx};
     // w J^T J, -w J^T e and w |e|^2 accumulated as FMA chains (the FP64 issue rate bounds this loop,
     // ~2 FMAs per term instead of 2 products and 2 sums)
     double wJ0[6], wJ1[6];
@@ -278,7 +291,7 @@ __device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T,
         v[21 + r] = acc;
     }
     v[27] = fma(w, e2, v[27]);
-    v[28] += 1.0;
+    v[28] += ok ? 1.0 : 0.0;
 }
 
 // Pose stage (local_ba.cpp:116-161): n_split workgroups per keyframe, each over a contiguous
@@ -928,11 +941,12 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 u0 = f.pobs_uv[wstart + 64 * (r + 1) + lane];
                 p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
             }
-            if (e.z + 64 * q + lane < e.w) {
+            const bool valid = e.z + 64 * q + lane < e.w;
+            if (kFT == kFTSmall || valid) {  // (512: padding lanes run too, weight 0 — no branch)
                 const int code = (int)P4.w;
                 const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]}
                                        : D3{P4.x, P4.y, P4.z};
-                pose_obs_accum<kFT == kFTSmall>(a, T, R, C, P, uv, v);
+                pose_obs_accum<kFT == kFTSmall>(a, T, R, C, P, uv, v, valid);
             }
         }
         if (j == wv) FKT(7);
