@@ -264,7 +264,7 @@ __device__ void se3_left_update(const double* dx, double* T) {
         const double t4 = t * t;
         imag = 0.5 - (1.0 / 48.0) * t + (1.0 / 3840.0) * t4;
         real = 1.0 - (1.0 / 8.0) * t + (1.0 / 384.0) * t4;
-    } else if (t < 1e-2) {
+    } else {
         // theta < 0.1 (every Gauss-Newton step of a converging window): Taylor series in
         // theta^2 (truncation < 1e-22 relative) of sin(theta/2)/theta, cos(theta/2),
         // (1 - cos theta)/theta^2 and (theta - sin theta)/theta^3 — no sqrt / sincos / division
@@ -272,17 +272,24 @@ __device__ void se3_left_update(const double* dx, double* T) {
         real = 1.0 + t * (-1.0 / 8 + t * (1.0 / 384 + t * (-1.0 / 46080 + t * (1.0 / 10321920 + t * (-1.0 / 3715891200.0)))));
         c1 = 0.5 + t * (-1.0 / 24 + t * (1.0 / 720 + t * (-1.0 / 40320 + t * (1.0 / 3628800 + t * (-1.0 / 479001600.0)))));
         c2 = 1.0 / 6 + t * (-1.0 / 120 + t * (1.0 / 5040 + t * (-1.0 / 362880 + t * (1.0 / 39916800 + t * (-1.0 / 6227020800.0)))));
-    } else {
-        const double theta = sqrt(t);
-        double sh, ch;
-        sincos(0.5 * theta, &sh, &ch);
-        const double it = frcp(theta);
-        imag = sh * it;
-        real = ch;
-        // 1 - cos theta = 2 sin^2(theta/2), sin theta = 2 sin(theta/2) cos(theta/2)
-        const double rsq = it * it;
-        c1 = (2.0 * sh * sh) * rsq;
-        c2 = (theta - 2.0 * sh * ch) * (rsq * it);
+    }
+    // theta >= 0.1: the exact forms.  The wave-uniform vote keeps this a real branch — as a plain
+    // per-lane branch the compiler if-converted it, and every pose solve paid the double-precision
+    // sincos (~150 FP64 instructions) whether or not a lane needed it.
+    const bool big = !tiny && !(t < 1e-2);
+    if (__ballot(big) != 0ull) {
+        if (big) {
+            const double theta = sqrt(t);
+            double sh, ch;
+            sincos(0.5 * theta, &sh, &ch);
+            const double it = frcp(theta);
+            imag = sh * it;
+            real = ch;
+            // 1 - cos theta = 2 sin^2(theta/2), sin theta = 2 sin(theta/2) cos(theta/2)
+            const double rsq = it * it;
+            c1 = (2.0 * sh * sh) * rsq;
+            c2 = (theta - 2.0 * sh * ch) * (rsq * it);
+        }
     }
     const double eq[4] = {imag * wx, imag * wy, imag * wz, real};
     const double O[9] = {0, -wz, wy, wz, 0, -wx, -wy, wx, 0};
