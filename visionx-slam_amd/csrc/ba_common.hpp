@@ -19,23 +19,20 @@ namespace ba {
 
 struct D3 { double x, y, z; };
 
-// 1 / b: v_rcp_f64 and two Newton steps (about 1 ulp) instead of the ~12-instruction IEEE division
-// sequence, which sits on every dependency chain below.  BA parity is a tolerance (1e-4), not a
-// bit pattern; b = 0 / denormal operands do not reach these call sites (gated by the caller).
+// 1 / b: v_rcp_f64 (~2.5e8 ulp, i.e. ~28 bits) and one Newton step: within 11 ulp (2.4e-15
+// relative; scripts/probes/rcp_accuracy.hip on gfx950) instead of the ~12-instruction IEEE division
+// sequence, which sits on every dependency chain below — a second step (0 ulp) costs two more
+// dependent FMAs.  BA parity is a tolerance (1e-4, gate margins >= 1e-8), not a bit pattern;
+// b = 0 / denormal operands do not reach these call sites (gated by the caller).
 __device__ __forceinline__ double frcp(double b) {
-    double r = __builtin_amdgcn_rcp(b);
-    r = fma(fma(-b, r, 1.0), r, r);
-    r = fma(fma(-b, r, 1.0), r, r);
-    return r;
+    const double r = __builtin_amdgcn_rcp(b);
+    return fma(fma(-b, r, 1.0), r, r);
 }
 
-// 1 / sqrt(x): v_rsq_f64 and two Newton steps (x > 0 at the call sites).
+// 1 / sqrt(x): v_rsq_f64 and one Newton step (within 20 ulp; x > 0 at the call sites).
 __device__ __forceinline__ double frsq(double x) {
-    double r = __builtin_amdgcn_rsq(x);
-    const double hx = 0.5 * x;
-    r = r * fma(-hx * r, r, 1.5);
-    r = r * fma(-hx * r, r, 1.5);
-    return r;
+    const double r = __builtin_amdgcn_rsq(x);
+    return r * fma(-(0.5 * x) * r, r, 1.5);
 }
 
 // 64-bit cross-lane exchanges for the reduction butterfly, on the VALU instead of the LDS crossbar
