@@ -219,7 +219,7 @@ def main():
                          "(vx_set_grid_share; default 1/3 with more than one stream, 1 otherwise)")
     ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
                     help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
-    ap.add_argument("--extract-ctx", type=int, default=2, choices=(1, 2),
+    ap.add_argument("--extract-ctx", type=int, default=2, choices=(1, 2, 3, 4),
                     help="extraction contexts (with --streams 3): frames alternate between them, so the "
                          "extraction of frame t+1 overlaps frame t's; Match and LocalBA stay in frame order")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),
@@ -308,8 +308,9 @@ def main():
     skip = args.diag_skip
     if skip == "ba":
         plan.run_async()  # (so the statistics fetched at the end exist)
-    if skip == "match":
-        mctx.match_device_async(slot[loc(-2)], slot[loc(-1)])
+    if skip == "match":  # (so the matches fetched at the end exist)
+        for mc in (ectxs if mon else [mctx]):
+            mc.match_device_async(slot[loc(-2)], slot[loc(-1)])
 
     def step(i):
         ci, si = loc(i)

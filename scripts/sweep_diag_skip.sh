@@ -1,7 +1,7 @@
 #!/bin/bash
 # which chain bounds the pipelined frame: bench.py with one stage left out (diagnostic), 2 runs each
 cd "$GRAFT_REPO_ROOT" || exit 1
-for e in 1 2; do
+for e in ${EXTRACT_CTX:-1 2}; do
   for sk in "" ba match extract; do
     vals=""
     for rep in 1 2; do
