@@ -178,14 +178,14 @@ __global__ __launch_bounds__(kT) void k_fixed_slots(WinArgs a, const int* scan, 
 }
 
 __global__ __launch_bounds__(kT) void k_pose_fill(WinArgs a, const int* pscan, const double* wuv, double2* puv,
-                                                  int* plm, int* kf_obs_ptr, int n_pose) {
+                                                  int* plm, int* kf_obs_ptr) {
     const int f = blockIdx.x * kT + threadIdx.x;
     if (f < a.nf && a.f_pv[f]) {
         const int o = pscan[f];
         puv[o] = make_double2(wuv[2 * f], wuv[2 * f + 1]);
         plm[o] = a.l_slot[a.f_lm[f]];
     }
-    if (f <= a.nk) kf_obs_ptr[f] = f < a.nk ? pscan[a.wptr[f]] : n_pose;  // (wptr[nk] == nf)
+    if (f <= a.nk) kf_obs_ptr[f] = pscan[a.wptr[f]];  // (wptr[nk] == nf: the total)
 }
 
 // landmark-stage observation check (local_ba.cpp:186-204); returns the window feature or -1
@@ -472,30 +472,31 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     // pose-stage CSR
     int* pscan = B.scan_b.as<int>();  // (first_scan consumed by k_fixed_slots above, stream-ordered)
     if ((rc = scan(c, B.tmp, a.f_pv, pscan, nf))) return rc;
-    int n_pose = 0;
-    VX_HIP(c, hipMemcpyAsync(&n_pose, pscan + nf, 4, hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipStreamSynchronize(s));
-    p->n_pose_obs = n_pose;
-    VX_HIP(c, p->pobs_uv.ensure((size_t)std::max(n_pose, 1) * sizeof(double2)));
-    VX_HIP(c, p->pobs_lm.ensure((size_t)std::max(n_pose, 1) * 4));
+    // (sized for every window feature: the count arrives with the next read-back, no sync for it)
+    VX_HIP(c, p->pobs_uv.ensure((size_t)std::max(nf, 1) * sizeof(double2)));
+    VX_HIP(c, p->pobs_lm.ensure((size_t)std::max(nf, 1) * 4));
     VX_HIP(c, p->kf_obs_ptr.ensure((size_t)(nk + 1) * 4));
     hipLaunchKernelGGL(k_pose_fill, dim3(grid(std::max(nf, nk + 1))), dim3(kT), 0, s, a, pscan,
-                       in.wuv, p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(),
-                       p->kf_obs_ptr.as<int>(), n_pose);
+                       in.wuv, p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(), p->kf_obs_ptr.as<int>());
     // landmark-stage CSR
     int* cnt = B.cnt.as<int>();
     hipLaunchKernelGGL(k_lobs_count, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, cnt);
     VX_LAUNCH_CHECK(c, "plan CSR kernels");
     VX_HIP(c, p->lobs_ptr.ensure((size_t)(n_opt + 1) * 4));
     if ((rc = scan(c, B.tmp, cnt, p->lobs_ptr.as<int>(), n_opt))) return rc;
-    std::vector<int> lptr(n_opt + 1);
-    std::vector<int> inv_h(std::max(n_lm, 1));
-    VX_HIP(c, hipMemcpyAsync(lptr.data(), p->lobs_ptr.p, (size_t)(n_opt + 1) * 4, hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipMemcpyAsync(inv_h.data(), inv, (size_t)n_lm * 4, hipMemcpyDeviceToHost, s));
+    // one read-back: the pose-stage count, the landmark-stage pointers, slot -> map index (pinned)
+    VX_HIP(c, B.rb_host.ensure((size_t)(n_opt + 1 + std::max(n_lm, 1) + 4) * 4, true));
+    int* RB = static_cast<int*>(B.rb_host.p);
+    VX_HIP(c, hipMemcpyAsync(RB, pscan + nf, 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(RB + 4, p->lobs_ptr.p, (size_t)(n_opt + 1) * 4, hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(RB + 4 + n_opt + 1, inv, (size_t)n_lm * 4, hipMemcpyDeviceToHost, s));
     VX_HIP(c, hipStreamSynchronize(s));
+    p->n_pose_obs = RB[0];
+    const std::vector<int> lptr(RB + 4, RB + 4 + n_opt + 1);
+    const int* inv_h = RB + 4 + n_opt + 1;
     const int n_lobs = lptr[n_opt];
     p->n_lm_obs = n_lobs;
-    p->lm_map_idx.assign(inv_h.begin(), inv_h.begin() + n_lm);
+    p->lm_map_idx.assign(inv_h, inv_h + n_lm);
     VX_HIP(c, p->lobs_kf.ensure((size_t)std::max(n_lobs, 1) * 4));
     VX_HIP(c, p->lobs_lm.ensure((size_t)std::max(n_lobs, 1) * 4));
     VX_HIP(c, p->lobs_uv.ensure((size_t)std::max(n_lobs, 1) * sizeof(double2)));
@@ -508,12 +509,22 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     VX_LAUNCH_CHECK(c, "plan fill kernels");
     const std::vector<int> blk = pack_lm_blocks(lptr, n_opt, &p->max_lm_obs);
     p->n_lm_blocks = (int)blk.size() / 2 - 1;
-    if ((rc = up(c, p->lm_blk, blk.data(), blk.size()))) return rc;
-    if ((rc = up(c, p->kf_flags, kf_flags.data(), kf_flags.size()))) return rc;
+    // both tables through a pinned block (no synchronisation here: the fused build below reads back
+    // and synchronises before the next plan build can reuse the block, and a plan without the fused
+    // layout synchronises at the end)
+    const size_t nblk = blk.size(), nflg = kf_flags.size();
+    VX_HIP(c, B.up_host.ensure((nblk + nflg) * 4, true));
+    int* UP = static_cast<int*>(B.up_host.p);
+    std::copy(blk.begin(), blk.end(), UP);
+    std::copy(kf_flags.begin(), kf_flags.end(), UP + nblk);
+    VX_HIP(c, p->lm_blk.ensure(nblk * 4));
+    VX_HIP(c, p->kf_flags.ensure(std::max<size_t>(nflg, 1) * 4));
+    VX_HIP(c, hipMemcpyAsync(p->lm_blk.p, UP, nblk * 4, hipMemcpyHostToDevice, s));
+    if (nflg) VX_HIP(c, hipMemcpyAsync(p->kf_flags.p, UP + nblk, nflg * 4, hipMemcpyHostToDevice, s));
     if ((rc = alloc_run_buffers(c, p))) return rc;
-    VX_HIP(c, hipStreamSynchronize(s));  // the host vectors above must outlive their async copies
     // the fused layout, on the device from the CSRs just built (every plan, sharded ones included)
     if ((rc = build_fused_device(c, p))) return rc;
+    if (!p->fused) VX_HIP(c, hipStreamSynchronize(s));  // (the pinned block above)
     return VX_OK;
 }
 }  // namespace
@@ -610,14 +621,18 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
                    B.wid.as<uint64_t>(), B.wuv.as<double>(), m->lm_id.as<uint64_t>(), m->lm_bad.as<uint8_t>(),
                    m->optr.as<int64_t>(), m->okf.as<uint64_t>(), m->ofi.as<uint64_t>(), m->lm_pos.as<double>()};
     rc = build_core(c, in, win, kf_flags, p);
-    VX_HIP(c, hipStreamSynchronize(c->stream));
-    if (rc) return rc;
-    // device copies of the slot -> map index tables for vx_ba_plan_apply_dmap
-    if (p->status == 0) {
-        if ((rc = up(c, p->kf_map_dev, p->kf_map_idx.data(), p->kf_map_idx.size()))) return rc;
-        if ((rc = up(c, p->lm_map_dev, p->lm_map_idx.data(), p->lm_map_idx.size()))) return rc;
-        VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (rc) {
+        (void)hipStreamSynchronize(c->stream);
+        return rc;
     }
+    // device copies of the slot -> map index tables for vx_ba_plan_apply_dmap (the landmark one is
+    // still on the device: build_core's slot -> map index array)
+    if (p->status == 0) {
+        VX_HIP(c, p->lm_map_dev.ensure((size_t)std::max(p->n_lm, 1) * 4));
+        VX_HIP(c, hipMemcpyAsync(p->lm_map_dev.p, B.inv.p, (size_t)p->n_lm * 4, hipMemcpyDeviceToDevice, c->stream));
+        if ((rc = up(c, p->kf_map_dev, p->kf_map_idx.data(), p->kf_map_idx.size()))) return rc;
+    }
+    VX_HIP(c, hipStreamSynchronize(c->stream));
     return VX_OK;
 }
 

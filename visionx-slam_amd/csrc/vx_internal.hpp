@@ -200,6 +200,7 @@ struct vx_ctx {
             l_ref, l_opt, l_slot, l_first, counts, scan_a, scan_b, scan_c, inv, cnt, tmp;
         vx::DevBuf fb, fb_groups, fb_tmp;  // device build of the fused layout (ba_fused_build.hip)
         vx::PinnedBuf fb_host;             // its two small read-backs
+        vx::PinnedBuf rb_host, up_host;    // build_core's read-back and its table uploads
     } plan_scratch;
     // LocalBA plans of this context: parked buffer sets of destroyed plans (adopted by the next
     // vx_ba_plan_create) and the live plans (detached when the context goes first)
