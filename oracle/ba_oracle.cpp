@@ -31,7 +31,8 @@ using namespace orc_ba;
 // wall time of the last call's two parts (bench.py's CPU baseline reports them apart): the window /
 // landmark-set selection (local_ba.cpp:66-108, what a GPU plan build replaces) and the iterations
 // (local_ba.cpp:110-248, what a GPU plan run replaces)
-static double g_setup_s = 0.0, g_iter_s = 0.0;
+// (per thread: bench.py's multi-threaded CPU baseline runs frames on several threads at once)
+static thread_local double g_setup_s = 0.0, g_iter_s = 0.0;
 
 extern "C" void orc_ba_last_timing(double* out2) {
     out2[0] = g_setup_s;

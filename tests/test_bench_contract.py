@@ -64,3 +64,17 @@ def test_bench_json_line():
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] < 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-4
+
+
+def test_cpu_baseline_mt_small():
+    """The multi-threaded CPU leg (SURVEY.md §8(d) best-effort CPU) on a tiny workload."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
+    import bench
+    from vxslam import synth
+
+    h, w, nf, nk, nl = 120, 160, 200, 5, 300
+    frames = synth.make_frames(7, 2, h, w)
+    m = synth.make_ba_map(7, nk, nl)
+    d = bench.cpu_baseline_mt((h, w, nf, nk, nl), frames, m, 2)
+    assert d["value"] > 0 and d["cores"] >= 1 and d["unit"] == "ms/frame" and d["kind"] == "port"
