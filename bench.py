@@ -35,8 +35,8 @@ METRIC = "ms/frame (feature-extract+match + BA solve), 640×480, 50 KF / 20k pts
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # profiling stage -> the HIP kernel it brackets (the name in the rocprofv3 summaries)
 HIP_KERNEL = {"orb_pyramid": "k_pyramid", "orb_fast_harris": "k_fast", "orb_select": "k_select",
-              "orb_blur": "k_blur", "orb_describe": "k_describe", "match_partial": "k_knn_partial",
-              "match_merge": "k_knn_merge+k_knn_compact", "ba_pose_partial": "k_pose_kf",
+              "orb_blur": "k_blur", "orb_describe": "k_describe", "match_partial": "k_knn_rows",
+              "match_merge": "k_knn_compact", "ba_pose_partial": "k_pose_kf",
               "ba_landmark": "k_landmark_solve", "ba_iter": "k_ba_iter", "ba_prologue": "k_ba_iter"}
 
 CONFIGS = {
@@ -69,10 +69,10 @@ def stage_bytes(stage, geo, counts):
         return 16 * counts["n_cand"] + 16 * N
     if stage == "orb_describe":
         return N * (16 + 20 + 32)
-    if stage == "match_partial":
-        return (counts["n_q"] + counts["n_t"]) * 32 + counts["n_q"] * 8 * ((counts["n_t"] + 63) // 64)
-    if stage == "match_merge":
-        return counts["n_q"] * 8 * ((counts["n_t"] + 63) // 64) + counts["n_match"] * 12
+    if stage == "match_partial":    # k_knn_rows: both descriptor sets in, one key per query out
+        return (counts["n_q"] + counts["n_t"]) * 32 + counts["n_q"] * 4
+    if stage == "match_merge":      # k_knn_compact: the keys in, the ordered matches out
+        return counts["n_q"] * 4 + counts["n_match"] * 12
     if stage == "ba_pose_partial":
         # per observation: uv 16 + landmark slot 4 + landmark position 24 (gathered); per slice
         # partial: 32 doubles written; per keyframe: pose 64 + intrinsics 32 read

@@ -13,6 +13,7 @@
 //                  v_med3: VALU-popcount bound.
 //   k_knn_merge    one block: merge chunk partials, ratio test, ordered compaction (ascending
 //                  query index) by block scan.
+#include <cstdlib>
 #include <cstring>
 
 #include "vx_internal.hpp"
@@ -65,6 +66,108 @@ __global__ __launch_bounds__(kQB) void k_knn_partial(const uint8_t* __restrict__
     }
     partial[(long long)chunk * q_stride + qi] = make_uint2(k1, k2);
     (void)n_chunks_cap;
+}
+
+// Whole-row kNN-2 (default): a workgroup takes kRQ queries against the whole train set, so no
+// chunk partials go through memory and no merge launch follows.  The queries are wave-uniform (their
+// 32 B each in SGPRs: every v_xor takes its query word as the scalar operand); thread tid holds train
+// rows tid, tid + kRT, ... (4 in registers per pass) and keeps a top-2 per query; the top-2s are
+// merged per query by one wave (LDS transpose, then DPP), then the ratio test.
+// The merge of two lexicographic top-2s is exact in any order, so the result is the sequential
+// scan's (the chunked kernels above stay for comparison: VX_MATCH_CHUNKED=1).
+constexpr int kRQ = 8;     // queries per workgroup
+constexpr int kRT = 512;   // threads per workgroup
+
+__device__ __forceinline__ void top2_merge(unsigned& k1, unsigned& k2, unsigned o1, unsigned o2) {
+    const unsigned n2 = min(max(k1, o1), min(k2, o2));
+    k1 = min(k1, o1);
+    k2 = n2;
+}
+
+// one DPP step of the top-2 reduction: merge with the pair `CTRL` moves here (lanes of rows outside
+// ROWS, or without a source, merge the empty pair)
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ void top2_dpp(unsigned& k1, unsigned& k2) {
+    const unsigned o1 = (unsigned)__builtin_amdgcn_update_dpp((int)kNone, (int)k1, CTRL, ROWS, 0xF, false);
+    const unsigned o2 = (unsigned)__builtin_amdgcn_update_dpp((int)kNone, (int)k2, CTRL, ROWS, 0xF, false);
+    top2_merge(k1, k2, o1, o2);
+}
+
+static_assert(kRT / 64 == kRQ, "k_knn_rows: one wave per query in the reduction");
+
+__global__ __launch_bounds__(kRT) void k_knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p,
+                                                  int nq_host, const uint8_t* __restrict__ t,
+                                                  const int* __restrict__ nt_p, int nt_host, float ratio,
+                                                  unsigned* __restrict__ best) {
+    __shared__ uint2 tr[kRQ][kRT];  // the threads' top-2s, query-major (32 KB)
+    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
+    const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
+    const int q0 = blockIdx.x * kRQ;
+    if (q0 >= nq) return;  // block-uniform
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    uint4 A0[kRQ], A1[kRQ];
+#pragma unroll
+    for (int i = 0; i < kRQ; ++i) {
+        const int qi = min(q0 + i, nq - 1);  // (past the end: a copy of the last query, not written)
+        A0[i] = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[0];
+        A1[i] = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[1];
+    }
+    unsigned k1[kRQ], k2[kRQ];
+#pragma unroll
+    for (int i = 0; i < kRQ; ++i) k1[i] = k2[i] = kNone;
+    for (int r0 = tid; r0 < nt; r0 += 4 * kRT) {
+        uint4 B0[4], B1[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = min(r0 + j * kRT, nt - 1);
+            B0[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[0];
+            B1[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[1];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = r0 + j * kRT;
+            const unsigned tag = row < nt ? (unsigned)row : 0u;
+#pragma unroll
+            for (int i = 0; i < kRQ; ++i) {
+                unsigned d = __builtin_popcount(A0[i].x ^ B0[j].x);
+                d += __builtin_popcount(A0[i].y ^ B0[j].y);
+                d += __builtin_popcount(A0[i].z ^ B0[j].z);
+                d += __builtin_popcount(A0[i].w ^ B0[j].w);
+                d += __builtin_popcount(A1[i].x ^ B1[j].x);
+                d += __builtin_popcount(A1[i].y ^ B1[j].y);
+                d += __builtin_popcount(A1[i].z ^ B1[j].z);
+                d += __builtin_popcount(A1[i].w ^ B1[j].w);
+                const unsigned key = row < nt ? (d << 22) | tag : kNone;
+                k2[i] = max(min(k1[i], key), min(k2[i], max(k1[i], key)));
+                k1[i] = min(k1[i], key);
+            }
+        }
+    }
+    // transpose through LDS: wave w then reduces query w — 8 entries per lane, then the 64 lanes by
+    // DPP (xor 1, xor 2, half-row and row mirrors, row broadcasts 15 / 31: lane 63 ends with all)
+#pragma unroll
+    for (int i = 0; i < kRQ; ++i) tr[i][tid] = make_uint2(k1[i], k2[i]);
+    __syncthreads();
+    unsigned a1 = kNone, a2 = kNone;
+#pragma unroll
+    for (int g = 0; g < kRT / 64; ++g) {
+        const uint2 v = tr[wv][64 * g + lane];
+        top2_merge(a1, a2, v.x, v.y);
+    }
+    top2_dpp<0xB1>(a1, a2);        // quad_perm [1,0,3,2]
+    top2_dpp<0x4E>(a1, a2);        // quad_perm [2,3,0,1]
+    top2_dpp<0x141>(a1, a2);       // row_half_mirror
+    top2_dpp<0x140>(a1, a2);       // row_mirror
+    top2_dpp<0x142, 0xA>(a1, a2);  // row_bcast:15 into rows 1, 3
+    top2_dpp<0x143, 0xC>(a1, a2);  // row_bcast:31 into rows 2, 3
+    if (lane == 63 && q0 + wv < nq) {
+        bool keep = false;
+        if (a2 != kNone) {  // knn.size() == 2 (orb_matcher.cpp:28)
+            const float d1 = (float)(a1 >> 22), d2 = (float)(a2 >> 22);
+            keep = d1 < ratio * d2;  // orb_matcher.cpp:33
+        }
+        best[q0 + wv] = keep ? a1 : kNone;
+    }
 }
 
 // Exclusive block scan: wave prefix by __shfl_up, then the NT/64 wave totals from LDS (two
@@ -136,19 +239,26 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __r
     __shared__ int sh[kMergeBlock / 64];
     const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
     int written = 0;
-    for (int base = 0; base < nq; base += kMergeBlock) {
-        const int qi = base + threadIdx.x;
-        const unsigned k1 = qi < nq ? best[qi] : kNone;
-        const int keep = k1 != kNone;
+    // 4 consecutive queries per thread (one pass up to 4096 queries: one load latency, one scan)
+    for (int base = 0; base < nq; base += 4 * kMergeBlock) {
+        const int q4 = base + 4 * threadIdx.x;
+        unsigned k[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = q4 + j < nq ? best[q4 + j] : kNone;
+        int n4 = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) n4 += k[j] != kNone;
         int cnt;
-        const int pos = scan_excl<kMergeBlock>(keep, sh, cnt);
-        if (keep) {
-            vx_match m;
-            m.query_idx = qi;
-            m.train_idx = (int)(k1 & 0x3fffffu);
-            m.distance = (float)(k1 >> 22);
-            out[written + pos] = m;
-        }
+        int pos = written + scan_excl<kMergeBlock>(n4, sh, cnt);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (k[j] != kNone) {
+                vx_match m;
+                m.query_idx = q4 + j;
+                m.train_idx = (int)(k[j] & 0x3fffffu);
+                m.distance = (float)(k[j] >> 22);
+                out[pos++] = m;
+            }
         written += cnt;
     }
     if (threadIdx.x == 0) *out_count = written;
@@ -162,6 +272,21 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
     VX_HIP(c, c->matches.ensure((size_t)std::max(q_cap, 1) * sizeof(vx_match)));
     VX_HIP(c, c->match_count.ensure(16));
     c->match_cap = q_cap;
+    static const bool chunked = [] {
+        const char* e = getenv("VX_MATCH_CHUNKED");
+        return e && e[0] == '1';
+    }();
+    if (!chunked) {
+        unsigned* best = reinterpret_cast<unsigned*>(c->partial.as<uint2>() + (size_t)n_chunks * q_stride);
+        VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows, dim3((q_cap + kRQ - 1) / kRQ), dim3(kRT), 0, c->stream, dq,
+                         dnq, nq_host, dt, dnt, nt_host, ratio, best));
+        ProfScope ps(c, kStMatchMerge);
+        hipLaunchKernelGGL(k_knn_compact, dim3(1), dim3(kMergeBlock), 0, c->stream, best, dnq, nq_host,
+                           c->matches.as<vx_match>(), c->match_count.as<int>());
+        VX_LAUNCH_CHECK(c, "k_knn_compact");
+        c->match_valid = true;
+        return VX_OK;
+    }
     VX_HIP(c, launch(c, kStMatchPartial, k_knn_partial, dim3((q_cap + kQB - 1) / kQB, n_chunks), dim3(kQB), 0,
                      c->stream, dq, dnq, nq_host, dt, dnt, nt_host, n_chunks, c->partial.as<uint2>(), q_stride));
     {
