@@ -148,6 +148,7 @@ def timed_loop(step, steps, warmup, sync, dist):
     t0 = time.perf_counter()
     for i in range(steps):
         step(warmup + i)
+    timed_loop.enqueue_s = time.perf_counter() - t0  # host enqueue alone (diagnostic)
     sync()
     dist.barrier()
     t1 = time.perf_counter()
@@ -258,6 +259,8 @@ def main():
                     help="fraction of the CUs reserved for the LocalBA context (disjoint CU masks; 0: shared)")
     ap.add_argument("--diag-skip", default="", choices=("", "ba", "match", "extract"),
                     help="diagnostics only (the JSON line is marked invalid): leave one stage out of every step")
+    ap.add_argument("--diag-nodep", action="store_true",
+                    help="diagnostics only (the JSON line is marked invalid): LocalBA(t) does not wait for Match(t)")
     ap.add_argument("--ba-priority", type=int, default=0, choices=(0, 1),
                     help="stream priority of the LocalBA context (1: the device's greatest)")
     ap.add_argument("--grid-share", type=float, default=None,
@@ -373,7 +376,8 @@ def main():
         if skip != "match":
             mx.match_device_async(slot[loc(i - 1)], slot[loc(i)])
         mx.record(ev_m[i % (4 * E)])
-        bctx.wait_event(ev_m[i % (4 * E)])
+        if not args.diag_nodep:
+            bctx.wait_event(ev_m[i % (4 * E)])
         if skip != "ba":
             plan.run_async()
 
@@ -399,6 +403,7 @@ def main():
 
     # ---- the timed region: no events inside (a timing event pair per launch costs ~25 % here)
     elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
+    enqueue_ms = 1e3 * timed_loop.enqueue_s / args.steps
 
     # ---- roofline pass: the same K steps again, HIP events around every launch of the dominant
     # kernel on the stream it runs on (each bracket also spans that launch's dispatch boundary)
@@ -473,7 +478,8 @@ def main():
         if skip:
             log(f"[bench] --diag-skip {skip}: diagnostic run, not the metric")
         out = {
-            "metric": METRIC if not skip else f"DIAGNOSTIC (stage {skip} skipped)",
+            "metric": (METRIC if not skip and not args.diag_nodep else
+                       f"DIAGNOSTIC ({f'stage {skip} skipped' if skip else 'LocalBA not ordered after Match'})"),
             "value": round(value, 4),
             "unit": "ms/frame",
             "n_gpus": N,
@@ -505,6 +511,9 @@ def main():
             # one frame alone through the same dependency chain (host enqueue to completion, median
             # of 20): the per-frame latency; `value` is the pipelined throughput
             "latency_ms_per_frame": round(latency_ms, 4),
+            # host time to enqueue one step (Python + C-ABI calls, graph launches), diagnostic: the
+            # GPU pipeline cannot run faster than this
+            "host_enqueue_ms_per_step": round(enqueue_ms, 4),
             # the LocalBA plan (SelectKeyFrames + landmark set + CSRs) built on the device from the
             # map snapshot, incl. upload: paid once per LocalBA::Optimize() call of a drop-in
             # (a new keyframe, tracking.cpp:76-84); the timed steps replay a resident plan

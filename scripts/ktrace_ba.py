@@ -41,15 +41,37 @@ def report(tr2, slots, name):
 
 
 def main():
+    if os.environ.get("KT_LOAD"):  # (torch's HIP initialisation must come before the library's)
+        import torch
+
+        torch.zeros(1, device="cuda")
     nk, nl, ns = synth.ba_config("C3")
     m = synth.make_ba_map(0x5EED0003, nk, nl)
     ctx = vxslam.Context(0)
     # fused path (default): the traced launch is k_ba_iter(it = 1) of a 5-iteration run
     plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk, iters=5))
     print("plan", plan.info())
-    for _ in range(30):
+    # KT_LOAD=extract: the traced runs beside ORB extraction on two other contexts (grid share 1/3,
+    # frames alternate), as in bench.py's pipeline — which phases the interference stretches
+    load = os.environ.get("KT_LOAD", "")
+    if load == "extract":
+        import torch
+
+        ex = [vxslam.Context(0), vxslam.Context(0)]
+        for c in ex:
+            c.set_grid_share(1.0 / 3.0)
+        frames = torch.from_numpy(synth.make_frames(7, 8, 480, 640)).cuda()
+        params = vxslam.default_orb_params(n_features=2000)
+        torch.cuda.synchronize()
+    for i in range(30):
+        if load == "extract":
+            for j in range(2):
+                ex[j].orb_extract_async(frames[(2 * i + j) % 8].data_ptr(), 640, 480, 3, 640 * 3, i % 3, params)
         plan.run_async()
     ctx.synchronize()
+    if load == "extract":
+        for c in ex:
+            c.synchronize()
     tr2 = read()
     report(tr2, [0, 1, 2, 3, 4, 6, 7, 5],
            "k_ba_iter (1 loads, 2 combine + totals + barrier, 3 pose solve + barrier, 4 landmark stage + barrier, "
