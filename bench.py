@@ -288,12 +288,13 @@ def main():
     # compute units (every k-th CU, spread over the XCDs) and extraction / matching the rest
     fe_mask = ba_mask = None
     if args.ba_cus > 0 and args.streams > 1:
-        # the smaller side gets every k-th CU (spread over the XCDs), the other side the rest
+        # the smaller side gets round(share x CUs) CUs evenly spaced over the CU indices (so over the
+        # XCDs), the other side the rest
         ncu = vxslam.lib().vx_device_cus(dist.local_rank)
         small = min(args.ba_cus, 1.0 - args.ba_cus)
-        k = max(2, int(round(1.0 / small)))
-        few = [i for i in range(ncu) if i % k == k - 1]
-        rest = [i for i in range(ncu) if i % k != k - 1]
+        n_few = max(1, int(round(small * ncu)))
+        few = sorted({int(j * ncu / n_few) for j in range(n_few)})
+        rest = [i for i in range(ncu) if i not in set(few)]
         ba_mask, fe_mask = (few, rest) if args.ba_cus <= 0.5 else (rest, few)
     n_ex = args.extract_ctx if args.streams == 3 else 1
     ectxs = [vxslam.Context(dist.local_rank, cu_mask=fe_mask) for _ in range(n_ex)]

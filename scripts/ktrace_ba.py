@@ -47,7 +47,18 @@ def main():
         torch.zeros(1, device="cuda")
     nk, nl, ns = synth.ba_config("C3")
     m = synth.make_ba_map(0x5EED0003, nk, nl)
-    ctx = vxslam.Context(0)
+    # KT_MASK=f (with KT_LOAD): LocalBA on a disjoint CU mask of that fraction of the CUs (every 3rd CU
+    # to the extraction contexts for f = 2/3, as bench.py --ba-cus does)
+    frac = float(os.environ.get("KT_MASK", "0"))
+    ba_mask = ex_mask = None
+    if frac > 0:
+        ncu = vxslam.lib().vx_device_cus(0)
+        small = min(frac, 1.0 - frac)
+        k = max(2, int(round(1.0 / small)))
+        few = [i for i in range(ncu) if i % k == k - 1]
+        rest = [i for i in range(ncu) if i % k != k - 1]
+        ba_mask, ex_mask = (few, rest) if frac <= 0.5 else (rest, few)
+    ctx = vxslam.Context(0, cu_mask=ba_mask)
     # fused path (default): the traced launch is k_ba_iter(it = 1) of a 5-iteration run
     plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk, iters=5))
     print("plan", plan.info())
@@ -57,7 +68,7 @@ def main():
     if load == "extract":
         import torch
 
-        ex = [vxslam.Context(0), vxslam.Context(0)]
+        ex = [vxslam.Context(0, cu_mask=ex_mask), vxslam.Context(0, cu_mask=ex_mask)]
         for c in ex:
             c.set_grid_share(1.0 / 3.0)
         frames = torch.from_numpy(synth.make_frames(7, 8, 480, 640)).cuda()
@@ -65,8 +76,8 @@ def main():
         torch.cuda.synchronize()
     for i in range(30):
         if load == "extract":
-            for j in range(2):
-                ex[j].orb_extract_async(frames[(2 * i + j) % 8].data_ptr(), 640, 480, 3, 640 * 3, i % 3, params)
+            for j in range(4):  # (twice the extraction work of a LocalBA run: the runs stay loaded)
+                ex[j % 2].orb_extract_async(frames[(4 * i + j) % 8].data_ptr(), 640, 480, 3, 640 * 3, (i + j // 2) % 3, params)
         plan.run_async()
     ctx.synchronize()
     if load == "extract":

@@ -698,6 +698,10 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // kernel; the 1024-thread one (128 VGPRs) keeps the indirect reads of the published poses and
     // positions, whose longer live ranges it cannot afford
     constexpr bool kEcopy = kFT == kFTSmall;
+    // highest wave priority: in the pipeline, extraction waves share these SIMDs, and the launch's
+    // dependent FP64 chains are what the frame waits for (instruction-issue arbitration prefers
+    // higher-priority waves; the co-resident waves fill the gaps of the chains)
+    __builtin_amdgcn_s_setprio(3);
     // (an iteration after the stop returns before its first write, below: its loads are issued
     // first so the flag's latency overlaps theirs)
     if (!kEcopy && !kPro && it > 0 && !a.state->active[it]) return;
