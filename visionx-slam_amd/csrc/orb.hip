@@ -644,6 +644,7 @@ constexpr int kSelBlock = 1024;
 constexpr int kCellsPer = 6;      // max cells per thread per gather pass
 constexpr int kRecBatch = 8;      // candidate records per thread loaded in one batch
 constexpr int kSelRecLds = 2048;  // survivors kept in LDS
+constexpr int kSelBins = 2048;    // one-pass select: histogram of the keys' top 11 bits
 
 // Descending-digit search over a 256-bin histogram held by threads 0..255: returns (via the
 // block) the largest digit d with count(bins >= d) >= k, and the count strictly above d.
@@ -666,8 +667,9 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
                                                       CandRec* __restrict__ stage,
                                                       int* __restrict__ level_count) {
     __shared__ int sw[kSelBlock / 64];
-    __shared__ int sh[256];
+    __shared__ int sh[kSelBins];  // radix histogram (256 bins) / the one-pass histogram (2048)
     __shared__ int s_out[2];
+    __shared__ unsigned s_bucket[64];
     __shared__ CandRec srec[kSelRecLds];  // retainBest(2q) survivors (32 KB)
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
@@ -808,7 +810,96 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
             }
             unsigned prefix = 0, mask = 0;
             int k = q;
-            for (int shift = 24; shift >= 0; shift -= 8) {
+            bool done = false;
+            if (in_regs) {
+                // one pass: a histogram of the keys over kSelBins equal bins of [min, max] (keys of
+                // similar responses share their top bits, so fixed top-bit bins crowd); wave 0
+                // finds the bin d holding the q-th largest key and the count above it; when that
+                // bin holds <= 64 keys they are compacted to LDS and wave 0 ranks them exactly
+                // (lane i: keys above / equal to its own) — the 4-pass radix below is the
+                // fallback for a crowded bin.  The bin is a monotone function of the key, so the
+                // counts above a bin are exact.
+                unsigned kmn = ~0u, kmx = 0u;
+                if (tid < K1) kmn = min(kmn, key0), kmx = max(kmx, key0);
+                if (tid + kSelBlock < K1) kmn = min(kmn, key1), kmx = max(kmx, key1);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    kmn = min(kmn, (unsigned)__shfl_xor((int)kmn, o, 64));
+                    kmx = max(kmx, (unsigned)__shfl_xor((int)kmx, o, 64));
+                }
+                if ((tid & 63) == 0) {
+                    s_bucket[tid >> 6] = kmn;
+                    s_bucket[32 + (tid >> 6)] = kmx;
+                }
+                for (int i = tid; i < kSelBins; i += kSelBlock) sh[i] = 0;
+                if (tid == 0) s_out[0] = 0;
+                __syncthreads();
+#pragma unroll
+                for (int w2 = 0; w2 < kSelBlock / 64; ++w2) {
+                    kmn = min(kmn, s_bucket[w2]);
+                    kmx = max(kmx, s_bucket[32 + w2]);
+                }
+                const float scale = (float)kSelBins / ((float)(kmx - kmn) + 1.0f);
+                auto bin_of = [&](unsigned key) { return min(kSelBins - 1, (int)((float)(key - kmn) * scale)); };
+                const int b0 = tid < K1 ? bin_of(key0) : -1, b1 = tid + kSelBlock < K1 ? bin_of(key1) : -1;
+                if (b0 >= 0) atomicAdd(&sh[b0], 1);
+                if (b1 >= 0) atomicAdd(&sh[b1], 1);
+                __syncthreads();
+                if ((tid >> 6) == 0) {
+                    const int lane = tid & 63;
+                    constexpr int kPer = kSelBins / 64;  // bins per lane, descending
+                    int c[kPer], ls = 0;
+#pragma unroll
+                    for (int j = 0; j < kPer; ++j) {
+                        c[j] = sh[kSelBins - 1 - (kPer * lane + j)];
+                        ls += c[j];
+                    }
+                    int incl = ls;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const int y = __shfl_up(incl, o, 64);
+                        if (lane >= o) incl += y;
+                    }
+                    const unsigned long long m = __ballot(incl >= q);  // (K1 > q: some lane reaches q)
+                    const int first = __ffsll((long long)m) - 1;
+                    if (lane == first) {
+                        int cum = incl - ls, d = -1, above = 0;
+#pragma unroll
+                        for (int j = 0; j < kPer; ++j)
+                            if (d < 0) {
+                                if (cum + c[j] >= q) {
+                                    d = kSelBins - 1 - (kPer * lane + j);
+                                    above = cum;
+                                }
+                                cum += c[j];
+                            }
+                        s_out[1] = d | (above << 12);
+                    }
+                }
+                __syncthreads();
+                const int d = s_out[1] & 0xfff, above = s_out[1] >> 12, nb = sh[d];
+                if (nb <= 64) {
+                    if (b0 == d) s_bucket[atomicAdd(&s_out[0], 1)] = key0;
+                    if (b1 == d) s_bucket[atomicAdd(&s_out[0], 1)] = key1;
+                    __syncthreads();
+                    if ((tid >> 6) == 0) {
+                        const int lane = tid & 63, kk = q - above;  // rank of the wanted key in the bin
+                        const unsigned mine = lane < nb ? s_bucket[lane] : 0u;
+                        int gt = 0, eq = 0;
+                        for (int j = 0; j < nb; ++j) {
+                            const unsigned o = (unsigned)__shfl((int)mine, j, 64);
+                            gt += o > mine;
+                            eq += o == mine;
+                        }
+                        if (lane < nb && gt < kk && gt + eq >= kk) s_out[1] = (int)mine;  // (equal keys: same value)
+                    }
+                    __syncthreads();
+                    prefix = (unsigned)s_out[1];
+                    done = true;
+                }
+                __syncthreads();  // (s_out / sh reused below)
+            }
+            for (int shift = 24; shift >= 0 && !done; shift -= 8) {
                 if (tid < 256) sh[tid] = 0;
                 __syncthreads();
                 if (in_regs) {
