@@ -248,8 +248,8 @@ def cpu_baseline_mt(cfg, frames_host, ba_map, n_frames):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
     ap.add_argument("--frames", type=int, default=8, help="distinct frames cycled through")
     ap.add_argument("--cpu-sample", type=int, default=30, help="frames timed for the CPU baseline")
