@@ -55,6 +55,9 @@ extern "C" {
 #define VX_ERR_STATE (-5)     /* call sequence error (e.g. fetch before extract) */
 
 #define VX_MAX_SLOTS 4        /* device-resident keypoint/descriptor slots per context */
+#define VX_BATCH_BANKS 2      /* batched-extraction output banks per context */
+#define VX_MAX_BATCH 64       /* frames per batched extraction call */
+#define VX_MAX_MATCH_PAIRS 16 /* descriptor-set pairs per batched matching call */
 
 typedef struct vx_ctx vx_ctx;
 
@@ -146,6 +149,20 @@ int vx_orb_fetch(vx_ctx* ctx, int slot, vx_keypoint* out_kp, uint8_t* out_desc, 
 int vx_orb_slot_device(vx_ctx* ctx, int slot, const uint8_t** d_desc, const int32_t** d_count,
                        int32_t* cap);
 
+/* Batched extraction (SURVEY.md 8(d) batched figures; the C5 multi-camera rig): n_frames images
+ * of one size, frame f at d_imgs + f * frame_stride (device memory), extracted by ONE launch per
+ * kernel (frame = grid z) instead of one extraction per frame — same results as vx_orb_extract
+ * for every frame.  Each frame's keypoints / descriptors stay in output bank `bank` (two banks,
+ * so a camera's batch t can be matched against its batch t-1) at index f: vx_orb_batch_fetch
+ * copies them out, vx_orb_batch_device hands their device rows to vx_match_*_async. */
+int vx_orb_extract_batch_async(vx_ctx* ctx, const vx_orb_params* params, const uint8_t* d_imgs,
+                               int n_frames, int64_t frame_stride, int width, int height, int channels,
+                               int64_t row_stride, int bank);
+int vx_orb_batch_fetch(vx_ctx* ctx, int bank, int frame, vx_keypoint* out_kp, uint8_t* out_desc,
+                       int cap, int* n_out);
+int vx_orb_batch_device(vx_ctx* ctx, int bank, int frame, const uint8_t** d_desc,
+                        const int32_t** d_count, int32_t* cap);
+
 /* ---------------------------------------------------------------- matching
  * knnMatch(query = last frame, train = current frame, k = 2) + ratio test
  * (m1.distance < ratio * m2.distance), matches in ascending query index. */
@@ -160,6 +177,15 @@ int vx_match_slots_async(vx_ctx* ctx, int query_slot, int train_slot, float rati
 int vx_match_device_async(vx_ctx* ctx, const uint8_t* d_query, const int32_t* d_n_query, int cap_query,
                           const uint8_t* d_train, const int32_t* d_n_train, int cap_train, float ratio);
 int vx_match_fetch(vx_ctx* ctx, vx_match* out, int cap, int* n_out);
+/* Batched matching: n_pairs (<= VX_MAX_MATCH_PAIRS) independent kNN-2 + ratio problems in one
+ * launch pair (pair = grid y), query set i = d_query[i] (d_n_query[i] rows on the device, at most
+ * cap_query), train set i likewise — e.g. each camera's frame t against its frame t-1 from two
+ * batch banks.  The pointer arrays are host arrays of device pointers.  Results per pair:
+ * vx_match_batch_fetch(ctx, i, ...), identical to vx_match_device_async on that pair alone. */
+int vx_match_batch_async(vx_ctx* ctx, int n_pairs, const uint8_t* const* d_query,
+                         const int32_t* const* d_n_query, int cap_query, const uint8_t* const* d_train,
+                         const int32_t* const* d_n_train, int cap_train, float ratio);
+int vx_match_batch_fetch(vx_ctx* ctx, int pair, vx_match* out, int cap, int* n_out);
 
 /* ---------------------------------------------------------------- local bundle adjustment
  * A flattened snapshot of visionx::Map (map.h:13-34): keyframes with their Feature vectors

@@ -95,13 +95,8 @@ __device__ __forceinline__ void top2_dpp(unsigned& k1, unsigned& k2) {
 
 static_assert(kRT / 64 == kRQ, "k_knn_rows: one wave per query in the reduction");
 
-__global__ __launch_bounds__(kRT) void k_knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p,
-                                                  int nq_host, const uint8_t* __restrict__ t,
-                                                  const int* __restrict__ nt_p, int nt_host, float ratio,
-                                                  unsigned* __restrict__ best) {
-    __shared__ uint2 tr[kRQ][kRT];  // the threads' top-2s, query-major (32 KB)
-    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
-    const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
+__device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ t,
+                                         int nt, float ratio, unsigned* __restrict__ best, uint2 (*tr)[kRT]) {
     const int q0 = blockIdx.x * kRQ;
     if (q0 >= nq) return;  // block-uniform
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -170,6 +165,33 @@ __global__ __launch_bounds__(kRT) void k_knn_rows(const uint8_t* __restrict__ q,
     }
 }
 
+__global__ __launch_bounds__(kRT) void k_knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p,
+                                                  int nq_host, const uint8_t* __restrict__ t,
+                                                  const int* __restrict__ nt_p, int nt_host, float ratio,
+                                                  unsigned* __restrict__ best) {
+    __shared__ uint2 tr[kRQ][kRT];  // the threads' top-2s, query-major (32 KB)
+    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
+    const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
+    knn_rows(q, nq, t, nt, ratio, best, tr);
+}
+
+// Batched matching (vx_match_batch_async): pair blockIdx.y's sets from the table, per-pair results
+// at best + pair * q_cap.
+struct PairTab {
+    const uint8_t* q[VX_MAX_MATCH_PAIRS];
+    const int* nq[VX_MAX_MATCH_PAIRS];
+    const uint8_t* t[VX_MAX_MATCH_PAIRS];
+    const int* nt[VX_MAX_MATCH_PAIRS];
+};
+
+__global__ __launch_bounds__(kRT) void k_knn_rows_batch(PairTab tab, int q_cap, int t_cap, float ratio,
+                                                        unsigned* __restrict__ best) {
+    __shared__ uint2 tr[kRQ][kRT];
+    const int p = blockIdx.y;
+    const int nq = min(*tab.nq[p], q_cap), nt = min(*tab.nt[p], t_cap);
+    knn_rows(tab.q[p], nq, tab.t[p], nt, ratio, best + (long long)p * q_cap, tr);
+}
+
 // Exclusive block scan: wave prefix by __shfl_up, then the NT/64 wave totals from LDS (two
 // barriers per call instead of a Hillis-Steele pass per doubling step).
 template <int NT>
@@ -232,12 +254,8 @@ __global__ __launch_bounds__(kMergeQB) void k_knn_merge(const uint2* __restrict_
 }
 
 // Ordered compaction (ascending query index) of the per-query results, one block.
-__global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __restrict__ best,
-                                                             const int* __restrict__ nq_p, int nq_host,
-                                                             vx_match* __restrict__ out,
-                                                             int* __restrict__ out_count) {
-    __shared__ int sh[kMergeBlock / 64];
-    const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
+__device__ __forceinline__ void knn_compact(const unsigned* __restrict__ best, int nq, vx_match* __restrict__ out,
+                                            int* __restrict__ out_count, int* sh) {
     int written = 0;
     // 4 consecutive queries per thread (one pass up to 4096 queries: one load latency, one scan)
     for (int base = 0; base < nq; base += 4 * kMergeBlock) {
@@ -262,6 +280,24 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __r
         written += cnt;
     }
     if (threadIdx.x == 0) *out_count = written;
+}
+
+__global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __restrict__ best,
+                                                             const int* __restrict__ nq_p, int nq_host,
+                                                             vx_match* __restrict__ out,
+                                                             int* __restrict__ out_count) {
+    __shared__ int sh[kMergeBlock / 64];
+    knn_compact(best, nq_p ? min(*nq_p, nq_host) : nq_host, out, out_count, sh);
+}
+
+// one workgroup per pair: matches of pair p at out + p * q_cap, its count at out_count[4 p]
+__global__ __launch_bounds__(kMergeBlock) void k_knn_compact_batch(const unsigned* __restrict__ best, PairTab tab,
+                                                                   int q_cap, vx_match* __restrict__ out,
+                                                                   int* __restrict__ out_count) {
+    __shared__ int sh[kMergeBlock / 64];
+    const int p = blockIdx.x;
+    knn_compact(best + (long long)p * q_cap, min(*tab.nq[p], q_cap), out + (long long)p * q_cap,
+                out_count + 4 * p, sh);
 }
 
 int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt,
@@ -300,6 +336,17 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
         VX_LAUNCH_CHECK(c, "k_knn_compact");
     }
     c->match_valid = true;
+    return VX_OK;
+}
+
+int match_batch_enqueue(vx_ctx* c, const PairTab& tab, int n_pairs, int q_cap, int t_cap, float ratio) {
+    unsigned* best = c->mb_best.as<unsigned>();
+    VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows_batch, dim3((q_cap + kRQ - 1) / kRQ, n_pairs), dim3(kRT), 0,
+                     c->stream, tab, q_cap, t_cap, ratio, best));
+    ProfScope ps(c, kStMatchMerge);
+    hipLaunchKernelGGL(k_knn_compact_batch, dim3(n_pairs), dim3(kMergeBlock), 0, c->stream, (const unsigned*)best, tab,
+                       q_cap, c->mb_matches.as<vx_match>(), c->mb_count.as<int>());
+    VX_LAUNCH_CHECK(c, "k_knn_compact_batch");
     return VX_OK;
 }
 
@@ -360,6 +407,76 @@ int vx_match_fetch(vx_ctx* c, vx_match* out, int cap, int* n_out) {
     if (n > 0 && out) {
         VX_HIP(c, hipMemcpyAsync(out, c->matches.p, (size_t)n * sizeof(vx_match), hipMemcpyDeviceToHost,
                                  c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    return VX_OK;
+}
+
+int vx_match_batch_async(vx_ctx* c, int n_pairs, const uint8_t* const* dq, const int32_t* const* dnq, int q_cap,
+                         const uint8_t* const* dt, const int32_t* const* dnt, int t_cap, float ratio) {
+    if (!c) return VX_ERR_INVALID;
+    if (n_pairs < 1 || n_pairs > VX_MAX_MATCH_PAIRS)
+        return set_error(c, VX_ERR_INVALID, "n_pairs %d outside [1, %d]", n_pairs, VX_MAX_MATCH_PAIRS);
+    if (!dq || !dnq || !dt || !dnt || q_cap < 0 || t_cap < 0)
+        return set_error(c, VX_ERR_INVALID, "vx_match_batch_async: null buffers or negative capacity");
+    if (t_cap > (1 << 22)) return set_error(c, VX_ERR_INVALID, "train set larger than 2^22 rows");
+    PairTab tab;
+    std::memset(&tab, 0, sizeof tab);
+    for (int i = 0; i < n_pairs; ++i) {
+        if (!dq[i] || !dnq[i] || !dt[i] || !dnt[i])
+            return set_error(c, VX_ERR_INVALID, "vx_match_batch_async: null buffers of pair %d", i);
+        tab.q[i] = dq[i];
+        tab.nq[i] = dnq[i];
+        tab.t[i] = dt[i];
+        tab.nt[i] = dnt[i];
+    }
+    VX_HIP(c, hipSetDevice(c->device));
+    c->mb_valid = 0;
+    const size_t qc = (size_t)std::max(q_cap, 1);
+    VX_HIP(c, c->mb_best.ensure(n_pairs * qc * sizeof(unsigned)));
+    VX_HIP(c, c->mb_matches.ensure(n_pairs * qc * sizeof(vx_match)));
+    VX_HIP(c, c->mb_count.ensure((size_t)n_pairs * 16));
+    if (q_cap > 0) {
+        struct A {
+            const PairTab* tab;
+            int n, q_cap, t_cap;
+            float ratio;
+        } a{&tab, n_pairs, q_cap, t_cap, ratio};
+        uint32_t rbits;
+        std::memcpy(&rbits, &ratio, 4);
+        std::vector<uint64_t> key{4, (uint64_t)n_pairs, (uint64_t)q_cap, (uint64_t)t_cap, rbits,
+                                  (uint64_t)(uintptr_t)c->mb_best.p, (uint64_t)(uintptr_t)c->mb_matches.p,
+                                  (uint64_t)(uintptr_t)c->mb_count.p};
+        for (int i = 0; i < n_pairs; ++i)
+            for (const void* v : {(const void*)dq[i], (const void*)dnq[i], (const void*)dt[i], (const void*)dnt[i]})
+                key.push_back((uint64_t)(uintptr_t)v);
+        const int rc = graph_run(c, key,
+                                 [](vx_ctx* cc, void* v) {
+                                     const A* x = static_cast<const A*>(v);
+                                     return match_batch_enqueue(cc, *x->tab, x->n, x->q_cap, x->t_cap, x->ratio);
+                                 },
+                                 &a);
+        if (rc) return rc;
+    } else {
+        VX_HIP(c, hipMemsetAsync(c->mb_count.p, 0, (size_t)n_pairs * 16, c->stream));
+    }
+    c->mb_valid = n_pairs;
+    c->mb_cap = q_cap;
+    return VX_OK;
+}
+
+int vx_match_batch_fetch(vx_ctx* c, int pair, vx_match* out, int cap, int* n_out) {
+    if (!c || !n_out) return VX_ERR_INVALID;
+    if (pair < 0 || pair >= c->mb_valid) return set_error(c, VX_ERR_STATE, "no batched match pair %d enqueued", pair);
+    int n = 0;
+    VX_HIP(c, hipMemcpyAsync(&n, c->mb_count.as<int>() + 4 * pair, sizeof n, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) prof_collect(c);
+    *n_out = n;
+    if (n > cap) return set_error(c, VX_ERR_CAPACITY, "need %d matches, cap %d", n, cap);
+    if (n > 0 && out) {
+        VX_HIP(c, hipMemcpyAsync(out, c->mb_matches.as<vx_match>() + (size_t)pair * std::max(c->mb_cap, 1),
+                                 (size_t)n * sizeof(vx_match), hipMemcpyDeviceToHost, c->stream));
         VX_HIP(c, hipStreamSynchronize(c->stream));
     }
     return VX_OK;

@@ -63,6 +63,9 @@ struct LevelArgs {
     long long xtab[kMaxLevels], ytab[kMaxLevels];
     long long pr_x, pr_y;
     int pr_buf;
+    // batched launches (vx_orb_extract_batch_async): frame blockIdx.z's buffers start this many
+    // elements after frame 0's (all zero-offset for a single frame: gridDim.z = 1)
+    long long fs_img, fs_pyr, fs_cells, fs_hist, fs_stage;
 };
 
 // Copies n elements into LDS, element i = load(i), with every load of a thread issued before the
@@ -103,7 +106,11 @@ __device__ __forceinline__ uint8_t lin_px(const uint8_t* r0, const uint8_t* r1, 
 
 // Unfused path only (the fused k_pyramid zeroes the histograms itself).
 __global__ void k_gray(const uint8_t* __restrict__ img, int W, int ch, long long stride,
-                       uint8_t* __restrict__ out, int* __restrict__ hist, int hist_n) {
+                       uint8_t* __restrict__ out, int* __restrict__ hist, int hist_n, long long fs_img,
+                       long long fs_pyr, long long fs_hist) {
+    img += blockIdx.z * fs_img;
+    out += blockIdx.z * fs_pyr;
+    hist += blockIdx.z * fs_hist;
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = threadIdx.x; i < hist_n; i += blockDim.x) hist[i] = 0;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
@@ -145,6 +152,9 @@ __global__ __launch_bounds__(NT) void k_pyramid(const uint8_t* __restrict__ img,
     int* stab = reinterpret_cast<int*>(prev + a.pr_buf);  // packed {ofs | c1 << 16} per level
     const int tid = threadIdx.x, lx = tid & 63, ly = tid >> 6;
     const int L = a.L;
+    img += blockIdx.z * a.fs_img;
+    pyr += blockIdx.z * a.fs_pyr;
+    hist += blockIdx.z * a.fs_hist;
     VX_KT(0);
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = tid; i < hist_n; i += NT) hist[i] = 0;
@@ -277,7 +287,9 @@ __global__ __launch_bounds__(NT) void k_pyramid(const uint8_t* __restrict__ img,
 
 // ------------------------------------------------------------------------------ resize
 __global__ void k_resize(const uint8_t* __restrict__ src, int sw, int sh, uint8_t* __restrict__ dst,
-                         int dw, const int4* __restrict__ xt, const int4* __restrict__ yt) {
+                         int dw, const int4* __restrict__ xt, const int4* __restrict__ yt, long long fs_pyr) {
+    src += blockIdx.z * fs_pyr;
+    dst += blockIdx.z * fs_pyr;
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
     if (x >= dw) return;
@@ -432,6 +444,11 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     __shared__ __attribute__((aligned(16))) uint8_t bin_[kBH * kBW];
     __shared__ __attribute__((aligned(16))) float brow[kBH * kTX];
     const int b = blockIdx.x;
+    pyr += blockIdx.z * a.fs_pyr;
+    blur += blockIdx.z * a.fs_pyr;
+    cand += blockIdx.z * a.fs_cells * kCellCap;
+    cell_count += blockIdx.z * a.fs_cells;
+    hist += blockIdx.z * a.fs_hist;
     int l = 0;
     while (l + 1 < a.L && b >= a.tile_base[l + 1]) ++l;
     const int W = a.lw[l], H = a.lh[l];
@@ -673,6 +690,11 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     __shared__ CandRec srec[kSelRecLds];  // retainBest(2q) survivors (32 KB)
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
+    cand += blockIdx.z * a.fs_cells * kCellCap;
+    cell_count += blockIdx.z * a.fs_cells;
+    hist += blockIdx.z * a.fs_hist;
+    stage += blockIdx.z * a.fs_stage;
+    level_count += blockIdx.z * kMaxLevels;
     VX_KT(12);
     const int ncell = a.lh[l] * a.ntx[l];
     const long long cbase = a.cell_base[l];
@@ -978,6 +1000,13 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
                                                      int* __restrict__ slot_count) {
     const int lane = threadIdx.x & 63;
     const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    pyr += blockIdx.z * a.fs_pyr;
+    blur += blockIdx.z * a.fs_pyr;
+    stage += blockIdx.z * a.fs_stage;
+    level_count += blockIdx.z * kMaxLevels;
+    kp += blockIdx.z * (long long)a.out_cap;
+    desc += blockIdx.z * (long long)a.out_cap * 32;
+    slot_count += blockIdx.z * 4;
     int total = 0, l = -1, j = 0;
     for (int i = 0; i < a.L; ++i) {
         const int c = level_count[i];
@@ -1261,6 +1290,10 @@ LevelArgs level_args(const OrbGeometry& g) {
     a.pr_x = g.pr_x;
     a.pr_y = g.pr_y;
     a.pr_buf = g.pr_buf;
+    a.fs_pyr = g.pyr_bytes;
+    a.fs_cells = g.cells_total;
+    a.fs_hist = (long long)g.L * kHistRep * 256;
+    a.fs_stage = g.stage_total;
     return a;
 }
 
@@ -1377,54 +1410,93 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
         VX_HIP(c, s.count.ensure(16));
         s.cap = g.out_cap;
     }
+    for (int b = 0; b < VX_BATCH_BANKS; ++b) c->batch_n[b] = 0;
     c->geo = g;
     c->geo_valid = true;
     ++c->geo_gen;
     return VX_OK;
 }
 
-static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t stride, int slot) {
+// Enqueues the extraction of nf frames (frame f at d_img + f * fs_img) into the outputs kp / desc /
+// count (frame f at kp + f * out_cap, desc + f * 32 * out_cap, count + 4 f): one launch per kernel,
+// frame = blockIdx.z, the scratch buffers hold nf frames (orb_reserve_frames).
+static int orb_enqueue_frames(vx_ctx* c, const uint8_t* d_img, int channels, int64_t stride, int64_t fs_img, int nf,
+                              vx_keypoint* kp, uint8_t* desc, int* count) {
     const OrbGeometry& g = c->geo;
-    const LevelArgs a = level_args(g);
+    LevelArgs a = level_args(g);
+    a.fs_img = fs_img;
     uint8_t* pyr = c->pyr.as<uint8_t>();
-    Slot& s = c->slots[slot];
     const int hist_n = g.L * kHistRep * 256;
     if (g.pyr_fused) {
         const int raw = (int)((pyr_raw_bytes(g, channels) + 15) & ~int64_t(15));
         VX_HIP(c, launch(c, kStPyramid, g.pr_block == 512 ? k_pyramid<512> : k_pyramid<1024>,
-                         dim3(g.pr_ntx, g.pr_nty), dim3(g.pr_block),
+                         dim3(g.pr_ntx, g.pr_nty, nf), dim3(g.pr_block),
                          (uint32_t)(raw + 2 * g.pr_buf + 4 * g.pr_tabn), c->stream, d_img, channels,
                          (long long)stride, pyr, (const int4*)c->tabs.as<int4>(), a, c->hist.as<int>(), hist_n, raw));
     } else {
         {
             ProfScope ps(c, kStGray);
-            hipLaunchKernelGGL(k_gray, dim3((g.W + kBlock - 1) / kBlock, g.H), dim3(kBlock), 0, c->stream,
-                               d_img, g.W, channels, (long long)stride, pyr, c->hist.as<int>(), hist_n);
+            hipLaunchKernelGGL(k_gray, dim3((g.W + kBlock - 1) / kBlock, g.H, nf), dim3(kBlock), 0, c->stream,
+                               d_img, g.W, channels, (long long)stride, pyr, c->hist.as<int>(), hist_n,
+                               (long long)fs_img, (long long)a.fs_pyr, (long long)a.fs_hist);
             VX_LAUNCH_CHECK(c, "k_gray");
         }
         ProfScope ps(c, kStResize);
         const int4* tabs = c->tabs.as<int4>();
         for (int l = 1; l < g.L; ++l) {
-            hipLaunchKernelGGL(k_resize, dim3((g.lw[l] + kBlock - 1) / kBlock, g.lh[l]), dim3(kBlock), 0,
+            hipLaunchKernelGGL(k_resize, dim3((g.lw[l] + kBlock - 1) / kBlock, g.lh[l], nf), dim3(kBlock), 0,
                                c->stream, pyr + g.off[l - 1], g.lw[l - 1], g.lh[l - 1], pyr + g.off[l],
-                               g.lw[l], tabs + g.xtab[l], tabs + g.ytab[l]);
+                               g.lw[l], tabs + g.xtab[l], tabs + g.ytab[l], (long long)a.fs_pyr);
             VX_LAUNCH_CHECK(c, "k_resize");
         }
     }
     // FAST + NMS + Harris and the GaussianBlur of every level, one launch over 64 x 16 tiles
-    VX_HIP(c, launch(c, kStFast, k_fast, dim3(g.total_tiles), dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, a,
+    VX_HIP(c, launch(c, kStFast, k_fast, dim3(g.total_tiles, 1, nf), dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, a,
                      c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>(), c->blur.as<uint8_t>()));
-    VX_HIP(c, launch(c, kStSelect, k_select, dim3(g.L), dim3(kSelBlock), 0, c->stream,
+    VX_HIP(c, launch(c, kStSelect, k_select, dim3(g.L, 1, nf), dim3(kSelBlock), 0, c->stream,
                      (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(),
                      (const int*)c->hist.as<int>(), a, c->stage.as<CandRec>(), c->level_count.as<int>()));
     {
         const int waves_per_block = kBlock / 64;
-        VX_HIP(c, launch(c, kStDescribe, k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block),
+        VX_HIP(c, launch(c, kStDescribe, k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block, 1, nf),
                          dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, (const uint8_t*)c->blur.as<uint8_t>(),
-                         (const CandRec*)c->stage.as<CandRec>(), (const int*)c->level_count.as<int>(), a,
-                         s.kp.as<vx_keypoint>(), s.desc.as<uint8_t>(), s.count.as<int>()));
+                         (const CandRec*)c->stage.as<CandRec>(), (const int*)c->level_count.as<int>(), a, kp, desc,
+                         count));
     }
+    return VX_OK;
+}
+
+static int orb_enqueue(vx_ctx* c, const uint8_t* d_img, int channels, int64_t stride, int slot) {
+    Slot& s = c->slots[slot];
+    const int rc = orb_enqueue_frames(c, d_img, channels, stride, 0, 1, s.kp.as<vx_keypoint>(), s.desc.as<uint8_t>(),
+                                      s.count.as<int>());
+    if (rc) return rc;
     s.valid = true;
+    return VX_OK;
+}
+
+// Scratch for nf frames of the current geometry and the batch bank's outputs.  A buffer that has to
+// grow moves, so the geometry serial is bumped (captured graphs of this context bake the old
+// pointers into their kernels and must not be replayed).
+static int orb_reserve_frames(vx_ctx* c, int nf, int bank) {
+    const OrbGeometry& g = c->geo;
+    const void* before[8] = {c->pyr.p, c->blur.p, c->cand.p, c->stage.p, c->band_count.p, c->hist.p, c->level_count.p,
+                             nullptr};
+    VX_HIP(c, c->pyr.ensure((size_t)nf * g.pyr_bytes));
+    VX_HIP(c, c->blur.ensure((size_t)nf * g.pyr_bytes));
+    VX_HIP(c, c->cand.ensure((size_t)nf * g.cells_total * kCellCap * sizeof(CandRec)));
+    VX_HIP(c, c->stage.ensure((size_t)nf * g.stage_total * sizeof(CandRec)));
+    VX_HIP(c, c->band_count.ensure((size_t)nf * g.cells_total * sizeof(int)));
+    VX_HIP(c, c->hist.ensure((size_t)nf * g.L * kHistRep * 256 * sizeof(int)));
+    VX_HIP(c, c->level_count.ensure((size_t)nf * kMaxLevels * sizeof(int)));
+    const void* after[8] = {c->pyr.p, c->blur.p, c->cand.p, c->stage.p, c->band_count.p, c->hist.p, c->level_count.p,
+                            nullptr};
+    if (std::memcmp(before, after, sizeof before)) ++c->geo_gen;
+    Slot& s = c->batch[bank];
+    VX_HIP(c, s.kp.ensure((size_t)nf * g.out_cap * sizeof(vx_keypoint)));
+    VX_HIP(c, s.desc.ensure((size_t)nf * g.out_cap * 32));
+    VX_HIP(c, s.count.ensure((size_t)nf * 16));
+    s.cap = g.out_cap;
     return VX_OK;
 }
 
@@ -1505,6 +1577,80 @@ int vx_orb_slot_device(vx_ctx* c, int slot, const uint8_t** d_desc, const int32_
     if (d_desc) *d_desc = c->slots[slot].desc.as<uint8_t>();
     if (d_count) *d_count = c->slots[slot].count.as<int32_t>();
     if (cap) *cap = c->slots[slot].cap;
+    return VX_OK;
+}
+
+int vx_orb_extract_batch_async(vx_ctx* c, const vx_orb_params* p, const uint8_t* d_imgs, int n_frames,
+                               int64_t frame_stride, int w, int h, int channels, int64_t stride, int bank) {
+    if (!c) return VX_ERR_INVALID;
+    if (bank < 0 || bank >= VX_BATCH_BANKS) return set_error(c, VX_ERR_INVALID, "bad batch bank %d", bank);
+    if (n_frames < 1 || n_frames > VX_MAX_BATCH)
+        return set_error(c, VX_ERR_INVALID, "n_frames %d outside [1, %d]", n_frames, VX_MAX_BATCH);
+    if (!d_imgs) return set_error(c, VX_ERR_INVALID, "null images");
+    if (channels != 1 && channels != 3 && channels != 4)
+        return set_error(c, VX_ERR_INVALID, "channels must be 1, 3 or 4");
+    if (stride < (int64_t)w * channels) return set_error(c, VX_ERR_INVALID, "row stride too small");
+    if (n_frames > 1 && frame_stride < (int64_t)(h - 1) * stride + (int64_t)w * channels)
+        return set_error(c, VX_ERR_INVALID, "frame stride smaller than one frame");
+    int rc = orb_prepare(c, p, w, h);
+    if (rc) return rc;
+    VX_HIP(c, hipSetDevice(c->device));
+    rc = orb_reserve_frames(c, n_frames, bank);
+    if (rc) return rc;
+    c->batch_n[bank] = 0;
+    Slot& s = c->batch[bank];
+    struct A {
+        const uint8_t* img;
+        int channels, nf;
+        int64_t stride, fs;
+        Slot* s;
+    } a{d_imgs, channels, n_frames, stride, n_frames > 1 ? frame_stride : 0, &s};
+    rc = graph_run(c, {3, (uint64_t)(uintptr_t)d_imgs, (uint64_t)channels, (uint64_t)stride, (uint64_t)a.fs,
+                       (uint64_t)n_frames, (uint64_t)(uintptr_t)s.kp.p, (uint64_t)(uintptr_t)s.desc.p,
+                       (uint64_t)(uintptr_t)s.count.p, c->geo_gen},
+                   [](vx_ctx* cc, void* v) {
+                       const A* x = static_cast<const A*>(v);
+                       return orb_enqueue_frames(cc, x->img, x->channels, x->stride, x->fs, x->nf,
+                                                 x->s->kp.as<vx_keypoint>(), x->s->desc.as<uint8_t>(),
+                                                 x->s->count.as<int>());
+                   },
+                   &a);
+    if (rc) return rc;
+    c->batch_n[bank] = n_frames;
+    return VX_OK;
+}
+
+int vx_orb_batch_device(vx_ctx* c, int bank, int frame, const uint8_t** d_desc, const int32_t** d_count,
+                        int32_t* cap) {
+    if (!c || bank < 0 || bank >= VX_BATCH_BANKS || frame < 0 || frame >= c->batch_n[bank]) return VX_ERR_INVALID;
+    const Slot& s = c->batch[bank];
+    if (d_desc) *d_desc = s.desc.as<uint8_t>() + (size_t)frame * s.cap * 32;
+    if (d_count) *d_count = s.count.as<int32_t>() + 4 * (size_t)frame;
+    if (cap) *cap = s.cap;
+    return VX_OK;
+}
+
+int vx_orb_batch_fetch(vx_ctx* c, int bank, int frame, vx_keypoint* out_kp, uint8_t* out_desc, int cap, int* n_out) {
+    if (!c || !n_out) return VX_ERR_INVALID;
+    if (bank < 0 || bank >= VX_BATCH_BANKS || frame < 0 || frame >= c->batch_n[bank])
+        return set_error(c, VX_ERR_STATE, "batch bank %d holds no frame %d", bank, frame);
+    const Slot& s = c->batch[bank];
+    int cnt[2];
+    VX_HIP(c, hipMemcpyAsync(cnt, s.count.as<int>() + 4 * (size_t)frame, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->prof) prof_collect(c);
+    *n_out = cnt[0];
+    if (cnt[1]) return set_error(c, VX_ERR_CAPACITY, "keypoints %d exceed slot capacity %d", cnt[0], s.cap);
+    if (cnt[0] > cap) return set_error(c, VX_ERR_CAPACITY, "need %d keypoints, cap %d", cnt[0], cap);
+    if (cnt[0] > 0) {
+        if (out_kp)
+            VX_HIP(c, hipMemcpyAsync(out_kp, s.kp.as<vx_keypoint>() + (size_t)frame * s.cap,
+                                     (size_t)cnt[0] * sizeof(vx_keypoint), hipMemcpyDeviceToHost, c->stream));
+        if (out_desc)
+            VX_HIP(c, hipMemcpyAsync(out_desc, s.desc.as<uint8_t>() + (size_t)frame * s.cap * 32, (size_t)cnt[0] * 32,
+                                     hipMemcpyDeviceToHost, c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+    }
     return VX_OK;
 }
 

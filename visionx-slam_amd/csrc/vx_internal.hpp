@@ -179,12 +179,16 @@ struct vx_ctx {
     bool geo_valid = false;
     vx::DevBuf img_in, pyr, blur, tabs, cand, band_count, hist, stage, level_count;
     vx::Slot slots[VX_MAX_SLOTS];
+    vx::Slot batch[VX_BATCH_BANKS];  // vx_orb_extract_batch_async outputs, frame-major
+    int batch_n[VX_BATCH_BANKS] = {0};
 
     // ---- matching
     vx::DevBuf mq, mt, mq_n, partial, matches, match_count;
     vx::PinnedBuf host_stage;
     int match_cap = 0;
     bool match_valid = false;
+    vx::DevBuf mb_best, mb_matches, mb_count;  // vx_match_batch_async: per-pair results
+    int mb_valid = 0, mb_cap = 0;
 
     // ---- landmark creation (landmarks.hip): inputs, per-item flags / points, compacted outputs
     vx::DevBuf lm_in0, lm_in1, lm_in2, lm_in3, lm_in4, lm_depth, lm_valid, lm_pw, lm_index, lm_out, lm_count, lm_aux;

@@ -88,6 +88,8 @@ EXPORTS = [
     "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run",
+    "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
+    "vx_match_batch_fetch",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
@@ -124,6 +126,16 @@ def lib():
                                          C.POINTER(C.c_int32)]
         L.vx_match_device_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                             C.c_int, C.c_float]
+        L.vx_orb_extract_batch_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_int,
+                                                 C.c_int, C.c_int, C.c_int64, C.c_int]
+        L.vx_orb_batch_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_void_p), C.POINTER(C.c_int32)]
+        L.vx_orb_batch_fetch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                                         C.POINTER(C.c_int)]
+        L.vx_match_batch_async.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                           C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.c_int,
+                                           C.c_float]
+        L.vx_match_batch_fetch.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]
         L.vx_prof_name.restype = C.c_char_p
         L.vx_ba_plan_destroy.argtypes = [C.c_void_p]
         L.vx_dmap_destroy.argtypes = [C.c_void_p]
@@ -273,6 +285,7 @@ class Context:
     def __init__(self, device: int = 0, priority: int = 0, cu_mask=None):
         """cu_mask: iterable of compute-unit indices this context may use (None: all)."""
         self._h = C.c_void_p()
+        self.device = int(device)
         words, nw = None, 0
         if cu_mask is not None:
             n = lib().vx_device_cus(int(device))
@@ -343,6 +356,42 @@ class Context:
         self._check(lib().vx_orb_fetch(self._h, slot, _p(kps), _p(desc), cap, C.byref(n)))
         return kps[:n.value].copy(), desc[:n.value].copy()
 
+    def orb_extract_batch_async(self, d_imgs_ptr: int, n_frames: int, frame_stride: int, w: int, h: int,
+                                channels: int, row_stride: int, bank: int = 0, params: OrbParams | None = None):
+        """Extract n_frames device-resident images (frame f at d_imgs_ptr + f * frame_stride) in one
+        launch per kernel; results stay in batch bank `bank`."""
+        params = params or default_orb_params()
+        self._check(lib().vx_orb_extract_batch_async(self._h, C.byref(params), C.c_void_p(d_imgs_ptr), n_frames,
+                                                     C.c_int64(frame_stride), w, h, channels, C.c_int64(row_stride),
+                                                     bank))
+
+    def orb_batch_fetch(self, bank: int, frame: int, cap: int = 8192):
+        kps = np.zeros(cap, KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n = C.c_int(0)
+        self._check(lib().vx_orb_batch_fetch(self._h, bank, frame, _p(kps), _p(desc), cap, C.byref(n)))
+        return kps[:n.value].copy(), desc[:n.value].copy()
+
+    def batch_device(self, bank: int, frame: int):
+        """(device descriptor pointer, device count pointer, row capacity) of a batch frame."""
+        d, n, cap = C.c_void_p(), C.c_void_p(), C.c_int32()
+        self._check(lib().vx_orb_batch_device(self._h, bank, frame, C.byref(d), C.byref(n), C.byref(cap)))
+        return d.value, n.value, cap.value
+
+    def orb_extract_batch(self, imgs: np.ndarray, params: OrbParams | None = None, bank: int = 0):
+        """Host convenience: upload a (B, H, W[, C]) stack and extract it as one batch; returns a list of
+        (keypoints, descriptors) per frame."""
+        import torch  # device memory for the upload (plumbing only)
+
+        imgs = np.ascontiguousarray(imgs)
+        b, h, w = imgs.shape[:3]
+        ch = 1 if imgs.ndim == 3 else imgs.shape[3]
+        d = torch.from_numpy(imgs).to(f"cuda:{self.device}")
+        self.orb_extract_batch_async(d.data_ptr(), b, d.stride(0), w, h, ch, d.stride(1), bank, params)
+        out = [self.orb_batch_fetch(bank, f) for f in range(b)]
+        del d
+        return out
+
     # ---------------------------------------------------------------- matching
     def match(self, q: np.ndarray, t: np.ndarray, ratio: float = 0.8):
         q = np.ascontiguousarray(q, np.uint8)
@@ -377,6 +426,22 @@ class Context:
 
     def wait_event(self, ev: "Event"):
         self._check(lib().vx_event_wait(self._h, ev._h))
+
+    def match_batch_async(self, pairs, ratio: float = 0.8):
+        """pairs: list of (query, train) device triples (slot_device() / batch_device())."""
+        n = len(pairs)
+        arr = lambda xs: (C.c_void_p * max(n, 1))(*[C.c_void_p(x) for x in xs])
+        dq, nq, dt, nt = (arr([p[0][0] for p in pairs]), arr([p[0][1] for p in pairs]),
+                          arr([p[1][0] for p in pairs]), arr([p[1][1] for p in pairs]))
+        cq = max([p[0][2] for p in pairs], default=0)
+        ct = max([p[1][2] for p in pairs], default=0)
+        self._check(lib().vx_match_batch_async(self._h, n, dq, nq, cq, dt, nt, ct, C.c_float(ratio)))
+
+    def match_batch_fetch(self, pair: int, cap: int = 8192):
+        out = np.zeros(cap, MATCH_DTYPE)
+        n = C.c_int(0)
+        self._check(lib().vx_match_batch_fetch(self._h, pair, _p(out), cap, C.byref(n)))
+        return out[:n.value].copy()
 
     def match_fetch(self, cap: int = 8192):
         out = np.zeros(cap, MATCH_DTYPE)
