@@ -42,6 +42,24 @@ def test_orb_batch_matches_oracle(ctx, oracle, b, h, w, n, gray):
         _eq(out[f], ref)
 
 
+@pytest.mark.parametrize("b", [2, 4])
+def test_orb_batch_fused_pyramid_with_grid_share(oracle, b):
+    """Grid share 1/B: the fused pyramid's grid for B frames fits one round, so the batch runs the
+    fused pyramid (blockIdx.z = frame) instead of the level chain; same results."""
+    import vxslam
+
+    c = vxslam.Context(0)
+    try:
+        c.set_grid_share(1.0 / b)
+        frames = synth.make_frames(0xBA7C8 + b, b, 480, 640)
+        p = vxslam.default_orb_params(n_features=2000)
+        out = c.orb_extract_batch(np.stack(frames), p)
+        for f in range(b):
+            _eq(out[f], oracle.orb_extract(frames[f], 2000, order=oracle.ORDER_RASTER))
+    finally:
+        c.close()
+
+
 def test_orb_batch_padded_strides_and_blank_frame(ctx, oracle):
     """Frames in a pitched allocation (row stride > width, frame stride > frame) and a blank frame
     (no corners: zero keypoints) inside the batch."""

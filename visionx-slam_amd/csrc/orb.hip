@@ -1370,6 +1370,7 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
     }
     int n_cu = 256;
     (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+    g.n_cu = n_cu;
     pyramid_rects(g, all, std::max(1, (int)(n_cu * c->grid_share)));
     g.tab_entries = (int64_t)all.size();
     // FAST tiles / cells and selection staging
@@ -1427,7 +1428,11 @@ static int orb_enqueue_frames(vx_ctx* c, const uint8_t* d_img, int channels, int
     a.fs_img = fs_img;
     uint8_t* pyr = c->pyr.as<uint8_t>();
     const int hist_n = g.L * kHistRep * 256;
-    if (g.pyr_fused) {
+    // the fused pyramid buys latency with redundant halo work; a batch whose fused grid would need more
+    // than one round of the device's CUs takes the level chain instead (C3, 8 frames on 18 x 14 tiles:
+    // 16.5 us per frame fused vs ~5.5 for gray + resizes; 2 and 4 frames with the grid share set to
+    // 1/B keep the fused pyramid: 35.9 / 25.1 against 39.4 / 27.4 us per frame)
+    if (g.pyr_fused && (nf == 1 || (int64_t)g.pr_ntx * g.pr_nty * nf <= g.n_cu)) {
         const int raw = (int)((pyr_raw_bytes(g, channels) + 15) & ~int64_t(15));
         VX_HIP(c, launch(c, kStPyramid, g.pr_block == 512 ? k_pyramid<512> : k_pyramid<1024>,
                          dim3(g.pr_ntx, g.pr_nty, nf), dim3(g.pr_block),

@@ -118,6 +118,7 @@ struct OrbGeometry {
     int pr_area0 = 0;               // max level-0 need area (pixels)
     int pr_w0 = 0, pr_h0 = 0;       // max level-0 need width / height
     int pr_tabn = 0;                // max packed coefficient entries per tile
+    int n_cu = 256;                 // compute units of the device (batched pyramid choice)
     // FAST tiles (64 x 16 pixels per workgroup) and output cells (row x tile column)
     int ntx[kMaxLevels], nty[kMaxLevels];
     int tile_base[kMaxLevels];     // first tile (workgroup) of level l
