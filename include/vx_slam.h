@@ -158,6 +158,11 @@ int vx_orb_slot_device(vx_ctx* ctx, int slot, const uint8_t** d_desc, const int3
 int vx_orb_extract_batch_async(vx_ctx* ctx, const vx_orb_params* params, const uint8_t* d_imgs,
                                int n_frames, int64_t frame_stride, int width, int height, int channels,
                                int64_t row_stride, int bank);
+/* Host-image variant: imgs[f] are host rows of row_stride bytes (all frames one size), uploaded
+ * into the context, then extracted as one batch into `bank`. */
+int vx_orb_extract_batch(vx_ctx* ctx, const vx_orb_params* params, const uint8_t* const* imgs,
+                         int n_frames, int width, int height, int channels, int64_t row_stride,
+                         int bank);
 int vx_orb_batch_fetch(vx_ctx* ctx, int bank, int frame, vx_keypoint* out_kp, uint8_t* out_desc,
                        int cap, int* n_out);
 int vx_orb_batch_device(vx_ctx* ctx, int bank, int frame, const uint8_t** d_desc,
@@ -185,6 +190,10 @@ int vx_match_fetch(vx_ctx* ctx, vx_match* out, int cap, int* n_out);
 int vx_match_batch_async(vx_ctx* ctx, int n_pairs, const uint8_t* const* d_query,
                          const int32_t* const* d_n_query, int cap_query, const uint8_t* const* d_train,
                          const int32_t* const* d_n_train, int cap_train, float ratio);
+/* Host-descriptor variant: pair i = query q[i] (nq[i] rows of 32 B) against train t[i] (nt[i]
+ * rows), uploaded in one copy; a pair with an empty side yields 0 matches (orb_matcher.cpp:18-20). */
+int vx_match_knn2_ratio_batch(vx_ctx* ctx, int n_pairs, const uint8_t* const* q, const int32_t* nq,
+                              const uint8_t* const* t, const int32_t* nt, float ratio);
 int vx_match_batch_fetch(vx_ctx* ctx, int pair, vx_match* out, int cap, int* n_out);
 
 /* ---------------------------------------------------------------- local bundle adjustment

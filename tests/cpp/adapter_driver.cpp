@@ -9,6 +9,8 @@
 //   adapter_driver triangulate <dir> <min_deg> <max_err>   (TriangulateWithLastKeyFrame)
 //   adapter_driver pnp <dir> <iterations> <reproj_err>    (solvePnPRansac as TrackWithPnP calls it)
 //   adapter_driver essential <dir>                         (EstimatePoseByEssential's two calls)
+//   adapter_driver extract_batch <dir> <n> <h> <w> <c> <n_features>   (ORBExtractor::ExtractBatch of
+//                  dir/img<i>.bin, then ORBMatcher::MatchBatch of the pairs (i, i + 1) -> dir/*.out)
 #include <cstdio>
 #include <cstdlib>
 #include <climits>
@@ -92,6 +94,53 @@ static int cmd_match(char** a) {
     }
     write_bin(a[4], out);
     std::printf("%d\n", n);
+    return 0;
+}
+
+static int cmd_extract_batch(char** a) {
+    const std::string dir = a[0];
+    const int n = std::atoi(a[1]);
+    auto cam = std::make_shared<Camera>(520.9, 521.0, 325.1, 249.7);
+    std::vector<Frame::Ptr> frames;
+    for (int i = 0; i < n; ++i) {
+        ImageU8 img;
+        img.rows = std::atoi(a[2]);
+        img.cols = std::atoi(a[3]);
+        img.channels = std::atoi(a[4]);
+        img.data = read_bin<uint8_t>(dir + "/img" + std::to_string(i) + ".bin");
+        frames.push_back(std::make_shared<Frame>(i, 0.0, cam, img));
+    }
+    ORBExtractor ex(std::atoi(a[5]), 1.2f, 8);
+    ex.ExtractBatch(frames);
+    for (int i = 0; i < n; ++i) {
+        std::vector<double> pos;
+        std::vector<float> resp;
+        for (const auto& f : frames[i]->Features()) {
+            pos.push_back(f.position.x);
+            pos.push_back(f.position.y);
+            resp.push_back(f.response);
+        }
+        const std::string o = dir + "/f" + std::to_string(i);
+        write_bin(o + ".pos", pos);
+        write_bin(o + ".resp", resp);
+        write_bin(o + ".desc", frames[i]->Descriptors().data);
+    }
+    std::vector<std::pair<Frame::Ptr, Frame::Ptr>> pairs;
+    for (int i = 0; i + 1 < n; ++i) pairs.emplace_back(frames[i], frames[i + 1]);
+    ORBMatcher m;
+    std::vector<std::vector<DMatch>> matches;
+    const auto counts = m.MatchBatch(pairs, matches);
+    for (size_t i = 0; i < pairs.size(); ++i) {
+        std::vector<float> out;
+        for (const auto& mm : matches[i]) {
+            out.push_back((float)mm.queryIdx);
+            out.push_back((float)mm.trainIdx);
+            out.push_back(mm.distance);
+        }
+        write_bin(dir + "/m" + std::to_string(i) + ".out", out);
+        std::printf("%d ", counts[i]);
+    }
+    std::printf("\n");
     return 0;
 }
 
@@ -323,6 +372,7 @@ int main(int argc, char** argv) {
         if (cmd == "triangulate" && argc >= 5) return cmd_triangulate(argv + 2);
         if (cmd == "pnp" && argc >= 5) return cmd_pnp(argv + 2);
         if (cmd == "essential" && argc >= 3) return cmd_essential(argv + 2);
+        if (cmd == "extract_batch" && argc >= 8) return cmd_extract_batch(argv + 2);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "error: %s\n", e.what());
         return 1;

@@ -90,6 +90,40 @@ def test_adapter_extract_and_match(driver, oracle, tmp_path):
 
 
 @pytest.mark.gpu
+def test_adapter_extract_and_match_batch(driver, oracle, tmp_path):
+    """ORBExtractor::ExtractBatch over a 5-frame multi-camera step (one blank frame: no features,
+    so its pairs match nothing) and ORBMatcher::MatchBatch over the consecutive pairs: every frame
+    and pair equal to the oracle, as Extract / Match would leave them."""
+    n = 5
+    frames = synth.make_frames(93, n)
+    frames[3] = np.full_like(frames[3], 117)
+    for i, f in enumerate(frames):
+        f.tofile(os.path.join(tmp_path, f"img{i}.bin"))
+    counts = [int(x) for x in run(driver, "extract_batch", tmp_path, n, 480, 640, 3, 1200)]
+    descs = []
+    for i, f in enumerate(frames):
+        pos = np.fromfile(os.path.join(tmp_path, f"f{i}.pos"), np.float64).reshape(-1, 2)
+        resp = np.fromfile(os.path.join(tmp_path, f"f{i}.resp"), np.float32)
+        desc = np.fromfile(os.path.join(tmp_path, f"f{i}.desc"), np.uint8).reshape(-1, 32)
+        kc, dc = oracle.orb_extract(f, 1200, order=oracle.ORDER_RASTER)
+        assert np.array_equal(pos[:, 0], kc["x"].astype(np.float64))
+        assert np.array_equal(pos[:, 1], kc["y"].astype(np.float64))
+        assert np.array_equal(resp, kc["response"]) and np.array_equal(desc, dc)
+        descs.append(dc)
+    assert len(descs[3]) == 0
+    assert len(counts) == n - 1
+    for i in range(n - 1):
+        got = np.fromfile(os.path.join(tmp_path, f"m{i}.out"), np.float32).reshape(-1, 3)
+        exp = oracle.match(descs[i], descs[i + 1]) if len(descs[i]) and len(descs[i + 1]) else oracle.match(
+            descs[0][:0], descs[0][:0])
+        assert counts[i] == len(exp) == len(got)
+        if len(exp):
+            assert np.array_equal(got[:, 0].astype(np.int32), exp["query_idx"])
+            assert np.array_equal(got[:, 1].astype(np.int32), exp["train_idx"])
+            assert np.array_equal(got[:, 2], exp["distance"])
+
+
+@pytest.mark.gpu
 def test_adapter_local_ba(driver, oracle, tmp_path):
     m = synth.make_ba_map(92, 10, 2000, n_old_kf=3)
     dump_map(m, tmp_path)

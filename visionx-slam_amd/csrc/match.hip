@@ -13,6 +13,7 @@
 //                  v_med3: VALU-popcount bound.
 //   k_knn_merge    one block: merge chunk partials, ratio test, ordered compaction (ascending
 //                  query index) by block scan.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -463,6 +464,50 @@ int vx_match_batch_async(vx_ctx* c, int n_pairs, const uint8_t* const* dq, const
     c->mb_valid = n_pairs;
     c->mb_cap = q_cap;
     return VX_OK;
+}
+
+int vx_match_knn2_ratio_batch(vx_ctx* c, int n_pairs, const uint8_t* const* q, const int32_t* nq,
+                              const uint8_t* const* t, const int32_t* nt, float ratio) {
+    if (!c) return VX_ERR_INVALID;
+    if (n_pairs < 1 || n_pairs > VX_MAX_MATCH_PAIRS)
+        return set_error(c, VX_ERR_INVALID, "n_pairs %d outside [1, %d]", n_pairs, VX_MAX_MATCH_PAIRS);
+    if (!q || !nq || !t || !nt) return set_error(c, VX_ERR_INVALID, "vx_match_knn2_ratio_batch: null arrays");
+    int q_cap = 0, t_cap = 0;
+    for (int i = 0; i < n_pairs; ++i) {
+        if (nq[i] < 0 || nt[i] < 0) return set_error(c, VX_ERR_INVALID, "negative descriptor count (pair %d)", i);
+        if ((nq[i] && !q[i]) || (nt[i] && !t[i])) return set_error(c, VX_ERR_INVALID, "null descriptors (pair %d)", i);
+        q_cap = std::max(q_cap, (int)nq[i]);
+        t_cap = std::max(t_cap, (int)nt[i]);
+    }
+    if (t_cap > (1 << 22)) return set_error(c, VX_ERR_INVALID, "train set larger than 2^22 rows");
+    VX_HIP(c, hipSetDevice(c->device));
+    // every pair's rows and both counts staged in one pinned block and uploaded with one copy
+    // (an empty side counts 0 rows: the pair yields no match, orb_matcher.cpp:18-20)
+    const size_t qb = (size_t)std::max(q_cap, 1) * 32, tb = (size_t)std::max(t_cap, 1) * 32;
+    const size_t cnt_off = (size_t)n_pairs * (qb + tb), total = cnt_off + (size_t)n_pairs * 8;
+    VX_HIP(c, hipStreamSynchronize(c->stream));  // the staging block may still feed a previous copy
+    VX_HIP(c, c->mb_host.ensure(total));
+    VX_HIP(c, c->mb_in.ensure(total));
+    uint8_t* H = static_cast<uint8_t*>(c->mb_host.p);
+    int32_t* hc = reinterpret_cast<int32_t*>(H + cnt_off);
+    for (int i = 0; i < n_pairs; ++i) {
+        if (nq[i]) std::memcpy(H + i * qb, q[i], (size_t)nq[i] * 32);
+        if (nt[i]) std::memcpy(H + n_pairs * qb + i * tb, t[i], (size_t)nt[i] * 32);
+        hc[2 * i] = nq[i] && nt[i] ? nq[i] : 0;
+        hc[2 * i + 1] = nq[i] && nt[i] ? nt[i] : 0;
+    }
+    VX_HIP(c, hipMemcpyAsync(c->mb_in.p, H, total, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* D = c->mb_in.as<uint8_t>();
+    const int32_t* dc = reinterpret_cast<const int32_t*>(D + cnt_off);
+    std::vector<const uint8_t*> dq(n_pairs), dt(n_pairs);
+    std::vector<const int32_t*> dnq(n_pairs), dnt(n_pairs);
+    for (int i = 0; i < n_pairs; ++i) {
+        dq[i] = D + i * qb;
+        dt[i] = D + n_pairs * qb + i * tb;
+        dnq[i] = dc + 2 * i;
+        dnt[i] = dc + 2 * i + 1;
+    }
+    return vx_match_batch_async(c, n_pairs, dq.data(), dnq.data(), q_cap, dt.data(), dnt.data(), t_cap, ratio);
 }
 
 int vx_match_batch_fetch(vx_ctx* c, int pair, vx_match* out, int cap, int* n_out) {

@@ -1625,6 +1625,30 @@ int vx_orb_extract_batch_async(vx_ctx* c, const vx_orb_params* p, const uint8_t*
     return VX_OK;
 }
 
+int vx_orb_extract_batch(vx_ctx* c, const vx_orb_params* p, const uint8_t* const* imgs, int n_frames, int w, int h,
+                         int channels, int64_t stride, int bank) {
+    if (!c) return VX_ERR_INVALID;
+    if (!imgs) return set_error(c, VX_ERR_INVALID, "null images");
+    if (n_frames < 1 || n_frames > VX_MAX_BATCH)
+        return set_error(c, VX_ERR_INVALID, "n_frames %d outside [1, %d]", n_frames, VX_MAX_BATCH);
+    if (channels != 1 && channels != 3 && channels != 4)
+        return set_error(c, VX_ERR_INVALID, "channels must be 1, 3 or 4");
+    if (stride < (int64_t)w * channels) return set_error(c, VX_ERR_INVALID, "row stride too small");
+    for (int f = 0; f < n_frames; ++f)
+        if (!imgs[f]) return set_error(c, VX_ERR_INVALID, "null image %d", f);
+    int rc = orb_prepare(c, p, w, h);
+    if (rc) return rc;
+    VX_HIP(c, hipSetDevice(c->device));
+    // frames packed back to back in the context's upload buffer, then the device-resident batch
+    const size_t packed = (size_t)w * channels, fbytes = packed * h;
+    VX_HIP(c, c->img_in.ensure(fbytes * n_frames));
+    for (int f = 0; f < n_frames; ++f)
+        VX_HIP(c, hipMemcpy2DAsync(c->img_in.as<uint8_t>() + f * fbytes, packed, imgs[f], (size_t)stride, packed, h,
+                                   hipMemcpyHostToDevice, c->stream));
+    return vx_orb_extract_batch_async(c, p, c->img_in.as<uint8_t>(), n_frames, (int64_t)fbytes, w, h, channels,
+                                      (int64_t)packed, bank);
+}
+
 int vx_orb_batch_device(vx_ctx* c, int bank, int frame, const uint8_t** d_desc, const int32_t** d_count,
                         int32_t* cap) {
     if (!c || bank < 0 || bank >= VX_BATCH_BANKS || frame < 0 || frame >= c->batch_n[bank]) return VX_ERR_INVALID;

@@ -189,6 +189,8 @@ struct vx_ctx {
     int match_cap = 0;
     bool match_valid = false;
     vx::DevBuf mb_best, mb_matches, mb_count;  // vx_match_batch_async: per-pair results
+    vx::DevBuf mb_in;                           // vx_match_knn2_ratio_batch: uploaded rows + counts
+    vx::PinnedBuf mb_host;
     int mb_valid = 0, mb_cap = 0;
 
     // ---- landmark creation (landmarks.hip): inputs, per-item flags / points, compacted outputs

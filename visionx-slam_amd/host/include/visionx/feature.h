@@ -13,6 +13,7 @@
 #pragma once
 
 #include <memory>
+#include <utility>
 #include <vector>
 
 #include "vx_slam.h"
@@ -38,6 +39,11 @@ class ORBExtractor : public FeatureExtractor {
 public:
     ORBExtractor(int n_features = 1000, float scale_factor = 1.2f, int n_levels = 8);
     void Extract(Frame& frame) override;
+    // Extension for multi-camera rigs (the C5 workload): Extract() of every frame of one time step
+    // in one batched launch sequence (vx_orb_extract_batch).  Each frame's Features() /
+    // Descriptors() end up exactly as Extract(frame) leaves them; frames of differing size or
+    // channel count, or empty ones, are extracted one by one.
+    void ExtractBatch(const std::vector<Frame::Ptr>& frames);
 
 private:
     vx_orb_params params_;
@@ -54,8 +60,13 @@ public:
     ORBMatcher() : ORBMatcher(Options()) {}
     explicit ORBMatcher(const Options& options);
     int Match(const Frame::Ptr& last, const Frame::Ptr& curr, std::vector<DMatch>& matches) override;
+    // Extension: Match(last_i, curr_i, matches[i]) for up to VX_MAX_MATCH_PAIRS pairs in one launch
+    // pair (vx_match_knn2_ratio_batch); returns the per-pair counts Match() would return.
+    std::vector<int> MatchBatch(const std::vector<std::pair<Frame::Ptr, Frame::Ptr>>& pairs,
+                                std::vector<std::vector<DMatch>>& matches);
 
 private:
+    void Finish(std::vector<DMatch>& matches, int n);
     Options options_;
     std::vector<vx_match> buf_;
 };

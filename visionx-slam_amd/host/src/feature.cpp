@@ -80,8 +80,94 @@ void ORBExtractor::Extract(Frame& frame) {
     frame.Descriptors() = std::move(d);
 }
 
+void ORBExtractor::ExtractBatch(const std::vector<Frame::Ptr>& frames) {
+    if (frames.empty()) return;
+    const ImageU8& i0 = frames[0]->Image();
+    bool uniform = (int)frames.size() <= VX_MAX_BATCH && !i0.empty();
+    for (const auto& f : frames)
+        uniform = uniform && f->Image().rows == i0.rows && f->Image().cols == i0.cols &&
+                  f->Image().channels == i0.channels && f->Image().step() == i0.step() && !f->Image().empty();
+    if (!uniform) {
+        for (const auto& f : frames) Extract(*f);
+        return;
+    }
+    vx_ctx* c = vxhost::ThreadContext();
+    std::vector<const uint8_t*> imgs;
+    for (const auto& f : frames) imgs.push_back(f->Image().ptr());
+    check(c, vx_orb_extract_batch(c, &params_, imgs.data(), (int)frames.size(), i0.cols, i0.rows, i0.channels,
+                                  (int64_t)i0.step(), 0),
+          "vx_orb_extract_batch");
+    for (size_t b = 0; b < frames.size(); ++b) {
+        Frame& frame = *frames[b];
+        int cap = 2 * params_.n_features + 256, n = 0;
+        kp_.resize(cap);
+        desc_.resize((size_t)cap * 32);
+        check(c, vx_orb_batch_fetch(c, 0, (int)b, kp_.data(), desc_.data(), cap, &n), "vx_orb_batch_fetch");
+        auto& features = frame.Features();
+        features.clear();
+        features.reserve(n);
+        for (int i = 0; i < n; ++i) {
+            Feature f;
+            f.position = Vec2d(kp_[i].x, kp_[i].y);
+            f.response = kp_[i].response;
+            features.emplace_back(f);
+        }
+        DescriptorMat d;
+        d.rows = n;
+        d.data.assign(desc_.begin(), desc_.begin() + (size_t)n * 32);
+        frame.Descriptors() = std::move(d);
+    }
+}
+
 // ------------------------------------------------------------------ ORBMatcher
 ORBMatcher::ORBMatcher(const Options& options) : options_(options) {}
+
+void ORBMatcher::Finish(std::vector<DMatch>& matches, int n) {
+    matches.reserve(n);
+    for (int i = 0; i < n; ++i) {
+        DMatch m;
+        m.queryIdx = buf_[i].query_idx;
+        m.trainIdx = buf_[i].train_idx;
+        m.imgIdx = 0;
+        m.distance = buf_[i].distance;
+        matches.push_back(m);
+    }
+    if (matches.size() < (size_t)options_.min_matches)          // orb_matcher.cpp:38-40
+        std::fprintf(stderr, "W [ORBMatcher] Too few matches: %zu\n", matches.size());
+}
+
+std::vector<int> ORBMatcher::MatchBatch(const std::vector<std::pair<Frame::Ptr, Frame::Ptr>>& pairs,
+                                        std::vector<std::vector<DMatch>>& matches) {
+    matches.assign(pairs.size(), {});
+    std::vector<int> counts(pairs.size(), 0);
+    vx_ctx* c = vxhost::ThreadContext();
+    for (size_t p0 = 0; p0 < pairs.size(); p0 += VX_MAX_MATCH_PAIRS) {
+        const int np = (int)std::min<size_t>(VX_MAX_MATCH_PAIRS, pairs.size() - p0);
+        std::vector<const uint8_t*> q(np), t(np);
+        std::vector<int32_t> nq(np), nt(np);
+        int cap = 1;
+        for (int i = 0; i < np; ++i) {
+            const DescriptorMat& d1 = pairs[p0 + i].first->Descriptors();
+            const DescriptorMat& d2 = pairs[p0 + i].second->Descriptors();
+            q[i] = d1.empty() ? nullptr : d1.ptr();
+            t[i] = d2.empty() ? nullptr : d2.ptr();
+            nq[i] = d1.empty() ? 0 : d1.rows;                    // orb_matcher.cpp:18-20
+            nt[i] = d2.empty() ? 0 : d2.rows;
+            cap = std::max(cap, nq[i]);
+        }
+        check(c, vx_match_knn2_ratio_batch(c, np, q.data(), nq.data(), t.data(), nt.data(), options_.nn_ratio),
+              "vx_match_knn2_ratio_batch");
+        buf_.resize(cap);
+        for (int i = 0; i < np; ++i) {
+            if (nq[i] == 0 || nt[i] == 0) continue;              // Match() returns 0 before warning
+            int n = 0;
+            check(c, vx_match_batch_fetch(c, i, buf_.data(), cap, &n), "vx_match_batch_fetch");
+            Finish(matches[p0 + i], n);
+            counts[p0 + i] = (int)matches[p0 + i].size();
+        }
+    }
+    return counts;
+}
 
 int ORBMatcher::Match(const Frame::Ptr& last, const Frame::Ptr& curr, std::vector<DMatch>& matches) {
     matches.clear();                                             // orb_matcher.cpp:13
@@ -94,17 +180,7 @@ int ORBMatcher::Match(const Frame::Ptr& last, const Frame::Ptr& curr, std::vecto
     check(c, vx_match_knn2_ratio(c, d1.ptr(), d1.rows, d2.ptr(), d2.rows, options_.nn_ratio, buf_.data(),
                                  (int)buf_.size(), &n),
           "vx_match_knn2_ratio");
-    matches.reserve(n);
-    for (int i = 0; i < n; ++i) {
-        DMatch m;
-        m.queryIdx = buf_[i].query_idx;
-        m.trainIdx = buf_[i].train_idx;
-        m.imgIdx = 0;
-        m.distance = buf_[i].distance;
-        matches.push_back(m);
-    }
-    if (matches.size() < (size_t)options_.min_matches)          // orb_matcher.cpp:38-40
-        std::fprintf(stderr, "W [ORBMatcher] Too few matches: %zu\n", matches.size());
+    Finish(matches, n);
     return (int)matches.size();
 }
 

@@ -89,7 +89,7 @@ EXPORTS = [
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
-    "vx_match_batch_fetch",
+    "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
