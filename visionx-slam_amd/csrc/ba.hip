@@ -709,6 +709,10 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // and waited for only at its use below)
     const int act = kPro ? 1 : __hip_atomic_load(&a.state->active[it], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     extern __shared__ __attribute__((aligned(16))) double fl[];
+    // the workgroup's keyframe entry records, staged once: the combine and the pose stage read them
+    // from LDS instead of issuing a dependent global load at the start of each
+    __shared__ int4 s_ke[kFK];
+    __shared__ int s_kd[kFK];
     double* kslot = fl;                                  // [kFK][kLdsStride]
     double* tslot = kslot + kFK * kLdsStride;            // [kFK][kTStride]
     double* terms = tslot + kFK * kTStride;              // [9][kFT]
@@ -749,9 +753,11 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // (c) the keyframe entry it solves: previous pose, intrinsics, flags -> tslot (the prologue
     // gathers them by keyframe row into the workgroup's entry copy; later launches read the copy)
     int4 ke = make_int4(-1, 0, 0, 0);
+    int kd = -1;
     double ev[13];
     if (tid < kFK) {
         ke = KE[2 * tid];
+        kd = KE[2 * tid + 1].x;
         // (the copy is read whether or not the entry exists — unused entries are valid memory — so
         // the load does not wait for the entry table)
         if (ke.x >= 0 || (!kPro && kEcopy)) {
@@ -796,12 +802,17 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     lpos[3 * tid] = PL.x;
     lpos[3 * tid + 1] = PL.y;
     lpos[3 * tid + 2] = PL.z;
+    if (tid < kFK) {
+        s_ke[tid] = ke;
+        s_kd[tid] = kd;
+    }
     FKT(1);
+    __syncthreads();  // s_ke / s_kd
     if (!kPro) {
         // ---- combine: S of entry j, term t = the row's partial slots summed in slot order
         for (int pr = tid; pr < n_ent * kNTerms; pr += kFT) {
             const int j = pr / kNTerms, t = pr - j * kNTerms;
-            const int4 e = KE[2 * j];
+            const int4 e = s_ke[j];
             if (e.x < 0) continue;  // a hole in the entry positions
             if (f.rowpart) {  // sharded: the all-reduced row (identical on every rank)
                 kslot[j * kLdsStride + t] = f.rowpart[(size_t)(e.x & 0x3fffffff) * kStride + t];
@@ -928,8 +939,8 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     int r = 0;
     FKT(6);
     for (int j = wv; j < n_ent; j += kFW) {
-        const int4 e = KE[2 * j];
-        const int dst = KE[2 * j + 1].x;
+        const int4 e = s_ke[j];
+        const int dst = s_kd[j];
         const int nr = (e.w - e.z + 63) >> 6;
         if (nr == 0) continue;
         const double* T = kslot + j * kLdsStride;
