@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
 import vxslam  # noqa: E402
 from vxslam import synth  # noqa: E402
 
-KT_BLOCKS, KT_SLOTS = 64, 16
+KT_BLOCKS, KT_SLOTS = 256, 16
 
 
 def read(fn="vx_ktrace_read_ba"):
@@ -109,6 +109,18 @@ def main():
     print("  slowest workgroups: wg  loads combine solve landmark pose-stage  total (us)")
     for b in order:
         print(f"    {b:3d}  " + "  ".join(f"{x:6.2f}" for x in d[b]) + f"  {end[b]:6.2f}")
+    # launch-absolute view over every traced workgroup (one launch: the last run's it = 1): which
+    # workgroups end last, and whether because they started late or ran long
+    t0 = tr[ok, 0].min()
+    st = (tr[:, 0] - t0) / 100.0
+    en = (tr[:, 5] - t0) / 100.0
+    nb = int(ok.sum())
+    print(f"  launch view ({nb} workgroups): start spread {st[ok].max():.2f} us, end median {np.median(en[ok]):.2f} "
+          f"max {en[ok].max():.2f} us; latest-ending (wg start +loads +combine +solve +landmark +pose = end, "
+          f"pose-stage rounds per wave):")
+    for b in [b for b in np.argsort(-en) if ok[b]][:8]:
+        rounds = [int(blk[b, 5 + 2 * i]) for i in range(min(fw, 8))] if b < len(blk) else []
+        print(f"    {b:3d}  {st[b]:5.2f} " + " ".join(f"{x:5.2f}" for x in d[b]) + f" = {en[b]:5.2f}  {rounds}")
     plan.close()
     # the two-kernel path (sharded plans, windows the fused layout does not fit)
     os.environ["VX_BA_FUSED"] = "0"

@@ -6,7 +6,7 @@
 #pragma once
 
 namespace vx {
-constexpr int kKtBlocks = 64, kKtSlots = 16;
+constexpr int kKtBlocks = 256, kKtSlots = 16;
 }
 
 #ifdef VX_KTRACE
