@@ -421,6 +421,17 @@ __device__ __forceinline__ int win_byte(const uint32_t (&w)[3], int b) {
     return (int)((w[b >> 2] >> (8 * (b & 3))) & 255u);
 }
 
+// Two adjacent bytes b, b + 1 (b in 0..8) of a 12-byte window, zero-extended into the two 16-bit
+// lanes of a register (one v_perm_b32): the FAST ring test below runs on pixel pairs with packed
+// 16-bit arithmetic.  Selector bytes 0..3 pick the low source's bytes, 4..7 the high one's, 0x0c a zero.
+typedef short vx_i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short vx_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ vx_i16x2 win_pair(const uint32_t (&w)[3], int b) {
+    const int lo = b >= 7 ? 1 : 0, bb = b - 4 * lo;
+    const uint32_t sel = (uint32_t)bb | 0x0c00u | ((uint32_t)(bb + 1) << 16) | 0x0c000000u;
+    return __builtin_bit_cast(vx_i16x2, __builtin_amdgcn_perm(w[lo + 1], w[lo], sel));
+}
+
 __device__ __forceinline__ int refl101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) {
@@ -488,19 +499,33 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
             for (int k = 0; k < 3; ++k) w[d][k] = rp[d * (kTW / 4) + k];
         const int y = y0 - 1 + r;
         unsigned cm = 0;
+        // pixel pairs (4g + 2h, 4g + 2h + 1) in 16-bit lanes: bright <=> (v + thr) - p < 0 and dark
+        // <=> p - (v - thr) < 0, exact in 16 bits (|results| <= 510); the sign bit of lane k's
+        // difference becomes bit k of the pixel's ring mask — no per-sample compare-to-mask round
+        // trip, and both masks branch-free
+        const vx_i16x2 T2 = {(short)thr, (short)thr};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int x = x0 - 1 + 4 * g + j;
-            const int v = win_byte(w[3], j + 3);
-            uint32_t bright = 0, dark = 0;
+        for (int h = 0; h < 2; ++h) {
+            const vx_i16x2 V = win_pair(w[3], 2 * h + 3);
+            const vx_i16x2 VT = V + T2, VM = V - T2;
+            vx_u16x2 mb = {0, 0}, md = {0, 0};
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                const int pk = win_byte(w[3 + ring_dy(k)], j + 3 + ring_dx(k));
-                bright |= (uint32_t)(pk > v + thr) << k;
-                dark |= (uint32_t)(pk < v - thr) << k;
+                const vx_i16x2 P = win_pair(w[3 + ring_dy(k)], 2 * h + 3 + ring_dx(k));
+                const vx_u16x2 db = __builtin_bit_cast(vx_u16x2, (vx_i16x2)(VT - P));
+                const vx_u16x2 dd = __builtin_bit_cast(vx_u16x2, (vx_i16x2)(P - VM));
+                const vx_u16x2 bit = {(unsigned short)(1u << k), (unsigned short)(1u << k)};
+                mb |= (db >> (unsigned short)(15 - k)) & bit;
+                md |= (dd >> (unsigned short)(15 - k)) & bit;
             }
-            const bool ok = 4 * g + j < kSW - 2 && y >= 3 && y < H - 3 && x >= 3 && x < W - 3;
-            cm |= (unsigned)(ok && (has_run9(bright) || has_run9(dark))) << j;
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const int j = 2 * h + jj;
+                const int x = x0 - 1 + 4 * g + j;
+                const uint32_t bright = jj ? mb.y : mb.x, dark = jj ? md.y : md.x;
+                const bool ok = 4 * g + j < kSW - 2 && y >= 3 && y < H - 3 && x >= 3 && x < W - 3;
+                cm |= (unsigned)(ok & (has_run9(bright) | has_run9(dark))) << j;
+            }
         }
         *reinterpret_cast<uint32_t*>(sc + r * kSW + 4 * g) = 0u;
         if (cm) {
