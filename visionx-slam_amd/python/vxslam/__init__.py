@@ -128,6 +128,8 @@ def lib():
                                             C.c_int, C.c_float]
         L.vx_orb_extract_batch_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int64, C.c_int,
                                                  C.c_int, C.c_int, C.c_int64, C.c_int]
+        L.vx_orb_extract_batch.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int,
+                                           C.c_int, C.c_int64, C.c_int]
         L.vx_orb_batch_device.argtypes = [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_void_p), C.POINTER(C.c_int32)]
         L.vx_orb_batch_fetch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
@@ -379,18 +381,17 @@ class Context:
         return d.value, n.value, cap.value
 
     def orb_extract_batch(self, imgs: np.ndarray, params: OrbParams | None = None, bank: int = 0):
-        """Host convenience: upload a (B, H, W[, C]) stack and extract it as one batch; returns a list of
-        (keypoints, descriptors) per frame."""
-        import torch  # device memory for the upload (plumbing only)
-
+        """Host convenience over vx_orb_extract_batch (host frames, uploaded by the library): a
+        (B, H, W[, C]) stack extracted as one batch; returns a list of (keypoints, descriptors) per
+        frame."""
         imgs = np.ascontiguousarray(imgs)
         b, h, w = imgs.shape[:3]
         ch = 1 if imgs.ndim == 3 else imgs.shape[3]
-        d = torch.from_numpy(imgs).to(f"cuda:{self.device}")
-        self.orb_extract_batch_async(d.data_ptr(), b, d.stride(0), w, h, ch, d.stride(1), bank, params)
-        out = [self.orb_batch_fetch(bank, f) for f in range(b)]
-        del d
-        return out
+        params = params or default_orb_params()
+        ptrs = (C.c_void_p * b)(*[C.c_void_p(imgs[f].ctypes.data) for f in range(b)])
+        self._check(lib().vx_orb_extract_batch(self._h, C.byref(params), ptrs, b, w, h, ch, C.c_int64(imgs.strides[1]),
+                                               bank))
+        return [self.orb_batch_fetch(bank, f) for f in range(b)]
 
     # ---------------------------------------------------------------- matching
     def match(self, q: np.ndarray, t: np.ndarray, ratio: float = 0.8):
