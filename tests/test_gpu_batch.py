@@ -134,6 +134,35 @@ def test_match_batch_matches_oracle(ctx, oracle):
         assert np.array_equal(ctx.match_fetch(), ctx.match_batch_fetch(c))
 
 
+def test_batch_maximum_sizes(ctx, oracle):
+    """VX_MAX_BATCH frames in one call and VX_MAX_MATCH_PAIRS pairs in one match call (small frames),
+    including pairs with an empty query or train side."""
+    import vxslam
+
+    h, w, n = 96, 128, 150
+    frames = synth.make_frames(0xBA800, 64, h, w)
+    for f in (5, 17):
+        frames[f] = np.full_like(frames[f], 90)
+    p = vxslam.default_orb_params(n_features=n)
+    out = ctx.orb_extract_batch(np.stack(frames), p, bank=0)
+    for f in (0, 5, 17, 63):
+        _eq(out[f], oracle.orb_extract(frames[f], n, order=oracle.ORDER_RASTER))
+    for f in range(64):
+        _eq(out[f], ctx.orb_extract(frames[f], p))
+    pairs = [(ctx.batch_device(0, 2 * i), ctx.batch_device(0, 2 * i + 1)) for i in range(16)]
+    pairs[2] = (ctx.batch_device(0, 5), ctx.batch_device(0, 6))    # empty query side
+    pairs[8] = (ctx.batch_device(0, 16), ctx.batch_device(0, 17))  # empty train side
+    ctx.match_batch_async(pairs)
+    idx = [(2 * i, 2 * i + 1) for i in range(16)]
+    idx[2], idx[8] = (5, 6), (16, 17)
+    for i, (a, b) in enumerate(idx):
+        ref = oracle.match(out[a][1], out[b][1]) if len(out[a][1]) and len(out[b][1]) else []
+        got = ctx.match_batch_fetch(i)
+        assert len(got) == len(ref), i
+        if len(ref):
+            assert np.array_equal(got, ref), i
+
+
 def test_batch_invalid_arguments(ctx):
     import vxslam
 
