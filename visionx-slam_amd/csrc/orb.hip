@@ -524,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
                 const int x = x0 - 1 + 4 * g + j;
                 const uint32_t bright = jj ? mb.y : mb.x, dark = jj ? md.y : md.x;
                 const bool ok = 4 * g + j < kSW - 2 && y >= 3 && y < H - 3 && x >= 3 && x < W - 3;
-                cm |= (unsigned)(ok & (has_run9(bright) | has_run9(dark))) << j;
+                cm |= ((unsigned)ok & ((unsigned)has_run9(bright) | (unsigned)has_run9(dark))) << j;
             }
         }
         *reinterpret_cast<uint32_t*>(sc + r * kSW + 4 * g) = 0u;
