@@ -157,7 +157,8 @@ def timed_loop(step, steps, warmup, sync, dist):
 
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(cfg, frames_host, ba_map, sample_frames):
-    """The CPU restatement (oracle/, single thread, -O2) on a bounded sample of the same workload."""
+    """The CPU restatement (oracle/, single thread, -O3 -march=x86-64-v3 -ffp-contract=off: SURVEY §8(d)'s
+    optimised build, portable to any AVX2 host) on a bounded sample of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as O
 
