@@ -27,7 +27,8 @@ def _device_stack(frames):
 
 
 @pytest.mark.parametrize("b,h,w,n,gray", [(1, 240, 320, 500, False), (3, 240, 320, 500, True),
-                                          (8, 480, 640, 2000, False), (5, 333, 517, 800, False)])
+                                          (8, 480, 640, 2000, False), (5, 333, 517, 800, False),
+                                          (6, 333, 517, 800, True), (3, 961, 1283, 4000, False)])
 def test_orb_batch_matches_oracle(ctx, oracle, b, h, w, n, gray):
     import vxslam
 
