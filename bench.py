@@ -156,6 +156,21 @@ def timed_loop(step, steps, warmup, sync, dist):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+def host_cpu():
+    """The host CPU model and the cores this process may use (record the host)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    return f"{model}; {usable} usable of {os.cpu_count()} logical CPUs"
+
+
 def cpu_baseline(cfg, frames_host, ba_map, sample_frames):
     """The CPU restatement (oracle/, single thread, -O3 -march=x86-64-v3 -ffp-contract=off: SURVEY §8(d)'s
     optimised build, portable to any AVX2 host) on a bounded sample of the same workload."""
@@ -191,6 +206,7 @@ def cpu_baseline(cfg, frames_host, ba_map, sample_frames):
         "unit": "ms/frame",
         "cores": 1,
         "kind": "port",
+        "host": host_cpu(),
         "sample": f"{sample_frames} frames of the same workload (extract {k * t_ext:.2f} + match {k * t_match:.2f} + "
                   f"BA iterations {k * t_iter:.2f} ms/frame; excluded: BA window/landmark-set selection "
                   f"{k * t_setup:.2f} ms, compare ba_plan_build_ms), oracle/ C++ restatement, 1 thread",
