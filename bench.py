@@ -536,6 +536,12 @@ def main():
             # map snapshot, incl. upload: paid once per LocalBA::Optimize() call of a drop-in
             # (a new keyframe, tracking.cpp:76-84); the timed steps replay a resident plan
             "ba_plan_build_ms": round(plan_build_ms, 3),
+            # what one step computed (the BA iteration count actually executed is
+            # reported): LocalBA iterations and their valid pose-stage observations, the last frame's
+            # keypoints and matches
+            "work_per_step": {"ba_iterations": int(st.iterations),
+                              "ba_observations_per_iteration": [int(x) for x in list(st.obs)[:int(st.iterations)]],
+                              "keypoints": int(len(kps)), "matches": int(len(matches))},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "stages_us": {k: round(v[0] * 1e3, 2) for k, v in stages.items()},
