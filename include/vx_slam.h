@@ -9,10 +9,14 @@
  *   vx_orb_extract        <- FeatureExtractor::Extract(Frame&)   core/feature/feature_extractor.h:15
  *                            ORBExtractor::Extract               core/feature/orb_extractor.cpp:9-27
  *                            ORBExtractor(n=1000, 1.2f, 8)       core/feature/orb_extractor.h:11-13
+ *   vx_orb_extract_batch* <- ORBExtractor::Extract once per camera of a multi-camera time step
+ *                            (orb_extractor.cpp:9-27; BASELINE config C5's 8 streams), B frames per launch
  *   vx_match_knn2_ratio   <- FeatureMatcher::Match(last, curr, matches)
  *                                                                core/feature/feature_matcher.h:11-12
  *                            ORBMatcher::Match + Options         core/feature/orb_matcher.cpp:11-43,
  *                                                                orb_matcher.h:11-14
+ *   vx_match_*batch*      <- ORBMatcher::Match once per camera pair (orb_matcher.cpp:11-43), up to
+ *                            VX_MAX_MATCH_PAIRS pairs per launch
  *   vx_ba_optimize_map    <- LocalBA::Optimize(map, ref_kf)      core/backend/local_ba.h:23,
  *                                                                local_ba.cpp:66-249
  *                            LocalBA::Options                    core/backend/local_ba.h:12-19
