@@ -282,7 +282,7 @@ def main():
                     help="stream priority of the LocalBA context (1: the device's greatest)")
     ap.add_argument("--grid-share", type=float, default=None,
                     help="share of the CUs the extraction context's one-round grids are sized for "
-                         "(vx_set_grid_share; default 1/3 with more than one stream, 1 otherwise)")
+                         "(vx_set_grid_share; default 1/4 with more than one stream, 1 otherwise: DESIGN.md §7)")
     ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
                     help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
     ap.add_argument("--extract-ctx", type=int, default=2, choices=(1, 2, 3, 4),
@@ -321,7 +321,8 @@ def main():
     bctx = ectx if args.streams < 2 else vxslam.Context(dist.local_rank, priority=args.ba_priority, cu_mask=ba_mask)
     ctxs = list({id(c): c for c in ectxs + [mctx, bctx]}.values())
     # extraction runs beside the previous frame's LocalBA: its pyramid grid leaves CUs free for it
-    grid_share = args.grid_share if args.grid_share else (1.0 / 3.0 if args.streams > 1 else 1.0)
+    # (1/4: 6 alternating runs each late in round 2, median 0.0684 against 0.0696 ms/frame at 1/3)
+    grid_share = args.grid_share if args.grid_share else (0.25 if args.streams > 1 else 1.0)
     for c in ectxs:
         c.set_grid_share(grid_share)
     cfg = CONFIGS[args.config]
