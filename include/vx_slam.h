@@ -126,7 +126,7 @@ int vx_graph_counts(const vx_ctx* ctx, int* captured, int* launched);
 /* Fraction (0, 1] of the device's compute units this context's one-round grids (the fused
  * pyramid of vx_orb_extract*) are sized for (default 1).  A frontend context whose extraction
  * runs beside other contexts' work (the LocalBA of the previous keyframe) gets a smaller grid
- * that leaves CUs free: 1/3 in the 3-context pipeline of bench.py.  Results are
+ * that leaves CUs free: 1/4 in the 3-context pipeline of bench.py.  Results are
  * identical for every share; the call drops the context's captured graphs. */
 int vx_set_grid_share(vx_ctx* ctx, float share);
 void vx_orb_default_params(vx_orb_params* p);
