@@ -135,10 +135,34 @@ int vx_orb_pattern(int32_t* out_1024);
 
 /* ---------------------------------------------------------------- ORB extraction
  * img: 8UC1 gray or 8UC3/8UC4 BGR(A) rows of row_stride bytes.  Keypoints are emitted level by
- * level (octave ascending) and in raster order inside a level; the keypoint SET per level is
- * exactly OpenCV's (retainBest keeps {response >= k-th largest}), the order inside a level is
- * canonical instead of the libstdc++ nth_element permutation.  out_desc gets
- * N rows of 32 bytes.  Returns VX_ERR_CAPACITY (with *n_out = N) if N > cap. */
+ * level (octave ascending) and, inside a level, in the order OpenCV's KeyPointsFilter::retainBest
+ * leaves them when built against libstdc++: std::nth_element + std::partition by FAST score, then
+ * again by Harris response (VX_ORDER_STL, the default) — the order ORBExtractor::Extract numbers
+ * Frame::Features() in (orb_extractor.cpp:13-24).  VX_ORDER_RASTER (opt-in, vx_orb_set_order)
+ * keeps the same keypoint set per level in raster order.  out_desc gets N rows of 32 bytes.
+ * Returns VX_ERR_CAPACITY (with *n_out = N) if N > cap. */
+#define VX_ORDER_STL 0
+#define VX_ORDER_RASTER 1
+/* Keypoint order of every later extraction on ctx (drops the context's captured graphs). */
+int vx_orb_set_order(vx_ctx* ctx, int order);
+int vx_orb_get_order(const vx_ctx* ctx);
+/* Test hooks for per-stage parity; single-frame extraction into slot 0
+ * (vx_orb_extract) only.  VX_ORB_DEBUG_FAST_NO_BORDER makes k_fast keep every FAST + NMS corner
+ * of [3, W-3) x [3, H-3) (the list before runByImageBorder; the later stages are then NOT the
+ * reference's); VX_ORB_DEBUG_STAGES records the selection's stages.  vx_orb_debug_read(level,
+ * what): 0 the gray / INTER_LINEAR_EXACT level (lw*lh bytes), 1 its GaussianBlur, 2 the level's
+ * candidates in raster order (16-byte records {x | y << 16, FAST score, float Harris, 0}),
+ * 3 retainBest(2q)'s output order (int32 indices into the candidates), 4 retainBest(q)'s output
+ * (16-byte records, the order k_describe emits).  *n_out = elements (bytes for 0/1). */
+#define VX_ORB_DEBUG_FAST_NO_BORDER 1
+#define VX_ORB_DEBUG_STAGES 2
+int vx_orb_set_debug(vx_ctx* ctx, int flags);
+int vx_orb_debug_read(vx_ctx* ctx, int level, int what, void* out, int64_t cap_bytes, int64_t* n_out);
+/* Test hook: KeyPointsFilter::retainBest(keys, npts) through the device selection code (one
+ * workgroup): elements u32 (key <= 255, the FAST-score path) or wide = u64 (the Harris path),
+ * in LDS or in global memory; out_idx = kept key indices in output order. */
+int vx_test_retain_best(vx_ctx* ctx, const uint32_t* keys, int n, int npts, int wide, int use_lds,
+                        int32_t* out_idx, int* n_out);
 int vx_orb_extract(vx_ctx* ctx, const vx_orb_params* params, const uint8_t* img, int width,
                    int height, int channels, int64_t row_stride, vx_keypoint* out_kp,
                    uint8_t* out_desc, int cap, int* n_out);

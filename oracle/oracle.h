@@ -40,9 +40,10 @@ typedef struct {
 
 /* Order of keypoints inside one pyramid level.
  *  ORC_ORDER_STL    : the std::nth_element / std::partition permutation of OpenCV's
- *                     KeyPointsFilter::retainBest as compiled against THIS libstdc++.
- *  ORC_ORDER_RASTER : the same keypoint set in raster order (y, then x) — the canonical order
- *                     emitted by the GPU path.                                               */
+ *                     KeyPointsFilter::retainBest as compiled against THIS libstdc++ (the order
+ *                     ORBExtractor::Extract numbers Frame::Features() in on Linux; the GPU default).
+ *  ORC_ORDER_RASTER : the same keypoint set in raster order (y, then x) — the GPU's opt-in
+ *                     VX_ORDER_RASTER.                                                        */
 enum { ORC_ORDER_STL = 0, ORC_ORDER_RASTER = 1 };
 
 int orc_orb_quotas(int n_features, float scale_factor, int n_levels, int32_t* quotas);
@@ -65,6 +66,21 @@ int orc_orb_extract(const uint8_t* img, int w, int h, int channels, int64_t row_
                     int n_features, float scale_factor, int n_levels, int fast_threshold,
                     const int32_t* pattern /* 256*4 ints */, int order,
                     orc_keypoint* kps, uint8_t* desc, int cap, int* n_out);
+/* Per-stage lists of one extraction, every level concatenated (level l's
+ * counts at counts[4l .. 4l+3], each list's capacity `cap` entries):
+ *   fast_xys : FAST + 3x3 NMS (x, y, score) in raster order, before runByImageBorder
+ *   cand     : after runByImageBorder, raster order: (x, y, FAST score, Harris response)
+ *   keep1    : retainBest(2q) by FAST score, output order, as indices into the level's cand
+ *   fin      : retainBest(q) by Harris, output order, as indices into the level's cand      */
+int orc_orb_stages(const uint8_t* img, int w, int h, int channels, int64_t row_stride, int n_features,
+                   float scale_factor, int n_levels, int fast_threshold, int order, int32_t* counts,
+                   int32_t* fast_xys, float* cand, int32_t* keep1, int32_t* fin, int64_t cap);
+/* KeyPointsFilter::retainBest over bare keys (std::nth_element + std::partition with
+ * comp = key-greater on (key, index) pairs): out_idx = kept indices in the library's order */
+int orc_retain_best_keys(const uint32_t* keys, int n, int npts, int32_t* out_idx, int* n_out);
+/* McIlroy's antiqsort adversary run against std::nth_element(begin, begin + nth, end, greater):
+ * keys that defeat its median-of-3 pivots (reaching the depth limit / heap select). */
+int orc_antiqsort(int n, int nth, uint32_t* out_keys);
 
 /* BFMatcher::knnMatch(k=2) raw result per query: (train idx, dist) x 2, -1 when absent */
 int orc_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx2, int32_t* dist2);

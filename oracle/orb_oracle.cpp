@@ -26,6 +26,8 @@ inline int cv_ceil(double v) { int i = (int)v; return i + (i < v); }
 struct KeyPoint {  // field order of cv::KeyPoint
     float x, y, size, angle, response;
     int octave;
+    int class_id;  // cv::KeyPoint::class_id (-1 from FAST); here: the level's raster index, carried
+                   // along by nth_element / partition so the per-stage dumps can name the order
 };
 
 struct Img {
@@ -219,7 +221,7 @@ std::vector<KeyPoint> fast_nms(const Img& im, int threshold) {
                     if (!dx && !dy) continue;
                     if (!(s > score[(size_t)(y + dy) * W + x + dx])) { keep = false; break; }
                 }
-            if (keep) out.push_back(KeyPoint{(float)x, (float)y, 7.f, -1.f, (float)s, 0});
+            if (keep) out.push_back(KeyPoint{(float)x, (float)y, 7.f, -1.f, (float)s, 0, -1});
         }
     return out;
 }
@@ -424,6 +426,57 @@ void build_pyramid(const uint8_t* img, int w, int h, int ch, int64_t stride, con
     for (int l = 1; l < L; ++l) resize_linear_exact(pyr[l - 1], pyr[l], g.w[l], g.h[l]);
 }
 
+// Per-level stage data of one extraction (SURVEY.md §8(c)(i) per-stage dumps).
+struct LevelStages {
+    std::vector<KeyPoint> fast;   // FAST + NMS, raster order, before runByImageBorder
+    std::vector<KeyPoint> cand;   // after runByImageBorder (raster order)
+    std::vector<float> harris;    // Harris response of every cand entry
+    std::vector<int> keep1;       // retainBest(2q) output order, as indices into cand
+    std::vector<int> fin;         // retainBest(q) output order, as indices into cand
+};
+
+// ORB_Impl::detectAndCompute's keypoint part (computeKeyPoints): FAST -> runByImageBorder ->
+// retainBest(2 q_l) per level -> Harris -> retainBest(q_l) per level -> IC angle -> scaling.
+// Fills st (when non-null) with every level's intermediate lists.
+std::vector<KeyPoint> compute_keypoints(const std::vector<Img>& pyr, const Geometry& g, const OrbParams& P,
+                                        int order, std::vector<LevelStages>* st) {
+    const int n_levels = (int)pyr.size();
+    const auto q = quotas(P.n_features, P.scale_factor, n_levels);
+    if (st) st->assign(n_levels, LevelStages{});
+    std::vector<KeyPoint> all;
+    std::vector<int> counters(n_levels);
+    for (int l = 0; l < n_levels; ++l) {
+        auto kps = fast_nms(pyr[l], P.fast_threshold);
+        if (st) (*st)[l].fast = kps;
+        run_by_image_border(kps, pyr[l].w, pyr[l].h, P.edge_threshold);
+        for (size_t i = 0; i < kps.size(); ++i) kps[i].class_id = (int)i;
+        if (st) {
+            (*st)[l].cand = kps;
+            for (auto& k : kps) (*st)[l].harris.push_back(harris(pyr[l], cv_roundf(k.x), cv_roundf(k.y)));
+        }
+        retain_best(kps, 2 * q[l], order);
+        counters[l] = (int)kps.size();
+        for (auto& k : kps) { k.octave = l; k.size = 31 * g.scale[l]; }
+        if (st) for (auto& k : kps) (*st)[l].keep1.push_back(k.class_id);
+        all.insert(all.end(), kps.begin(), kps.end());
+    }
+    if (all.empty()) return all;
+    for (auto& k : all) k.response = harris(pyr[k.octave], cv_roundf(k.x), cv_roundf(k.y));
+    std::vector<KeyPoint> sel;
+    size_t off = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        std::vector<KeyPoint> kps(all.begin() + off, all.begin() + off + counters[l]);
+        off += counters[l];
+        retain_best(kps, q[l], order);
+        if (st) for (auto& k : kps) (*st)[l].fin.push_back(k.class_id);
+        sel.insert(sel.end(), kps.begin(), kps.end());
+    }
+    const auto umax = make_umax(15);
+    for (auto& k : sel) k.angle = ic_angle(pyr[k.octave], cv_roundf(k.x), cv_roundf(k.y), umax);
+    for (auto& k : sel) { const float s = g.scale[k.octave]; k.x *= s; k.y *= s; }
+    return sel;
+}
+
 }  // namespace
 
 extern "C" {
@@ -507,35 +560,10 @@ int orc_orb_extract(const uint8_t* img, int w, int h, int channels, int64_t stri
     const Geometry g = level_geometry(w, h, scale_factor, n_levels);
     std::vector<Img> pyr;
     build_pyramid(img, w, h, channels, stride, g, pyr);
-    const auto q = quotas(n_features, scale_factor, n_levels);
-
-    // computeKeyPoints: FAST -> runByImageBorder -> retainBest(2 q_l) per level
-    std::vector<KeyPoint> all;
-    std::vector<int> counters(n_levels);
-    for (int l = 0; l < n_levels; ++l) {
-        auto kps = fast_nms(pyr[l], P.fast_threshold);
-        run_by_image_border(kps, pyr[l].w, pyr[l].h, P.edge_threshold);
-        retain_best(kps, 2 * q[l], order);
-        counters[l] = (int)kps.size();
-        for (auto& k : kps) { k.octave = l; k.size = 31 * g.scale[l]; }
-        all.insert(all.end(), kps.begin(), kps.end());
-    }
-    if (all.empty()) return 0;
-    for (auto& k : all) k.response = harris(pyr[k.octave], cv_roundf(k.x), cv_roundf(k.y));
-    std::vector<KeyPoint> sel;
-    size_t off = 0;
-    for (int l = 0; l < n_levels; ++l) {
-        std::vector<KeyPoint> kps(all.begin() + off, all.begin() + off + counters[l]);
-        off += counters[l];
-        retain_best(kps, q[l], order);
-        sel.insert(sel.end(), kps.begin(), kps.end());
-    }
-    const auto umax = make_umax(15);
-    for (auto& k : sel) k.angle = ic_angle(pyr[k.octave], cv_roundf(k.x), cv_roundf(k.y), umax);
-    for (auto& k : sel) { const float s = g.scale[k.octave]; k.x *= s; k.y *= s; }
-
+    const std::vector<KeyPoint> sel = compute_keypoints(pyr, g, P, order, nullptr);
     const int n = (int)sel.size();
     *n_out = n;
+    if (n == 0) return 0;
     if (n > cap) return -1;
 
     // computeOrbDescriptors on the blurred levels (WTA_K 2, bit_pattern_31_).
@@ -569,6 +597,86 @@ int orc_orb_extract(const uint8_t* img, int w, int h, int channels, int64_t stri
         out_kp[i].x = k.x; out_kp[i].y = k.y; out_kp[i].response = k.response;
         out_kp[i].angle = k.angle; out_kp[i].octave = k.octave;
     }
+    return 0;
+}
+
+int orc_orb_stages(const uint8_t* img, int w, int h, int channels, int64_t stride, int n_features,
+                   float scale_factor, int n_levels, int fast_threshold, int order, int32_t* counts,
+                   int32_t* fast_xys, float* cand, int32_t* keep1, int32_t* fin, int64_t cap) {
+    for (int i = 0; i < 4 * n_levels; ++i) counts[i] = 0;
+    if (!img || w <= 0 || h <= 0 || n_levels <= 0) return 0;
+    OrbParams P;
+    P.n_features = n_features; P.scale_factor = scale_factor; P.n_levels = n_levels;
+    P.fast_threshold = fast_threshold;
+    const Geometry g = level_geometry(w, h, scale_factor, n_levels);
+    std::vector<Img> pyr;
+    build_pyramid(img, w, h, channels, stride, g, pyr);
+    std::vector<LevelStages> st;
+    compute_keypoints(pyr, g, P, order, &st);
+    int64_t of = 0, oc = 0, o1 = 0, o2 = 0;
+    for (int l = 0; l < n_levels; ++l) {
+        const LevelStages& s = st[l];
+        counts[4 * l] = (int)s.fast.size();
+        counts[4 * l + 1] = (int)s.cand.size();
+        counts[4 * l + 2] = (int)s.keep1.size();
+        counts[4 * l + 3] = (int)s.fin.size();
+        if (of + (int64_t)s.fast.size() > cap || oc + (int64_t)s.cand.size() > cap ||
+            o1 + (int64_t)s.keep1.size() > cap || o2 + (int64_t)s.fin.size() > cap)
+            return -1;
+        for (const auto& k : s.fast) {
+            fast_xys[3 * of] = (int)k.x; fast_xys[3 * of + 1] = (int)k.y; fast_xys[3 * of + 2] = (int)k.response;
+            ++of;
+        }
+        for (size_t i = 0; i < s.cand.size(); ++i) {
+            cand[4 * oc] = s.cand[i].x; cand[4 * oc + 1] = s.cand[i].y;
+            cand[4 * oc + 2] = s.cand[i].response; cand[4 * oc + 3] = s.harris[i];
+            ++oc;
+        }
+        for (int v : s.keep1) keep1[o1++] = v;
+        for (int v : s.fin) fin[o2++] = v;
+    }
+    return 0;
+}
+
+int orc_retain_best_keys(const uint32_t* keys, int n, int npts, int32_t* out_idx, int* n_out) {
+    struct E { uint32_t key; int32_t idx; };
+    std::vector<E> a(n > 0 ? n : 0);
+    for (int i = 0; i < n; ++i) a[i] = E{keys[i], i};
+    int kept = n;
+    if (npts >= 0 && n > npts) {
+        if (npts == 0) {
+            kept = 0;
+        } else {
+            auto gt = [](const E& x, const E& y) { return x.key > y.key; };
+            std::nth_element(a.begin(), a.begin() + npts - 1, a.end(), gt);
+            const uint32_t thr = a[npts - 1].key;
+            kept = (int)(std::partition(a.begin() + npts, a.end(), [thr](const E& x) { return x.key >= thr; }) -
+                         a.begin());
+        }
+    }
+    for (int i = 0; i < kept; ++i) out_idx[i] = a[i].idx;
+    *n_out = kept;
+    return 0;
+}
+
+int orc_antiqsort(int n, int nth, uint32_t* out_keys) {
+    if (n <= 0 || nth < 0 || nth >= n) return -1;
+    std::vector<int> val(n, n - 1);  // every item starts as "gas" (= n - 1)
+    const int gas = n - 1;
+    int nsolid = 0, candidate = 0;
+    std::vector<int> ptr(n);
+    for (int i = 0; i < n; ++i) ptr[i] = i;
+    auto greater = [&](int x, int y) {  // McIlroy's adversary, as the comparator of a descending select
+        if (val[x] == gas && val[y] == gas) {
+            if (x == candidate) val[x] = nsolid++;
+            else val[y] = nsolid++;
+        }
+        if (val[x] == gas) candidate = x;
+        else if (val[y] == gas) candidate = y;
+        return val[x] > val[y];
+    };
+    std::nth_element(ptr.begin(), ptr.begin() + nth, ptr.end(), greater);
+    for (int i = 0; i < n; ++i) out_keys[i] = (uint32_t)val[i];
     return 0;
 }
 

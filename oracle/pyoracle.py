@@ -122,7 +122,7 @@ def blur_level(level):
 
 
 def orb_extract(img, n_features=1000, scale=1.2, levels=8, fast_threshold=20,
-                order=ORDER_RASTER, pattern=None):
+                order=ORDER_STL, pattern=None):
     img = np.ascontiguousarray(img)
     h, w = img.shape[:2]
     ch = 1 if img.ndim == 2 else img.shape[2]
@@ -136,6 +136,48 @@ def orb_extract(img, n_features=1000, scale=1.2, levels=8, fast_threshold=20,
                                _p(desc), cap, C.byref(n))
     assert rc == 0, rc
     return kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def orb_stages(img, n_features=1000, scale=1.2, levels=8, fast_threshold=20, order=ORDER_STL):
+    """Per-level stage lists of one extraction (orc_orb_stages): a list of dicts with keys
+    fast (x, y, score; before runByImageBorder), cand (x, y, score, harris; raster order after the
+    border), keep1 / fin (indices into cand: the two retainBest outputs, in output order)."""
+    img = np.ascontiguousarray(img)
+    h, w = img.shape[:2]
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    cap = w * h // 2 + 64
+    counts = np.zeros(4 * levels, np.int32)
+    fast = np.zeros((cap, 3), np.int32)
+    cand = np.zeros((cap, 4), np.float32)
+    k1 = np.zeros(cap, np.int32)
+    fin = np.zeros(cap, np.int32)
+    rc = lib().orc_orb_stages(_p(img), w, h, ch, C.c_int64(img.strides[0]), n_features, C.c_float(scale), levels,
+                              fast_threshold, order, _p(counts), _p(fast), _p(cand), _p(k1), _p(fin), C.c_int64(cap))
+    assert rc == 0, rc
+    out, o = [], np.zeros(4, np.int64)
+    for l in range(levels):
+        c = counts[4 * l:4 * l + 4]
+        out.append(dict(fast=fast[o[0]:o[0] + c[0]].copy(), cand=cand[o[1]:o[1] + c[1]].copy(),
+                        keep1=k1[o[2]:o[2] + c[2]].copy(), fin=fin[o[3]:o[3] + c[3]].copy()))
+        o += c
+    return out
+
+
+def retain_best_keys(keys, npts):
+    """retainBest over bare u32 keys with the real std::nth_element / std::partition: kept indices
+    in the library's order."""
+    keys = np.ascontiguousarray(keys, np.uint32)
+    out = np.zeros(max(len(keys), 1), np.int32)
+    n = C.c_int(0)
+    assert lib().orc_retain_best_keys(_p(keys), len(keys), int(npts), _p(out), C.byref(n)) == 0
+    return out[:n.value].copy()
+
+
+def antiqsort(n, nth):
+    """McIlroy's adversary against std::nth_element(.., nth, .., greater): killer keys (u32)."""
+    out = np.zeros(n, np.uint32)
+    assert lib().orc_antiqsort(int(n), int(nth), _p(out)) == 0
+    return out
 
 
 def knn2(q, t):

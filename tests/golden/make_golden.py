@@ -35,6 +35,31 @@ ORB_CASES = [
 ]
 
 
+# ---- per-stage ORB cases: (name, seed, h, w, channels, n_features)
+STAGE_CASES = [
+    ("vga_bgr_n2000", 0x5EED0010, 480, 640, 3, 2000),
+    ("qqvga_bgr_n500", 0x5EED0011, 120, 160, 3, 500),
+]
+
+
+def orb_stage_arrays(img, n):
+    """The per-level stage lists of the oracle as flat arrays (key -> array)."""
+    out = {}
+    pyr = O.pyramid(img)
+    st = O.orb_stages(img, n)
+    kps, desc = O.orb_extract(img, n)
+    for l, s in enumerate(st):
+        out[f"L{l}_pyr_sha"] = np.frombuffer(sha(pyr[l]).encode(), np.uint8)
+        out[f"L{l}_blur_sha"] = np.frombuffer(sha(O.blur_level(pyr[l])).encode(), np.uint8)
+        out[f"L{l}_fast"] = s["fast"]
+        out[f"L{l}_cand"] = s["cand"]
+        out[f"L{l}_keep1"] = s["keep1"]
+        out[f"L{l}_fin"] = s["fin"]
+    out["kp"] = kps
+    out["desc"] = desc
+    return out
+
+
 def orb_input(seed, h, w, ch):
     f = synth.make_frames(seed, 1, h, w)[0]
     if ch == 1:
@@ -68,11 +93,24 @@ def main():
     out = {}
     for name, seed, h, w, ch, n in ORB_CASES:
         img = orb_input(seed, h, w, ch)
-        kps, desc = O.orb_extract(img, n, order=O.ORDER_RASTER)
+        # the reference's order: OpenCV retainBest's libstdc++ nth_element + partition permutation
+        kps, desc = O.orb_extract(img, n, order=O.ORDER_STL)
         out[f"orb_{name}_sha"] = np.frombuffer(sha(img).encode(), np.uint8)
         out[f"orb_{name}_kp"] = kps
         out[f"orb_{name}_desc"] = desc
+        # the same keypoint set per level in raster order (VX_ORDER_RASTER, opt-in)
+        kr, dr = O.orb_extract(img, n, order=O.ORDER_RASTER)
+        out[f"orb_{name}_kp_raster"] = kr
+        out[f"orb_{name}_desc_raster"] = dr
     np.savez_compressed(os.path.join(HERE, "orb_golden.npz"), **out)
+
+    out = {}
+    for name, seed, h, w, ch, n in STAGE_CASES:
+        img = orb_input(seed, h, w, ch)
+        out[f"{name}_sha"] = np.frombuffer(sha(img).encode(), np.uint8)
+        for k, v in orb_stage_arrays(img, n).items():
+            out[f"{name}_{k}"] = v
+    np.savez_compressed(os.path.join(HERE, "orb_stages_golden.npz"), **out)
 
     q, t = match_input(77, 512)
     idx, dist = O.knn2(q, t)
@@ -91,7 +129,7 @@ def main():
         out[f"ba_{name}_obs"] = np.array(st.obs[:st.iterations], np.int64)
         out[f"ba_{name}_margin"] = np.array([st.gate_margin])
     np.savez_compressed(os.path.join(HERE, "ba_golden.npz"), **out)
-    for f in ("orb_golden.npz", "match_golden.npz", "ba_golden.npz"):
+    for f in ("orb_golden.npz", "orb_stages_golden.npz", "match_golden.npz", "ba_golden.npz"):
         print(f, os.path.getsize(os.path.join(HERE, f)))
 
 

@@ -70,7 +70,7 @@ def test_adapter_extract_and_match(driver, oracle, tmp_path):
         pos = np.fromfile(os.path.join(tmp_path, f"f{i}.pos"), np.float64).reshape(-1, 2)
         resp = np.fromfile(os.path.join(tmp_path, f"f{i}.resp"), np.float32)
         desc = np.fromfile(os.path.join(tmp_path, f"f{i}.desc"), np.uint8).reshape(-1, 32)
-        kc, dc = oracle.orb_extract(f, 1500, order=oracle.ORDER_RASTER)
+        kc, dc = oracle.orb_extract(f, 1500)
         assert n == len(kc)
         # Feature.position = Eigen::Vector2d(kp.pt.x, kp.pt.y), response = kp.response
         assert np.array_equal(pos[:, 0], kc["x"].astype(np.float64))
@@ -105,7 +105,7 @@ def test_adapter_extract_and_match_batch(driver, oracle, tmp_path):
         pos = np.fromfile(os.path.join(tmp_path, f"f{i}.pos"), np.float64).reshape(-1, 2)
         resp = np.fromfile(os.path.join(tmp_path, f"f{i}.resp"), np.float32)
         desc = np.fromfile(os.path.join(tmp_path, f"f{i}.desc"), np.uint8).reshape(-1, 32)
-        kc, dc = oracle.orb_extract(f, 1200, order=oracle.ORDER_RASTER)
+        kc, dc = oracle.orb_extract(f, 1200)
         assert np.array_equal(pos[:, 0], kc["x"].astype(np.float64))
         assert np.array_equal(pos[:, 1], kc["y"].astype(np.float64))
         assert np.array_equal(resp, kc["response"]) and np.array_equal(desc, dc)

@@ -39,7 +39,7 @@ def test_orb_batch_matches_oracle(ctx, oracle, b, h, w, n, gray):
     out = ctx.orb_extract_batch(np.stack(frames), p, bank=b % 2)
     assert len(out) == b
     for f in range(b):
-        ref = oracle.orb_extract(frames[f], n, order=oracle.ORDER_RASTER) if f < 3 else ctx.orb_extract(frames[f], p)
+        ref = oracle.orb_extract(frames[f], n) if f < 3 else ctx.orb_extract(frames[f], p)
         _eq(out[f], ref)
 
 
@@ -56,7 +56,7 @@ def test_orb_batch_fused_pyramid_with_grid_share(oracle, b):
         p = vxslam.default_orb_params(n_features=2000)
         out = c.orb_extract_batch(np.stack(frames), p)
         for f in range(b):
-            _eq(out[f], oracle.orb_extract(frames[f], 2000, order=oracle.ORDER_RASTER))
+            _eq(out[f], oracle.orb_extract(frames[f], 2000))
     finally:
         c.close()
 
@@ -79,7 +79,7 @@ def test_orb_batch_padded_strides_and_blank_frame(ctx, oracle):
     ctx.orb_extract_batch_async(d.data_ptr(), 3, d.stride(0), w, h, 3, d.stride(1), 0, p)
     for f in range(3):
         got = ctx.orb_batch_fetch(0, f)
-        _eq(got, oracle.orb_extract(frames[f], n, order=oracle.ORDER_RASTER))
+        _eq(got, oracle.orb_extract(frames[f], n))
     assert len(ctx.orb_batch_fetch(0, 1)[0]) == 0
 
 
@@ -91,7 +91,7 @@ def test_orb_batch_interleaved_with_single_frames(ctx, oracle):
     h, w, n = 240, 320, 500
     frames = synth.make_frames(0xBA7E0, 6, h, w)
     p = vxslam.default_orb_params(n_features=n)
-    ref = [oracle.orb_extract(f, n, order=oracle.ORDER_RASTER) for f in frames[:2]]
+    ref = [oracle.orb_extract(f, n) for f in frames[:2]]
     d = _device_stack(frames)
     for _ in range(3):  # eager, capture, replay
         ctx.orb_extract_async(d[0].data_ptr(), w, h, 3, d.stride(1), 0, p)
@@ -147,7 +147,7 @@ def test_batch_maximum_sizes(ctx, oracle):
     p = vxslam.default_orb_params(n_features=n)
     out = ctx.orb_extract_batch(np.stack(frames), p, bank=0)
     for f in (0, 5, 17, 63):
-        _eq(out[f], oracle.orb_extract(frames[f], n, order=oracle.ORDER_RASTER))
+        _eq(out[f], oracle.orb_extract(frames[f], n))
     for f in range(64):
         _eq(out[f], ctx.orb_extract(frames[f], p))
     pairs = [(ctx.batch_device(0, 2 * i), ctx.batch_device(0, 2 * i + 1)) for i in range(16)]

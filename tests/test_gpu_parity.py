@@ -55,7 +55,7 @@ def test_orb_random_frames(ctx, oracle, seed, h, w, n):
 
     img = synth.make_frames(seed, 1, h, w)[0]
     kps, desc = ctx.orb_extract(img, _orb_params(vxslam, n))
-    kc, dc = oracle.orb_extract(img, n, order=oracle.ORDER_RASTER)
+    kc, dc = oracle.orb_extract(img, n)
     _assert_orb_equal(kps, desc, kc, dc)
 
 
@@ -74,14 +74,14 @@ def test_orb_edge_inputs(ctx, oracle):
     chk = (((yy // 7) + (xx // 9)) % 2 * 120 + 60).astype(np.uint8)
     for img in (chk, np.ascontiguousarray(chk[:, ::-1])):
         k, d = ctx.orb_extract(img, p)
-        kc, dc = oracle.orb_extract(img, 500, order=oracle.ORDER_RASTER)
+        kc, dc = oracle.orb_extract(img, 500)
         _assert_orb_equal(k, d, kc, dc)
     # strided input (row_stride > width * channels): a view into a wider buffer
     big = synth.make_frames(21, 1, 480, 700)[0]
     view = big[:, 20:660]
     assert not view.flags["C_CONTIGUOUS"]
     k, d = ctx.orb_extract(np.ascontiguousarray(view), p)
-    kc, dc = oracle.orb_extract(np.ascontiguousarray(view), 500, order=oracle.ORDER_RASTER)
+    kc, dc = oracle.orb_extract(np.ascontiguousarray(view), 500)
     _assert_orb_equal(k, d, kc, dc)
 
 
@@ -96,7 +96,7 @@ def test_orb_grid_share(oracle, share):
         for seed, h, w, n in [(31, 480, 640, 2000), (32, 960, 1280, 4000)]:
             f = synth.make_frames(seed, 1, h, w)[0]
             k, d = c.orb_extract(f, vxslam.default_orb_params(n_features=n))
-            kc, dc = oracle.orb_extract(f, n, order=oracle.ORDER_RASTER)
+            kc, dc = oracle.orb_extract(f, n)
             assert np.array_equal(k, kc) and np.array_equal(d, dc)
         with pytest.raises(Exception):
             c.set_grid_share(0.0)
@@ -170,8 +170,8 @@ def test_slot_pipeline_matches_sync(ctx, oracle):
     m = ctx.match_fetch()
     k0, d0 = ctx.orb_fetch(0)
     k1, d1 = ctx.orb_fetch(1)
-    kc0, dc0 = oracle.orb_extract(frames[0], 2000, order=oracle.ORDER_RASTER)
-    kc1, dc1 = oracle.orb_extract(frames[1], 2000, order=oracle.ORDER_RASTER)
+    kc0, dc0 = oracle.orb_extract(frames[0], 2000)
+    kc1, dc1 = oracle.orb_extract(frames[1], 2000)
     _assert_orb_equal(k0, d0, kc0, dc0)
     _assert_orb_equal(k1, d1, kc1, dc1)
     assert np.array_equal(m, oracle.match(dc0, dc1))
@@ -336,8 +336,8 @@ def test_frontend_backend_contexts_overlap(ctx, oracle):
         mg = m.copy()
         st_g = plan.fetch(mg)
         got = mctx.match_fetch()
-        _, dc4 = oracle.orb_extract(frames[n - 2], 2000, order=oracle.ORDER_RASTER)
-        kc5, dc5 = oracle.orb_extract(frames[n - 1], 2000, order=oracle.ORDER_RASTER)
+        _, dc4 = oracle.orb_extract(frames[n - 2], 2000)
+        kc5, dc5 = oracle.orb_extract(frames[n - 1], 2000)
         _assert_orb_equal(*desc[n - 1], kc5, dc5)
         assert np.array_equal(desc[n - 2][1], dc4)
         assert np.array_equal(got, oracle.match(dc4, dc5))
@@ -365,7 +365,7 @@ def test_graph_replay_matches_eager(ctx, oracle):
         frames = synth.make_frames(0x5EED0077, 2, 480, 640)
         d = torch.from_numpy(frames).cuda()
         p = vxslam.default_orb_params(n_features=2000)
-        kc = [oracle.orb_extract(frames[i], 2000, order=oracle.ORDER_RASTER) for i in range(2)]
+        kc = [oracle.orb_extract(frames[i], 2000) for i in range(2)]
         nk, nl, _ = synth.ba_config("C2")
         m = synth.make_ba_map(91, nk, nl)
         plan = c.ba_plan(m, vxslam.default_ba_options(window=nk))

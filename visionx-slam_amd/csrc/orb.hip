@@ -988,6 +988,444 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
     VX_KT(15);
 }
 
+// ------------------------------------------------------------------------------ select, libstdc++ order
+// OpenCV's KeyPointsFilter::retainBest leaves the keypoints in the order std::nth_element +
+// std::partition produce (ORB calls it twice per level: by FAST score, then by Harris; SURVEY.md
+// App. A.3), and ORBExtractor::Extract numbers Frame::Features() in that order
+// (core/feature/orb_extractor.cpp:13-24).  k_select_stl reproduces libstdc++'s permutation
+// exactly: introselect (median-of-3 moved to the front, unguarded Hoare partition, depth limit
+// 2*lg(n) -> heap select, insertion sort of the last <= 3), then the bidirectional std::partition.
+//
+// One Hoare partition is done as ONE parallel pass instead of two scanning pointers: with pivot
+// value P, the left scanner stops at every x with !(x > P) ("L"), the right one at every x with
+// !(P > x) ("R"); swap k exchanges the k-th L from the left with the k-th R from the right for
+// k < K, K = max over x of min(#L before x, #R at or after x), and the returned cut is
+// min(L[K], R[K-1]).  std::partition is the same pairing with complementary predicates.  That
+// formulation is checked against the real STL (random, tie-heavy, sorted and McIlroy-adversarial
+// inputs reaching the heap select) by tests/cpp/stl_select_model.cpp.
+//
+// A pass over a range longer than kStlMulti runs on all 16 waves (4 barriers); shorter ranges,
+// most of the passes, run on wave 0 alone without barriers.  Elements are u32 (FAST score << 24 |
+// raster index) for the first retainBest and u64 (order-preserving Harris key << 32 | raster
+// index) for the second; they live in LDS when they fit, in the level's global scratch otherwise.
+constexpr int kStlNT = 1024;
+constexpr int kStlWaves = kStlNT / 64;
+constexpr int kStlMulti = 1024;
+constexpr int kStlLds = 96 * 1024;  // dynamic LDS of k_select_stl
+
+__device__ __forceinline__ unsigned sel_key(unsigned v) { return v >> 24; }
+__device__ __forceinline__ unsigned sel_key(unsigned long long v) { return (unsigned)(v >> 32); }
+
+// order-preserving key of a Harris response (-0 and +0 compare equal as floats: one key)
+__device__ __forceinline__ unsigned harris_key(float f) {
+    unsigned u = __float_as_uint(f);
+    if ((u << 1) == 0u) u = 0u;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ int lane_rank(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
+template <int NW>
+__device__ __forceinline__ void team_sync() {
+    if (NW > 1) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// One partition pass over [f0, l) by the first NW waves of the workgroup (NW = 1: wave 0 only).
+// m >= 0: position m is read as `oldf` (the median-of-3 swap with the pivot slot f0 - 1, which
+// receives pv; both written here).  Returns the cut; n_r = number of R elements.
+// s: LDS scratch of >= 3 * NW + 2 ints.
+template <int NW, class T, class IsL, class IsR>
+__device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f0, int l,
+                                         int m, T oldf, T pv, IsL isl, IsR isr, int* s, int& n_r) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nb = (l - f0 + 63) >> 6;
+    const int b0 = w * nb / NW, b1 = (w + 1) * nb / NW;
+    auto rd = [&](int p) -> T { return p == m ? oldf : A[p]; };
+    int cl = 0, cr = 0;
+    for (int b = b0; b < b1; ++b) {
+        const int p = f0 + 64 * b + lane;
+        const bool in = p < l;
+        const T v = in ? rd(p) : T(0);
+        cl += __popcll(__ballot(in && isl(v)));
+        cr += __popcll(__ballot(in && isr(v)));
+    }
+    int pl = 0, pr = 0, nl = cl, nr = cr;
+    if (NW > 1) {
+        if (lane == 0) {
+            s[2 * w] = cl;
+            s[2 * w + 1] = cr;
+        }
+        __syncthreads();
+        nl = nr = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int x = s[2 * i], y = s[2 * i + 1];
+            pl += i < w ? x : 0;
+            pr += i < w ? y : 0;
+            nl += x;
+            nr += y;
+        }
+    }
+    // K = max over positions x of min(#L in [f0, x), #R in [x, l))
+    int km = 0;
+    {
+        int ql = pl, qr = pr;
+        for (int b = b0; b < b1; ++b) {
+            const int p = f0 + 64 * b + lane;
+            const bool in = p < l;
+            const T v = in ? rd(p) : T(0);
+            const unsigned long long ml = __ballot(in && isl(v)), mr = __ballot(in && isr(v));
+            if (in) km = max(km, min(ql + lane_rank(ml), nr - (qr + lane_rank(mr))));
+            ql += __popcll(ml);
+            qr += __popcll(mr);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) km = max(km, __shfl_xor(km, o, 64));
+    if (NW > 1) {
+        if (lane == 0) s[2 * NW + w] = km;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NW; ++i) km = max(km, s[2 * NW + i]);
+    }
+    const int K = km;
+    // mailboxes: the k-th L and the k-th R from the right (k < K); the cut's two candidates
+    {
+        int ql = pl, qr = pr;
+        for (int b = b0; b < b1; ++b) {
+            const int p = f0 + 64 * b + lane;
+            const bool in = p < l;
+            const T v = in ? rd(p) : T(0);
+            const bool il = in && isl(v), ir = in && isr(v);
+            const unsigned long long ml = __ballot(il), mr = __ballot(ir);
+            const int lb = ql + lane_rank(ml), rr = nr - 1 - (qr + lane_rank(mr));
+            if (il) {
+                if (lb < K) bl[lb] = v;
+                else if (lb == K) s[3 * NW] = p;
+            }
+            if (ir) {
+                if (rr < K) br[rr] = v;
+                if (rr == K - 1) s[3 * NW + 1] = p;
+            }
+            ql += __popcll(ml);
+            qr += __popcll(mr);
+        }
+    }
+    team_sync<NW>();
+    {
+        int ql = pl, qr = pr;
+        for (int b = b0; b < b1; ++b) {
+            const int p = f0 + 64 * b + lane;
+            const bool in = p < l;
+            const T v = in ? rd(p) : T(0);
+            const bool il = in && isl(v), ir = in && isr(v);
+            const unsigned long long ml = __ballot(il), mr = __ballot(ir);
+            const int lb = ql + lane_rank(ml), rr = nr - 1 - (qr + lane_rank(mr));
+            if (il && lb < K) A[p] = br[lb];
+            else if (ir && rr < K) A[p] = bl[rr];
+            else if (p == m) A[p] = oldf;
+            ql += __popcll(ml);
+            qr += __popcll(mr);
+        }
+        if (m >= 0 && threadIdx.x == 0) A[f0 - 1] = pv;
+    }
+    team_sync<NW>();
+    n_r = nr;
+    int cut = INT_MAX;
+    if (K < nl) cut = s[3 * NW];
+    if (K > 0) cut = min(cut, s[3 * NW + 1]);
+    return cut;
+}
+
+// __unguarded_partition_pivot(first = f, last = l) as one team pass; returns the cut
+template <int NW, class T>
+__device__ __forceinline__ int pivot_pass(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f, int l,
+                                          int* s) {
+    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+    const T vf = A[f], va = A[a], vb = A[b], vc = A[c];
+    const unsigned ka = sel_key(va), kb = sel_key(vb), kc = sel_key(vc);
+    int m;  // __move_median_to_first(f, a, b, c, greater)
+    if (ka > kb) m = kb > kc ? b : ka > kc ? c : a;
+    else m = ka > kc ? a : kb > kc ? c : b;
+    const T pv = m == a ? va : m == b ? vb : vc;
+    const unsigned P = sel_key(pv);
+    int nr;
+    return team_pass<NW>(A, bl, br, f + 1, l, m, vf, pv, [P](T v) { return sel_key(v) <= P; },
+                         [P](T v) { return sel_key(v) >= P; }, s, nr);
+}
+
+// libstdc++ __adjust_heap / __push_heap / __make_heap / __heap_select with comp = greater (one lane)
+template <class T>
+__device__ void stl_adjust_heap(T* a, int hole, int len, T v) {
+    const int top = hole;
+    int child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (sel_key(a[child]) > sel_key(a[child - 1])) --child;
+        a[hole] = a[child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        a[hole] = a[child - 1];
+        hole = child - 1;
+    }
+    int parent = (hole - 1) / 2;
+    while (hole > top && sel_key(a[parent]) > sel_key(v)) {
+        a[hole] = a[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    a[hole] = v;
+}
+
+template <class T>
+__device__ void stl_heap_select(T* a, int mid, int last) {
+    if (mid >= 2)
+        for (int parent = (mid - 2) / 2;; --parent) {
+            stl_adjust_heap(a, parent, mid, a[parent]);
+            if (parent == 0) break;
+        }
+    for (int i = mid; i < last; ++i)
+        if (sel_key(a[i]) > sel_key(a[0])) {
+            const T v = a[i];
+            a[i] = a[0];
+            stl_adjust_heap(a, 0, mid, v);
+        }
+}
+
+template <class T>
+__device__ void stl_insertion_sort(T* A, int f, int l) {
+    for (int i = f + 1; i < l; ++i) {
+        const T v = A[i];
+        if (sel_key(v) > sel_key(A[f])) {
+            for (int j = i; j > f; --j) A[j] = A[j - 1];
+            A[f] = v;
+        } else {
+            int j = i;
+            while (sel_key(v) > sel_key(A[j - 1])) {
+                A[j] = A[j - 1];
+                --j;
+            }
+            A[j] = v;
+        }
+    }
+}
+
+// std::nth_element(A, A + nth, A + n, greater); every thread of the workgroup calls it
+template <class T>
+__device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int n,
+                                                int nth, int* s) {
+    if (n <= 0 || nth >= n) return;
+    int f = 0, l = n, depth = 2 * (31 - __clz(n));
+    bool heap = false;
+    while (l - f > kStlMulti) {
+        if (depth == 0) {
+            heap = true;
+            break;
+        }
+        --depth;
+        const int cut = pivot_pass<kStlWaves>(A, bl, br, f, l, s);
+        if (cut <= nth) f = cut;
+        else l = cut;
+    }
+    if ((threadIdx.x >> 6) == 0) {
+        while (!heap && l - f > 3) {
+            if (depth == 0) {
+                heap = true;
+                break;
+            }
+            --depth;
+            const int cut = pivot_pass<1>(A, bl, br, f, l, s);
+            if (cut <= nth) f = cut;
+            else l = cut;
+        }
+        if (threadIdx.x == 0) {
+            if (heap) {
+                stl_heap_select(A + f, nth + 1 - f, l - f);
+                const T t = A[f];
+                A[f] = A[nth];
+                A[nth] = t;
+            } else {
+                stl_insertion_sort(A, f, l);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// KeyPointsFilter::retainBest(A[0..size), npts): returns the kept length; every thread calls it
+template <class T>
+__device__ __forceinline__ int stl_retain_best(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int size,
+                                               int npts, int* s) {
+    if (size <= npts) return size;
+    if (npts <= 0) return 0;
+    stl_nth_element(A, bl, br, size, npts - 1, s);
+    const unsigned thr = sel_key(A[npts - 1]);
+    auto isl = [thr](T v) { return sel_key(v) < thr; };
+    auto isr = [thr](T v) { return sel_key(v) >= thr; };
+    int nr = 0;
+    if (size - npts > kStlMulti) {
+        team_pass<kStlWaves>(A, bl, br, npts, size, -1, T(0), T(0), isl, isr, s, nr);
+    } else {
+        if ((threadIdx.x >> 6) == 0) {
+            team_pass<1>(A, bl, br, npts, size, -1, T(0), T(0), isl, isr, s, nr);
+            if (threadIdx.x == 0) s[3 * kStlWaves + 2] = nr;
+        }
+        __syncthreads();
+        nr = s[3 * kStlWaves + 2];
+    }
+    return npts + nr;
+}
+
+// One workgroup per (level, frame): retainBest(2q) by FAST score and retainBest(q) by Harris in
+// libstdc++ order.  Staging of level l: kept[0..cap) = every border-passing NMS corner in raster
+// order, fin[0..cap) = the result, then 32 B x cap of selection scratch.
+// dbg (test hook vx_orb_set_debug, single frame; nullptr otherwise): dbg[l] = candidates,
+// dbg[kMaxLevels + l] = retainBest(2q) survivors, then per level (at the prefix of level_cap) the
+// survivors' raster indices in output order.
+__global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict__ cand,
+                                                       const int* __restrict__ cell_count, LevelArgs a,
+                                                       CandRec* __restrict__ stage, int* __restrict__ level_count,
+                                                       int* __restrict__ dbg) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
+    __shared__ int s[3 * kStlWaves + 4];
+    __shared__ int sw[kStlWaves];
+    const int l = blockIdx.x;
+    const int tid = threadIdx.x;
+    cand += blockIdx.z * a.fs_cells * kCellCap;
+    cell_count += blockIdx.z * a.fs_cells;
+    stage += blockIdx.z * a.fs_stage;
+    level_count += blockIdx.z * kMaxLevels;
+    VX_KT(12);
+    const int ncell = a.lh[l] * a.ntx[l];
+    const long long cbase = a.cell_base[l];
+    const int cap = a.level_cap[l];
+    CandRec* kept = stage + a.stage_base[l];
+    CandRec* fin = kept + cap;
+    unsigned char* gscr = reinterpret_cast<unsigned char*>(kept + 2 * (long long)cap);
+    unsigned* gA1 = reinterpret_cast<unsigned*>(gscr);
+    const int q = a.quota[l];
+    const int k1 = 2 * q;
+    constexpr int kCap1 = (kStlLds - 64) / 8;  // pass-1 elements that fit in LDS with their mailboxes
+    unsigned* lA1 = reinterpret_cast<unsigned*>(sdyn);
+    // ---- every border-passing NMS corner in raster (cell) order: records to kept[], pass-1
+    // elements (score << 24 | raster index) to LDS (when they fit) and to the global scratch
+    const int cpt = min(kCellsPer, (ncell + kStlNT - 1) / kStlNT);
+    int n0 = 0;
+    for (int base = 0; base < ncell; base += kStlNT * cpt) {
+        const int c0 = base + tid * cpt;
+        int cnts[kCellsPer];
+        int tot = 0;
+#pragma unroll
+        for (int j = 0; j < kCellsPer; ++j) cnts[j] = (j < cpt && c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
+#pragma unroll
+        for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
+        auto rec_index = [&](int k) {
+            int j = 0, i = k;
+#pragma unroll
+            for (int jj = 0; jj < kCellsPer; ++jj)
+                if (j == jj && i >= cnts[jj]) {
+                    i -= cnts[jj];
+                    j = jj + 1;
+                }
+            return (cbase + c0 + j) * kCellCap + i;
+        };
+        CandRec rr[kRecBatch];
+#pragma unroll
+        for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? cand[rec_index(k)] : CandRec{};
+        int btot;
+        int pos = n0 + block_scan_excl<kStlNT>(tot, sw, btot);
+        auto put = [&](const CandRec& r) {
+            kept[pos] = r;
+            const unsigned e = ((unsigned)r.score << 24) | (unsigned)pos;
+            gA1[pos] = e;
+            if (pos < kCap1) lA1[pos] = e;
+            ++pos;
+        };
+#pragma unroll
+        for (int k = 0; k < kRecBatch; ++k)
+            if (k < tot) put(rr[k]);
+        for (int k = kRecBatch; k < tot; ++k) put(cand[rec_index(k)]);
+        n0 += btot;
+    }
+    __syncthreads();
+    VX_KT(13);
+    // ---- retainBest(2q) by FAST score (the pass-1 elements are u32, mailboxes of n0 / 2 + 1 each)
+    const int hb = n0 / 2 + 1;
+    int K1;
+    const bool lds1 = n0 <= kCap1;
+    if (lds1) K1 = stl_retain_best(lA1, lA1 + n0, lA1 + n0 + hb, n0, k1, s);
+    else K1 = stl_retain_best(gA1, gA1 + n0, gA1 + n0 + hb, n0, k1, s);
+    // ---- retainBest(q) by Harris over the survivors in their new order (u64 elements)
+    const long long o2 = ((long long)(n0 + 2 * hb) * 4 + 15) & ~15ll;  // bytes after the pass-1 arrays
+    const int hb2 = K1 / 2 + 1;
+    const bool lds2 = lds1 && o2 + (long long)(K1 + 2 * hb2) * 8 <= kStlLds;
+    unsigned long long* A2 = lds2 ? reinterpret_cast<unsigned long long*>(sdyn + o2)
+                                  : reinterpret_cast<unsigned long long*>(gscr + 16 * (long long)cap);
+    const unsigned* A1 = lds1 ? lA1 : gA1;
+    if (dbg) {
+        long long off = 2 * kMaxLevels;
+        for (int i = 0; i < l; ++i) off += a.level_cap[i];
+        if (tid == 0) {
+            dbg[l] = n0;
+            dbg[kMaxLevels + l] = K1;
+        }
+        for (int j = tid; j < K1; j += kStlNT) dbg[off + j] = (int)(A1[j] & 0xffffffu);
+    }
+    for (int j = tid; j < K1; j += kStlNT) {
+        const unsigned idx = A1[j] & 0xffffffu;
+        A2[j] = ((unsigned long long)harris_key(kept[idx].harris) << 32) | idx;
+    }
+    __syncthreads();
+    VX_KT(14);
+    int K2;
+    if (lds2) {  // (separate call sites: the LDS one compiles to ds_ instructions)
+        unsigned long long* L2 = reinterpret_cast<unsigned long long*>(sdyn + o2);
+        K2 = stl_retain_best(L2, L2 + K1, L2 + K1 + hb2, K1, q, s);
+    } else {
+        unsigned long long* G2 = reinterpret_cast<unsigned long long*>(gscr + 16 * (long long)cap);
+        K2 = stl_retain_best(G2, G2 + K1, G2 + K1 + hb2, K1, q, s);
+    }
+    for (int j = tid; j < K2; j += kStlNT) fin[j] = kept[(unsigned)A2[j]];
+    if (tid == 0) level_count[l] = K2;
+    VX_KT(15);
+}
+
+// Test hook (vx_test_retain_best): retainBest over caller keys through the device code above.
+template <class T>
+__device__ __forceinline__ void test_retain_body(T* A, const unsigned* __restrict__ keys, int n, int npts,
+                                                 int* __restrict__ out, int* s) {
+    const int hb = n / 2 + 1;
+    for (int i = threadIdx.x; i < n; i += kStlNT)
+        A[i] = sizeof(T) == 4 ? (T)((keys[i] << 24) | (unsigned)i) : (T)(((unsigned long long)keys[i] << 32) | (unsigned)i);
+    __syncthreads();
+    const int K = stl_retain_best(A, A + n, A + n + hb, n, npts, s);
+    for (int j = threadIdx.x; j < K; j += kStlNT) out[1 + j] = (int)(sizeof(T) == 4 ? (A[j] & 0xffffffu) : (unsigned)A[j]);
+    if (threadIdx.x == 0) out[0] = K;
+}
+
+__global__ __launch_bounds__(kStlNT) void k_test_retain(const unsigned* __restrict__ keys, int n, int npts, int wide,
+                                                        int use_lds, unsigned char* __restrict__ gscr,
+                                                        int* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
+    __shared__ int s[3 * kStlWaves + 4];
+    if (!wide) {
+        if (use_lds) test_retain_body(reinterpret_cast<unsigned*>(sdyn), keys, n, npts, out, s);
+        else test_retain_body(reinterpret_cast<unsigned*>(gscr), keys, n, npts, out, s);
+    } else {
+        if (use_lds) test_retain_body(reinterpret_cast<unsigned long long*>(sdyn), keys, n, npts, out, s);
+        else test_retain_body(reinterpret_cast<unsigned long long*>(gscr), keys, n, npts, out, s);
+    }
+}
+
 // ------------------------------------------------------------------------------ describe
 __device__ __forceinline__ float ocv_fast_atan2(float y, float x) {
     const float p1 = 0.9997878412794807f * (float)(180 / M_PI);
@@ -1411,7 +1849,8 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
         cells += (int64_t)g.lh[l] * g.ntx[l];
         g.level_cap[l] = (g.lw[l] / 2 + 1) * (g.lh[l] / 2 + 1);
         g.stage_base[l] = stg;
-        stg += 2 * (int64_t)g.level_cap[l];
+        // kept + fin (level_cap records each) + k_select_stl's scratch (32 B x level_cap + slack)
+        stg += 4 * (int64_t)g.level_cap[l] + 4;
         g.max_w = std::max(g.max_w, g.lw[l]);
     }
     g.total_tiles = tiles;
@@ -1429,6 +1868,11 @@ int orb_prepare(vx_ctx* c, const vx_orb_params* p, int w, int h) {
     VX_HIP(c, c->band_count.ensure(g.cells_total * sizeof(int)));
     VX_HIP(c, c->hist.ensure(g.L * kHistRep * 256 * sizeof(int)));
     VX_HIP(c, c->level_count.ensure(kMaxLevels * sizeof(int)));
+    if (c->orb_debug) {
+        int64_t caps = 0;
+        for (int l = 0; l < g.L; ++l) caps += g.level_cap[l];
+        VX_HIP(c, c->orb_dbg.ensure((size_t)(2 * kMaxLevels + caps) * sizeof(int)));
+    }
     for (auto& s : c->slots) {
         s.valid = false;
         VX_HIP(c, s.kp.ensure((size_t)g.out_cap * sizeof(vx_keypoint)));
@@ -1451,6 +1895,9 @@ static int orb_enqueue_frames(vx_ctx* c, const uint8_t* d_img, int channels, int
     const OrbGeometry& g = c->geo;
     LevelArgs a = level_args(g);
     a.fs_img = fs_img;
+    // test hooks (vx_orb_set_debug): the FAST list before runByImageBorder, the selection's stages
+    if (c->orb_debug & VX_ORB_DEBUG_FAST_NO_BORDER) a.edge = 3;
+    int* dbg = (c->orb_debug && nf == 1) ? c->orb_dbg.as<int>() : nullptr;
     uint8_t* pyr = c->pyr.as<uint8_t>();
     const int hist_n = g.L * kHistRep * 256;
     // the fused pyramid buys latency with redundant halo work; a batch whose fused grid would need more
@@ -1483,10 +1930,23 @@ static int orb_enqueue_frames(vx_ctx* c, const uint8_t* d_img, int channels, int
     // FAST + NMS + Harris and the GaussianBlur of every level, one launch over 64 x 16 tiles
     VX_HIP(c, launch(c, kStFast, k_fast, dim3(g.total_tiles, 1, nf), dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, a,
                      c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>(), c->blur.as<uint8_t>()));
-    VX_HIP(c, launch(c, kStSelect, k_select, dim3(g.L, 1, nf), dim3(kSelBlock), 0, c->stream,
-                     (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(),
-                     (const int*)c->hist.as<int>(), a, c->stage.as<CandRec>(), c->level_count.as<int>()));
-    {
+    if (c->kp_order == VX_ORDER_STL) {
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_stl),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kStlLds);
+        VX_HIP(c, attr);
+        VX_HIP(c, launch(c, kStSelect, k_select_stl, dim3(g.L, 1, nf), dim3(kStlNT), (uint32_t)kStlLds, c->stream,
+                         (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(), a,
+                         c->stage.as<CandRec>(), c->level_count.as<int>(), dbg));
+    } else {
+        VX_HIP(c, launch(c, kStSelect, k_select, dim3(g.L, 1, nf), dim3(kSelBlock), 0, c->stream,
+                         (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(),
+                         (const int*)c->hist.as<int>(), a, c->stage.as<CandRec>(), c->level_count.as<int>()));
+    }
+    if (c->orb_debug & VX_ORB_DEBUG_FAST_NO_BORDER) {
+        // corners within 31 px of the edge are no keypoints: the descriptor patch would leave the
+        // level.  The debug run only exposes the FAST list; it reports no keypoints.
+        VX_HIP(c, hipMemsetAsync(count, 0, (size_t)nf * 16, c->stream));
+    } else {
         const int waves_per_block = kBlock / 64;
         VX_HIP(c, launch(c, kStDescribe, k_describe, dim3((g.out_cap + waves_per_block - 1) / waves_per_block, 1, nf),
                          dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, (const uint8_t*)c->blur.as<uint8_t>(),
@@ -1547,6 +2007,122 @@ void vx_orb_default_params(vx_orb_params* p) {
     p->n_levels = 8;
     p->fast_threshold = 20;
     p->edge_threshold = 31;
+}
+
+int vx_orb_set_order(vx_ctx* c, int order) {
+    if (!c) return VX_ERR_INVALID;
+    if (order != VX_ORDER_STL && order != VX_ORDER_RASTER)
+        return set_error(c, VX_ERR_INVALID, "keypoint order must be VX_ORDER_STL or VX_ORDER_RASTER");
+    if (order == c->kp_order) return VX_OK;
+    VX_HIP(c, hipSetDevice(c->device));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    // captured extraction graphs bake the selection kernel in
+    for (auto& e : c->graphs.entries)
+        if (e.exec) (void)hipGraphExecDestroy(e.exec);
+    c->graphs.entries.clear();
+    c->kp_order = order;
+    for (auto& s : c->slots) s.valid = false;
+    for (int b = 0; b < VX_BATCH_BANKS; ++b) c->batch_n[b] = 0;
+    return VX_OK;
+}
+
+int vx_orb_get_order(const vx_ctx* c) { return c ? c->kp_order : VX_ERR_INVALID; }
+
+int vx_orb_set_debug(vx_ctx* c, int flags) {
+    if (!c) return VX_ERR_INVALID;
+    if (flags & ~(VX_ORB_DEBUG_FAST_NO_BORDER | VX_ORB_DEBUG_STAGES))
+        return set_error(c, VX_ERR_INVALID, "unknown debug flags %#x", flags);
+    if (flags == c->orb_debug) return VX_OK;
+    VX_HIP(c, hipSetDevice(c->device));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    for (auto& e : c->graphs.entries)
+        if (e.exec) (void)hipGraphExecDestroy(e.exec);
+    c->graphs.entries.clear();
+    c->orb_debug = flags;
+    c->geo_valid = false;  // orb_prepare sizes the debug buffer
+    return VX_OK;
+}
+
+int vx_orb_debug_read(vx_ctx* c, int level, int what, void* out, int64_t cap_bytes, int64_t* n_out) {
+    if (!c || !n_out) return VX_ERR_INVALID;
+    *n_out = 0;
+    if (!c->geo_valid || !c->slots[0].valid)
+        return set_error(c, VX_ERR_STATE, "no single-frame extraction to inspect");
+    const OrbGeometry& g = c->geo;
+    if (level < 0 || level >= g.L) return set_error(c, VX_ERR_INVALID, "bad level %d", level);
+    if (what >= 2 && (!c->orb_debug || c->kp_order != VX_ORDER_STL))
+        return set_error(c, VX_ERR_STATE, "selection stages need vx_orb_set_debug and VX_ORDER_STL");
+    VX_HIP(c, hipSetDevice(c->device));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    int info[2 * kMaxLevels];
+    if (what >= 2) VX_HIP(c, hipMemcpy(info, c->orb_dbg.p, sizeof info, hipMemcpyDeviceToHost));
+    const CandRec* st = c->stage.as<CandRec>() + g.stage_base[level];
+    const void* src = nullptr;
+    int64_t n = 0, esz = 1;
+    switch (what) {
+        case 0: src = c->pyr.as<uint8_t>() + g.off[level]; n = (int64_t)g.lw[level] * g.lh[level]; break;
+        case 1: src = c->blur.as<uint8_t>() + g.off[level]; n = (int64_t)g.lw[level] * g.lh[level]; break;
+        case 2: src = st; n = info[level]; esz = sizeof(CandRec); break;
+        case 3: {
+            int64_t off = 2 * kMaxLevels;
+            for (int i = 0; i < level; ++i) off += g.level_cap[i];
+            src = c->orb_dbg.as<int>() + off;
+            n = info[kMaxLevels + level];
+            esz = sizeof(int);
+            break;
+        }
+        case 4: {
+            int cnt[kMaxLevels];
+            VX_HIP(c, hipMemcpy(cnt, c->level_count.p, sizeof cnt, hipMemcpyDeviceToHost));
+            src = st + g.level_cap[level];
+            n = cnt[level];
+            esz = sizeof(CandRec);
+            break;
+        }
+        default: return set_error(c, VX_ERR_INVALID, "bad stage %d", what);
+    }
+    *n_out = n;
+    if (n * esz > cap_bytes) return set_error(c, VX_ERR_CAPACITY, "need %lld bytes", (long long)(n * esz));
+    if (n > 0) VX_HIP(c, hipMemcpy(out, src, (size_t)(n * esz), hipMemcpyDeviceToHost));
+    return VX_OK;
+}
+
+int vx_test_retain_best(vx_ctx* c, const uint32_t* keys, int n, int npts, int wide, int use_lds, int32_t* out_idx,
+                        int* n_out) {
+    if (!c || !n_out || (n > 0 && (!keys || !out_idx)) || n < 0 || n >= (1 << 24)) return VX_ERR_INVALID;
+    *n_out = 0;
+    if (!wide)
+        for (int i = 0; i < n; ++i)
+            if (keys[i] > 255u) return set_error(c, VX_ERR_INVALID, "narrow keys must be <= 255");
+    const int64_t esz = wide ? 8 : 4, need = esz * ((int64_t)n + 2 * (n / 2 + 1));
+    if (use_lds && need > kStlLds) return set_error(c, VX_ERR_INVALID, "%lld bytes exceed the LDS", (long long)need);
+    VX_HIP(c, hipSetDevice(c->device));
+    void *dk = nullptr, *ds = nullptr, *dout = nullptr;
+    int rc = VX_OK;
+    if (hipMalloc(&dk, std::max<int64_t>(4, 4 * (int64_t)n)) != hipSuccess || hipMalloc(&ds, need) != hipSuccess ||
+        hipMalloc(&dout, 4 * ((int64_t)n + 1)) != hipSuccess) {
+        rc = set_error(c, VX_ERR_HIP, "hipMalloc failed");
+    } else {
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_test_retain),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kStlLds);
+        (void)attr;
+        hipError_t e = hipMemcpyAsync(dk, keys, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_test_retain, dim3(1), dim3(kStlNT), use_lds ? kStlLds : 0, c->stream,
+                               (const unsigned*)dk, n, npts, wide, use_lds, (unsigned char*)ds, (int*)dout);
+            e = hipGetLastError();
+        }
+        int k = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&k, dout, 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess && k > 0) e = hipMemcpy(out_idx, (int*)dout + 1, 4 * (size_t)k, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hip_fail(c, e, "vx_test_retain_best");
+        else *n_out = k;
+    }
+    if (dk) (void)hipFree(dk);
+    if (ds) (void)hipFree(ds);
+    if (dout) (void)hipFree(dout);
+    return rc;
 }
 
 int vx_orb_pattern(int32_t* out) {

@@ -126,7 +126,7 @@ struct OrbGeometry {
     int64_t cell_base[kMaxLevels]; // first cell of level l
     int64_t cells_total = 0;
     int level_cap[kMaxLevels];     // max strict-NMS corners of level l
-    int64_t stage_base[kMaxLevels];// selection staging (2 * level_cap records) of level l
+    int64_t stage_base[kMaxLevels];// selection staging (4 * level_cap + 4 records) of level l
     int64_t stage_total = 0;
     int max_w = 0;
     int out_cap = 0;               // keypoint capacity of one slot
@@ -178,6 +178,9 @@ struct vx_ctx {
     // ---- ORB
     vx::OrbGeometry geo;
     bool geo_valid = false;
+    int kp_order = VX_ORDER_STL;  // vx_orb_set_order: keypoint order inside a level
+    int orb_debug = 0;            // vx_orb_set_debug flags (test hooks)
+    vx::DevBuf orb_dbg;           // their device record (k_select_stl)
     vx::DevBuf img_in, pyr, blur, tabs, cand, band_count, hist, stage, level_count;
     vx::Slot slots[VX_MAX_SLOTS];
     vx::Slot batch[VX_BATCH_BANKS];  // vx_orb_extract_batch_async outputs, frame-major

@@ -21,6 +21,9 @@ HEADER_PATH = os.path.join(REPO_ROOT, "include", "vx_slam.h")
 
 VX_OK, VX_ERR_INVALID, VX_ERR_HIP, VX_ERR_CAPACITY, VX_ERR_COMM, VX_ERR_STATE = 0, -1, -2, -3, -4, -5
 MAX_SLOTS = 4
+ORDER_STL, ORDER_RASTER = 0, 1  # vx_orb_set_order (include/vx_slam.h)
+DEBUG_FAST_NO_BORDER, DEBUG_STAGES = 1, 2  # vx_orb_set_debug test hooks
+CAND_DTYPE = np.dtype([("xy", "<u4"), ("score", "<i4"), ("harris", "<f4"), ("pad", "<i4")])
 
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("response", "<f4"), ("angle", "<f4"),
                            ("octave", "<i4")])
@@ -89,7 +92,8 @@ EXPORTS = [
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
-    "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch",
+    "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
+    "vx_orb_get_order", "vx_orb_set_debug", "vx_orb_debug_read", "vx_test_retain_best",
 ]
 
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
@@ -116,6 +120,12 @@ def lib():
         L.vx_stream.argtypes = [C.c_void_p]
         L.vx_synchronize.argtypes = [C.c_void_p]
         L.vx_set_grid_share.argtypes = [C.c_void_p, C.c_float]
+        L.vx_orb_set_order.argtypes = [C.c_void_p, C.c_int]
+        L.vx_orb_get_order.argtypes = [C.c_void_p]
+        L.vx_orb_set_debug.argtypes = [C.c_void_p, C.c_int]
+        L.vx_orb_debug_read.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.POINTER(C.c_int64)]
+        L.vx_test_retain_best.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                          C.POINTER(C.c_int)]
         L.vx_stream_wait_ctx.argtypes = [C.c_void_p, C.c_void_p]
         L.vx_event_create.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
         L.vx_event_record.argtypes = [C.c_void_p, C.c_void_p]
@@ -470,6 +480,40 @@ class Context:
     def set_grid_share(self, share: float):
         """vx_set_grid_share: size one-round grids for this share of the CUs (concurrent contexts)."""
         self._check(lib().vx_set_grid_share(self._h, C.c_float(share)))
+
+    def set_order(self, order: int):
+        """vx_orb_set_order: ORDER_STL (default: OpenCV's libstdc++ retainBest permutation) or
+        ORDER_RASTER (the same keypoint set per level in raster order)."""
+        self._check(lib().vx_orb_set_order(self._h, int(order)))
+
+    @property
+    def order(self) -> int:
+        return lib().vx_orb_get_order(self._h)
+
+    def set_debug(self, flags: int):
+        """vx_orb_set_debug (test hook): DEBUG_FAST_NO_BORDER | DEBUG_STAGES."""
+        self._check(lib().vx_orb_set_debug(self._h, int(flags)))
+
+    def debug_read(self, level: int, what: int):
+        """vx_orb_debug_read after orb_extract: 0 level bytes, 1 blurred level, 2 candidate records
+        (raster order), 3 retainBest(2q) order (indices into 2), 4 final records (CAND_DTYPE)."""
+        n = C.c_int64(0)
+        rc = lib().vx_orb_debug_read(self._h, level, what, None, 0, C.byref(n))
+        if rc not in (VX_OK, VX_ERR_CAPACITY):
+            self._check(rc)
+        dt = {0: np.uint8, 1: np.uint8, 2: CAND_DTYPE, 3: np.int32, 4: CAND_DTYPE}[what]
+        out = np.zeros(max(n.value, 1), dt)
+        self._check(lib().vx_orb_debug_read(self._h, level, what, _p(out), out.nbytes, C.byref(n)))
+        return out[:n.value]
+
+    def test_retain_best(self, keys, npts: int, wide: bool = False, use_lds: bool = True):
+        """vx_test_retain_best: the device retainBest over bare keys; kept indices in output order."""
+        keys = np.ascontiguousarray(keys, np.uint32)
+        out = np.zeros(max(len(keys), 1), np.int32)
+        n = C.c_int(0)
+        self._check(lib().vx_test_retain_best(self._h, _p(keys), len(keys), int(npts), int(wide), int(use_lds),
+                                              _p(out), C.byref(n)))
+        return out[:n.value].copy()
 
     def graph_counts(self):
         """(graphs captured, graph launches) of this context's hipGraph replay."""
