@@ -1,8 +1,8 @@
 // ba_oracle.cpp — CPU restatement of LocalBA::Optimize.  TEST INFRASTRUCTURE ONLY.
 //
 // Line-for-line restatement of /root/reference/core/backend/local_ba.cpp:66-249 (alternating
-// pose / landmark Gauss-Newton, including the reference's b = -J^T e step sign :185,:253, the
-// 5 px gate :177,:243 and the relative-cost stop :269-276), ProjectToPixel
+// pose / landmark Gauss-Newton, including the reference's b = -J^T e step sign :156,:224, the
+// 5 px gate :148,:214 and the stop rule :240-247), ProjectToPixel
 // (core/common/projection.h:11-31), ProjectionJacobian / PoseJacobian / HuberWeight
 // (local_ba.cpp:15-40) and SelectKeyFrames (:42-62).  Third-party pieces restated from their
 // published algorithms (Eigen 3 / Sophus, unpinned versions, vcpkg.json):

@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+# $VX_ORACLE_LIB: another build of the same sources (the ASan/UBSan one, tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("VX_ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 PATTERN_PATH = os.path.join(os.path.dirname(HERE), "tests", "golden", "orb_bit_pattern_31.txt")
 
 ORDER_STL, ORDER_RASTER = 0, 1
@@ -23,7 +24,7 @@ MATCH_DTYPE = np.dtype([("query_idx", "<i4"), ("train_idx", "<i4"), ("distance",
 
 
 def build():
-    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    subprocess.run(["make", "-s", "-C", HERE, "asan" if os.environ.get("VX_ORACLE_LIB") else "all"], check=True)
 
 
 _lib = None

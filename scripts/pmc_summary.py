@@ -13,7 +13,7 @@ import sys
 
 # kernel -> the profiling stage (vx_prof_name) whose HIP-event bracket contains it
 STAGE = {"k_gray": "orb_gray", "k_resize": "orb_resize", "k_pyramid": "orb_pyramid", "k_fast": "orb_fast_harris",
-         "k_select": "orb_select", "k_blur": "orb_blur", "k_describe": "orb_describe",
+         "k_select": "orb_select", "k_select_stl": "orb_select", "k_blur": "orb_blur", "k_describe": "orb_describe",
          "k_knn_partial": "match_partial", "k_knn_rows": "match_partial", "k_knn_merge": "match_merge",
          "k_knn_compact": "match_merge", "k_ba_reset": "ba_reset",
          "k_pose_kf": "ba_pose_partial", "k_landmark_solve": "ba_landmark", "k_pose_solve_g": "ba_landmark",

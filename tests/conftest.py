@@ -7,10 +7,13 @@ import pytest
 # both carry the soname libamdhip64.so.7, so whichever a process loads first serves both.  torch only
 # initialises on its own copy: load it before any test loads libvxslam (a full-suite run does this
 # anyway when collecting the modules that import torch; a narrower selection might not).
-try:
-    import torch  # noqa: F401
-except ImportError:  # pragma: no cover
-    torch = None
+# (not under the ASan run of tests/test_sanitizers.py, which preloads libasan: the CPU tests it runs
+# need no torch, and torch's ROCm libraries are not built for a preloaded sanitizer runtime)
+if not os.environ.get("VX_SANITIZE"):
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover
+        torch = None
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "visionx-slam_amd", "python"), os.path.join(ROOT, "oracle"), ROOT):
@@ -21,6 +24,7 @@ for p in (os.path.join(ROOT, "visionx-slam_amd", "python"), os.path.join(ROOT, "
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP library)")
     config.addinivalue_line("markers", "slow: larger-than-default sizes")
+    config.addinivalue_line("markers", "sanitizer: runs the CPU suite under ASan/UBSan (not inside itself)")
 
 
 @pytest.fixture(scope="session")

@@ -14,7 +14,8 @@ import pytest
 from vxslam import synth
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DRIVER = os.path.join(ROOT, "visionx-slam_amd", "build", "adapter_driver")
+# $VX_ADAPTER_DRIVER: the ASan/UBSan build of the driver (tests/test_sanitizers.py)
+DRIVER = os.environ.get("VX_ADAPTER_DRIVER") or os.path.join(ROOT, "visionx-slam_amd", "build", "adapter_driver")
 
 MAP_KEYS = ["kf_id", "kf_pose", "kf_intr", "kf_has_cam", "kf_feat_ptr", "feat_uv", "feat_lm_id", "feat_flags",
             "lm_id", "lm_pos", "lm_bad", "lm_obs_ptr", "obs_kf_id", "obs_feat_idx"]

@@ -132,3 +132,52 @@ def _shard_worker(rank, world, port):
 
 def test_sharded_pose_normal_equations_allreduce():
     _spawn(_shard_worker)
+
+
+def _parity_worker(rank, world, port):
+    """bench.py's N > 1 parity path (shard_result -> Dist.gather -> parity_vs_unsharded -> the JSON
+    field) with the restatement standing in for the GPU runs: the unsharded result split by the shard
+    hash is what a correct sharded run returns."""
+    import json
+
+    dist = _init(rank, world, port)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    import pyoracle
+    import vxslam
+    from vxslam import synth
+
+    m = synth.make_ba_map(23, 6, 800, n_old_kf=2)
+    opts = vxslam.default_ba_options(window=6)
+    mm = m.copy()
+    st = pyoracle.ba_optimize(mm, pyoracle.ba_options(window=6))
+    mine = bench.shard_result(mm, vxslam.ba_plan_inspect(m, opts, shard_rank=rank, shard_count=world), st)
+    d = bench.Dist(world)
+    shards = d.gather(mine)
+    if rank == 0:
+        assert len(shards) == world
+        ref = bench.shard_result(mm, vxslam.ba_plan_inspect(m, opts), st)
+        par = bench.parity_vs_unsharded(shards, ref)
+        assert par["ok"] and par["shards_partition"] and par["ranks_agree"] and par["gate_flips"] == 0, par
+        assert par["landmarks"] == sum(len(s["lm_idx"]) for s in shards) > 0
+        json.dumps(par)  # (goes into the JSON line)
+        bad = [dict(s) for s in shards]
+        bad[1]["lm_pos"] = bad[1]["lm_pos"] * (1 + 1e-3)
+        assert not bench.parity_vs_unsharded(bad, ref)["ok"]
+        bad = [dict(s) for s in shards]
+        bad[0]["lm_idx"], bad[0]["lm_pos"] = bad[0]["lm_idx"][1:], bad[0]["lm_pos"][1:]
+        assert not bench.parity_vs_unsharded(bad, ref)["shards_partition"]
+        bad = [dict(s) for s in shards]
+        bad[1]["pose"] = bad[1]["pose"].copy()
+        bad[1]["pose"][0, 4] += 1e-12  # ranks must agree bitwise
+        assert not bench.parity_vs_unsharded(bad, ref)["ranks_agree"]
+        bad = [dict(s) for s in shards]
+        bad[0]["obs"] = [o + 1 for o in bad[0]["obs"]]
+        assert bench.parity_vs_unsharded(bad, ref)["gate_flips"] > 0
+    else:
+        assert shards is None
+    dist.destroy_process_group()
+
+
+def test_bench_sharded_parity_field():
+    _spawn(_parity_worker)

@@ -156,14 +156,19 @@ def test_dmap_errors(ctx):
     dm.close()
 
 
-def test_dmap_culling_and_reobservation(ctx):
+@pytest.mark.parametrize("compact", [False, True], ids=["tombstones", "compacted"])
+def test_dmap_culling_and_reobservation(ctx, monkeypatch, compact):
     """The map edits of culling and re-association (tracking.cpp:652-773, landmark.h:32-40,
     map.cpp:15-23) on the resident map: Tracking::RemoveKeyFrame of a window keyframe
     (RemoveObservation of each of its landmarks + feature reset + Map::RemoveKeyFrame),
     CullLandmarks (SetBad + feature reset + Map::RemoveLandmark), AddObservation of a pair that is
     already present (the entry keeps its place, takes the new feature index: observations_[kf] = i)
     and of a new pair twice in one batch.  Every plan afterwards equals the snapshot plan of the
-    map as it then stands (ObservationCount, window and landmark table all follow the removals)."""
+    map as it then stands (ObservationCount, window and landmark table all follow the removals).
+    compacted: $VX_DMAP_COMPACT_MIN=0 drops the dead observation rows (tombstones and removed
+    landmarks' pairs) at every plan build (removal reclaims storage); plans unchanged."""
+    if compact:
+        monkeypatch.setenv("VX_DMAP_COMPACT_MIN", "0")
     m = synth.make_ba_map(0xD9, 14, 3000, n_old_kf=2)
     for key in ("obs_kf_id", "obs_feat_idx", "feat_lm_id", "feat_flags", "lm_bad"):
         m[key] = m[key].copy()
@@ -192,6 +197,8 @@ def test_dmap_culling_and_reobservation(ctx):
         live = dm.live_counts()
         assert live == {"kf": len(kr), "lm": len(lr),
                         "obs": int(sum(mir.obs_lm[r] in mir.lm_set() for r in mir.obs_rows))}
+        if compact:  # every dead row reclaimed
+            assert dm.counts()["obs"] == live["obs"]
         pd.close(), ps.close()
         return m2
 

@@ -480,3 +480,30 @@ def test_device_plan_build_edges(ctx):
     mm["lm_bad"][:] = 1  # no optimisable landmark
     (rd, _), (rh, _) = (_plan_result(ctx, mm, vxslam.default_ba_options(window=6), None, 0, 1, hb) for hb in (False, True))
     assert rd == rh and rd[1] == 1
+
+
+def test_failed_plan_build_then_destroy(monkeypatch):
+    """A plan build that fails after the plan was registered with its context (the
+    failed plan was deleted without leaving c->plan_live, so vx_destroy wrote into freed memory):
+    $VX_TEST_FAIL_PLAN=1 fails every build, snapshot and resident-map alike; later builds on the
+    same context work and the context is destroyed cleanly."""
+    import vxslam
+
+    c = vxslam.Context(0)
+    m = synth.make_ba_map(0xF0, 8, 800, n_old_kf=2)
+    opts = vxslam.default_ba_options(window=8, iters=3)
+    dm = vxslam.DMap(c)
+    vxslam.dmap_load(dm, m)
+    monkeypatch.setenv("VX_TEST_FAIL_PLAN", "1")
+    for _ in range(3):
+        with pytest.raises(vxslam.VxError):
+            c.ba_plan(m, opts)
+        with pytest.raises(vxslam.VxError):
+            dm.plan(opts)
+    monkeypatch.delenv("VX_TEST_FAIL_PLAN")
+    p = c.ba_plan(m, opts)
+    p.run_async()
+    assert p.fetch().iterations >= 1
+    p.close()
+    dm.close()
+    c.close()

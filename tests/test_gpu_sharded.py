@@ -152,3 +152,32 @@ def test_landmark_with_more_observations_than_a_workgroup(ctx, oracle):
     mc = m.copy()
     stc = oracle.ba_optimize(mc, oracle.ba_options(window=10))
     _assert_ba_close(mg, mc, stg, stc)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_sharded_sequence_graph_replay(ctx, n, ba_path):
+    """The sharded iteration sequence (row sums -> the reduction that stands in for ncclAllReduce ->
+    k_ba_iter, or pose stage -> reduction -> landmark stage) through the graph cache, as a real
+    sharded plan's runs after its first (vx_ba_plan_run_async): run 1 decides the kernels eagerly,
+    run 2 is the first sighting (eager), run 3 is captured, runs 4-5 replay — every run bitwise equal."""
+    nk, nl = 50 * n, 20000 * n
+    m = synth.make_ba_map(0x5EED0003, nk, nl, n_streams=n, n_old_kf=2 * n)
+    opts = vxslam.default_ba_options(window=nk)
+    plans = [ctx.ba_plan(m, opts, shard_rank=r, shard_count=n) for r in range(n)]
+    cap0, lau0 = ctx.graph_counts()
+    runs = []
+    for _ in range(5):
+        ctx.ba_shard_emulate(plans)
+        res = []
+        for p in plans:
+            mm = m.copy()
+            st = p.fetch(mm)
+            res.append((mm["kf_pose"].copy(), mm["lm_pos"].copy(), st.iterations, list(st.obs[:16]), list(st.cost[:16])))
+        runs.append(res)
+    cap1, lau1 = ctx.graph_counts()
+    assert cap1 == cap0 + 1 and lau1 >= lau0 + 3, (cap0, lau0, cap1, lau1)
+    for res in runs[1:]:
+        for a, b in zip(res, runs[0]):
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+    for p in plans:
+        p.close()

@@ -1142,6 +1142,13 @@ vx_ba_plan* plan_new(vx_ctx* c) {
     return p;
 }
 
+// Test hook: $VX_TEST_FAIL_PLAN=1 makes every plan build fail after the plan was registered with
+// its context (tests/test_gpu_parity.py::test_failed_plan_build_then_destroy).
+int plan_fault_injected(vx_ctx* c) {
+    const char* e = getenv("VX_TEST_FAIL_PLAN");
+    return (e && e[0] == '1') ? set_error(c, VX_ERR_STATE, "plan build failed ($VX_TEST_FAIL_PLAN)") : VX_OK;
+}
+
 void plan_pool_release(vx_ctx* c) {
     for (vx_ba_plan* h : c->plan_husks) delete h;
     c->plan_husks.clear();
@@ -1324,6 +1331,9 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kptr, const st
         n_o += cnt;
     }
     const int nb = (int)K.size();
+    // the device build's workgroup limit (k_fb_pose_rank's LDS counters, ba_fused_build.hip): beyond
+    // it both builds give the plan no fused layout, so host- and device-built plans stay identical
+    if (nb > kFusedMaxGroups) return VX_OK;
     const int fw = ft / 64;
     lap(0);
     // 3. owners
@@ -1871,9 +1881,10 @@ int vx_ba_plan_create_ex(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_
     p->shard_rank = shard_rank;
     p->shard_count = shard_count;
     p->global_poses = (flags & VX_PLAN_GLOBAL_POSES) != 0;
-    const int rc = (flags & VX_PLAN_HOST_BUILD) ? build_plan(c, m, ref, has_ref, p) : build_plan_device(c, m, ref, has_ref, p);
+    int rc = plan_fault_injected(c);
+    if (!rc) rc = (flags & VX_PLAN_HOST_BUILD) ? build_plan(c, m, ref, has_ref, p) : build_plan_device(c, m, ref, has_ref, p);
     if (rc) {
-        delete p;
+        vx_ba_plan_destroy(p);  // (also leaves c->plan_live)
         return rc;
     }
     *out = p;
@@ -1893,9 +1904,10 @@ int vx_ba_plan_create_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, con
     p->shard_rank = shard_rank;
     p->shard_count = shard_count;
     p->from_dmap = true;
-    const int rc = build_plan_dmap(c, m, ref, has_ref, p);
+    int rc = plan_fault_injected(c);
+    if (!rc) rc = build_plan_dmap(c, m, ref, has_ref, p);
     if (rc) {
-        delete p;
+        vx_ba_plan_destroy(p);  // (also leaves c->plan_live)
         return rc;
     }
     *out = p;
@@ -1918,13 +1930,57 @@ int vx_ba_plan_apply_dmap(vx_ctx* c, vx_ba_plan* p, vx_dmap* m) {
 
 int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
-    if (p->shard_count > 1 || p->status != 0) return plan_run(c, p);  // (RCCL calls stay outside graphs)
+    if (p->status != 0) return plan_run(c, p);
+    // Sharded plans: the first run is eager (its one small all-reduce fixes the kernel set on every
+    // rank and synchronises); later runs replay ONE hipGraph of the whole sequence, the per-iteration
+    // k_row_sum -> ncclAllReduce -> k_ba_iter chain included (RCCL collectives are capturable: the
+    // graph holds their kernels).  A capture that fails leaves the plan eager; $VX_SHARDED_GRAPHS=0
+    // keeps every sharded run eager.
+    if (p->shard_count > 1) {
+        const char* e = std::getenv("VX_SHARDED_GRAPHS");
+        if (!p->choice_made || p->graph_eager || (e && e[0] == '0')) return plan_run(c, p);
+        const bool capturing = c->use_graphs && !c->prof && p->graph.seen && !p->graph.exec;
+        p->ran = true;
+        const int rc =
+            graph_run_owned(c, p->graph, [](vx_ctx* cc, void* v) { return plan_run(cc, static_cast<vx_ba_plan*>(v)); }, p);
+        if (rc != VX_OK && capturing) {
+            p->graph_eager = true;
+            return plan_run(c, p);
+        }
+        return rc;
+    }
     p->ran = true;
     return graph_run_owned(c, p->graph, [](vx_ctx* cc, void* v) { return plan_run(cc, static_cast<vx_ba_plan*>(v)); }, p);
 }
 
+namespace {
+int shard_emulate_enqueue(vx_ctx* c, vx_ba_plan* const* plans, int n);
+struct EmuArgs {
+    vx_ba_plan* const* plans;
+    int n;
+};
+}  // namespace
+
+// The emulated sharded run goes through the context's graph cache like a real sharded run's
+// sequence: eager on its first sighting, captured on the second, replayed afterwards (keyed by the
+// shard plans), so the tests exercise the captured form of the row sum -> reduction -> k_ba_iter chain.
 int vx_ba_shard_emulate_run(vx_ctx* c, vx_ba_plan* const* plans, int n) {
     if (!c || !plans || n < 1 || n > kMaxEmuShards) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_shard_emulate_run: bad arguments") : VX_ERR_INVALID;
+    for (int r = 0; r < n; ++r)
+        if (!plans[r] || plans[r]->c != c) return set_error(c, VX_ERR_INVALID, "shard %d: plan of another context", r);
+    std::vector<uint64_t> key{0xE3u, (uint64_t)n};
+    for (int r = 0; r < n; ++r) key.push_back((uint64_t)(uintptr_t)plans[r]);
+    EmuArgs ea{plans, n};
+    if (plans[0]->status != 0 || !plans[0]->choice_made) return shard_emulate_enqueue(c, plans, n);  // (decides the kernels)
+    for (int r = 0; r < n; ++r) plans[r]->ran = true;
+    return graph_run(c, key, [](vx_ctx* cc, void* v) {
+        const EmuArgs* x = static_cast<const EmuArgs*>(v);
+        return shard_emulate_enqueue(cc, x->plans, x->n);
+    }, &ea);
+}
+
+namespace {
+int shard_emulate_enqueue(vx_ctx* c, vx_ba_plan* const* plans, int n) {
     vx_ba_plan* p0 = plans[0];
     for (int r = 0; r < n; ++r) {
         const vx_ba_plan* p = plans[r];
@@ -1996,6 +2052,7 @@ int vx_ba_shard_emulate_run(vx_ctx* c, vx_ba_plan* const* plans, int n) {
     for (int r = 0; r < n; ++r) plans[r]->ran = true;
     return VX_OK;
 }
+}  // namespace
 
 int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
@@ -2042,6 +2099,19 @@ void vx_ba_plan_destroy(vx_ba_plan* p) {
     if (c) {
         auto& live = c->plan_live;
         live.erase(std::remove(live.begin(), live.end(), p), live.end());
+        // captured emulated sharded sequences naming this plan (vx_ba_shard_emulate_run's keys
+        // {0xE3, n, plans...}) bake its buffers in: drop them before the address can be reused
+        auto& ge = c->graphs.entries;
+        for (auto it = ge.begin(); it != ge.end();) {
+            const bool names = !it->key.empty() && it->key[0] == 0xE3u &&
+                               std::find(it->key.begin() + 2, it->key.end(), (uint64_t)(uintptr_t)p) != it->key.end();
+            if (names) {
+                if (it->exec) (void)hipGraphExecDestroy(it->exec);
+                it = ge.erase(it);
+            } else {
+                ++it;
+            }
+        }
         if (c->plan_husks.size() < kMaxPlanHusks) {  // park the buffers (no hipFree)
             auto* h = new vx_ba_plan();
             adopt_buffers(h, p);

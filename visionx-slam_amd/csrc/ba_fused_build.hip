@@ -37,7 +37,7 @@ constexpr int kT = 256;
 constexpr int kFK = kBaFusedK;
 constexpr int kMaxW = (kBaMaxKfLds + 63) / 64;  // 64-bit words of a keyframe set
 constexpr int kChainWin = 12288;                 // next[] window of the chain walk (ints of LDS)
-constexpr int kMaxGroupsRank = 8192;             // workgroup counters of k_fb_pose_rank (LDS)
+constexpr int kMaxGroupsRank = kFusedMaxGroups;  // workgroup counters of k_fb_pose_rank (LDS)
 constexpr int kMaxWaves = kBaFTLarge / 64;
 static_assert(kBaFTLarge <= kChainWin / 2, "the chain walk advances at most cap landmarks per step");
 

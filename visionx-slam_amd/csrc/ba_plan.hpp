@@ -29,6 +29,7 @@ struct vx_ba_plan {
     bool lds_poses = true;
     bool ran = false;
     vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
+    bool graph_eager = false;  // sharded: capturing the RCCL sequence failed once -> stay eager
     vx::DevBuf kf_map_dev, lm_map_dev;  // plans built from a vx_dmap: window row / slot -> map index
     bool from_dmap = false;
     bool global_poses = false;  // VX_PLAN_GLOBAL_POSES
@@ -94,6 +95,7 @@ int build_fused(vx_ctx* c, vx_ba_plan* p, const std::vector<int>& kf_obs_ptr, co
 // byte for byte (tests/test_gpu_fused_build.py), without the CSR download or host packing
 int build_fused_device(vx_ctx* c, vx_ba_plan* p);
 constexpr int kBaFusedK = 64;      // keyframes per fused workgroup
+constexpr int kFusedMaxGroups = 8192;  // most fused workgroups of a plan (host and device builds alike)
 constexpr int kBaFTSmall = 512, kBaFTLarge = 1024;  // threads per fused workgroup
 constexpr int kBaStride = 32;      // doubles per partial block
 constexpr int kBaMaxKfLds = 448;   // most window keyframes of the LDS-pose / fused kernels

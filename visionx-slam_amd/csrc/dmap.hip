@@ -96,9 +96,60 @@ __global__ void k_csr_fill(const int* perm, int64_t n, const uint64_t* okf_in, c
     if (i <= n_lm) optr[i] = scan[i];
 }
 
+// Drops the dead observation rows (RemoveObservation tombstones and the pairs of removed
+// landmarks), keeping the live rows in order — so every landmark's list and the CSR stay as they
+// were — and re-points / erases obs_index entries.  Host round trip of the three observation arrays:
+// amortised, it runs only once dead rows exceed a quarter of the list.
+int dmap_compact(vx_ctx* c, vx_dmap* m) {
+    const int64_t n = m->n_obs;
+    std::vector<int> lm(n);
+    std::vector<uint64_t> kf(n), fi(n);
+    VX_HIP(c, hipMemcpyAsync(lm.data(), m->obs_lm.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipMemcpyAsync(kf.data(), m->obs_kf.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipMemcpyAsync(fi.data(), m->obs_fi.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    std::vector<int64_t> row(n, -1);
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (lm[i] != kDeadObs && !m->lm_removed[lm[i]]) {
+            row[i] = k;
+            lm[k] = lm[i];
+            kf[k] = kf[i];
+            fi[k] = fi[i];
+            ++k;
+        }
+    if (k) {
+        VX_HIP(c, hipMemcpyAsync(m->obs_lm.p, lm.data(), (size_t)k * 4, hipMemcpyHostToDevice, c->stream));
+        VX_HIP(c, hipMemcpyAsync(m->obs_kf.p, kf.data(), (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
+        VX_HIP(c, hipMemcpyAsync(m->obs_fi.p, fi.data(), (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+    }
+    for (auto it = m->obs_index.begin(); it != m->obs_index.end();) {
+        const int64_t r = row[it->second];
+        if (r < 0) {
+            it = m->obs_index.erase(it);
+        } else {
+            it->second = r;
+            ++it;
+        }
+    }
+    m->n_obs = k;
+    m->csr_dirty = true;
+    return VX_OK;
+}
+
 }  // namespace
 
 int dmap_build_csr(vx_ctx* c, vx_dmap* m) {
+    // $VX_DMAP_COMPACT_MIN: fewest rows worth compacting (default 4096; 0: compact whenever a dead
+    // row exists — the tests' setting)
+    const char* e = getenv("VX_DMAP_COMPACT_MIN");
+    const int64_t kMin = e ? (int64_t)atoll(e) : (int64_t)4096;
+    const int64_t dead = m->n_obs - m->n_obs_live;
+    if (dead > 0 && (kMin == 0 || (m->n_obs >= kMin && 4 * dead > m->n_obs))) {
+        const int rc = dmap_compact(c, m);
+        if (rc) return rc;
+    }
     if (!m->csr_dirty) return VX_OK;
     const int64_t n = m->n_obs, nl = m->n_lm;
     hipStream_t s = c->stream;
@@ -205,6 +256,7 @@ int vx_dmap_add_landmarks(vx_dmap* m, int n, const uint64_t* id, const double* p
     m->n_lm += n;
     m->n_lm_live += n;
     m->lm_obs_live.resize(m->n_lm, 0);
+    m->lm_removed.resize(m->n_lm, 0);
     m->csr_dirty = true;
     return VX_OK;
 }
@@ -228,21 +280,27 @@ int vx_dmap_add_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uin
     std::vector<uint64_t> a_kf, a_fi;
     std::vector<int64_t> w_row;
     std::vector<uint64_t> w_fi;
+    // pairs first seen in this batch -> their new rows; entered into obs_index (and the live counts)
+    // only once the device rows are written (a failed append leaves the map unchanged)
+    std::unordered_map<std::pair<int, uint64_t>, int64_t, vx_dmap::PairHash> fresh;
+    std::vector<std::pair<int, uint64_t>> fresh_order;
     for (int i = 0; i < n; ++i) {
         const auto key = std::make_pair(li[i], kf_id[i]);
         auto it = m->obs_index.find(key);
-        if (it == m->obs_index.end()) {
-            m->obs_index.emplace(key, m->n_obs + (int64_t)a_lm.size());
-            ++m->lm_obs_live[li[i]];
-            ++m->n_obs_live;
+        if (it != m->obs_index.end()) {
+            w_row.push_back(it->second);
+            w_fi.push_back(fi[i]);
+            continue;
+        }
+        auto f = fresh.find(key);
+        if (f != fresh.end()) {
+            a_fi[f->second] = fi[i];
+        } else {
+            fresh.emplace(key, (int64_t)a_lm.size());
+            fresh_order.push_back(key);
             a_lm.push_back(li[i]);
             a_kf.push_back(kf_id[i]);
             a_fi.push_back(fi[i]);
-        } else if (it->second >= m->n_obs) {
-            a_fi[it->second - m->n_obs] = fi[i];
-        } else {
-            w_row.push_back(it->second);
-            w_fi.push_back(fi[i]);
         }
     }
     VX_HIP(c, hipSetDevice(c->device));
@@ -252,6 +310,11 @@ int vx_dmap_add_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uin
     if ((rc = append(c, m->obs_kf, m->n_obs, a_kf.data(), na))) return rc;
     if ((rc = append(c, m->obs_fi, m->n_obs, a_fi.data(), na))) return rc;
     if ((rc = scatter(c, m->obs_fi, w_row, w_fi.data(), 1))) return rc;
+    for (const auto& key : fresh_order) {
+        m->obs_index.emplace(key, m->n_obs + fresh[key]);
+        ++m->lm_obs_live[key.first];
+        ++m->n_obs_live;
+    }
     m->n_obs += na;
     if (na || !w_row.empty()) m->csr_dirty = true;
     return VX_OK;
@@ -307,6 +370,8 @@ int vx_dmap_remove_landmarks(vx_dmap* m, int n, const uint64_t* lm_id) {
         if (it == m->lm_index.end()) continue;  // unordered_map::erase of an absent key
         rows.push_back(it->second);
         m->n_obs_live -= m->lm_obs_live[it->second];  // (its pairs can no longer be named: lm_index)
+        m->lm_obs_live[it->second] = 0;
+        m->lm_removed[it->second] = 1;                // (its observation rows go at the next compaction)
         m->lm_index.erase(it);
     }
     if (rows.empty()) return VX_OK;

@@ -33,6 +33,7 @@ struct vx_dmap {
     int64_t n_lm = 0, n_obs = 0;                 // rows (removed ones included)
     int64_t n_kf_live = 0, n_lm_live = 0, n_obs_live = 0;
     std::vector<int> lm_obs_live;                // live observations per landmark row
+    std::vector<uint8_t> lm_removed;             // 1 after Map::RemoveLandmark (row kept as dead storage)
     // device arrays, insertion order, grown by doubling (used sizes from the counts above)
     vx::DevBuf kf_pose, kf_intr;                 // 7 / 4 doubles per keyframe
     vx::DevBuf feat_uv, feat_lm, feat_fl;        // 2 doubles / u64 / u8 per feature
@@ -49,6 +50,7 @@ namespace vx {
 constexpr int kDeadObs = 0x7fffffff;
 // lm_bad value of a removed landmark (Map::RemoveLandmark): the plan build's landmark table skips it
 constexpr uint8_t kLmRemoved = 2;
-// stable landmark-major CSR of the observation list into m->optr / okf / ofi
+// stable landmark-major CSR of the observation list into m->optr / okf / ofi (compacting the
+// observation rows first when dead ones — removed pairs, removed landmarks' pairs — exceed a quarter)
 int dmap_build_csr(vx_ctx* c, vx_dmap* m);
 }  // namespace vx

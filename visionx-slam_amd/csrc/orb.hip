@@ -1010,8 +1010,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 // index) for the second; they live in LDS when they fit, in the level's global scratch otherwise.
 constexpr int kStlNT = 1024;
 constexpr int kStlWaves = kStlNT / 64;
-constexpr int kStlMulti = 1024;
-constexpr int kStlLds = 96 * 1024;  // dynamic LDS of k_select_stl
+constexpr int kStlRegBlocks = 4;               // 64-element blocks per wave in registers (team_pass_rg;
+                                               // 8 spills at the 128 VGPRs of a 1024-thread workgroup)
+constexpr int kStlMulti = 64 * kStlRegBlocks;  // longer ranges: all 16 waves; shorter: wave 0
+constexpr int kStlLds = 96 * 1024;             // dynamic LDS of k_select_stl
 
 __device__ __forceinline__ unsigned sel_key(unsigned v) { return v >> 24; }
 __device__ __forceinline__ unsigned sel_key(unsigned long long v) { return (unsigned)(v >> 32); }
@@ -1144,10 +1146,218 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
     return cut;
 }
 
+// team_pass with the range held in registers (every range of up to NW x 64 x kStlRegBlocks
+// elements), organised around the crossing: g(x) = #L in [f0, x) - #R in [x, l) never decreases,
+// the max-min K sits where it crosses zero (K = max(#R from x*, #L before x* - 1), x* the first
+// position with g >= 0), and the swapped elements are exactly the L ones before x* - 1 and the R
+// ones from x* on (the first K L's all lie before x*, the last K R's all from x* - 1 on).  So a
+// block wholly before x* - 1 writes its L elements to the L mailboxes by rank and later takes its
+// partners from the R mailboxes; a block wholly from x* on does the converse; only the one or two
+// blocks around x* test ranks against K per lane.  The block masks are two ballots, prefix counts
+// and the crossing are scalar popcounts (plus one ballot in the crossing block), so a block costs
+// ~20 instructions per pass.  (The generic team_pass re-reads LDS in each of four sweeps and
+// shuffles K across lanes; a per-lane rank / compare form of this one still cost ~150 VALU
+// instructions per block: 1.7 us per pass on 300 elements, 60 us per level-0 select at C3.)
+// Two LDS round trips per pass on one wave; NW waves add four barriers.
+// kPivot: [f0 - 1, l) is an introselect range — the median of 3 of (f0, f0 - 1 + (l - f0 + 1) / 2,
+// l - 1), i.e. libstdc++'s (first + 1, first + n / 2, last - 1), becomes the pivot (its slot takes
+// A[f0 - 1]'s element, A[f0 - 1] the pivot), L = !(x > P), R = !(P > x); otherwise [f0, l) is
+// std::partition'ed by x >= thr (L = x < thr, R = x >= thr).  s: >= 4 NW + 4 ints (NW > 1).
+template <int NW, bool kPivot, class T>
+__device__ __forceinline__ int team_pass_rg(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f0, int l,
+                                            unsigned thr, int* s, int& n_r) {
+    constexpr int MB = kStlRegBlocks;
+    typedef unsigned long long u64;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nb = (l - f0 + 63) >> 6;
+    const int b0 = w * nb / NW, cnt = (w + 1) * nb / NW - b0;  // this wave's blocks
+    const int base0 = f0 + 64 * b0;                              // their first position
+    // ---- loads (one round trip): the wave's blocks, the pivot slot and the median-of-3 candidates
+    T v[MB];
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+        const int p = base0 + 64 * j + lane;
+        v[j] = (j < cnt && p < l) ? A[p] : T(0);
+    }
+    int m = -1;
+    T oldf = T(0), pv = T(0);
+    unsigned P = thr;
+    if (kPivot) {  // __move_median_to_first(first, first + 1, mid, last - 1, greater)
+        const int f = f0 - 1, a = f0, b = f + (l - f) / 2, c = l - 1;
+        oldf = A[f];
+        const T va = A[a], vb = A[b], vc = A[c];
+        const unsigned ka = sel_key(va), kb = sel_key(vb), kc = sel_key(vc);
+        if (ka > kb) m = kb > kc ? b : ka > kc ? c : a;
+        else m = ka > kc ? a : kb > kc ? c : b;
+        pv = m == a ? va : m == b ? vb : vc;
+        P = sel_key(pv);
+#pragma unroll
+        for (int j = 0; j < MB; ++j)
+            if (j < cnt && base0 + 64 * j + lane == m) v[j] = oldf;
+    }
+    auto isl = [P](T x) { return kPivot ? sel_key(x) <= P : sel_key(x) < P; };
+    auto isr = [P](T x) { return sel_key(x) >= P; };
+    // ---- block masks (uniform) and this wave's counts
+    u64 ml[MB], mr[MB];
+    int cl = 0, cr = 0;
+#pragma unroll
+    for (int j = 0; j < MB; ++j) {
+        ml[j] = mr[j] = 0ull;
+        if (j < cnt) {
+            const int rem = l - (base0 + 64 * j);
+            const u64 in = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
+            ml[j] = __ballot(isl(v[j])) & in;
+            mr[j] = __ballot(isr(v[j])) & in;
+            cl += __popcll(ml[j]);
+            cr += __popcll(mr[j]);
+        }
+    }
+    int pl = 0, pr = 0, nr = cr;
+    if (NW > 1) {
+        if (lane == 0) {
+            s[2 * w] = cl;
+            s[2 * w + 1] = cr;
+        }
+        __syncthreads();
+        nr = 0;
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            pl += i < w ? s[2 * i] : 0;
+            pr += i < w ? s[2 * i + 1] : 0;
+            nr += s[2 * i + 1];
+        }
+    }
+    // ---- the crossing x* and K: the wave whose range holds x* (g(start) < 0 <= g(end), or x* = f0)
+    int xs = -1, K = 0;
+    {
+        int ql = pl, qr = pr;
+        const bool first_wave = b0 == 0;
+#pragma unroll
+        for (int j = 0; j < MB; ++j)
+            if (j < cnt && xs < 0) {
+                const int start = base0 + 64 * j;
+                const int gs = ql + qr - nr;
+                const int ge = gs + __popcll(ml[j]) + __popcll(mr[j]);
+                if (gs >= 0 && j == 0 && first_wave) {  // x* = f0: no R at all (partition of an all-L tail)
+                    xs = start;
+                    K = 0;
+                } else if (gs < 0 && ge >= 0) {
+                    // g(start + i + 1) over the lanes; the first lane reaching 0 gives x* = start + t + 1
+                    const int own = (int)((ml[j] >> lane) & 1ull) + (int)((mr[j] >> lane) & 1ull);
+                    const int gi = gs + lane_rank(ml[j]) + lane_rank(mr[j]) + own;
+                    const u64 hit = __ballot(gi >= 0) & ~0ull;
+                    const int t = __ffsll((long long)hit) - 1;
+                    xs = start + t + 1;
+                    const u64 bt = (1ull << t) - 1ull;  // positions below start + t
+                    const int lbefore = ql + __popcll(ml[j] & bt);                                 // #L in [f0, x* - 1)
+                    const int rfrom = nr - (qr + __popcll(mr[j] & (t == 63 ? ~0ull : ((bt << 1) | 1ull))));  // #R in [x*, l)
+                    K = max(rfrom, lbefore);
+                }
+                ql += __popcll(ml[j]);
+                qr += __popcll(mr[j]);
+            }
+    }
+    if (NW > 1) {
+        if (lane == 0 && xs >= 0) {
+            s[2 * NW] = xs;
+            s[2 * NW + 1] = K;
+        }
+        __syncthreads();
+        xs = s[2 * NW];
+        K = s[2 * NW + 1];
+    }
+    // ---- the cut min(L[K], R[K-1]) (the L of rank K, the R of left rank nr - K) and the mailboxes
+    int cutw = INT_MAX;
+    {
+        int ql = pl, qr = pr;
+#pragma unroll
+        for (int j = 0; j < MB; ++j)
+            if (j < cnt) {
+                const int start = base0 + 64 * j;
+                const int nlj = __popcll(ml[j]), nrj = __popcll(mr[j]);
+                const int rl = ql + lane_rank(ml[j]);           // L rank of this lane (if L)
+                const int rr = nr - 1 - (qr + lane_rank(mr[j]));  // R rank from the right (if R)
+                const bool il = (ml[j] >> lane) & 1ull, ir = (mr[j] >> lane) & 1ull;
+                if (K >= ql && K < ql + nlj) {
+                    const u64 hit = __ballot(il && rl == K);
+                    cutw = min(cutw, start + __ffsll((long long)hit) - 1);
+                }
+                if (K > 0 && nr - K >= qr && nr - K < qr + nrj) {
+                    const u64 hit = __ballot(ir && rr == K - 1);
+                    cutw = min(cutw, start + __ffsll((long long)hit) - 1);
+                }
+                if (start + 64 <= xs - 1) {  // wholly before x* - 1: every L swaps
+                    if (il) bl[rl] = v[j];
+                } else if (start >= xs) {    // wholly from x* on: every R swaps
+                    if (ir) br[rr] = v[j];
+                } else {
+                    if (il && rl < K) bl[rl] = v[j];
+                    if (ir && rr < K) br[rr] = v[j];
+                }
+                ql += nlj;
+                qr += nrj;
+            }
+    }
+    if (NW > 1 && lane == 0) s[3 * NW + w] = cutw;
+    team_sync<NW>();
+    int cut = cutw;
+    if (NW > 1) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) cut = min(cut, s[3 * NW + i]);
+    }
+    // ---- swap partners (all reads in flight together), then the writes
+    T nv[MB];
+    unsigned sw = 0;
+    {
+        int ql = pl, qr = pr;
+#pragma unroll
+        for (int j = 0; j < MB; ++j) {
+            nv[j] = T(0);
+            if (j < cnt) {
+                const int start = base0 + 64 * j;
+                const int rl = ql + lane_rank(ml[j]);
+                const int rr = nr - 1 - (qr + lane_rank(mr[j]));
+                const bool il = (ml[j] >> lane) & 1ull, ir = (mr[j] >> lane) & 1ull;
+                bool sl, sr;
+                if (start + 64 <= xs - 1) {
+                    sl = il;
+                    sr = false;
+                } else if (start >= xs) {
+                    sl = false;
+                    sr = ir;
+                } else {
+                    sl = il && rl < K;
+                    sr = ir && rr < K;
+                }
+                if (sl) nv[j] = br[rl];
+                else if (sr) nv[j] = bl[rr];
+                sw |= (sl || sr ? 1u : 0u) << j;
+                ql += __popcll(ml[j]);
+                qr += __popcll(mr[j]);
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < MB; ++j)
+        if (j < cnt) {
+            const int p = base0 + 64 * j + lane;
+            if ((sw >> j) & 1u) A[p] = nv[j];
+            else if (p == m) A[p] = oldf;
+        }
+    if (kPivot && threadIdx.x == 0) A[f0 - 1] = pv;
+    team_sync<NW>();
+    n_r = nr;
+    return cut;
+}
+
 // __unguarded_partition_pivot(first = f, last = l) as one team pass; returns the cut
 template <int NW, class T>
 __device__ __forceinline__ int pivot_pass(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f, int l,
                                           int* s) {
+    if (l - f - 1 <= NW * 64 * kStlRegBlocks) {
+        int nr;
+        return team_pass_rg<NW, true>(A, bl, br, f + 1, l, 0u, s, nr);
+    }
     const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
     const T vf = A[f], va = A[a], vb = A[b], vc = A[c];
     const unsigned ka = sel_key(va), kb = sel_key(vb), kc = sel_key(vc);
@@ -1272,15 +1482,17 @@ __device__ __forceinline__ int stl_retain_best(T* __restrict__ A, T* __restrict_
     auto isl = [thr](T v) { return sel_key(v) < thr; };
     auto isr = [thr](T v) { return sel_key(v) >= thr; };
     int nr = 0;
-    if (size - npts > kStlMulti) {
+    if (size - npts > kStlWaves * kStlMulti) {
         team_pass<kStlWaves>(A, bl, br, npts, size, -1, T(0), T(0), isl, isr, s, nr);
+    } else if (size - npts > kStlMulti) {
+        team_pass_rg<kStlWaves, false>(A, bl, br, npts, size, thr, s, nr);
     } else {
         if ((threadIdx.x >> 6) == 0) {
-            team_pass<1>(A, bl, br, npts, size, -1, T(0), T(0), isl, isr, s, nr);
-            if (threadIdx.x == 0) s[3 * kStlWaves + 2] = nr;
+            team_pass_rg<1, false>(A, bl, br, npts, size, thr, s, nr);
+            if (threadIdx.x == 0) s[4 * kStlWaves + 2] = nr;
         }
         __syncthreads();
-        nr = s[3 * kStlWaves + 2];
+        nr = s[4 * kStlWaves + 2];
     }
     return npts + nr;
 }
@@ -1296,7 +1508,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
                                                        CandRec* __restrict__ stage, int* __restrict__ level_count,
                                                        int* __restrict__ dbg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
-    __shared__ int s[3 * kStlWaves + 4];
+    __shared__ int s[4 * kStlWaves + 4];
     __shared__ int sw[kStlWaves];
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
@@ -1357,7 +1569,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         n0 += btot;
     }
     __syncthreads();
-    VX_KT(13);
+    VX_KT(9);
     // ---- retainBest(2q) by FAST score (the pass-1 elements are u32, mailboxes of n0 / 2 + 1 each)
     const int hb = n0 / 2 + 1;
     int K1;
@@ -1370,6 +1582,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
     const bool lds2 = lds1 && o2 + (long long)(K1 + 2 * hb2) * 8 <= kStlLds;
     unsigned long long* A2 = lds2 ? reinterpret_cast<unsigned long long*>(sdyn + o2)
                                   : reinterpret_cast<unsigned long long*>(gscr + 16 * (long long)cap);
+    VX_KT(10);
     const unsigned* A1 = lds1 ? lA1 : gA1;
     if (dbg) {
         long long off = 2 * kMaxLevels;
@@ -1385,7 +1598,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         A2[j] = ((unsigned long long)harris_key(kept[idx].harris) << 32) | idx;
     }
     __syncthreads();
-    VX_KT(14);
+    VX_KT(11);
     int K2;
     if (lds2) {  // (separate call sites: the LDS one compiles to ds_ instructions)
         unsigned long long* L2 = reinterpret_cast<unsigned long long*>(sdyn + o2);
@@ -1394,6 +1607,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         unsigned long long* G2 = reinterpret_cast<unsigned long long*>(gscr + 16 * (long long)cap);
         K2 = stl_retain_best(G2, G2 + K1, G2 + K1 + hb2, K1, q, s);
     }
+    VX_KT(13);
     for (int j = tid; j < K2; j += kStlNT) fin[j] = kept[(unsigned)A2[j]];
     if (tid == 0) level_count[l] = K2;
     VX_KT(15);
@@ -1416,7 +1630,7 @@ __global__ __launch_bounds__(kStlNT) void k_test_retain(const unsigned* __restri
                                                         int use_lds, unsigned char* __restrict__ gscr,
                                                         int* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
-    __shared__ int s[3 * kStlWaves + 4];
+    __shared__ int s[4 * kStlWaves + 4];
     if (!wide) {
         if (use_lds) test_retain_body(reinterpret_cast<unsigned*>(sdyn), keys, n, npts, out, s);
         else test_retain_body(reinterpret_cast<unsigned*>(gscr), keys, n, npts, out, s);

@@ -100,9 +100,17 @@ void ORBExtractor::ExtractBatch(const std::vector<Frame::Ptr>& frames) {
     for (size_t b = 0; b < frames.size(); ++b) {
         Frame& frame = *frames[b];
         int cap = 2 * params_.n_features + 256, n = 0;
-        kp_.resize(cap);
-        desc_.resize((size_t)cap * 32);
-        check(c, vx_orb_batch_fetch(c, 0, (int)b, kp_.data(), desc_.data(), cap, &n), "vx_orb_batch_fetch");
+        for (int attempt = 0; attempt < 2; ++attempt) {  // as Extract(): resize to the count and fetch again
+            kp_.resize(cap);
+            desc_.resize((size_t)cap * 32);
+            const int rc = vx_orb_batch_fetch(c, 0, (int)b, kp_.data(), desc_.data(), cap, &n);
+            if (rc == VX_ERR_CAPACITY && n > cap) {
+                cap = n;
+                continue;
+            }
+            check(c, rc, "vx_orb_batch_fetch");
+            break;
+        }
         auto& features = frame.Features();
         features.clear();
         features.reserve(n);
