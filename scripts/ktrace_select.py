@@ -34,7 +34,8 @@ def main():
             t = tr[l, s]
             row.append(f"{nm} {(t - t0) / 100:6.2f} ({(t - prev) / 100:5.2f})")
             prev = t
-        print(f"  L{l}: " + "  ".join(row))
+        ghz = (cy[l, 15] - cy[l, 12]) / max((tr[l, 15] - tr[l, 12]) / 100.0, 1e-3) / 1e3
+        print(f"  L{l}: " + "  ".join(row) + f"  [{ghz:.2f} GHz]")
     ctx.close()
 
 

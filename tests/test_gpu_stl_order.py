@@ -28,7 +28,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "golden"))
 import make_golden as G  # noqa: E402
 
-LDS_BYTES = 96 * 1024  # kStlLds
+LDS_BYTES = 160 * 1024 - 256 - 65920  # kStlLds - kRgBytes: the arrays after the engine scratch
 
 
 def _fits_lds(n, wide):

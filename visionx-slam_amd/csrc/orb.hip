@@ -1004,16 +1004,13 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 // formulation is checked against the real STL (random, tie-heavy, sorted and McIlroy-adversarial
 // inputs reaching the heap select) by tests/cpp/stl_select_model.cpp.
 //
-// A pass over a range longer than kStlMulti runs on all 16 waves (4 barriers); shorter ranges,
-// most of the passes, run on wave 0 alone without barriers.  Elements are u32 (FAST score << 24 |
-// raster index) for the first retainBest and u64 (order-preserving Harris key << 32 | raster
-// index) for the second; they live in LDS when they fit, in the level's global scratch otherwise.
+// The passes run on a register-resident engine (below): the range stays in registers across
+// them.  Elements are u32 (FAST score << 24 | raster index) for the first retainBest and u64
+// (order-preserving Harris key << 32 | raster index) for the second; the arrays live in LDS when
+// they fit, in the level's global scratch otherwise.
 constexpr int kStlNT = 1024;
 constexpr int kStlWaves = kStlNT / 64;
-constexpr int kStlRegBlocks = 4;               // 64-element blocks per wave in registers (team_pass_rg;
-                                               // 8 spills at the 128 VGPRs of a 1024-thread workgroup)
-constexpr int kStlMulti = 64 * kStlRegBlocks;  // longer ranges: all 16 waves; shorter: wave 0
-constexpr int kStlLds = 96 * 1024;             // dynamic LDS of k_select_stl
+constexpr int kStlLds = 160 * 1024 - 256;      // dynamic LDS of k_select_stl: the engine's, then the arrays
 
 __device__ __forceinline__ unsigned sel_key(unsigned v) { return v >> 24; }
 __device__ __forceinline__ unsigned sel_key(unsigned long long v) { return (unsigned)(v >> 32); }
@@ -1024,6 +1021,12 @@ __device__ __forceinline__ unsigned harris_key(float f) {
     if ((u << 1) == 0u) u = 0u;
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+
+typedef unsigned long long u64;
+// a wave-uniform value read from memory, declared uniform (keeps the pass's control flow scalar)
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ unsigned uni(unsigned x) { return (unsigned)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ u64 uni(u64 x) { return ((u64)uni((unsigned)(x >> 32)) << 32) | uni((unsigned)x); }
 
 __device__ __forceinline__ int lane_rank(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -1068,7 +1071,7 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
         nl = nr = 0;
 #pragma unroll
         for (int i = 0; i < NW; ++i) {
-            const int x = s[2 * i], y = s[2 * i + 1];
+            const int x = uni(s[2 * i]), y = uni(s[2 * i + 1]);
             pl += i < w ? x : 0;
             pr += i < w ? y : 0;
             nl += x;
@@ -1095,7 +1098,7 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
         if (lane == 0) s[2 * NW + w] = km;
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < NW; ++i) km = max(km, s[2 * NW + i]);
+        for (int i = 0; i < NW; ++i) km = max(km, uni(s[2 * NW + i]));
     }
     const int K = km;
     // mailboxes: the k-th L and the k-th R from the right (k < K); the cut's two candidates
@@ -1141,234 +1144,354 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
     team_sync<NW>();
     n_r = nr;
     int cut = INT_MAX;
-    if (K < nl) cut = s[3 * NW];
-    if (K > 0) cut = min(cut, s[3 * NW + 1]);
+    if (K < nl) cut = uni(s[3 * NW]);
+    if (K > 0) cut = min(cut, uni(s[3 * NW + 1]));
     return cut;
 }
 
-// team_pass with the range held in registers (every range of up to NW x 64 x kStlRegBlocks
-// elements), organised around the crossing: g(x) = #L in [f0, x) - #R in [x, l) never decreases,
-// the max-min K sits where it crosses zero (K = max(#R from x*, #L before x* - 1), x* the first
-// position with g >= 0), and the swapped elements are exactly the L ones before x* - 1 and the R
-// ones from x* on (the first K L's all lie before x*, the last K R's all from x* - 1 on).  So a
-// block wholly before x* - 1 writes its L elements to the L mailboxes by rank and later takes its
-// partners from the R mailboxes; a block wholly from x* on does the converse; only the one or two
-// blocks around x* test ranks against K per lane.  The block masks are two ballots, prefix counts
-// and the crossing are scalar popcounts (plus one ballot in the crossing block), so a block costs
-// ~20 instructions per pass.  (The generic team_pass re-reads LDS in each of four sweeps and
-// shuffles K across lanes; a per-lane rank / compare form of this one still cost ~150 VALU
-// instructions per block: 1.7 us per pass on 300 elements, 60 us per level-0 select at C3.)
-// Two LDS round trips per pass on one wave; NW waves add four barriers.
-// kPivot: [f0 - 1, l) is an introselect range — the median of 3 of (f0, f0 - 1 + (l - f0 + 1) / 2,
-// l - 1), i.e. libstdc++'s (first + 1, first + n / 2, last - 1), becomes the pivot (its slot takes
-// A[f0 - 1]'s element, A[f0 - 1] the pivot), L = !(x > P), R = !(P > x); otherwise [f0, l) is
-// std::partition'ed by x >= thr (L = x < thr, R = x >= thr).  s: >= 4 NW + 4 ints (NW > 1).
-template <int NW, bool kPivot, class T>
-__device__ __forceinline__ int team_pass_rg(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f0, int l,
-                                            unsigned thr, int* s, int& n_r) {
-    constexpr int MB = kStlRegBlocks;
-    typedef unsigned long long u64;
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int nb = (l - f0 + 63) >> 6;
-    const int b0 = w * nb / NW, cnt = (w + 1) * nb / NW - b0;  // this wave's blocks
-    const int base0 = f0 + 64 * b0;                              // their first position
-    // ---- loads (one round trip): the wave's blocks, the pivot slot and the median-of-3 candidates
-    T v[MB];
+// ---- the pass engine
+// Between passes the array lives in memory (LDS, or the level's global scratch).  A pass loads
+// exactly its range into registers, densely (block j = the 64 positions from 64 j, one per lane;
+// NB blocks, a power of two fixed at compile time), partitions it there and stores it back: its
+// instruction count follows the range, so the long tail of short introselect steps stays cheap
+// (a wave issues ~3.5 cycles per instruction here; a pass that paid for a fixed 8-block layout
+// cost ~4000 cycles whatever its range).  Ranges of up to kRgWave run on wave 0 alone: pivot
+// candidates are broadcast loads, the crossing and the cut come from scalar popcounts and one
+// ballot, the mailboxes need no barrier.  Longer ranges (up to RgCap: 8192 u32 / 4096 u64) run as
+// team passes over about four waves (one per SIMD; up to 16 with 8 blocks each): counts, crossing
+// candidates and every L / R with its position go through LDS, three barriers a pass.
+// The crossing (per wave, the K of the Hoare formulation above): g(x) = #L in [lo, x) -
+// #R in [x, l) never decreases, K = max(#R from x*, #L before x* - 1) at the first x* with
+// g(x*) >= 0 (K = 0 when there is no R), so only the block holding x* needs per-lane work.
+template <class T> struct RgCap { static constexpr int v = sizeof(T) == 4 ? 8192 : 4096; };
+constexpr int kRgCap32 = 8192;                 // C4 level 0: ~6.9k FAST candidates
+constexpr int kRgWave = 512;                   // wave-0 passes up to 8 blocks
+constexpr int kRgMail = 16400;                 // bytes per mailbox: (8192 / 2 + 1) u32 = (4096 / 2 + 1) u64
+constexpr int kRgBytes = 4 * kRgMail + 32 + 64 * 4 + 32;  // + 4 spare slots + 64 ints; 16-aligned
+static_assert(kRgBytes % 16 == 0, "engine scratch alignment");
+
+// the engine's LDS: value mailboxes bl / br, position mailboxes lp / rp (team passes), a few ints
+// (per-wave counts and crossing candidates, results)
+struct RgLds {
+    unsigned char* p;
+    template <class T> __device__ __forceinline__ T* bl() const { return reinterpret_cast<T*>(p); }
+    template <class T> __device__ __forceinline__ T* br() const { return reinterpret_cast<T*>(p + kRgMail); }
+    __device__ __forceinline__ int* lp() const { return reinterpret_cast<int*>(p + 2 * kRgMail); }
+    __device__ __forceinline__ int* rp() const { return reinterpret_cast<int*>(p + 3 * kRgMail); }
+    __device__ __forceinline__ int* s() const { return reinterpret_cast<int*>(p + 4 * kRgMail + 32); }
+};
+
+// bits [lo, hi) of a 64-lane block (clamped)
+__device__ __forceinline__ u64 lane_bits(int lo, int hi) {
+    lo = max(lo, 0);
+    hi = min(hi, 64);
+    if (hi <= lo) return 0ull;
+    const u64 a = ~0ull << lo;
+    return hi >= 64 ? a : a & ((1ull << hi) - 1ull);
+}
+// position x of the blocks starting at q0 := val (x anywhere; compares positions, never the block
+// index with a runtime value: GVN would turn v[i] into a dynamically indexed v[j] -> scratch)
+template <int NB, class T>
+__device__ __forceinline__ void rg_put(T (&v)[NB], int q0, int x, T val) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int j = 0; j < MB; ++j) {
-        const int p = base0 + 64 * j + lane;
-        v[j] = (j < cnt && p < l) ? A[p] : T(0);
+    for (int i = 0; i < NB; ++i)
+        if (q0 + 64 * i + lane == x) v[i] = val;
+}
+// __move_median_to_first(first, a, b, c, greater): the median's position; pv its value
+template <class T>
+__device__ __forceinline__ int stl_median(int a, int b, int c, T va, T vb, T vc, T& pv) {
+    const unsigned ka = sel_key(va), kb = sel_key(vb), kc = sel_key(vc);
+    int m;
+    if (ka > kb) m = kb > kc ? b : ka > kc ? c : a;
+    else m = ka > kc ? a : kb > kc ? c : b;
+    pv = m == a ? va : m == b ? vb : vc;
+    return m;
+}
+template <int NB, class T>
+__device__ __forceinline__ void rg_load(T (&v)[NB], const T* __restrict__ A, int q0, int len) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int q = q0 + 64 * j + lane;
+        v[j] = q < len ? A[q] : T(0);
     }
-    int m = -1;
-    T oldf = T(0), pv = T(0);
+}
+template <int NB, class T>
+__device__ __forceinline__ void rg_store(const T (&v)[NB], T* __restrict__ A, int q0, int len) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int q = q0 + 64 * j + lane;
+        if (q < len) A[q] = v[j];
+    }
+}
+
+// Per block and lane the pass keeps one int, the lane code: bit 0 L, bit 1 R, bits 2..8 the L
+// and bits 9..15 the R below the lane in the block (in range); per block one uniform int, #L |
+// #R << 16.
+__device__ __forceinline__ int lane_code(u64 ml, u64 mr) {
+    const int lane = threadIdx.x & 63;
+    return (int)((ml >> lane) & 1ull) | ((int)((mr >> lane) & 1ull) << 1) | (lane_rank(ml) << 2) |
+           (lane_rank(mr) << 9);
+}
+__device__ __forceinline__ int code_lrank(int c) { return (c >> 2) & 127; }
+__device__ __forceinline__ int code_rrank(int c) { return (c >> 9) & 127; }
+
+// Block masks of the range [lo, len) for the blocks from q0: key <= P / < P (L), >= P (R)
+template <int NB, bool kPivot, class T>
+__device__ __forceinline__ int rg_masks(const T (&v)[NB], int q0, int lo, int len, unsigned P, int (&code)[NB],
+                                        int (&cnt)[NB]) {
+    int cr = 0;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const u64 in = lane_bits(lo - q0 - 64 * j, len - q0 - 64 * j);
+        const unsigned k = sel_key(v[j]);
+        const u64 ml = __ballot(kPivot ? k <= P : k < P) & in, mr = __ballot(k >= P) & in;
+        code[j] = lane_code(ml, mr);
+        cnt[j] = __popcll(ml) | (__popcll(mr) << 16);
+        cr += __popcll(mr);
+    }
+    return cr;
+}
+
+// The crossing in one wave's blocks (prefix counts ql / qr of the L / R before them, nr R in the
+// whole range): K if x* lies in them, else 0.
+template <int NB>
+__device__ __forceinline__ int rg_crossing(const int (&code)[NB], const int (&cnt)[NB], int ql, int qr, int nr) {
+    int K = 0;
+    bool done = false;
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+        if (!done) {
+            const int cl = cnt[j] & 0xffff, cr = cnt[j] >> 16;
+            const int gs = ql + qr - nr;
+            if (gs < 0 && gs + cl + cr >= 0) {
+                // g(start + i + 1) over the lanes (the last in-range lane has g(l) = #L >= 0); the
+                // first lane t reaching 0 gives x* = start + t + 1
+                const int c = code[j];
+                const int gi = gs + code_lrank(c) + code_rrank(c) + (c & 1) + ((c >> 1) & 1);
+                const int t = __ffsll((long long)__ballot(gi >= 0)) - 1;
+                const int ct = __builtin_amdgcn_readlane(c, t);
+                // K = max(#R in [x*, l), #L in [lo, x* - 1))
+                K = max(nr - (qr + code_rrank(ct) + ((ct >> 1) & 1)), ql + code_lrank(ct));
+                done = true;
+            }
+            ql += cl;
+            qr += cr;
+        }
+    return K;
+}
+
+// One pass by wave 0 alone over A[0, len) (A = the range's first element): kPivot, an
+// introselect step (median of (1, len / 2, len - 1) moved to 0, unguarded partition of [1, len)
+// around it, L = !(x > P), R = !(P > x)); otherwise std::partition of [0, len) by key >= thr
+// (L = key < thr, R = key >= thr).  Returns the cut (relative to A); n_r = #R.
+template <int NB, bool kPivot, class T>
+__device__ __forceinline__ int rg_wave_pass(T* __restrict__ A, int len, unsigned thr, T* __restrict__ bl,
+                                            T* __restrict__ br, int& n_r) {
+    T v[NB];
+    rg_load(v, A, 0, len);
     unsigned P = thr;
-    if (kPivot) {  // __move_median_to_first(first, first + 1, mid, last - 1, greater)
-        const int f = f0 - 1, a = f0, b = f + (l - f) / 2, c = l - 1;
-        oldf = A[f];
-        const T va = A[a], vb = A[b], vc = A[c];
-        const unsigned ka = sel_key(va), kb = sel_key(vb), kc = sel_key(vc);
-        if (ka > kb) m = kb > kc ? b : ka > kc ? c : a;
-        else m = ka > kc ? a : kb > kc ? c : b;
-        pv = m == a ? va : m == b ? vb : vc;
+    int lo = 0;
+    if (kPivot) {
+        const int b = len / 2, c = len - 1;
+        const T vf = uni(A[0]), va = uni(A[1]), vb = uni(A[b]), vc = uni(A[c]);
+        T pv;
+        const int m = stl_median(1, b, c, va, vb, vc, pv);
         P = sel_key(pv);
-#pragma unroll
-        for (int j = 0; j < MB; ++j)
-            if (j < cnt && base0 + 64 * j + lane == m) v[j] = oldf;
+        rg_put(v, 0, 0, pv);
+        rg_put(v, 0, m, vf);
+        lo = 1;
     }
-    auto isl = [P](T x) { return kPivot ? sel_key(x) <= P : sel_key(x) < P; };
-    auto isr = [P](T x) { return sel_key(x) >= P; };
-    // ---- block masks (uniform) and this wave's counts
-    u64 ml[MB], mr[MB];
-    int cl = 0, cr = 0;
-#pragma unroll
-    for (int j = 0; j < MB; ++j) {
-        ml[j] = mr[j] = 0ull;
-        if (j < cnt) {
-            const int rem = l - (base0 + 64 * j);
-            const u64 in = rem >= 64 ? ~0ull : ((1ull << rem) - 1ull);
-            ml[j] = __ballot(isl(v[j])) & in;
-            mr[j] = __ballot(isr(v[j])) & in;
-            cl += __popcll(ml[j]);
-            cr += __popcll(mr[j]);
-        }
-    }
-    int pl = 0, pr = 0, nr = cr;
-    if (NW > 1) {
-        if (lane == 0) {
-            s[2 * w] = cl;
-            s[2 * w + 1] = cr;
-        }
-        __syncthreads();
-        nr = 0;
-#pragma unroll
-        for (int i = 0; i < NW; ++i) {
-            pl += i < w ? s[2 * i] : 0;
-            pr += i < w ? s[2 * i + 1] : 0;
-            nr += s[2 * i + 1];
-        }
-    }
-    // ---- the crossing x* and K: the wave whose range holds x* (g(start) < 0 <= g(end), or x* = f0)
-    int xs = -1, K = 0;
+    int code[NB], cnt[NB];
+    const int nr = rg_masks<NB, kPivot>(v, 0, lo, len, P, code, cnt);
+    const int K = rg_crossing(code, cnt, 0, 0, nr);
+    // the cut min(L[K], R[K - 1]) (the L of rank K, the R of left rank nr - K), the mailboxes
+    int cut = INT_MAX;
     {
-        int ql = pl, qr = pr;
-        const bool first_wave = b0 == 0;
+        int ql = 0, qr = 0;
 #pragma unroll
-        for (int j = 0; j < MB; ++j)
-            if (j < cnt && xs < 0) {
-                const int start = base0 + 64 * j;
-                const int gs = ql + qr - nr;
-                const int ge = gs + __popcll(ml[j]) + __popcll(mr[j]);
-                if (gs >= 0 && j == 0 && first_wave) {  // x* = f0: no R at all (partition of an all-L tail)
-                    xs = start;
-                    K = 0;
-                } else if (gs < 0 && ge >= 0) {
-                    // g(start + i + 1) over the lanes; the first lane reaching 0 gives x* = start + t + 1
-                    const int own = (int)((ml[j] >> lane) & 1ull) + (int)((mr[j] >> lane) & 1ull);
-                    const int gi = gs + lane_rank(ml[j]) + lane_rank(mr[j]) + own;
-                    const u64 hit = __ballot(gi >= 0) & ~0ull;
-                    const int t = __ffsll((long long)hit) - 1;
-                    xs = start + t + 1;
-                    const u64 bt = (1ull << t) - 1ull;  // positions below start + t
-                    const int lbefore = ql + __popcll(ml[j] & bt);                                 // #L in [f0, x* - 1)
-                    const int rfrom = nr - (qr + __popcll(mr[j] & (t == 63 ? ~0ull : ((bt << 1) | 1ull))));  // #R in [x*, l)
-                    K = max(rfrom, lbefore);
-                }
-                ql += __popcll(ml[j]);
-                qr += __popcll(mr[j]);
-            }
-    }
-    if (NW > 1) {
-        if (lane == 0 && xs >= 0) {
-            s[2 * NW] = xs;
-            s[2 * NW + 1] = K;
+        for (int j = 0; j < NB; ++j) {
+            const int cl = cnt[j] & 0xffff, cr = cnt[j] >> 16, c = code[j];
+            const bool il = c & 1, ir = c & 2;
+            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
+            if (K >= ql && K < ql + cl) cut = min(cut, 64 * j + __ffsll((long long)__ballot(il && a == K)) - 1);
+            if (K > 0 && nr - K >= qr && nr - K < qr + cr)
+                cut = min(cut, 64 * j + __ffsll((long long)__ballot(ir && b == K - 1)) - 1);
+            if (il && a < K) bl[a] = v[j];
+            if (ir && b < K) br[b] = v[j];
+            ql += cl;
+            qr += cr;
         }
-        __syncthreads();
-        xs = s[2 * NW];
-        K = s[2 * NW + 1];
     }
-    // ---- the cut min(L[K], R[K-1]) (the L of rank K, the R of left rank nr - K) and the mailboxes
-    int cutw = INT_MAX;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     {
-        int ql = pl, qr = pr;
+        int ql = 0, qr = 0;
 #pragma unroll
-        for (int j = 0; j < MB; ++j)
-            if (j < cnt) {
-                const int start = base0 + 64 * j;
-                const int nlj = __popcll(ml[j]), nrj = __popcll(mr[j]);
-                const int rl = ql + lane_rank(ml[j]);           // L rank of this lane (if L)
-                const int rr = nr - 1 - (qr + lane_rank(mr[j]));  // R rank from the right (if R)
-                const bool il = (ml[j] >> lane) & 1ull, ir = (mr[j] >> lane) & 1ull;
-                if (K >= ql && K < ql + nlj) {
-                    const u64 hit = __ballot(il && rl == K);
-                    cutw = min(cutw, start + __ffsll((long long)hit) - 1);
-                }
-                if (K > 0 && nr - K >= qr && nr - K < qr + nrj) {
-                    const u64 hit = __ballot(ir && rr == K - 1);
-                    cutw = min(cutw, start + __ffsll((long long)hit) - 1);
-                }
-                if (start + 64 <= xs - 1) {  // wholly before x* - 1: every L swaps
-                    if (il) bl[rl] = v[j];
-                } else if (start >= xs) {    // wholly from x* on: every R swaps
-                    if (ir) br[rr] = v[j];
-                } else {
-                    if (il && rl < K) bl[rl] = v[j];
-                    if (ir && rr < K) br[rr] = v[j];
-                }
-                ql += nlj;
-                qr += nrj;
-            }
-    }
-    if (NW > 1 && lane == 0) s[3 * NW + w] = cutw;
-    team_sync<NW>();
-    int cut = cutw;
-    if (NW > 1) {
-#pragma unroll
-        for (int i = 0; i < NW; ++i) cut = min(cut, s[3 * NW + i]);
-    }
-    // ---- swap partners (all reads in flight together), then the writes
-    T nv[MB];
-    unsigned sw = 0;
-    {
-        int ql = pl, qr = pr;
-#pragma unroll
-        for (int j = 0; j < MB; ++j) {
-            nv[j] = T(0);
-            if (j < cnt) {
-                const int start = base0 + 64 * j;
-                const int rl = ql + lane_rank(ml[j]);
-                const int rr = nr - 1 - (qr + lane_rank(mr[j]));
-                const bool il = (ml[j] >> lane) & 1ull, ir = (mr[j] >> lane) & 1ull;
-                bool sl, sr;
-                if (start + 64 <= xs - 1) {
-                    sl = il;
-                    sr = false;
-                } else if (start >= xs) {
-                    sl = false;
-                    sr = ir;
-                } else {
-                    sl = il && rl < K;
-                    sr = ir && rr < K;
-                }
-                if (sl) nv[j] = br[rl];
-                else if (sr) nv[j] = bl[rr];
-                sw |= (sl || sr ? 1u : 0u) << j;
-                ql += __popcll(ml[j]);
-                qr += __popcll(mr[j]);
-            }
+        for (int j = 0; j < NB; ++j) {  // (an element is swapped at most once: its L and R ranks are never both < K)
+            const int c = code[j];
+            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
+            if ((c & 1) && a < K) v[j] = br[a];
+            else if ((c & 2) && b < K) v[j] = bl[b];
+            ql += cnt[j] & 0xffff;
+            qr += cnt[j] >> 16;
         }
     }
-#pragma unroll
-    for (int j = 0; j < MB; ++j)
-        if (j < cnt) {
-            const int p = base0 + 64 * j + lane;
-            if ((sw >> j) & 1u) A[p] = nv[j];
-            else if (p == m) A[p] = oldf;
-        }
-    if (kPivot && threadIdx.x == 0) A[f0 - 1] = pv;
-    team_sync<NW>();
+    rg_store(v, A, 0, len);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the next pass reloads; global scratch too)
     n_r = nr;
     return cut;
 }
 
-// __unguarded_partition_pivot(first = f, last = l) as one team pass; returns the cut
-template <int NW, class T>
-__device__ __forceinline__ int pivot_pass(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f, int l,
-                                          int* s) {
-    if (l - f - 1 <= NW * 64 * kStlRegBlocks) {
-        int nr;
-        return team_pass_rg<NW, true>(A, bl, br, f + 1, l, 0u, s, nr);
+// The same pass by the workgroup over A[0, len), len <= 64 NB kStlWaves: wave w holds the blocks
+// [NB w, NB (w + 1)); waves past the range only meet the barriers.
+template <int NB, bool kPivot, class T>
+__device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
+    constexpr int NW = kStlWaves;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int q0 = 64 * NB * w;
+    const bool act = q0 < len;
+    int* s = E.s();
+    T* bl = E.bl<T>();
+    T* br = E.br<T>();
+    int* lp = E.lp();
+    int* rp = E.rp();
+    T v[NB];
+    int code[NB], cnt[NB];
+    unsigned P = thr;
+    int lo = 0;
+    if (kPivot) {
+        const int b = len / 2, c = len - 1;
+        const T vf = uni(A[0]), va = uni(A[1]), vb = uni(A[b]), vc = uni(A[c]);
+        T pv;
+        const int m = stl_median(1, b, c, va, vb, vc, pv);
+        P = sel_key(pv);
+        if (act) {
+            rg_load(v, A, q0, len);
+            rg_put(v, q0, 0, pv);
+            rg_put(v, q0, m, vf);
+        }
+        lo = 1;
+    } else if (act) {
+        rg_load(v, A, q0, len);
     }
-    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
-    const T vf = A[f], va = A[a], vb = A[b], vc = A[c];
-    const unsigned ka = sel_key(va), kb = sel_key(vb), kc = sel_key(vc);
-    int m;  // __move_median_to_first(f, a, b, c, greater)
-    if (ka > kb) m = kb > kc ? b : ka > kc ? c : a;
-    else m = ka > kc ? a : kb > kc ? c : b;
-    const T pv = m == a ? va : m == b ? vb : vc;
-    const unsigned P = sel_key(pv);
-    int nr;
-    return team_pass<NW>(A, bl, br, f + 1, l, m, vf, pv, [P](T v) { return sel_key(v) <= P; },
-                         [P](T v) { return sel_key(v) >= P; }, s, nr);
+    int cl = 0, cr = 0;
+    if (act) {
+        cr = rg_masks<NB, kPivot>(v, q0, lo, len, P, code, cnt);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) cl += cnt[j] & 0xffff;
+    }
+    if (lane == 0) {
+        s[2 * w] = cl;
+        s[2 * w + 1] = cr;
+    }
+    __syncthreads();
+    int pl = 0, pr = 0, nl = 0, nr = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const int x = uni(s[2 * i]), y = uni(s[2 * i + 1]);
+        pl += i < w ? x : 0;
+        pr += i < w ? y : 0;
+        nl += x;
+        nr += y;
+    }
+    // mailboxes: every L by rank and every R by rank from the right below hb (K <= (len - lo) / 2)
+    const int hb = (len - lo) / 2 + 1;
+    if (act) {
+        const int km = rg_crossing(code, cnt, pl, pr, nr);
+        if (lane == 0) s[2 * NW + w] = km;
+        int ql = pl, qr = pr;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int c = code[j];
+            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
+            const int x = q0 + 64 * j + lane;
+            if ((c & 1) && a < hb) {
+                bl[a] = v[j];
+                lp[a] = x;
+            }
+            if ((c & 2) && b < hb) {
+                br[b] = v[j];
+                rp[b] = x;
+            }
+            ql += cnt[j] & 0xffff;
+            qr += cnt[j] >> 16;
+        }
+    } else if (lane == 0) {
+        s[2 * NW + w] = 0;
+    }
+    __syncthreads();
+    int K = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) K = max(K, uni(s[2 * NW + i]));
+    int cut = K < nl ? uni(lp[K]) : INT_MAX;
+    if (K > 0) cut = min(cut, uni(rp[K - 1]));
+    if (act) {
+        int ql = pl, qr = pr;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int c = code[j];
+            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
+            if ((c & 1) && a < K) v[j] = br[a];
+            else if ((c & 2) && b < K) v[j] = bl[b];
+            ql += cnt[j] & 0xffff;
+            qr += cnt[j] >> 16;
+        }
+        rg_store(v, A, q0, len);
+    }
+    __syncthreads();
+    n_r = nr;
+    return cut;
+}
+
+// dispatch on the range: the smallest power-of-two block count that holds it
+template <bool kPivot, class T>
+__device__ __forceinline__ int rg_wave_any(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
+    T* bl = E.bl<T>();
+    T* br = E.br<T>();
+    if (len <= 64) return rg_wave_pass<1, kPivot>(A, len, thr, bl, br, n_r);
+    if (len <= 128) return rg_wave_pass<2, kPivot>(A, len, thr, bl, br, n_r);
+    if (len <= 256) return rg_wave_pass<4, kPivot>(A, len, thr, bl, br, n_r);
+    return rg_wave_pass<8, kPivot>(A, len, thr, bl, br, n_r);
+}
+// team passes spread the blocks over about four waves (one per SIMD), 8 blocks a wave beyond that
+template <bool kPivot, class T>
+__device__ __forceinline__ int rg_team_any(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
+    const int per = ((len + 63) / 64 + 3) / 4;
+    if (per <= 2) return rg_team_pass<2, kPivot>(A, len, thr, E, n_r);
+    if (per <= 4) return rg_team_pass<4, kPivot>(A, len, thr, E, n_r);
+    return rg_team_pass<8, kPivot>(A, len, thr, E, n_r);
+}
+
+// libstdc++'s closing __insertion_sort of A[0, n) (n <= 3; a stable sort by key, descending):
+// every lane of the calling wave reads the elements, lane 0 writes them back
+template <class T>
+__device__ __forceinline__ void stl_small_sort(T* __restrict__ A, int n) {
+    if (n < 2) return;
+    T e0 = uni(A[0]), e1 = uni(A[1]), e2 = n > 2 ? uni(A[2]) : T(0);
+    if (sel_key(e1) > sel_key(e0)) {
+        const T t = e0;
+        e0 = e1;
+        e1 = t;
+    }
+    if (n > 2 && sel_key(e2) > sel_key(e1)) {
+        const T t = e1;
+        e1 = e2;
+        e2 = t;
+        if (sel_key(e1) > sel_key(e0)) {
+            const T u = e0;
+            e0 = e1;
+            e1 = u;
+        }
+    }
+    if ((threadIdx.x & 63) == 0) {
+        A[0] = e0;
+        A[1] = e1;
+        if (n > 2) A[2] = e2;
+    }
 }
 
 // libstdc++ __adjust_heap / __push_heap / __make_heap / __heap_select with comp = greater (one lane)
@@ -1429,23 +1552,51 @@ __device__ void stl_insertion_sort(T* A, int f, int l) {
     }
 }
 
-// std::nth_element(A, A + nth, A + n, greater); every thread of the workgroup calls it
+// __unguarded_partition_pivot(first = f, last = l) as one team pass over memory (ranges longer than
+// the engine takes); bl / br: mailboxes of (l - f) / 2 + 1 elements.  Returns the cut.
+template <class T>
+__device__ __forceinline__ int pivot_pass_mem(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int f, int l,
+                                              int* s) {
+    const int a = f + 1, b = f + (l - f) / 2, c = l - 1;
+    const T vf = uni(A[f]), va = uni(A[a]), vb = uni(A[b]), vc = uni(A[c]);
+    T pv;
+    const int m = stl_median(a, b, c, va, vb, vc, pv);
+    const unsigned P = sel_key(pv);
+    int nr;
+    return team_pass<kStlWaves>(A, bl, br, f + 1, l, m, vf, pv, [P](T v) { return sel_key(v) <= P; },
+                                [P](T v) { return sel_key(v) >= P; }, s, nr);
+}
+
+// std::nth_element(A, A + nth, A + n, greater); every thread of the workgroup calls it.  Ranges
+// beyond the engine's capacity first take team passes over memory (bl / br: n / 2 + 1 each).
 template <class T>
 __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int n,
-                                                int nth, int* s) {
+                                                int nth, const RgLds& E) {
     if (n <= 0 || nth >= n) return;
     int f = 0, l = n, depth = 2 * (31 - __clz(n));
     bool heap = false;
-    while (l - f > kStlMulti) {
+    while (l - f > RgCap<T>::v) {
         if (depth == 0) {
             heap = true;
             break;
         }
         --depth;
-        const int cut = pivot_pass<kStlWaves>(A, bl, br, f, l, s);
+        const int cut = pivot_pass_mem(A, bl, br, f, l, E.s());
         if (cut <= nth) f = cut;
         else l = cut;
     }
+    while (!heap && l - f > kRgWave) {
+        if (depth == 0) {
+            heap = true;
+            break;
+        }
+        --depth;
+        int nr;
+        const int cut = f + rg_team_any<true>(A + f, l - f, 0u, E, nr);
+        if (cut <= nth) f = cut;
+        else l = cut;
+    }
+    VX_KT(2);
     if ((threadIdx.x >> 6) == 0) {
         while (!heap && l - f > 3) {
             if (depth == 0) {
@@ -1453,47 +1604,53 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
                 break;
             }
             --depth;
-            const int cut = pivot_pass<1>(A, bl, br, f, l, s);
+            int nr;
+            const int cut = f + rg_wave_any<true>(A + f, l - f, 0u, E, nr);
             if (cut <= nth) f = cut;
             else l = cut;
         }
-        if (threadIdx.x == 0) {
-            if (heap) {
+        if (!heap) {
+            stl_small_sort(A + f, l - f);
+        } else {  // introselect's depth limit: __heap_select + iter_swap (one lane)
+            if (threadIdx.x == 0) {
                 stl_heap_select(A + f, nth + 1 - f, l - f);
                 const T t = A[f];
                 A[f] = A[nth];
                 A[nth] = t;
-            } else {
-                stl_insertion_sort(A, f, l);
             }
         }
+        VX_KT(3);
     }
     __syncthreads();
 }
 
-// KeyPointsFilter::retainBest(A[0..size), npts): returns the kept length; every thread calls it
+// KeyPointsFilter::retainBest(A[0..size), npts): nth_element, then std::partition of the tail by
+// key >= the npts-th key.  Returns the kept length; every thread calls it.
 template <class T>
 __device__ __forceinline__ int stl_retain_best(T* __restrict__ A, T* __restrict__ bl, T* __restrict__ br, int size,
-                                               int npts, int* s) {
+                                               int npts, const RgLds& E) {
     if (size <= npts) return size;
     if (npts <= 0) return 0;
-    stl_nth_element(A, bl, br, size, npts - 1, s);
-    const unsigned thr = sel_key(A[npts - 1]);
-    auto isl = [thr](T v) { return sel_key(v) < thr; };
-    auto isr = [thr](T v) { return sel_key(v) >= thr; };
+    stl_nth_element(A, bl, br, size, npts - 1, E);
+    VX_KT(4);
+    const unsigned thr = uni(sel_key(A[npts - 1]));
+    const int len = size - npts;
+    int* s = E.s();
     int nr = 0;
-    if (size - npts > kStlWaves * kStlMulti) {
-        team_pass<kStlWaves>(A, bl, br, npts, size, -1, T(0), T(0), isl, isr, s, nr);
-    } else if (size - npts > kStlMulti) {
-        team_pass_rg<kStlWaves, false>(A, bl, br, npts, size, thr, s, nr);
+    if (len > RgCap<T>::v) {
+        team_pass<kStlWaves>(A, bl, br, npts, size, -1, T(0), T(0), [thr](T v) { return sel_key(v) < thr; },
+                             [thr](T v) { return sel_key(v) >= thr; }, s, nr);
+    } else if (len > kRgWave) {
+        rg_team_any<false>(A + npts, len, thr, E, nr);
     } else {
         if ((threadIdx.x >> 6) == 0) {
-            team_pass_rg<1, false>(A, bl, br, npts, size, thr, s, nr);
-            if (threadIdx.x == 0) s[4 * kStlWaves + 2] = nr;
+            rg_wave_any<false>(A + npts, len, thr, E, nr);
+            if (threadIdx.x == 0) s[60] = nr;
         }
         __syncthreads();
-        nr = s[4 * kStlWaves + 2];
+        nr = uni(s[60]);
     }
+    VX_KT(5);
     return npts + nr;
 }
 
@@ -1508,8 +1665,8 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
                                                        CandRec* __restrict__ stage, int* __restrict__ level_count,
                                                        int* __restrict__ dbg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
-    __shared__ int s[4 * kStlWaves + 4];
     __shared__ int sw[kStlWaves];
+    const RgLds E{sdyn};
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
     cand += blockIdx.z * a.fs_cells * kCellCap;
@@ -1526,10 +1683,14 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
     unsigned* gA1 = reinterpret_cast<unsigned*>(gscr);
     const int q = a.quota[l];
     const int k1 = 2 * q;
-    constexpr int kCap1 = (kStlLds - 64) / 8;  // pass-1 elements that fit in LDS with their mailboxes
-    unsigned* lA1 = reinterpret_cast<unsigned*>(sdyn);
+    // LDS after the engine's scratch: the pass-1 elements and the candidates' Harris keys (up to
+    // kRgCap32 each), later the pass-2 elements over them
+    unsigned* lA1 = reinterpret_cast<unsigned*>(sdyn + kRgBytes);
+    unsigned* lhk = lA1 + kRgCap32;
+    static_assert(kRgBytes + 8 * kRgCap32 <= kStlLds, "k_select_stl LDS");
     // ---- every border-passing NMS corner in raster (cell) order: records to kept[], pass-1
-    // elements (score << 24 | raster index) to LDS (when they fit) and to the global scratch
+    // elements (score << 24 | raster index) to the global scratch and (when they fit) to LDS with
+    // the Harris keys
     const int cpt = min(kCellsPer, (ncell + kStlNT - 1) / kStlNT);
     int n0 = 0;
     for (int base = 0; base < ncell; base += kStlNT * cpt) {
@@ -1559,84 +1720,105 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
             kept[pos] = r;
             const unsigned e = ((unsigned)r.score << 24) | (unsigned)pos;
             gA1[pos] = e;
-            if (pos < kCap1) lA1[pos] = e;
+            if (pos < kRgCap32) {
+                lA1[pos] = e;
+                lhk[pos] = harris_key(r.harris);
+            }
             ++pos;
         };
 #pragma unroll
         for (int k = 0; k < kRecBatch; ++k)
             if (k < tot) put(rr[k]);
         for (int k = kRecBatch; k < tot; ++k) put(cand[rec_index(k)]);
-        n0 += btot;
+        n0 += uni(btot);
     }
     __syncthreads();
     VX_KT(9);
-    // ---- retainBest(2q) by FAST score (the pass-1 elements are u32, mailboxes of n0 / 2 + 1 each)
+    // ---- retainBest(2q) by FAST score (u32 elements; beyond the engine's capacity the first
+    // passes run over the global scratch with mailboxes of n0 / 2 + 1 each after it)
     const int hb = n0 / 2 + 1;
     int K1;
-    const bool lds1 = n0 <= kCap1;
-    if (lds1) K1 = stl_retain_best(lA1, lA1 + n0, lA1 + n0 + hb, n0, k1, s);
-    else K1 = stl_retain_best(gA1, gA1 + n0, gA1 + n0 + hb, n0, k1, s);
-    // ---- retainBest(q) by Harris over the survivors in their new order (u64 elements)
-    const long long o2 = ((long long)(n0 + 2 * hb) * 4 + 15) & ~15ll;  // bytes after the pass-1 arrays
-    const int hb2 = K1 / 2 + 1;
-    const bool lds2 = lds1 && o2 + (long long)(K1 + 2 * hb2) * 8 <= kStlLds;
-    unsigned long long* A2 = lds2 ? reinterpret_cast<unsigned long long*>(sdyn + o2)
-                                  : reinterpret_cast<unsigned long long*>(gscr + 16 * (long long)cap);
+    const bool lds1 = n0 <= kRgCap32;
+    if (lds1) K1 = stl_retain_best(lA1, (unsigned*)nullptr, (unsigned*)nullptr, n0, k1, E);
+    else K1 = stl_retain_best(gA1, gA1 + n0, gA1 + n0 + hb, n0, k1, E);
+    // ---- retainBest(q) by Harris over the survivors in their new order (u64 elements: in LDS over
+    // the pass-1 arrays when they fit the engine, else in the global scratch after the pass-1 one)
+    constexpr int kCap2 = RgCap<u64>::v;
+    const bool lds2 = K1 <= kCap2;
+    u64* L2 = reinterpret_cast<u64*>(sdyn + kRgBytes);
+    u64* G2 = reinterpret_cast<u64*>(gscr + 16 * (long long)cap);
     VX_KT(10);
-    const unsigned* A1 = lds1 ? lA1 : gA1;
+    long long doff = 2 * kMaxLevels;
     if (dbg) {
-        long long off = 2 * kMaxLevels;
-        for (int i = 0; i < l; ++i) off += a.level_cap[i];
+        for (int i = 0; i < l; ++i) doff += a.level_cap[i];
         if (tid == 0) {
             dbg[l] = n0;
             dbg[kMaxLevels + l] = K1;
         }
-        for (int j = tid; j < K1; j += kStlNT) dbg[off + j] = (int)(A1[j] & 0xffffffu);
     }
-    for (int j = tid; j < K1; j += kStlNT) {
-        const unsigned idx = A1[j] & 0xffffffu;
-        A2[j] = ((unsigned long long)harris_key(kept[idx].harris) << 32) | idx;
+    auto elem2 = [&](int j) -> u64 {
+        const unsigned idx = (lds1 ? lA1[j] : gA1[j]) & 0xffffffu;
+        if (dbg) dbg[doff + j] = (int)idx;
+        const unsigned hk = lds1 ? lhk[idx] : harris_key(kept[idx].harris);
+        return ((u64)hk << 32) | idx;
+    };
+    if (lds2) {
+        constexpr int kPer = kCap2 / kStlNT;
+        u64 e2[kPer];
+#pragma unroll
+        for (int i = 0; i < kPer; ++i) e2[i] = tid + i * kStlNT < K1 ? elem2(tid + i * kStlNT) : 0ull;
+        __syncthreads();  // (L2 overlays the pass-1 arrays)
+#pragma unroll
+        for (int i = 0; i < kPer; ++i)
+            if (tid + i * kStlNT < K1) L2[tid + i * kStlNT] = e2[i];
+    } else {
+        for (int j = tid; j < K1; j += kStlNT) G2[j] = elem2(j);
     }
     __syncthreads();
     VX_KT(11);
     int K2;
     if (lds2) {  // (separate call sites: the LDS one compiles to ds_ instructions)
-        unsigned long long* L2 = reinterpret_cast<unsigned long long*>(sdyn + o2);
-        K2 = stl_retain_best(L2, L2 + K1, L2 + K1 + hb2, K1, q, s);
+        K2 = stl_retain_best(L2, (u64*)nullptr, (u64*)nullptr, K1, q, E);
     } else {
-        unsigned long long* G2 = reinterpret_cast<unsigned long long*>(gscr + 16 * (long long)cap);
-        K2 = stl_retain_best(G2, G2 + K1, G2 + K1 + hb2, K1, q, s);
+        const int hb2 = K1 / 2 + 1;
+        K2 = stl_retain_best(G2, G2 + K1, G2 + K1 + hb2, K1, q, E);
     }
     VX_KT(13);
-    for (int j = tid; j < K2; j += kStlNT) fin[j] = kept[(unsigned)A2[j]];
+    for (int j = tid; j < K2; j += kStlNT) fin[j] = kept[(unsigned)(lds2 ? L2[j] : G2[j])];
     if (tid == 0) level_count[l] = K2;
     VX_KT(15);
 }
 
-// Test hook (vx_test_retain_best): retainBest over caller keys through the device code above.
+// Test hook (vx_test_retain_best): retainBest over caller keys through the device code above
+// (A in LDS after the engine's scratch, or in the global scratch; mailboxes for the passes beyond
+// the engine after A).
 template <class T>
 __device__ __forceinline__ void test_retain_body(T* A, const unsigned* __restrict__ keys, int n, int npts,
-                                                 int* __restrict__ out, int* s) {
+                                                 int* __restrict__ out, const RgLds& E) {
     const int hb = n / 2 + 1;
     for (int i = threadIdx.x; i < n; i += kStlNT)
-        A[i] = sizeof(T) == 4 ? (T)((keys[i] << 24) | (unsigned)i) : (T)(((unsigned long long)keys[i] << 32) | (unsigned)i);
+        A[i] = sizeof(T) == 4 ? (T)((keys[i] << 24) | (unsigned)i) : (T)(((u64)keys[i] << 32) | (unsigned)i);
     __syncthreads();
-    const int K = stl_retain_best(A, A + n, A + n + hb, n, npts, s);
+    VX_KT(1);
+    const int K = stl_retain_best(A, A + n, A + n + hb, n, npts, E);
     for (int j = threadIdx.x; j < K; j += kStlNT) out[1 + j] = (int)(sizeof(T) == 4 ? (A[j] & 0xffffffu) : (unsigned)A[j]);
     if (threadIdx.x == 0) out[0] = K;
+    VX_KT(6);
 }
 
 __global__ __launch_bounds__(kStlNT) void k_test_retain(const unsigned* __restrict__ keys, int n, int npts, int wide,
                                                         int use_lds, unsigned char* __restrict__ gscr,
                                                         int* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
-    __shared__ int s[4 * kStlWaves + 4];
+    VX_KT(0);
+    const RgLds E{sdyn};
+    unsigned char* ra = sdyn + kRgBytes;
     if (!wide) {
-        if (use_lds) test_retain_body(reinterpret_cast<unsigned*>(sdyn), keys, n, npts, out, s);
-        else test_retain_body(reinterpret_cast<unsigned*>(gscr), keys, n, npts, out, s);
+        if (use_lds) test_retain_body(reinterpret_cast<unsigned*>(ra), keys, n, npts, out, E);
+        else test_retain_body(reinterpret_cast<unsigned*>(gscr), keys, n, npts, out, E);
     } else {
-        if (use_lds) test_retain_body(reinterpret_cast<unsigned long long*>(sdyn), keys, n, npts, out, s);
-        else test_retain_body(reinterpret_cast<unsigned long long*>(gscr), keys, n, npts, out, s);
+        if (use_lds) test_retain_body(reinterpret_cast<u64*>(ra), keys, n, npts, out, E);
+        else test_retain_body(reinterpret_cast<u64*>(gscr), keys, n, npts, out, E);
     }
 }
 
@@ -2309,7 +2491,8 @@ int vx_test_retain_best(vx_ctx* c, const uint32_t* keys, int n, int npts, int wi
         for (int i = 0; i < n; ++i)
             if (keys[i] > 255u) return set_error(c, VX_ERR_INVALID, "narrow keys must be <= 255");
     const int64_t esz = wide ? 8 : 4, need = esz * ((int64_t)n + 2 * (n / 2 + 1));
-    if (use_lds && need > kStlLds) return set_error(c, VX_ERR_INVALID, "%lld bytes exceed the LDS", (long long)need);
+    if (use_lds && need > kStlLds - kRgBytes)
+        return set_error(c, VX_ERR_INVALID, "%lld bytes exceed the LDS", (long long)need);
     VX_HIP(c, hipSetDevice(c->device));
     void *dk = nullptr, *ds = nullptr, *dout = nullptr;
     int rc = VX_OK;
@@ -2322,7 +2505,7 @@ int vx_test_retain_best(vx_ctx* c, const uint32_t* keys, int n, int npts, int wi
         (void)attr;
         hipError_t e = hipMemcpyAsync(dk, keys, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_test_retain, dim3(1), dim3(kStlNT), use_lds ? kStlLds : 0, c->stream,
+            hipLaunchKernelGGL(k_test_retain, dim3(1), dim3(kStlNT), kStlLds, c->stream,
                                (const unsigned*)dk, n, npts, wide, use_lds, (unsigned char*)ds, (int*)dout);
             e = hipGetLastError();
         }
