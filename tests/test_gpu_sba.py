@@ -58,10 +58,12 @@ def test_sba_reduced_system_matches_restatement(ctx, oracle):
         plan.close()
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5", "C5-small"])
 def test_sba_baseline_configs(ctx, oracle, cfg):
-    nk, nl, ns = synth.ba_config(cfg)
-    if cfg == "C5":  # 8 streams: 8 independent covisibility components (one dense solve each)
+    # C4: 100 KF / 50k, one stream; C5: the true 200 KF / 100k over 8 streams (BASELINE configs[4]:
+    # 8 independent covisibility components, one dense solve each); C5-small: 96 KF / 16k, 8 streams
+    nk, nl, ns = synth.ba_config(cfg.split("-")[0])
+    if cfg == "C5-small":
         nk, nl = 8 * 12, 16000
     m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=ns * 2)
     st_g, st_c = _case(ctx, oracle, m, dict(window=nk, iters=8))
