@@ -341,7 +341,7 @@ def main():
                          "(vx_set_grid_share; default 1/4 with more than one stream, 1 otherwise: DESIGN.md §7)")
     ap.add_argument("--streams", type=int, default=3, choices=(1, 2, 3),
                     help="1: everything on one stream; 2: Extract+Match | LocalBA; 3: Extract | Match | LocalBA")
-    ap.add_argument("--extract-ctx", type=int, default=2, choices=(1, 2, 3, 4),
+    ap.add_argument("--extract-ctx", type=int, default=3, choices=(1, 2, 3, 4),
                     help="extraction contexts (with --streams 3): frames alternate between them, so the "
                          "extraction of frame t+1 overlaps frame t's; Match and LocalBA stay in frame order")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),

@@ -41,6 +41,7 @@ constexpr int kBlock = 256;
 constexpr int kHistRep = 8;
 
 VX_KT_TABLE();
+VX_KP_TABLE();
 
 __constant__ signed char c_pattern[1024];
 __constant__ int c_umax[16];
@@ -56,6 +57,7 @@ struct LevelArgs {
     long long stage_base[kMaxLevels];               // selection staging of level l
     int level_cap[kMaxLevels];                      // max NMS corners of level l
     int fast_threshold, edge, out_cap;
+    int raster_rank;                                // k_select_stl wrote the survivors' raster ranks
     // blur tiling
     int btx[kMaxLevels], bty[kMaxLevels], bbase[kMaxLevels];
     float gk[7];
@@ -1165,9 +1167,10 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
 // g(x*) >= 0 (K = 0 when there is no R), so only the block holding x* needs per-lane work.
 template <class T> struct RgCap { static constexpr int v = sizeof(T) == 4 ? 8192 : 4096; };
 constexpr int kRgCap32 = 8192;                 // C4 level 0: ~6.9k FAST candidates
-constexpr int kRgWave = 512;                   // wave-0 passes up to 8 blocks
+constexpr int kRgWave = 256;                   // wave-0 passes up to 4 blocks (longer ranges: team passes over four SIMDs)
 constexpr int kRgMail = 16400;                 // bytes per mailbox: (8192 / 2 + 1) u32 = (4096 / 2 + 1) u64
-constexpr int kRgBytes = 4 * kRgMail + 32 + 64 * 4 + 32;  // + 4 spare slots + 64 ints; 16-aligned
+constexpr int kRgTrash = 4 * kRgMail + 32 + 64 * 4 + 32;  // + 4 spare slots + 64 ints; 16-aligned
+constexpr int kRgBytes = kRgTrash + 64 * 8 + 64 * 4;       // + one value and one int trash slot per lane
 static_assert(kRgBytes % 16 == 0, "engine scratch alignment");
 
 // the engine's LDS: value mailboxes bl / br, position mailboxes lp / rp (team passes), a few ints
@@ -1179,16 +1182,20 @@ struct RgLds {
     __device__ __forceinline__ int* lp() const { return reinterpret_cast<int*>(p + 2 * kRgMail); }
     __device__ __forceinline__ int* rp() const { return reinterpret_cast<int*>(p + 3 * kRgMail); }
     __device__ __forceinline__ int* s() const { return reinterpret_cast<int*>(p + 4 * kRgMail + 32); }
+    // per-lane trash slots: the target of a lane's write when it has nothing to write (keeps the
+    // passes' LDS traffic free of divergent branches)
+    template <class T> __device__ __forceinline__ T* tv() const {
+        return reinterpret_cast<T*>(p + kRgTrash) + (threadIdx.x & 63);
+    }
+    __device__ __forceinline__ int* ti() const { return reinterpret_cast<int*>(p + kRgTrash + 64 * 8) + (threadIdx.x & 63); }
+    // the same as element indices from p (selects between LDS slots stay integer selects: a select
+    // between pointers is turned into branches around each access)
+    template <class T> static constexpr int kBr = kRgMail / (int)sizeof(T);
+    template <class T> static constexpr int kTv = kRgTrash / (int)sizeof(T);
+    static constexpr int kS = (4 * kRgMail + 32) / 4, kLp = 2 * kRgMail / 4, kRp = 3 * kRgMail / 4;
+    static constexpr int kTi = (kRgTrash + 64 * 8) / 4;
 };
 
-// bits [lo, hi) of a 64-lane block (clamped)
-__device__ __forceinline__ u64 lane_bits(int lo, int hi) {
-    lo = max(lo, 0);
-    hi = min(hi, 64);
-    if (hi <= lo) return 0ull;
-    const u64 a = ~0ull << lo;
-    return hi >= 64 ? a : a & ((1ull << hi) - 1ull);
-}
 // position x of the blocks starting at q0 := val (x anywhere; compares positions, never the block
 // index with a runtime value: GVN would turn v[i] into a dynamically indexed v[j] -> scratch)
 template <int NB, class T>
@@ -1213,8 +1220,7 @@ __device__ __forceinline__ void rg_load(T (&v)[NB], const T* __restrict__ A, int
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        const int q = q0 + 64 * j + lane;
-        v[j] = q < len ? A[q] : T(0);
+        v[j] = A[min(q0 + 64 * j + lane, len - 1)];  // (lanes past the range: masked out by rg_masks)
     }
 }
 template <int NB, class T>
@@ -1227,126 +1233,161 @@ __device__ __forceinline__ void rg_store(const T (&v)[NB], T* __restrict__ A, in
     }
 }
 
-// Per block and lane the pass keeps one int, the lane code: bit 0 L, bit 1 R, bits 2..8 the L
-// and bits 9..15 the R below the lane in the block (in range); per block one uniform int, #L |
-// #R << 16.
-__device__ __forceinline__ int lane_code(u64 ml, u64 mr) {
-    const int lane = threadIdx.x & 63;
-    return (int)((ml >> lane) & 1ull) | ((int)((mr >> lane) & 1ull) << 1) | (lane_rank(ml) << 2) |
-           (lane_rank(mr) << 9);
+// Per block the pass keeps the lane's L / R flags (lane masks; their ballots are the block's
+// masks), its L rank (#L before it in the range) and its R rank from the left, both from mbcnt
+// with the running prefix as base.  Block counts are scalar popcounts of the masks.
+__device__ __forceinline__ int mbcnt(u64 m, int base) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)base));
 }
-__device__ __forceinline__ int code_lrank(int c) { return (c >> 2) & 127; }
-__device__ __forceinline__ int code_rrank(int c) { return (c >> 9) & 127; }
 
-// Block masks of the range [lo, len) for the blocks from q0: key <= P / < P (L), >= P (R)
+// Flags and masks of the blocks from q0 over the range [lo, len): L = key <= P (pivot pass) /
+// key < P (partition), R = key >= P
 template <int NB, bool kPivot, class T>
-__device__ __forceinline__ int rg_masks(const T (&v)[NB], int q0, int lo, int len, unsigned P, int (&code)[NB],
-                                        int (&cnt)[NB]) {
-    int cr = 0;
+__device__ __forceinline__ void rg_masks(const T (&v)[NB], int q0, int lo, int len, unsigned P, bool (&il)[NB],
+                                         bool (&ir)[NB]) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        const u64 in = lane_bits(lo - q0 - 64 * j, len - q0 - 64 * j);
+        const int x = q0 + 64 * j + lane;
+        const bool in = x >= lo && x < len;
         const unsigned k = sel_key(v[j]);
-        const u64 ml = __ballot(kPivot ? k <= P : k < P) & in, mr = __ballot(k >= P) & in;
-        code[j] = lane_code(ml, mr);
-        cnt[j] = __popcll(ml) | (__popcll(mr) << 16);
-        cr += __popcll(mr);
+        il[j] = in && (kPivot ? k <= P : k < P);
+        ir[j] = in && k >= P;
     }
-    return cr;
+}
+template <int NB>
+__device__ __forceinline__ void rg_ranks(const bool (&il)[NB], const bool (&ir)[NB], int ql, int qr, int (&ra)[NB],
+                                         int (&rb)[NB]) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const u64 ml = __ballot(il[j]), mr = __ballot(ir[j]);
+        ra[j] = mbcnt(ml, ql);
+        rb[j] = mbcnt(mr, qr);
+        ql += __popcll(ml);
+        qr += __popcll(mr);
+    }
 }
 
 // The crossing in one wave's blocks (prefix counts ql / qr of the L / R before them, nr R in the
-// whole range): K if x* lies in them, else 0.
+// whole range): K if x* lies in them, else 0.  Per lane, g(x + 1) = #L + #R in [lo, x] - nr =
+// ra + rb + il + ir - nr never decreases along the range, so x* - 1 is the first set bit of the
+// first nonzero ballot(g(x + 1) >= 0); K = max(#R in [x*, l), #L in [lo, x* - 1)) from that
+// block's prefix counts and masks.  Branch-free: a scalar select chain over the blocks.
 template <int NB>
-__device__ __forceinline__ int rg_crossing(const int (&code)[NB], const int (&cnt)[NB], int ql, int qr, int nr) {
-    int K = 0;
-    bool done = false;
+__device__ __forceinline__ int rg_crossing(const bool (&il)[NB], const bool (&ir)[NB], const int (&ra)[NB],
+                                           const int (&rb)[NB], int ql, int qr, int nr) {
+    if (ql + qr - nr >= 0) return 0;  // g >= 0 already before these blocks: x* lies before them
+    u64 gx = 0, mlx = 0, mrx = 0;
+    int qlx = 0, qrx = 0;
+    bool found = false;
 #pragma unroll
-    for (int j = 0; j < NB; ++j)
-        if (!done) {
-            const int cl = cnt[j] & 0xffff, cr = cnt[j] >> 16;
-            const int gs = ql + qr - nr;
-            if (gs < 0 && gs + cl + cr >= 0) {
-                // g(start + i + 1) over the lanes (the last in-range lane has g(l) = #L >= 0); the
-                // first lane t reaching 0 gives x* = start + t + 1
-                const int c = code[j];
-                const int gi = gs + code_lrank(c) + code_rrank(c) + (c & 1) + ((c >> 1) & 1);
-                const int t = __ffsll((long long)__ballot(gi >= 0)) - 1;
-                const int ct = __builtin_amdgcn_readlane(c, t);
-                // K = max(#R in [x*, l), #L in [lo, x* - 1))
-                K = max(nr - (qr + code_rrank(ct) + ((ct >> 1) & 1)), ql + code_lrank(ct));
-                done = true;
-            }
-            ql += cl;
-            qr += cr;
-        }
-    return K;
+    for (int j = 0; j < NB; ++j) {
+        const u64 ml = __ballot(il[j]), mr = __ballot(ir[j]);
+        const u64 g = __ballot(ra[j] + rb[j] + (int)il[j] + (int)ir[j] - nr >= 0);
+        const bool take = !found && g != 0ull;
+        gx = take ? g : gx;
+        mlx = take ? ml : mlx;
+        mrx = take ? mr : mrx;
+        qlx = take ? ql : qlx;
+        qrx = take ? qr : qrx;
+        found = found || g != 0ull;
+        ql += __popcll(ml);
+        qr += __popcll(mr);
+    }
+    if (!found) return 0;
+    const int t = __ffsll((long long)gx) - 1;
+    const u64 below = (1ull << t) - 1ull;
+    return max(nr - (qrx + __popcll(mrx & (below | (1ull << t)))), qlx + __popcll(mlx & below));
 }
+
+// inclusive prefix sum / max over each 16-lane row (DPP row shifts; lanes shifted in read 0)
+__device__ __forceinline__ int row_scan_add(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);
+    return x;
+}
+__device__ __forceinline__ int row_scan_max(int x) {
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false));
+    x = max(x, __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false));
+    return x;
+}
+static_assert(kStlWaves <= 16, "team counts are scanned within one DPP row");
 
 // One pass by wave 0 alone over A[0, len) (A = the range's first element): kPivot, an
 // introselect step (median of (1, len / 2, len - 1) moved to 0, unguarded partition of [1, len)
 // around it, L = !(x > P), R = !(P > x)); otherwise std::partition of [0, len) by key >= thr
-// (L = key < thr, R = key >= thr).  Returns the cut (relative to A); n_r = #R.
+// (L = key < thr, R = key >= thr).  Swap k < K exchanges the L of rank k with the R of rank k from
+// the right through the mailboxes (an element is swapped at most once: its L and R ranks are never
+// both < K).  Every LDS access is unconditional, lanes with nothing to move using their trash
+// slot: the pass is straight-line VALU + LDS code, no exec-mask branches.  Returns the cut
+// min(L[K], R[K - 1]) (relative to A; both candidates written to s[50] / s[51]); n_r = #R.
 template <int NB, bool kPivot, class T>
-__device__ __forceinline__ int rg_wave_pass(T* __restrict__ A, int len, unsigned thr, T* __restrict__ bl,
-                                            T* __restrict__ br, int& n_r) {
+__device__ __forceinline__ int rg_wave_pass(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
+    const int lane = threadIdx.x & 63;
+    int* s = E.s();
     T v[NB];
     rg_load(v, A, 0, len);
     unsigned P = thr;
-    int lo = 0;
+    int lo = 0, m = -1;
     if (kPivot) {
         const int b = len / 2, c = len - 1;
         const T vf = uni(A[0]), va = uni(A[1]), vb = uni(A[b]), vc = uni(A[c]);
         T pv;
-        const int m = stl_median(1, b, c, va, vb, vc, pv);
+        m = stl_median(1, b, c, va, vb, vc, pv);
         P = sel_key(pv);
         rg_put(v, 0, 0, pv);
         rg_put(v, 0, m, vf);
         lo = 1;
     }
-    int code[NB], cnt[NB];
-    const int nr = rg_masks<NB, kPivot>(v, 0, lo, len, P, code, cnt);
-    const int K = rg_crossing(code, cnt, 0, 0, nr);
-    // the cut min(L[K], R[K - 1]) (the L of rank K, the R of left rank nr - K), the mailboxes
-    int cut = INT_MAX;
-    {
-        int ql = 0, qr = 0;
+    bool il[NB], ir[NB];
+    int ra[NB], rb[NB];
+    rg_masks<NB, kPivot>(v, 0, lo, len, P, il, ir);
+    rg_ranks(il, ir, 0, 0, ra, rb);
+    int nr = 0;
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int cl = cnt[j] & 0xffff, cr = cnt[j] >> 16, c = code[j];
-            const bool il = c & 1, ir = c & 2;
-            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
-            if (K >= ql && K < ql + cl) cut = min(cut, 64 * j + __ffsll((long long)__ballot(il && a == K)) - 1);
-            if (K > 0 && nr - K >= qr && nr - K < qr + cr)
-                cut = min(cut, 64 * j + __ffsll((long long)__ballot(ir && b == K - 1)) - 1);
-            if (il && a < K) bl[a] = v[j];
-            if (ir && b < K) br[b] = v[j];
-            ql += cl;
-            qr += cr;
-        }
+    for (int j = 0; j < NB; ++j) nr += __popcll(__ballot(ir[j]));
+    const int K = rg_crossing(il, ir, ra, rb, 0, 0, nr);
+    const int hr = K > 0 ? nr - K : INT_MAX;  // the R with left rank >= hr are swapped; R[K - 1] has rank hr
+    T* eb = E.bl<T>();                          // element slots: bl, then br, then the trash
+    int* ei = reinterpret_cast<int*>(E.p);      // int slots: s, trash
+    constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
+    if (lane == 0) *reinterpret_cast<int2*>(s + 50) = make_int2(INT_MAX, INT_MAX);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
+        eb[sl ? ra[j] : sr ? kBr + (nr - 1 - rb[j]) : kTv + lane] = v[j];
+        ei[(il[j] && ra[j] == K) ? RgLds::kS + 50 : (ir[j] && rb[j] == hr) ? RgLds::kS + 51 : RgLds::kTi + lane] =
+            64 * j + lane;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    {
-        int ql = 0, qr = 0;
+    T nv[NB];
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {  // (an element is swapped at most once: its L and R ranks are never both < K)
-            const int c = code[j];
-            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
-            if ((c & 1) && a < K) v[j] = br[a];
-            else if ((c & 2) && b < K) v[j] = bl[b];
-            ql += cnt[j] & 0xffff;
-            qr += cnt[j] >> 16;
-        }
+    for (int j = 0; j < NB; ++j) {  // every read issued before the first store
+        const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
+        nv[j] = eb[sl ? kBr + ra[j] : sr ? nr - 1 - rb[j] : kTv + lane];
     }
-    rg_store(v, A, 0, len);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+        const int x = 64 * j + lane;
+        const bool sw = (il[j] && ra[j] < K) || (ir[j] && rb[j] >= hr);
+        if (sw || (kPivot && (x == 0 || x == m))) A[x] = sw ? nv[j] : v[j];
+    }
+    const int2 cc = *reinterpret_cast<const int2*>(s + 50);
+    const int cut = min(max(min(uni(cc.x), uni(cc.y)), 1), len);  // (clamped: memory-safe whatever happens)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the next pass reloads; global scratch too)
     n_r = nr;
     return cut;
 }
 
 // The same pass by the workgroup over A[0, len), len <= 64 NB kStlWaves: wave w holds the blocks
-// [NB w, NB (w + 1)); waves past the range only meet the barriers.
+// [NB w, NB (w + 1)); waves past the range only meet the barriers.  Before the second barrier every
+// L and every R of rank below hb = (len - lo) / 2 + 1 >= K goes to the mailboxes with its position
+// (the cut's candidates), so the swaps need no third exchange.  Branch-free LDS traffic as above.
 template <int NB, bool kPivot, class T>
 __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
     constexpr int NW = kStlWaves;
@@ -1355,19 +1396,21 @@ __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned
     const int q0 = 64 * NB * w;
     const bool act = q0 < len;
     int* s = E.s();
-    T* bl = E.bl<T>();
-    T* br = E.br<T>();
     int* lp = E.lp();
     int* rp = E.rp();
+    T* eb = E.bl<T>();
+    int* ei = reinterpret_cast<int*>(E.p);
+    constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
     T v[NB];
-    int code[NB], cnt[NB];
+    bool il[NB], ir[NB];
+    int ra[NB], rb[NB];
     unsigned P = thr;
-    int lo = 0;
+    int lo = 0, m = -1;
     if (kPivot) {
         const int b = len / 2, c = len - 1;
         const T vf = uni(A[0]), va = uni(A[1]), vb = uni(A[b]), vc = uni(A[c]);
         T pv;
-        const int m = stl_median(1, b, c, va, vb, vc, pv);
+        m = stl_median(1, b, c, va, vb, vc, pv);
         P = sel_key(pv);
         if (act) {
             rg_load(v, A, q0, len);
@@ -1380,67 +1423,60 @@ __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned
     }
     int cl = 0, cr = 0;
     if (act) {
-        cr = rg_masks<NB, kPivot>(v, q0, lo, len, P, code, cnt);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) cl += cnt[j] & 0xffff;
-    }
-    if (lane == 0) {
-        s[2 * w] = cl;
-        s[2 * w + 1] = cr;
-    }
-    __syncthreads();
-    int pl = 0, pr = 0, nl = 0, nr = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-        const int x = uni(s[2 * i]), y = uni(s[2 * i + 1]);
-        pl += i < w ? x : 0;
-        pr += i < w ? y : 0;
-        nl += x;
-        nr += y;
-    }
-    // mailboxes: every L by rank and every R by rank from the right below hb (K <= (len - lo) / 2)
-    const int hb = (len - lo) / 2 + 1;
-    if (act) {
-        const int km = rg_crossing(code, cnt, pl, pr, nr);
-        if (lane == 0) s[2 * NW + w] = km;
-        int ql = pl, qr = pr;
+        rg_masks<NB, kPivot>(v, q0, lo, len, P, il, ir);
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const int c = code[j];
-            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
-            const int x = q0 + 64 * j + lane;
-            if ((c & 1) && a < hb) {
-                bl[a] = v[j];
-                lp[a] = x;
-            }
-            if ((c & 2) && b < hb) {
-                br[b] = v[j];
-                rp[b] = x;
-            }
-            ql += cnt[j] & 0xffff;
-            qr += cnt[j] >> 16;
+            cl += __popcll(__ballot(il[j]));
+            cr += __popcll(__ballot(ir[j]));
+        }
+    }
+    if (lane == 0) *reinterpret_cast<int2*>(s + 2 * w) = make_int2(cl, cr);
+    __syncthreads();
+    int pl, pr, nl, nr;
+    {
+        const int2 c2 = lane < NW ? *reinterpret_cast<const int2*>(s + 2 * lane) : make_int2(0, 0);
+        const int sl = row_scan_add(c2.x), sr = row_scan_add(c2.y);
+        pl = w > 0 ? __builtin_amdgcn_readlane(sl, w - 1) : 0;
+        pr = w > 0 ? __builtin_amdgcn_readlane(sr, w - 1) : 0;
+        nl = __builtin_amdgcn_readlane(sl, NW - 1);
+        nr = __builtin_amdgcn_readlane(sr, NW - 1);
+    }
+    const int hb = (len - lo) / 2 + 1;
+    if (act) {
+        rg_ranks(il, ir, pl, pr, ra, rb);
+        const int km = rg_crossing(il, ir, ra, rb, pl, pr, nr);
+        if (lane == 0) s[2 * NW + w] = km;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int x = q0 + 64 * j + lane, b = nr - 1 - rb[j];
+            const bool wl = il[j] && ra[j] < hb, wr = ir[j] && b < hb;
+            eb[wl ? ra[j] : kTv + lane] = v[j];
+            ei[wl ? RgLds::kLp + ra[j] : RgLds::kTi + lane] = x;
+            eb[wr ? kBr + b : kTv + lane] = v[j];
+            ei[wr ? RgLds::kRp + b : RgLds::kTi + lane] = x;
         }
     } else if (lane == 0) {
         s[2 * NW + w] = 0;
     }
     __syncthreads();
-    int K = 0;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) K = max(K, uni(s[2 * NW + i]));
+    const int K = __builtin_amdgcn_readlane(row_scan_max(lane < NW ? s[2 * NW + lane] : 0), NW - 1);
     int cut = K < nl ? uni(lp[K]) : INT_MAX;
     if (K > 0) cut = min(cut, uni(rp[K - 1]));
+    cut = min(max(cut, 1), len);  // (clamped: memory-safe whatever happens)
     if (act) {
-        int ql = pl, qr = pr;
+        const int hr = nr - K;
+        T nv[NB];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const int c = code[j];
-            const int a = ql + code_lrank(c), b = nr - 1 - (qr + code_rrank(c));
-            if ((c & 1) && a < K) v[j] = br[a];
-            else if ((c & 2) && b < K) v[j] = bl[b];
-            ql += cnt[j] & 0xffff;
-            qr += cnt[j] >> 16;
+            const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr && K > 0;
+            nv[j] = eb[sl ? kBr + ra[j] : sr ? nr - 1 - rb[j] : kTv + lane];
         }
-        rg_store(v, A, q0, len);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int x = q0 + 64 * j + lane;
+            const bool sw = (il[j] && ra[j] < K) || (ir[j] && rb[j] >= hr && K > 0);
+            if (sw || (kPivot && (x == 0 || x == m))) A[x] = sw ? nv[j] : v[j];
+        }
     }
     __syncthreads();
     n_r = nr;
@@ -1450,12 +1486,10 @@ __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned
 // dispatch on the range: the smallest power-of-two block count that holds it
 template <bool kPivot, class T>
 __device__ __forceinline__ int rg_wave_any(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
-    T* bl = E.bl<T>();
-    T* br = E.br<T>();
-    if (len <= 64) return rg_wave_pass<1, kPivot>(A, len, thr, bl, br, n_r);
-    if (len <= 128) return rg_wave_pass<2, kPivot>(A, len, thr, bl, br, n_r);
-    if (len <= 256) return rg_wave_pass<4, kPivot>(A, len, thr, bl, br, n_r);
-    return rg_wave_pass<8, kPivot>(A, len, thr, bl, br, n_r);
+    if (len <= 64) return rg_wave_pass<1, kPivot>(A, len, thr, E, n_r);
+    if (len <= 128) return rg_wave_pass<2, kPivot>(A, len, thr, E, n_r);
+    if (len <= 256) return rg_wave_pass<4, kPivot>(A, len, thr, E, n_r);
+    return rg_wave_pass<8, kPivot>(A, len, thr, E, n_r);
 }
 // team passes spread the blocks over about four waves (one per SIMD), 8 blocks a wave beyond that
 template <bool kPivot, class T>
@@ -1581,6 +1615,7 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
             break;
         }
         --depth;
+        VX_KP(l - f);
         const int cut = pivot_pass_mem(A, bl, br, f, l, E.s());
         if (cut <= nth) f = cut;
         else l = cut;
@@ -1592,6 +1627,7 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
         }
         --depth;
         int nr;
+        VX_KP((1 << 24) | (l - f));
         const int cut = f + rg_team_any<true>(A + f, l - f, 0u, E, nr);
         if (cut <= nth) f = cut;
         else l = cut;
@@ -1605,6 +1641,7 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
             }
             --depth;
             int nr;
+            VX_KP((2 << 24) | (l - f));
             const int cut = f + rg_wave_any<true>(A + f, l - f, 0u, E, nr);
             if (cut <= nth) f = cut;
             else l = cut;
@@ -1633,6 +1670,7 @@ __device__ __forceinline__ int stl_retain_best(T* __restrict__ A, T* __restrict_
     if (npts <= 0) return 0;
     stl_nth_element(A, bl, br, size, npts - 1, E);
     VX_KT(4);
+    VX_KP((3 << 24) | (size - npts));
     const unsigned thr = uni(sel_key(A[npts - 1]));
     const int len = size - npts;
     int* s = E.s();
@@ -1651,6 +1689,7 @@ __device__ __forceinline__ int stl_retain_best(T* __restrict__ A, T* __restrict_
         nr = uni(s[60]);
     }
     VX_KT(5);
+    VX_KP(4 << 24);
     return npts + nr;
 }
 
@@ -1669,6 +1708,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
     const RgLds E{sdyn};
     const int l = blockIdx.x;
     const int tid = threadIdx.x;
+    VX_KP_RESET();
     cand += blockIdx.z * a.fs_cells * kCellCap;
     cell_count += blockIdx.z * a.fs_cells;
     stage += blockIdx.z * a.fs_stage;
@@ -1786,6 +1826,37 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
     VX_KT(13);
     for (int j = tid; j < K2; j += kStlNT) fin[j] = kept[(unsigned)(lds2 ? L2[j] : G2[j])];
     if (tid == 0) level_count[l] = K2;
+    // The survivors in raster order for k_describe's walk (rast[p] = output index of the p-th
+    // survivor in raster order, over the dead pass-1 scratch): a bitmap of their raster indices in
+    // the engine's LDS (free now), word popcounts scanned, one rank per survivor.
+    int* rast = reinterpret_cast<int*>(gscr);
+    unsigned* bm = reinterpret_cast<unsigned*>(sdyn);
+    const int nw32 = (n0 + 31) >> 5;
+    int* wpre = reinterpret_cast<int*>(bm + nw32);
+    if (2 * nw32 * 4 <= kRgBytes) {
+        for (int i = tid; i < nw32; i += kStlNT) bm[i] = 0u;
+        __syncthreads();
+        for (int j = tid; j < K2; j += kStlNT) {
+            const unsigned idx = (unsigned)(lds2 ? L2[j] : G2[j]);
+            atomicOr(&bm[idx >> 5], 1u << (idx & 31u));
+        }
+        __syncthreads();
+        int base = 0;
+        for (int i0 = 0; i0 < nw32; i0 += kStlNT) {
+            const int i = i0 + tid;
+            int tot;
+            const int e = block_scan_excl<kStlNT>(i < nw32 ? __popc(bm[i]) : 0, sw, tot);
+            if (i < nw32) wpre[i] = base + e;
+            base += uni(tot);
+        }
+        __syncthreads();
+        for (int j = tid; j < K2; j += kStlNT) {
+            const unsigned idx = (unsigned)(lds2 ? L2[j] : G2[j]);
+            rast[wpre[idx >> 5] + __popc(bm[idx >> 5] & ((1u << (idx & 31u)) - 1u))] = j;
+        }
+    } else {
+        for (int j = tid; j < K2; j += kStlNT) rast[j] = j;  // (no room: output order, no locality)
+    }
     VX_KT(15);
 }
 
@@ -1811,6 +1882,7 @@ __global__ __launch_bounds__(kStlNT) void k_test_retain(const unsigned* __restri
                                                         int* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char sdyn[];
     VX_KT(0);
+    VX_KP_RESET();
     const RgLds E{sdyn};
     unsigned char* ra = sdyn + kRgBytes;
     if (!wide) {
@@ -1857,8 +1929,8 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
                                                      LevelArgs a, vx_keypoint* __restrict__ kp,
                                                      uint8_t* __restrict__ desc,
                                                      int* __restrict__ slot_count) {
+    constexpr int kWpb = kBlock / 64;
     const int lane = threadIdx.x & 63;
-    const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     pyr += blockIdx.z * a.fs_pyr;
     blur += blockIdx.z * a.fs_pyr;
     stage += blockIdx.z * a.fs_stage;
@@ -1866,20 +1938,42 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
     kp += blockIdx.z * (long long)a.out_cap;
     desc += blockIdx.z * (long long)a.out_cap * 32;
     slot_count += blockIdx.z * 4;
-    int total = 0, l = -1, j = 0;
-    for (int i = 0; i < a.L; ++i) {
-        const int c = level_count[i];
-        if (l < 0 && w < total + c) {
-            l = i;
-            j = w - total;
-        }
-        total += c;
-    }
-    if (w == 0 && lane == 0) {
+    int total = 0;
+    for (int i = 0; i < a.L; ++i) total += level_count[i];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
         slot_count[0] = total;
         slot_count[1] = total > a.out_cap;
     }
-    if (l < 0 || w >= a.out_cap) return;
+    // Wave rank rk walks the keypoints in (level, raster) order, and the first nact blocks take
+    // the ranks XCD by XCD (block x runs on XCD x mod 8): each XCD's L2 fetches the rows of one
+    // band of the levels instead of every XCD fetching every patch row.  Keypoint rk's output
+    // index is its STL-order index (rast, from k_select_stl).  Overflow: output order.
+    const bool remap = a.raster_rank && total <= a.out_cap;
+    const int nact = (min(total, a.out_cap) + kWpb - 1) / kWpb;
+    int bx = blockIdx.x;
+    if (remap) {
+        if ((int)blockIdx.x >= nact) return;
+        const int xcd = blockIdx.x & 7, qb = nact >> 3, rem = nact & 7;
+        bx = xcd * qb + min(xcd, rem) + (blockIdx.x >> 3);
+    }
+    const int rk = bx * kWpb + (threadIdx.x >> 6);
+    int l = -1, j = 0, w = 0;
+    {
+        int pre = 0;
+        for (int i = 0; i < a.L; ++i) {
+            const int c = level_count[i];
+            if (l < 0 && rk < pre + c) {
+                l = i;
+                j = rk - pre;
+                w = pre;
+            }
+            pre += c;
+        }
+    }
+    if (l < 0) return;
+    if (remap) j = reinterpret_cast<const int*>(stage + a.stage_base[l] + 2 * (long long)a.level_cap[l])[j];
+    w += j;
+    if (w >= a.out_cap) return;
     const CandRec r = stage[a.stage_base[l] + a.level_cap[l] + j];
     const int W = a.lw[l];
     const int xl = (int)(r.xy & 0xffffu), yl = (int)(r.xy >> 16);
@@ -2115,7 +2209,7 @@ int upload_constants(vx_ctx* c) {
 }
 
 LevelArgs level_args(const OrbGeometry& g) {
-    LevelArgs a;
+    LevelArgs a{};
     std::memset(&a, 0, sizeof a);
     a.L = g.L;
     for (int l = 0; l < g.L; ++l) {
@@ -2290,6 +2384,7 @@ static int orb_enqueue_frames(vx_ctx* c, const uint8_t* d_img, int channels, int
                               vx_keypoint* kp, uint8_t* desc, int* count) {
     const OrbGeometry& g = c->geo;
     LevelArgs a = level_args(g);
+    a.raster_rank = c->kp_order == VX_ORDER_STL && !(c->orb_debug & VX_ORB_DEBUG_FAST_NO_BORDER);
     a.fs_img = fs_img;
     // test hooks (vx_orb_set_debug): the FAST list before runByImageBorder, the selection's stages
     if (c->orb_debug & VX_ORB_DEBUG_FAST_NO_BORDER) a.edge = 3;
@@ -2389,6 +2484,7 @@ static int orb_reserve_frames(vx_ctx* c, int nf, int bank) {
 }  // namespace vx
 
 namespace vx {
+VX_KP_EXPORT(vx_kpass_read_orb);
 VX_KT_EXPORT(vx_ktrace_read_orb);  // extern "C": the namespace does not enter the symbol
 }
 

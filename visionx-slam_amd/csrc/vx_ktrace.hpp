@@ -35,7 +35,38 @@ constexpr int kKtBlocks = 256, kKtSlots = 16;
     extern "C" int name(long long* out) {                                                  \
         return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ktrace), sizeof(g_ktrace)) == hipSuccess ? 0 : -1; \
     }
+// pass log (workgroup 0 only): entry i = (wall_clock64, tag); VX_KP_TABLE / VX_KP(tag) /
+// VX_KP_EXPORT(name), entry 0 holds the count
+#define VX_KP_TABLE() __device__ long long g_kpass[2 * 512]
+#define VX_KP(tag)                                                                         \
+    do {                                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                                     \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {   \
+            const int kp_i = (int)g_kpass[0] + 1;                                          \
+            if (kp_i < 512) {                                                              \
+                g_kpass[2 * kp_i] = (long long)wall_clock64();                             \
+                g_kpass[2 * kp_i + 1] = (long long)(tag);                                  \
+                g_kpass[0] = kp_i;                                                         \
+            }                                                                              \
+        }                                                                                  \
+    } while (0)
+#define VX_KP_RESET()                                                                      \
+    do {                                                                                   \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) g_kpass[0] = 0; \
+    } while (0)
+#define VX_KP_EXPORT(name)                                                                 \
+    extern "C" int name(long long* out) {                                                  \
+        return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kpass), sizeof(g_kpass)) == hipSuccess ? 0 : -1; \
+    }
 #else
+#define VX_KP_TABLE() static_assert(true, "")
+#define VX_KP(tag) \
+    do {           \
+    } while (0)
+#define VX_KP_RESET() \
+    do {              \
+    } while (0)
+#define VX_KP_EXPORT(name) static_assert(true, "")
 #define VX_KT_TABLE() static_assert(true, "")
 #define VX_KT(slot) \
     do {            \
