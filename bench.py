@@ -95,6 +95,47 @@ def stage_bytes(stage, geo, counts):
     return None
 
 
+# ----------------------------------------------------------------------------- drop-in LocalBA
+def per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam):
+    """What one drop-in LocalBA::Optimize() (local_ba.cpp:66-249) costs end to end, host clock,
+    median of 7 after 2 warm-ups: plan build + solve + the results written back, (a) from the
+    host map snapshot (upload, device build, run, download into the snapshot) and (b) from the
+    device-resident map (vx_dmap: build from the resident map, run, scatter into it)."""
+    def med(f):
+        t = []
+        for i in range(9):
+            t0 = time.perf_counter()
+            f()
+            if i >= 2:
+                t.append(1e3 * (time.perf_counter() - t0))
+        return round(float(np.median(t)), 3)
+
+    m = ba_map.copy()
+
+    def snap():
+        p = bctx.ba_plan(m, opts)
+        p.run_async()
+        p.fetch(m)
+        p.close()
+
+    dm = vxslam.DMap(bctx)
+    vxslam.dmap_load(dm, ba_map)
+    bctx.synchronize()
+
+    def resident():
+        p = dm.plan(opts)
+        p.run_async()
+        p.apply(dm)
+        bctx.synchronize()
+        p.close()
+
+    try:
+        return {"snapshot": med(snap), "resident": med(resident),
+                "note": "plan + solve + apply; value excludes the plan build (a resident plan is replayed per frame)"}
+    finally:
+        dm.close()
+
+
 # ----------------------------------------------------------------------------- distributed
 class Dist:
     def __init__(self, n_gpus):
@@ -421,6 +462,7 @@ def main():
         bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N).close()
         plan_ms.append(1e3 * (time.perf_counter() - t0))
     plan_build_ms = float(np.median(plan_ms))
+    per_kf = per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam) if N == 1 else None
     torch.cuda.synchronize()
 
     # Pipeline.  Frame t: Extract(t) on extraction context t % E (E = --extract-ctx) into that
@@ -625,6 +667,9 @@ def main():
             # map snapshot, incl. upload: paid once per LocalBA::Optimize() call of a drop-in
             # (a new keyframe, tracking.cpp:76-84); the timed steps replay a resident plan
             "ba_plan_build_ms": round(plan_build_ms, 3),
+            # one whole drop-in LocalBA::Optimize() (plan build + solve + results back into the
+            # map), median of 7, from the host snapshot and from the device-resident map (N = 1)
+            "per_keyframe_ms": per_kf,
             # N > 1: the sharded LocalBA against the unsharded run of the same window (ok = within
             # 1e-4, no gate flips, same iterations, ranks bitwise agreed); null at N = 1
             "parity_vs_unsharded": parity,

@@ -1167,7 +1167,14 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
 // g(x*) >= 0 (K = 0 when there is no R), so only the block holding x* needs per-lane work.
 template <class T> struct RgCap { static constexpr int v = sizeof(T) == 4 ? 8192 : 4096; };
 constexpr int kRgCap32 = 8192;                 // C4 level 0: ~6.9k FAST candidates
-constexpr int kRgWave = 256;                   // wave-0 passes up to 4 blocks (longer ranges: team passes over four SIMDs)
+#ifndef VX_SEL_WAVE
+#define VX_SEL_WAVE 256
+#endif
+#ifndef VX_SEL_SPREAD
+#define VX_SEL_SPREAD 16
+#endif
+constexpr int kRgWave = VX_SEL_WAVE;           // wave-0 passes up to this range (longer: team passes)
+constexpr int kRgSpread = VX_SEL_SPREAD;       // team passes spread their blocks over this many waves
 constexpr int kRgMail = 16400;                 // bytes per mailbox: (8192 / 2 + 1) u32 = (4096 / 2 + 1) u64
 constexpr int kRgTrash = 4 * kRgMail + 32 + 64 * 4 + 32;  // + 4 spare slots + 64 ints; 16-aligned
 constexpr int kRgBytes = kRgTrash + 64 * 8 + 64 * 4;       // + one value and one int trash slot per lane
@@ -1491,13 +1498,82 @@ __device__ __forceinline__ int rg_wave_any(T* __restrict__ A, int len, unsigned 
     if (len <= 256) return rg_wave_pass<4, kPivot>(A, len, thr, E, n_r);
     return rg_wave_pass<8, kPivot>(A, len, thr, E, n_r);
 }
-// team passes spread the blocks over about four waves (one per SIMD), 8 blocks a wave beyond that
+// team passes spread the blocks over kRgSpread waves (16: four per SIMD, so each SIMD hides the
+// others' LDS latency; measured 20 -> 14 us for the first retainBest of a C3 level 0)
 template <bool kPivot, class T>
 __device__ __forceinline__ int rg_team_any(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
-    const int per = ((len + 63) / 64 + 3) / 4;
+    const int per = ((len + 63) / 64 + kRgSpread - 1) / kRgSpread;
+    if (per <= 1) return rg_team_pass<1, kPivot>(A, len, thr, E, n_r);
     if (per <= 2) return rg_team_pass<2, kPivot>(A, len, thr, E, n_r);
     if (per <= 4) return rg_team_pass<4, kPivot>(A, len, thr, E, n_r);
     return rg_team_pass<8, kPivot>(A, len, thr, E, n_r);
+}
+
+// v_readlane of a wave-uniform lane, for u32 / u64 elements
+__device__ __forceinline__ unsigned rdl(unsigned v, int i) { return (unsigned)__builtin_amdgcn_readlane((int)v, i); }
+__device__ __forceinline__ u64 rdl(u64 v, int i) {
+    return ((u64)(unsigned)__builtin_amdgcn_readlane((int)(v >> 32), i) << 32) |
+           (unsigned)__builtin_amdgcn_readlane((int)v, i);
+}
+
+// The introselect steps of a range of <= 64 elements on wave 0 with the range in registers: lane i
+// holds A[f0 + i] for the whole tail, a step's range is a lane interval [lf, ll) and its pivot
+// candidates come from v_readlane; only the swapped pairs go through the mailboxes (one LDS round
+// trip a step, no loads or stores of A until the range is written back once).  Same step as
+// rg_wave_pass<1, true>; stops at a range of <= 3 or at the depth limit (heap = true), with f / l
+// the final range and A updated.
+template <class T>
+__device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int nth, int& depth, bool& heap,
+                                          const RgLds& E) {
+    const int lane = threadIdx.x & 63;
+    const int f0 = f, n0 = l - f;
+    T v = A[f0 + min(lane, n0 - 1)];
+    T* eb = E.bl<T>();
+    constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
+    const int kth = nth - f0;
+    int lf = 0, ll = n0;
+    while (ll - lf > 3) {
+        if (depth == 0) {
+            heap = true;
+            break;
+        }
+        --depth;
+        const int a = lf + 1, b = lf + (ll - lf) / 2, c = ll - 1;
+        const T vf = rdl(v, lf), va = rdl(v, a), vb = rdl(v, b), vc = rdl(v, c);
+        T pv;
+        const int m = stl_median(a, b, c, va, vb, vc, pv);
+        const unsigned P = sel_key(pv);
+        v = lane == lf ? pv : lane == m ? vf : v;
+        const unsigned k = sel_key(v);
+        const bool in = lane > lf && lane < ll;
+        const bool il = in && k <= P, ir = in && k >= P;
+        const u64 ml = __ballot(il), mr = __ballot(ir);
+        const int ra = mbcnt(ml, 0), rb = mbcnt(mr, 0), nr = __popcll(mr);
+        // crossing: the first range lane with g(x + 1) = ra + rb + il + ir - nr >= 0
+        const u64 g = __ballot(in && ra + rb + (int)il + (int)ir - nr >= 0);
+        const int t = g ? __ffsll((long long)g) - 1 : 63;
+        const u64 below = (1ull << t) - 1ull;
+        const int K = g ? max(nr - __popcll(mr & (below | (1ull << t))), __popcll(ml & below)) : 0;
+        const int hr = K > 0 ? nr - K : INT_MAX;
+        const bool sl = il && ra < K, sr = ir && rb >= hr;
+        eb[sl ? ra : sr ? kBr + (nr - 1 - rb) : kTv + lane] = v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const T nv = eb[sl ? kBr + ra : sr ? nr - 1 - rb : kTv + lane];
+        const u64 cl = __ballot(il && ra == K), cr = __ballot(ir && rb == hr);
+        int cut = cl ? __ffsll((long long)cl) - 1 : INT_MAX;
+        if (cr) cut = min(cut, __ffsll((long long)cr) - 1);
+        cut = min(max(cut, lf + 1), ll);  // (clamped: memory-safe whatever happens)
+        v = (sl || sr) ? nv : v;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (next step's mailbox writes after these reads)
+        __builtin_amdgcn_wave_barrier();
+        if (cut <= kth) lf = cut;
+        else ll = cut;
+    }
+    if (lane < n0) A[f0 + lane] = v;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    f = f0 + lf;
+    l = f0 + ll;
 }
 
 // libstdc++'s closing __insertion_sort of A[0, n) (n <= 3; a stable sort by key, descending):
@@ -1635,6 +1711,11 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
     VX_KT(2);
     if ((threadIdx.x >> 6) == 0) {
         while (!heap && l - f > 3) {
+            if (l - f <= 64) {  // the rest of the introselect in registers (rg_tail64)
+                VX_KP((5 << 24) | (l - f));
+                rg_tail64(A, f, l, nth, depth, heap, E);
+                break;
+            }
             if (depth == 0) {
                 heap = true;
                 break;
