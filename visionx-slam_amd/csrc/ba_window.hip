@@ -264,6 +264,17 @@ __global__ __launch_bounds__(kT) void k_lm_gather(const int* inv, int n, const d
 
 inline unsigned grid(long long n) { return (unsigned)std::max(1ll, (n + kT - 1) / kT); }
 
+// $VX_PLAN_TIMING: host timestamps of the plan build's stages on stderr (ms since the build began)
+struct PlanClock {
+    bool on = getenv("VX_PLAN_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void mark(const char* what) const {
+        if (on)
+            fprintf(stderr, "[vx plan] %-28s %.3f ms\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
+
 template <class T>
 int up(vx_ctx* c, DevBuf& d, const T* h, size_t n) {
     VX_HIP(c, d.ensure(std::max<size_t>(1, n) * sizeof(T)));
@@ -397,6 +408,7 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     const vx_ba_options& o = p->opt;
     const int nk = in.nk, nf = in.nf, nl = in.nl;
     vx_ctx::PlanScratch& B = c->plan_scratch;
+    const PlanClock clk;
     int rc;
     unsigned hcap = 1024;
     while (hcap < 2u * (unsigned)std::max(nl, 1)) hcap <<= 1;
@@ -459,7 +471,9 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     VX_HIP(c, hipMemcpyAsync(&hc[0], opt_scan + nl, 4, hipMemcpyDeviceToHost, s));
     VX_HIP(c, hipMemcpyAsync(&hc[1], first_scan + nf, 4, hipMemcpyDeviceToHost, s));
     VX_HIP(c, hipMemcpyAsync(&hc[2], B.counts.p, 4, hipMemcpyDeviceToHost, s));
+    clk.mark("core: counts requested");
     VX_HIP(c, hipStreamSynchronize(s));
+    clk.mark("core: counts back");
     p->n_landmarks_global = hc[2];
     if (hc[2] == 0) return VX_OK;  // no optimised landmark anywhere (local_ba.cpp:106-108)
     p->status = 0;
@@ -490,7 +504,9 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     VX_HIP(c, hipMemcpyAsync(RB, pscan + nf, 4, hipMemcpyDeviceToHost, s));
     VX_HIP(c, hipMemcpyAsync(RB + 4, p->lobs_ptr.p, (size_t)(n_opt + 1) * 4, hipMemcpyDeviceToHost, s));
     VX_HIP(c, hipMemcpyAsync(RB + 4 + n_opt + 1, inv, (size_t)n_lm * 4, hipMemcpyDeviceToHost, s));
+    clk.mark("core: CSR pointers requested");
     VX_HIP(c, hipStreamSynchronize(s));
+    clk.mark("core: CSR pointers back");
     p->n_pose_obs = RB[0];
     const std::vector<int> lptr(RB + 4, RB + 4 + n_opt + 1);
     const int* inv_h = RB + 4 + n_opt + 1;
@@ -522,8 +538,10 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     VX_HIP(c, hipMemcpyAsync(p->lm_blk.p, UP, nblk * 4, hipMemcpyHostToDevice, s));
     if (nflg) VX_HIP(c, hipMemcpyAsync(p->kf_flags.p, UP + nblk, nflg * 4, hipMemcpyHostToDevice, s));
     if ((rc = alloc_run_buffers(c, p))) return rc;
+    clk.mark("core: fill launched");
     // the fused layout, on the device from the CSRs just built (every plan, sharded ones included)
     if ((rc = build_fused_device(c, p))) return rc;
+    clk.mark("core: fused layout built");
     if (!p->fused) VX_HIP(c, hipStreamSynchronize(s));  // (the pinned block above)
     return VX_OK;
 }
@@ -571,6 +589,7 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
     p->n_landmarks_global = 0;
     const int n_kf = (int)m->kf_id.size();
     if (n_kf <= 0) return VX_OK;
+    const PlanClock clk;
     const std::vector<int> win = select_ids(m->kf_id.data(), n_kf, ref_kf_id, has_ref, o.window_size, m->kf_alive.data());
     const int nk = (int)win.size();
     p->n_window_kf = nk;
@@ -615,7 +634,9 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
                        (const double*)m->kf_pose.as<double>(), (const double*)m->kf_intr.as<double>(),
                        p->kf_pose0.as<double>(), p->kf_intr.as<double>());
     VX_LAUNCH_CHECK(c, "k_gather_kf");
+    clk.mark("dmap: window gathered");
     if ((rc = dmap_build_csr(c, m))) return rc;
+    clk.mark("dmap: CSR ready");
     const int nl = (int)m->n_lm;
     BuildInputs in{nk, nf, nl, B.wptr.as<int>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(), B.cam.as<uint8_t>(),
                    B.wid.as<uint64_t>(), B.wuv.as<double>(), m->lm_id.as<uint64_t>(), m->lm_bad.as<uint8_t>(),
@@ -632,7 +653,9 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
         VX_HIP(c, hipMemcpyAsync(p->lm_map_dev.p, B.inv.p, (size_t)p->n_lm * 4, hipMemcpyDeviceToDevice, c->stream));
         if ((rc = up(c, p->kf_map_dev, p->kf_map_idx.data(), p->kf_map_idx.size()))) return rc;
     }
+    clk.mark("dmap: tables queued");
     VX_HIP(c, hipStreamSynchronize(c->stream));
+    clk.mark("dmap: done");
     return VX_OK;
 }
 
