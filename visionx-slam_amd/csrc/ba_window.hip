@@ -169,8 +169,15 @@ __global__ __launch_bounds__(kT) void k_is_first(WinArgs a) {
     a.f_first[f] = (a.f_pv[f] && !a.l_opt[l] && a.l_first[l] == f) ? 1 : 0;
 }
 
-__global__ __launch_bounds__(kT) void k_fixed_slots(WinArgs a, const int* scan, int n_opt, int* inv) {
+// (n_opt: the optimised-landmark scan's total, read on the device; thread 0 also records it and
+// the fixed-landmark count for the build's single read-back: counts[4], counts[5])
+__global__ __launch_bounds__(kT) void k_fixed_slots(WinArgs a, const int* scan, const int* n_opt_dev, int* inv) {
     const int f = blockIdx.x * kT + threadIdx.x;
+    const int n_opt = *n_opt_dev;
+    if (f == 0) {
+        a.counts[4] = (unsigned)n_opt;
+        a.counts[5] = (unsigned)scan[a.nf];
+    }
     if (f >= a.nf || !a.f_first[f]) return;
     const int l = a.f_lm[f];
     a.l_slot[l] = n_opt + scan[f];
@@ -186,6 +193,7 @@ __global__ __launch_bounds__(kT) void k_pose_fill(WinArgs a, const int* pscan, c
         plm[o] = a.l_slot[a.f_lm[f]];
     }
     if (f <= a.nk) kf_obs_ptr[f] = pscan[a.wptr[f]];  // (wptr[nk] == nf: the total)
+    if (f == 0) a.counts[6] = (unsigned)pscan[a.nf];  // pose-stage observations, for the read-back
 }
 
 // landmark-stage observation check (local_ba.cpp:186-204); returns the window feature or -1
@@ -209,10 +217,17 @@ __device__ __forceinline__ int lobs_feature(const WinArgs& a, int l, int64_t o, 
     return f;
 }
 
-__global__ __launch_bounds__(kT) void k_lobs_count(WinArgs a, const int* inv, int n_opt, int* cnt) {
+// over the slots [0, cap) (cap: the map's landmark count, an upper bound of n_opt, which is read
+// on the device): slots >= n_opt count 0, so the scan over cap + 1 elements agrees with one over
+// n_opt + 1 on its first n_opt + 1 outputs
+__global__ __launch_bounds__(kT) void k_lobs_count(WinArgs a, const int* inv, const int* n_opt_dev, int cap, int* cnt) {
     const int s = blockIdx.x * kT + threadIdx.x;
-    if (s == 0) cnt[n_opt] = 0;  // (the scan's extra element)
-    if (s >= n_opt) return;
+    if (s == 0) cnt[cap] = 0;  // (the scan's extra element)
+    if (s >= cap) return;
+    if (s >= *n_opt_dev) {
+        cnt[s] = 0;
+        return;
+    }
     const int l = inv[s];
     int c = 0, row;
     for (int64_t o = a.optr[l]; o < a.optr[l + 1]; ++o) c += lobs_feature(a, l, o, row) >= 0 ? 1 : 0;
@@ -467,49 +482,46 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     VX_LAUNCH_CHECK(c, "plan slot kernels");
     int* first_scan = B.scan_b.as<int>();
     if ((rc = scan(c, B.tmp, a.f_first, first_scan, nf))) return rc;
-    int hc[3] = {0, 0, 0};  // n_opt, n_fixed, n_landmarks_global
-    VX_HIP(c, hipMemcpyAsync(&hc[0], opt_scan + nl, 4, hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipMemcpyAsync(&hc[1], first_scan + nf, 4, hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipMemcpyAsync(&hc[2], B.counts.p, 4, hipMemcpyDeviceToHost, s));
-    clk.mark("core: counts requested");
-    VX_HIP(c, hipStreamSynchronize(s));
-    clk.mark("core: counts back");
-    p->n_landmarks_global = hc[2];
-    if (hc[2] == 0) return VX_OK;  // no optimised landmark anywhere (local_ba.cpp:106-108)
-    p->status = 0;
-    p->n_kf = nk;
-    p->kf_map_idx = win;
-    const int n_opt = hc[0], n_lm = hc[0] + hc[1];
-    p->n_opt = n_opt;
-    p->n_lm = n_lm;
-    hipLaunchKernelGGL(k_fixed_slots, dim3(grid(nf)), dim3(kT), 0, s, a, first_scan, n_opt, inv);
+    // No read-back here: the counts stay on the device (n_opt = opt_scan[nl]) and every size below
+    // is bounded by the map (n_opt, n_lm <= nl): one synchronisation for the whole core build.
+    const int* n_opt_dev = opt_scan + nl;
+    hipLaunchKernelGGL(k_fixed_slots, dim3(grid(nf)), dim3(kT), 0, s, a, (const int*)first_scan, n_opt_dev, inv);
     // pose-stage CSR
     int* pscan = B.scan_b.as<int>();  // (first_scan consumed by k_fixed_slots above, stream-ordered)
     if ((rc = scan(c, B.tmp, a.f_pv, pscan, nf))) return rc;
-    // (sized for every window feature: the count arrives with the next read-back, no sync for it)
+    // (sized for every window feature: the count arrives with the read-back)
     VX_HIP(c, p->pobs_uv.ensure((size_t)std::max(nf, 1) * sizeof(double2)));
     VX_HIP(c, p->pobs_lm.ensure((size_t)std::max(nf, 1) * 4));
     VX_HIP(c, p->kf_obs_ptr.ensure((size_t)(nk + 1) * 4));
     hipLaunchKernelGGL(k_pose_fill, dim3(grid(std::max(nf, nk + 1))), dim3(kT), 0, s, a, pscan,
                        in.wuv, p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(), p->kf_obs_ptr.as<int>());
-    // landmark-stage CSR
+    // landmark-stage CSR over all nl slots (those past n_opt count 0)
     int* cnt = B.cnt.as<int>();
-    hipLaunchKernelGGL(k_lobs_count, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, cnt);
+    hipLaunchKernelGGL(k_lobs_count, dim3(grid(nl)), dim3(kT), 0, s, a, inv, n_opt_dev, nl, cnt);
     VX_LAUNCH_CHECK(c, "plan CSR kernels");
-    VX_HIP(c, p->lobs_ptr.ensure((size_t)(n_opt + 1) * 4));
-    if ((rc = scan(c, B.tmp, cnt, p->lobs_ptr.as<int>(), n_opt))) return rc;
-    // one read-back: the pose-stage count, the landmark-stage pointers, slot -> map index (pinned)
-    VX_HIP(c, B.rb_host.ensure((size_t)(n_opt + 1 + std::max(n_lm, 1) + 4) * 4, true));
+    VX_HIP(c, p->lobs_ptr.ensure((size_t)(nl + 1) * 4));
+    if ((rc = scan(c, B.tmp, cnt, p->lobs_ptr.as<int>(), nl))) return rc;
+    // the one read-back: counts (global optimised landmarks, n_opt, n_fixed, pose-stage
+    // observations), the landmark-stage pointers, slot -> map index (pinned)
+    VX_HIP(c, B.rb_host.ensure((size_t)(8 + 2 * (size_t)nl + 1) * 4, true));
     int* RB = static_cast<int*>(B.rb_host.p);
-    VX_HIP(c, hipMemcpyAsync(RB, pscan + nf, 4, hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipMemcpyAsync(RB + 4, p->lobs_ptr.p, (size_t)(n_opt + 1) * 4, hipMemcpyDeviceToHost, s));
-    VX_HIP(c, hipMemcpyAsync(RB + 4 + n_opt + 1, inv, (size_t)n_lm * 4, hipMemcpyDeviceToHost, s));
-    clk.mark("core: CSR pointers requested");
+    VX_HIP(c, hipMemcpyAsync(RB, B.counts.p, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
+    VX_HIP(c, hipMemcpyAsync(RB + 8, p->lobs_ptr.p, (size_t)(nl + 1) * 4, hipMemcpyDeviceToHost, s));
+    if (nl) VX_HIP(c, hipMemcpyAsync(RB + 8 + nl + 1, inv, (size_t)nl * 4, hipMemcpyDeviceToHost, s));
+    clk.mark("core: counts + CSR requested");
     VX_HIP(c, hipStreamSynchronize(s));
-    clk.mark("core: CSR pointers back");
-    p->n_pose_obs = RB[0];
-    const std::vector<int> lptr(RB + 4, RB + 4 + n_opt + 1);
-    const int* inv_h = RB + 4 + n_opt + 1;
+    clk.mark("core: counts + CSR back");
+    p->n_landmarks_global = RB[0];
+    if (RB[0] == 0) return VX_OK;  // no optimised landmark anywhere (local_ba.cpp:106-108)
+    p->status = 0;
+    p->n_kf = nk;
+    p->kf_map_idx = win;
+    const int n_opt = RB[4], n_lm = RB[4] + RB[5];
+    p->n_opt = n_opt;
+    p->n_lm = n_lm;
+    p->n_pose_obs = RB[6];
+    const std::vector<int> lptr(RB + 8, RB + 8 + n_opt + 1);
+    const int* inv_h = RB + 8 + nl + 1;
     const int n_lobs = lptr[n_opt];
     p->n_lm_obs = n_lobs;
     p->lm_map_idx.assign(inv_h, inv_h + n_lm);
@@ -614,23 +626,39 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
     VX_HIP(c, hipSetDevice(c->device));
     vx_ctx::PlanScratch& B = c->plan_scratch;
     int rc;
-    if ((rc = up(c, B.wptr, wptr.data(), wptr.size()))) return rc;
-    if ((rc = up(c, B.cam, cam.data(), cam.size()))) return rc;
-    if ((rc = up(c, B.wid, wid.data(), wid.size()))) return rc;
-    if ((rc = up(c, B.optr /* staging: source offsets, then window rows */, src.data(), src.size()))) return rc;
+    // the window's keyframe tables in one pinned block, one upload: source offsets (i64), ids
+    // (u64), rows (i32, nk + 1), map indices (i32), camera flags (u8)
+    const size_t o_src = 0, o_wid = o_src + 8 * (size_t)nk, o_wptr = o_wid + 8 * (size_t)nk,
+                 o_win = o_wptr + 4 * ((size_t)nk + 2), o_cam = o_win + 4 * ((size_t)nk + 2),
+                 o_end = o_cam + (size_t)nk + 8;
+    VX_HIP(c, B.win_host.ensure(o_end, true));
+    VX_HIP(c, B.win.ensure(o_end));
+    {
+        uint8_t* H = static_cast<uint8_t*>(B.win_host.p);
+        std::memcpy(H + o_src, src.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_wid, wid.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_wptr, wptr.data(), 4 * ((size_t)nk + 1));
+        for (int r = 0; r < nk; ++r) reinterpret_cast<int*>(H + o_win)[r] = win[r];
+        std::memcpy(H + o_cam, cam.data(), (size_t)nk);
+    }
+    VX_HIP(c, hipMemcpyAsync(B.win.p, B.win_host.p, o_end, hipMemcpyHostToDevice, c->stream));
+    uint8_t* WD = B.win.as<uint8_t>();
+    const int64_t* d_src = reinterpret_cast<const int64_t*>(WD + o_src);
+    const uint64_t* d_wid = reinterpret_cast<const uint64_t*>(WD + o_wid);
+    const int* d_wptr = reinterpret_cast<const int*>(WD + o_wptr);
+    const int* d_win = reinterpret_cast<const int*>(WD + o_win);
+    const uint8_t* d_cam = WD + o_cam;
     VX_HIP(c, B.wlm.ensure((size_t)std::max(nf, 1) * 8));
     VX_HIP(c, B.wfl.ensure((size_t)std::max(nf, 1)));
     VX_HIP(c, B.wuv.ensure((size_t)std::max(nf, 1) * 16));
-    hipLaunchKernelGGL(k_gather_window, dim3(grid(nf)), dim3(kT), 0, c->stream, nk, nf, (const int*)B.wptr.as<int>(),
-                       (const int64_t*)B.optr.as<int64_t>(), (const double*)m->feat_uv.as<double>(),
+    hipLaunchKernelGGL(k_gather_window, dim3(grid(nf)), dim3(kT), 0, c->stream, nk, nf, d_wptr,
+                       d_src, (const double*)m->feat_uv.as<double>(),
                        (const uint64_t*)m->feat_lm.as<uint64_t>(), (const uint8_t*)m->feat_fl.as<uint8_t>(),
                        B.wuv.as<double>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>());
     VX_LAUNCH_CHECK(c, "k_gather_window");
-    std::vector<int> win_i(win.begin(), win.end());
-    if ((rc = up(c, B.okf /* staging: window keyframe indices */, win_i.data(), win_i.size()))) return rc;
     VX_HIP(c, p->kf_pose0.ensure((size_t)nk * 8 * sizeof(double)));
     VX_HIP(c, p->kf_intr.ensure((size_t)nk * 4 * sizeof(double)));
-    hipLaunchKernelGGL(k_gather_kf, dim3(grid(nk)), dim3(kT), 0, c->stream, nk, (const int*)B.okf.as<int>(),
+    hipLaunchKernelGGL(k_gather_kf, dim3(grid(nk)), dim3(kT), 0, c->stream, nk, d_win,
                        (const double*)m->kf_pose.as<double>(), (const double*)m->kf_intr.as<double>(),
                        p->kf_pose0.as<double>(), p->kf_intr.as<double>());
     VX_LAUNCH_CHECK(c, "k_gather_kf");
@@ -638,8 +666,8 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
     if ((rc = dmap_build_csr(c, m))) return rc;
     clk.mark("dmap: CSR ready");
     const int nl = (int)m->n_lm;
-    BuildInputs in{nk, nf, nl, B.wptr.as<int>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(), B.cam.as<uint8_t>(),
-                   B.wid.as<uint64_t>(), B.wuv.as<double>(), m->lm_id.as<uint64_t>(), m->lm_bad.as<uint8_t>(),
+    BuildInputs in{nk, nf, nl, d_wptr, B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(), d_cam,
+                   d_wid, B.wuv.as<double>(), m->lm_id.as<uint64_t>(), m->lm_bad.as<uint8_t>(),
                    m->optr.as<int64_t>(), m->okf.as<uint64_t>(), m->ofi.as<uint64_t>(), m->lm_pos.as<double>()};
     rc = build_core(c, in, win, kf_flags, p);
     if (rc) {
@@ -651,7 +679,8 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
     if (p->status == 0) {
         VX_HIP(c, p->lm_map_dev.ensure((size_t)std::max(p->n_lm, 1) * 4));
         VX_HIP(c, hipMemcpyAsync(p->lm_map_dev.p, B.inv.p, (size_t)p->n_lm * 4, hipMemcpyDeviceToDevice, c->stream));
-        if ((rc = up(c, p->kf_map_dev, p->kf_map_idx.data(), p->kf_map_idx.size()))) return rc;
+        VX_HIP(c, p->kf_map_dev.ensure((size_t)std::max(nk, 1) * 4));
+        VX_HIP(c, hipMemcpyAsync(p->kf_map_dev.p, d_win, (size_t)nk * 4, hipMemcpyDeviceToDevice, c->stream));
     }
     clk.mark("dmap: tables queued");
     VX_HIP(c, hipStreamSynchronize(c->stream));

@@ -211,6 +211,8 @@ struct vx_ctx {
         vx::DevBuf fb, fb_groups, fb_tmp;  // device build of the fused layout (ba_fused_build.hip)
         vx::PinnedBuf fb_host;             // its two small read-backs
         vx::PinnedBuf rb_host, up_host;    // build_core's read-back and its table uploads
+        vx::PinnedBuf win_host;            // the resident-map build's window tables, one upload ...
+        vx::DevBuf win;                    // ... into one device block
     } plan_scratch;
     // LocalBA plans of this context: parked buffer sets of destroyed plans (adopted by the next
     // vx_ba_plan_create) and the live plans (detached when the context goes first)
