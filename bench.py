@@ -4,7 +4,8 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
     torchrun --nproc-per-node N ... bench.py --gpus N ...
 
-One step = one frame through the hot path, everything resident in HBM before timing starts:
+One step = two rounds of the pipeline: F frames (F = twice the extraction contexts, 6 by default;
+--frames-per-step), each through the hot path, everything resident in HBM before timing starts:
   1. ORBExtractor::Extract of a 640x480 BGR8 frame (n_features 2000 at C3)   -> slot i % 3
   2. ORBMatcher::Match(previous frame, this frame): BF Hamming kNN-2 + ratio -> matches
   3. LocalBA::Optimize over the sliding window (C3: 50 KF / 20k landmarks, <= 5 iterations)
@@ -385,6 +386,9 @@ def main():
     ap.add_argument("--extract-ctx", type=int, default=3, choices=(1, 2, 3, 4),
                     help="extraction contexts (with --streams 3): frames alternate between them, so the "
                          "extraction of frame t+1 overlaps frame t's; Match and LocalBA stay in frame order")
+    ap.add_argument("--frames-per-step", type=int, default=0,
+                    help="frames per timed step (default: twice the extraction contexts with --streams 3, i.e. "
+                         "two rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),
                     help="with --streams 3: Match(t) on frame t's extraction context right after Extract(t) "
                          "(default: one hardware queue fewer; measured 0.073 vs 0.073-0.076 ms/frame, steadier) "
@@ -519,6 +523,16 @@ def main():
         for c in ctxs:
             c.synchronize()
 
+    # One timed step = F frames, two rounds of the pipeline (F = 2 E by default): each of them runs
+    # Extract, Match and LocalBA.  With one frame per step the pipeline's fill (one frame's whole
+    # latency, ~0.19 ms at C3) weighed ~10 % in the driver's 20-step run; over 20 x 6 frames it is
+    # ~1.5 % (scripts/gpu_r03_short_vs_long.sh)
+    F = args.frames_per_step if args.frames_per_step > 0 else (2 * E if args.streams == 3 else 1)
+
+    def fstep(i):
+        for f in range(F):
+            step(i * F + f)
+
     # ---- fixed internal pre-warm, outside the reported warm-up: every launch sequence a step can
     # take is keyed by (context, slot, frame buffer) — lcm(frames, 3 E) distinct extraction keys, 3 E
     # match keys, one LocalBA plan — and is replayed from a hipGraph only from its third sighting
@@ -537,7 +551,7 @@ def main():
         for c in ctxs:
             c.prof_enable(True)
         for i in range(args.warmup):
-            step(i)
+            fstep(i)
         prof = {}
         for c in ctxs:  # (a stage that runs on several contexts — the extraction ones — is summed)
             for k, v in c.prof_read(reset=True).items():
@@ -548,7 +562,7 @@ def main():
         stages = {k: (v[0] / max(v[1], 1), v[1] / args.warmup) for k, v in prof.items() if v[1]}
 
     # ---- the timed region: no events inside (a timing event pair per launch costs ~25 % here)
-    elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
+    elapsed = timed_loop(fstep, args.steps, args.warmup, sync, dist)
     enqueue_ms = 1e3 * timed_loop.enqueue_s / args.steps
 
     # ---- roofline pass: the same K steps again, HIP events around every launch of the dominant
@@ -558,7 +572,7 @@ def main():
     dom_prof, elapsed_ev = (0.0, 0), None
     if dominant:
         dctx.prof_enable(True, stages=[dominant])
-        elapsed_ev = timed_loop(step, args.steps, 0, sync, dist)
+        elapsed_ev = timed_loop(fstep, args.steps, 0, sync, dist)
         dom_prof = dctx.prof_read(reset=True).get(dominant, (0.0, 0))
         dctx.prof_enable(False)
 
@@ -567,13 +581,13 @@ def main():
     for i in range(20):
         sync()
         t0 = time.perf_counter()
-        step(args.warmup + args.steps + i)
+        step((args.warmup + args.steps) * F + i)
         sync()
         lat.append(time.perf_counter() - t0)
     latency_ms = 1e3 * float(np.median(lat))
 
     # counts for the byte formulas
-    last = args.warmup + args.steps + 19
+    last = (args.warmup + args.steps) * F + 19
     kps, _ = ectxs[loc(last)[0]].orb_fetch(loc(last)[1])
     matches = (ectxs[loc(last)[0]] if mon else mctx).match_fetch()
     st = plan.fetch(None)
@@ -584,7 +598,7 @@ def main():
               "n_match": len(matches), "n_pose_obs": info["n_pose_obs"], "n_lm_obs": info["n_lm_obs"],
               "n_split": info["n_split"], "n_opt": info["n_opt"], "n_kf": info["n_kf"]}
 
-    frames_total = args.steps * N
+    frames_total = args.steps * F * N
     ms_per_step = 1e3 * elapsed / args.steps
     value = 1e3 * elapsed / frames_total
 
@@ -638,10 +652,10 @@ def main():
             "dtype": "u8/i32 (FAST, pyramid, BRIEF), f32 (Harris, blur, angle), f64 (BA)",
             "data": "synthetic",
             "config": {
-                "workload": (f"{args.config}: per rank one {w}x{h} BGR8 frame, {nf} ORB, kNN-2 Hamming match vs the "
-                             f"previous frame; one LocalBA window of {nk * N} KF / {nl * N} landmarks per step "
-                             f"(<= 5 alternating iterations), landmark-sharded over {N} GPU(s)"),
-                "frames_per_step": N,
+                "workload": (f"{args.config}: per rank and step {F} {w}x{h} BGR8 frame(s), each: {nf} ORB, kNN-2 "
+                             f"Hamming match vs the previous frame, one LocalBA window of {nk * N} KF / {nl * N} "
+                             f"landmarks (<= 5 alternating iterations), landmark-sharded over {N} GPU(s)"),
+                "frames_per_step": F * N,
                 "parallelism": f"frames: 1 per rank; BA: landmark shards x{N}" + (" + RCCL all-reduce" if N > 1 else ""),
                 "streams": {1: "1: Extract, Match, LocalBA back to back",
                             2: "2: Extract+Match | LocalBA (LocalBA(t) after Match(t))",

@@ -583,6 +583,12 @@ __global__ __launch_bounds__(kT) void k_gather_window(int nk, int nf, const int*
     wfl[f] = fl[g];
 }
 // window keyframes' poses (8-double rows, last 0) and intrinsics
+// the finished plan's slot -> map index tables for vx_ba_plan_apply_dmap, one launch
+__global__ void k_map_tables(const int* inv, int n_lm, const int* win, int nk, int* lm_map, int* kf_map) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_lm) lm_map[i] = inv[i];
+    if (i < nk) kf_map[i] = win[i];
+}
 __global__ void k_gather_kf(int nk, const int* win, const double* pose, const double* intr, double* pose0,
                             double* intr0) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
@@ -678,9 +684,11 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
     // still on the device: build_core's slot -> map index array)
     if (p->status == 0) {
         VX_HIP(c, p->lm_map_dev.ensure((size_t)std::max(p->n_lm, 1) * 4));
-        VX_HIP(c, hipMemcpyAsync(p->lm_map_dev.p, B.inv.p, (size_t)p->n_lm * 4, hipMemcpyDeviceToDevice, c->stream));
         VX_HIP(c, p->kf_map_dev.ensure((size_t)std::max(nk, 1) * 4));
-        VX_HIP(c, hipMemcpyAsync(p->kf_map_dev.p, d_win, (size_t)nk * 4, hipMemcpyDeviceToDevice, c->stream));
+        hipLaunchKernelGGL(k_map_tables, dim3(grid(std::max(p->n_lm, nk))), dim3(kT), 0, c->stream,
+                           (const int*)B.inv.as<int>(), p->n_lm, d_win, nk, p->lm_map_dev.as<int>(),
+                           p->kf_map_dev.as<int>());
+        VX_LAUNCH_CHECK(c, "k_map_tables");
     }
     clk.mark("dmap: tables queued");
     VX_HIP(c, hipStreamSynchronize(c->stream));
