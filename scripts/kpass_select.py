@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "visionx-slam_amd", "python"))
 import vxslam  # noqa: E402
 from vxslam import synth  # noqa: E402
 
-KIND = {0: "mem", 1: "team", 2: "wave", 3: "nth-done/part", 4: "part-done", 5: "tail64"}
+KIND = {0: "mem", 1: "team", 2: "wave", 3: "nth-done/part", 4: "part-done", 5: "tail64", 6: "tail128", 7: "tail256"}
 
 
 def read():
