@@ -16,8 +16,10 @@ python3 scripts/pmc_summary.py "$(find gpurun_out/pmc_fetch_${TAG} -name '*count
     "$(find gpurun_out/pmc_write_${TAG} -name '*counter_collection.csv' | head -1)" gpurun_out/pmc_traffic_${TAG}.json \
     > gpurun_out/pmc_traffic_${TAG}.txt || exit 1
 cp gpurun_out/pmc_traffic_${TAG}.json profiles/pmc_traffic.json
+rm -rf gpurun_out/pmc_fetch_${TAG} gpurun_out/pmc_write_${TAG}  # (raw counter CSVs: tens of MB)
 cat gpurun_out/pmc_traffic_${TAG}.txt
 timeout -k 10 600 python bench.py > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { echo "bench failed"; tail -20 gpurun_out/bench_${TAG}.err; exit 1; }
 cat gpurun_out/bench_${TAG}.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --no-cpu-baseline > gpurun_out/prof_${TAG}.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/prof_${TAG}.log; exit 1; }
+rm -f gpurun_out/prof_${TAG}/*kernel_trace.csv  # (one row per launch: tens of MB; the stats stay)
 find gpurun_out/prof_${TAG} -name "*kernel_stats.csv"
