@@ -189,19 +189,27 @@ class Dist:
 
 def timed_loop(step, steps, warmup, sync, dist):
     """W untimed warm-up steps, then K steps bracketed by barrier + device sync on both sides;
-    returns the max over ranks of the elapsed seconds."""
+    returns the max over ranks of the elapsed seconds.  Python's cyclic collector is paused over
+    the timed steps (a collection there is a host stall the pipeline cannot hide)."""
+    import gc
+
     for i in range(warmup):
         step(i)
     sync()
     dist.barrier()
     sync()
-    t0 = time.perf_counter()
-    for i in range(steps):
-        step(warmup + i)
-    timed_loop.enqueue_s = time.perf_counter() - t0  # host enqueue alone (diagnostic)
-    sync()
-    dist.barrier()
-    t1 = time.perf_counter()
+    gc.collect()
+    gc.disable()
+    try:
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(warmup + i)
+        timed_loop.enqueue_s = time.perf_counter() - t0  # host enqueue alone (diagnostic)
+        sync()
+        dist.barrier()
+        t1 = time.perf_counter()
+    finally:
+        gc.enable()
     return dist.max(t1 - t0)
 
 
