@@ -2089,7 +2089,9 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
     const int cx = __float2int_rn(px * inv), cy = __float2int_rn(py * inv);
     float ang = angle;
     ang *= (float)(M_PI / 180.f);
-    const float ca = (float)cos((double)ang), sa = (float)sin((double)ang);
+    double sd, cd;  // OpenCV: (float)cos((double)angle), (float)sin(...); one shared argument reduction
+    sincos((double)ang, &sd, &cd);
+    const float ca = (float)cd, sa = (float)sd;
     const uint8_t* ctr = blur + a.off[l] + (long long)cy * W + cx;
     unsigned long long words[4];
 #pragma unroll
