@@ -4,7 +4,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
     torchrun --nproc-per-node N ... bench.py --gpus N ...
 
-One step = two rounds of the pipeline: F frames (F = twice the extraction contexts, 6 by default;
+One step = four rounds of the pipeline: F frames (F = 4 x the extraction contexts, 12 by default;
 --frames-per-step), each through the hot path, everything resident in HBM before timing starts:
   1. ORBExtractor::Extract of a 640x480 BGR8 frame (n_features 2000 at C3)   -> slot i % 3
   2. ORBMatcher::Match(previous frame, this frame): BF Hamming kNN-2 + ratio -> matches
@@ -395,8 +395,8 @@ def main():
                     help="extraction contexts (with --streams 3): frames alternate between them, so the "
                          "extraction of frame t+1 overlaps frame t's; Match and LocalBA stay in frame order")
     ap.add_argument("--frames-per-step", type=int, default=0,
-                    help="frames per timed step (default: twice the extraction contexts with --streams 3, i.e. "
-                         "two rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
+                    help="frames per timed step (default: four times the extraction contexts with --streams 3, "
+                         "i.e. four rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),
                     help="with --streams 3: Match(t) on frame t's extraction context right after Extract(t) "
                          "(default: one hardware queue fewer; measured 0.073 vs 0.073-0.076 ms/frame, steadier) "
@@ -568,11 +568,12 @@ def main():
         for c in ctxs:
             c.synchronize()
 
-    # One timed step = F frames, two rounds of the pipeline (F = 2 E by default): each of them runs
+    # One timed step = F frames, four rounds of the pipeline (F = 4 E by default): each of them runs
     # Extract, Match and LocalBA.  With one frame per step the pipeline's fill (one frame's whole
-    # latency, ~0.19 ms at C3) weighed ~10 % in the driver's 20-step run; over 20 x 6 frames it is
-    # ~1.5 % (scripts/gpu_r03_short_vs_long.sh)
-    F = args.frames_per_step if args.frames_per_step > 0 else (2 * E if args.streams == 3 else 1)
+    # latency, ~0.19 ms at C3) weighed ~10 % in the driver's 20-step run; over 20 x 12 frames it is
+    # < 1 % (measured 20-step / 2000-step: 1.5-4.6 % with 12 frames, 1-6 % with 6, box noise ~2 %;
+    # scripts/gpu_r03_short_vs_long.sh)
+    F = args.frames_per_step if args.frames_per_step > 0 else (4 * E if args.streams == 3 else 1)
 
     def fstep(i):
         for f in range(F):
