@@ -38,6 +38,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <unordered_map>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 #include "vx_internal.hpp"
@@ -884,6 +886,73 @@ int find_root(std::vector<int>& par, int x) {
     return x;
 }
 
+// Host threads of the plan build: at most 16 (the CPU share of one GPU on the target node),
+// $VX_SBA_PLAN_THREADS overrides (1: serial).
+int plan_threads() {
+    static const int t = [] {
+        if (const char* e = std::getenv("VX_SBA_PLAN_THREADS")) return std::max(1, std::atoi(e));
+        return (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    }();
+    return t;
+}
+// fn(t) for t in [0, T) on T threads (fn(0) on the caller); every t writes disjoint data
+template <class F>
+void run_threads(int T, F&& fn) {
+    if (T <= 1) {
+        fn(0);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (int t = 1; t < T; ++t) th.emplace_back([&fn, t] { fn(t); });
+    fn(0);
+    for (auto& x : th) x.join();
+}
+
+// select_window (ba_common.hpp, SelectKeyFrames + the optimised landmark set) keeping its landmark
+// lookups for the observation pass: feat_l[fbase[r] + i] = map index of window keyframe r's feature i
+// (features with has_landmark set and a landmark in the map; -1 otherwise), kept for the
+// observation pass.  Same window, same opt_all.
+void select_window_lookup(const vx_map_view* m, uint64_t ref_kf_id, int has_ref, int window_size,
+                          int min_point_observations, Window& w, std::vector<int64_t>& fbase,
+                          std::vector<int>& feat_l) {
+    w = Window{};
+    if (!m || m->n_kf <= 0) return;
+    std::vector<int> order(m->n_kf);
+    for (int i = 0; i < m->n_kf; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int x, int y) { return m->kf_id[x] < m->kf_id[y]; });
+    const int window = std::max(1, window_size);
+    const uint64_t max_id = has_ref ? ref_kf_id : m->kf_id[order.back()];
+    for (int i = m->n_kf - 1; i >= 0 && (int)w.win.size() < window; --i) {
+        if (m->kf_id[order[i]] > max_id) continue;
+        w.win.push_back(order[i]);
+    }
+    std::reverse(w.win.begin(), w.win.end());
+    if (w.win.size() < 2) return;
+    w.lm_by_id.build(m->lm_id, m->n_lm);
+    const int nk = (int)w.win.size();
+    fbase.assign(nk + 1, 0);
+    for (int r = 0; r < nk; ++r) fbase[r + 1] = fbase[r] + (m->kf_feat_ptr[w.win[r] + 1] - m->kf_feat_ptr[w.win[r]]);
+    feat_l.assign((size_t)fbase[nk], -1);
+    // (serial: on 16 threads this pass measured no faster at C5 — the hash build, the sort and the
+    // filter dominate the stage — and thread start-up made C3 slower)
+    for (int r = 0; r < nk; ++r) {
+        const int64_t f0 = m->kf_feat_ptr[w.win[r]], f1 = m->kf_feat_ptr[w.win[r] + 1];
+        for (int64_t f = f0; f < f1; ++f)
+            if (m->feat_flags[f] & 1) feat_l[(size_t)(fbase[r] + (f - f0))] = w.lm_by_id.get(m->feat_lm_id[f]);
+    }
+    // landmarks referenced by a window feature, then the filter, in map-index order
+    std::vector<uint8_t> ref((size_t)std::max(m->n_lm, 1), 0);
+    for (const int l : feat_l)
+        if (l >= 0) ref[l] = 1;
+    for (int l = 0; l < m->n_lm; ++l) {
+        if (!ref[l] || m->lm_bad[l]) continue;
+        if (m->lm_obs_ptr[l + 1] - m->lm_obs_ptr[l] < (int64_t)min_point_observations) continue;
+        w.opt_all.push_back(l);
+    }
+    if (!w.opt_all.empty()) w.status = 0;
+}
+
 int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_ref, vx_sba_plan* p) {
     const vx_sba_options& o = p->opt;
     static const bool timing = std::getenv("VX_SBA_PLAN_TIMING") != nullptr;
@@ -896,7 +965,9 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     };
     p->status = 1;
     Window W;
-    select_window(m, ref_kf_id, has_ref, o.window_size, o.min_point_observations, W);
+    std::vector<int64_t> wfbase;  // window feature ranges and their landmark lookups
+    std::vector<int> wfeat_l;
+    select_window_lookup(m, ref_kf_id, has_ref, o.window_size, o.min_point_observations, W, wfbase, wfeat_l);
     p->n_window_kf = (int)W.win.size();
     p->n_landmarks_global = (int)W.opt_all.size();
     if (W.status != 0) return VX_OK;
@@ -927,23 +998,39 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     struct HObs { int kf, slot; double u, v; };
     std::vector<HObs> all;
     all.reserve(4096);
+    // the window features' landmark of each pose-stage observation (or -1): the hash probes, in
+    // parallel over keyframes; then one sequential pass numbers the fixed landmarks as met
+    std::vector<int64_t> fbase(nk + 1, 0);
     for (int r = 0; r < nk; ++r) {
         const int k = win[r];
         for (int j = 0; j < 7; ++j) pose0[8 * r + j] = m->kf_pose[7 * k + j];
         for (int j = 0; j < 4; ++j) intr[4 * r + j] = m->kf_intr[4 * k + j];
         const bool cam = m->kf_has_cam[k] != 0;
         flags[r] = (cam ? 1 : 0) | ((r < o.fixed_keyframes || !cam) ? 2 : 0);
-        if (!cam) continue;
-        for (int64_t f = m->kf_feat_ptr[k]; f < m->kf_feat_ptr[k + 1]; ++f) {
-            const uint8_t fl = m->feat_flags[f];
-            if (!(fl & 1) || (fl & 2)) continue;
-            const int l = W.lm_by_id.get(m->feat_lm_id[f]);
+        fbase[r + 1] = fbase[r] + (cam ? m->kf_feat_ptr[k + 1] - m->kf_feat_ptr[k] : 0);
+    }
+    std::vector<int> feat_l((size_t)fbase[nk]);
+    for (int r = 0; r < nk; ++r) {  // (the lookups from select_window_lookup; the pose-stage checks)
+        if (!(flags[r] & 1)) continue;
+        const int64_t f0 = m->kf_feat_ptr[win[r]];
+        for (int64_t i = 0; i < fbase[r + 1] - fbase[r]; ++i) {
+            const uint8_t fl = m->feat_flags[f0 + i];
+            int l = (fl & 2) ? -1 : wfeat_l[(size_t)(wfbase[r] + i)];
+            if (l >= 0 && (m->lm_bad[l] || !owned(l))) l = -1;
+            feat_l[(size_t)(fbase[r] + i)] = l;
+        }
+    }
+    for (int r = 0; r < nk; ++r) {
+        if (!(flags[r] & 1)) continue;
+        const int64_t f0 = m->kf_feat_ptr[win[r]];
+        for (int64_t i = fbase[r]; i < fbase[r + 1]; ++i) {
+            const int l = feat_l[(size_t)i];
             if (l < 0) continue;
-            if (m->lm_bad[l] || !owned(l)) continue;
             if (slot_of[l] < 0) {  // a landmark the pose stage sees but BA does not optimise
                 slot_of[l] = (int)p->lm_map_idx.size();
                 p->lm_map_idx.push_back(l);
             }
+            const int64_t f = f0 + (i - fbase[r]);
             all.push_back(HObs{r, slot_of[l], m->feat_uv[2 * f], m->feat_uv[2 * f + 1]});
         }
     }
@@ -1003,19 +1090,84 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     }
 
     lap("observations");
-    // ---- connected components of the free keyframes' covisibility graph
-    std::vector<int> par(nk);
-    std::iota(par.begin(), par.end(), 0);
-    for (int s = 0; s < n_opt; ++s) {
-        int first = -1;
-        for (int ob = lptr[s]; ob < lptr[s + 1]; ++ob) {
-            if (flags[okf[ob]] & 2) continue;
-            if (first < 0)
-                first = okf[ob];
-            else
-                par[find_root(par, okf[ob])] = find_root(par, first);
+    // ---- blocks of the reduced system: every keyframe's diagonal block, then the off-diagonal
+    // (i > j) blocks of co-observing free keyframes, each with its co-observation pairs
+    // Every (i >= j) pair of free keyframes co-observing a landmark contributes the pair of its two
+    // observations to block (i, j).  Blocks: the nk diagonal blocks in keyframe order, then the
+    // non-empty off-diagonal blocks by (i, j); pairs inside a block by (o1, o2).  The pairs are
+    // generated in (o1, o2) order, so a two-pass counting sort by block key keeps that order; the
+    // passes run on T threads over contiguous slot ranges, thread t's pairs of a block placed after
+    // those of threads < t (the serial order exactly).
+    const int64_t nkey = (int64_t)nk * nk;
+    // (threads: one per 8192 slots — thread start-up costs tens of us — and at most 64 MB of
+    // per-thread key counts)
+    const int T = std::max(1, std::min({plan_threads(), n_opt / 8192,
+                                        (int)std::max<int64_t>(1, ((int64_t)1 << 24) / std::max<int64_t>(nkey, 1))}));
+    auto for_pairs = [&](int s0, int s1, auto&& emit) {
+        for (int sl = s0; sl < s1; ++sl)
+            for (int a1 = lptr[sl]; a1 < lptr[sl + 1]; ++a1) {
+                const int i = okf[a1];
+                if (flags[i] & 2) continue;
+                for (int a2 = lptr[sl]; a2 < lptr[sl + 1]; ++a2) {
+                    const int j = okf[a2];
+                    if ((flags[j] & 2) || j > i) continue;
+                    emit((int64_t)i * nk + j, a1, a2);
+                }
+            }
+    };
+    std::vector<int> sb(T + 1);  // thread t: slots [sb[t], sb[t + 1]), balanced by observations
+    for (int t = 0; t <= T; ++t)
+        sb[t] = (int)(std::lower_bound(lptr.begin(), lptr.end(), (int)((int64_t)n_oo * t / T)) - lptr.begin());
+    sb[0] = 0;
+    sb[T] = n_opt;
+    for (int t = 1; t < T; ++t) sb[t] = std::min(std::max(sb[t], sb[t - 1]), n_opt);
+    std::vector<std::vector<int>> kc(T, std::vector<int>((size_t)nkey, 0));
+    run_threads(T, [&](int t) { for_pairs(sb[t], sb[t + 1], [&](int64_t key, int, int) { ++kc[t][key]; }); });
+    std::vector<int> kcnt((size_t)nkey, 0);
+    for (int t = 0; t < T; ++t)
+        for (int64_t key = 0; key < nkey; ++key) kcnt[key] += kc[t][key];
+    std::vector<int2> bij;
+    std::vector<int> bptr{0};
+    std::vector<int> kpos((size_t)nkey, -1);  // output offset of each block key
+    int64_t total = 0;
+    for (int r = 0; r < nk; ++r) {
+        const int64_t key = (int64_t)r * nk + r;
+        bij.push_back(make_int2(r, r));
+        kpos[key] = (int)total;
+        total += kcnt[key];
+        bptr.push_back((int)total);
+    }
+    for (int64_t key = 0; key < nkey; ++key) {
+        const int i = (int)(key / nk), j = (int)(key % nk);
+        if (i == j || kcnt[key] == 0) continue;
+        bij.push_back(make_int2(i, j));
+        kpos[key] = (int)total;
+        total += kcnt[key];
+        bptr.push_back((int)total);
+    }
+    for (int64_t key = 0; key < nkey; ++key) {  // kc[t][key] := thread t's first output position
+        int run = kpos[key];
+        for (int t = 0; t < T; ++t) {
+            const int c = kc[t][key];
+            kc[t][key] = run;
+            run += c;
         }
     }
+    std::vector<int2> prs((size_t)total);
+    run_threads(T, [&](int t) {
+        for_pairs(sb[t], sb[t + 1], [&](int64_t key, int a1, int a2) { prs[kc[t][key]++] = make_int2(a1, a2); });
+    });
+    p->n_blocks = (int)bij.size();
+    p->n_pairs = (int64_t)prs.size();
+    lap("blocks");
+
+    // ---- connected components of the free keyframes' covisibility graph
+    // (over the off-diagonal blocks: two free keyframes share a block exactly when a landmark's
+    // observations join them, so the components are those of the landmark walk; numbered below
+    // by their first keyframe, whatever the union order)
+    std::vector<int> par(nk);
+    std::iota(par.begin(), par.end(), 0);
+    for (size_t b = (size_t)nk; b < bij.size(); ++b) par[find_root(par, bij[b].x)] = find_root(par, bij[b].y);
     std::vector<int> kcomp(nk, -1), klocal(nk, 0), root_comp(nk, -1);
     p->comp_kf_ptr_h.assign(1, 0);
     p->comp_kf_h.clear();
@@ -1056,51 +1208,6 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     p->comp_loff_h = loff;
 
     lap("components");
-    // ---- blocks of the reduced system: every keyframe's diagonal block, then the off-diagonal
-    // (i > j) blocks of co-observing free keyframes, each with its co-observation pairs
-    // Every (i >= j) pair of free keyframes co-observing a landmark contributes the pair of its two
-    // observations to block (i, j).  Blocks: the nk diagonal blocks in keyframe order, then the
-    // non-empty off-diagonal blocks by (i, j); pairs inside a block by (o1, o2).  The pairs are
-    // generated in (o1, o2) order, so a two-pass counting sort by block key keeps that order.
-    const int64_t nkey = (int64_t)nk * nk;
-    std::vector<int> kcnt((size_t)nkey, 0);
-    auto for_pairs = [&](auto&& emit) {
-        for (int sl = 0; sl < n_opt; ++sl)
-            for (int a1 = lptr[sl]; a1 < lptr[sl + 1]; ++a1) {
-                const int i = okf[a1];
-                if (flags[i] & 2) continue;
-                for (int a2 = lptr[sl]; a2 < lptr[sl + 1]; ++a2) {
-                    const int j = okf[a2];
-                    if ((flags[j] & 2) || j > i) continue;
-                    emit((int64_t)i * nk + j, a1, a2);
-                }
-            }
-    };
-    for_pairs([&](int64_t key, int, int) { ++kcnt[key]; });
-    std::vector<int2> bij;
-    std::vector<int> bptr{0};
-    std::vector<int> kpos((size_t)nkey, -1);  // output offset of each block key
-    int64_t total = 0;
-    for (int r = 0; r < nk; ++r) {
-        const int64_t key = (int64_t)r * nk + r;
-        bij.push_back(make_int2(r, r));
-        kpos[key] = (int)total;
-        total += kcnt[key];
-        bptr.push_back((int)total);
-    }
-    for (int64_t key = 0; key < nkey; ++key) {
-        const int i = (int)(key / nk), j = (int)(key % nk);
-        if (i == j || kcnt[key] == 0) continue;
-        bij.push_back(make_int2(i, j));
-        kpos[key] = (int)total;
-        total += kcnt[key];
-        bptr.push_back((int)total);
-    }
-    std::vector<int2> prs((size_t)total);
-    for_pairs([&](int64_t key, int a1, int a2) { prs[kpos[key]++] = make_int2(a1, a2); });
-    p->n_blocks = (int)bij.size();
-    p->n_pairs = (int64_t)prs.size();
-    lap("blocks");
 
     // ---- symbolic tile factorisation per component: which 16 x 16 tiles of L are nonzero (the
     // pattern of S's blocks plus Cholesky fill), and per step the panel / trailing-update / back-
