@@ -1010,7 +1010,10 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 // them.  Elements are u32 (FAST score << 24 | raster index) for the first retainBest and u64
 // (order-preserving Harris key << 32 | raster index) for the second; the arrays live in LDS when
 // they fit, in the level's global scratch otherwise.
-constexpr int kStlNT = 1024;
+#ifndef VX_SEL_THREADS
+#define VX_SEL_THREADS 1024
+#endif
+constexpr int kStlNT = VX_SEL_THREADS;
 constexpr int kStlWaves = kStlNT / 64;
 constexpr int kStlLds = 160 * 1024 - 256;      // dynamic LDS of k_select_stl: the engine's, then the arrays
 
