@@ -1182,6 +1182,8 @@ constexpr int kRgMail = 16400;                 // bytes per mailbox: (8192 / 2 +
 constexpr int kRgTrash = 4 * kRgMail + 32 + 64 * 4 + 32;  // + 4 spare slots + 64 ints; 16-aligned
 constexpr int kRgBytes = kRgTrash + 64 * 8 + 64 * 4;       // + one value and one int trash slot per lane
 static_assert(kRgBytes % 16 == 0, "engine scratch alignment");
+static_assert(kRgCap32 <= 64 * 8 * kStlWaves && RgCap<u64>::v <= 64 * 8 * kStlWaves,
+              "a team pass (<= 8 blocks a wave) must cover the engine's capacity: VX_SEL_THREADS >= 1024");
 
 // the engine's LDS: value mailboxes bl / br, position mailboxes lp / rp (team passes), a few ints
 // (per-wave counts and crossing candidates, results)
