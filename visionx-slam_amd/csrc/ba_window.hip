@@ -217,21 +217,28 @@ __device__ __forceinline__ int lobs_feature(const WinArgs& a, int l, int64_t o, 
     return f;
 }
 
-// over the slots [0, cap) (cap: the map's landmark count, an upper bound of n_opt, which is read
+// One wave per slot, its lanes over the landmark's observations (each lane's check is a chain of
+// dependent loads: a thread per slot walking them one after the other took 13 us at C3).
+// Over the slots [0, cap) (cap: the map's landmark count, an upper bound of n_opt, which is read
 // on the device): slots >= n_opt count 0, so the scan over cap + 1 elements agrees with one over
 // n_opt + 1 on its first n_opt + 1 outputs
 __global__ __launch_bounds__(kT) void k_lobs_count(WinArgs a, const int* inv, const int* n_opt_dev, int cap, int* cnt) {
-    const int s = blockIdx.x * kT + threadIdx.x;
-    if (s == 0) cnt[cap] = 0;  // (the scan's extra element)
+    const int s = (int)((blockIdx.x * (unsigned)kT + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+    if (s == 0 && lane == 0) cnt[cap] = 0;  // (the scan's extra element)
     if (s >= cap) return;
     if (s >= *n_opt_dev) {
-        cnt[s] = 0;
+        if (lane == 0) cnt[s] = 0;
         return;
     }
     const int l = inv[s];
-    int c = 0, row;
-    for (int64_t o = a.optr[l]; o < a.optr[l + 1]; ++o) c += lobs_feature(a, l, o, row) >= 0 ? 1 : 0;
-    cnt[s] = c;
+    const int64_t o0 = a.optr[l], o1 = a.optr[l + 1];
+    int c = 0;
+    for (int64_t base = o0; base < o1; base += 64) {
+        const int64_t o = base + lane;
+        int row;
+        c += __popcll(__ballot(o < o1 && lobs_feature(a, l, o, row) >= 0));
+    }
+    if (lane == 0) cnt[s] = c;
 }
 
 // the build's scratch state in one launch: empty hash slots, zeroed per-landmark / per-feature
@@ -251,19 +258,26 @@ __global__ __launch_bounds__(kT) void k_build_init(uint64_t* hkey, size_t hcap, 
     if (i < 16) counts[i] = 0;
 }
 
+// one wave per slot as in k_lobs_count; the valid observations keep their CSR order (ballot ranks)
 __global__ __launch_bounds__(kT) void k_lobs_fill(WinArgs a, const int* inv, int n_opt, const int* lptr,
                                                   const double* wuv, int* lkf, int* llm, double2* luv) {
-    const int s = blockIdx.x * kT + threadIdx.x;
+    const int s = (int)((blockIdx.x * (unsigned)kT + threadIdx.x) >> 6), lane = threadIdx.x & 63;
     if (s >= n_opt) return;
     const int l = inv[s];
-    int w = lptr[s], row = 0;
-    for (int64_t o = a.optr[l]; o < a.optr[l + 1]; ++o) {
-        const int f = lobs_feature(a, l, o, row);
-        if (f < 0) continue;
-        lkf[w] = row;
-        llm[w] = s;
-        luv[w] = make_double2(wuv[2 * f], wuv[2 * f + 1]);
-        ++w;
+    const int64_t o0 = a.optr[l], o1 = a.optr[l + 1];
+    int w = lptr[s];
+    for (int64_t base = o0; base < o1; base += 64) {
+        const int64_t o = base + lane;
+        int row = 0, f = -1;
+        if (o < o1) f = lobs_feature(a, l, o, row);
+        const unsigned long long m = __ballot(f >= 0);
+        if (f >= 0) {
+            const int at = w + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            lkf[at] = row;
+            llm[at] = s;
+            luv[at] = make_double2(wuv[2 * f], wuv[2 * f + 1]);
+        }
+        w += __popcll(m);
     }
 }
 
@@ -497,7 +511,7 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
                        in.wuv, p->pobs_uv.as<double2>(), p->pobs_lm.as<int>(), p->kf_obs_ptr.as<int>());
     // landmark-stage CSR over all nl slots (those past n_opt count 0)
     int* cnt = B.cnt.as<int>();
-    hipLaunchKernelGGL(k_lobs_count, dim3(grid(nl)), dim3(kT), 0, s, a, inv, n_opt_dev, nl, cnt);
+    hipLaunchKernelGGL(k_lobs_count, dim3(grid(64ll * std::max(nl, 1))), dim3(kT), 0, s, a, inv, n_opt_dev, nl, cnt);
     VX_LAUNCH_CHECK(c, "plan CSR kernels");
     VX_HIP(c, p->lobs_ptr.ensure((size_t)(nl + 1) * 4));
     if ((rc = scan(c, B.tmp, cnt, p->lobs_ptr.as<int>(), nl))) return rc;
@@ -528,7 +542,7 @@ int build_core(vx_ctx* c, const BuildInputs& in, const std::vector<int>& win, co
     VX_HIP(c, p->lobs_kf.ensure((size_t)std::max(n_lobs, 1) * 4));
     VX_HIP(c, p->lobs_lm.ensure((size_t)std::max(n_lobs, 1) * 4));
     VX_HIP(c, p->lobs_uv.ensure((size_t)std::max(n_lobs, 1) * sizeof(double2)));
-    hipLaunchKernelGGL(k_lobs_fill, dim3(grid(n_opt)), dim3(kT), 0, s, a, inv, n_opt, p->lobs_ptr.as<int>(),
+    hipLaunchKernelGGL(k_lobs_fill, dim3(grid(64ll * n_opt)), dim3(kT), 0, s, a, inv, n_opt, p->lobs_ptr.as<int>(),
                        in.wuv, p->lobs_kf.as<int>(), p->lobs_lm.as<int>(),
                        p->lobs_uv.as<double2>());
     VX_HIP(c, p->lm_pos0.ensure((size_t)std::max(n_lm, 1) * 4 * sizeof(double)));
