@@ -1157,17 +1157,17 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
 // ---- the pass engine
 // Between passes the array lives in memory (LDS, or the level's global scratch).  A pass loads
 // exactly its range into registers, densely (block j = the 64 positions from 64 j, one per lane;
-// NB blocks, a power of two fixed at compile time), partitions it there and stores it back: its
-// instruction count follows the range, so the long tail of short introselect steps stays cheap
-// (a wave issues ~3.5 cycles per instruction here; a pass that paid for a fixed 8-block layout
-// cost ~4000 cycles whatever its range).  Ranges of up to kRgWave run on wave 0 alone: pivot
-// candidates are broadcast loads, the crossing and the cut come from scalar popcounts and one
-// ballot, the mailboxes need no barrier.  Longer ranges (up to RgCap: 8192 u32 / 4096 u64) run as
-// team passes over about four waves (one per SIMD; up to 16 with 8 blocks each): counts, crossing
-// candidates and every L / R with its position go through LDS, three barriers a pass.
+// NB blocks, a power of two fixed at compile time), partitions it there and writes back the
+// elements that moved: its instruction count follows the range, so the long tail of short
+// introselect steps stays cheap.  Ranges of up to kRgWave run on wave 0 alone (pivot candidates
+// are broadcast loads, the crossing and the cut come from ballots and scalar selects, the mailboxes
+// need no barrier); the last steps of a range of <= 64 stay in wave 0's registers (rg_tail64).
+// Longer ranges (up to RgCap: 8192 u32 / 4096 u64) run as team passes spread over kRgSpread waves
+// (16: four per SIMD, up to 8 blocks each): counts, crossing candidates and every L / R of rank
+// below the mailbox bound with its position go through LDS, three barriers a pass.
 // The crossing (per wave, the K of the Hoare formulation above): g(x) = #L in [lo, x) -
 // #R in [x, l) never decreases, K = max(#R from x*, #L before x* - 1) at the first x* with
-// g(x*) >= 0 (K = 0 when there is no R), so only the block holding x* needs per-lane work.
+// g(x*) >= 0 (K = 0 when there is no R), read off the first nonzero per-block ballot of g >= 0.
 template <class T> struct RgCap { static constexpr int v = sizeof(T) == 4 ? 8192 : 4096; };
 constexpr int kRgCap32 = 8192;                 // C4 level 0: ~6.9k FAST candidates
 #ifndef VX_SEL_WAVE
