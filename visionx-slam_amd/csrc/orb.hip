@@ -2064,6 +2064,26 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
     const int W = a.lw[l];
     const int xl = (int)(r.xy & 0xffffu), yl = (int)(r.xy >> 16);
     const uint8_t* img = pyr + a.off[l];
+    const float sc = a.scale[l];
+    const float px = (float)xl * sc, py = (float)yl * sc;
+    const float inv = a.inv_scale[l];
+    const int cx = __float2int_rn(px * inv), cy = __float2int_rn(py * inv);
+    // The blurred patch the rBRIEF tests sample (the pattern's points lie in [-13, 12]^2, so rotated
+    // they stay within +-18 of the centre; keypoints are >= 31 px from the level's edges): rows
+    // cy-18..cy+18 on lanes 0..36, 40 bytes from cx-18 each, loaded as aligned dwords together with
+    // the IC-angle taps below and parked in this wave's LDS — the tests then read LDS instead of
+    // waiting on 512 dependent L2 gathers after the angle.
+    __shared__ unsigned s_patch[kBlock / 64][37 * 10];
+    unsigned* patch = s_patch[threadIdx.x >> 6];
+    unsigned pq[11];
+    unsigned psh = 0;
+    if (lane < 37) {
+        const uintptr_t ad = (uintptr_t)(blur + a.off[l] + (long long)(cy + lane - 18) * W + (cx - 18));
+        const unsigned* al = reinterpret_cast<const unsigned*>(ad & ~(uintptr_t)3);
+        psh = (unsigned)(ad & 3u);
+#pragma unroll
+        for (int j = 0; j < 11; ++j) pq[j] = al[j];
+    }
     // ICAngles (half_k 15): lane v+15 sums row v of the circular patch
     int m10 = 0, m01 = 0;
     if (lane < 31) {
@@ -2084,20 +2104,22 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
         m10 = su;
         m01 = v * s;
     }
+    if (lane < 37) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) patch[lane * 10 + j] = __builtin_amdgcn_alignbyte(pq[j + 1], pq[j], psh);
+    }
     m10 = wave_sum(m10);
     m01 = wave_sum(m01);
     const float angle = ocv_fast_atan2((float)m01, (float)m10);
     // computeOrbDescriptors
-    const float sc = a.scale[l];
-    const float px = (float)xl * sc, py = (float)yl * sc;
-    const float inv = a.inv_scale[l];
-    const int cx = __float2int_rn(px * inv), cy = __float2int_rn(py * inv);
     float ang = angle;
     ang *= (float)(M_PI / 180.f);
     double sd, cd;  // OpenCV: (float)cos((double)angle), (float)sin(...); one shared argument reduction
     sincos((double)ang, &sd, &cd);
     const float ca = (float)cd, sa = (float)sd;
-    const uint8_t* ctr = blur + a.off[l] + (long long)cy * W + cx;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (the patch rows written above, by other lanes)
+    __builtin_amdgcn_wave_barrier();
+    const uint8_t* pb = reinterpret_cast<const uint8_t*>(patch);
     unsigned long long words[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -2109,7 +2131,7 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
             const float qx = (float)c_pattern[2 * pi], qy = (float)c_pattern[2 * pi + 1];
             const float x = qx * ca - qy * sa;
             const float y = qx * sa + qy * ca;
-            v[e] = ctr[(long long)__float2int_rn(y) * W + __float2int_rn(x)];
+            v[e] = pb[(__float2int_rn(y) + 18) * 40 + __float2int_rn(x) + 18];
         }
         words[s] = __ballot(v[0] < v[1]);
     }
