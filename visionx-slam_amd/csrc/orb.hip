@@ -45,6 +45,9 @@ VX_KP_TABLE();
 
 __constant__ signed char c_pattern[1024];
 __constant__ int c_umax[16];
+// ICAngles row masks: row lane (v = lane - 15), byte k of the 32-byte window starting at u = -15
+// is 0xff iff |k - 15| <= umax[|v|] (row 31 empty)
+__constant__ __attribute__((aligned(16))) unsigned c_icmask[32][8];
 
 struct LevelArgs {
     int L;
@@ -2084,25 +2087,32 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
 #pragma unroll
         for (int j = 0; j < 11; ++j) pq[j] = al[j];
     }
-    // ICAngles (half_k 15): lane v+15 sums row v of the circular patch
+    // ICAngles (half_k 15): lane v+15 sums row v of the circular patch — the row's 32-byte window
+    // (u = -15..16) from 9 aligned dwords, bytes outside |u| <= umax[|v|] masked, then
+    // sum p and sum (u + 15) p as byte dot products (integer: exact in any order)
     int m10 = 0, m01 = 0;
     if (lane < 31) {
         const int v = lane - 15;
-        const int d = c_umax[v < 0 ? -v : v];
-        const uint8_t* row = img + (long long)(yl + v) * W + xl;
-        // all 31 taps of the row issued before the first is used (|u| <= d predicated): one
-        // exposed load latency per row instead of one per tap
-        int px[31];
+        const uintptr_t ad = (uintptr_t)(img + (long long)(yl + v) * W + (xl - 15));
+        const unsigned* al = reinterpret_cast<const unsigned*>(ad & ~(uintptr_t)3);
+        const unsigned sh = (unsigned)(ad & 3u);
+        unsigned q[9];
 #pragma unroll
-        for (int u = -15; u <= 15; ++u) px[u + 15] = (u >= -d && u <= d) ? (int)row[u] : 0;
-        int s = 0, su = 0;
+        for (int j = 0; j < 9; ++j) q[j] = al[j];
+        const uint4* mk = reinterpret_cast<const uint4*>(c_icmask[lane]);
+        const uint4 ma = mk[0], mb = mk[1];
+        const unsigned mw[8] = {ma.x, ma.y, ma.z, ma.w, mb.x, mb.y, mb.z, mb.w};
+        unsigned s = 0, sr = 0;
 #pragma unroll
-        for (int u = -15; u <= 15; ++u) {
-            s += px[u + 15];
-            su += u * px[u + 15];
+        for (int j = 0; j < 8; ++j) {
+            const unsigned p = __builtin_amdgcn_alignbyte(q[j + 1], q[j], sh) & mw[j];
+            const unsigned ramp = (unsigned)(4 * j) | (unsigned)(4 * j + 1) << 8 | (unsigned)(4 * j + 2) << 16 |
+                                  (unsigned)(4 * j + 3) << 24;
+            s = __builtin_amdgcn_udot4(p, 0x01010101u, s, false);
+            sr = __builtin_amdgcn_udot4(p, ramp, sr, false);
         }
-        m10 = su;
-        m01 = v * s;
+        m10 = (int)sr - 15 * (int)s;
+        m01 = v * (int)s;
     }
     if (lane < 37) {
 #pragma unroll
@@ -2314,6 +2324,13 @@ int upload_constants(vx_ctx* c) {
         ++v0;
     }
     VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax, sizeof(umax)));
+    unsigned icmask[32][8] = {{0}};
+    for (int r = 0; r < 31; ++r) {
+        const int d = umax[r < 15 ? 15 - r : r - 15];
+        for (int k = 0; k < 32; ++k)
+            if (k - 15 >= -d && k - 15 <= d) icmask[r][k >> 2] |= 0xffu << (8 * (k & 3));
+    }
+    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icmask, sizeof(icmask)));
     if (c->device >= 0 && c->device < 64) g_constants_uploaded[c->device] = true;
     return VX_OK;
 }
