@@ -437,6 +437,33 @@ __device__ __forceinline__ vx_i16x2 win_pair(const uint32_t (&w)[3], int b) {
     return __builtin_bit_cast(vx_i16x2, __builtin_amdgcn_perm(w[lo + 1], w[lo], sel));
 }
 
+// An interior tile (every staged byte inside the level, no clamp / reflection) staged a dword at a
+// time: ROWS rows of 4*DW bytes from src (row pitch W, any byte alignment) into dst, each dword from
+// two aligned loads and one v_alignbyte, all loads of a thread issued before its first LDS store.
+template <int ROWS, int DW>
+__device__ __forceinline__ void stage_dw(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int W) {
+    constexpr int N = ROWS * DW, KM = (N + kBlock - 1) / kBlock;
+    unsigned lo[KM], hi[KM], sh[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        const int i = (int)threadIdx.x + k * kBlock;
+        lo[k] = hi[k] = sh[k] = 0;
+        if (i < N) {
+            const int r = i / DW, c = i - r * DW;
+            const uintptr_t ad = (uintptr_t)(src + (long long)r * W + 4 * c);
+            const unsigned* al = reinterpret_cast<const unsigned*>(ad & ~(uintptr_t)3);
+            sh[k] = (unsigned)(ad & 3u);
+            lo[k] = al[0];
+            hi[k] = al[1];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        const int i = (int)threadIdx.x + k * kBlock;
+        if (i < N) reinterpret_cast<unsigned*>(dst)[i] = __builtin_amdgcn_alignbyte(hi[k], lo[k], sh[k]);
+    }
+}
+
 __device__ __forceinline__ int refl101(int p, int n) {
     if (n == 1) return 0;
     while (p < 0 || p >= n) {
@@ -478,16 +505,23 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     if (tid == 0) s_n = s_nc = 0;
     s_hist[tid] = 0;
     static_assert(kBlock == 256, "one histogram bin per thread");
-    stage_lds<kBlock, (kTH * kTW + kBlock - 1) / kBlock>(tile, kTH * kTW, [&](int i) {
-        const int r = i / kTW, c = i - r * kTW;
-        const int gy = min(max(y0 - 4 + r, 0), H - 1);
-        const int gx = min(max(x0 - 4 + c, 0), W - 1);
-        return img[(long long)gy * W + gx];
-    });
-    stage_lds<kBlock, (kBH * kBW + kBlock - 1) / kBlock>(bin_, kBH * kBW, [&](int i) {
-        const int r = i / kBW, c = i - r * kBW;
-        return img[(long long)refl101(y0 - 3 + r, H) * W + refl101(x0 - 4 + c, W)];
-    });
+    // (interior tiles: the aligned dword reads of the last column reach 3 bytes past the staged row)
+    if (x0 >= 4 && x0 + kTW <= W && y0 >= 4 && y0 - 4 + kTH <= H)
+        stage_dw<kTH, kTW / 4>(tile, img + (long long)(y0 - 4) * W + (x0 - 4), W);
+    else
+        stage_lds<kBlock, (kTH * kTW + kBlock - 1) / kBlock>(tile, kTH * kTW, [&](int i) {
+            const int r = i / kTW, c = i - r * kTW;
+            const int gy = min(max(y0 - 4 + r, 0), H - 1);
+            const int gx = min(max(x0 - 4 + c, 0), W - 1);
+            return img[(long long)gy * W + gx];
+        });
+    if (x0 >= 4 && x0 + kBW <= W && y0 >= 3 && y0 - 3 + kBH <= H)
+        stage_dw<kBH, kBW / 4>(bin_, img + (long long)(y0 - 3) * W + (x0 - 4), W);
+    else
+        stage_lds<kBlock, (kBH * kBW + kBlock - 1) / kBlock>(bin_, kBH * kBW, [&](int i) {
+            const int r = i / kBW, c = i - r * kBW;
+            return img[(long long)refl101(y0 - 3 + r, H) * W + refl101(x0 - 4 + c, W)];
+        });
     __syncthreads();
     VX_KT(5);
     const int thr = a.fast_threshold;
