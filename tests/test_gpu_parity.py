@@ -128,6 +128,36 @@ def test_orb_invalid_arguments(ctx):
     assert e.value.code == vxslam.VX_ERR_CAPACITY
 
 
+def test_orb_min_edge_threshold(ctx):
+    """edge_threshold 19 (the smallest the descriptor footprint allows: k_describe's aligned row
+    loads reach up to 21 px left / 26 px right of a keypoint): the run is memory-safe, keeps
+    keypoints closer to the border than the default 31, and every keypoint both runs keep (same
+    octave and position) has the same response, angle and descriptor — those depend only on the
+    image around it.  (The oracle restates the reference's fixed ORB defaults, edge 31.)"""
+    import vxslam
+
+    for seed, h, w, n in ((41, 480, 640, 2000), (42, 333, 517, 1500)):
+        img = synth.make_frames(seed, 1, h, w)[0]
+        k19, d19 = ctx.orb_extract(img, vxslam.default_orb_params(n_features=n, edge_threshold=19))
+        k31, d31 = ctx.orb_extract(img, vxslam.default_orb_params(n_features=n, edge_threshold=31))
+        scale = 1.2 ** k19["octave"].astype(np.float64)
+        xl, yl = k19["x"] / scale, k19["y"] / scale
+        lw = np.round(w / scale)
+        lh = np.round(h / scale)
+        near = (xl < 30.5) | (yl < 30.5) | (xl > lw - 31.5) | (yl > lh - 31.5)
+        assert near.any()
+        at = {(int(k["octave"]), float(k["x"]), float(k["y"])): i for i, k in enumerate(k31)}
+        common = 0
+        for i, k in enumerate(k19):
+            j = at.get((int(k["octave"]), float(k["x"]), float(k["y"])))
+            if j is None:
+                continue
+            common += 1
+            assert k["response"] == k31[j]["response"] and k["angle"] == k31[j]["angle"], (i, j)
+            assert np.array_equal(d19[i], d31[j]), (i, j)
+        assert common > len(k31) // 2, (common, len(k31))
+
+
 # ---------------------------------------------------------------------------- matching
 def test_match_golden_gpu(ctx):
     g = np.load(os.path.join(HERE, "golden", "match_golden.npz"))
