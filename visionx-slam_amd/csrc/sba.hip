@@ -1020,6 +1020,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
             feat_l[(size_t)(fbase[r] + i)] = l;
         }
     }
+    lap("obs lookups");
     for (int r = 0; r < nk; ++r) {
         if (!(flags[r] & 1)) continue;
         const int64_t f0 = m->kf_feat_ptr[win[r]];
@@ -1035,6 +1036,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
         }
     }
     p->n_lm = (int)p->lm_map_idx.size();
+    lap("obs slots");
     // pass 2: stable counting sort into landmark-major order for the optimised slots (keyframe
     // order within a landmark), then the fixed landmarks' observations in keyframe-major order
     std::vector<int> lptr(n_opt + 1, 0);
@@ -1061,6 +1063,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     }
     p->n_oo = n_oo;
     p->n_obs = (int)okf.size();
+    lap("obs sort");
     std::vector<double> lm0((size_t)std::max(p->n_lm, 1) * 4, 0.0);
     for (int s = 0; s < p->n_lm; ++s)
         for (int j = 0; j < 3; ++j) lm0[4 * s + j] = m->lm_pos[3 * p->lm_map_idx[s] + j];
