@@ -486,7 +486,13 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
     __shared__ int s_hist[256];               // this tile's NMS corners by FAST score
     __shared__ __attribute__((aligned(16))) uint8_t bin_[kBH * kBW];
     __shared__ __attribute__((aligned(16))) float brow[kBH * kTX];
-    const int b = blockIdx.x;
+    // Tiles XCD by XCD (block x runs on XCD x mod 8): XCD i takes the i-th contiguous run of the
+    // (level, raster) tile order, so a tile's vertical and horizontal neighbours — which stage the
+    // same halo rows and columns — mostly share its L2 instead of fetching them again from HBM.
+    const int b = [] {
+        const int nb = (int)gridDim.x, xcd = (int)(blockIdx.x & 7u), qb = nb >> 3, rem = nb & 7;
+        return xcd * qb + min(xcd, rem) + (int)(blockIdx.x >> 3);
+    }();
     pyr += blockIdx.z * a.fs_pyr;
     blur += blockIdx.z * a.fs_pyr;
     cand += blockIdx.z * a.fs_cells * kCellCap;
