@@ -163,8 +163,19 @@ __global__ __launch_bounds__(NT) void k_pyramid(const uint8_t* __restrict__ img,
     VX_KT(0);
     if (blockIdx.x == 0 && blockIdx.y == 0)
         for (int i = tid; i < hist_n; i += NT) hist[i] = 0;
-    if (tid < L) srx[tid] = tabs[a.pr_x + (long long)blockIdx.x * L + tid];
-    if (tid >= 64 && tid < 64 + L) sry[tid - 64] = tabs[a.pr_y + (long long)blockIdx.y * L + tid - 64];
+    // tiles XCD by XCD (workgroup i of the dispatch runs on XCD i mod 8): XCD k takes the k-th
+    // contiguous run of the raster tile order, so neighbouring tiles' overlapping need rectangles
+    // meet in one L2 (the k_fast mapping)
+    int bx, by;
+    {
+        const int nb = (int)(gridDim.x * gridDim.y), lin = (int)(blockIdx.x + blockIdx.y * gridDim.x);
+        const int xcd = lin & 7, qb = nb >> 3, rem = nb & 7;
+        const int t = xcd * qb + min(xcd, rem) + (lin >> 3);
+        by = t / (int)gridDim.x;
+        bx = t - by * (int)gridDim.x;
+    }
+    if (tid < L) srx[tid] = tabs[a.pr_x + (long long)bx * L + tid];
+    if (tid >= 64 && tid < 64 + L) sry[tid - 64] = tabs[a.pr_y + (long long)by * L + tid - 64];
     __syncthreads();
     if (tid == 0) {
         int o = 0;
