@@ -422,6 +422,12 @@ __device__ __forceinline__ int block_scan_excl(int v, int* sh, int& total) {
 // instructions per wave).  cornerScore<16> runs only for the compacted corner list (3-7 % of the
 // pixels), not under a divergent branch that nearly every wave takes.
 constexpr int kTX = 64, kTY = 16, kCellCap = 32;
+// Candidate records are stored slot-major within a frame: slot i of cell c at i * fs_cells + c.
+// Most cells hold 0-2 records, so the selection's gather (consecutive cells per thread, slot 0
+// first) reads whole cache lines of records instead of one line per record.
+__device__ __forceinline__ long long cand_at(long long cell, int i, long long fs_cells) {
+    return (long long)i * fs_cells + cell;
+}
 constexpr int kTW = kTX + 12, kTH = kTY + 8;  // staged tile: x0-4 .. x0+71 (quad reads up to x0+71)
 constexpr int kSW = kTX + 4, kSH = kTY + 2;   // score tile (66 used + 2 pad: dword rows)
 constexpr int kSQ = 17;                       // score quads per row (68 columns)
@@ -716,7 +722,7 @@ __global__ __launch_bounds__(kBlock) void k_fast(const uint8_t* __restrict__ pyr
             c.score = sco;
             c.harris = (fa * fb - fc * fc - 0.04f * (fa + fb) * (fa + fb)) * s4;
             c.pad = 0;
-            cand[(long long)(a.cell_base[l] + (y0 + r) * ntx + tx) * kCellCap + rank] = c;
+            cand[cand_at(a.cell_base[l] + (y0 + r) * ntx + tx, rank, a.fs_cells)] = c;
             atomicAdd(&s_hist[sco], 1);
         }
     }
@@ -806,7 +812,7 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
                 i -= cn[jj];
                 j = jj + 1;
             }
-        return (cbase + c0 + j) * kCellCap + i;
+        return cand_at(cbase + c0 + j, i, a.fs_cells);
     };
     CandRec rr0[kRecBatch];
 #pragma unroll
@@ -1889,7 +1895,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
                     i -= cnts[jj];
                     j = jj + 1;
                 }
-            return (cbase + c0 + j) * kCellCap + i;
+            return cand_at(cbase + c0 + j, i, a.fs_cells);
         };
         CandRec rr[kRecBatch];
 #pragma unroll
