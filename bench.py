@@ -52,6 +52,47 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+# LocalBA::Options as the reference runner names them (apps/main.cpp:42-47 -> tracking options)
+BA_FLAGS = {"ba_window_size": int, "ba_iterations": int, "ba_min_pose_observations": int,
+            "ba_min_point_observations": int, "ba_huber_delta": float, "ba_max_reproj_error": float}
+
+
+def load_config_file(path):
+    """apps/main.cpp LoadConfig: key=value lines, '#' comments, surrounding whitespace trimmed; the
+    reference warns about keys it does not know — here everything but the ba_* keys is outside the
+    measured path and ignored with a note."""
+    kv = {}
+    with open(path) as f:
+        for line in f:
+            line = line.split("#", 1)[0].strip()
+            if not line or "=" not in line:
+                continue
+            k, v = (x.strip() for x in line.split("=", 1))
+            kv[k] = v
+    return kv
+
+
+def resolve_ba_flags(args, window_default):
+    """The LocalBA options of this run: command-line flags over the config file's ba_* keys over the
+    workload's defaults (window = the configuration's keyframes; the rest the reference defaults,
+    default.cfg)."""
+    vals = {"ba_window_size": window_default, "ba_iterations": 5, "ba_min_pose_observations": 20,
+            "ba_min_point_observations": 2, "ba_huber_delta": 5.0, "ba_max_reproj_error": 5.0}
+    if getattr(args, "config_file", None):
+        kv = load_config_file(args.config_file)
+        for k, typ in BA_FLAGS.items():
+            if k in kv:
+                vals[k] = typ(kv[k])
+        other = sorted(k for k in kv if k not in BA_FLAGS)
+        if other:
+            log(f"note: config keys outside the measured path ignored: {', '.join(other)}")
+    for k in BA_FLAGS:
+        v = getattr(args, k, None)
+        if v is not None:
+            vals[k] = v
+    return vals
+
+
 # ----------------------------------------------------------------------------- algorithmic bytes
 def stage_bytes(stage, geo, counts):
     """Algorithmic (compulsory) HBM bytes of ONE launch of a stage.  Formulas: DESIGN.md §4."""
@@ -261,6 +302,40 @@ def parity_vs_unsharded(shards, ref, tol=1e-4):
     return out
 
 
+def measured_candidates(vxslam, frame, params):
+    """FAST candidates kept after runByImageBorder over all levels of `frame` (what k_fast writes and
+    k_select reads, 16 B each): one extraction on a scratch context with the stage hooks on."""
+    ctx = vxslam.Context(int(os.environ.get("LOCAL_RANK", "0")))
+    try:
+        ctx.set_debug(vxslam.DEBUG_STAGES)
+        ctx.orb_extract(frame, params)
+        return int(sum(len(ctx.debug_read(lv, 2)) for lv in range(params.n_levels)))
+    finally:
+        ctx.close()
+
+
+def replay_equals_eager(a, b):
+    """Two runs of one sharded plan (eager and graph replay) must agree bitwise."""
+    return (a["iterations"] == b["iterations"] and a["obs"] == b["obs"] and np.array_equal(a["pose"], b["pose"])
+            and np.array_equal(a["lm_idx"], b["lm_idx"]) and np.array_equal(a["lm_pos"], b["lm_pos"]))
+
+
+def sharded_parity_gate(parity, dist, args):
+    """N > 1: a sharded LocalBA that disagrees with the unsharded run makes the whole measurement
+    invalid.  Rank 0's verdict is shared with every rank; on failure rank 0 prints a JSON line whose
+    metric says INVALID (value null) and every rank exits with status 3."""
+    ok = bool(parity and parity.get("ok"))
+    ok = dist.broadcast_bytes(b"1" if ok else b"0") == b"1"
+    if ok:
+        return True
+    if dist.rank == 0:
+        print(json.dumps({"metric": "INVALID: sharded LocalBA differs from the unsharded run", "value": None,
+                          "unit": "ms/frame", "n_gpus": dist.world, "steps": args.steps, "warmup": args.warmup,
+                          "higher_is_better": False, "parity_vs_unsharded": parity}), flush=True)
+    dist.close()
+    raise SystemExit(3)
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def host_cpu():
     """The host CPU model and the cores this process may use (record the host)."""
@@ -373,7 +448,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--config", default="C3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="C3",
+                    help="workload C2 / C3 / C4, or a key=value file with the reference's flag names "
+                         "(apps/main.cpp --config; its ba_* keys set the LocalBA options below)")
+    # the reference runner's LocalBA flags (apps/main.cpp:42-47, config/default.cfg), same names;
+    # unset: the workload's values (window = the config's keyframes, the reference defaults otherwise)
+    for k, typ in BA_FLAGS.items():
+        ap.add_argument(f"--{k}", type=typ, default=None)
     ap.add_argument("--frames", type=int, default=8, help="distinct frames cycled through")
     ap.add_argument("--cpu-sample", type=int, default=30, help="frames timed for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -402,6 +483,11 @@ def main():
                          "(default: one hardware queue fewer; measured 0.073 vs 0.073-0.076 ms/frame, steadier) "
                          "or on a context of its own")
     args = ap.parse_args()
+    args.config_file = None
+    if args.config not in CONFIGS:
+        if not os.path.isfile(args.config):
+            ap.error(f"--config: neither a workload ({', '.join(sorted(CONFIGS))}) nor a file: {args.config}")
+        args.config_file, args.config = args.config, "C3"
 
     dist = Dist(args.gpus)
     import torch
@@ -443,20 +529,39 @@ def main():
     frames_dev = torch.from_numpy(frames_host).cuda()
     params = vxslam.default_orb_params(n_features=nf)
     ba_map = synth.make_ba_map(0x5EED0003, nk * N, nl * N, n_streams=N, n_old_kf=2 * N)
-    opts = vxslam.default_ba_options(window=nk * N)
+    ba_flags = resolve_ba_flags(args, nk * N)
+    opts = vxslam.default_ba_options(window=ba_flags["ba_window_size"], iters=ba_flags["ba_iterations"],
+                                     min_pose=ba_flags["ba_min_pose_observations"],
+                                     min_point=ba_flags["ba_min_point_observations"],
+                                     huber=ba_flags["ba_huber_delta"], max_err=ba_flags["ba_max_reproj_error"])
+    rccl = None
     if N > 1:
         uid = dist.broadcast_bytes(vxslam.Context.comm_unique_id() if dist.rank == 0 else None)
         bctx.comm_init(uid, N, dist.rank)
+        # what RCCL itself reports must be this launch's world (a communicator of the wrong size would
+        # all-reduce a different set of shards)
+        nr, rk = bctx.comm_info()
+        infos = dist.gather((nr, rk))
+        rccl = {"nranks": nr, "world_size": N, "ranks": [list(x) for x in infos] if infos else None}
+        if nr != N or rk != dist.rank:
+            raise SystemExit(f"rank {dist.rank}: RCCL communicator reports {nr} ranks / rank {rk}, "
+                             f"WORLD_SIZE {N} / RANK {dist.rank}")
     plan = bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N)
     info = plan.info()
     # N > 1: the sharded run checked against the unsharded run of the same global window (rank 0
     # runs it on its own GPU) before anything is timed
     parity = None
     if N > 1:
-        m_s = ba_map.copy()
-        plan.run_async()
-        st_s = plan.fetch(m_s)
-        mine = shard_result(m_s, vxslam.ba_plan_inspect(ba_map, opts, shard_rank=dist.rank, shard_count=N), st_s)
+        # runs 1, 2, 3 of the sharded plan: eager, graph capture, graph replay (include/vx_slam.h);
+        # every timed run replays the captured graph, so the replay is checked as well as the eager run
+        insp = vxslam.ba_plan_inspect(ba_map, opts, shard_rank=dist.rank, shard_count=N)
+        mine = []
+        for r in range(3):
+            m_s = ba_map.copy()
+            plan.run_async()
+            st_s = plan.fetch(m_s)
+            if r in (0, 2):
+                mine.append(shard_result(m_s, insp, st_s))
         shards = dist.gather(mine)
         if dist.rank == 0:
             m_u = ba_map.copy()
@@ -464,8 +569,13 @@ def main():
             pu.run_async()
             st_u = pu.fetch(m_u)
             pu.close()
-            parity = parity_vs_unsharded(shards, shard_result(m_u, vxslam.ba_plan_inspect(ba_map, opts), st_u))
+            ref = shard_result(m_u, vxslam.ba_plan_inspect(ba_map, opts), st_u)
+            parity = parity_vs_unsharded([s[1] for s in shards], ref)
+            parity["eager"] = parity_vs_unsharded([s[0] for s in shards], ref)["ok"]
+            parity["replay_equals_eager"] = all(replay_equals_eager(s[0], s[1]) for s in shards)
+            parity["ok"] = bool(parity["ok"] and parity["eager"] and parity["replay_equals_eager"])
             log(f"[bench] sharded vs unsharded LocalBA: {parity}")
+        sharded_parity_gate(parity, dist, args)
     # what a drop-in LocalBA::Optimize() adds per call on top of the solve: the window / CSR
     # build from the map snapshot (device build), reported beside `value`
     plan_ms = []
@@ -640,7 +750,8 @@ def main():
     lw = [int(round(w / 1.2 ** l)) for l in range(8)]
     lh = [int(round(h / 1.2 ** l)) for l in range(8)]
     geo = {"W": w, "H": h, "level_px": [a * b for a, b in zip(lw, lh)]}
-    counts = {"n_kp": len(kps), "n_cand": 4 * nf, "n_q": len(kps), "n_t": len(kps),
+    counts = {"n_kp": len(kps), "n_cand": measured_candidates(vxslam, frames_host[last % args.frames], params),
+              "n_q": len(kps), "n_t": len(kps),
               "n_match": len(matches), "n_pose_obs": info["n_pose_obs"], "n_lm_obs": info["n_lm_obs"],
               "n_split": info["n_split"], "n_opt": info["n_opt"], "n_kf": info["n_kf"]}
 
@@ -713,6 +824,10 @@ def main():
                 "ba_window_kf": nk * N,
                 "ba_landmarks": nl * N,
                 "orb_features": nf,
+                # LocalBA::Options of this run under the reference runner's flag names
+                # (apps/main.cpp:42-47; --config FILE / --ba_* flags)
+                "ba_options": ba_flags,
+                "config_file": args.config_file,
             },
             # one frame alone through the same dependency chain (host enqueue to completion, median
             # of 20): the per-frame latency; `value` is the pipelined throughput
@@ -733,6 +848,8 @@ def main():
             # N > 1: the sharded LocalBA against the unsharded run of the same window (ok = within
             # 1e-4, no gate flips, same iterations, ranks bitwise agreed); null at N = 1
             "parity_vs_unsharded": parity,
+            # N > 1: the communicator's size and rank as RCCL reports them (checked against the launch)
+            "rccl": rccl,
             # what one step computed (the BA iteration count actually executed is
             # reported): LocalBA iterations and their valid pose-stage observations, the last frame's
             # keypoints and matches

@@ -540,6 +540,9 @@ int vx_essential_ransac_batch(vx_ctx* ctx, int n_problems, const int32_t* offset
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);
 int vx_comm_init(vx_ctx* ctx, const uint8_t* id_128, int nranks, int rank);
+/* What RCCL itself reports for the context's communicator (ncclCommCount / ncclCommUserRank), so a
+ * multi-GPU run can check it against WORLD_SIZE / RANK.  VX_ERR_STATE without a communicator. */
+int vx_comm_info(vx_ctx* ctx, int* nranks, int* rank);
 
 /* ---------------------------------------------------------------- profiling
  * When enabled, the library brackets its kernels with hipEvents on its own stream; read back

@@ -78,3 +78,28 @@ def test_cpu_baseline_mt_small():
     m = synth.make_ba_map(7, nk, nl)
     d = bench.cpu_baseline_mt((h, w, nf, nk, nl), frames, m, 2)
     assert d["value"] > 0 and d["cores"] >= 1 and d["unit"] == "ms/frame" and d["kind"] == "port"
+
+
+def test_ba_flags_reference_names(tmp_path):
+    """bench.py takes the reference runner's LocalBA flags (apps/main.cpp:42-47) on the command line
+    and from a key=value --config file (the reference's LoadConfig format, default.cfg's keys);
+    command-line flags win over the file, the file over the workload's defaults."""
+    sys.path.insert(0, ROOT)
+    import argparse
+
+    import bench
+
+    cfg = tmp_path / "run.cfg"
+    cfg.write_text("# Local BA\nenable_local_ba=false\nba_window_size=7\n ba_iterations = 3 \n"
+                   "ba_huber_delta=2.5\nsequence=rgbd_dataset_freiburg1_desk\n")
+    ns = argparse.Namespace(config_file=str(cfg), **{k: None for k in bench.BA_FLAGS})
+    ns.ba_iterations = 4
+    v = bench.resolve_ba_flags(ns, 50)
+    assert v == {"ba_window_size": 7, "ba_iterations": 4, "ba_min_pose_observations": 20,
+                 "ba_min_point_observations": 2, "ba_huber_delta": 2.5, "ba_max_reproj_error": 5.0}
+    ns = argparse.Namespace(config_file=None, **{k: None for k in bench.BA_FLAGS})
+    assert bench.resolve_ba_flags(ns, 50)["ba_window_size"] == 50
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--help"], capture_output=True, text=True,
+                       timeout=120)
+    for k in bench.BA_FLAGS:
+        assert f"--{k}" in r.stdout

@@ -181,3 +181,36 @@ def _parity_worker(rank, world, port):
 
 def test_bench_sharded_parity_field():
     _spawn(_parity_worker)
+
+
+def _gate_worker(rank, world, port):
+    """bench.py's N > 1 parity gate: a passing verdict lets every rank through; a failing one (rank 0's
+    verdict, broadcast) makes rank 0 print an INVALID JSON line and every rank exit with status 3."""
+    import contextlib
+    import io
+    import json
+    import types
+
+    _init(rank, world, port)
+    import bench
+
+    d = bench.Dist(world)
+    args = types.SimpleNamespace(steps=5, warmup=2)
+    assert bench.sharded_parity_gate({"ok": True} if rank == 0 else None, d, args) is True
+    out = io.StringIO()
+    with contextlib.redirect_stdout(out):
+        try:
+            bench.sharded_parity_gate({"ok": False, "gate_flips": 1} if rank == 0 else None, d, args)
+            raise AssertionError("a failing sharded parity must stop the run")
+        except SystemExit as e:
+            assert e.code == 3
+    if rank == 0:
+        line = json.loads(out.getvalue().strip())
+        assert line["metric"].startswith("INVALID") and line["value"] is None
+        assert line["parity_vs_unsharded"]["gate_flips"] == 1 and line["n_gpus"] == world
+    else:
+        assert out.getvalue() == ""
+
+
+def test_bench_parity_gate_failing_branch():
+    _spawn(_gate_worker)

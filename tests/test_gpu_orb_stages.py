@@ -119,5 +119,13 @@ def test_debug_hook_guards(ctx):
             c.debug_read(0, 3)  # selection stages need the debug flag
         with pytest.raises(vxslam.VxError):
             c.set_debug(8)
+        # the stage buffers are shared with the other slots and the batches: after a batch (or an
+        # extraction into another slot) they no longer hold slot 0's frame, so the hook refuses
+        fr = synth.make_frames(4, 2, 120, 160)
+        c.orb_extract_batch(np.stack(fr), vxslam.default_orb_params(n_features=200))
+        with pytest.raises(vxslam.VxError):
+            c.debug_read(0, 0)
+        c.orb_extract(fr[0], vxslam.default_orb_params(n_features=200))
+        assert len(c.debug_read(0, 0)) == 120 * 160
     finally:
         c.close()

@@ -2129,8 +2129,12 @@ __global__ __launch_bounds__(kBlock) void k_describe(const uint8_t* __restrict__
     const float inv = a.inv_scale[l];
     const int cx = __float2int_rn(px * inv), cy = __float2int_rn(py * inv);
     // The blurred patch the rBRIEF tests sample (the pattern's points lie in [-13, 12]^2, so rotated
-    // they stay within +-18 of the centre; keypoints are >= 31 px from the level's edges): rows
-    // cy-18..cy+18 on lanes 0..36, 40 bytes from cx-18 each, loaded as aligned dwords together with
+    // they stay within +-18 of the centre): rows cy-18..cy+18 on lanes 0..36, 40 bytes from cx-18
+    // each.  Keypoints lie >= edge_threshold px from the level's edges and validate_params requires
+    // edge_threshold >= 19, so every row is inside the level; the 11 aligned dwords of a row reach
+    // from (cx-18) & ~3 >= cx-21 to cx+25, i.e. at most 2 bytes before the row's first pixel and 6
+    // past its last — neighbouring rows of the same level buffer, whose bytes v_alignbyte drops
+    // (tests/test_gpu_parity.py::test_orb_min_edge_threshold).  They are loaded together with
     // the IC-angle taps below and parked in this wave's LDS — the tests then read LDS instead of
     // waiting on 512 dependent L2 gathers after the angle.
     __shared__ unsigned s_patch[kBlock / 64][37 * 10];
@@ -2388,6 +2392,12 @@ int upload_constants(vx_ctx* c) {
             if (k - 15 >= -d && k - 15 <= d) icmask[r][k >> 2] |= 0xffu << (8 * (k & 3));
     }
     VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icmask, sizeof(icmask)));
+    // the selection kernels' 160 KB of dynamic LDS, per device (set with the device current; a failure
+    // is reported every time, since the device is only marked done after it succeeded: ADVICE r3)
+    VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_stl), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kStlLds));
+    VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_test_retain),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kStlLds));
     if (c->device >= 0 && c->device < 64) g_constants_uploaded[c->device] = true;
     return VX_OK;
 }
@@ -2606,9 +2616,6 @@ static int orb_enqueue_frames(vx_ctx* c, const uint8_t* d_img, int channels, int
     VX_HIP(c, launch(c, kStFast, k_fast, dim3(g.total_tiles, 1, nf), dim3(kBlock), 0, c->stream, (const uint8_t*)pyr, a,
                      c->cand.as<CandRec>(), c->band_count.as<int>(), c->hist.as<int>(), c->blur.as<uint8_t>()));
     if (c->kp_order == VX_ORDER_STL) {
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_stl),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kStlLds);
-        VX_HIP(c, attr);
         VX_HIP(c, launch(c, kStSelect, k_select_stl, dim3(g.L, 1, nf), dim3(kStlNT), (uint32_t)kStlLds, c->stream,
                          (const CandRec*)c->cand.as<CandRec>(), (const int*)c->band_count.as<int>(), a,
                          c->stage.as<CandRec>(), c->level_count.as<int>(), dbg));
@@ -2722,8 +2729,10 @@ int vx_orb_set_debug(vx_ctx* c, int flags) {
 int vx_orb_debug_read(vx_ctx* c, int level, int what, void* out, int64_t cap_bytes, int64_t* n_out) {
     if (!c || !n_out) return VX_ERR_INVALID;
     *n_out = 0;
-    if (!c->geo_valid || !c->slots[0].valid)
-        return set_error(c, VX_ERR_STATE, "no single-frame extraction to inspect");
+    // the scratch (pyramid, blur, candidates, stages) is shared by every slot and the batches: it
+    // must still hold slot 0's single-frame extraction
+    if (!c->geo_valid || !c->slots[0].valid || c->scratch_slot != 0)
+        return set_error(c, VX_ERR_STATE, "no single-frame extraction into slot 0 is the last one to inspect");
     const OrbGeometry& g = c->geo;
     if (level < 0 || level >= g.L) return set_error(c, VX_ERR_INVALID, "bad level %d", level);
     if (what >= 2 && (!c->orb_debug || c->kp_order != VX_ORDER_STL))
@@ -2780,10 +2789,8 @@ int vx_test_retain_best(vx_ctx* c, const uint32_t* keys, int n, int npts, int wi
         hipMalloc(&dout, 4 * ((int64_t)n + 1)) != hipSuccess) {
         rc = set_error(c, VX_ERR_HIP, "hipMalloc failed");
     } else {
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_test_retain),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, kStlLds);
-        (void)attr;
-        hipError_t e = hipMemcpyAsync(dk, keys, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
+        hipError_t e = upload_constants(c) == VX_OK ? hipSuccess : hipErrorUnknown;  // (k_test_retain's LDS size)
+        if (e == hipSuccess) e = hipMemcpyAsync(dk, keys, 4 * (size_t)n, hipMemcpyHostToDevice, c->stream);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_test_retain, dim3(1), dim3(kStlNT), kStlLds, c->stream,
                                (const unsigned*)dk, n, npts, wide, use_lds, (unsigned char*)ds, (int*)dout);
@@ -2824,12 +2831,14 @@ int vx_orb_extract_async(vx_ctx* c, const vx_orb_params* p, const uint8_t* d_img
         int64_t stride;
         int slot;
     } a{d_img, channels, stride, slot};
-    return graph_run(c, {1, (uint64_t)(uintptr_t)d_img, (uint64_t)channels, (uint64_t)stride, (uint64_t)slot, c->geo_gen},
-                     [](vx_ctx* cc, void* v) {
-                         const A* x = static_cast<const A*>(v);
-                         return orb_enqueue(cc, x->img, x->channels, x->stride, x->slot);
-                     },
-                     &a);
+    rc = graph_run(c, {1, (uint64_t)(uintptr_t)d_img, (uint64_t)channels, (uint64_t)stride, (uint64_t)slot, c->geo_gen},
+                   [](vx_ctx* cc, void* v) {
+                       const A* x = static_cast<const A*>(v);
+                       return orb_enqueue(cc, x->img, x->channels, x->stride, x->slot);
+                   },
+                   &a);
+    c->scratch_slot = rc ? -1 : slot;  // (a graph replay writes the scratch too: set here, not in orb_enqueue)
+    return rc;
 }
 
 int vx_orb_fetch(vx_ctx* c, int slot, vx_keypoint* out_kp, uint8_t* out_desc, int cap, int* n_out) {
@@ -2898,6 +2907,7 @@ int vx_orb_extract_batch_async(vx_ctx* c, const vx_orb_params* p, const uint8_t*
                                                  x->s->count.as<int>());
                    },
                    &a);
+    c->scratch_slot = -1;  // the batch overwrote the shared scratch
     if (rc) return rc;
     c->batch_n[bank] = n_frames;
     return VX_OK;

@@ -378,4 +378,17 @@ int vx_comm_init(vx_ctx* c, const uint8_t* id128, int nranks, int rank) {
 #endif
 }
 
+int vx_comm_info(vx_ctx* c, int* nranks, int* rank) {
+    if (!c || !nranks || !rank) return VX_ERR_INVALID;
+#ifndef VX_NO_RCCL
+    if (!c->comm) return vx::set_error(c, VX_ERR_STATE, "vx_comm_info: no communicator (vx_comm_init)");
+    ncclResult_t r = ncclCommCount(c->comm, nranks);
+    if (r == ncclSuccess) r = ncclCommUserRank(c->comm, rank);
+    if (r != ncclSuccess) return vx::set_error(c, VX_ERR_COMM, "ncclCommCount/UserRank: %s", ncclGetErrorString(r));
+    return VX_OK;
+#else
+    return VX_ERR_COMM;
+#endif
+}
+
 }  // extern "C"

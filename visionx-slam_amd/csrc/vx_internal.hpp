@@ -180,6 +180,8 @@ struct vx_ctx {
     bool geo_valid = false;
     int kp_order = VX_ORDER_STL;  // vx_orb_set_order: keypoint order inside a level
     int orb_debug = 0;            // vx_orb_set_debug flags (test hooks)
+    int scratch_slot = -1;        // slot whose single-frame extraction last wrote the shared ORB scratch
+                                  // (pyramid, blur, candidates, stages); -1 after a batch
     vx::DevBuf orb_dbg;           // their device record (k_select_stl)
     vx::DevBuf img_in, pyr, blur, tabs, cand, band_count, hist, stage, level_count;
     vx::Slot slots[VX_MAX_SLOTS];

@@ -83,7 +83,7 @@ EXPORTS = [
     "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
     "vx_match_device_async", "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
     "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info", "vx_ba_plan_layout", "vx_ba_plan_fused_tables",
-    "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
+    "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_comm_info", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
     "vx_sba_optimize_map", "vx_depth_landmarks", "vx_triangulate", "vx_graph_enable", "vx_graph_counts", "vx_create_ex", "vx_device_cus", "vx_ba_plan_create_ex",
@@ -646,6 +646,12 @@ class Context:
     def comm_init(self, uid: bytes, nranks: int, rank: int):
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._check(lib().vx_comm_init(self._h, buf, nranks, rank))
+
+    def comm_info(self):
+        """(nranks, rank) as RCCL reports them for this context's communicator (vx_comm_info)."""
+        n, r = C.c_int(0), C.c_int(0)
+        self._check(lib().vx_comm_info(self._h, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
     # ---------------------------------------------------------------- profiling
     def prof_enable(self, on=True, stages=None):
