@@ -171,11 +171,51 @@ def per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam):
         bctx.synchronize()
         p.close()
 
+    def one_call():
+        dm.optimize(opts)
+
     try:
-        return {"snapshot": med(snap), "resident": med(resident),
-                "note": "plan + solve + apply; value excludes the plan build (a resident plan is replayed per frame)"}
+        out = {"snapshot": med(snap), "resident": med(resident), "resident_one_call": med(one_call)}
     finally:
         dm.close()
+    out["cpp_adapter"] = cpp_adapter_ms(ba_map, opts)
+    out["note"] = ("host wall clock of one LocalBA::Optimize, median of 7: snapshot = plan from the map snapshot "
+                   "(upload, device build) + run + download; resident = vx_ba_plan_create_dmap + run + "
+                   "vx_ba_plan_apply_dmap; resident_one_call = vx_ba_optimize_dmap (ba_lean.hip: build, run and "
+                   "scatter with no host synchronisation before the end); cpp_adapter = visionx::LocalBA::Optimize "
+                   "through tests/cpp/adapter_driver (median of 20 calls, results written back into the C++ "
+                   "Frame / Landmark objects) with a DeviceMap attached and on the snapshot (Flatten) path. "
+                   "value excludes all of these (a resident plan is replayed per frame)")
+    return out
+
+
+def cpp_adapter_ms(ba_map, opts, reps=20):
+    """visionx::LocalBA::Optimize through the C++ drop-in (tests/cpp/adapter_driver ba_calls) on this
+    window: median ms of one call after the first, resident (DeviceMap) and snapshot (Flatten)."""
+    import subprocess
+    import tempfile
+
+    drv = os.path.join(ROOT, "visionx-slam_amd", "build", "adapter_driver")
+    if not os.path.exists(drv):
+        return None
+    keys = ["kf_id", "kf_pose", "kf_intr", "kf_has_cam", "kf_feat_ptr", "feat_uv", "feat_lm_id", "feat_flags",
+            "lm_id", "lm_pos", "lm_bad", "lm_obs_ptr", "obs_kf_id", "obs_feat_idx"]
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        for k in keys:
+            np.ascontiguousarray(ba_map[k]).tofile(os.path.join(d, k + ".bin"))
+        env = dict(os.environ, VX_DEVICE=os.environ.get("LOCAL_RANK", "0"))
+        for mode in ("resident", "snapshot"):
+            r = subprocess.run([drv, "ba_calls", d, str(opts.window_size), str(opts.max_iterations), "-1", str(reps),
+                                mode], capture_output=True, text=True, timeout=300, env=env)
+            if r.returncode != 0:
+                log(f"[bench] adapter_driver {mode}: {r.stderr[-500:]}")
+                out[mode] = None
+                continue
+            st = r.stdout.split()
+            out[mode] = float(st[4])
+            out[mode + "_stats"] = [int(x) for x in st[:4]]
+    return out
 
 
 # ----------------------------------------------------------------------------- distributed
@@ -478,6 +518,8 @@ def main():
     ap.add_argument("--frames-per-step", type=int, default=0,
                     help="frames per timed step (default: four times the extraction contexts with --streams 3, "
                          "i.e. four rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
+    ap.add_argument("--no-seq", action="store_true",
+                    help="timed steps through per-frame binding calls instead of one recorded vx_seq per step")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),
                     help="with --streams 3: Match(t) on frame t's extraction context right after Extract(t) "
                          "(default: one hardware queue fewer; measured 0.073 vs 0.073-0.076 ms/frame, steadier) "
@@ -689,6 +731,39 @@ def main():
         for f in range(F):
             step(i * F + f)
 
+    # The timed steps through recorded sequences (vx_seq): the calls of step() above for F frames,
+    # recorded once per phase of the pipeline's period (frame buffers, slots and events repeat every
+    # lcm(frames, 3E, 4E) frames) and replayed from C — one binding call per step instead of ~8 per
+    # frame.  --no-seq keeps the per-frame calls.
+    host_path = "per-frame ctypes calls"
+    if not skip and not args.diag_nodep and not args.no_seq:
+        period = int(np.lcm.reduce([args.frames, 3 * E, 4 * E]))
+        n_seq = int(np.lcm(period, F)) // F
+        seqs = []
+        for k in range(n_seq):
+            sq = vxslam.Seq()
+            for f in range(F):
+                i = k * F + f
+                ci, si = loc(i)
+                x = ectxs[ci]
+                sq.wait(x, ev_m[(i - 3 * E + 1) % (4 * E)])
+                sq.extract(x, params, frames_dev[i % args.frames].data_ptr(), w, h, 3, w * 3, si)
+                sq.record(x, ev_e[ci])
+                mx = x if mon else mctx
+                if mon and E > 1:
+                    sq.wait(mx, ev_e[(i - 1) % E])
+                elif not mon:
+                    sq.wait(mx, ev_e[ci])
+                sq.match(mx, slot[loc(i - 1)], slot[loc(i)], 0.8)
+                sq.record(mx, ev_m[i % (4 * E)])
+                sq.wait(bctx, ev_m[i % (4 * E)])
+                sq.ba_run(bctx, plan)
+            seqs.append(sq)
+        host_path = f"vx_seq: one C call per step ({n_seq} recorded phases of {F} frames, {len(seqs[0])} calls each)"
+
+        def fstep(i):  # noqa: F811
+            seqs[i % n_seq].run()
+
     # ---- fixed internal pre-warm, outside the reported warm-up: every launch sequence a step can
     # take is keyed by (context, slot, frame buffer) — lcm(frames, 3 E) distinct extraction keys, 3 E
     # match keys, one LocalBA plan — and is replayed from a hipGraph only from its third sighting
@@ -835,6 +910,7 @@ def main():
             # host time to enqueue one step (Python + C-ABI calls, graph launches), diagnostic: the
             # GPU pipeline cannot run faster than this
             "host_enqueue_ms_per_step": round(enqueue_ms, 4),
+            "host_path": host_path,
             # untimed steps run before the warm-up so that every step of the timed region replays
             # captured graphs (see the pre-warm above)
             "prewarm_steps": prewarm,

@@ -379,6 +379,22 @@ int vx_ba_plan_create_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int ha
 /* enqueue the scatter of a run's window poses and optimised landmark positions into the map (stream
  * ordered after the run; no host synchronisation) */
 int vx_ba_plan_apply_dmap(vx_ctx* ctx, vx_ba_plan* plan, vx_dmap* map);
+/* LocalBA::Optimize(map, ref_kf) (local_ba.cpp:66-249) on the resident map in ONE call: window
+ * selection over the host id mirror, then plan build, iterations and the scatter of the results into
+ * the map's rows as one stream-ordered sequence over buffers sized by capacity, with the counts kept
+ * on the device — the call synchronises once, at its end, to fill `stats` (ba_lean.hip).  Windows of
+ * more than 255 keyframes (or $VX_LEAN=0) take the general build (vx_ba_plan_create_dmap + run +
+ * apply) inside the same call.  Same status / iteration / observation counts as vx_ba_optimize_map on
+ * the equivalent snapshot; poses and positions within the BA tolerance. */
+int vx_ba_optimize_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_ref, const vx_ba_options* opt,
+                        vx_ba_stats* stats);
+/* What the last vx_ba_optimize_dmap changed (for a host Map mirror: Frame::SetPose /
+ * Landmark::SetPosition, local_ba.cpp:173,237): *n_kf window keyframe rows (insertion order rows of
+ * the map) with their poses (7 each) and *n_lm optimised landmark rows with their positions (3 each);
+ * both 0 when nothing was optimised.  Any output pointer may be NULL; VX_ERR_CAPACITY if a count
+ * exceeds its cap (the counts are set either way). */
+int vx_ba_dmap_results(vx_ctx* ctx, vx_dmap* map, int cap_kf, int64_t* kf_rows, double* kf_pose7, int cap_lm,
+                       int64_t* lm_rows, double* lm_pos3, int* n_kf, int* n_lm);
 
 /* ---------------------------------------------------------------- Schur-complement joint BA
  * NOT a reference entry point: the reference's LocalBA alternates per-keyframe and per-landmark
@@ -536,6 +552,27 @@ int vx_essential_ransac(vx_ctx* ctx, const float* pts_last, const float* pts_cur
 int vx_essential_ransac_batch(vx_ctx* ctx, int n_problems, const int32_t* offsets, const float* pts_last,
                               const float* pts_curr, const double* intr4, const vx_essential_options* opt,
                               uint8_t* mask, vx_essential_result* out);
+
+/* ---------------------------------------------------------------- recorded enqueue sequences
+ * A list of the async calls above (event waits / records, vx_orb_extract_async,
+ * vx_match_device_async, vx_ba_plan_run_async), recorded once with every argument and replayed by
+ * vx_seq_run in the recorded order, exactly as the individual calls would run — for a pipelined
+ * caller whose per-frame calls would otherwise each cross a language binding (bench.py: one step of
+ * F frames = one vx_seq_run).  The recorded pointers (contexts, events, plans, device buffers) must
+ * outlive the sequence.  vx_seq_run stops at the first failing call: its status is returned and
+ * *failed_op (may be NULL) set to its index (-1 when every call succeeded). */
+typedef struct vx_seq vx_seq;
+int vx_seq_create(vx_seq** out);
+void vx_seq_destroy(vx_seq* seq);
+int vx_seq_wait(vx_seq* seq, vx_ctx* ctx, vx_event* ev);
+int vx_seq_record(vx_seq* seq, vx_ctx* ctx, vx_event* ev);
+int vx_seq_extract(vx_seq* seq, vx_ctx* ctx, const vx_orb_params* params, const uint8_t* d_img, int width,
+                   int height, int channels, int64_t row_stride, int slot);
+int vx_seq_match(vx_seq* seq, vx_ctx* ctx, const uint8_t* d_query, const int32_t* d_n_query, int cap_query,
+                 const uint8_t* d_train, const int32_t* d_n_train, int cap_train, float ratio);
+int vx_seq_ba_run(vx_seq* seq, vx_ctx* ctx, vx_ba_plan* plan);
+int vx_seq_length(const vx_seq* seq);
+int vx_seq_run(vx_seq* seq, int* failed_op);
 
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);

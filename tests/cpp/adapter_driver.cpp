@@ -5,12 +5,17 @@
 //   adapter_driver extract <img.bin> <h> <w> <c> <n_features> <out_prefix>
 //   adapter_driver match <q.bin> <nq> <t.bin> <nt> <out.bin>
 //   adapter_driver ba <dir> <window> <iters> <ref_id or -1> [flatten]
+//   adapter_driver ba_calls <dir> <window> <iters> <ref_id or -1> <reps> resident|snapshot
+//                  (LocalBA::Optimize with a DeviceMap attached, or on the snapshot path; the first
+//                  call dumped like `ba`, then the median ms of `reps` further calls)
 //   adapter_driver depth <dir>                     (KeyFrameLandmarks::CreateLandmarksFromDepth)
 //   adapter_driver triangulate <dir> <min_deg> <max_err>   (TriangulateWithLastKeyFrame)
 //   adapter_driver pnp <dir> <iterations> <reproj_err>    (solvePnPRansac as TrackWithPnP calls it)
 //   adapter_driver essential <dir>                         (EstimatePoseByEssential's two calls)
 //   adapter_driver extract_batch <dir> <n> <h> <w> <c> <n_features>   (ORBExtractor::ExtractBatch of
 //                  dir/img<i>.bin, then ORBMatcher::MatchBatch of the pairs (i, i + 1) -> dir/*.out)
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <climits>
@@ -21,6 +26,7 @@
 #include <string>
 #include <vector>
 
+#include "visionx/device_map.h"
 #include "visionx/feature.h"
 #include "visionx/geometry.h"
 #include "visionx/mapping.h"
@@ -144,8 +150,88 @@ static int cmd_extract_batch(char** a) {
     return 0;
 }
 
+struct BaInput {
+    Map::Ptr map;
+    std::vector<Frame::Ptr> frames;
+    std::vector<Landmark::Ptr> lms;
+};
+
+static BaInput build_map(const std::string& dir);
+static void dump_ba(const std::string& dir, const BaInput& in, const vx_ba_stats& st);
+
 static int cmd_ba(int argc, char** a) {
     const std::string dir = a[0];
+    const int window = std::atoi(a[1]), iters = std::atoi(a[2]);
+    const long long ref = std::atoll(a[3]);
+    const bool flatten_only = argc > 4 && std::string(a[4]) == "flatten";
+    BaInput in = build_map(dir);
+    auto map = in.map;
+    Frame::Ptr ref_kf = ref >= 0 ? map->GetFrame((uint64_t)ref) : nullptr;
+    if (flatten_only) {
+        FlatMap f = LocalBA::Flatten(*map, ref_kf, window);
+        std::printf("%zu %zu %zu\n", f.kf_id.size(), f.lm_id.size(), f.obs_kf_id.size());
+        write_bin(dir + "/flat_kf_id.out", f.kf_id);
+        write_bin(dir + "/flat_lm_id.out", f.lm_id);
+        return 0;
+    }
+    LocalBA::Options o;
+    o.window_size = window;
+    o.max_iterations = iters;
+    LocalBA ba(o);
+    ba.Optimize(map, ref_kf);
+    dump_ba(dir, in, ba.LastStats());
+    return 0;
+}
+
+static void dump_ba(const std::string& dir, const BaInput& in, const vx_ba_stats& st) {
+    std::vector<double> pose_out, lm_out;
+    for (const auto& fr : in.frames) {
+        const SE3d T = fr->Pose();
+        pose_out.insert(pose_out.end(), {T.qx, T.qy, T.qz, T.qw, T.tx, T.ty, T.tz});
+    }
+    for (const auto& lm : in.lms) {
+        const Vec3d p = lm->Position();
+        lm_out.insert(lm_out.end(), {p.x, p.y, p.z});
+    }
+    write_bin(dir + "/kf_pose.out", pose_out);
+    write_bin(dir + "/lm_pos.out", lm_out);
+    std::printf("%d %d %d %d\n", st.status, st.iterations, st.n_window_kf, st.n_landmarks);
+}
+
+// LocalBA::Optimize with a DeviceMap attached (resident mode) or on the snapshot path ("flatten"):
+// the first call's result is dumped like `ba`; then `reps` more calls, one after the other on the
+// evolving map as a keyframe-by-keyframe run makes them, and the median wall time of one call (ms,
+// the write-back into the Frame / Landmark objects included) is printed as the second line
+static int cmd_ba_calls(char** a) {
+    const std::string dir = a[0];
+    const int window = std::atoi(a[1]), iters = std::atoi(a[2]), reps = std::atoi(a[4]);
+    const long long ref = std::atoll(a[3]);
+    const bool resident = std::string(a[5]) == "resident";
+    BaInput in = build_map(dir);
+    Frame::Ptr ref_kf = ref >= 0 ? in.map->GetFrame((uint64_t)ref) : nullptr;
+    LocalBA::Options o;
+    o.window_size = window;
+    o.max_iterations = iters;
+    LocalBA ba(o);
+    if (resident) {
+        auto dm = std::make_shared<DeviceMap>();
+        dm->Mirror(*in.map);
+        ba.UseDeviceMap(dm);
+    }
+    ba.Optimize(in.map, ref_kf);
+    dump_ba(dir, in, ba.LastStats());
+    std::vector<double> ms;
+    for (int r = 0; r < reps; ++r) {
+        const auto t0 = std::chrono::steady_clock::now();
+        ba.Optimize(in.map, ref_kf);
+        ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+    std::sort(ms.begin(), ms.end());
+    std::printf("%.4f\n", ms.empty() ? 0.0 : ms[ms.size() / 2]);
+    return 0;
+}
+
+static BaInput build_map(const std::string& dir) {
     auto rd64 = [&](const char* n) { return read_bin<uint64_t>(dir + "/" + n + ".bin"); };
     auto rdd = [&](const char* n) { return read_bin<double>(dir + "/" + n + ".bin"); };
     auto rdi = [&](const char* n) { return read_bin<int64_t>(dir + "/" + n + ".bin"); };
@@ -155,9 +241,6 @@ static int cmd_ba(int argc, char** a) {
     const auto kf_pose = rdd("kf_pose"), kf_intr = rdd("kf_intr"), feat_uv = rdd("feat_uv"), lm_pos = rdd("lm_pos");
     const auto kf_ptr = rdi("kf_feat_ptr"), obs_ptr = rdi("lm_obs_ptr");
     const auto has_cam = rdb("kf_has_cam"), flags = rdb("feat_flags"), lm_bad = rdb("lm_bad");
-    const int window = std::atoi(a[1]), iters = std::atoi(a[2]);
-    const long long ref = std::atoll(a[3]);
-    const bool flatten_only = argc > 4 && std::string(a[4]) == "flatten";
 
     // Build visionx::Map exactly as Tracking would have populated it.
     auto map = std::make_shared<Map>();
@@ -189,33 +272,7 @@ static int cmd_ba(int argc, char** a) {
         map->InsertLandmark(lm);
         lms.push_back(lm);
     }
-    Frame::Ptr ref_kf = ref >= 0 ? map->GetFrame((uint64_t)ref) : nullptr;
-    if (flatten_only) {
-        FlatMap f = LocalBA::Flatten(*map, ref_kf, window);
-        std::printf("%zu %zu %zu\n", f.kf_id.size(), f.lm_id.size(), f.obs_kf_id.size());
-        write_bin(dir + "/flat_kf_id.out", f.kf_id);
-        write_bin(dir + "/flat_lm_id.out", f.lm_id);
-        return 0;
-    }
-    LocalBA::Options o;
-    o.window_size = window;
-    o.max_iterations = iters;
-    LocalBA ba(o);
-    ba.Optimize(map, ref_kf);
-    std::vector<double> pose_out, lm_out;
-    for (const auto& fr : frames) {
-        const SE3d T = fr->Pose();
-        pose_out.insert(pose_out.end(), {T.qx, T.qy, T.qz, T.qw, T.tx, T.ty, T.tz});
-    }
-    for (const auto& lm : lms) {
-        const Vec3d p = lm->Position();
-        lm_out.insert(lm_out.end(), {p.x, p.y, p.z});
-    }
-    write_bin(dir + "/kf_pose.out", pose_out);
-    write_bin(dir + "/lm_pos.out", lm_out);
-    const auto& st = ba.LastStats();
-    std::printf("%d %d %d %d\n", st.status, st.iterations, st.n_window_kf, st.n_landmarks);
-    return 0;
+    return BaInput{map, frames, lms};
 }
 
 // Frame with the features of <dir>/<pfx>uv.bin / <pfx>has.bin, the pose <pfx>pose.bin (7) and the
@@ -368,6 +425,7 @@ int main(int argc, char** argv) {
         if (cmd == "extract" && argc >= 8) return cmd_extract(argv + 2);
         if (cmd == "match" && argc >= 7) return cmd_match(argv + 2);
         if (cmd == "ba" && argc >= 6) return cmd_ba(argc - 2, argv + 2);
+        if (cmd == "ba_calls" && argc >= 8) return cmd_ba_calls(argv + 2);
         if (cmd == "depth" && argc >= 3) return cmd_depth(argv + 2);
         if (cmd == "triangulate" && argc >= 5) return cmd_triangulate(argv + 2);
         if (cmd == "pnp" && argc >= 5) return cmd_pnp(argv + 2);

@@ -125,11 +125,19 @@ def test_adapter_extract_and_match_batch(driver, oracle, tmp_path):
 
 
 @pytest.mark.gpu
-def test_adapter_local_ba(driver, oracle, tmp_path):
+@pytest.mark.parametrize("mode", ["snapshot", "resident"])
+def test_adapter_local_ba(driver, oracle, tmp_path, mode):
+    """LocalBA::Optimize through the C++ adapter against the restatement: the snapshot path (Flatten
+    + vx_ba_optimize_map) and the resident path (DeviceMap mirroring the Map, vx_ba_optimize_dmap,
+    results written back into the Frame / Landmark objects)."""
     m = synth.make_ba_map(92, 10, 2000, n_old_kf=3)
     dump_map(m, tmp_path)
     ref = int(m["kf_id"][-1])
-    status, iters, nkf, nlm = map(int, run(driver, "ba", tmp_path, 10, 5, ref))
+    if mode == "snapshot":
+        status, iters, nkf, nlm = map(int, run(driver, "ba", tmp_path, 10, 5, ref))
+    else:
+        status, iters, nkf, nlm, _ = run(driver, "ba_calls", tmp_path, 10, 5, ref, 2, "resident")
+        status, iters, nkf, nlm = map(int, (status, iters, nkf, nlm))
     mc = m.copy()
     st = oracle.ba_optimize(mc, oracle.ba_options(window=10), ref_kf_id=ref)
     assert (status, iters, nkf, nlm) == (st.status, st.iterations, st.n_window_kf, st.n_landmarks)

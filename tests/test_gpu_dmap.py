@@ -282,3 +282,171 @@ def test_dmap_culling_and_reobservation(ctx, monkeypatch, compact):
     mir.obs_rows.append(len(m["obs_kf_id"]) - 1)
     check()
     dm.close()
+
+
+# ---------------------------------------------------------------- one-call LocalBA on the resident map
+# vx_ba_optimize_dmap (csrc/ba_lean.hip): plan, iterations and scatter as one device sequence.  Pinned
+# to the CPU restatement (oracle/ba_oracle.cpp, local_ba.cpp:66-249) on the equivalent snapshot, at
+# the BA tolerance with identical iteration / per-iteration observation counts (no gate flips).
+BA_RTOL = 1e-4
+
+
+def _canon(q):
+    q = np.array(q, np.float64)
+    q[q[:, 3] < 0, :4] *= -1
+    return q
+
+
+def _assert_close(pose_g, pos_g, pose_c, pos_c, st_g, st_c):
+    assert (st_g.status, st_g.n_window_kf, st_g.n_landmarks) == (st_c.status, st_c.n_window_kf, st_c.n_landmarks)
+    assert st_g.iterations == st_c.iterations
+    assert list(st_g.obs[:st_g.iterations]) == list(st_c.obs[:st_c.iterations])
+    for a, b in zip(st_g.cost[:st_g.iterations], st_c.cost[:st_c.iterations]):
+        assert abs(a - b) <= 1e-6 * abs(b)
+    for a, b in ((_canon(pose_g), _canon(pose_c)), (pos_g, pos_c)):
+        err = np.abs(a - b) / np.maximum(np.abs(b), 1e-3)
+        assert err.max() <= BA_RTOL, err.max()
+
+
+def _oracle_on(oracle, m2, opts_kw, ref):
+    mc = m2.copy()
+    st = oracle.ba_optimize(mc, oracle.ba_options(**opts_kw), ref_kf_id=ref)
+    if st.status == 0 and st.gate_margin < 1e-8:
+        pytest.skip(f"gate margin {st.gate_margin} too small for a stable comparison")
+    return mc, st
+
+
+@pytest.mark.parametrize("cfg", [("C2", 10, 2000, 1), ("C3", 50, 20000, 1), ("C5s", 40, 8000, 4)])
+def test_dmap_optimize_matches_oracle(ctx, oracle, cfg, monkeypatch):
+    """One call on the resident map == the restatement on the equivalent snapshot; the general
+    build (VX_LEAN=0) gives the same counts; results() names exactly the rows that changed."""
+    name, nk, nl, ns = cfg
+    m = synth.make_ba_map(0xE0 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
+    kw = dict(window=nk, iters=5)
+    for lean in ("1", "0"):
+        monkeypatch.setenv("VX_LEAN", lean)
+        dm = vxslam.DMap(ctx)
+        kf_order, lm_order = vxslam.dmap_load(dm, m)
+        m2 = vxslam.map_reorder(m, kf_order, lm_order)
+        pose0, pos0 = dm.download()
+        st = dm.optimize(vxslam.default_ba_options(**kw), ref_kf_id=m["ref_kf_id"])
+        mc, sc = _oracle_on(oracle, m2, kw, m["ref_kf_id"])
+        pose, pos = dm.download()
+        _assert_close(pose, pos, mc["kf_pose"].reshape(-1, 7), mc["lm_pos"].reshape(-1, 3), st, sc)
+        kr, kp, lr, lp = dm.results()
+        assert len(kr) == st.n_window_kf and len(lr) == st.n_landmarks
+        assert np.array_equal(kp, pose[kr]) and np.array_equal(lp, pos[lr])
+        untouched = np.ones(len(pos), bool)
+        untouched[lr] = False
+        assert np.array_equal(pos[untouched], pos0[untouched])  # every other row as it was
+        # a second call starts from the scattered state, as the next keyframe's Optimize would
+        m2["kf_pose"], m2["lm_pos"] = pose.copy(), pos.copy()
+        st2 = dm.optimize(vxslam.default_ba_options(**kw), ref_kf_id=m["ref_kf_id"])
+        mc2, sc2 = _oracle_on(oracle, m2, kw, m["ref_kf_id"])
+        pose, pos = dm.download()
+        _assert_close(pose, pos, mc2["kf_pose"].reshape(-1, 7), mc2["lm_pos"].reshape(-1, 3), st2, sc2)
+        dm.close()
+
+
+def test_dmap_optimize_incremental_culling_vs_oracle(ctx, oracle):
+    """Keyframes one at a time with edits in between (outlier toggles, bad flags, poses), then a
+    keyframe removed from inside the window and landmarks culled; after every event one
+    vx_ba_optimize_dmap, compared with the restatement on the mirror snapshot as it then stands."""
+    m = synth.make_ba_map(0xE7, 14, 3000, n_old_kf=2)
+    for key in ("obs_kf_id", "obs_feat_idx", "feat_lm_id", "feat_flags", "lm_bad"):
+        m[key] = m[key].copy()
+    dm = vxslam.DMap(ctx)
+    mir = _Mirror(m, dm)
+    kw = dict(window=6, iters=3)
+    opts = vxslam.default_ba_options(**kw)
+    rng = np.random.default_rng(21)
+
+    def check(ref=None):
+        m2 = mir.snapshot()
+        st = dm.optimize(opts, ref_kf_id=ref)
+        mc, sc = _oracle_on(oracle, m2, kw, ref)
+        pose_d, pos_d = dm.download()
+        row_kf = {int(k): i for i, k in enumerate(mir.all_kf)}
+        row_lm = {int(l): i for i, l in enumerate(mir.all_lm)}
+        kr, lr = np.asarray(mir.kf_rows), np.asarray(mir.lm_rows, np.int64)
+        pg = pose_d[[row_kf[int(k)] for k in kr]] if len(kr) else np.zeros((0, 7))
+        lg = pos_d[[row_lm[int(l)] for l in lr]] if len(lr) else np.zeros((0, 3))
+        _assert_close(pg, lg, mc["kf_pose"].reshape(-1, 7), mc["lm_pos"].reshape(-1, 3), st, sc)
+        # the optimised state becomes the source map's for what follows
+        m["kf_pose"].reshape(-1, 7)[kr] = pg
+        m["lm_pos"].reshape(-1, 3)[lr] = lg
+        return st
+
+    order = np.argsort(m["kf_id"], kind="stable")
+    mir.all_kf, mir.all_lm = [], []
+    ran = 0
+    for step, k in enumerate(order):
+        before = len(mir.lm_rows)
+        mir.add(k)
+        mir.all_kf.append(int(k))
+        mir.all_lm.extend(mir.lm_rows[before:])
+        if step < 2:
+            continue
+        kid = int(m["kf_id"][k])
+        f0, f1 = m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]
+        fi = rng.choice(f1 - f0, 5, replace=False).astype(np.int32)
+        fl = m["feat_flags"][f0 + fi] ^ 2
+        m["feat_flags"][f0 + fi] = fl
+        dm.set_features(kid, fi, m["feat_lm_id"][f0 + fi], fl)
+        bad = rng.choice(np.asarray(mir.lm_rows), 3, replace=False)
+        m["lm_bad"][bad] = 1
+        dm.set_landmark_bad(m["lm_id"][bad], np.ones(3, np.uint8))
+        ran += check(kid).status == 0
+    assert ran >= 8
+
+    # Tracking::RemoveKeyFrame of a window keyframe (tracking.cpp:752-773)
+    k = int(order[-3])
+    kid = int(m["kf_id"][k])
+    f0, f1 = m["kf_feat_ptr"][k], m["kf_feat_ptr"][k + 1]
+    fidx = np.nonzero(m["feat_flags"][f0:f1] & 1)[0]
+    lms = m["feat_lm_id"][f0 + fidx]
+    known = np.isin(lms, m["lm_id"][np.asarray(mir.lm_rows)])
+    dm.remove_observations(lms[known], np.full(int(known.sum()), kid, np.uint64))
+    lm_row = {int(i): r for r, i in enumerate(m["lm_id"])}
+    drop = {(lm_row[int(i)], kid) for i in lms[known]}
+    mir.obs_rows = [r for r in mir.obs_rows if (int(mir.obs_lm[r]), int(m["obs_kf_id"][r])) not in drop]
+    m["feat_lm_id"][f0 + fidx] = 0
+    m["feat_flags"][f0 + fidx] = 2
+    dm.set_features(kid, fidx.astype(np.int32), np.zeros(len(fidx), np.uint64), np.full(len(fidx), 2, np.uint8))
+    dm.remove_keyframe(kid)
+    mir.kf_rows.remove(k)
+    assert check().status == 0
+
+    # CullLandmarks: SetBad, features reset, Map::RemoveLandmark (tracking.cpp:652-750)
+    cull = rng.choice(np.asarray(mir.lm_rows), 60, replace=False)
+    for k2 in mir.kf_rows:
+        g0, g1 = m["kf_feat_ptr"][k2], m["kf_feat_ptr"][k2 + 1]
+        hit = np.nonzero(np.isin(m["feat_lm_id"][g0:g1], m["lm_id"][cull]) & (m["feat_flags"][g0:g1] & 1 > 0))[0]
+        if len(hit):
+            m["feat_lm_id"][g0 + hit] = 0
+            m["feat_flags"][g0 + hit] = 2
+            dm.set_features(int(m["kf_id"][k2]), hit.astype(np.int32), np.zeros(len(hit), np.uint64),
+                            np.full(len(hit), 2, np.uint8))
+    dm.set_landmark_bad(m["lm_id"][cull], np.ones(len(cull), np.uint8))
+    dm.remove_landmarks(m["lm_id"][cull])
+    for l in cull:
+        mir.lm_rows.remove(int(l))
+    assert check().status == 0
+    dm.close()
+
+
+def test_dmap_optimize_edges(ctx):
+    """One keyframe (local_ba.cpp:73-75) and no optimisable landmark (:106-108): status 1, nothing
+    written; results() then reports no rows."""
+    dm = vxslam.DMap(ctx)
+    dm.add_keyframe(1, [0, 0, 0, 1, 0, 0, 0], [500, 500, 320, 240], 1, np.zeros((3, 2)), np.zeros(3, np.uint64),
+                    np.zeros(3, np.uint8))
+    st = dm.optimize(vxslam.default_ba_options(window=5, iters=2))
+    assert st.status == 1 and st.n_window_kf == 1
+    assert [len(x) for x in dm.results()] == [0, 0, 0, 0]
+    dm.add_keyframe(2, [0, 0, 0, 1, 0, 0, 0], [500, 500, 320, 240], 1, np.zeros((3, 2)), np.zeros(3, np.uint64),
+                    np.zeros(3, np.uint8))
+    dm.add_landmarks([9], [[0, 0, 5]])
+    st = dm.optimize(vxslam.default_ba_options(window=5, iters=2))
+    assert st.status == 1 and st.n_window_kf == 2 and st.n_landmarks == 0
+    dm.close()

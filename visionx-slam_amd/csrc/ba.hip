@@ -29,6 +29,7 @@
 // iteration 0 reads the initial poses / positions directly, so a run needs no reset launch.
 // The step keeps the reference's sign (b = -J^T e, :156 and :224): this is a drop-in, not a fix.
 #include <algorithm>
+#include <cstddef>
 #include <chrono>
 #include <cmath>
 #include <type_traits>
@@ -99,7 +100,20 @@ struct BAArgs {
     const int* lm_blk;       // k_landmark_solve workgroup -> {first landmark, first observation} (n_blocks + 1)
     const double2* lobs_uv;
     BAState* state;
+    // resident one-call build (ba_lean.hip): counts known only on the device — {n_opt, n_lm, landmark
+    // workgroups, status (1: no optimisable landmark, nothing runs), ...}; null for built plans
+    const int* dyn;
 };
+
+// A lean plan's counts from the device (the launch grid is a capacity bound; surplus workgroups of
+// the landmark stage exit); false when nothing runs (no optimisable landmark, local_ba.cpp:106-108)
+__device__ __forceinline__ bool dyn_counts(BAArgs& a) {
+    if (!a.dyn) return true;
+    if (a.dyn[kDynStatus]) return false;
+    a.n_opt = a.dyn[kDynNOpt];
+    a.n_lm = a.dyn[kDynNLm];
+    return true;
+}
 
 
 // Iteration `it` reads the poses of iteration it-1 (the initial poses at it == 0) and writes the
@@ -299,7 +313,9 @@ __device__ __forceinline__ void pose_obs_accum(const BAArgs& a, const double* T,
 // (strided) in registers; a fixed-order wave butterfly + LDS tree reduces them into the slice's
 // partial block kf_part[k * n_split + slice].  Partials are summed later in slice order, so the
 // result is deterministic (and identical on every rank after the sharded all-reduce).
-__global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a, int it) {
+__global__ __launch_bounds__(kPoseBlock) void k_pose_kf(BAArgs a0, int it) {
+    BAArgs a = a0;
+    if (!dyn_counts(a)) return;
     if (it > 0 && !a.state->active[it]) return;
     __shared__ double red[kPoseBlock / 64][kNTerms];
     VX_KT(0);
@@ -465,7 +481,9 @@ __device__ __forceinline__ D3 lm_update(const BAArgs& a, int l, D3 P, const doub
 // Every load of the landmark stage is issued first, so it lands during the combine and solve.
 // LDS: one kLdsStride-double slot per keyframe (combined normal equations S, then T 8 | R 9 | C 4) and
 // 9 x kLmBlock observation terms.
-__global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a, int it) {
+__global__ __launch_bounds__(kLmBlock) void k_landmark_solve(BAArgs a0, int it) {
+    BAArgs a = a0;
+    if (!dyn_counts(a) || (a.dyn && (int)blockIdx.x >= a.dyn[kDynBlocks])) return;
     if (it > 0 && !a.state->active[it]) return;
     extern __shared__ __attribute__((aligned(16))) double kf_lds[];
     double* terms = kf_lds + (long long)a.n_kf * kLdsStride;  // [9][kLmBlock]
@@ -1830,6 +1848,70 @@ int plan_run(vx_ctx* c, vx_ba_plan* p) {
     return VX_OK;
 }
 
+}  // namespace
+
+size_t ba_state_bytes() { return sizeof(BAState); }
+
+size_t ba_state_iter_offset() { return offsetof(BAState, iterations); }
+
+void ba_state_to_stats(const void* host_state, vx_ba_stats* s) {
+    const BAState& hs = *static_cast<const BAState*>(host_state);
+    s->iterations = hs.iterations;
+    for (int i = 0; i < 16; ++i) {
+        s->cost[i] = hs.cost[i];
+        s->obs[i] = hs.obs[i];
+    }
+}
+
+// The iterations of a lean plan (ba_lean.hip): the two-kernel LDS path (k_pose_kf, k_landmark_solve)
+// over capacity grids, the counts read from d.dyn on the device — no host synchronisation.
+int ba_run_dyn(vx_ctx* c, const DynPlan& d) {
+    BAArgs a{};
+    a.n_kf = d.n_kf;
+    a.n_opt = 0;  // (from dyn)
+    a.n_lm = 0;
+    a.min_pose_obs = d.opt.min_pose_observations;
+    a.min_point_obs = d.opt.min_point_observations;
+    a.max_iter = d.opt.max_iterations;
+    a.huber = d.opt.huber_delta;
+    a.max_err = d.opt.max_reproj_error;
+    a.huber2 = a.huber * a.huber;
+    a.max_err2 = a.max_err * a.max_err;
+    a.kf_pose0 = d.kf_pose0;
+    a.kf_pose = d.kf_pose;
+    a.kf_intr = d.kf_intr;
+    a.kf_rot = d.kf_rot;
+    a.kf_flags = d.kf_flags;
+    a.kf_obs_ptr = d.kf_obs_ptr;
+    a.kf_part = d.kf_part;
+    a.n_split = d.n_split;
+    a.kf_cost = d.kf_cost;
+    a.lm_pos0 = d.lm_pos0;
+    a.lm_pos = d.lm_pos;
+    a.pobs_uv = d.pobs_uv;
+    a.pobs_lm = d.pobs_lm;
+    a.lobs_ptr = d.lobs_ptr;
+    a.lobs_kf = d.lobs_kf;
+    a.lobs_lm = d.lobs_lm;
+    a.lm_blk = d.lm_blk;
+    a.lobs_uv = d.lobs_uv;
+    a.state = static_cast<BAState*>(d.state);
+    a.dyn = d.dyn;
+    const size_t lds = (size_t)d.n_kf * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
+    if (lds > 64 * 1024) {
+        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        VX_HIP(c, attr);
+    }
+    for (int it = 0; it < d.opt.max_iterations; ++it) {
+        VX_HIP(c, launch(c, kStBaPose, k_pose_kf, dim3(d.n_kf * d.n_split), dim3(kPoseBlock), 0, c->stream, a, it));
+        VX_HIP(c, launch(c, kStBaLandmark, k_landmark_solve, dim3(d.grid_blocks), dim3(kLmBlock), (uint32_t)lds,
+                         c->stream, a, it));
+    }
+    return VX_OK;
+}
+
+namespace {
 // Test hook for the sharded path on one device: the element-wise sum of the shards' partial blocks
 // (in rank order) written back to every shard, in place of the per-iteration ncclAllReduce.
 constexpr int kMaxEmuShards = 16;

@@ -1,0 +1,700 @@
+// ba_lean.hip — LocalBA::Optimize from the device-resident map in one call, with no host
+// synchronisation between the window selection and the end (vx_ba_optimize_dmap).
+//
+// The reference rebuilds its problem on every keyframe (local_ba.cpp:66-108: SelectKeyFrames, the
+// landmark set from the window's features, then per landmark its observations — mutex-guarded
+// GetLandmark / GetFrame, map.cpp:31-47, and unordered_map walks, landmark.h:42-49) and then
+// iterates (:110-248).  The plan build of ba_window.hip does the same on the device but reads three
+// counts back to size its outputs, packs the landmark-stage workgroups on the host and rebuilds the
+// map's landmark-major observation CSR with a radix sort whenever observations were added (every
+// keyframe).  Here every size is a capacity the host already knows (window features, map rows,
+// observation rows), every count stays in a small device header (dyn[], ba_plan.hpp), and the
+// landmark-stage lists are built from the window side, so no sort is needed:
+//
+//   k_lb_clear    per map landmark row: referenced / pose-referenced flags and the live observation
+//                 count cleared; the header zeroed
+//   k_lb_feat     per window feature (binary search of its keyframe row): its resident row, the
+//                 landmark row from the device id table (Map::GetLandmark), the pose-stage validity
+//                 (local_ba.cpp:126-138), the referenced marks (:83-92); rows < nk gather the window
+//                 keyframes' poses / intrinsics
+//   k_lb_obs      per observation row (Landmark::observations_): the landmark's live observation
+//                 count (ObservationCount, :99-101) and, when the pair's keyframe is in the window and
+//                 the feature it names is a non-outlier observation of this very landmark (:186-204),
+//                 a back-link on that window feature
+//   k_lb_flags    per landmark row: optimised = referenced && !bad && count >= min (:93-104), fixed =
+//                 seen by the pose stage but not optimised -> one 64-bit key (1 | fixed << 32)
+//   (scan)        slots: optimised rows first (map-row order), then fixed rows (map-row order)
+//   k_lb_slots    slot tables, initial positions, the counts into the header
+//   (scan)        pose-stage CSR positions
+//   k_lb_pose     the pose-stage CSR (feature order inside a keyframe, local_ba.cpp:131), keyframe
+//                 pointers; each back-linked feature of an optimised landmark sets its window row's
+//                 bit in the landmark's keyframe bit set
+//   k_lb_lcount   per slot: landmark-stage observations = popcount of its bit set
+//   (scan)        landmark-stage CSR pointers
+//   k_lb_lfill    the landmark-stage CSR (a landmark's observations in window order: rank = the bits
+//                 below its row) and the k_landmark_solve workgroup table: slot s goes to workgroup
+//                 (lobs_ptr[s] + s) / Q with Q = 512 - nk, so a workgroup holds < Q landmarks and
+//                 < Q + nk <= 512 observations — no sequential packing
+//   iterations    ba.hip k_pose_kf + k_landmark_solve over capacity grids (ba_run_dyn)
+//   k_lb_apply    the window poses and optimised positions into the resident rows
+// A landmark's observations are summed in window (keyframe id) order instead of insertion order;
+// the reference's own order is unordered_map iteration order, so parity is the usual 1e-4 with
+// identical iteration and observation counts (tests/test_gpu_dmap.py).
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <vector>
+
+#include <rocprim/rocprim.hpp>
+
+#include "vx_internal.hpp"
+#include "ba_common.hpp"
+#include "ba_plan.hpp"
+#include "dmap.hpp"
+
+namespace vx {
+namespace {
+
+constexpr int kT = 256;
+constexpr uint64_t kEmptyKey = ~0ull;
+inline unsigned grid(long long n) { return (unsigned)std::max(1ll, (n + kT - 1) / kT); }
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {  // splitmix64
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+// ---------------------------------------------------------------- landmark id table (resident)
+__global__ void k_ht_clear(uint64_t* key, unsigned cap) {
+    const unsigned i = blockIdx.x * kT + threadIdx.x;
+    if (i < cap) key[i] = kEmptyKey;
+}
+// rows [r0, r1); a removed row is skipped (a later row may hold its id again)
+__global__ void k_ht_add(uint64_t* key, int* val, unsigned mask, const uint64_t* lid, const uint8_t* bad, int64_t r0,
+                         int64_t r1) {
+    const int64_t r = r0 + (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (r >= r1 || bad[r] == kLmRemoved) return;
+    const uint64_t k = lid[r];
+    unsigned h = (unsigned)mix(k) & mask;
+    for (;;) {
+        const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(&key[h]),
+                                                  (unsigned long long)kEmptyKey, (unsigned long long)k);
+        if (prev == kEmptyKey || prev == k) {
+            val[h] = (int)r;
+            return;
+        }
+        h = (h + 1) & mask;
+    }
+}
+__device__ __forceinline__ int ht_get(const uint64_t* key, const int* val, unsigned mask, uint64_t k) {
+    unsigned h = (unsigned)mix(k) & mask;
+    for (unsigned probe = 0; probe <= mask; ++probe) {
+        const uint64_t x = key[h];
+        if (x == k) return val[h];
+        if (x == kEmptyKey) return -1;
+        h = (h + 1) & mask;
+    }
+    return -1;
+}
+
+// ---------------------------------------------------------------- build kernels
+struct LeanArgs {
+    // window (host tables, one upload): rows in ascending keyframe id order
+    int nk, nf, mw;                 // keyframes, features, 64-bit words of a keyframe bit set
+    const int64_t* src;             // nk: first resident feature row of window row r
+    const uint64_t* wid;            // nk: keyframe ids (ascending)
+    const int* wptr;                // nk + 1: window feature offsets
+    const int* win;                 // nk: resident keyframe rows
+    const uint8_t* cam;             // nk
+    // resident map
+    int64_t nl, nobs;
+    const double* feat_uv;
+    const uint64_t* feat_lm;
+    const uint8_t* feat_fl;
+    const uint64_t* lm_id;
+    const uint8_t* lm_bad;
+    const double* lm_pos;
+    const int* obs_lm;
+    const uint64_t* obs_kf;
+    const uint64_t* obs_fi;
+    const double* map_pose;
+    const double* map_intr;
+    const uint64_t* ht_key;
+    const int* ht_val;
+    unsigned ht_mask;
+    int min_point;
+    // per window feature
+    int* f_l;                       // landmark row or -1
+    int* f_code;                    // window row << 2 | pose-stage valid | landmark-stage candidate << 1
+    int* f_pv;                      // pose-stage valid (scan input, nf + 1)
+    int* f_back;                    // a live observation of its landmark names it (landmark stage)
+    double2* wuv;
+    // per landmark row
+    int* l_ref;
+    int* l_pv;
+    int* l_cnt;
+    unsigned long long* key;        // nl + 1
+    const unsigned long long* ex;   // its exclusive scan
+    int* l_slot;
+    int* inv;                       // slot -> landmark row
+    int* cnt;                       // slot -> landmark-stage observations (scan input, nl + 1)
+    unsigned long long* mask;       // slot x mw keyframe bit sets
+    const int* pscan;
+    const int* lobs_ptr;
+    // plan outputs
+    double* lm_pos0;
+    double2* puv;
+    int* plm;
+    int* kf_obs_ptr;
+    int* lkf;
+    int* llm;
+    double2* luv;
+    int* lm_blk;
+    double* kf_pose0;
+    double* kf_intr;
+    int* kf_flags;
+    int* dyn;
+    int q;                          // landmark-stage workgroup key span (512 - nk)
+};
+
+__global__ __launch_bounds__(kT) void k_lb_clear(LeanArgs a) {
+    const int64_t l = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (l < a.nl) {
+        a.l_ref[l] = 0;
+        a.l_pv[l] = 0;
+        a.l_cnt[l] = 0;
+    }
+    if (l < kDynInts) a.dyn[l] = 0;
+}
+
+__device__ __forceinline__ int window_row(const int* wptr, int nk, int f) {
+    int lo = 0, hi = nk - 1;  // last row with wptr[row] <= f
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (wptr[mid] <= f) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kT) void k_lb_feat(LeanArgs a) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f < a.nk) {  // the window keyframes' initial poses, intrinsics and camera flags
+        const int k = a.win[f];
+        for (int j = 0; j < 7; ++j) a.kf_pose0[8 * f + j] = a.map_pose[7 * (int64_t)k + j];
+        a.kf_pose0[8 * f + 7] = 0.0;
+        for (int j = 0; j < 4; ++j) a.kf_intr[4 * f + j] = a.map_intr[4 * (int64_t)k + j];
+        a.kf_flags[f] = a.cam[f];
+    }
+    if (f == a.nf) a.f_pv[f] = 0;  // (the scan's extra element)
+    if (f >= a.nf) return;
+    const int r = window_row(a.wptr, a.nk, f);
+    const int64_t g = a.src[r] + (f - a.wptr[r]);
+    const uint8_t fl = a.feat_fl[g];
+    a.wuv[f] = make_double2(a.feat_uv[2 * g], a.feat_uv[2 * g + 1]);
+    int l = -1;
+    if (fl & 1) {
+        l = ht_get(a.ht_key, a.ht_val, a.ht_mask, a.feat_lm[g]);
+        if (l >= 0 && a.lm_bad[l] == kLmRemoved) l = -1;  // Map::GetLandmark -> nullptr
+        if (l >= 0) a.l_ref[l] = 1;                       // local_ba.cpp:83-92
+    }
+    const bool good = (fl & 1) && !(fl & 2) && a.cam[r];
+    const bool pv = good && l >= 0 && !a.lm_bad[l];     // local_ba.cpp:126-138
+    if (pv) a.l_pv[l] = 1;
+    a.f_l[f] = l;
+    a.f_code[f] = (r << 2) | (good && l >= 0 ? 2 : 0) | (pv ? 1 : 0);
+    a.f_pv[f] = pv ? 1 : 0;
+    a.f_back[f] = 0;
+}
+
+__global__ __launch_bounds__(kT) void k_lb_obs(LeanArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i >= a.nobs) return;
+    const int l = a.obs_lm[i];
+    if (l == kDeadObs || a.lm_bad[l] == kLmRemoved) return;
+    atomicAdd(&a.l_cnt[l], 1);  // ObservationCount (live pairs)
+    const uint64_t kid = a.obs_kf[i];
+    int lo = 0, hi = a.nk - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (a.wid[mid] < kid) lo = mid + 1;
+        else hi = mid;
+    }
+    if (a.wid[lo] != kid) return;  // local_kf_ids.find (local_ba.cpp:187)
+    const uint64_t fi = a.obs_fi[i];
+    if (fi >= (uint64_t)(a.wptr[lo + 1] - a.wptr[lo])) return;  // :196
+    const int f = a.wptr[lo] + (int)fi;
+    // camera, has_landmark, !is_outlier (code bit 1) and feature.landmark_id_ == this landmark
+    // (:193-201); the pair is unique per (landmark, keyframe), and a feature names one landmark, so
+    // at most one row writes a feature
+    if ((a.f_code[f] & 2) && a.f_l[f] == l) a.f_back[f] = 1;
+}
+
+__global__ __launch_bounds__(kT) void k_lb_flags(LeanArgs a) {
+    const int64_t l = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (l == a.nl) a.key[l] = 0;
+    if (l >= a.nl) return;
+    const bool opt = a.l_ref[l] && !a.lm_bad[l] && a.l_cnt[l] >= a.min_point;
+    if (opt) atomicAdd(&a.dyn[kDynGlobal], 1);
+    const bool fixed = !opt && a.l_pv[l];
+    a.key[l] = (opt ? 1ull : 0ull) | (fixed ? 1ull << 32 : 0ull);
+}
+
+__global__ __launch_bounds__(kT) void k_lb_slots(LeanArgs a) {
+    const int64_t l = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const unsigned long long tot = a.ex[a.nl];
+    const int n_opt = (int)(unsigned)tot, n_fixed = (int)(tot >> 32);
+    if (l == 0) {
+        a.dyn[kDynNOpt] = n_opt;
+        a.dyn[kDynNLm] = n_opt + n_fixed;
+        a.dyn[kDynNFixed] = n_fixed;
+        a.dyn[kDynStatus] = n_opt == 0 ? 1 : 0;  // no optimisable landmark (local_ba.cpp:106-108)
+    }
+    if (l >= a.nl) return;
+    const unsigned long long k = a.key[l], e = a.ex[l];
+    int s = -1;
+    if (k & 1ull) s = (int)(unsigned)e;
+    else if (k >> 32) s = n_opt + (int)(e >> 32);
+    a.l_slot[l] = s;
+    if (s < 0) return;
+    a.inv[s] = (int)l;
+    a.lm_pos0[4 * (int64_t)s] = a.lm_pos[3 * l];
+    a.lm_pos0[4 * (int64_t)s + 1] = a.lm_pos[3 * l + 1];
+    a.lm_pos0[4 * (int64_t)s + 2] = a.lm_pos[3 * l + 2];
+    a.lm_pos0[4 * (int64_t)s + 3] = 0.0;
+    if (s < n_opt)
+        for (int w = 0; w < a.mw; ++w) a.mask[(int64_t)s * a.mw + w] = 0ull;
+}
+
+__global__ __launch_bounds__(kT) void k_lb_pose(LeanArgs a) {
+    const int f = blockIdx.x * kT + threadIdx.x;
+    if (f <= a.nk) a.kf_obs_ptr[f] = a.pscan[a.wptr[f]];  // (wptr[nk] == nf: the total)
+    if (f == 0) a.dyn[kDynPoseObs] = a.pscan[a.nf];
+    if (f >= a.nf) return;
+    const int code = a.f_code[f];
+    const int l = a.f_l[f];
+    if (code & 1) {
+        const int o = a.pscan[f];
+        a.puv[o] = a.wuv[f];
+        a.plm[o] = a.l_slot[l];
+    }
+    if (a.f_back[f]) {
+        const int s = a.l_slot[l];
+        if (s >= 0 && s < a.dyn[kDynNOpt]) {
+            const int r = code >> 2;
+            atomicOr(&a.mask[(int64_t)s * a.mw + (r >> 6)], 1ull << (r & 63));
+        }
+    }
+}
+
+__global__ __launch_bounds__(kT) void k_lb_lcount(LeanArgs a) {
+    const int64_t s = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (s > a.nl) return;
+    int c = 0;
+    if (s < a.dyn[kDynNOpt])
+        for (int w = 0; w < a.mw; ++w) c += __popcll(a.mask[s * a.mw + w]);
+    a.cnt[s] = c;  // (slots past n_opt and the scan's extra element: 0)
+    if (c) atomicMax(&a.dyn[kDynMaxObs], c);
+}
+
+__global__ __launch_bounds__(kT) void k_lb_lfill(LeanArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    const int n_opt = a.dyn[kDynNOpt];
+    if (i < a.nf && a.f_back[i]) {
+        const int s = a.l_slot[a.f_l[i]];
+        if (s >= 0 && s < n_opt) {
+            const int r = a.f_code[i] >> 2;
+            const unsigned long long* m = a.mask + (int64_t)s * a.mw;
+            int rank = __popcll(m[r >> 6] & ((1ull << (r & 63)) - 1ull));
+            for (int w = 0; w < (r >> 6); ++w) rank += __popcll(m[w]);
+            const int at = a.lobs_ptr[s] + rank;
+            a.lkf[at] = r;
+            a.llm[at] = s;
+            a.luv[at] = a.wuv[i];
+        }
+    }
+    if (i < n_opt) {  // landmark-stage workgroups: slot s -> (lobs_ptr[s] + s) / q
+        const int s = (int)i;
+        const int b = (a.lobs_ptr[s] + s) / a.q;
+        const int bp = s ? (a.lobs_ptr[s - 1] + s - 1) / a.q : -1;
+        if (b != bp) {
+            a.lm_blk[2 * b] = s;
+            a.lm_blk[2 * b + 1] = a.lobs_ptr[s];
+        }
+        if (s == n_opt - 1) {
+            a.lm_blk[2 * (b + 1)] = n_opt;
+            a.lm_blk[2 * (b + 1) + 1] = a.lobs_ptr[n_opt];
+            a.dyn[kDynBlocks] = b + 1;
+            a.dyn[kDynLmObs] = a.lobs_ptr[n_opt];
+        }
+    }
+}
+
+// the finished run into the resident rows (the last iteration's ping-pong pose buffer)
+__global__ __launch_bounds__(kT) void k_lb_apply(const int* dyn, const int* iters, int nk, const int* win,
+                                                 const double* kf_pose, const int* inv, int64_t nl,
+                                                 const double* lm_pos, double* map_pose, double* map_pos) {
+    if (dyn[kDynStatus]) return;
+    const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (i < nk) {
+        const double* src = kf_pose + (size_t)(*iters & 1) * nk * 8 + 8 * i;
+        for (int j = 0; j < 7; ++j) map_pose[7 * (int64_t)win[i] + j] = src[j];
+    }
+    if (i < nl && i < dyn[kDynNOpt])
+        for (int j = 0; j < 3; ++j) map_pos[3 * (int64_t)inv[i] + j] = lm_pos[4 * i + j];
+}
+
+// grow-only with headroom (the map grows every keyframe: no hipFree / hipMalloc per call)
+hipError_t grow(DevBuf& d, size_t want) {
+    if (want <= d.bytes) return hipSuccess;
+    size_t cap = 4096;
+    while (cap < want) cap += cap / 2;
+    return d.ensure(cap);
+}
+
+template <class T>
+int scan_ex(vx_ctx* c, DevBuf& tmp, const T* in, T* out, int64_t n) {  // n + 1 outputs
+    size_t bytes = 0;
+    VX_HIP(c, rocprim::exclusive_scan(nullptr, bytes, in, out, T(0), (size_t)n + 1, rocprim::plus<T>(), c->stream));
+    VX_HIP(c, grow(tmp, std::max<size_t>(bytes, 16)));
+    VX_HIP(c, rocprim::exclusive_scan(tmp.p, bytes, in, out, T(0), (size_t)n + 1, rocprim::plus<T>(), c->stream));
+    return VX_OK;
+}
+
+// the resident id table covers rows [0, n_lm): new rows added, rebuilt when it has to grow
+int ht_sync(vx_ctx* c, vx_dmap* m) {
+    const int64_t nl = m->n_lm;
+    unsigned need = 1024;
+    while ((int64_t)need < 2 * std::max<int64_t>(nl, 1)) need <<= 1;
+    int64_t r0 = m->ht_rows;
+    if (need > m->ht_cap) {
+        unsigned cap = need;
+        if (cap < 4 * (unsigned)std::max<int64_t>(nl, 1) && cap < (1u << 30)) cap <<= 1;  // room for growth
+        VX_HIP(c, m->ht_key.ensure((size_t)cap * 8));
+        VX_HIP(c, m->ht_val.ensure((size_t)cap * 4));
+        m->ht_cap = cap;
+        hipLaunchKernelGGL(k_ht_clear, dim3(grid(cap)), dim3(kT), 0, c->stream, m->ht_key.as<uint64_t>(), cap);
+        r0 = 0;
+    }
+    if (nl > r0)
+        hipLaunchKernelGGL(k_ht_add, dim3(grid(nl - r0)), dim3(kT), 0, c->stream, m->ht_key.as<uint64_t>(),
+                           m->ht_val.as<int>(), m->ht_cap - 1, (const uint64_t*)m->lm_id.as<uint64_t>(),
+                           (const uint8_t*)m->lm_bad.as<uint8_t>(), r0, nl);
+    VX_LAUNCH_CHECK(c, "landmark id table");
+    m->ht_rows = nl;
+    return VX_OK;
+}
+
+}  // namespace
+
+// SelectKeyFrames over the resident keyframes (ba_window.hip)
+std::vector<int> dmap_select_window(const vx_dmap* m, uint64_t ref_kf_id, int has_ref, int window_size);
+
+// The lean build + run + apply; returns VX_ERR_STATE (*fallback = true) for a window it does not take
+// (more than 255 keyframes, a landmark-stage grid beyond the LDS-pose kernels' range).
+int lean_optimize(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_options& o, vx_ba_stats* st,
+                  bool* fallback) {
+    *fallback = false;
+    auto& L = m->lean;
+    L.nk = 0;
+    L.status = 1;
+    L.ran = false;
+    L.win_rows.clear();
+    vx_ba_stats s{};
+    s.gate_margin = -1.0;
+    s.status = 1;
+    const int n_kf = (int)m->kf_id.size();
+    std::vector<int> win = n_kf > 0 ? dmap_select_window(m, ref, has_ref, o.window_size) : std::vector<int>{};
+    const int nk = (int)win.size();
+    s.n_window_kf = nk;
+    if (nk < 2) {  // local_ba.cpp:73-75
+        L.ran = true;
+        if (st) *st = s;
+        return VX_OK;
+    }
+    const int q = kBaLmBlock - nk;
+    // capacities the host knows: window features, has_landmark features (>= landmark-stage
+    // observations and >= optimised landmarks), map rows, observation rows
+    std::vector<int> wptr(nk + 1, 0);
+    std::vector<int64_t> src(nk);
+    std::vector<uint64_t> wid(nk);
+    std::vector<uint8_t> cam(nk);
+    int64_t nvalid = 0, mx = 0;
+    for (int r = 0; r < nk; ++r) {
+        const int k = win[r];
+        src[r] = m->kf_feat_ptr[k];
+        wptr[r + 1] = wptr[r] + (int)(m->kf_feat_ptr[k + 1] - m->kf_feat_ptr[k]);
+        wid[r] = m->kf_id[k];
+        cam[r] = m->kf_has_cam[k];
+        nvalid += m->kf_valid_cnt[k];
+        if (cam[r]) mx = std::max<int64_t>(mx, m->kf_valid_cnt[k]);
+    }
+    const int nf = wptr[nk];
+    const int64_t nl = m->n_lm, nobs = m->n_obs;
+    const int cap_blocks = (int)((2 * nvalid + q - 1) / q) + 1;
+    if (nk > 255 || cap_blocks > 480 || (int64_t)nk * cap_blocks > 80000 || nl >= INT_MAX / 2) {
+        *fallback = true;
+        return VX_ERR_STATE;
+    }
+    const int n_split = ba_split(mx, 1);
+    const int mw = (nk + 63) / 64;
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = ht_sync(c, m))) return rc;
+    // window tables: one pinned block, one upload
+    const size_t o_src = 0, o_wid = o_src + 8 * (size_t)nk, o_wptr = o_wid + 8 * (size_t)nk,
+                 o_win = o_wptr + 4 * ((size_t)nk + 2), o_cam = o_win + 4 * ((size_t)nk + 2), o_end = o_cam + (size_t)nk + 8;
+    VX_HIP(c, L.win_host.ensure(o_end, true));
+    VX_HIP(c, grow(L.win, o_end));
+    {
+        uint8_t* H = static_cast<uint8_t*>(L.win_host.p);
+        std::memcpy(H + o_src, src.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_wid, wid.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_wptr, wptr.data(), 4 * ((size_t)nk + 1));
+        std::memcpy(H + o_win, win.data(), 4 * (size_t)nk);
+        std::memcpy(H + o_cam, cam.data(), (size_t)nk);
+    }
+    VX_HIP(c, hipMemcpyAsync(L.win.p, L.win_host.p, o_end, hipMemcpyHostToDevice, c->stream));
+    const size_t fN = (size_t)nf + 1, lN = (size_t)nl + 1, kN = (size_t)nk + 1;
+    for (DevBuf* d : {&L.f_l, &L.f_code, &L.f_pv, &L.f_back, &L.pscan, &L.plm, &L.lkf, &L.llm}) VX_HIP(c, grow(*d, fN * 4));
+    for (DevBuf* d : {&L.wuv, &L.puv, &L.luv}) VX_HIP(c, grow(*d, fN * 16));
+    for (DevBuf* d : {&L.l_ref, &L.l_pv, &L.l_cnt, &L.l_slot, &L.inv, &L.cnt, &L.lobs_ptr}) VX_HIP(c, grow(*d, lN * 4));
+    for (DevBuf* d : {&L.key, &L.ex}) VX_HIP(c, grow(*d, lN * 8));
+    VX_HIP(c, grow(L.mask, lN * mw * 8));
+    VX_HIP(c, grow(L.lm_pos0, lN * 32));
+    VX_HIP(c, grow(L.lm_pos, lN * 32));
+    VX_HIP(c, grow(L.lm_blk, (size_t)(cap_blocks + 2) * 8));
+    VX_HIP(c, grow(L.kf_pose0, kN * 64));
+    VX_HIP(c, grow(L.kf_pose, kN * 128));
+    VX_HIP(c, grow(L.kf_intr, kN * 32));
+    VX_HIP(c, grow(L.kf_rot, kN * 72));
+    VX_HIP(c, grow(L.kf_flags, kN * 4));
+    VX_HIP(c, grow(L.kf_obs_ptr, kN * 4));
+    VX_HIP(c, grow(L.kf_part, kN * n_split * kBaStrideDoubles * 8));
+    VX_HIP(c, grow(L.kf_cost, kN * 16));
+    VX_HIP(c, grow(L.state, ba_state_bytes()));
+    VX_HIP(c, grow(L.dyn, kDynInts * 4));
+
+    uint8_t* WD = L.win.as<uint8_t>();
+    LeanArgs a{};
+    a.nk = nk;
+    a.nf = nf;
+    a.mw = mw;
+    a.src = reinterpret_cast<const int64_t*>(WD + o_src);
+    a.wid = reinterpret_cast<const uint64_t*>(WD + o_wid);
+    a.wptr = reinterpret_cast<const int*>(WD + o_wptr);
+    a.win = reinterpret_cast<const int*>(WD + o_win);
+    a.cam = WD + o_cam;
+    a.nl = nl;
+    a.nobs = nobs;
+    a.feat_uv = m->feat_uv.as<double>();
+    a.feat_lm = m->feat_lm.as<uint64_t>();
+    a.feat_fl = m->feat_fl.as<uint8_t>();
+    a.lm_id = m->lm_id.as<uint64_t>();
+    a.lm_bad = m->lm_bad.as<uint8_t>();
+    a.lm_pos = m->lm_pos.as<double>();
+    a.obs_lm = m->obs_lm.as<int>();
+    a.obs_kf = m->obs_kf.as<uint64_t>();
+    a.obs_fi = m->obs_fi.as<uint64_t>();
+    a.map_pose = m->kf_pose.as<double>();
+    a.map_intr = m->kf_intr.as<double>();
+    a.ht_key = m->ht_key.as<uint64_t>();
+    a.ht_val = m->ht_val.as<int>();
+    a.ht_mask = m->ht_cap - 1;
+    a.min_point = o.min_point_observations;
+    a.f_l = L.f_l.as<int>();
+    a.f_code = L.f_code.as<int>();
+    a.f_pv = L.f_pv.as<int>();
+    a.f_back = L.f_back.as<int>();
+    a.wuv = L.wuv.as<double2>();
+    a.l_ref = L.l_ref.as<int>();
+    a.l_pv = L.l_pv.as<int>();
+    a.l_cnt = L.l_cnt.as<int>();
+    a.key = L.key.as<unsigned long long>();
+    a.ex = L.ex.as<unsigned long long>();
+    a.l_slot = L.l_slot.as<int>();
+    a.inv = L.inv.as<int>();
+    a.cnt = L.cnt.as<int>();
+    a.mask = L.mask.as<unsigned long long>();
+    a.pscan = L.pscan.as<int>();
+    a.lobs_ptr = L.lobs_ptr.as<int>();
+    a.lm_pos0 = L.lm_pos0.as<double>();
+    a.puv = L.puv.as<double2>();
+    a.plm = L.plm.as<int>();
+    a.kf_obs_ptr = L.kf_obs_ptr.as<int>();
+    a.lkf = L.lkf.as<int>();
+    a.llm = L.llm.as<int>();
+    a.luv = L.luv.as<double2>();
+    a.lm_blk = L.lm_blk.as<int>();
+    a.kf_pose0 = L.kf_pose0.as<double>();
+    a.kf_intr = L.kf_intr.as<double>();
+    a.kf_flags = L.kf_flags.as<int>();
+    a.dyn = L.dyn.as<int>();
+    a.q = q;
+    hipStream_t sm = c->stream;
+    const long long n_big = std::max<long long>((long long)nl + 1, kDynInts);
+    hipLaunchKernelGGL(k_lb_clear, dim3(grid(n_big)), dim3(kT), 0, sm, a);
+    hipLaunchKernelGGL(k_lb_feat, dim3(grid(std::max<long long>(nf + 1, nk))), dim3(kT), 0, sm, a);
+    if (nobs) hipLaunchKernelGGL(k_lb_obs, dim3(grid(nobs)), dim3(kT), 0, sm, a);
+    hipLaunchKernelGGL(k_lb_flags, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: features / observations / flags");
+    if ((rc = scan_ex<unsigned long long>(c, L.tmp, a.key, L.ex.as<unsigned long long>(), nl))) return rc;
+    hipLaunchKernelGGL(k_lb_slots, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    if ((rc = scan_ex<int>(c, L.tmp, a.f_pv, L.pscan.as<int>(), nf))) return rc;
+    hipLaunchKernelGGL(k_lb_pose, dim3(grid(std::max<long long>(nf, nk + 1))), dim3(kT), 0, sm, a);
+    hipLaunchKernelGGL(k_lb_lcount, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: slots / pose CSR / counts");
+    if ((rc = scan_ex<int>(c, L.tmp, a.cnt, L.lobs_ptr.as<int>(), nl))) return rc;
+    hipLaunchKernelGGL(k_lb_lfill, dim3(grid(std::max<long long>(nf, nl))), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: landmark-stage CSR");
+
+    DynPlan d;
+    d.n_kf = nk;
+    d.n_split = n_split;
+    d.grid_blocks = cap_blocks;
+    d.opt = o;
+    d.kf_pose0 = a.kf_pose0;
+    d.kf_pose = L.kf_pose.as<double>();
+    d.kf_intr = a.kf_intr;
+    d.kf_rot = L.kf_rot.as<double>();
+    d.kf_flags = a.kf_flags;
+    d.kf_obs_ptr = a.kf_obs_ptr;
+    d.kf_part = L.kf_part.as<double>();
+    d.kf_cost = L.kf_cost.as<double>();
+    d.lm_pos0 = a.lm_pos0;
+    d.lm_pos = L.lm_pos.as<double>();
+    d.pobs_uv = a.puv;
+    d.pobs_lm = a.plm;
+    d.lobs_ptr = a.lobs_ptr;
+    d.lobs_kf = a.lkf;
+    d.lobs_lm = a.llm;
+    d.lm_blk = a.lm_blk;
+    d.lobs_uv = a.luv;
+    d.state = L.state.p;
+    d.dyn = a.dyn;
+    if (o.max_iterations > 0) {
+        if ((rc = ba_run_dyn(c, d))) return rc;
+        // (the apply takes the last iteration's pose buffer from BAState::iterations on the device)
+        const int* iters = reinterpret_cast<const int*>(static_cast<const uint8_t*>(L.state.p) + ba_state_iter_offset());
+        hipLaunchKernelGGL(k_lb_apply, dim3(grid(std::max<long long>(nk, nl))), dim3(kT), 0, sm, (const int*)a.dyn,
+                           iters, nk, a.win, (const double*)L.kf_pose.as<double>(), (const int*)a.inv, nl,
+                           (const double*)L.lm_pos.as<double>(), m->kf_pose.as<double>(), m->lm_pos.as<double>());
+        VX_LAUNCH_CHECK(c, "k_lb_apply");
+    }
+    // the end: the header (and the iteration state) back — the call's only synchronisation
+    const size_t sb = ba_state_bytes();
+    VX_HIP(c, L.rb_host.ensure(kDynInts * 4 + sb));
+    int* H = static_cast<int*>(L.rb_host.p);
+    VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
+    if (o.max_iterations > 0) VX_HIP(c, hipMemcpyAsync(H + kDynInts, L.state.p, sb, hipMemcpyDeviceToHost, sm));
+    VX_HIP(c, hipStreamSynchronize(sm));
+    s.status = H[kDynStatus];
+    s.n_landmarks = H[kDynGlobal];
+    // (with no optimisable landmark no kernel of the run touched the state: iterations stay 0)
+    if (s.status == 0 && o.max_iterations > 0) ba_state_to_stats(H + kDynInts, &s);
+    L.nk = nk;
+    L.status = s.status;
+    L.n_opt = H[kDynNOpt];
+    L.iterations = s.iterations;
+    L.win_rows = std::move(win);
+    L.ran = true;
+    if (st) *st = s;
+    return VX_OK;
+}
+
+}  // namespace vx
+
+vx_dmap::~vx_dmap() {
+    if (lean.fallback) vx_ba_plan_destroy(lean.fallback);
+}
+
+using namespace vx;
+
+extern "C" {
+
+int vx_ba_optimize_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_options* opt, vx_ba_stats* st) {
+    if (!c || !m || !opt || m->c != c)
+        return c ? set_error(c, VX_ERR_INVALID, "vx_ba_optimize_dmap: bad arguments") : VX_ERR_INVALID;
+    if (opt->max_iterations < 0 || opt->max_iterations > 64)
+        return set_error(c, VX_ERR_INVALID, "max_iterations must be in [0, 64]");
+    auto& L = m->lean;
+    if (L.fallback) {
+        vx_ba_plan_destroy(L.fallback);
+        L.fallback = nullptr;
+    }
+    L.ran = false;
+    // $VX_LEAN=0: always the general build (ba_window.hip), for A/B runs
+    const char* e = getenv("VX_LEAN");
+    bool fb = e && e[0] == '0';
+    if (!fb) {
+        const int rc = lean_optimize(c, m, ref, has_ref, *opt, st, &fb);
+        if (!fb) return rc;
+    }
+    // a window the lean build does not take: plan from the resident map, run, scatter
+    vx_ba_plan* p = nullptr;
+    int rc = vx_ba_plan_create_dmap(c, m, ref, has_ref, opt, 0, 1, &p);
+    if (rc) return rc;
+    rc = vx_ba_plan_run_async(c, p);
+    if (!rc) rc = vx_ba_plan_apply_dmap(c, p, m);
+    vx_ba_stats s{};
+    if (!rc) rc = vx_ba_plan_fetch(c, p, nullptr, &s);
+    if (rc) {
+        vx_ba_plan_destroy(p);
+        return rc;
+    }
+    L.fallback = p;
+    L.nk = s.status == 0 ? (int)p->kf_map_idx.size() : 0;
+    L.status = s.status;
+    L.n_opt = s.status == 0 ? p->n_opt : 0;
+    L.iterations = s.iterations;
+    L.win_rows = p->kf_map_idx;
+    L.ran = true;
+    if (st) *st = s;
+    return VX_OK;
+}
+
+int vx_ba_dmap_results(vx_ctx* c, vx_dmap* m, int cap_kf, int64_t* kf_rows, double* kf_pose7, int cap_lm,
+                       int64_t* lm_rows, double* lm_pos3, int* n_kf, int* n_lm) {
+    if (!c || !m || m->c != c || !n_kf || !n_lm) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_dmap_results: bad arguments") : VX_ERR_INVALID;
+    auto& L = m->lean;
+    if (!L.ran) return set_error(c, VX_ERR_STATE, "no vx_ba_optimize_dmap to report");
+    const bool changed = L.status == 0 && L.iterations > 0;
+    *n_kf = changed ? L.nk : 0;
+    *n_lm = changed ? L.n_opt : 0;
+    if (!changed) return VX_OK;
+    if (cap_kf < *n_kf || cap_lm < *n_lm) return set_error(c, VX_ERR_CAPACITY, "need %d keyframes / %d landmarks", *n_kf, *n_lm);
+    VX_HIP(c, hipSetDevice(c->device));
+    const int nk = L.nk, n = L.n_opt;
+    std::vector<double> pose((size_t)nk * 8), pos((size_t)std::max(n, 1) * 4);
+    std::vector<int> rows(std::max(n, 1));
+    const double* dpose;
+    const double* dpos;
+    if (L.fallback) {
+        vx_ba_plan* p = L.fallback;
+        dpose = p->kf_pose.as<double>() + (size_t)(L.iterations & 1) * nk * 8;
+        dpos = p->lm_pos.as<double>();
+        std::copy(p->lm_map_idx.begin(), p->lm_map_idx.begin() + n, rows.begin());
+    } else {
+        dpose = L.kf_pose.as<double>() + (size_t)(L.iterations & 1) * nk * 8;
+        dpos = L.lm_pos.as<double>();
+        if (n) VX_HIP(c, hipMemcpyAsync(rows.data(), L.inv.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    VX_HIP(c, hipMemcpyAsync(pose.data(), dpose, pose.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    if (n) VX_HIP(c, hipMemcpyAsync(pos.data(), dpos, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    for (int r = 0; r < nk; ++r) {
+        if (kf_rows) kf_rows[r] = L.win_rows[r];
+        if (kf_pose7)
+            for (int j = 0; j < 7; ++j) kf_pose7[7 * r + j] = pose[8 * (size_t)r + j];
+    }
+    for (int i = 0; i < n; ++i) {
+        if (lm_rows) lm_rows[i] = rows[i];
+        if (lm_pos3)
+            for (int j = 0; j < 3; ++j) lm_pos3[3 * (size_t)i + j] = pos[4 * (size_t)i + j];
+    }
+    return VX_OK;
+}
+
+}  // extern "C"

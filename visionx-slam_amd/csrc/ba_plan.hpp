@@ -146,4 +146,41 @@ int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_b
 // greedy k_landmark_solve workgroup packing over the landmark-stage CSR pointers: {first landmark,
 // first observation} per workgroup, n_blocks + 1 pairs; *max_cnt = most observations of one landmark
 std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt, int* max_cnt);
+
+// ---- lean resident LocalBA (ba_lean.hip, vx_ba_optimize_dmap): a plan whose counts stay on the
+// device.  dyn[] holds what the build finds out: optimisable landmarks (slots [0, n_opt)), table
+// size n_lm, landmark-stage workgroups, status (1: nothing to optimise), pose- and landmark-stage
+// observations, optimisable landmarks over all shards, most landmark-stage observations of one
+// landmark, fixed landmarks.
+enum : int { kDynNOpt = 0, kDynNLm, kDynBlocks, kDynStatus, kDynPoseObs, kDynLmObs, kDynGlobal, kDynMaxObs,
+             kDynNFixed, kDynInts = 16 };
+struct DynPlan {
+    int n_kf = 0, n_split = 1, grid_blocks = 0;
+    vx_ba_options opt{};
+    const double* kf_pose0 = nullptr;
+    double* kf_pose = nullptr;
+    const double* kf_intr = nullptr;
+    double* kf_rot = nullptr;
+    const int* kf_flags = nullptr;
+    const int* kf_obs_ptr = nullptr;
+    double* kf_part = nullptr;
+    double* kf_cost = nullptr;
+    const double* lm_pos0 = nullptr;
+    double* lm_pos = nullptr;
+    const double2* pobs_uv = nullptr;
+    const int* pobs_lm = nullptr;
+    const int* lobs_ptr = nullptr;
+    const int* lobs_kf = nullptr;
+    const int* lobs_lm = nullptr;
+    const int* lm_blk = nullptr;
+    const double2* lobs_uv = nullptr;
+    void* state = nullptr;
+    const int* dyn = nullptr;
+};
+int ba_run_dyn(vx_ctx* c, const DynPlan& d);
+size_t ba_state_bytes();
+size_t ba_state_iter_offset();  // byte offset of BAState::iterations (the run's last iteration count)
+// a host copy of BAState -> the stats' iterations / cost / obs
+void ba_state_to_stats(const void* host_state, vx_ba_stats* s);
+constexpr int kBaStrideDoubles = 32;  // (= kBaStride: doubles per pose-stage partial block)
 }  // namespace vx

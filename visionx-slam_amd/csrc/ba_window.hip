@@ -614,6 +614,10 @@ __global__ void k_gather_kf(int nk, const int* win, const double* pose, const do
 }
 }  // namespace
 
+std::vector<int> dmap_select_window(const vx_dmap* m, uint64_t ref_kf_id, int has_ref, int window_size) {
+    return select_ids(m->kf_id.data(), (int)m->kf_id.size(), ref_kf_id, has_ref, window_size, m->kf_alive.data());
+}
+
 int build_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref_kf_id, int has_ref, vx_ba_plan* p) {
     const vx_ba_options& o = p->opt;
     p->status = 1;

@@ -43,6 +43,25 @@ struct vx_dmap {
     // rebuilt lazily when landmarks or observations were added since the last plan build
     bool csr_dirty = true;
     vx::DevBuf optr, okf, ofi, sort_keys, sort_keys2, sort_vals, sort_vals2, tmp, cnt;
+    // landmark id -> row, open addressing on the device (ba_lean.hip): rows [0, ht_rows) inserted,
+    // kept across calls (a removed landmark's row stays, its lm_bad says so); rebuilt when it grows
+    vx::DevBuf ht_key, ht_val;
+    unsigned ht_cap = 0;
+    int64_t ht_rows = 0;
+    // the lean one-call LocalBA (vx_ba_optimize_dmap): its device buffers, sized by capacity and
+    // reused call after call, and the window of its last call (for vx_ba_dmap_results)
+    struct Lean {
+        vx::DevBuf win, f_l, f_code, f_pv, f_back, pscan, wuv, l_ref, l_pv, l_cnt, key, ex, l_slot, inv, cnt, mask,
+            lobs_ptr, lm_pos0, lm_pos, puv, plm, lkf, llm, luv, lm_blk, kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags,
+            kf_obs_ptr, kf_part, kf_cost, state, dyn, tmp;
+        vx::PinnedBuf win_host, rb_host;
+        int nk = 0;                        // window of the last call (0: none)
+        int status = 1, n_opt = 0, iterations = 0;
+        std::vector<int> win_rows;         // its keyframe rows
+        bool ran = false;
+        vx_ba_plan* fallback = nullptr;    // the last call's plan when it took the general build
+    } lean;
+    ~vx_dmap();
 };
 
 namespace vx {

@@ -4,7 +4,8 @@
 //   FeatureMatcher    core/feature/feature_matcher.h:7-13      (virtual int Match(last, curr, matches))
 //   ORBExtractor      core/feature/orb_extractor.h:9-19        -> vx_orb_extract (include/vx_slam.h)
 //   ORBMatcher        core/feature/orb_matcher.h:11-26         -> vx_match_knn2_ratio
-//   LocalBA           core/backend/local_ba.h:10-27            -> vx_ba_optimize_map
+//   LocalBA           core/backend/local_ba.h:10-27            -> vx_ba_optimize_map (snapshot) or
+//                                                               vx_ba_optimize_dmap (DeviceMap attached)
 //
 // Same class names, constructor defaults and member signatures as the reference, so
 // core/system/system.cpp:15-16 and core/frontend/tracking.cpp:25-34 compile against them
@@ -90,6 +91,8 @@ struct FlatMap {
     vx_map_view view();                    // pointers into the vectors above
 };
 
+class DeviceMap;
+
 class LocalBA {
 public:
     struct Options {
@@ -102,6 +105,11 @@ public:
     };
     explicit LocalBA(const Options& options) : options_(options) {}
     void Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf);
+    // Resident mode: with a DeviceMap attached (one that mirrors `map`, device_map.h), Optimize is one
+    // vx_ba_optimize_dmap call on the resident map — no Flatten, no snapshot upload — and then
+    // writes the window poses and optimised positions back into the Frame / Landmark objects
+    // (Frame::SetPose / Landmark::SetPosition, local_ba.cpp:173,237).  nullptr: the snapshot path.
+    void UseDeviceMap(std::shared_ptr<DeviceMap> dm) { dmap_ = std::move(dm); }
 
     // The keyframes SelectKeyFrames picks (local_ba.cpp:42-62), every landmark their features
     // reference, and those landmarks' full observation maps.
@@ -109,8 +117,13 @@ public:
     const vx_ba_stats& LastStats() const { return stats_; }
 
 private:
+    vx_ba_options VxOptions() const;
+    void OptimizeResident(const Frame::Ptr& ref_kf);
     Options options_;
     vx_ba_stats stats_{};
+    std::shared_ptr<DeviceMap> dmap_;
+    std::vector<int64_t> kf_rows_, lm_rows_;
+    std::vector<double> kf_out_, lm_out_;
 };
 
 namespace vxhost {

@@ -1,6 +1,8 @@
 // feature.cpp — ORBExtractor / ORBMatcher / LocalBA adapters over the C ABI (see feature.h).
 #include "visionx/feature.h"
 
+#include "visionx/device_map.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -267,12 +269,7 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
     return f;
 }
 
-void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
-    stats_ = vx_ba_stats{};
-    stats_.status = 1;
-    if (!map) return;                                            // local_ba.cpp:67-69
-    FlatMap f = Flatten(*map, ref_kf, options_.window_size);
-    if (f.frames.size() < 2) return;                            // local_ba.cpp:73-75
+vx_ba_options LocalBA::VxOptions() const {
     vx_ba_options o;
     o.window_size = options_.window_size;
     o.max_iterations = options_.max_iterations;
@@ -280,6 +277,52 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
     o.min_point_observations = options_.min_point_observations;
     o.huber_delta = options_.huber_delta;
     o.max_reproj_error = options_.max_reproj_error;
+    return o;
+}
+
+void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
+    DeviceMap& dm = *dmap_;
+    dm.Flush();
+    vx_ctx* c = dm.context();
+    const vx_ba_options o = VxOptions();
+    check(c, vx_ba_optimize_dmap(c, dm.handle(), ref_kf ? ref_kf->Id() : 0, ref_kf ? 1 : 0, &o, &stats_),
+          "vx_ba_optimize_dmap");
+    int nk = 0, nl = 0;
+    int rc = vx_ba_dmap_results(c, dm.handle(), (int)kf_rows_.size(), kf_rows_.data(), kf_out_.data(),
+                                (int)lm_rows_.size(), lm_rows_.data(), lm_out_.data(), &nk, &nl);
+    if (rc == VX_ERR_CAPACITY) {  // (the buffers keep the largest window seen)
+        kf_rows_.resize(nk);
+        kf_out_.resize(7 * (size_t)nk);
+        lm_rows_.resize(nl);
+        lm_out_.resize(3 * (size_t)nl);
+        rc = vx_ba_dmap_results(c, dm.handle(), nk, kf_rows_.data(), kf_out_.data(), nl, lm_rows_.data(),
+                                lm_out_.data(), &nk, &nl);
+    }
+    check(c, rc, "vx_ba_dmap_results");
+    // Frame::SetPose / Landmark::SetPosition (local_ba.cpp:173,237) on the host objects
+    for (int i = 0; i < nk; ++i) {
+        const double* p = &kf_out_[7 * (size_t)i];
+        SE3d T;
+        T.qx = p[0]; T.qy = p[1]; T.qz = p[2]; T.qw = p[3];
+        T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
+        if (auto fr = dm.FrameAt(kf_rows_[i])) fr->SetPose(T);
+    }
+    for (int i = 0; i < nl; ++i)
+        if (auto lm = dm.LandmarkAt(lm_rows_[i]))
+            lm->SetPosition(Vec3d(lm_out_[3 * (size_t)i], lm_out_[3 * (size_t)i + 1], lm_out_[3 * (size_t)i + 2]));
+}
+
+void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
+    stats_ = vx_ba_stats{};
+    stats_.status = 1;
+    if (!map) return;                                            // local_ba.cpp:67-69
+    if (dmap_) {
+        OptimizeResident(ref_kf);
+        return;
+    }
+    FlatMap f = Flatten(*map, ref_kf, options_.window_size);
+    if (f.frames.size() < 2) return;                            // local_ba.cpp:73-75
+    const vx_ba_options o = VxOptions();
     vx_map_view v = f.view();
     vx_ctx* c = vxhost::ThreadContext();
     check(c, vx_ba_optimize_map(c, &v, ref_kf ? ref_kf->Id() : 0, ref_kf ? 1 : 0, &o, &stats_), "vx_ba_optimize_map");

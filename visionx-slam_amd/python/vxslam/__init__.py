@@ -90,7 +90,9 @@ EXPORTS = [
     "vx_dmap_create", "vx_dmap_add_keyframe", "vx_dmap_add_landmarks", "vx_dmap_add_observations",
     "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
-    "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run",
+    "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run", "vx_ba_optimize_dmap",
+    "vx_ba_dmap_results", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
+    "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
     "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
     "vx_orb_get_order", "vx_orb_set_debug", "vx_orb_debug_read", "vx_test_retain_best",
@@ -160,6 +162,17 @@ def lib():
         L.vx_sba_default_options.restype = None
         L.vx_pnp_default_options.restype = None
         L.vx_essential_default_options.restype = None
+        L.vx_seq_destroy.argtypes = [C.c_void_p]
+        L.vx_seq_destroy.restype = None
+        for f in ("vx_seq_wait", "vx_seq_record"):
+            getattr(L, f).argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.vx_seq_extract.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                     C.c_int64, C.c_int]
+        L.vx_seq_match.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                   C.c_int, C.c_float]
+        L.vx_seq_ba_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.vx_seq_length.argtypes = [C.c_void_p]
+        L.vx_seq_run.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
         L.vx_ba_shard_of.restype = C.c_uint32
         L.vx_ba_shard_of.argtypes = [C.c_uint64, C.c_int]
         _lib = L
@@ -741,6 +754,60 @@ class BAPlan:
             pass
 
 
+class Seq:
+    """vx_seq: a recorded list of async calls replayed from C by run() (include/vx_slam.h)."""
+
+    def __init__(self):
+        self._h = C.c_void_p()
+        if lib().vx_seq_create(C.byref(self._h)) != VX_OK:
+            raise VxError(VX_ERR_INVALID, "vx_seq_create failed")
+        self._ctxs = {}
+
+    def _add(self, rc, ctx):
+        if rc != VX_OK:
+            raise VxError(rc, "vx_seq: bad arguments")
+        self._ctxs[len(self)] = ctx
+
+    def wait(self, ctx, ev):
+        self._add(lib().vx_seq_wait(self._h, ctx.handle, ev._h), ctx)
+
+    def record(self, ctx, ev):
+        self._add(lib().vx_seq_record(self._h, ctx.handle, ev._h), ctx)
+
+    def extract(self, ctx, params, d_img, w, h, ch, stride, slot):
+        self._add(lib().vx_seq_extract(self._h, ctx.handle, C.byref(params), C.c_void_p(d_img), w, h, ch, stride, slot),
+                  ctx)
+
+    def match(self, ctx, q, t, ratio=0.8):
+        """q / t: (desc, count, cap) device triples (Context.slot_device)."""
+        self._add(lib().vx_seq_match(self._h, ctx.handle, C.c_void_p(q[0]), C.c_void_p(q[1]), q[2], C.c_void_p(t[0]),
+                                     C.c_void_p(t[1]), t[2], C.c_float(ratio)), ctx)
+
+    def ba_run(self, ctx, plan):
+        self._add(lib().vx_seq_ba_run(self._h, ctx.handle, plan._h), ctx)
+
+    def __len__(self):
+        return lib().vx_seq_length(self._h)
+
+    def run(self):
+        bad = C.c_int(-1)
+        rc = lib().vx_seq_run(self._h, C.byref(bad))
+        if rc != VX_OK:
+            ctx = self._ctxs.get(bad.value + 1)
+            raise VxError(rc, f"vx_seq_run: call {bad.value}: " + (lib().vx_last_error(ctx.handle).decode() if ctx else ""))
+
+    def close(self):
+        if self._h:
+            lib().vx_seq_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class DMap:
     """vx_dmap: visionx::Map resident on the device, updated incrementally (include/vx_slam.h)."""
 
@@ -833,6 +900,29 @@ class DMap:
                                                      0 if ref_kf_id is None else 1, C.byref(opts), shard_rank,
                                                      shard_count, C.byref(plan._h)))
         return plan
+
+    def optimize(self, opts, ref_kf_id=None) -> BAStats:
+        """vx_ba_optimize_dmap: LocalBA::Optimize on the resident map in one call (plan, run and the
+        scatter into the map; synchronises once, at its end)."""
+        st = BAStats()
+        self.ctx._check(lib().vx_ba_optimize_dmap(self.ctx.handle, self._h,
+                                                  C.c_uint64(0 if ref_kf_id is None else int(ref_kf_id)),
+                                                  0 if ref_kf_id is None else 1, C.byref(opts), C.byref(st)))
+        return st
+
+    def results(self):
+        """vx_ba_dmap_results: (keyframe rows, their poses (n, 7), landmark rows, positions (n, 3)) the
+        last optimize() changed."""
+        nk, nl = C.c_int(0), C.c_int(0)
+        rc = lib().vx_ba_dmap_results(self.ctx.handle, self._h, 0, None, None, 0, None, None, C.byref(nk),
+                                      C.byref(nl))
+        if rc not in (VX_OK, VX_ERR_CAPACITY):
+            self.ctx._check(rc)
+        kr, kp = np.zeros(max(nk.value, 1), np.int64), np.zeros((max(nk.value, 1), 7))
+        lr, lp = np.zeros(max(nl.value, 1), np.int64), np.zeros((max(nl.value, 1), 3))
+        self.ctx._check(lib().vx_ba_dmap_results(self.ctx.handle, self._h, len(kr), _p(kr), _p(kp), len(lr), _p(lr),
+                                                 _p(lp), C.byref(nk), C.byref(nl)))
+        return kr[:nk.value], kp[:nk.value], lr[:nl.value], lp[:nl.value]
 
     def close(self):
         if self._h:
