@@ -103,3 +103,27 @@ def test_sba_plan_is_repeatable(ctx):
         assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
     info = plan.info()
     assert info["n_kf"] == 20 and info["n_comp"] == 1 and info["n_pairs"] > 0
+
+
+def test_sba_connected_c5(ctx, oracle):
+    """BASELINE configs[4] as one rig: the 8 cameras sit on one body and 3 % of the landmarks lie in
+    the field of view neighbouring cameras share (synth cross_frac), so the 200-keyframe / 100k-landmark
+    window is ONE covisibility component — 198 free keyframes, a 1188 x 1188 dense pose system (padded
+    to 1200, 75 x 75 tiles) factored by k_sba_solve's MFMA tiles — against the restatement."""
+    import vxslam
+
+    m = synth.make_ba_map(0x5EED00C5, 200, 100000, n_streams=8, n_old_kf=16, cross_frac=0.03)
+    plan = ctx.sba_plan(m, vxslam.default_sba_options(window=200, iters=1))
+    info = plan.info()
+    plan.close()
+    assert info["n_kf"] == 200 and info["n_comp"] == 1 and info["n"] == 6 * 200
+    st_g, st_c = _case(ctx, oracle, m, dict(window=200, iters=5))
+    assert st_g.status == 0 and st_g.accepted >= 2 and st_g.final_cost < 0.2 * st_g.initial_cost
+
+
+def test_sba_panel_from_global(ctx, oracle, monkeypatch):
+    """Factor steps whose panel does not fit the LDS slots read their tiles from global memory (dense
+    components of several hundred keyframes); forced here with two slots on a 50-keyframe window."""
+    monkeypatch.setenv("VX_SBA_PANEL_SLOTS", "2")
+    m = synth.make_ba_map(0x5EED0032, 50, 12000, n_old_kf=2)
+    _case(ctx, oracle, m, dict(window=50, iters=6))

@@ -57,7 +57,7 @@ constexpr int kBlkThreads = 256;    // k_sba_blocks
 constexpr int kSolveThreads = 256;  // k_sba_solve: 4 waves, one per SIMD (512 registers each: no spills)
 constexpr int kSolveWaves = kSolveThreads / 64;
 constexpr int kUpdThreads = 256;
-constexpr int kMaxCompKf = 128;     // keyframes of one connected component (dense n <= 768)
+constexpr int kMaxCompKf = 448;     // keyframes of one connected component (dense n <= 2688)
 constexpr int kWy = 36;             // doubles per optimised observation: W (6x3) | Y (6x3)
 constexpr int kLmSys = 12;          // doubles per optimised landmark: V^-1 (6) | g_p (3) | pad
 constexpr int kBlkTerms = 50;       // 36 block + 6 rhs + 6 D + cost + count
@@ -131,6 +131,7 @@ struct SBAArgs {
     double* Linv;           // per component: nt x 256, at the component's L offset
     double* dx;             // 6 nk
     SBAState* st;
+    int panel_slots;        // k_sba_solve: LDS panel tiles (a step with more panel tiles reads global)
 };
 
 // ------------------------------------------------------------------------- state selection
@@ -465,6 +466,19 @@ __device__ __forceinline__ d4 mfma_abt(const double* A, const double* B, d4 c, b
     return c;
 }
 
+// The same product with both tiles read in operand order straight from the row-major factor in
+// global memory (ld = np): for the steps whose panel does not fit the LDS slots.
+__device__ __forceinline__ d4 mfma_abt_g(const double* A, const double* B, int ld, d4 c) {
+    const int lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
+    const double4 av = *reinterpret_cast<const double4*>(A + (long long)cl * ld + 4 * r0);
+    const double4 bv = *reinterpret_cast<const double4*>(B + (long long)cl * ld + 4 * r0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.x, bv.x, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.y, bv.y, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.z, bv.z, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f64_16x16x4f64(-av.w, bv.w, c, 0, 0, 0);
+    return c;
+}
+
 // Accumulator layout of v_mfma_f64_16x16x4: lane l, register r -> row (l >> 4) + 4 r, col l & 15.
 __device__ __forceinline__ d4 load_acc(const double* T, int ld) {
     const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
@@ -607,10 +621,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     double* L = a.L + a.comp_loff[comp];
     double* Linv = a.Linv + a.comp_loff[comp];  // same offsets as L (>= 16 np per component)
     const int* tl = a.tl;
-    double* panel = smem;                                       // (nt + 1) operand-order tiles
-    double* dlds = smem + (long long)(nt + 1) * kPanelStride;   // L_kk^-1 of the current step
+    // LDS: the step's panel tiles in slots (position in the column's panel list), L_kk^-1, the POTRF
+    // column images, y / x, and tile row -> panel slot of the current step.  A column with more
+    // panel tiles than slots (dense components of several hundred keyframes) is read from global.
+    const int ps = a.panel_slots;
+    double* panel = smem;                                       // ps operand-order tiles
+    double* dlds = smem + (long long)ps * kPanelStride;         // L_kk^-1 of the current step
     double* lcol = dlds + kPanelStride;                         // POTRF column images (272 doubles)
     double* ys = lcol + 2 * kPanelStride;                       // np: y, then x
+    int* slot_of = reinterpret_cast<int*>(ys + np);             // nt + 1
     const int r0 = lane >> 4, cl = lane & 15;
     // ---- k_sba_blocks wrote the component matrix straight into L (the all-reduce did, sharded);
     // add the damping on the diagonal, the identity on padding rows and the rhs tile row
@@ -639,8 +658,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
         __syncthreads();
         if (kts >= 0) VX_KT(kts);
         // panel: L_ik = A_ik L_kk^-T over the nonzero tiles of column k (and the rhs row)
+        const bool in_lds = pptr[k + 1] - pptr[k] <= ps;
         for (int q = pptr[k] + wv; q < pptr[k + 1]; q += kSolveWaves) {
             const int i = tl[q];
+            const int slot = q - pptr[k];
             double* Aik = L + (long long)(16 * i) * np + 16 * k;
             // the A operand in operand order straight from global: row l & 15, columns 4 (l >> 4) ..
             const double4 av = *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0);
@@ -651,7 +672,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
             c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.z, bv.z, c, 0, 0, 0);
             c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, c, 0, 0, 0);
             store_acc(Aik, np, c);
-            store_acc_opo(panel + (long long)i * kPanelStride, c);
+            if (in_lds) store_acc_opo(panel + (long long)slot * kPanelStride, c);
+            if (lane == 0) slot_of[i] = slot;
         }
         __syncthreads();
         if (kts >= 0) VX_KT(kts + 1);
@@ -674,8 +696,12 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 if (ti[q] < 0) continue;
-                c[q] = mfma_abt(panel + (long long)ti[q] * kPanelStride, panel + (long long)tj[q] * kPanelStride, c[q],
-                                true);
+                if (in_lds)
+                    c[q] = mfma_abt(panel + (long long)slot_of[ti[q]] * kPanelStride,
+                                    panel + (long long)slot_of[tj[q]] * kPanelStride, c[q], true);
+                else
+                    c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * k, L + (long long)(16 * tj[q]) * np + 16 * k,
+                                      np, c[q]);
                 store_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np, c[q]);
             }
         }
@@ -808,6 +834,7 @@ struct vx_sba_plan {
     int nk = 0, n_opt = 0, n_lm = 0, n_oo = 0, n_obs = 0;
     int64_t n_pairs = 0;
     int n_blocks = 0, n_lm_blocks = 0, n_comp = 0, max_np = 0;
+    int max_panel = 1;  // most panel tiles (rhs row included) of one column of any component's factor
     long long s_total = 0, l_total = 0;
     std::vector<int> kf_map_idx, lm_map_idx;
     std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
@@ -823,6 +850,8 @@ struct vx_sba_plan {
 
 namespace vx {
 namespace {
+
+int solve_panel_slots(int np, int max_panel);
 
 SBAArgs make_args(vx_sba_plan* p) {
     SBAArgs a{};
@@ -875,6 +904,7 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.Linv = p->Linv.as<double>();
     a.dx = p->dx.as<double>();
     a.st = p->state.as<SBAState>();
+    a.panel_slots = solve_panel_slots(p->max_np, p->max_panel);
     return a;
 }
 
@@ -1218,6 +1248,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     // most tiles of the dense matrix are never touched.
     std::vector<int> hdr((size_t)kHdrN * std::max(p->n_comp, 1), 0), tlist;
     p->n_lfactor_tiles = p->n_trail_updates = 0;
+    p->max_panel = 1;
     {
         std::vector<std::vector<std::pair<int, int>>> cblk(p->n_comp);
         for (const int2& b : bij) {
@@ -1258,6 +1289,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
                 for (int i = k + 1; i < nt; ++i)
                     if (NZ(i, k)) tlist.push_back(i);
                 tlist.push_back(nt);
+                p->max_panel = std::max(p->max_panel, (int)tlist.size() - tlist[pp + k]);
             }
             tlist[pp + nt] = (int)tlist.size();
             // trailing-update lists
@@ -1336,9 +1368,17 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     return VX_OK;
 }
 
-size_t solve_lds_bytes(int np) {
-    const int nt = np / 16;  // panel (nt + 1 tiles) | L_kk^-1 | POTRF columns (2 tiles) | y
-    return ((size_t)(nt + 4) * kPanelStride + (size_t)np) * sizeof(double);
+// k_sba_solve's LDS for ps panel slots: panel | L_kk^-1 | POTRF columns (2 tiles) | y | slot map
+size_t solve_lds_bytes(int np, int ps) {
+    return ((size_t)(ps + 3) * kPanelStride + (size_t)np) * sizeof(double) + (size_t)(np / 16 + 1) * sizeof(int);
+}
+// panel slots: the largest column panel of any component, as many as fit gfx950's 160 KB
+int solve_panel_slots(int np, int max_panel) {
+    int ps = std::max(max_panel, 1);
+    // $VX_SBA_PANEL_SLOTS caps the slots (tests: the global-operand steps on small windows)
+    if (const char* e = std::getenv("VX_SBA_PANEL_SLOTS")) ps = std::max(1, std::min(ps, std::atoi(e)));
+    while (ps > 1 && solve_lds_bytes(np, ps) > 160 * 1024) --ps;
+    return ps;
 }
 
 int sba_run(vx_ctx* c, vx_sba_plan* p) {
@@ -1356,7 +1396,7 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
 #endif
     }
     const SBAArgs a = make_args(p);
-    const size_t lds = solve_lds_bytes(p->max_np);
+    const size_t lds = solve_lds_bytes(p->max_np, a.panel_slots);
     if (lds > 64 * 1024)
         VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_solve),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

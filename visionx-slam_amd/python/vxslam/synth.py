@@ -133,10 +133,14 @@ def make_ba_map(seed: int, n_kf: int = 10, n_lm: int = 2000, *, n_old_kf: int = 
                 frac_outlier: float = 0.01, noise_px: float = 0.5, noise_clip: float = 1.5,
                 rot_deg: float = 0.2, trans_m: float = 0.01, lm_sigma: float = 0.01,
                 width: int = 640, height: int = 480, intr=(FX, FY, CX, CY),
-                n_streams: int = 1) -> BAMap:
+                n_streams: int = 1, cross_frac: float = 0.0) -> BAMap:
     """A BA window of ``n_kf`` keyframes (+ ``n_old_kf`` older keyframes outside the window) and
     ``n_lm`` landmarks.  ``n_streams`` > 1 builds a multi-camera rig (configs C5): keyframes are
-    split into streams, each stream observing its own landmark subset.
+    split into streams, each stream observing its own landmark subset.  ``cross_frac`` > 0 makes
+    the rig one body: that fraction of the landmarks lies in the field of view the stream shares
+    with its neighbour (the next camera, 360 / n_streams degrees further round the rig) and is
+    observed by both, so the streams' keyframes form ONE covisibility component (config C5's
+    global window; with 0 every stream is a component of its own).
 
     Returns a BAMap with the vx_map_view / orc_map_view fields.  Landmark ids are random uint64,
     keyframe ids increase with time but are not contiguous."""
@@ -181,6 +185,32 @@ def make_ba_map(seed: int, n_kf: int = 10, n_lm: int = 2000, *, n_old_kf: int = 
     within = np.arange(obs_lm.shape[0]) - np.repeat(np.cumsum(L) - L, L)
     obs_t = start[obs_lm] + within
     obs_kf = obs_t * n_streams + lm_stream[obs_lm]
+    if cross_frac > 0 and n_streams > 1:
+        # shared landmarks: 15-28 degrees off the anchor camera's axis towards the next camera
+        # (its yaw is 360 / n_streams degrees larger), 2-5 m deep, observed by that camera too at
+        # the same times wherever the point projects inside its image (separate generator, so the
+        # maps of cross_frac = 0 are unchanged)
+        rc = np.random.default_rng(seed ^ 0xC5C5C5)
+        cand = np.nonzero(L >= 2)[0]
+        sh = np.sort(rc.choice(cand, size=min(len(cand), int(round(cross_frac * n_lm))), replace=False))
+        th = np.deg2rad(rc.uniform(15.0, 28.0, size=len(sh)))
+        zs = rc.uniform(2.0, 5.0, size=len(sh))
+        u[sh] = cx + np.tan(th) * fx
+        v[sh] = rc.uniform(60, height - 60, size=len(sh))
+        z[sh] = zs
+        pcs_a = np.stack([(u[sh] - cx) / fx * zs, (v[sh] - cy) / fy * zs, zs], -1)
+        p_true[sh] = np.einsum("nij,nj->ni", R_wc[anchor[sh]], pcs_a) + centres[anchor[sh]]
+        x_lm = np.repeat(sh, L[sh])
+        x_t = start[x_lm] + (np.arange(len(x_lm)) - np.repeat(np.cumsum(L[sh]) - L[sh], L[sh]))
+        x_kf = x_t * n_streams + (lm_stream[x_lm] + 1) % n_streams
+        pc2 = np.einsum("oij,oj->oi", R_cw[x_kf], p_true[x_lm]) + t_cw[x_kf]
+        z2 = np.where(pc2[:, 2] > 0.3, pc2[:, 2], 1.0)
+        u2, v2 = fx * pc2[:, 0] / z2 + cx, fy * pc2[:, 1] / z2 + cy
+        vis = (pc2[:, 2] > 0.3) & (u2 > 20) & (u2 < width - 20) & (v2 > 20) & (v2 < height - 20)
+        obs_lm = np.concatenate([obs_lm, x_lm[vis]])
+        obs_t = np.concatenate([obs_t, x_t[vis]])
+        obs_kf = np.concatenate([obs_kf, x_kf[vis]])
+        L = np.bincount(obs_lm, minlength=n_lm)
     pcs = np.einsum("oij,oj->oi", R_cw[obs_kf], p_true[obs_lm]) + t_cw[obs_kf]
     uv = np.stack([fx * pcs[:, 0] / pcs[:, 2] + cx, fy * pcs[:, 1] / pcs[:, 2] + cy], -1)
     nz = np.clip(rng.normal(0, noise_px, size=uv.shape), -noise_clip, noise_clip)
