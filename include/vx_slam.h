@@ -442,6 +442,14 @@ int vx_sba_plan_info(const vx_sba_plan* plan, int64_t* out8);
 /* The reduced system of the LAST assembly of the last run (S row-major n x n, lower triangle
  * meaningful, damping included; rhs n), for verification against the restatement. */
 int vx_sba_plan_system(vx_ctx* ctx, vx_sba_plan* plan, double* S, double* rhs, int n);
+/* The same plan from the device-resident map (vx_dmap): window, landmark set and observation set as
+ * for the equivalent snapshot, the observation / pair / block tables sorted on the device (two small
+ * read-backs: the counts, then the block list for the host's covisibility components and symbolic
+ * factorisation).  Unsharded.  Fetch statistics with vx_sba_plan_fetch(map = NULL); the result goes
+ * into the map's rows with vx_sba_plan_apply_dmap (stream ordered, no host synchronisation). */
+int vx_sba_plan_create_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_ref, const vx_sba_options* opt,
+                            vx_sba_plan** out);
+int vx_sba_plan_apply_dmap(vx_ctx* ctx, vx_sba_plan* plan, vx_dmap* map);
 int vx_sba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                         const vx_sba_options* opt, vx_sba_stats* stats);
 

@@ -127,3 +127,35 @@ def test_sba_panel_from_global(ctx, oracle, monkeypatch):
     monkeypatch.setenv("VX_SBA_PANEL_SLOTS", "2")
     m = synth.make_ba_map(0x5EED0032, 50, 12000, n_old_kf=2)
     _case(ctx, oracle, m, dict(window=50, iters=6))
+
+
+@pytest.mark.parametrize("cfg", [("C3", 50, 20000, 1, 0.0), ("C5s", 96, 16000, 8, 0.03)])
+def test_sba_plan_from_resident_map(ctx, oracle, cfg):
+    """vx_sba_plan_create_dmap builds the Schur plan's tables on the device from the resident map
+    (ba_lean.hip): the same problem as the snapshot host build on the equivalent vx_map_view — same
+    sizes, and runs that agree bitwise (identical observation, pair and block orders) — and the
+    scatter into the map equals the snapshot fetch; pinned to the restatement through the snapshot."""
+    import vxslam
+
+    name, nk, nl, ns, cf = cfg
+    m = synth.make_ba_map(0x5BD0 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns, cross_frac=cf)
+    dm = vxslam.DMap(ctx)
+    kf_order, lm_order = vxslam.dmap_load(dm, m)
+    m2 = vxslam.map_reorder(m, kf_order, lm_order)
+    opts = vxslam.default_sba_options(window=nk, iters=6)
+    pd = dm.sba_plan(opts, ref_kf_id=m["ref_kf_id"])
+    ps = ctx.sba_plan(m2, opts, ref_kf_id=m["ref_kf_id"])
+    assert pd.info() == ps.info()
+    pd.run_async()
+    ps.run_async()
+    sd, ss = pd.fetch(), ps.fetch(m2)
+    for f in ("status", "iterations", "accepted", "n_window_kf", "n_landmarks", "initial_cost", "final_cost"):
+        assert getattr(sd, f) == getattr(ss, f), f
+    assert list(sd.cost) == list(ss.cost) and list(sd.obs) == list(ss.obs) and list(sd.step) == list(ss.step)
+    pd.apply(dm)
+    pose, pos = dm.download()
+    assert np.array_equal(pose, m2["kf_pose"].reshape(-1, 7)) and np.array_equal(pos, m2["lm_pos"].reshape(-1, 3))
+    pd.close(), ps.close(), dm.close()
+    # the snapshot plan against the restatement (the dmap plan equals it bitwise)
+    m3 = vxslam.map_reorder(m, kf_order, lm_order)
+    _case(ctx, oracle, m3, dict(window=nk, iters=6), ref=m["ref_kf_id"])

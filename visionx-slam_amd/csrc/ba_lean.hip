@@ -51,6 +51,7 @@
 #include "ba_common.hpp"
 #include "ba_plan.hpp"
 #include "dmap.hpp"
+#include "sba_plan.hpp"
 
 namespace vx {
 namespace {
@@ -147,6 +148,7 @@ struct LeanArgs {
     double* lm_pos0;
     double2* puv;
     int* plm;
+    int* pkf;                       // (SBA plans) window row of each pose-stage observation, or null
     int* kf_obs_ptr;
     int* lkf;
     int* llm;
@@ -279,6 +281,7 @@ __global__ __launch_bounds__(kT) void k_lb_pose(LeanArgs a) {
         const int o = a.pscan[f];
         a.puv[o] = a.wuv[f];
         a.plm[o] = a.l_slot[l];
+        if (a.pkf) a.pkf[o] = code >> 2;
     }
     if (a.f_back[f]) {
         const int s = a.l_slot[l];
@@ -389,6 +392,347 @@ int ht_sync(vx_ctx* c, vx_dmap* m) {
 
 }  // namespace
 
+// What a lean build needs to know about the window before launching anything (host mirrors only)
+struct LeanCore {
+    std::vector<int> win, wptr;
+    std::vector<int64_t> src;
+    std::vector<uint64_t> wid;
+    std::vector<uint8_t> cam;
+    int nk = 0, nf = 0, mw = 1;
+    int64_t nl = 0, nobs = 0, nvalid = 0, mx = 0;
+    LeanArgs a{};
+};
+
+void lean_window(const vx_dmap* m, const std::vector<int>& win, LeanCore& K) {
+    const int nk = (int)win.size();
+    K.win = win;
+    K.nk = nk;
+    K.wptr.assign(nk + 1, 0);
+    K.src.resize(nk);
+    K.wid.resize(nk);
+    K.cam.resize(nk);
+    K.nvalid = K.mx = 0;
+    for (int r = 0; r < nk; ++r) {
+        const int k = win[r];
+        K.src[r] = m->kf_feat_ptr[k];
+        K.wptr[r + 1] = K.wptr[r] + (int)(m->kf_feat_ptr[k + 1] - m->kf_feat_ptr[k]);
+        K.wid[r] = m->kf_id[k];
+        K.cam[r] = m->kf_has_cam[k];
+        K.nvalid += m->kf_valid_cnt[k];
+        if (K.cam[r]) K.mx = std::max<int64_t>(K.mx, m->kf_valid_cnt[k]);
+    }
+    K.nf = K.wptr[nk];
+    K.nl = m->n_lm;
+    K.nobs = m->n_obs;
+}
+
+// The window tables (one pinned upload) and the build kernels up to the pose-stage CSR: slots
+// (optimised rows first, then fixed rows, map-row order), initial positions by slot, keyframe tables,
+// the pose-stage CSR; lstage: also the landmark-stage CSR and workgroup table (key span q).  Every
+// count stays in dyn[]; nothing synchronises.
+int lean_build_core(vx_ctx* c, vx_dmap* m, int min_point, int q, bool lstage, int cap_blocks, bool with_pkf,
+                    LeanCore& K) {
+    auto& L = m->lean;
+    const int nk = K.nk, nf = K.nf;
+    const std::vector<int>& win = K.win;
+    const std::vector<int>& wptr = K.wptr;
+    const int64_t nl = K.nl, nobs = K.nobs;
+    const int mw = (nk + 63) / 64;
+    K.mw = mw;
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = ht_sync(c, m))) return rc;
+    // window tables: one pinned block, one upload
+    const size_t o_src = 0, o_wid = o_src + 8 * (size_t)nk, o_wptr = o_wid + 8 * (size_t)nk,
+                 o_win = o_wptr + 4 * ((size_t)nk + 2), o_cam = o_win + 4 * ((size_t)nk + 2), o_end = o_cam + (size_t)nk + 8;
+    VX_HIP(c, L.win_host.ensure(o_end, true));
+    VX_HIP(c, grow(L.win, o_end));
+    {
+        uint8_t* H = static_cast<uint8_t*>(L.win_host.p);
+        std::memcpy(H + o_src, K.src.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_wid, K.wid.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_wptr, wptr.data(), 4 * ((size_t)nk + 1));
+        std::memcpy(H + o_win, win.data(), 4 * (size_t)nk);
+        std::memcpy(H + o_cam, K.cam.data(), (size_t)nk);
+    }
+    VX_HIP(c, hipMemcpyAsync(L.win.p, L.win_host.p, o_end, hipMemcpyHostToDevice, c->stream));
+    const size_t fN = (size_t)nf + 1, lN = (size_t)nl + 1, kN = (size_t)nk + 1;
+    for (DevBuf* d : {&L.f_l, &L.f_code, &L.f_pv, &L.f_back, &L.pscan, &L.plm, &L.lkf, &L.llm}) VX_HIP(c, grow(*d, fN * 4));
+    for (DevBuf* d : {&L.wuv, &L.puv, &L.luv}) VX_HIP(c, grow(*d, fN * 16));
+    for (DevBuf* d : {&L.l_ref, &L.l_pv, &L.l_cnt, &L.l_slot, &L.inv, &L.cnt, &L.lobs_ptr}) VX_HIP(c, grow(*d, lN * 4));
+    for (DevBuf* d : {&L.key, &L.ex}) VX_HIP(c, grow(*d, lN * 8));
+    VX_HIP(c, grow(L.mask, lN * mw * 8));
+    VX_HIP(c, grow(L.lm_pos0, lN * 32));
+    VX_HIP(c, grow(L.lm_blk, (size_t)(cap_blocks + 2) * 8));
+    VX_HIP(c, grow(L.kf_pose0, kN * 64));
+    VX_HIP(c, grow(L.kf_intr, kN * 32));
+    VX_HIP(c, grow(L.kf_flags, kN * 4));
+    VX_HIP(c, grow(L.kf_obs_ptr, kN * 4));
+    VX_HIP(c, grow(L.dyn, kDynInts * 4));
+    if (with_pkf) VX_HIP(c, grow(L.pkf, fN * 4));
+
+    uint8_t* WD = L.win.as<uint8_t>();
+    LeanArgs& a = K.a;
+    a = LeanArgs{};
+    a.nk = nk;
+    a.nf = nf;
+    a.mw = mw;
+    a.src = reinterpret_cast<const int64_t*>(WD + o_src);
+    a.wid = reinterpret_cast<const uint64_t*>(WD + o_wid);
+    a.wptr = reinterpret_cast<const int*>(WD + o_wptr);
+    a.win = reinterpret_cast<const int*>(WD + o_win);
+    a.cam = WD + o_cam;
+    a.nl = nl;
+    a.nobs = nobs;
+    a.feat_uv = m->feat_uv.as<double>();
+    a.feat_lm = m->feat_lm.as<uint64_t>();
+    a.feat_fl = m->feat_fl.as<uint8_t>();
+    a.lm_id = m->lm_id.as<uint64_t>();
+    a.lm_bad = m->lm_bad.as<uint8_t>();
+    a.lm_pos = m->lm_pos.as<double>();
+    a.obs_lm = m->obs_lm.as<int>();
+    a.obs_kf = m->obs_kf.as<uint64_t>();
+    a.obs_fi = m->obs_fi.as<uint64_t>();
+    a.map_pose = m->kf_pose.as<double>();
+    a.map_intr = m->kf_intr.as<double>();
+    a.ht_key = m->ht_key.as<uint64_t>();
+    a.ht_val = m->ht_val.as<int>();
+    a.ht_mask = m->ht_cap - 1;
+    a.min_point = min_point;
+    a.f_l = L.f_l.as<int>();
+    a.f_code = L.f_code.as<int>();
+    a.f_pv = L.f_pv.as<int>();
+    a.f_back = L.f_back.as<int>();
+    a.wuv = L.wuv.as<double2>();
+    a.l_ref = L.l_ref.as<int>();
+    a.l_pv = L.l_pv.as<int>();
+    a.l_cnt = L.l_cnt.as<int>();
+    a.key = L.key.as<unsigned long long>();
+    a.ex = L.ex.as<unsigned long long>();
+    a.l_slot = L.l_slot.as<int>();
+    a.inv = L.inv.as<int>();
+    a.cnt = L.cnt.as<int>();
+    a.mask = L.mask.as<unsigned long long>();
+    a.pscan = L.pscan.as<int>();
+    a.lobs_ptr = L.lobs_ptr.as<int>();
+    a.lm_pos0 = L.lm_pos0.as<double>();
+    a.puv = L.puv.as<double2>();
+    a.plm = L.plm.as<int>();
+    a.pkf = with_pkf ? L.pkf.as<int>() : nullptr;
+    a.kf_obs_ptr = L.kf_obs_ptr.as<int>();
+    a.lkf = L.lkf.as<int>();
+    a.llm = L.llm.as<int>();
+    a.luv = L.luv.as<double2>();
+    a.lm_blk = L.lm_blk.as<int>();
+    a.kf_pose0 = L.kf_pose0.as<double>();
+    a.kf_intr = L.kf_intr.as<double>();
+    a.kf_flags = L.kf_flags.as<int>();
+    a.dyn = L.dyn.as<int>();
+    a.q = q;
+    hipStream_t sm = c->stream;
+    const long long n_big = std::max<long long>((long long)nl + 1, kDynInts);
+    hipLaunchKernelGGL(k_lb_clear, dim3(grid(n_big)), dim3(kT), 0, sm, a);
+    hipLaunchKernelGGL(k_lb_feat, dim3(grid(std::max<long long>(nf + 1, nk))), dim3(kT), 0, sm, a);
+    if (nobs) hipLaunchKernelGGL(k_lb_obs, dim3(grid(nobs)), dim3(kT), 0, sm, a);
+    hipLaunchKernelGGL(k_lb_flags, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: features / observations / flags");
+    if ((rc = scan_ex<unsigned long long>(c, L.tmp, a.key, L.ex.as<unsigned long long>(), nl))) return rc;
+    hipLaunchKernelGGL(k_lb_slots, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    if ((rc = scan_ex<int>(c, L.tmp, a.f_pv, L.pscan.as<int>(), nf))) return rc;
+    hipLaunchKernelGGL(k_lb_pose, dim3(grid(std::max<long long>(nf, nk + 1))), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: slots / pose CSR");
+    if (!lstage) return VX_OK;
+    hipLaunchKernelGGL(k_lb_lcount, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: landmark-stage counts");
+    if ((rc = scan_ex<int>(c, L.tmp, a.cnt, L.lobs_ptr.as<int>(), nl))) return rc;
+    hipLaunchKernelGGL(k_lb_lfill, dim3(grid(std::max<long long>(nf, nl))), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "lean build: landmark-stage CSR");
+    return VX_OK;
+}
+
+
+// ---------------------------------------------------------------- Schur plan from the resident map
+// vx_sba_plan_create_dmap: the observation, pair and block tables of sba.hip's build_sba_plan,
+// made on the device from the lean core build's pose-stage CSR (same window, landmark set, slots and
+// observation set as the snapshot build: sba.hip keeps the reference's LocalBA selection):
+//   observations   the pose-stage observations stably sorted by (optimised slot, or n_opt for the
+//                  fixed landmarks): optimised landmarks landmark-major with their keyframes in window
+//                  order, then the fixed landmarks' observations keyframe-major (radix sort)
+//   keyframe lists every keyframe's observation indices, ascending (stable sort by keyframe row)
+//   pairs          per optimised landmark every (a1, a2) of its observations with free keyframes
+//                  i = kf(a1) >= j = kf(a2), counted, scanned and emitted in (slot, a1, a2) order,
+//                  then stably sorted by block: the diagonal blocks (every window keyframe) first,
+//                  then the non-empty off-diagonal blocks by (i, j) — the snapshot build's order
+//   k_sba_lm       whole landmarks per workgroup, slot s -> (lm_ptr[s] + s) / (256 - most observations)
+// Two read-backs size what follows (the counts; then the block list for the host's covisibility
+// components and symbolic factorisation, sba_plan_finish).
+struct SbaArgs {
+    int nk, nf;
+    int64_t nl;
+    int pad_key, pad_kf;
+    const int* dyn_r;
+    int* dyn;
+    const int* plm;
+    const int* pkf;
+    const double2* puv;
+    const int* kflags;        // window row flags (bit1: fixed)
+    int* pkey;
+    int* pval;
+    const int* skey;
+    const int* perm;
+    int* scnt;                // per optimised slot: observations (scan input)
+    const int* lm_ptr;
+    double2* obs_uv;
+    int* obs_lm;
+    int* obs_kf;
+    int* k2;
+    int* v2;
+    int* pc;                  // per optimised slot: pairs (scan input)
+    const int* pptr;
+    int* kcnt;                // per (i, j) key: pairs
+    int* oflag;
+    const int* orank;
+    int* bidx;
+    int* bcnt;
+    int2* bij;
+    int* ekey;
+    unsigned long long* eval;
+    int* lm_blk;
+    int q;
+};
+
+__global__ __launch_bounds__(kT) void k_sb_keys(SbaArgs a) {
+    const int o = blockIdx.x * kT + threadIdx.x;
+    if (o >= a.nf) return;
+    const int n_obs = a.dyn[kDynPoseObs], n_opt = a.dyn[kDynNOpt];
+    int key = a.pad_key;
+    if (o < n_obs) {
+        const int s = a.plm[o];
+        key = s < n_opt ? s : n_opt;
+        if (s < n_opt) atomicAdd(&a.scnt[s], 1);
+    }
+    a.pkey[o] = key;
+    a.pval[o] = o;
+}
+
+__global__ __launch_bounds__(kT) void k_sb_obs(SbaArgs a) {
+    const int p = blockIdx.x * kT + threadIdx.x;
+    if (p >= a.nf) return;
+    const int n_obs = a.dyn[kDynPoseObs];
+    if (p == 0) a.dyn[kDynSbaOo] = a.lm_ptr[a.dyn[kDynNOpt]];
+    int kf = a.pad_kf;
+    if (p < n_obs) {
+        const int o = a.perm[p];
+        kf = a.pkf[o];
+        a.obs_uv[p] = a.puv[o];
+        a.obs_lm[p] = a.plm[o];
+        a.obs_kf[p] = kf;
+    }
+    a.k2[p] = kf;
+    a.v2[p] = p;
+}
+
+// pairs of slot s: (a1, a2) over its observations, both keyframes free, kf(a2) <= kf(a1)
+template <bool kEmit>
+__device__ __forceinline__ int sb_pairs(const SbaArgs& a, int s) {
+    const int o0 = a.lm_ptr[s], o1 = a.lm_ptr[s + 1];
+    int c = 0;
+    const int base = kEmit ? a.pptr[s] : 0;
+    for (int a1 = o0; a1 < o1; ++a1) {
+        const int i = a.obs_kf[a1];
+        if (a.kflags[i] & 2) continue;
+        for (int a2 = o0; a2 < o1; ++a2) {
+            const int j = a.obs_kf[a2];
+            if ((a.kflags[j] & 2) || j > i) continue;
+            const int key = i * a.nk + j;
+            if (kEmit) {
+                a.ekey[base + c] = a.bidx[key];
+                a.eval[base + c] = (unsigned long long)(unsigned)a1 | ((unsigned long long)(unsigned)a2 << 32);
+            } else {
+                atomicAdd(&a.kcnt[key], 1);
+            }
+            ++c;
+        }
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kT) void k_sb_pcount(SbaArgs a) {
+    const int64_t s = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (s > a.nl) return;
+    const int n_opt = a.dyn[kDynNOpt];
+    int c = 0;
+    if (s < n_opt) {
+        c = sb_pairs<false>(a, (int)s);
+        atomicMax(&a.dyn[kDynSbaMaxObs], a.lm_ptr[s + 1] - a.lm_ptr[s]);
+    }
+    a.pc[s] = c;
+}
+
+__global__ __launch_bounds__(kT) void k_sb_bflag(SbaArgs a) {
+    const int key = blockIdx.x * kT + threadIdx.x;
+    const int n2 = a.nk * a.nk;
+    if (key > n2) return;
+    int f = 0;
+    if (key < n2) {
+        const int i = key / a.nk, j = key - i * a.nk;
+        f = (i != j && a.kcnt[key] > 0) ? 1 : 0;
+    }
+    a.oflag[key] = f;
+}
+
+__global__ __launch_bounds__(kT) void k_sb_btab(SbaArgs a) {
+    const int key = blockIdx.x * kT + threadIdx.x;
+    const int n2 = a.nk * a.nk;
+    if (key == 0) {
+        a.dyn[kDynSbaBlocks] = a.nk + a.orank[n2];
+        a.dyn[kDynSbaPairs] = a.pptr[a.dyn[kDynNOpt]];
+    }
+    if (key >= n2) return;
+    const int i = key / a.nk, j = key - i * a.nk;
+    int b = -1;
+    if (i == j) b = i;
+    else if (a.kcnt[key] > 0) b = a.nk + a.orank[key];
+    a.bidx[key] = b;
+    if (b < 0) return;
+    a.bcnt[b] = a.kcnt[key];
+    a.bij[b] = make_int2(i, j);
+}
+
+__global__ __launch_bounds__(kT) void k_sb_pemit(SbaArgs a) {
+    const int s = blockIdx.x * kT + threadIdx.x;
+    if (s < a.dyn_r[kDynNOpt]) sb_pairs<true>(a, s);
+}
+
+// k_sba_lm workgroups (q = 256 - most observations of one landmark >= that count + 1)
+__global__ __launch_bounds__(kT) void k_sb_lmblk(SbaArgs a) {
+    const int s = blockIdx.x * kT + threadIdx.x;
+    const int n_opt = a.dyn_r[kDynNOpt];
+    if (s >= n_opt) return;
+    const int b = (a.lm_ptr[s] + s) / a.q;
+    const int bp = s ? (a.lm_ptr[s - 1] + s - 1) / a.q : -1;
+    if (b != bp) a.lm_blk[b] = s;
+    if (s == n_opt - 1) {
+        a.lm_blk[b + 1] = n_opt;
+        a.dyn[kDynSbaLmBlocks] = b + 1;
+    }
+}
+
+unsigned bits_for(int64_t v) {  // radix bits holding [0, v]
+    unsigned b = 1;
+    while ((1ll << b) <= v) ++b;
+    return b;
+}
+
+template <class K, class V>
+int sort_pairs(vx_ctx* c, DevBuf& tmp, K* ki, K* ko, V* vi, V* vo, size_t n, unsigned bits) {
+    size_t bytes = 0;
+    VX_HIP(c, rocprim::radix_sort_pairs(nullptr, bytes, ki, ko, vi, vo, n, 0, bits, c->stream));
+    VX_HIP(c, grow(tmp, std::max<size_t>(bytes, 16)));
+    VX_HIP(c, rocprim::radix_sort_pairs(tmp.p, bytes, ki, ko, vi, vo, n, 0, bits, c->stream));
+    return VX_OK;
+}
+
 // SelectKeyFrames over the resident keyframes (ba_window.hip)
 std::vector<int> dmap_select_window(const vx_dmap* m, uint64_t ref_kf_id, int has_ref, int window_size);
 
@@ -415,140 +759,25 @@ int lean_optimize(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_
         return VX_OK;
     }
     const int q = kBaLmBlock - nk;
-    // capacities the host knows: window features, has_landmark features (>= landmark-stage
-    // observations and >= optimised landmarks), map rows, observation rows
-    std::vector<int> wptr(nk + 1, 0);
-    std::vector<int64_t> src(nk);
-    std::vector<uint64_t> wid(nk);
-    std::vector<uint8_t> cam(nk);
-    int64_t nvalid = 0, mx = 0;
-    for (int r = 0; r < nk; ++r) {
-        const int k = win[r];
-        src[r] = m->kf_feat_ptr[k];
-        wptr[r + 1] = wptr[r] + (int)(m->kf_feat_ptr[k + 1] - m->kf_feat_ptr[k]);
-        wid[r] = m->kf_id[k];
-        cam[r] = m->kf_has_cam[k];
-        nvalid += m->kf_valid_cnt[k];
-        if (cam[r]) mx = std::max<int64_t>(mx, m->kf_valid_cnt[k]);
-    }
-    const int nf = wptr[nk];
-    const int64_t nl = m->n_lm, nobs = m->n_obs;
-    const int cap_blocks = (int)((2 * nvalid + q - 1) / q) + 1;
-    if (nk > 255 || cap_blocks > 480 || (int64_t)nk * cap_blocks > 80000 || nl >= INT_MAX / 2) {
+    LeanCore K;
+    lean_window(m, win, K);
+    const int cap_blocks = (int)((2 * K.nvalid + q - 1) / q) + 1;
+    if (nk > 255 || cap_blocks > 480 || (int64_t)nk * cap_blocks > 80000 || K.nl >= INT_MAX / 2) {
         *fallback = true;
         return VX_ERR_STATE;
     }
-    const int n_split = ba_split(mx, 1);
-    const int mw = (nk + 63) / 64;
-    VX_HIP(c, hipSetDevice(c->device));
+    const int n_split = ba_split(K.mx, 1);
     int rc;
-    if ((rc = ht_sync(c, m))) return rc;
-    // window tables: one pinned block, one upload
-    const size_t o_src = 0, o_wid = o_src + 8 * (size_t)nk, o_wptr = o_wid + 8 * (size_t)nk,
-                 o_win = o_wptr + 4 * ((size_t)nk + 2), o_cam = o_win + 4 * ((size_t)nk + 2), o_end = o_cam + (size_t)nk + 8;
-    VX_HIP(c, L.win_host.ensure(o_end, true));
-    VX_HIP(c, grow(L.win, o_end));
-    {
-        uint8_t* H = static_cast<uint8_t*>(L.win_host.p);
-        std::memcpy(H + o_src, src.data(), 8 * (size_t)nk);
-        std::memcpy(H + o_wid, wid.data(), 8 * (size_t)nk);
-        std::memcpy(H + o_wptr, wptr.data(), 4 * ((size_t)nk + 1));
-        std::memcpy(H + o_win, win.data(), 4 * (size_t)nk);
-        std::memcpy(H + o_cam, cam.data(), (size_t)nk);
-    }
-    VX_HIP(c, hipMemcpyAsync(L.win.p, L.win_host.p, o_end, hipMemcpyHostToDevice, c->stream));
-    const size_t fN = (size_t)nf + 1, lN = (size_t)nl + 1, kN = (size_t)nk + 1;
-    for (DevBuf* d : {&L.f_l, &L.f_code, &L.f_pv, &L.f_back, &L.pscan, &L.plm, &L.lkf, &L.llm}) VX_HIP(c, grow(*d, fN * 4));
-    for (DevBuf* d : {&L.wuv, &L.puv, &L.luv}) VX_HIP(c, grow(*d, fN * 16));
-    for (DevBuf* d : {&L.l_ref, &L.l_pv, &L.l_cnt, &L.l_slot, &L.inv, &L.cnt, &L.lobs_ptr}) VX_HIP(c, grow(*d, lN * 4));
-    for (DevBuf* d : {&L.key, &L.ex}) VX_HIP(c, grow(*d, lN * 8));
-    VX_HIP(c, grow(L.mask, lN * mw * 8));
-    VX_HIP(c, grow(L.lm_pos0, lN * 32));
-    VX_HIP(c, grow(L.lm_pos, lN * 32));
-    VX_HIP(c, grow(L.lm_blk, (size_t)(cap_blocks + 2) * 8));
-    VX_HIP(c, grow(L.kf_pose0, kN * 64));
-    VX_HIP(c, grow(L.kf_pose, kN * 128));
-    VX_HIP(c, grow(L.kf_intr, kN * 32));
-    VX_HIP(c, grow(L.kf_rot, kN * 72));
-    VX_HIP(c, grow(L.kf_flags, kN * 4));
-    VX_HIP(c, grow(L.kf_obs_ptr, kN * 4));
-    VX_HIP(c, grow(L.kf_part, kN * n_split * kBaStrideDoubles * 8));
-    VX_HIP(c, grow(L.kf_cost, kN * 16));
-    VX_HIP(c, grow(L.state, ba_state_bytes()));
-    VX_HIP(c, grow(L.dyn, kDynInts * 4));
-
-    uint8_t* WD = L.win.as<uint8_t>();
-    LeanArgs a{};
-    a.nk = nk;
-    a.nf = nf;
-    a.mw = mw;
-    a.src = reinterpret_cast<const int64_t*>(WD + o_src);
-    a.wid = reinterpret_cast<const uint64_t*>(WD + o_wid);
-    a.wptr = reinterpret_cast<const int*>(WD + o_wptr);
-    a.win = reinterpret_cast<const int*>(WD + o_win);
-    a.cam = WD + o_cam;
-    a.nl = nl;
-    a.nobs = nobs;
-    a.feat_uv = m->feat_uv.as<double>();
-    a.feat_lm = m->feat_lm.as<uint64_t>();
-    a.feat_fl = m->feat_fl.as<uint8_t>();
-    a.lm_id = m->lm_id.as<uint64_t>();
-    a.lm_bad = m->lm_bad.as<uint8_t>();
-    a.lm_pos = m->lm_pos.as<double>();
-    a.obs_lm = m->obs_lm.as<int>();
-    a.obs_kf = m->obs_kf.as<uint64_t>();
-    a.obs_fi = m->obs_fi.as<uint64_t>();
-    a.map_pose = m->kf_pose.as<double>();
-    a.map_intr = m->kf_intr.as<double>();
-    a.ht_key = m->ht_key.as<uint64_t>();
-    a.ht_val = m->ht_val.as<int>();
-    a.ht_mask = m->ht_cap - 1;
-    a.min_point = o.min_point_observations;
-    a.f_l = L.f_l.as<int>();
-    a.f_code = L.f_code.as<int>();
-    a.f_pv = L.f_pv.as<int>();
-    a.f_back = L.f_back.as<int>();
-    a.wuv = L.wuv.as<double2>();
-    a.l_ref = L.l_ref.as<int>();
-    a.l_pv = L.l_pv.as<int>();
-    a.l_cnt = L.l_cnt.as<int>();
-    a.key = L.key.as<unsigned long long>();
-    a.ex = L.ex.as<unsigned long long>();
-    a.l_slot = L.l_slot.as<int>();
-    a.inv = L.inv.as<int>();
-    a.cnt = L.cnt.as<int>();
-    a.mask = L.mask.as<unsigned long long>();
-    a.pscan = L.pscan.as<int>();
-    a.lobs_ptr = L.lobs_ptr.as<int>();
-    a.lm_pos0 = L.lm_pos0.as<double>();
-    a.puv = L.puv.as<double2>();
-    a.plm = L.plm.as<int>();
-    a.kf_obs_ptr = L.kf_obs_ptr.as<int>();
-    a.lkf = L.lkf.as<int>();
-    a.llm = L.llm.as<int>();
-    a.luv = L.luv.as<double2>();
-    a.lm_blk = L.lm_blk.as<int>();
-    a.kf_pose0 = L.kf_pose0.as<double>();
-    a.kf_intr = L.kf_intr.as<double>();
-    a.kf_flags = L.kf_flags.as<int>();
-    a.dyn = L.dyn.as<int>();
-    a.q = q;
+    if ((rc = lean_build_core(c, m, o.min_point_observations, q, true, cap_blocks, false, K))) return rc;
+    const LeanArgs& a = K.a;
+    const int64_t nl = K.nl;
     hipStream_t sm = c->stream;
-    const long long n_big = std::max<long long>((long long)nl + 1, kDynInts);
-    hipLaunchKernelGGL(k_lb_clear, dim3(grid(n_big)), dim3(kT), 0, sm, a);
-    hipLaunchKernelGGL(k_lb_feat, dim3(grid(std::max<long long>(nf + 1, nk))), dim3(kT), 0, sm, a);
-    if (nobs) hipLaunchKernelGGL(k_lb_obs, dim3(grid(nobs)), dim3(kT), 0, sm, a);
-    hipLaunchKernelGGL(k_lb_flags, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
-    VX_LAUNCH_CHECK(c, "lean build: features / observations / flags");
-    if ((rc = scan_ex<unsigned long long>(c, L.tmp, a.key, L.ex.as<unsigned long long>(), nl))) return rc;
-    hipLaunchKernelGGL(k_lb_slots, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
-    if ((rc = scan_ex<int>(c, L.tmp, a.f_pv, L.pscan.as<int>(), nf))) return rc;
-    hipLaunchKernelGGL(k_lb_pose, dim3(grid(std::max<long long>(nf, nk + 1))), dim3(kT), 0, sm, a);
-    hipLaunchKernelGGL(k_lb_lcount, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
-    VX_LAUNCH_CHECK(c, "lean build: slots / pose CSR / counts");
-    if ((rc = scan_ex<int>(c, L.tmp, a.cnt, L.lobs_ptr.as<int>(), nl))) return rc;
-    hipLaunchKernelGGL(k_lb_lfill, dim3(grid(std::max<long long>(nf, nl))), dim3(kT), 0, sm, a);
-    VX_LAUNCH_CHECK(c, "lean build: landmark-stage CSR");
+    VX_HIP(c, grow(L.kf_pose, ((size_t)nk + 1) * 128));
+    VX_HIP(c, grow(L.kf_rot, ((size_t)nk + 1) * 72));
+    VX_HIP(c, grow(L.kf_part, ((size_t)nk + 1) * n_split * kBaStrideDoubles * 8));
+    VX_HIP(c, grow(L.kf_cost, ((size_t)nk + 1) * 16));
+    VX_HIP(c, grow(L.state, ba_state_bytes()));
+    VX_HIP(c, grow(L.lm_pos, ((size_t)nl + 1) * 32));
 
     DynPlan d;
     d.n_kf = nk;
@@ -604,6 +833,194 @@ int lean_optimize(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_
     return VX_OK;
 }
 
+
+// The Schur plan's tables from the resident map (see above); p->opt set by the caller
+int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba_plan* p) {
+    const vx_sba_options& o = p->opt;
+    p->status = 1;
+    p->from_dmap = true;
+    const int n_kf = (int)m->kf_id.size();
+    std::vector<int> win = n_kf > 0 ? dmap_select_window(m, ref, has_ref, o.window_size) : std::vector<int>{};
+    const int nk = (int)win.size();
+    p->n_window_kf = nk;
+    p->n_landmarks_global = 0;
+    if (nk < 2) return VX_OK;
+    LeanCore K;
+    lean_window(m, win, K);
+    if (nk > 448 || K.nl >= INT_MAX / 2 || (int64_t)K.nf * 2 >= INT_MAX)
+        return set_error(c, VX_ERR_INVALID, "vx_sba_plan_create_dmap: window of %d keyframes (max 448)", nk);
+    int rc;
+    if ((rc = lean_build_core(c, m, o.min_point_observations, 1, false, 0, true, K))) return rc;
+    auto& L = m->lean;
+    auto& B = m->sba;
+    const int nf = K.nf;
+    const int64_t nl = K.nl;
+    hipStream_t sm = c->stream;
+    // keyframe flags (bit0 camera, bit1 fixed: the oldest fixed_keyframes and camera-less ones)
+    std::vector<int> flags(nk);
+    for (int r = 0; r < nk; ++r) flags[r] = (K.cam[r] ? 1 : 0) | ((r < o.fixed_keyframes || !K.cam[r]) ? 2 : 0);
+    VX_HIP(c, p->kf_flags.ensure((size_t)nk * 4));
+    VX_HIP(c, hipMemcpyAsync(p->kf_flags.p, flags.data(), (size_t)nk * 4, hipMemcpyHostToDevice, sm));
+    const size_t fN = (size_t)nf + 1, lN = (size_t)nl + 2;
+    const int n2 = nk * nk;
+    for (DevBuf* d : {&B.pkey, &B.pval, &B.skey, &B.perm, &B.k2, &B.v2}) VX_HIP(c, grow(*d, fN * 4));
+    for (DevBuf* d : {&B.scnt, &B.pc, &B.pptr}) VX_HIP(c, grow(*d, lN * 4));
+    for (DevBuf* d : {&B.kcnt, &B.oflag, &B.orank, &B.bidx}) VX_HIP(c, grow(*d, ((size_t)n2 + 1) * 4));
+    VX_HIP(c, grow(B.bcnt, ((size_t)n2 + nk + 1) * 4));
+    VX_HIP(c, p->blk_ij.ensure(((size_t)n2 + nk + 1) * 8));
+    VX_HIP(c, p->blk_ptr.ensure(((size_t)n2 + nk + 1) * 4));
+    VX_HIP(c, p->obs_uv.ensure(fN * 16));
+    VX_HIP(c, p->obs_lm.ensure(fN * 4));
+    VX_HIP(c, p->obs_kf.ensure(fN * 4));
+    VX_HIP(c, p->kf_obs.ensure(fN * 4));
+    VX_HIP(c, p->lm_ptr.ensure(lN * 4));
+    VX_HIP(c, hipMemsetAsync(B.scnt.p, 0, lN * 4, sm));
+    VX_HIP(c, hipMemsetAsync(B.kcnt.p, 0, ((size_t)n2 + 1) * 4, sm));
+    VX_HIP(c, hipMemsetAsync(B.bcnt.p, 0, ((size_t)n2 + nk + 1) * 4, sm));
+    SbaArgs a{};
+    a.nk = nk;
+    a.nf = nf;
+    a.nl = nl;
+    a.pad_key = (int)((1ll << bits_for(nl + 1)) - 1);
+    a.pad_kf = (int)((1ll << bits_for(nk)) - 1);
+    a.dyn = K.a.dyn;
+    a.dyn_r = K.a.dyn;
+    a.plm = K.a.plm;
+    a.pkf = K.a.pkf;
+    a.puv = K.a.puv;
+    a.kflags = p->kf_flags.as<int>();
+    a.pkey = B.pkey.as<int>();
+    a.pval = B.pval.as<int>();
+    a.skey = B.skey.as<int>();
+    a.perm = B.perm.as<int>();
+    a.scnt = B.scnt.as<int>();
+    a.lm_ptr = p->lm_ptr.as<int>();
+    a.obs_uv = p->obs_uv.as<double2>();
+    a.obs_lm = p->obs_lm.as<int>();
+    a.obs_kf = p->obs_kf.as<int>();
+    a.k2 = B.k2.as<int>();
+    a.v2 = B.v2.as<int>();
+    a.pc = B.pc.as<int>();
+    a.pptr = B.pptr.as<int>();
+    a.kcnt = B.kcnt.as<int>();
+    a.oflag = B.oflag.as<int>();
+    a.orank = B.orank.as<int>();
+    a.bidx = B.bidx.as<int>();
+    a.bcnt = B.bcnt.as<int>();
+    a.bij = p->blk_ij.as<int2>();
+    // observations: stable sort by (optimised slot | n_opt), landmark pointers
+    hipLaunchKernelGGL(k_sb_keys, dim3(grid(nf)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "k_sb_keys");
+    if (nf && (rc = sort_pairs(c, B.tmp, a.pkey, B.skey.as<int>(), a.pval, B.perm.as<int>(), (size_t)nf,
+                               bits_for(a.pad_key))))
+        return rc;
+    if ((rc = scan_ex<int>(c, L.tmp, a.scnt, p->lm_ptr.as<int>(), nl))) return rc;
+    hipLaunchKernelGGL(k_sb_obs, dim3(grid(nf)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "k_sb_obs");
+    // keyframe lists: observation indices by window row, ascending within a row
+    if (nf && (rc = sort_pairs(c, B.tmp, a.k2, B.pkey.as<int>(), a.v2, p->kf_obs.as<int>(), (size_t)nf,
+                               bits_for(a.pad_kf))))
+        return rc;
+    // pairs: counts per slot and per block key, block table
+    hipLaunchKernelGGL(k_sb_pcount, dim3(grid((long long)nl + 1)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "k_sb_pcount");
+    if ((rc = scan_ex<int>(c, L.tmp, a.pc, B.pptr.as<int>(), nl))) return rc;
+    hipLaunchKernelGGL(k_sb_bflag, dim3(grid((long long)n2 + 1)), dim3(kT), 0, sm, a);
+    if ((rc = scan_ex<int>(c, L.tmp, a.oflag, B.orank.as<int>(), n2))) return rc;
+    hipLaunchKernelGGL(k_sb_btab, dim3(grid(n2)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "k_sb_btab");
+    if ((rc = scan_ex<int>(c, L.tmp, a.bcnt, p->blk_ptr.as<int>(), (int64_t)n2 + nk))) return rc;
+    // ---- read-back 1: the counts
+    VX_HIP(c, B.rb.ensure(kDynInts * 4 + ((size_t)n2 + nk + 1) * 8));
+    int* H = static_cast<int*>(B.rb.p);
+    VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
+    VX_HIP(c, hipStreamSynchronize(sm));
+    p->n_landmarks_global = H[kDynGlobal];
+    if (H[kDynStatus]) return VX_OK;  // no optimisable landmark (local_ba.cpp:106-108)
+    const int n_opt = H[kDynNOpt], n_lm = H[kDynNLm], n_obs = H[kDynPoseObs], n_oo = H[kDynSbaOo];
+    const int64_t n_pairs = H[kDynSbaPairs];
+    const int max_obs = H[kDynSbaMaxObs], n_blocks = H[kDynSbaBlocks];
+    if (max_obs > kSbaLmThreads)
+        return set_error(c, VX_ERR_INVALID, "landmark with %d observations in the window (max %d)", max_obs,
+                         kSbaLmThreads);
+    p->status = 0;
+    p->nk = nk;
+    p->n_opt = n_opt;
+    p->n_lm = n_lm;
+    p->n_oo = n_oo;
+    p->n_obs = n_obs;
+    p->n_pairs = n_pairs;
+    p->n_blocks = n_blocks;
+    p->kf_map_idx = win;
+    p->lm_map_idx.clear();  // (on the device: lm_map_dev)
+    // pairs: emitted in (slot, a1, a2) order, stably sorted by block
+    for (DevBuf* d : {&B.ekey, &B.ekey2}) VX_HIP(c, grow(*d, ((size_t)n_pairs + 1) * 4));
+    VX_HIP(c, grow(B.eval, ((size_t)n_pairs + 1) * 8));
+    VX_HIP(c, p->pairs.ensure(((size_t)n_pairs + 1) * 8));
+    a.ekey = B.ekey.as<int>();
+    a.eval = B.eval.as<unsigned long long>();
+    hipLaunchKernelGGL(k_sb_pemit, dim3(grid(n_opt)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "k_sb_pemit");
+    if (n_pairs && (rc = sort_pairs(c, B.tmp, a.ekey, B.ekey2.as<int>(), a.eval, p->pairs.as<unsigned long long>(),
+                                    (size_t)n_pairs, bits_for(n_blocks))))
+        return rc;
+    // k_sba_lm workgroups
+    a.q = kSbaLmThreads - max_obs;
+    VX_HIP(c, p->lm_blk.ensure(((size_t)(n_oo + n_opt) / std::max(a.q, 1) + 3) * 4));
+    a.lm_blk = p->lm_blk.as<int>();
+    if (max_obs <= kSbaLmThreads / 2 - 1) {
+        hipLaunchKernelGGL(k_sb_lmblk, dim3(grid(n_opt)), dim3(kT), 0, sm, a);
+        VX_LAUNCH_CHECK(c, "k_sb_lmblk");
+    }
+    // tables the run reads from the core build: keyframe poses / intrinsics / observation pointers,
+    // initial positions by slot, and the scatter tables
+    VX_HIP(c, p->pose0.ensure((size_t)nk * 64));
+    VX_HIP(c, p->intr.ensure((size_t)nk * 32));
+    VX_HIP(c, p->kf_ptr.ensure(((size_t)nk + 1) * 4));
+    VX_HIP(c, p->lm0.ensure((size_t)std::max(n_lm, 1) * 32));
+    VX_HIP(c, p->lm_map_dev.ensure((size_t)std::max(n_lm, 1) * 4));
+    VX_HIP(c, p->kf_map_dev.ensure((size_t)nk * 4));
+    VX_HIP(c, hipMemcpyAsync(p->pose0.p, K.a.kf_pose0, (size_t)nk * 64, hipMemcpyDeviceToDevice, sm));
+    VX_HIP(c, hipMemcpyAsync(p->intr.p, K.a.kf_intr, (size_t)nk * 32, hipMemcpyDeviceToDevice, sm));
+    VX_HIP(c, hipMemcpyAsync(p->kf_ptr.p, K.a.kf_obs_ptr, ((size_t)nk + 1) * 4, hipMemcpyDeviceToDevice, sm));
+    if (n_lm) {
+        VX_HIP(c, hipMemcpyAsync(p->lm0.p, K.a.lm_pos0, (size_t)n_lm * 32, hipMemcpyDeviceToDevice, sm));
+        VX_HIP(c, hipMemcpyAsync(p->lm_map_dev.p, K.a.inv, (size_t)n_lm * 4, hipMemcpyDeviceToDevice, sm));
+    }
+    VX_HIP(c, hipMemcpyAsync(p->kf_map_dev.p, K.a.win, (size_t)nk * 4, hipMemcpyDeviceToDevice, sm));
+    // ---- read-back 2: the workgroup count and the block list (the host's components and symbolic
+    // factorisation need it)
+    int2* HB = reinterpret_cast<int2*>(H + kDynInts);
+    VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
+    VX_HIP(c, hipMemcpyAsync(HB, p->blk_ij.p, (size_t)n_blocks * 8, hipMemcpyDeviceToHost, sm));
+    std::vector<int> lptr_h;
+    if (max_obs > kSbaLmThreads / 2 - 1) {  // (a landmark seen by more than 127 window keyframes)
+        lptr_h.resize((size_t)n_opt + 1);
+        VX_HIP(c, hipMemcpyAsync(lptr_h.data(), p->lm_ptr.p, lptr_h.size() * 4, hipMemcpyDeviceToHost, sm));
+    }
+    VX_HIP(c, hipStreamSynchronize(sm));
+    if (!lptr_h.empty()) {  // greedy packing on the host, as build_sba_plan does
+        std::vector<int> blk{0};
+        int n_o = 0, n_l = 0;
+        for (int sl = 0; sl < n_opt; ++sl) {
+            const int cnt = lptr_h[sl + 1] - lptr_h[sl];
+            if (n_l + 1 > kSbaLmThreads || n_o + cnt > kSbaLmThreads) {
+                blk.push_back(sl);
+                n_o = n_l = 0;
+            }
+            n_o += cnt;
+            ++n_l;
+        }
+        blk.push_back(n_opt);
+        VX_HIP(c, p->lm_blk.ensure(blk.size() * 4));
+        VX_HIP(c, hipMemcpy(p->lm_blk.p, blk.data(), blk.size() * 4, hipMemcpyHostToDevice));
+        p->n_lm_blocks = (int)blk.size() - 1;
+    } else {
+        p->n_lm_blocks = n_opt ? H[kDynSbaLmBlocks] : 0;
+    }
+    const std::vector<int2> bij(HB, HB + n_blocks);
+    return sba_plan_finish(c, p, flags, bij);
+}
 }  // namespace vx
 
 vx_dmap::~vx_dmap() {

@@ -153,7 +153,11 @@ std::vector<int> pack_lm_blocks(const std::vector<int>& lptr, int n_opt, int* ma
 // observations, optimisable landmarks over all shards, most landmark-stage observations of one
 // landmark, fixed landmarks.
 enum : int { kDynNOpt = 0, kDynNLm, kDynBlocks, kDynStatus, kDynPoseObs, kDynLmObs, kDynGlobal, kDynMaxObs,
-             kDynNFixed, kDynInts = 16 };
+             kDynNFixed,
+             // Schur plans from the resident map (vx_sba_plan_create_dmap): optimised-landmark
+             // observations, co-observation pairs, most observations of one landmark, blocks of the
+             // reduced system, k_sba_lm workgroups
+             kDynSbaOo, kDynSbaPairs, kDynSbaMaxObs, kDynSbaBlocks, kDynSbaLmBlocks, kDynInts = 16 };
 struct DynPlan {
     int n_kf = 0, n_split = 1, grid_blocks = 0;
     vx_ba_options opt{};

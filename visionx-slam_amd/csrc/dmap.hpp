@@ -53,7 +53,7 @@ struct vx_dmap {
     struct Lean {
         vx::DevBuf win, f_l, f_code, f_pv, f_back, pscan, wuv, l_ref, l_pv, l_cnt, key, ex, l_slot, inv, cnt, mask,
             lobs_ptr, lm_pos0, lm_pos, puv, plm, lkf, llm, luv, lm_blk, kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags,
-            kf_obs_ptr, kf_part, kf_cost, state, dyn, tmp;
+            kf_obs_ptr, kf_part, kf_cost, state, dyn, tmp, pkf;
         vx::PinnedBuf win_host, rb_host;
         int nk = 0;                        // window of the last call (0: none)
         int status = 1, n_opt = 0, iterations = 0;
@@ -61,6 +61,11 @@ struct vx_dmap {
         bool ran = false;
         vx_ba_plan* fallback = nullptr;    // the last call's plan when it took the general build
     } lean;
+    // scratch of the Schur plan build from this map (vx_sba_plan_create_dmap)
+    struct SbaScratch {
+        vx::DevBuf pkey, pval, skey, perm, k2, v2, scnt, pc, pptr, kcnt, oflag, orank, bidx, bcnt, ekey, eval, ekey2, tmp;
+        vx::PinnedBuf rb;
+    } sba;
     ~vx_dmap();
 };
 

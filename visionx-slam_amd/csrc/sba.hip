@@ -45,6 +45,8 @@
 #include "vx_internal.hpp"
 #include "vx_ktrace.hpp"
 #include "ba_common.hpp"
+#include "sba_plan.hpp"
+#include "dmap.hpp"
 
 namespace vx {
 namespace {
@@ -52,7 +54,7 @@ namespace {
 using namespace vx::ba;
 
 constexpr int kSbaMaxIter = 64;
-constexpr int kLmThreads = 256;     // k_sba_lm: max observations (and landmarks) per workgroup
+constexpr int kLmThreads = kSbaLmThreads;  // k_sba_lm: max observations (and landmarks) per workgroup
 constexpr int kBlkThreads = 256;    // k_sba_blocks
 constexpr int kSolveThreads = 256;  // k_sba_solve: 4 waves, one per SIMD (512 registers each: no spills)
 constexpr int kSolveWaves = kSolveThreads / 64;
@@ -825,28 +827,7 @@ int upload(vx_ctx* c, DevBuf& d, const std::vector<T>& h) {
 }  // namespace
 }  // namespace vx
 
-struct vx_sba_plan {
-    vx_ctx* c = nullptr;
-    vx_sba_options opt{};
-    int status = 1;
-    int shard_rank = 0, shard_count = 1;
-    int n_window_kf = 0, n_landmarks_global = 0;
-    int nk = 0, n_opt = 0, n_lm = 0, n_oo = 0, n_obs = 0;
-    int64_t n_pairs = 0;
-    int n_blocks = 0, n_lm_blocks = 0, n_comp = 0, max_np = 0;
-    int max_panel = 1;  // most panel tiles (rhs row included) of one column of any component's factor
-    long long s_total = 0, l_total = 0;
-    std::vector<int> kf_map_idx, lm_map_idx;
-    std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
-    std::vector<long long> comp_off_h, comp_loff_h;
-    int64_t n_lfactor_tiles = 0, n_trail_updates = 0;  // symbolic factorisation (all components)
-    vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
-    vx::DevBuf pose0, pose, intr, kf_flags, kf_comp, kf_local, lm0, lm, obs_uv, obs_kf, obs_lm, lm_ptr, lm_blk,
-        kf_ptr, kf_obs, blk_ij, blk_ptr, pairs, comp_kf_ptr, comp_kf, comp_off, comp_loff, comp_np, comp_hdr, tl, wy,
-        lm_sys,
-        red, red_sum, L, Linv, dx, state;
-    bool ran = false;
-};
+// (struct vx_sba_plan: sba_plan.hpp)
 
 namespace vx {
 namespace {
@@ -1193,6 +1174,30 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     p->n_blocks = (int)bij.size();
     p->n_pairs = (int64_t)prs.size();
     lap("blocks");
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = upload(c, p->pose0, pose0))) return rc;
+    if ((rc = upload(c, p->intr, intr))) return rc;
+    if ((rc = upload(c, p->lm0, lm0))) return rc;
+    if ((rc = upload(c, p->obs_uv, ouv))) return rc;
+    if ((rc = upload(c, p->obs_kf, okf))) return rc;
+    if ((rc = upload(c, p->obs_lm, olm))) return rc;
+    if ((rc = upload(c, p->lm_ptr, lptr))) return rc;
+    if ((rc = upload(c, p->lm_blk, blk))) return rc;
+    if ((rc = upload(c, p->kf_ptr, kptr))) return rc;
+    if ((rc = upload(c, p->kf_obs, kobs))) return rc;
+    if ((rc = upload(c, p->blk_ij, bij))) return rc;
+    if ((rc = upload(c, p->blk_ptr, bptr))) return rc;
+    if ((rc = upload(c, p->pairs, prs))) return rc;
+    rc = sba_plan_finish(c, p, flags, bij);
+    lap("finish");
+    return rc;
+}
+
+}  // namespace
+
+int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, const std::vector<int2>& bij) {
+    const int nk = p->nk, n_opt = p->n_opt;
 
     // ---- connected components of the free keyframes' covisibility graph
     // (over the off-diagonal blocks: two free keyframes share a block exactly when a landmark's
@@ -1240,7 +1245,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     p->l_total = lo;
     p->comp_loff_h = loff;
 
-    lap("components");
+    
 
     // ---- symbolic tile factorisation per component: which 16 x 16 tiles of L are nonzero (the
     // pattern of S's blocks plus Cholesky fill), and per step the panel / trailing-update / back-
@@ -1320,25 +1325,12 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
         }
     }
 
-    lap("symbolic");
+    
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
-    if ((rc = upload(c, p->pose0, pose0))) return rc;
-    if ((rc = upload(c, p->intr, intr))) return rc;
     if ((rc = upload(c, p->kf_flags, flags))) return rc;
     if ((rc = upload(c, p->kf_comp, kcomp))) return rc;
     if ((rc = upload(c, p->kf_local, klocal))) return rc;
-    if ((rc = upload(c, p->lm0, lm0))) return rc;
-    if ((rc = upload(c, p->obs_uv, ouv))) return rc;
-    if ((rc = upload(c, p->obs_kf, okf))) return rc;
-    if ((rc = upload(c, p->obs_lm, olm))) return rc;
-    if ((rc = upload(c, p->lm_ptr, lptr))) return rc;
-    if ((rc = upload(c, p->lm_blk, blk))) return rc;
-    if ((rc = upload(c, p->kf_ptr, kptr))) return rc;
-    if ((rc = upload(c, p->kf_obs, kobs))) return rc;
-    if ((rc = upload(c, p->blk_ij, bij))) return rc;
-    if ((rc = upload(c, p->blk_ptr, bptr))) return rc;
-    if ((rc = upload(c, p->pairs, prs))) return rc;
     if ((rc = upload(c, p->comp_kf_ptr, p->comp_kf_ptr_h))) return rc;
     if ((rc = upload(c, p->comp_kf, p->comp_kf_h))) return rc;
     if ((rc = upload(c, p->comp_off, p->comp_off_h))) return rc;
@@ -1364,10 +1356,10 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     VX_HIP(c, hipMemset(p->dx.p, 0, (size_t)nk * 6 * sizeof(double)));
     VX_HIP(c, p->state.ensure(sizeof(SBAState)));
     VX_HIP(c, hipMemset(p->state.p, 0, sizeof(SBAState)));
-    lap("upload");
     return VX_OK;
 }
 
+namespace {
 // k_sba_solve's LDS for ps panel slots: panel | L_kk^-1 | POTRF columns (2 tiles) | y | slot map
 size_t solve_lds_bytes(int np, int ps) {
     return ((size_t)(ps + 3) * kPanelStride + (size_t)np) * sizeof(double) + (size_t)(np / 16 + 1) * sizeof(int);
@@ -1422,7 +1414,25 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
     return VX_OK;
 }
 
+// the best state of a finished run (LM selection of the last iteration) into the resident rows
+__global__ void k_sba_apply_dmap(const SBAState* st, int nk, int n_opt, const double* pose0, const double* pose,
+                                 const double* lm0, const double* lm, const int* kf_map, const int* lm_map,
+                                 double* map_pose, double* map_pos) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const LMVars& v = st->lm[st->iterations & 1];
+    if (i < nk) {
+        const double* src = (v.sel < 0 ? pose0 : pose + (size_t)v.sel * nk * 8) + 8 * (size_t)i;
+        for (int j = 0; j < 7; ++j) map_pose[7 * (size_t)kf_map[i] + j] = src[j];
+    }
+    if (i < n_opt) {
+        const double* src = (v.sel < 0 ? lm0 : lm + (size_t)v.sel * n_opt * 4) + 4 * (size_t)i;
+        for (int j = 0; j < 3; ++j) map_pos[3 * (size_t)lm_map[i] + j] = src[j];
+    }
+}
+
 }  // namespace
+
+int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba_plan* p);  // ba_lean.hip
 }  // namespace vx
 
 using namespace vx;
@@ -1467,6 +1477,44 @@ int vx_sba_plan_create(vx_ctx* c, const vx_map_view* m, uint64_t ref, int has_re
     return VX_OK;
 }
 
+int vx_sba_plan_create_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_sba_options* opt,
+                            vx_sba_plan** out) {
+    if (!c || !out || !opt || !m || m->c != c)
+        return c ? set_error(c, VX_ERR_INVALID, "vx_sba_plan_create_dmap: bad arguments") : VX_ERR_INVALID;
+    *out = nullptr;
+    if (opt->max_iterations < 0 || opt->max_iterations > kSbaMaxIter)
+        return set_error(c, VX_ERR_INVALID, "max_iterations must be in [0, %d]", kSbaMaxIter);
+    if (opt->fixed_keyframes < 0 || !(opt->lambda_init >= 0.0))
+        return set_error(c, VX_ERR_INVALID, "fixed_keyframes >= 0 and lambda_init >= 0 required");
+    auto* p = new vx_sba_plan();
+    p->c = c;
+    p->opt = *opt;
+    const int rc = build_sba_plan_dmap(c, m, ref, has_ref, p);
+    if (rc) {
+        (void)hipStreamSynchronize(c->stream);
+        delete p;
+        return rc;
+    }
+    *out = p;
+    return VX_OK;
+}
+
+int vx_sba_plan_apply_dmap(vx_ctx* c, vx_sba_plan* p, vx_dmap* m) {
+    if (!c || !p || !m || p->c != c || m->c != c)
+        return c ? set_error(c, VX_ERR_INVALID, "vx_sba_plan_apply_dmap: bad arguments") : VX_ERR_INVALID;
+    if (!p->from_dmap) return set_error(c, VX_ERR_STATE, "plan was not built from a vx_dmap");
+    if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
+    if (p->status != 0 || p->opt.max_iterations == 0) return VX_OK;
+    const int n = std::max(p->nk, p->n_opt);
+    hipLaunchKernelGGL(k_sba_apply_dmap, dim3((n + 255) / 256), dim3(256), 0, c->stream,
+                       (const SBAState*)p->state.as<SBAState>(), p->nk, p->n_opt, (const double*)p->pose0.as<double>(),
+                       (const double*)p->pose.as<double>(), (const double*)p->lm0.as<double>(),
+                       (const double*)p->lm.as<double>(), (const int*)p->kf_map_dev.as<int>(),
+                       (const int*)p->lm_map_dev.as<int>(), m->kf_pose.as<double>(), m->lm_pos.as<double>());
+    VX_LAUNCH_CHECK(c, "k_sba_apply_dmap");
+    return VX_OK;
+}
+
 int vx_sba_plan_run_async(vx_ctx* c, vx_sba_plan* p) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
     if (p->shard_count > 1 || p->status != 0) return sba_run(c, p);  // (RCCL calls stay outside graphs)
@@ -1477,6 +1525,7 @@ int vx_sba_plan_run_async(vx_ctx* c, vx_sba_plan* p) {
 int vx_sba_plan_fetch(vx_ctx* c, vx_sba_plan* p, vx_map_view* m, vx_sba_stats* st) {
     if (!c || !p || p->c != c) return VX_ERR_INVALID;
     if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
+    if (m && p->from_dmap) return set_error(c, VX_ERR_STATE, "dmap plan: scatter with vx_sba_plan_apply_dmap");
     vx_sba_stats s{};
     s.status = p->status;
     s.n_window_kf = p->n_window_kf;

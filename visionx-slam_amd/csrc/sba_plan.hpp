@@ -1,0 +1,44 @@
+// sba_plan.hpp — the Schur-complement BA plan (vx_sba_plan) shared by its host build (sba.hip,
+// build_sba_plan, from a vx_map_view snapshot) and its device build from the resident map
+// (ba_lean.hip, vx_sba_plan_create_dmap).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "vx_internal.hpp"
+
+struct vx_sba_plan {
+    vx_ctx* c = nullptr;
+    vx_sba_options opt{};
+
+    int status = 1;
+    int shard_rank = 0, shard_count = 1;
+    int n_window_kf = 0, n_landmarks_global = 0;
+    int nk = 0, n_opt = 0, n_lm = 0, n_oo = 0, n_obs = 0;
+    int64_t n_pairs = 0;
+    int n_blocks = 0, n_lm_blocks = 0, n_comp = 0, max_np = 0;
+    int max_panel = 1;  // most panel tiles (rhs row included) of one column of any component's factor
+    long long s_total = 0, l_total = 0;
+    std::vector<int> kf_map_idx, lm_map_idx;
+    std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
+    std::vector<long long> comp_off_h, comp_loff_h;
+    int64_t n_lfactor_tiles = 0, n_trail_updates = 0;  // symbolic factorisation (all components)
+    vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
+    vx::DevBuf pose0, pose, intr, kf_flags, kf_comp, kf_local, lm0, lm, obs_uv, obs_kf, obs_lm, lm_ptr, lm_blk,
+        kf_ptr, kf_obs, blk_ij, blk_ptr, pairs, comp_kf_ptr, comp_kf, comp_off, comp_loff, comp_np, comp_hdr, tl, wy,
+        lm_sys,
+        red, red_sum, L, Linv, dx, state;
+    bool ran = false;
+    bool from_dmap = false;
+    vx::DevBuf lm_map_dev, kf_map_dev;  // dmap plans: slot -> resident landmark row, window row -> keyframe row
+};
+
+
+namespace vx {
+constexpr int kSbaLmThreads = 256;  // k_sba_lm: max observations (and landmarks) per workgroup
+// The tail every SBA plan build ends with: p->nk / n_opt / n_oo / n_lm / n_blocks / n_pairs and the
+// observation, landmark, pair and block tables on the device; flags (bit0 camera, bit1 fixed) and
+// the block list (i, j) on the host.  Covisibility components, the symbolic tile factorisation, their
+// uploads and the run buffers.
+int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, const std::vector<int2>& bij);
+}  // namespace vx
