@@ -30,6 +30,7 @@
 // The step keeps the reference's sign (b = -J^T e, :156 and :224): this is a drop-in, not a fix.
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <type_traits>
@@ -204,6 +205,10 @@ __global__ void k_ba_reset(BAArgs a) {
         s->iterations = 0;
         for (int k = 0; k < 16; ++k) { s->cost[k] = 0; s->obs[k] = 0; }
     }
+}
+
+__device__ __forceinline__ int mbcnt_lo_hi(unsigned long long m) {  // lanes below this one in m
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 
 // Camera-frame point of pose (R, t) (T_cw * p, projection.h:16): R p + t as three FMA chains (the
@@ -702,6 +707,45 @@ constexpr size_t fused_lds(int ft) {
            (size_t)ft * sizeof(int) + (size_t)3 * ft * sizeof(double) + (size_t)2 * (ft / 64) * sizeof(double);
 }
 static_assert(fused_lds(kFTLarge) <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's 160 KB per workgroup");
+// compacted pose stage (kCmp): per wave a ring of kQ accepted observations, kQRec doubles each
+constexpr int kQ = 128, kQRec = 8;
+constexpr size_t fused_lds_cmp(int ft) { return fused_lds(ft) + (size_t)(ft / 64) * kQ * kQRec * sizeof(double); }
+static_assert(fused_lds_cmp(kFTSmall) <= 160 * 1024, "k_ba_iter (compacted) LDS exceeds 160 KB");
+
+// The Jacobian / normal-equation half of pose_obs_accum for one accepted observation given its
+// camera-frame point (xx, yy, zz), 1 / z, residual and weight (the gate already passed): the same
+// FMA chains as the branch-free form (terms 0-26; cost and count are added at the gate).
+__device__ __forceinline__ void pose_obs_terms(const double* C, double xx, double yy, double zz, double inv_z,
+                                               double e0, double e1, double w, double* v) {
+    const double fx = C[0], fy = C[1];
+    const double x = xx * inv_z, y = yy * inv_z;
+    const double jp0 = fx * inv_z, jp2 = -jp0 * x, jp4 = fy * inv_z, jp5 = -jp4 * y;
+    const double J0[6] = {jp0, 0.0, jp2, jp2 * yy, fma(jp0, zz, -jp2 * xx), -jp0 * yy};
+    const double J1[6] = {0.0, jp4, jp5, fma(jp5, yy, -jp4 * zz), -jp5 * xx, jp4 * xx};
+    double wJ0[6], wJ1[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        wJ0[r] = w * J0[r];
+        wJ1[r] = w * J1[r];
+    }
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) {
+            const bool u0 = r != 1 && c != 1, u1 = r != 0 && c != 0;
+            double acc = v[hidx(r, c)];
+            if (u0) acc = fma(wJ0[r], J0[c], acc);
+            if (u1) acc = fma(wJ1[r], J1[c], acc);
+            v[hidx(r, c)] = acc;
+        }
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        double acc = v[21 + r];
+        if (r != 1) acc = fma(-wJ0[r], e0, acc);
+        if (r != 0) acc = fma(-wJ1[r], e1, acc);
+        v[21 + r] = acc;
+    }
+}
 
 // trace build: phases of the it == 1 launch only (the last launch of a run has no pose stage)
 #define FKT(slot)                              \
@@ -709,7 +753,7 @@ static_assert(fused_lds(kFTLarge) <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's
         if (!kPro && it == 1) VX_KT(slot);     \
     } while (0)
 
-template <bool kPro, int kFT>
+template <bool kPro, int kFT, bool kCmp = false>
 __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) {
     constexpr int kFW = kFT / 64;  // waves per workgroup
     // per-entry pose copies (f.epose) and fused-order landmark positions (f.lpos) in the 512-thread
@@ -737,6 +781,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     int* tcount = reinterpret_cast<int*>(terms + 9 * kFT);
     double* lpos = terms + 9 * kFT + kFT / 2;            // [kFT][3] (after kFT ints)
     double* red = lpos + 3 * kFT;                        // [2][kFW]
+    double* qbuf = red + 2 * kFW;                        // (kCmp) [kFW][kQ][kQRec] accepted observations
     const int tid = threadIdx.x, b = blockIdx.x, wv = tid >> 6, lane = tid & 63;
     const size_t base = (size_t)b * kFT;
     const int4* KE = f.kent + (size_t)b * kFK * 2;
@@ -967,6 +1012,68 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         double v[kStride];
 #pragma unroll
         for (int t = 0; t < kStride; ++t) v[t] = 0.0;
+        if constexpr (kCmp) {
+            // Projection and gate (local_ba.cpp:131-146) for every observation; the Jacobian and
+            // normal-equation half (:148-159) only for the accepted ones, 64 at a time from a per-wave
+            // ring in LDS: after the first iterations most observations fail the gate (the
+            // reference's step sign grows the residuals), so most rounds skip that half.  Accepted
+            // observations keep their order within a lane slot only up to the summation order of
+            // the terms (the tolerance-level change documented in DESIGN.md §2).
+            double* qw = qbuf + (size_t)wv * kQ * kQRec;
+            int qh = 0, qn = 0;  // ring head (next write) and queued count (wave-uniform)
+            auto drain = [&](int n) {  // terms of the n oldest queued observations
+                const int slot = (qh - qn + lane + kQ) & (kQ - 1);
+                const double4 r0 = *reinterpret_cast<const double4*>(qw + (size_t)slot * kQRec);
+                const double4 r1 = *reinterpret_cast<const double4*>(qw + (size_t)slot * kQRec + 4);
+                pose_obs_terms(C, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lane < n ? r1.z : 0.0, v);
+                qn -= n;
+            };
+            for (int q = 0; q < nr; ++q, ++r) {
+                const double2 uv = u0;
+                const double4 P4 = p0;
+                if (r + 1 < wrounds) {
+                    u0 = f.pobs_uv[wstart + 64 * (r + 1) + lane];
+                    p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
+                }
+                const bool valid = e.z + 64 * q + lane < e.w;
+                const int code = (int)P4.w;
+                const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]} : D3{P4.x, P4.y, P4.z};
+                const D3 pc = rt_apply(R, T + 4, P);
+                const bool front = pc.z > 1e-6;
+                const double inv_z = frcp(front ? pc.z : 1.0);
+                const double e0 = uv.x - (C[0] * (pc.x * inv_z) + C[2]);
+                const double e1 = uv.y - (C[1] * (pc.y * inv_z) + C[3]);
+                const double e2 = e0 * e0 + e1 * e1;
+                const bool ok = valid && front && !(e2 > a.max_err2);
+                const double w = ok ? (e2 > a.huber2 ? a.huber * frsq(e2) : 1.0) : 0.0;
+                v[27] = fma(w, e2, v[27]);
+                v[28] += ok ? 1.0 : 0.0;
+                const unsigned long long m = __ballot(ok);
+                const int slot = ok ? ((qh + mbcnt_lo_hi(m)) & (kQ - 1)) : -1;
+                if (ok) {
+                    double4* rec = reinterpret_cast<double4*>(qw + (size_t)slot * kQRec);
+                    rec[0] = make_double4(pc.x, pc.y, pc.z, inv_z);
+                    rec[1] = make_double4(e0, e1, w, 0.0);
+                }
+                const int na = __popcll(m);
+                qh = (qh + na) & (kQ - 1);
+                qn += na;
+                if (qn >= 64) {
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    drain(64);
+                }
+            }
+            if (qn > 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                drain(qn);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // (the ring is reused by the next entry)
+            __builtin_amdgcn_wave_barrier();
+        } else {
         for (int q = 0; q < nr; ++q, ++r) {
             const double2 uv = u0;
             const double4 P4 = p0;
@@ -981,6 +1088,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                                        : D3{P4.x, P4.y, P4.z};
                 pose_obs_accum<kFT == kFTSmall>(a, T, R, C, P, uv, v, valid);
             }
+        }
         }
         if (j == wv) FKT(7);
         const double tot = wave_sum32(v);
@@ -1748,18 +1856,34 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
 }
 
 // the fused path's launches: prologue (iteration 0's pose stage, it = -1) or k_ba_iter(it)
+// $VX_BA_COMPACT=0: the 512-thread iterations without the compacted pose stage (A/B runs)
+bool ba_compact() {
+    static const bool on = [] {
+        const char* e = std::getenv("VX_BA_COMPACT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 template <int kFT>
 int fused_launch_t(vx_ctx* c, vx_ba_plan* p, const BAArgs& a, const FusedArgs& f, int it) {
     constexpr int lds = (int)fused_lds(kFT);
+    constexpr int lds_c = (int)fused_lds_cmp(kFTSmall);
     static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<true, kFT>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false, kFT>),
                                                      hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false, kFTSmall, true>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_c);
     VX_HIP(c, a0);
     VX_HIP(c, a1);
+    VX_HIP(c, a2);
     if (it < 0)
         VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
                          a, f, -1));
+    else if (kFT == kFTSmall && ba_compact())
+        VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false, kFTSmall, true>, dim3(p->f_blocks), dim3(kFTSmall),
+                         (uint32_t)lds_c, c->stream, a, f, it));
     else
         VX_HIP(c, launch(c, kStBaIter, k_ba_iter<false, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
                          a, f, it));
