@@ -137,6 +137,22 @@ def stage_bytes(stage, geo, counts):
     return None
 
 
+FP64_PEAK_TFS = 78.6  # MI355X FP64 vector rate (half the 157.3 TF FP32 vector peak, MI355X_MICROARCH.md)
+
+
+def stage_flops(stage, counts):
+    """FP64 operations of ONE fused LocalBA launch: per pose-stage observation the
+    projection, gate, Huber weight, 2x6 Jacobian and the 27 normal-equation terms (~132 flops, every
+    observation issued by the branch-free form); per landmark-stage observation projection, 2x3
+    Jacobian and 9 terms (~80); per landmark the 3x3 solve (~50); per keyframe entry the 6x6 block
+    solve and the SE(3) update (~400)."""
+    if stage in ("ba_iter", "ba_prologue"):
+        lm = stage == "ba_iter"
+        return (132 * counts["n_pose_obs"] + (80 * counts["n_lm_obs"] + 50 * counts["n_opt"] if lm else 0) +
+                400 * counts["n_kf"])
+    return None
+
+
 # ----------------------------------------------------------------------------- drop-in LocalBA
 def per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam):
     """What one drop-in LocalBA::Optimize() (local_ba.cpp:66-249) costs end to end, host clock,
@@ -845,6 +861,12 @@ def main():
                         "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_ms * 1e3, 2),
                         "launches_per_step": round(dom_prof[1] / args.steps, 2),
                         "pass_ms_per_step": round(1e3 * elapsed_ev / args.steps, 4)}
+            fl = stage_flops(dominant, counts)
+            if fl:
+                tfs = fl / (avg_ms * 1e-3) / 1e12
+                roofline.update({"flops_per_launch": int(fl), "fp64_achieved_tflops": round(tfs, 4),
+                                 "fp64_peak_tflops": FP64_PEAK_TFS, "fp64_frac": round(tfs / FP64_PEAK_TFS, 5),
+                                 "note": "latency-bound: neither HBM nor FP64 throughput binds (DESIGN.md §7)"})
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if roofline and os.path.exists(pmc):
         try:

@@ -15,8 +15,13 @@ from vxslam import synth  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 ctx = vxslam.Context(0)
-for cfg, (nk, nl, ns) in [("C3", synth.ba_config("C3")), ("C5", synth.ba_config("C5"))]:
-    m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
+CFGS = [("C3", synth.ba_config("C3"), 0.0), ("C5", synth.ba_config("C5"), 0.0),
+        ("C5-connected", synth.ba_config("C5"), 0.03)]  # (round 4: the rig as one covisibility component)
+only = os.environ.get("SBA_CFGS")
+for cfg, (nk, nl, ns), cf in CFGS:
+    if only and cfg not in only.split(","):
+        continue
+    m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns, cross_frac=cf)
     opts = vxslam.default_sba_options(window=nk, iters=8)
     builds = []
     for rep in range(3):  # the first build also allocates the plan's device buffers
