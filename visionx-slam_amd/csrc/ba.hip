@@ -1025,7 +1025,11 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 const int slot = (qh - qn + lane + kQ) & (kQ - 1);
                 const double4 r0 = *reinterpret_cast<const double4*>(qw + (size_t)slot * kQRec);
                 const double4 r1 = *reinterpret_cast<const double4*>(qw + (size_t)slot * kQRec + 4);
-                pose_obs_terms(C, r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, lane < n ? r1.z : 0.0, v);
+                // lanes past n read stale ring entries (or never-written LDS): finite stand-ins with
+                // weight 0, so their terms are exactly +-0.0
+                const bool use = lane < n;
+                pose_obs_terms(C, use ? r0.x : 0.0, use ? r0.y : 0.0, use ? r0.z : 1.0, use ? r0.w : 1.0,
+                               use ? r1.x : 0.0, use ? r1.y : 0.0, use ? r1.z : 0.0, v);
                 qn -= n;
             };
             for (int q = 0; q < nr; ++q, ++r) {
