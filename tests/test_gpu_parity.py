@@ -537,3 +537,51 @@ def test_failed_plan_build_then_destroy(monkeypatch):
     p.close()
     dm.close()
     c.close()
+
+
+def test_seq_replay_matches_direct_calls(ctx, oracle):
+    """vx_seq: a recorded list of async calls over two contexts (extract into a slot, event record /
+    wait across the contexts, match, a LocalBA plan run) replayed by vx_seq_run gives exactly what the
+    same calls made one by one give — and replays again identically (the bench's timed steps)."""
+    import vxslam
+    import torch
+
+    frames = synth.make_frames(0x5E9, 2, 480, 640)
+    fd = torch.from_numpy(frames).cuda()
+    p = _orb_params(vxslam, 1500)
+    e, b = vxslam.Context(0), vxslam.Context(0)
+    m = synth.make_ba_map(0x5E9, 10, 2000)
+    plan = b.ba_plan(m, vxslam.default_ba_options(window=10))
+    ev = e.event()
+    sq = vxslam.Seq()
+    for i in range(2):
+        sq.extract(e, p, fd[i].data_ptr(), 640, 480, 3, 640 * 3, i)
+    sq.match(e, e.slot_device(0), e.slot_device(1), 0.8)
+    sq.record(e, ev)
+    sq.wait(b, ev)
+    sq.ba_run(b, plan)
+    assert len(sq) == 6
+    for rep in range(3):
+        sq.run()
+        e.synchronize()
+        b.synchronize()
+        k0, d0 = e.orb_fetch(0)
+        k1, d1 = e.orb_fetch(1)
+        kc0, dc0 = oracle.orb_extract(frames[0], 1500)
+        assert np.array_equal(k0, kc0) and np.array_equal(d0, dc0)
+        assert np.array_equal(e.match_fetch(), oracle.match(d0, d1))
+        mm = m.copy()
+        st = plan.fetch(mm)
+        if rep == 0:
+            ref = (st.iterations, list(st.obs), mm["kf_pose"].copy(), mm["lm_pos"].copy())
+        else:
+            assert (st.iterations, list(st.obs)) == ref[:2]
+            assert np.array_equal(mm["kf_pose"], ref[2]) and np.array_equal(mm["lm_pos"], ref[3])
+    # a failing call stops the replay and is reported
+    bad = vxslam.Seq()
+    bad.extract(e, p, fd[0].data_ptr(), 640, 480, 2, 640 * 3, 0)  # 2 channels: VX_ERR_INVALID
+    with pytest.raises(vxslam.VxError):
+        bad.run()
+    for x in (sq, bad, plan, ev):
+        x.close()
+    e.close(), b.close()
