@@ -534,6 +534,8 @@ def main():
     ap.add_argument("--frames-per-step", type=int, default=0,
                     help="frames per timed step (default: four times the extraction contexts with --streams 3, "
                          "i.e. four rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
+    ap.add_argument("--seq-threads", type=int, default=1,
+                    help="> 1: each context's recorded calls replayed on a host thread of its own (vx_seq_set_threads)")
     ap.add_argument("--no-seq", action="store_true",
                     help="timed steps through per-frame binding calls instead of one recorded vx_seq per step")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),
@@ -774,8 +776,11 @@ def main():
                 sq.record(mx, ev_m[i % (4 * E)])
                 sq.wait(bctx, ev_m[i % (4 * E)])
                 sq.ba_run(bctx, plan)
+            if args.seq_threads > 1:
+                sq.set_threads(args.seq_threads)
             seqs.append(sq)
-        host_path = f"vx_seq: one C call per step ({n_seq} recorded phases of {F} frames, {len(seqs[0])} calls each)"
+        host_path = (f"vx_seq: one C call per step ({n_seq} recorded phases of {F} frames, {len(seqs[0])} calls each"
+                     + (", one host thread per context)" if args.seq_threads > 1 else ")"))
 
         def fstep(i):  # noqa: F811
             seqs[i % n_seq].run()

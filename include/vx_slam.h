@@ -581,6 +581,11 @@ int vx_seq_match(vx_seq* seq, vx_ctx* ctx, const uint8_t* d_query, const int32_t
 int vx_seq_ba_run(vx_seq* seq, vx_ctx* ctx, vx_ba_plan* plan);
 int vx_seq_length(const vx_seq* seq);
 int vx_seq_run(vx_seq* seq, int* failed_op);
+/* threads > 1: vx_seq_run replays each context's calls on a host thread of its own (persistent
+ * workers, one per context after the first), keeping on the host every cross-context order the
+ * device semantics depend on (a wait after the record it follows in the sequence; a record after the
+ * waits on the event's previous record).  1 (default): one thread, the recorded order. */
+int vx_seq_set_threads(vx_seq* seq, int threads);
 
 /* ---------------------------------------------------------------- multi-GPU (RCCL over xGMI) */
 int vx_comm_unique_id(uint8_t* out_128);

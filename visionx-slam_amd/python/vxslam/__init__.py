@@ -92,7 +92,7 @@ EXPORTS = [
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run", "vx_ba_optimize_dmap",
     "vx_ba_dmap_results", "vx_sba_plan_create_dmap", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
-    "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run",
+    "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run", "vx_seq_set_threads",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
     "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
     "vx_orb_get_order", "vx_orb_set_debug", "vx_orb_debug_read", "vx_test_retain_best",
@@ -173,6 +173,7 @@ def lib():
         L.vx_seq_ba_run.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.vx_seq_length.argtypes = [C.c_void_p]
         L.vx_seq_run.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+        L.vx_seq_set_threads.argtypes = [C.c_void_p, C.c_int]
         L.vx_ba_shard_of.restype = C.c_uint32
         L.vx_ba_shard_of.argtypes = [C.c_uint64, C.c_int]
         _lib = L
@@ -788,6 +789,11 @@ class Seq:
 
     def __len__(self):
         return lib().vx_seq_length(self._h)
+
+    def set_threads(self, n: int):
+        """vx_seq_set_threads: > 1 replays each context's calls on a host thread of its own."""
+        if lib().vx_seq_set_threads(self._h, int(n)) != VX_OK:
+            raise VxError(VX_ERR_INVALID, "vx_seq_set_threads")
 
     def run(self):
         bad = C.c_int(-1)
