@@ -319,9 +319,13 @@ __global__ __launch_bounds__(kT) void k_lb_lfill(LeanArgs a) {
         }
     }
     if (i < n_opt) {  // landmark-stage workgroups: slot s -> (lobs_ptr[s] + s) / q
+        // q = 512 - (most landmark-stage observations of one landmark, <= nk <= 255): consecutive
+        // keys differ by <= q, so no workgroup is empty, and a workgroup holds < q landmarks and
+        // <= q - 1 + that many <= 511 observations (a.q = 512 - nk sizes the host's capacity grid)
+        const int q = kBaLmBlock - a.dyn[kDynMaxObs];
         const int s = (int)i;
-        const int b = (a.lobs_ptr[s] + s) / a.q;
-        const int bp = s ? (a.lobs_ptr[s - 1] + s - 1) / a.q : -1;
+        const int b = (a.lobs_ptr[s] + s) / q;
+        const int bp = s ? (a.lobs_ptr[s - 1] + s - 1) / q : -1;
         if (b != bp) {
             a.lm_blk[2 * b] = s;
             a.lm_blk[2 * b + 1] = a.lobs_ptr[s];
