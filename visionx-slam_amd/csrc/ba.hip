@@ -1863,8 +1863,9 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
 // $VX_BA_COMPACT=0: the 512-thread iterations without the compacted pose stage (A/B runs)
 bool ba_compact() {
     static const bool on = [] {
+        // off by default: measured 0.0559 vs 0.0540 ms per C3 window (profiles/r04), VX_BA_COMPACT=1 on
         const char* e = std::getenv("VX_BA_COMPACT");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }

@@ -2985,6 +2985,7 @@ int vx_orb_extract(vx_ctx* c, const vx_orb_params* p, const uint8_t* img, int w,
     VX_HIP(c, hipMemcpy2DAsync(c->img_in.p, packed, img, (size_t)stride, packed, h, hipMemcpyHostToDevice,
                                c->stream));
     rc = orb_enqueue(c, c->img_in.as<uint8_t>(), channels, (int64_t)packed, 0);
+    c->scratch_slot = rc ? -1 : 0;
     if (rc) return rc;
     return vx_orb_fetch(c, 0, out_kp, out_desc, cap, n_out);
 }

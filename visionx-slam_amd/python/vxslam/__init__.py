@@ -1039,8 +1039,9 @@ def dmap_load(dmap: DMap, m, kf_rows=None):
 
 
 def map_reorder(m, kf_order, lm_order):
-    """The snapshot with its keyframe / landmark rows permuted (per-landmark observation lists kept)."""
-    out = dict(m)
+    """The snapshot with its keyframe / landmark rows permuted (per-landmark observation lists kept);
+    the result has the input's type (a synth.BAMap stays one, so its deep .copy() is kept)."""
+    out = type(m)(m)
     fp = m["kf_feat_ptr"]
     cnt = np.diff(fp)[kf_order]
     out["kf_id"] = m["kf_id"][kf_order].copy()
