@@ -281,6 +281,33 @@ def test_dmap_culling_and_reobservation(ctx, monkeypatch, compact):
     mir.obs_lm = np.append(mir.obs_lm, l)
     mir.obs_rows.append(len(m["obs_kf_id"]) - 1)
     check()
+
+    # --- RemoveObservation of live pairs after the rows were compacted (compacted: the pairs are
+    #     found through their observation ids, whose rows moved) and a re-observation of one of them
+    live = set(mir.lm_rows)
+    cand = [r for r in mir.obs_rows if int(mir.obs_lm[r]) in live]
+    gone = [int(r) for r in rng.choice(np.asarray(cand), 12, replace=False)]
+    for r in gone:
+        l, kq = int(mir.obs_lm[r]), int(m["obs_kf_id"][r])
+        q = int(np.nonzero(m["kf_id"] == kq)[0][0])
+        clear_features(q, np.array([int(m["obs_feat_idx"][r])]))
+    dm.remove_observations(m["lm_id"][[int(mir.obs_lm[r]) for r in gone]],
+                           np.array([int(m["obs_kf_id"][r]) for r in gone], np.uint64))
+    mir.obs_rows = [r for r in mir.obs_rows if r not in set(gone)]
+    check()
+    r = gone[0]
+    l, kq = int(mir.obs_lm[r]), int(m["obs_kf_id"][r])
+    q = int(np.nonzero(m["kf_id"] == kq)[0][0])
+    g0 = m["kf_feat_ptr"][q]
+    fr = int(m["obs_feat_idx"][r])
+    m["feat_lm_id"][g0 + fr], m["feat_flags"][g0 + fr] = m["lm_id"][l], 1
+    dm.set_features(kq, np.array([fr], np.int32), m["lm_id"][[l]], np.array([1], np.uint8))
+    dm.add_observations(m["lm_id"][[l]], [kq], [fr])
+    m["obs_kf_id"] = np.append(m["obs_kf_id"], np.uint64(kq))
+    m["obs_feat_idx"] = np.append(m["obs_feat_idx"], np.uint64(fr))
+    mir.obs_lm = np.append(mir.obs_lm, l)
+    mir.obs_rows.append(len(m["obs_kf_id"]) - 1)
+    check()
     dm.close()
 
 

@@ -49,17 +49,20 @@ int append(vx_ctx* c, DevBuf& d, int64_t at, const T* h, int64_t n) {
     return VX_OK;
 }
 
-// scatter rows of `width` elements: dst[idx[i] * width + j] = src[i * width + j]
+// scatter rows of `width` elements: dst[r(i) * width + j] = src[i * width + j], r(i) = idx[i], or
+// id_row[idx[i]] when idx holds observation ids
 template <class T>
-__global__ void k_scatter_rows(T* dst, const int64_t* idx, const T* src, int n, int width) {
+__global__ void k_scatter_rows(T* dst, const int64_t* idx, const int64_t* id_row, const T* src, int n, int width) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)n * width) return;
     const int64_t i = e / width, j = e - i * width;
-    dst[idx[i] * width + j] = src[e];
+    const int64_t r = id_row ? id_row[idx[i]] : idx[i];
+    dst[r * width + j] = src[e];
 }
 
 template <class T>
-int scatter(vx_ctx* c, DevBuf& dst, const std::vector<int64_t>& idx, const T* src, int width) {
+int scatter(vx_ctx* c, DevBuf& dst, const std::vector<int64_t>& idx, const T* src, int width,
+            const DevBuf* id_row = nullptr) {
     const int n = (int)idx.size();
     if (!n) return VX_OK;
     // one staging allocation: indices then values
@@ -69,7 +72,8 @@ int scatter(vx_ctx* c, DevBuf& dst, const std::vector<int64_t>& idx, const T* sr
     VX_HIP(c, hipMemcpyAsync(tmp.p, idx.data(), ib, hipMemcpyHostToDevice, c->stream));
     VX_HIP(c, hipMemcpyAsync(tmp.as<uint8_t>() + ib, src, vb, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(k_scatter_rows<T>, dim3(grid((long long)n * width)), dim3(kT), 0, c->stream, dst.as<T>(),
-                       tmp.as<int64_t>(), reinterpret_cast<const T*>(tmp.as<uint8_t>() + ib), n, width);
+                       tmp.as<int64_t>(), id_row ? (const int64_t*)id_row->as<int64_t>() : nullptr,
+                       reinterpret_cast<const T*>(tmp.as<uint8_t>() + ib), n, width);
     VX_LAUNCH_CHECK(c, "k_scatter_rows");
     VX_HIP(c, hipStreamSynchronize(c->stream));  // tmp is freed on return
     return VX_OK;
@@ -96,42 +100,79 @@ __global__ void k_csr_fill(const int* perm, int64_t n, const uint64_t* okf_in, c
     if (i <= n_lm) optr[i] = scan[i];
 }
 
+// live row flags: not tombstoned (RemoveObservation) and its landmark not removed
+__global__ void k_live_rows(const int* obs_lm, const uint8_t* lm_bad, int64_t n, int* flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int l = obs_lm[i];
+    flag[i] = (l != kDeadObs && lm_bad[l] != kLmRemoved) ? 1 : 0;
+}
+// live row i -> row pos[i] of the target arrays (order kept); every id re-pointed (-1: dropped)
+__global__ void k_compact_rows(const int* flag, const int* pos, int64_t n, const int* lm, const uint64_t* kf,
+                               const uint64_t* fi, const int64_t* id, int* lm2, uint64_t* kf2, uint64_t* fi2,
+                               int64_t* id2, int64_t* id_row) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t o = id[i];
+    if (!flag[i]) {
+        id_row[o] = -1;
+        return;
+    }
+    const int64_t r = pos[i];
+    lm2[r] = lm[i];
+    kf2[r] = kf[i];
+    fi2[r] = fi[i];
+    id2[r] = o;
+    id_row[o] = r;
+}
+
 // Drops the dead observation rows (RemoveObservation tombstones and the pairs of removed
 // landmarks), keeping the live rows in order — so every landmark's list and the CSR stay as they
-// were — and re-points / erases obs_index entries.  Host round trip of the three observation arrays:
-// amortised, it runs only once dead rows exceed a quarter of the list.
+// were — on the device: flags, a scan, one gather into the second set of arrays, which are then
+// swapped in; id_row re-points every observation id, so obs_index is untouched.  The live row
+// count is the host's n_obs_live (no read-back).  Amortised: it runs once dead rows exceed a
+// quarter of the list.
 int dmap_compact(vx_ctx* c, vx_dmap* m) {
     const int64_t n = m->n_obs;
-    std::vector<int> lm(n);
-    std::vector<uint64_t> kf(n), fi(n);
-    VX_HIP(c, hipMemcpyAsync(lm.data(), m->obs_lm.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
-    VX_HIP(c, hipMemcpyAsync(kf.data(), m->obs_kf.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
-    VX_HIP(c, hipMemcpyAsync(fi.data(), m->obs_fi.p, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
-    VX_HIP(c, hipStreamSynchronize(c->stream));
-    std::vector<int64_t> row(n, -1);
-    int64_t k = 0;
-    for (int64_t i = 0; i < n; ++i)
-        if (lm[i] != kDeadObs && !m->lm_removed[lm[i]]) {
-            row[i] = k;
-            lm[k] = lm[i];
-            kf[k] = kf[i];
-            fi[k] = fi[i];
-            ++k;
-        }
-    if (k) {
-        VX_HIP(c, hipMemcpyAsync(m->obs_lm.p, lm.data(), (size_t)k * 4, hipMemcpyHostToDevice, c->stream));
-        VX_HIP(c, hipMemcpyAsync(m->obs_kf.p, kf.data(), (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
-        VX_HIP(c, hipMemcpyAsync(m->obs_fi.p, fi.data(), (size_t)k * 8, hipMemcpyHostToDevice, c->stream));
-        VX_HIP(c, hipStreamSynchronize(c->stream));
+    hipStream_t s = c->stream;
+    VX_HIP(c, m->cflag.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    VX_HIP(c, m->cpos.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    const int64_t k = m->n_obs_live;
+    const size_t keep = (size_t)std::max<int64_t>(k, 1);
+    VX_HIP(c, m->obs_lm2.ensure(keep * 4));
+    VX_HIP(c, m->obs_kf2.ensure(keep * 8));
+    VX_HIP(c, m->obs_fi2.ensure(keep * 8));
+    VX_HIP(c, m->obs_id2.ensure(keep * 8));
+    if (n > 0) {
+        hipLaunchKernelGGL(k_live_rows, dim3(grid(n)), dim3(kT), 0, s, (const int*)m->obs_lm.as<int>(),
+                           (const uint8_t*)m->lm_bad.as<uint8_t>(), n, m->cflag.as<int>());
+        VX_LAUNCH_CHECK(c, "dmap compact flags");
+        size_t bytes = 0;
+        VX_HIP(c, rocprim::exclusive_scan(nullptr, bytes, m->cflag.as<int>(), m->cpos.as<int>(), 0, (size_t)n,
+                                          rocprim::plus<int>(), s));
+        VX_HIP(c, m->tmp.ensure(std::max<size_t>(bytes, 16)));
+        VX_HIP(c, rocprim::exclusive_scan(m->tmp.p, bytes, m->cflag.as<int>(), m->cpos.as<int>(), 0, (size_t)n,
+                                          rocprim::plus<int>(), s));
+        hipLaunchKernelGGL(k_compact_rows, dim3(grid(n)), dim3(kT), 0, s, (const int*)m->cflag.as<int>(),
+                           (const int*)m->cpos.as<int>(), n, (const int*)m->obs_lm.as<int>(),
+                           (const uint64_t*)m->obs_kf.as<uint64_t>(), (const uint64_t*)m->obs_fi.as<uint64_t>(),
+                           (const int64_t*)m->obs_id.as<int64_t>(), m->obs_lm2.as<int>(), m->obs_kf2.as<uint64_t>(),
+                           m->obs_fi2.as<uint64_t>(), m->obs_id2.as<int64_t>(), m->id_row.as<int64_t>());
+        VX_LAUNCH_CHECK(c, "dmap compact rows");
+        // the host's live count must be the device's (8 bytes back; compaction is rare)
+        int tail[2];
+        VX_HIP(c, hipMemcpyAsync(&tail[0], m->cflag.as<int>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+        VX_HIP(c, hipMemcpyAsync(&tail[1], m->cpos.as<int>() + n - 1, 4, hipMemcpyDeviceToHost, s));
+        VX_HIP(c, hipStreamSynchronize(s));
+        if (tail[0] + tail[1] != k)
+            return set_error(c, VX_ERR_STATE, "dmap compaction: %d live rows on the device, %lld on the host",
+                             tail[0] + tail[1], (long long)k);
     }
-    for (auto it = m->obs_index.begin(); it != m->obs_index.end();) {
-        const int64_t r = row[it->second];
-        if (r < 0) {
-            it = m->obs_index.erase(it);
-        } else {
-            it->second = r;
-            ++it;
-        }
+    // (the pointers only: DevBuf frees on destruction, so no temporary DevBuf may hold one)
+    for (auto pr : {std::make_pair(&m->obs_lm, &m->obs_lm2), std::make_pair(&m->obs_kf, &m->obs_kf2),
+                    std::make_pair(&m->obs_fi, &m->obs_fi2), std::make_pair(&m->obs_id, &m->obs_id2)}) {
+        std::swap(pr.first->p, pr.second->p);
+        std::swap(pr.first->bytes, pr.second->bytes);
     }
     m->n_obs = k;
     m->csr_dirty = true;
@@ -278,9 +319,9 @@ int vx_dmap_add_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uin
     // and takes the new feature index
     std::vector<int> a_lm;
     std::vector<uint64_t> a_kf, a_fi;
-    std::vector<int64_t> w_row;
+    std::vector<int64_t> w_row;  // (observation ids)
     std::vector<uint64_t> w_fi;
-    // pairs first seen in this batch -> their new rows; entered into obs_index (and the live counts)
+    // pairs first seen in this batch -> their new rows / ids; entered into obs_index (and the live counts)
     // only once the device rows are written (a failed append leaves the map unchanged)
     std::unordered_map<std::pair<int, uint64_t>, int64_t, vx_dmap::PairHash> fresh;
     std::vector<std::pair<int, uint64_t>> fresh_order;
@@ -309,13 +350,21 @@ int vx_dmap_add_observations(vx_dmap* m, int n, const uint64_t* lm_id, const uin
     if ((rc = append(c, m->obs_lm, m->n_obs, a_lm.data(), na))) return rc;
     if ((rc = append(c, m->obs_kf, m->n_obs, a_kf.data(), na))) return rc;
     if ((rc = append(c, m->obs_fi, m->n_obs, a_fi.data(), na))) return rc;
-    if ((rc = scatter(c, m->obs_fi, w_row, w_fi.data(), 1))) return rc;
+    std::vector<int64_t> a_id(na), a_row(na);
+    for (int64_t j = 0; j < na; ++j) {
+        a_id[j] = m->n_ids + j;
+        a_row[j] = m->n_obs + j;
+    }
+    if ((rc = append(c, m->obs_id, m->n_obs, a_id.data(), na))) return rc;
+    if ((rc = append(c, m->id_row, m->n_ids, a_row.data(), na))) return rc;
+    if ((rc = scatter(c, m->obs_fi, w_row, w_fi.data(), 1, &m->id_row))) return rc;
     for (const auto& key : fresh_order) {
-        m->obs_index.emplace(key, m->n_obs + fresh[key]);
+        m->obs_index.emplace(key, m->n_ids + fresh[key]);
         ++m->lm_obs_live[key.first];
         ++m->n_obs_live;
     }
     m->n_obs += na;
+    m->n_ids += na;
     if (na || !w_row.empty()) m->csr_dirty = true;
     return VX_OK;
 }
@@ -332,7 +381,7 @@ int vx_dmap_remove_observations(vx_dmap* m, int n, const uint64_t* lm_id, const 
             return set_error(c, VX_ERR_INVALID, "unknown landmark %llu", (unsigned long long)lm_id[i]);
         li[i] = it->second;
     }
-    std::vector<int64_t> rows;
+    std::vector<int64_t> rows;  // (observation ids)
     for (int i = 0; i < n; ++i) {
         auto it = m->obs_index.find(std::make_pair(li[i], kf_id[i]));
         if (it == m->obs_index.end()) continue;  // unordered_map::erase of an absent key
@@ -345,7 +394,7 @@ int vx_dmap_remove_observations(vx_dmap* m, int n, const uint64_t* lm_id, const 
     const std::vector<int> dead(rows.size(), kDeadObs);
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
-    if ((rc = scatter(c, m->obs_lm, rows, dead.data(), 1))) return rc;
+    if ((rc = scatter(c, m->obs_lm, rows, dead.data(), 1, &m->id_row))) return rc;
     m->csr_dirty = true;
     return VX_OK;
 }
@@ -376,6 +425,11 @@ int vx_dmap_remove_landmarks(vx_dmap* m, int n, const uint64_t* lm_id) {
     }
     if (rows.empty()) return VX_OK;
     m->n_lm_live -= (int64_t)rows.size();
+    // the removed landmarks' pairs left in obs_index: purged once they outnumber the live ones
+    // (amortised host work, off the plan build)
+    if ((int64_t)m->obs_index.size() > 2 * m->n_obs_live + 4096)
+        for (auto it = m->obs_index.begin(); it != m->obs_index.end();)
+            it = m->lm_removed[it->first.first] ? m->obs_index.erase(it) : std::next(it);
     const std::vector<uint8_t> removed(rows.size(), kLmRemoved);
     VX_HIP(c, hipSetDevice(c->device));
     return scatter(c, m->lm_bad, rows, removed.data(), 1);

@@ -20,9 +20,12 @@ struct vx_dmap {
     std::vector<int> kf_valid_cnt;
     std::vector<uint8_t> feat_flags;
     std::unordered_map<uint64_t, int> kf_index, lm_index;  // live keyframes / landmarks only
-    // (landmark row, keyframe id) -> observation row of the live pair: Landmark::observations_ is
+    // (landmark row, keyframe id) -> observation id of the live pair: Landmark::observations_ is
     // keyed by keyframe id, so AddObservation of a present pair overwrites it in place and
-    // RemoveObservation tombstones it (obs_lm = kDeadObs: skipped by the CSR rebuild)
+    // RemoveObservation tombstones it (obs_lm = kDeadObs: skipped by the CSR rebuild).  Ids are
+    // issued in insertion order and never change; the device table id_row maps each to its current
+    // row, so compacting the rows (on the device) leaves this map alone.  A removed landmark's
+    // pairs stay here (they can no longer be named) until purged with the rest of its kind.
     struct PairHash {
         size_t operator()(const std::pair<int, uint64_t>& k) const {
             uint64_t x = k.second * 0x9e3779b97f4a7c15ull ^ ((uint64_t)(uint32_t)k.first << 1);
@@ -31,6 +34,7 @@ struct vx_dmap {
     };
     std::unordered_map<std::pair<int, uint64_t>, int64_t, PairHash> obs_index;
     int64_t n_lm = 0, n_obs = 0;                 // rows (removed ones included)
+    int64_t n_ids = 0;                           // observation ids issued
     int64_t n_kf_live = 0, n_lm_live = 0, n_obs_live = 0;
     std::vector<int> lm_obs_live;                // live observations per landmark row
     std::vector<uint8_t> lm_removed;             // 1 after Map::RemoveLandmark (row kept as dead storage)
@@ -39,6 +43,8 @@ struct vx_dmap {
     vx::DevBuf feat_uv, feat_lm, feat_fl;        // 2 doubles / u64 / u8 per feature
     vx::DevBuf lm_id, lm_pos, lm_bad;            // u64 / 3 doubles / u8 per landmark
     vx::DevBuf obs_lm, obs_kf, obs_fi;           // i32 landmark index / u64 / u64 per observation
+    vx::DevBuf obs_id, id_row;                   // i64 id per row / i64 row per id (-1: compacted away)
+    vx::DevBuf obs_lm2, obs_kf2, obs_fi2, obs_id2, cflag, cpos;  // compaction targets (swapped in)
     // landmark-major observation CSR (a stable sort of the observation list by landmark index),
     // rebuilt lazily when landmarks or observations were added since the last plan build
     bool csr_dirty = true;
