@@ -12,7 +12,7 @@ import numpy as np
 
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if "k_ba_iter" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-pro = [("ILb1E" in r["Kernel_Name"]) for r in rows]
+pro = [("ILb1E" in r["Kernel_Name"] or "k_ba_iter<true" in r["Kernel_Name"]) for r in rows]
 dur = np.array([(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in rows])
 obs = [int(x) for x in sys.argv[2:]]
 runs, cur = [], None

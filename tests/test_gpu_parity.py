@@ -553,6 +553,9 @@ def test_seq_replay_matches_direct_calls(ctx, oracle):
     m = synth.make_ba_map(0x5E9, 10, 2000)
     plan = b.ba_plan(m, vxslam.default_ba_options(window=10))
     ev = e.event()
+    for i in range(2):  # (the slots exist once an extraction has run into them)
+        e.orb_extract_async(fd[i].data_ptr(), 640, 480, 3, 640 * 3, i, p)
+    e.synchronize()
     sq = vxslam.Seq()
     for i in range(2):
         sq.extract(e, p, fd[i].data_ptr(), 640, 480, 3, 640 * 3, i)

@@ -1088,22 +1088,26 @@ int vx_ba_dmap_results(vx_ctx* c, vx_dmap* m, int cap_kf, int64_t* kf_rows, doub
     if (cap_kf < *n_kf || cap_lm < *n_lm) return set_error(c, VX_ERR_CAPACITY, "need %d keyframes / %d landmarks", *n_kf, *n_lm);
     VX_HIP(c, hipSetDevice(c->device));
     const int nk = L.nk, n = L.n_opt;
-    std::vector<double> pose((size_t)nk * 8), pos((size_t)std::max(n, 1) * 4);
-    std::vector<int> rows(std::max(n, 1));
+    // one pinned staging block (poses, positions, landmark rows), one synchronisation
+    const size_t pose_b = (size_t)nk * 64, pos_b = (size_t)n * 32, rows_b = (size_t)n * 4;
+    VX_HIP(c, L.res_host.ensure(pose_b + pos_b + rows_b + 64, true));
+    double* pose = reinterpret_cast<double*>(L.res_host.p);
+    double* pos = pose + (size_t)nk * 8;
+    int* rows = reinterpret_cast<int*>(pos + (size_t)n * 4);
     const double* dpose;
     const double* dpos;
     if (L.fallback) {
         vx_ba_plan* p = L.fallback;
         dpose = p->kf_pose.as<double>() + (size_t)(L.iterations & 1) * nk * 8;
         dpos = p->lm_pos.as<double>();
-        std::copy(p->lm_map_idx.begin(), p->lm_map_idx.begin() + n, rows.begin());
+        std::copy(p->lm_map_idx.begin(), p->lm_map_idx.begin() + n, rows);
     } else {
         dpose = L.kf_pose.as<double>() + (size_t)(L.iterations & 1) * nk * 8;
         dpos = L.lm_pos.as<double>();
-        if (n) VX_HIP(c, hipMemcpyAsync(rows.data(), L.inv.p, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+        if (n) VX_HIP(c, hipMemcpyAsync(rows, L.inv.p, rows_b, hipMemcpyDeviceToHost, c->stream));
     }
-    VX_HIP(c, hipMemcpyAsync(pose.data(), dpose, pose.size() * 8, hipMemcpyDeviceToHost, c->stream));
-    if (n) VX_HIP(c, hipMemcpyAsync(pos.data(), dpos, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipMemcpyAsync(pose, dpose, pose_b, hipMemcpyDeviceToHost, c->stream));
+    if (n) VX_HIP(c, hipMemcpyAsync(pos, dpos, pos_b, hipMemcpyDeviceToHost, c->stream));
     VX_HIP(c, hipStreamSynchronize(c->stream));
     for (int r = 0; r < nk; ++r) {
         if (kf_rows) kf_rows[r] = L.win_rows[r];

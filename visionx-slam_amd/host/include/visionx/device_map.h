@@ -58,8 +58,11 @@ public:
     vx_dmap* handle() { return dm_; }
     vx_ctx* context() { return ctx_; }
     // the objects behind the resident rows, for writing results back (nullptr: removed)
-    Frame::Ptr FrameAt(int64_t row) const { return row < (int64_t)frames_.size() ? frames_[row] : nullptr; }
-    Landmark::Ptr LandmarkAt(int64_t row) const { return row < (int64_t)landmarks_.size() ? landmarks_[row] : nullptr; }
+    // (references: no reference-count traffic in the per-landmark write-back loop)
+    const Frame::Ptr& FrameAt(int64_t row) const { return row < (int64_t)frames_.size() ? frames_[row] : kNoFrame; }
+    const Landmark::Ptr& LandmarkAt(int64_t row) const {
+        return row < (int64_t)landmarks_.size() ? landmarks_[row] : kNoLandmark;
+    }
 
 private:
     void Check(int rc, const char* what) const;
@@ -67,6 +70,8 @@ private:
     void FlushObservations();
     vx_ctx* ctx_ = nullptr;
     vx_dmap* dm_ = nullptr;
+    inline static const Frame::Ptr kNoFrame{};
+    inline static const Landmark::Ptr kNoLandmark{};
     std::vector<Frame::Ptr> frames_;        // by resident keyframe row
     std::vector<Landmark::Ptr> landmarks_;  // by resident landmark row
     std::unordered_map<uint64_t, int64_t> lm_row_, kf_row_;

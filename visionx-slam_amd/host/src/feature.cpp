@@ -305,10 +305,10 @@ void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
         SE3d T;
         T.qx = p[0]; T.qy = p[1]; T.qz = p[2]; T.qw = p[3];
         T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
-        if (auto fr = dm.FrameAt(kf_rows_[i])) fr->SetPose(T);
+        if (const auto& fr = dm.FrameAt(kf_rows_[i])) fr->SetPose(T);
     }
     for (int i = 0; i < nl; ++i)
-        if (auto lm = dm.LandmarkAt(lm_rows_[i]))
+        if (const auto& lm = dm.LandmarkAt(lm_rows_[i]))
             lm->SetPosition(Vec3d(lm_out_[3 * (size_t)i], lm_out_[3 * (size_t)i + 1], lm_out_[3 * (size_t)i + 2]));
 }
 
