@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 4: the multi-workgroup Schur factorisation — SBA tests, then single vs multi per config
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r04e
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_sba.py -m gpu > $O/tests.log 2>&1
+rc=$?
+echo "tests rc $rc" >> $O/tests.log
+[ $rc -le 1 ] || exit $rc
+VX_SBA_FACTOR=single timeout -k 10 300 python3 scripts/sba_bench.py 10 > $O/sba_bench_single.jsonl 2>&1 || exit 4
+timeout -k 10 300 python3 scripts/sba_bench.py 10 > $O/sba_bench_multi.jsonl 2>&1 || exit 5
+for g in 4 8 16 32; do
+  VX_SBA_FACTOR_GROUPS=$g SBA_CFGS=C5-connected timeout -k 10 200 python3 scripts/sba_bench.py 10 >> $O/sba_groups.jsonl 2>&1 || exit 6
+done

@@ -125,8 +125,40 @@ def test_sba_panel_from_global(ctx, oracle, monkeypatch):
     """Factor steps whose panel does not fit the LDS slots read their tiles from global memory (dense
     components of several hundred keyframes); forced here with two slots on a 50-keyframe window."""
     monkeypatch.setenv("VX_SBA_PANEL_SLOTS", "2")
+    monkeypatch.setenv("VX_SBA_FACTOR", "single")  # (the slots are the one-workgroup factor's)
     m = synth.make_ba_map(0x5EED0032, 50, 12000, n_old_kf=2)
     _case(ctx, oracle, m, dict(window=50, iters=6))
+
+
+@pytest.mark.parametrize("cfg", [("C3", 50, 20000, 1, 0.0), ("rig8", 96, 16000, 8, 0.0), ("rig8c", 96, 16000, 8, 0.03)])
+def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
+    """The factorisation spread over G workgroups per component, one launch per tile step with the
+    look-ahead column on workgroup 0 (k_sba_fac_begin / k_sba_fac_step / k_sba_backsub, the default),
+    equals the one-workgroup k_sba_solve ($VX_SBA_FACTOR=single) bitwise, for one component, eight
+    independent ones and eight connected ones, with G = 1, 2 and the plan's own choice."""
+    import vxslam
+
+    name, nk, nl, ns, cf = cfg
+    m = synth.make_ba_map(0x5EED0F00 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns, cross_frac=cf)
+    opts = vxslam.default_sba_options(window=nk, iters=6)
+    out = {}
+    for form, groups in (("single", None), ("multi", "1"), ("multi", "2"), ("multi", None)):
+        monkeypatch.setenv("VX_SBA_FACTOR", form)
+        if groups:
+            monkeypatch.setenv("VX_SBA_FACTOR_GROUPS", groups)
+        else:
+            monkeypatch.delenv("VX_SBA_FACTOR_GROUPS", raising=False)
+        mm = m.copy()
+        plan = ctx.sba_plan(mm, opts)
+        plan.run_async()
+        st = plan.fetch(mm)
+        plan.close()
+        out[(form, groups)] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
+                               mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
+    ref = out[("single", None)]
+    assert ref[1] >= 1
+    for k, v in out.items():
+        assert v == ref, k
 
 
 @pytest.mark.parametrize("cfg", [("C3", 50, 20000, 1, 0.0), ("C5s", 96, 16000, 8, 0.03)])

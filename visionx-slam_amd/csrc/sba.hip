@@ -558,19 +558,16 @@ enum {
     kHdrTrail,      // nt + 1 pointers, then per step the trailing tiles
     kHdrBack,       // nt + 1 pointers, then per step k the tile columns m < k of row k
     kHdrNt,
+    kHdrTrailSplit, // nt pointers: per step k, the end of its column-(k + 1) tiles (listed first)
     kHdrN = 8
 };
 
-__global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) {
-    if (it > 0 && !a.st->active[it]) return;
-    extern __shared__ __attribute__((aligned(32))) double smem[];
-    __shared__ int s_solve;
-    __shared__ double s_lambda;
+// Levenberg-Marquardt decision (wave 0 of every workgroup computes it from the fixed-order totals,
+// identically; workgroup 0 of component 0 publishes the state): *s_solve / *s_lambda in LDS.
+__device__ void solve_decide(const SBAArgs& a, int it, bool publish, int* s_solve, double* s_lambda) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    const int comp = blockIdx.x;
     const int n6 = 6 * a.nk;
     const double* rhs_g = a.red_sum + a.s_total;
-    // ---- decision (wave 0; fixed-order totals, identical in every workgroup)
     if (wv == 0) {
         double tot = 0.0, cnt = 0.0;
         for (int q = lane; q < a.nk; q += 64) {
@@ -586,9 +583,9 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
             LMVars nx;
             bool act;
             const int step = lm_decide(a, it, tot, (int)cnt, nx, act);
-            s_solve = nx.do_solve;
-            s_lambda = it == 0 ? a.lambda0 : a.st->lm[it & 1].lambda;  // the damping S was assembled with
-            if (comp == 0) {
+            *s_solve = nx.do_solve;
+            *s_lambda = it == 0 ? a.lambda0 : a.st->lm[it & 1].lambda;  // the damping S was assembled with
+            if (publish) {
                 SBAState* st = a.st;
                 st->lm[(it + 1) & 1] = nx;
                 if (it == 0) {
@@ -613,6 +610,35 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
         }
     }
     __syncthreads();
+}
+
+// k_sba_blocks wrote the component matrix straight into L (the all-reduce did, sharded): add the
+// damping on the diagonal, the identity on padding rows and the rhs tile row
+__device__ void solve_damp(const SBAArgs& a, int comp, double lambda, double* L, int np, int threads) {
+    const int n6 = 6 * a.nk;
+    const double* rhs_g = a.red_sum + a.s_total;
+    const int kq0 = a.comp_kf_ptr[comp], nc = 6 * (a.comp_kf_ptr[comp + 1] - kq0);
+    for (int e = threadIdx.x; e < np; e += threads) {
+        double* dg = L + (long long)e * np + e;
+        if (e < nc) {
+            const int g = 6 * a.comp_kf[kq0 + e / 6] + e % 6;
+            *dg += lambda * rhs_g[n6 + g] + 1e-6;
+            L[(long long)np * np + e] = rhs_g[g];
+        } else {
+            *dg = 1.0;
+            L[(long long)np * np + e] = 0.0;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    extern __shared__ __attribute__((aligned(32))) double smem[];
+    __shared__ int s_solve;
+    __shared__ double s_lambda;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int comp = blockIdx.x;
+    solve_decide(a, it, comp == 0, &s_solve, &s_lambda);
     if (!s_solve) return;
     VX_KT(0);
     const double lambda = s_lambda;
@@ -633,19 +659,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     double* ys = lcol + 2 * kPanelStride;                       // np: y, then x
     int* slot_of = reinterpret_cast<int*>(ys + np);             // nt + 1
     const int r0 = lane >> 4, cl = lane & 15;
-    // ---- k_sba_blocks wrote the component matrix straight into L (the all-reduce did, sharded);
-    // add the damping on the diagonal, the identity on padding rows and the rhs tile row
-    for (int e = tid; e < np; e += kSolveThreads) {
-        double* dg = L + (long long)e * np + e;
-        if (e < nc) {
-            const int g = 6 * a.comp_kf[kq0 + e / 6] + e % 6;
-            *dg += lambda * rhs_g[n6 + g] + 1e-6;
-            L[(long long)np * np + e] = rhs_g[g];
-        } else {
-            *dg = 1.0;
-            L[(long long)np * np + e] = 0.0;
-        }
-    }
+    solve_damp(a, comp, lambda, L, np, kSolveThreads);
     __syncthreads();
     VX_KT(1);
     bool ok = true;
@@ -750,6 +764,161 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
         for (int t = wv; t < ncp; t += kSolveWaves)
             store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
     }
+}
+
+// ------------------------------------------------------------------------- multi-workgroup factor
+// The same right-looking tiled Cholesky as k_sba_solve, spread over G workgroups per component and
+// one launch per step (the kernel boundary is the step's synchronisation): launch k applies step k's
+// trailing update A_ij -= L_ik L_jk^T — workgroup 0 to the tiles of column k + 1 (listed first by
+// the symbolic factorisation), which it then factors (POTRF + L_kk^-1 of tile k + 1) and turns into
+// the panel L_i,k+1 (look-ahead), the other G - 1 workgroups to the rest, operands read in operand
+// order from the factor in global memory.  Every tile sees the same operations in the same order as
+// in k_sba_solve, so the factor is bitwise the same; a connected window's 75-column factor no longer
+// runs on one CU.  k_sba_fac_begin: decision, damping, step 0's factor + panel; k_sba_backsub: the
+// back-substitution, dx and the clearing of the touched tiles (k_sba_solve's tail).
+
+// wave-parallel panel of column k: L_ik = A_ik L_kk^-T (dlds: L_kk^-1 in operand order)
+__device__ __forceinline__ void panel_column(double* L, int np, const int* tl, const int* pptr, int k,
+                                             const double* dlds, int waves) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
+    for (int q = pptr[k] + wv; q < pptr[k + 1]; q += waves) {
+        double* Aik = L + (long long)(16 * tl[q]) * np + 16 * k;
+        const double4 av = *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0);
+        const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
+        d4 c = {0.0, 0.0, 0.0, 0.0};
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.z, bv.z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, c, 0, 0, 0);
+        store_acc(Aik, np, c);
+    }
+}
+
+// trailing tiles tl[beg + m * stride] (m = 0, 1, ..., < end) of step k, four per wave in flight
+__device__ __forceinline__ void trail_tiles(double* L, int np, const int* tl, int k, int beg, int end, int stride,
+                                            int waves) {
+    const int wv = threadIdx.x >> 6;
+    const int cnt = end > beg ? (end - beg + stride - 1) / stride : 0;
+    for (int m0 = wv * 4; m0 < cnt; m0 += waves * 4) {
+        d4 c[4];
+        int ti[4], tj[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ti[q] = -1;
+            if (m0 + q < cnt) {
+                const int e = tl[beg + (m0 + q) * stride];
+                ti[q] = e >> 16;
+                tj[q] = e & 0xffff;
+                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (ti[q] < 0) continue;
+            c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * k, L + (long long)(16 * tj[q]) * np + 16 * k, np,
+                              c[q]);
+            store_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np, c[q]);
+        }
+    }
+}
+
+// factor of tile column k (wave 0) and its panel (all waves); a non-positive pivot flags the iteration
+__device__ __forceinline__ void factor_column(const SBAArgs& a, int it, double* L, double* Linv, int np, const int* tl,
+                                              const int* pptr, int k, double* lcol, double* dlds) {
+    const int wv = threadIdx.x >> 6;
+    if (wv == 0) {
+        const bool ok = potrf_inv16(L + (long long)(16 * k) * np + 16 * k, np, lcol, dlds, Linv + 256 * k);
+        if (!ok && threadIdx.x == 0) atomicOr(&a.st->fail[it], 1);
+    }
+    __syncthreads();
+    panel_column(L, np, tl, pptr, k, dlds, kSolveWaves);
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    __shared__ int s_solve;
+    __shared__ double s_lambda;
+    __shared__ __attribute__((aligned(32))) double lds[3 * kPanelStride];  // L_kk^-1 | POTRF columns
+    const int comp = blockIdx.x;
+    solve_decide(a, it, comp == 0, &s_solve, &s_lambda);
+    if (!s_solve) return;
+    const int* hdr = a.comp_hdr + kHdrN * comp;
+    const int nt = hdr[kHdrNt], np = 16 * nt;
+    double* L = a.L + a.comp_loff[comp];
+    solve_damp(a, comp, s_lambda, L, np, kSolveThreads);
+    __syncthreads();
+    factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, a.tl, a.tl + hdr[kHdrPanel], 0, lds + kPanelStride, lds);
+}
+
+// launch k of the factorisation (k = 0 .. max_nt - 2): blockIdx.x = component * G + g
+__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int it, int k, int G) {
+    if (it > 0 && !a.st->active[it]) return;
+    if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (k_sba_fac_begin's decision)
+    __shared__ __attribute__((aligned(32))) double lds[3 * kPanelStride];
+    const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
+    const int* hdr = a.comp_hdr + kHdrN * comp;
+    const int nt = hdr[kHdrNt], np = 16 * nt;
+    if (k + 1 >= nt) return;
+    double* L = a.L + a.comp_loff[comp];
+    const int* tl = a.tl;
+    const int* tptr = tl + hdr[kHdrTrail];
+    const int split = tl[hdr[kHdrTrailSplit] + k];
+    if (g == 0) {
+        trail_tiles(L, np, tl, k, tptr[k], split, 1, kSolveWaves);
+        if (G == 1) trail_tiles(L, np, tl, k, split, tptr[k + 1], 1, kSolveWaves);
+        __syncthreads();
+        factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, tl, tl + hdr[kHdrPanel], k + 1, lds + kPanelStride,
+                      lds);
+    } else {
+        trail_tiles(L, np, tl, k, split + (g - 1), tptr[k + 1], G - 1, kSolveWaves);
+    }
+}
+
+__global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    if (!a.st->lm[(it + 1) & 1].do_solve) return;
+    extern __shared__ __attribute__((aligned(32))) double ys[];  // np: y, then x
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
+    const int comp = blockIdx.x;
+    const int* hdr = a.comp_hdr + kHdrN * comp;
+    const int nt = hdr[kHdrNt], np = 16 * nt;
+    const int kq0 = a.comp_kf_ptr[comp], nc = 6 * (a.comp_kf_ptr[comp + 1] - kq0);
+    double* L = a.L + a.comp_loff[comp];
+    const double* Linv = a.Linv + a.comp_loff[comp];
+    const int* tl = a.tl;
+    const int* bptr = tl + hdr[kHdrBack];
+    for (int c = tid; c < np; c += kSolveThreads) ys[c] = L[(long long)np * np + c];
+    __syncthreads();
+    for (int k = nt - 1; k >= 0; --k) {
+        double xk = 0.0;
+        if (wv == 0) {  // x_k = L_kk^-T y_k
+            const double* Li = Linv + 256 * k;
+#pragma unroll
+            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) xk += Li[r * 16 + cl] * ys[16 * k + r];
+            xk += __shfl_xor(xk, 16, 64);
+            xk += __shfl_xor(xk, 32, 64);
+        }
+        __syncthreads();
+        if (wv == 0 && r0 == 0) ys[16 * k + cl] = xk;
+        __syncthreads();
+        for (int q = bptr[k] + wv; q < bptr[k + 1]; q += kSolveWaves) {
+            const int mm = tl[q];
+            const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
+            double p = 0.0;
+#pragma unroll
+            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) p += Lkm[(long long)r * np + cl] * ys[16 * k + r];
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (r0 == 0) ys[16 * mm + cl] -= p;
+        }
+        __syncthreads();
+    }
+    for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
+    const int* cp = tl + hdr[kHdrCopy];
+    const int ncp = hdr[kHdrNCopy];
+    const d4 z = {0.0, 0.0, 0.0, 0.0};
+    for (int t = wv; t < ncp; t += kSolveWaves)
+        store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
 }
 
 // ------------------------------------------------------------------------- k_sba_update
@@ -1254,6 +1423,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     std::vector<int> hdr((size_t)kHdrN * std::max(p->n_comp, 1), 0), tlist;
     p->n_lfactor_tiles = p->n_trail_updates = 0;
     p->max_panel = 1;
+    p->max_nt = p->max_trail_rest = 0;
     {
         std::vector<std::vector<std::pair<int, int>>> cblk(p->n_comp);
         for (const int2& b : bij) {
@@ -1297,21 +1467,34 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                 p->max_panel = std::max(p->max_panel, (int)tlist.size() - tlist[pp + k]);
             }
             tlist[pp + nt] = (int)tlist.size();
-            // trailing-update lists
+            // trailing-update lists; per step k the tiles of column k + 1 first (the look-ahead
+            // column the multi-workgroup factorisation updates and factors in the same launch), then
+            // the rest; every tile is updated once per step, so the order inside a step is free
             h[kHdrTrail] = (int)tlist.size();
             const int tp = (int)tlist.size();
             tlist.resize(tlist.size() + nt + 1);
+            std::vector<int> split(nt, 0);
             for (int k = 0; k < nt; ++k) {
                 tlist[tp + k] = (int)tlist.size();
+                if (k + 1 < nt && NZ(k + 1, k)) {
+                    for (int i = k + 1; i < nt; ++i)
+                        if (NZ(i, k)) tlist.push_back(i << 16 | (k + 1));
+                    tlist.push_back(nt << 16 | (k + 1));
+                }
+                split[k] = (int)tlist.size();
                 for (int i = k + 1; i < nt; ++i)
                     if (NZ(i, k))
-                        for (int j = k + 1; j <= i; ++j)
+                        for (int j = k + 2; j <= i; ++j)
                             if (NZ(j, k)) tlist.push_back(i << 16 | j);
-                for (int j = k + 1; j < nt; ++j)
+                for (int j = k + 2; j < nt; ++j)
                     if (NZ(j, k)) tlist.push_back(nt << 16 | j);
                 p->n_trail_updates += (int)tlist.size() - tlist[tp + k];
+                p->max_trail_rest = std::max(p->max_trail_rest, (int)tlist.size() - split[k]);
             }
             tlist[tp + nt] = (int)tlist.size();
+            h[kHdrTrailSplit] = (int)tlist.size();
+            tlist.insert(tlist.end(), split.begin(), split.end());
+            p->max_nt = std::max(p->max_nt, nt);
             // back-substitution lists: tile columns m < k of row k
             h[kHdrBack] = (int)tlist.size();
             const int bp = (int)tlist.size();
@@ -1373,6 +1556,18 @@ int solve_panel_slots(int np, int max_panel) {
     return ps;
 }
 
+bool factor_multi() {  // (read per run: a plan captured into a graph keeps the form it was captured with)
+    const char* e = std::getenv("VX_SBA_FACTOR");
+    return !(e && std::strcmp(e, "single") == 0);
+}
+// workgroups per component and step: workgroup 0 takes the look-ahead column, the others about 8
+// trailing tiles each (two per wave); $VX_SBA_FACTOR_GROUPS overrides
+int factor_groups(int max_trail_rest) {
+    int g = 1 + (max_trail_rest + 7) / 8;
+    if (const char* e = std::getenv("VX_SBA_FACTOR_GROUPS")) g = std::atoi(e);
+    return std::max(1, std::min(g, 128));
+}
+
 int sba_run(vx_ctx* c, vx_sba_plan* p) {
     if (p->status != 0) {
         p->ran = true;
@@ -1393,6 +1588,10 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
         VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_solve),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int upd_blocks = (std::max(p->n_opt, p->nk) + kUpdThreads - 1) / kUpdThreads;
+    // the factorisation: one launch per tile step over G workgroups per component (default), or the
+    // whole factor in one workgroup per component ($VX_SBA_FACTOR=single, the round-3 form)
+    const bool multi = factor_multi();
+    const int G = factor_groups(p->max_trail_rest);
     const size_t red_n = (size_t)p->l_total + (size_t)p->nk * 14;
     for (int it = 0; it < p->opt.max_iterations; ++it) {
         if (p->n_lm_blocks > 0)
@@ -1405,8 +1604,18 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
             if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
         }
 #endif
-        VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
-                         (uint32_t)lds, c->stream, a, it));
+        if (multi) {
+            VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
+                             c->stream, a, it));
+            for (int k = 0; k + 1 < p->max_nt; ++k)
+                VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_step, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads),
+                                 0, c->stream, a, it, k, G));
+            VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+                             (uint32_t)(p->max_np * sizeof(double)), c->stream, a, it));
+        } else {
+            VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+                             (uint32_t)lds, c->stream, a, it));
+        }
         VX_HIP(c, launch(c, kStSbaUpdate, k_sba_update, dim3(std::max(upd_blocks, 1)), dim3(kUpdThreads), 0,
                          c->stream, a, it));
     }

@@ -18,6 +18,8 @@ struct vx_sba_plan {
     int64_t n_pairs = 0;
     int n_blocks = 0, n_lm_blocks = 0, n_comp = 0, max_np = 0;
     int max_panel = 1;  // most panel tiles (rhs row included) of one column of any component's factor
+    int max_nt = 0;          // most 16 x 16 tile columns of one component
+    int max_trail_rest = 0;  // most trailing-update tiles of one step outside its look-ahead column
     long long s_total = 0, l_total = 0;
     std::vector<int> kf_map_idx, lm_map_idx;
     std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
