@@ -13,3 +13,6 @@ timeout -k 10 300 python3 scripts/sba_bench.py 10 > $O/sba_bench_multi.jsonl 2>&
 for g in 4 8 16 32; do
   VX_SBA_FACTOR_GROUPS=$g SBA_CFGS=C5-connected timeout -k 10 200 python3 scripts/sba_bench.py 10 >> $O/sba_groups.jsonl 2>&1 || exit 6
 done
+export TMPDIR=/tmp
+SBA_CFGS=C5-connected timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_F64 SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES --output-format csv -d $O/pmc_sba -o pmc -- python3 scripts/sba_bench.py 2 > /dev/null 2>&1 || exit 7
+python3 scripts/pmc_sba_summary.py "$(find $O/pmc_sba -name "*counter_collection.csv" | head -1)" > $O/pmc_sba_c5_connected_multi.txt 2>&1
