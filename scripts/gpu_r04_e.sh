@@ -8,6 +8,8 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method threa
 rc=$?
 echo "tests rc $rc" >> $O/tests.log
 [ $rc -le 1 ] || exit $rc
+timeout -k 10 60 scripts/probe/xcd_probe > $O/xcd_probe.txt 2>&1 || exit 3
+timeout -k 10 120 python3 scripts/ba_cumask.py > $O/ba_cumask.txt 2>&1 || exit 3
 VX_SBA_FACTOR=single timeout -k 10 300 python3 scripts/sba_bench.py 10 > $O/sba_bench_single.jsonl 2>&1 || exit 4
 timeout -k 10 300 python3 scripts/sba_bench.py 10 > $O/sba_bench_multi.jsonl 2>&1 || exit 5
 for g in 4 8 16 32; do
