@@ -27,7 +27,9 @@
 //                diagonal tile, one wave factors it and forms L_kk^-1 from registers
 //                (v_readlane broadcasts); the panel L_ik = A_ik L_kk^-T and the trailing update
 //                A_ij -= L_ik L_jk^T are v_mfma_f64_16x16x4 tiles (panel staged in LDS); then the
-//                blocked back-substitution L^T x = y.
+//                blocked back-substitution L^T x = y.  ($VX_SBA_FACTOR=single; the default spreads the
+//                same factorisation over G workgroups per component, one launch per tile step:
+//                k_sba_fac_begin / k_sba_fac_step / k_sba_backsub below.)
 //   k_sba_update landmark back-substitution dp = V^-1 (g_p - sum W_o^T dx) and T <- exp(dx) T into
 //                the trial buffers.
 #include <algorithm>
