@@ -517,11 +517,6 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--ba-cus", type=float, default=0.0,
                     help="fraction of the CUs reserved for the LocalBA context (disjoint CU masks; 0: shared)")
-    ap.add_argument("--ba-xcds", type=int, default=0,
-                    help="> 0: LocalBA on the CUs of this many whole XCDs, extraction / matching on the others "
-                         "(separate L2s; --cu-xcd-map says how CU-mask bits map to XCDs)")
-    ap.add_argument("--cu-xcd-map", default="rr", choices=("rr", "block"),
-                    help="CU-mask bit i lies on XCD i mod 8 (rr) or i // (CUs / 8) (block)")
     ap.add_argument("--diag-skip", default="", choices=("", "ba", "match", "extract"),
                     help="diagnostics only (the JSON line is marked invalid): leave one stage out of every step")
     ap.add_argument("--diag-nodep", action="store_true",
@@ -573,12 +568,6 @@ def main():
         few = sorted({int(j * ncu / n_few) for j in range(n_few)})
         rest = [i for i in range(ncu) if i not in set(few)]
         ba_mask, fe_mask = (few, rest) if args.ba_cus <= 0.5 else (rest, few)
-    if args.ba_xcds > 0 and args.streams > 1:
-        ncu = vxslam.lib().vx_device_cus(dist.local_rank)
-        per = ncu // 8
-        xcd = (lambda i: i % 8) if args.cu_xcd_map == "rr" else (lambda i: i // per)
-        ba_mask = [i for i in range(ncu) if xcd(i) < args.ba_xcds]
-        fe_mask = [i for i in range(ncu) if xcd(i) >= args.ba_xcds]
     n_ex = args.extract_ctx if args.streams == 3 else 1
     ectxs = [vxslam.Context(dist.local_rank, cu_mask=fe_mask) for _ in range(n_ex)]
     ectx = ectxs[0]
@@ -941,10 +930,6 @@ def main():
                 # (apps/main.cpp:42-47; --config FILE / --ba_* flags)
                 "ba_options": ba_flags,
                 "config_file": args.config_file,
-                "cu_partition": (f"LocalBA on {args.ba_xcds} XCD(s), extraction / matching on the rest "
-                                 f"(CU-mask map {args.cu_xcd_map})" if args.ba_xcds > 0 and args.streams > 1
-                                 else (f"LocalBA on {args.ba_cus:.3f} of the CUs (every k-th)" if args.ba_cus > 0
-                                       and args.streams > 1 else "shared")),
             },
             # one frame alone through the same dependency chain (host enqueue to completion, median
             # of 20): the per-frame latency; `value` is the pipelined throughput
