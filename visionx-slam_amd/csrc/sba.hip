@@ -1558,9 +1558,15 @@ int solve_panel_slots(int np, int max_panel) {
     return ps;
 }
 
-bool factor_multi() {  // (read per run: a plan captured into a graph keeps the form it was captured with)
+// Measured per LM iteration (r04e, profiles/r04/sba_bench_*_r04e.jsonl): one component of 75 tile
+// columns (connected C5) 2004 -> 1004 us multi; 19 columns (C3) 153 vs 165 us and eight components of
+// 10 (C5) 86 vs 99 us favour the single workgroup, whose steps need no launch.  $VX_SBA_FACTOR=single
+// | multi forces one (read per run: a plan captured into a graph keeps the form it was captured with).
+bool factor_multi(int max_nt) {
     const char* e = std::getenv("VX_SBA_FACTOR");
-    return !(e && std::strcmp(e, "single") == 0);
+    if (e && std::strcmp(e, "single") == 0) return false;
+    if (e && std::strcmp(e, "multi") == 0) return true;
+    return max_nt > 32;
 }
 // workgroups per component and step: workgroup 0 takes the look-ahead column, the others about 8
 // trailing tiles each (two per wave); $VX_SBA_FACTOR_GROUPS overrides
@@ -1590,9 +1596,9 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
         VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_solve),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const int upd_blocks = (std::max(p->n_opt, p->nk) + kUpdThreads - 1) / kUpdThreads;
-    // the factorisation: one launch per tile step over G workgroups per component (default), or the
-    // whole factor in one workgroup per component ($VX_SBA_FACTOR=single, the round-3 form)
-    const bool multi = factor_multi();
+    // the factorisation: one launch per tile step over G workgroups per component (components of
+    // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
+    const bool multi = factor_multi(p->max_nt);
     const int G = factor_groups(p->max_trail_rest);
     const size_t red_n = (size_t)p->l_total + (size_t)p->nk * 14;
     for (int it = 0; it < p->opt.max_iterations; ++it) {
