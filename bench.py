@@ -557,15 +557,18 @@ def main():
 
     torch.cuda.set_device(dist.local_rank)
     # one context (HIP stream) per pipeline stage; see Pipeline.  --ba-cus > 0 gives LocalBA its own
-    # compute units (every k-th CU, spread over the XCDs) and extraction / matching the rest
+    # compute units (a contiguous range of CU-mask bits: the same number on every XCD) and extraction /
+    # matching the rest
     fe_mask = ba_mask = None
     if args.ba_cus > 0 and args.streams > 1:
-        # the smaller side gets round(share x CUs) CUs evenly spaced over the CU indices (so over the
-        # XCDs), the other side the rest
+        # the smaller side gets the first round(share x CUs) CU-mask bits, the other side the rest:
+        # bit i lies on XCD i mod 8 (scripts/probe/xcd_probe.hip), so a contiguous range is spread
+        # evenly over the XCDs — a mask that leaves an XCD without CUs (e.g. every 8th bit) is not
+        # applied at all by the runtime
         ncu = vxslam.lib().vx_device_cus(dist.local_rank)
         small = min(args.ba_cus, 1.0 - args.ba_cus)
-        n_few = max(1, int(round(small * ncu)))
-        few = sorted({int(j * ncu / n_few) for j in range(n_few)})
+        n_few = max(8, int(round(small * ncu / 8)) * 8)
+        few = list(range(n_few))
         rest = [i for i in range(ncu) if i not in set(few)]
         ba_mask, fe_mask = (few, rest) if args.ba_cus <= 0.5 else (rest, few)
     n_ex = args.extract_ctx if args.streams == 3 else 1
