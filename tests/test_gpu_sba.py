@@ -135,15 +135,18 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
     """The factorisation spread over G workgroups per component, one launch per tile step with the
     look-ahead column on workgroup 0 (k_sba_fac_begin / k_sba_fac_step / k_sba_backsub, the default),
     equals the one-workgroup k_sba_solve ($VX_SBA_FACTOR=single) bitwise, for one component, eight
-    independent ones and eight connected ones, with G = 1, 2 and the plan's own choice."""
+    independent ones and eight connected ones, with G = 1, 2 and the plan's own choice, and with the
+    look-ahead column in LDS (default) or over global memory ($VX_SBA_LOOKAHEAD_LDS=0)."""
     import vxslam
 
     name, nk, nl, ns, cf = cfg
     m = synth.make_ba_map(0x5EED0F00 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns, cross_frac=cf)
     opts = vxslam.default_sba_options(window=nk, iters=6)
     out = {}
-    for form, groups in (("single", None), ("multi", "1"), ("multi", "2"), ("multi", None)):
+    for form, groups, la in (("single", None, "1"), ("multi", "1", "1"), ("multi", "2", "1"), ("multi", None, "1"),
+                             ("multi", "2", "0")):
         monkeypatch.setenv("VX_SBA_FACTOR", form)
+        monkeypatch.setenv("VX_SBA_LOOKAHEAD_LDS", la)
         if groups:
             monkeypatch.setenv("VX_SBA_FACTOR_GROUPS", groups)
         else:
@@ -153,9 +156,9 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
         plan.run_async()
         st = plan.fetch(mm)
         plan.close()
-        out[(form, groups)] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
-                               mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
-    ref = out[("single", None)]
+        out[(form, groups, la)] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
+                                   mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
+    ref = out[("single", None, "1")]
     assert ref[1] >= 1
     for k, v in out.items():
         assert v == ref, k

@@ -852,11 +852,86 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
     factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, a.tl, a.tl + hdr[kHdrPanel], 0, lds + kPanelStride, lds);
 }
 
-// launch k of the factorisation (k = 0 .. max_nt - 2): blockIdx.x = component * G + g
-__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int it, int k, int G) {
+// Workgroup 0's look-ahead in launch k: column k + 1 kept in LDS from its step-k update to its panel.
+// The updated diagonal tile goes to LDS row-major (POTRF reads it there), the updated panel tiles as
+// MFMA operand images (the panel reads them there); neither is stored to global memory, since the
+// panel overwrites the off-diagonal ones and only L_kk^-1 of a diagonal tile is read later.  Same
+// operations, same order as factor_column over global memory.  sm: diagonal tile | L_kk^-1 | POTRF
+// columns (2 tiles) | ps panel images | tile row -> slot (nt + 1) | updated flags (ps).
+__device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt, const int* tl,
+                                 const int* hdr, int k, int la_beg, int la_end, double* sm, int ps) {
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
+    double* dtile = sm;
+    double* dlds = sm + kPanelStride;
+    double* lcol = sm + 2 * kPanelStride;
+    double* pan = sm + 4 * kPanelStride;
+    int* slot_of = reinterpret_cast<int*>(pan + (size_t)ps * kPanelStride);
+    int* upd = slot_of + nt + 1;
+    const int* pptr = tl + hdr[kHdrPanel];
+    const int c1 = k + 1, p0 = pptr[c1], pn = pptr[c1 + 1] - p0;
+    const bool in_lds = pn <= ps;
+    for (int q = tid; q < pn; q += kSolveThreads) {
+        slot_of[tl[p0 + q]] = q;
+        if (in_lds) upd[q] = 0;
+    }
+    __syncthreads();
+    // step k's update of column k + 1 (the diagonal tile is the first entry when the column has one)
+    const bool diag = la_end > la_beg;
+    const int cnt = la_end - la_beg;
+    for (int m0 = wv * 4; m0 < cnt; m0 += kSolveWaves * 4) {
+        d4 c[4];
+        int ti[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ti[q] = -1;
+            if (m0 + q < cnt) {
+                ti[q] = tl[la_beg + m0 + q] >> 16;
+                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * c1, np);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (ti[q] < 0) continue;
+            c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * k, L + (long long)(16 * c1) * np + 16 * k, np, c[q]);
+            if (ti[q] == c1) {
+                store_acc(dtile, 16, c[q]);
+            } else if (in_lds) {
+                const int sl = slot_of[ti[q]];
+                store_acc_opo(pan + (size_t)sl * kPanelStride, c[q]);
+                if (lane == 0) upd[sl] = 1;
+            } else {
+                store_acc(L + (long long)(16 * ti[q]) * np + 16 * c1, np, c[q]);
+            }
+        }
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const bool ok = diag ? potrf_inv16(dtile, 16, lcol, dlds, Linv + 256 * c1)
+                             : potrf_inv16(L + (long long)(16 * c1) * np + 16 * c1, np, lcol, dlds, Linv + 256 * c1);
+        if (!ok && tid == 0) atomicOr(&a.st->fail[it], 1);
+    }
+    __syncthreads();
+    // the panel L_i,k+1 = A_i,k+1 L_k+1,k+1^-T: updated tiles from LDS, the others from global
+    for (int q = wv; q < pn; q += kSolveWaves) {
+        double* Aik = L + (long long)(16 * tl[p0 + q]) * np + 16 * c1;
+        const double4 av = (in_lds && upd[q]) ? *reinterpret_cast<const double4*>(pan + (size_t)q * kPanelStride + 4 * lane)
+                                              : *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0);
+        const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
+        d4 c = {0.0, 0.0, 0.0, 0.0};
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.z, bv.z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, c, 0, 0, 0);
+        store_acc(Aik, np, c);
+    }
+}
+
+// launch k of the factorisation (k = 0 .. max_nt - 2): blockIdx.x = component * G + g; ps: LDS panel
+// images of workgroup 0's look-ahead (0: the look-ahead over global memory, factor_column)
+__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int it, int k, int G, int ps) {
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (k_sba_fac_begin's decision)
-    __shared__ __attribute__((aligned(32))) double lds[3 * kPanelStride];
+    extern __shared__ __attribute__((aligned(32))) double sm[];
     const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
     const int* hdr = a.comp_hdr + kHdrN * comp;
     const int nt = hdr[kHdrNt], np = 16 * nt;
@@ -866,11 +941,15 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int i
     const int* tptr = tl + hdr[kHdrTrail];
     const int split = tl[hdr[kHdrTrailSplit] + k];
     if (g == 0) {
-        trail_tiles(L, np, tl, k, tptr[k], split, 1, kSolveWaves);
         if (G == 1) trail_tiles(L, np, tl, k, split, tptr[k + 1], 1, kSolveWaves);
-        __syncthreads();
-        factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, tl, tl + hdr[kHdrPanel], k + 1, lds + kPanelStride,
-                      lds);
+        if (ps > 0) {
+            lookahead_column(a, it, L, a.Linv + a.comp_loff[comp], np, nt, tl, hdr, k, tptr[k], split, sm, ps);
+        } else {
+            trail_tiles(L, np, tl, k, tptr[k], split, 1, kSolveWaves);
+            __syncthreads();
+            factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, tl, tl + hdr[kHdrPanel], k + 1, sm + kPanelStride,
+                          sm);
+        }
     } else {
         trail_tiles(L, np, tl, k, split + (g - 1), tptr[k + 1], G - 1, kSolveWaves);
     }
@@ -1562,6 +1641,12 @@ int solve_panel_slots(int np, int max_panel) {
 // columns (connected C5) 2004 -> 1004 us multi; 19 columns (C3) 153 vs 165 us and eight components of
 // 10 (C5) 86 vs 99 us favour the single workgroup, whose steps need no launch.  $VX_SBA_FACTOR=single
 // | multi forces one (read per run: a plan captured into a graph keeps the form it was captured with).
+// LDS of k_sba_fac_step's look-ahead: 4 tiles (diagonal, L^-1, POTRF columns) + ps panel images +
+// the tile row -> slot map and the updated flags
+size_t lookahead_lds_bytes(int max_nt, int ps) {
+    return (size_t)(4 + ps) * kPanelStride * sizeof(double) + (size_t)(max_nt + 1 + ps) * sizeof(int);
+}
+
 bool factor_multi(int max_nt) {
     const char* e = std::getenv("VX_SBA_FACTOR");
     if (e && std::strcmp(e, "single") == 0) return false;
@@ -1600,6 +1685,16 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
     // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
     const bool multi = factor_multi(p->max_nt);
     const int G = factor_groups(p->max_trail_rest);
+    // workgroup 0's look-ahead column in LDS when its panel fits ($VX_SBA_LOOKAHEAD_LDS=0: global)
+    int la_ps = std::max(p->max_panel, 1);
+    size_t la_lds = lookahead_lds_bytes(p->max_nt, la_ps);
+    if (la_lds > 160 * 1024 || (std::getenv("VX_SBA_LOOKAHEAD_LDS") && std::atoi(std::getenv("VX_SBA_LOOKAHEAD_LDS")) == 0)) {
+        la_ps = 0;
+        la_lds = 4 * kPanelStride * sizeof(double);
+    }
+    if (multi && la_lds > 64 * 1024)
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_fac_step),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)la_lds));
     const size_t red_n = (size_t)p->l_total + (size_t)p->nk * 14;
     for (int it = 0; it < p->opt.max_iterations; ++it) {
         if (p->n_lm_blocks > 0)
@@ -1617,7 +1712,7 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
                              c->stream, a, it));
             for (int k = 0; k + 1 < p->max_nt; ++k)
                 VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_step, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads),
-                                 0, c->stream, a, it, k, G));
+                                 (uint32_t)la_lds, c->stream, a, it, k, G, la_ps));
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
                              (uint32_t)(p->max_np * sizeof(double)), c->stream, a, it));
         } else {
