@@ -633,6 +633,87 @@ __device__ void solve_damp(const SBAArgs& a, int comp, double lambda, double* L,
     }
 }
 
+// Blocked back-substitution L^T x = y over the component's tile rows, descending (ys: y in LDS,
+// overwritten with x): x_k = L_kk^-T y_k by wave 0, then y_m -= L_km^T x_k over row k's nonzero tiles,
+// one wave per tile.  The operands of step k - 1 (L_kk^-1 and up to kBsPre tiles per wave) are
+// loaded while step k runs — they do not depend on x — so a step waits on LDS and two barriers, not
+// on global memory; tiles beyond kBsPre per wave are read in place.  Same sums in the same order as
+// the plain loop (bitwise).
+constexpr int kBsPre = 4;
+__device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, const int* tl, const int* bptr,
+                                        int k, double (&li)[4], double (&tv)[kBsPre][4], int (&tm)[kBsPre]) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
+    if (wv == 0) {
+        const double* Li = Linv + 256 * k;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) li[r] = Li[(4 * r0 + r) * 16 + cl];
+    }
+#pragma unroll
+    for (int j = 0; j < kBsPre; ++j) {
+        const int q = bptr[k] + wv + kSolveWaves * j;
+        tm[j] = q < bptr[k + 1] ? tl[q] : -1;
+        if (tm[j] >= 0) {
+            const double* Lkm = L + (long long)(16 * k) * np + 16 * tm[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tv[j][r] = Lkm[(long long)(4 * r0 + r) * np + cl];
+        }
+    }
+}
+__device__ void back_substitute(const double* L, const double* Linv, int np, int nt, const int* tl, const int* bptr,
+                                double* ys) {
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
+    for (int c = tid; c < np; c += kSolveThreads) ys[c] = L[(long long)np * np + c];
+    double li[4] = {0, 0, 0, 0}, tv[kBsPre][4];
+    int tm[kBsPre];
+    bs_load(L, Linv, np, tl, bptr, nt - 1, li, tv, tm);
+    __syncthreads();
+    for (int k = nt - 1; k >= 0; --k) {
+        double nli[4] = {0, 0, 0, 0}, ntv[kBsPre][4];
+        int ntm[kBsPre];
+        if (k > 0) bs_load(L, Linv, np, tl, bptr, k - 1, nli, ntv, ntm);
+        if (wv == 0) {  // x_k = L_kk^-T y_k (wave 0 reads y_k before it writes x_k over it)
+            double xk = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xk += li[r] * ys[16 * k + 4 * r0 + r];
+            xk += __shfl_xor(xk, 16, 64);
+            xk += __shfl_xor(xk, 32, 64);
+            // (every lane's reads of y_k precede this write: the shuffles consumed them)
+            if (r0 == 0) ys[16 * k + cl] = xk;
+        }
+        __syncthreads();
+        // y_m -= L_km^T x_k for the nonzero tiles of row k, one wave per tile
+#pragma unroll
+        for (int j = 0; j < kBsPre; ++j) {
+            if (tm[j] < 0) continue;
+            double p = 0.0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) p += tv[j][r] * ys[16 * k + 4 * r0 + r];
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (r0 == 0) ys[16 * tm[j] + cl] -= p;
+        }
+        for (int q = bptr[k] + wv + kSolveWaves * kBsPre; q < bptr[k + 1]; q += kSolveWaves) {
+            const int mm = tl[q];
+            const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
+            double p = 0.0;
+#pragma unroll
+            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) p += Lkm[(long long)r * np + cl] * ys[16 * k + r];
+            p += __shfl_xor(p, 16, 64);
+            p += __shfl_xor(p, 32, 64);
+            if (r0 == 0) ys[16 * mm + cl] -= p;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) li[r] = nli[r];
+#pragma unroll
+        for (int j = 0; j < kBsPre; ++j) {
+            tm[j] = ntm[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) tv[j][r] = ntv[j][r];
+        }
+    }
+}
+
 __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     extern __shared__ __attribute__((aligned(32))) double smem[];
@@ -729,33 +810,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     VX_KT(11);
     if (wv == 0 && lane == 0 && !ok) atomicOr(&a.st->fail[it], 1);
     // ---- back-substitution L^T x = y (y = row np of the factored rhs tile row)
-    for (int c = tid; c < np; c += kSolveThreads) ys[c] = L[(long long)np * np + c];
-    __syncthreads();
-    for (int k = nt - 1; k >= 0; --k) {
-        double xk = 0.0;
-        if (wv == 0) {  // x_k = L_kk^-T y_k
-            const double* Li = Linv + 256 * k;
-#pragma unroll
-            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) xk += Li[r * 16 + cl] * ys[16 * k + r];
-            xk += __shfl_xor(xk, 16, 64);
-            xk += __shfl_xor(xk, 32, 64);
-        }
-        __syncthreads();  // every lane has read y_k before it is overwritten with x_k
-        if (wv == 0 && r0 == 0) ys[16 * k + cl] = xk;
-        __syncthreads();
-        // y_m -= L_km^T x_k for the nonzero tiles of row k, one wave per tile
-        for (int q = bptr[k] + wv; q < bptr[k + 1]; q += kSolveWaves) {
-            const int mm = tl[q];
-            const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
-            double p = 0.0;
-#pragma unroll
-            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) p += Lkm[(long long)r * np + cl] * ys[16 * k + r];
-            p += __shfl_xor(p, 16, 64);
-            p += __shfl_xor(p, 32, 64);
-            if (r0 == 0) ys[16 * mm + cl] -= p;
-        }
-        __syncthreads();
-    }
+    back_substitute(L, Linv, np, nt, tl, bptr, ys);
     VX_KT(12);
     for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
     // the next assembly writes only S's blocks into L: clear every tile the factorisation touched
@@ -959,7 +1014,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;
     extern __shared__ __attribute__((aligned(32))) double ys[];  // np: y, then x
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
+    const int tid = threadIdx.x, wv = tid >> 6;
     const int comp = blockIdx.x;
     const int* hdr = a.comp_hdr + kHdrN * comp;
     const int nt = hdr[kHdrNt], np = 16 * nt;
@@ -968,32 +1023,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it
     const double* Linv = a.Linv + a.comp_loff[comp];
     const int* tl = a.tl;
     const int* bptr = tl + hdr[kHdrBack];
-    for (int c = tid; c < np; c += kSolveThreads) ys[c] = L[(long long)np * np + c];
-    __syncthreads();
-    for (int k = nt - 1; k >= 0; --k) {
-        double xk = 0.0;
-        if (wv == 0) {  // x_k = L_kk^-T y_k
-            const double* Li = Linv + 256 * k;
-#pragma unroll
-            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) xk += Li[r * 16 + cl] * ys[16 * k + r];
-            xk += __shfl_xor(xk, 16, 64);
-            xk += __shfl_xor(xk, 32, 64);
-        }
-        __syncthreads();
-        if (wv == 0 && r0 == 0) ys[16 * k + cl] = xk;
-        __syncthreads();
-        for (int q = bptr[k] + wv; q < bptr[k + 1]; q += kSolveWaves) {
-            const int mm = tl[q];
-            const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
-            double p = 0.0;
-#pragma unroll
-            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) p += Lkm[(long long)r * np + cl] * ys[16 * k + r];
-            p += __shfl_xor(p, 16, 64);
-            p += __shfl_xor(p, 32, 64);
-            if (r0 == 0) ys[16 * mm + cl] -= p;
-        }
-        __syncthreads();
-    }
+    back_substitute(L, Linv, np, nt, tl, bptr, ys);
     for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
     const int* cp = tl + hdr[kHdrCopy];
     const int ncp = hdr[kHdrNCopy];
