@@ -136,6 +136,14 @@ struct SBAArgs {
     double* dx;             // 6 nk
     SBAState* st;
     int panel_slots;        // k_sba_solve: LDS panel tiles (a step with more panel tiles reads global)
+    const int* fac_steps;   // k_sba_fac_step descriptors (vx_sba_plan::fac_steps), fac_nk per component
+    int fac_nk;
+};
+
+// one launch of the multi-workgroup factor for one component (vx_sba_plan::fac_steps)
+struct FacStep {
+    long long loff;
+    int la_beg, split, t_end, p0, p1, nt;
 };
 
 // ------------------------------------------------------------------------- state selection
@@ -835,10 +843,10 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
 // back-substitution, dx and the clearing of the touched tiles (k_sba_solve's tail).
 
 // wave-parallel panel of column k: L_ik = A_ik L_kk^-T (dlds: L_kk^-1 in operand order)
-__device__ __forceinline__ void panel_column(double* L, int np, const int* tl, const int* pptr, int k,
+__device__ __forceinline__ void panel_column(double* L, int np, const int* tl, int p0, int p1, int k,
                                              const double* dlds, int waves) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
-    for (int q = pptr[k] + wv; q < pptr[k + 1]; q += waves) {
+    for (int q = p0 + wv; q < p1; q += waves) {
         double* Aik = L + (long long)(16 * tl[q]) * np + 16 * k;
         const double4 av = *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0);
         const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
@@ -881,14 +889,14 @@ __device__ __forceinline__ void trail_tiles(double* L, int np, const int* tl, in
 
 // factor of tile column k (wave 0) and its panel (all waves); a non-positive pivot flags the iteration
 __device__ __forceinline__ void factor_column(const SBAArgs& a, int it, double* L, double* Linv, int np, const int* tl,
-                                              const int* pptr, int k, double* lcol, double* dlds) {
+                                              int p0, int p1, int k, double* lcol, double* dlds) {
     const int wv = threadIdx.x >> 6;
     if (wv == 0) {
         const bool ok = potrf_inv16(L + (long long)(16 * k) * np + 16 * k, np, lcol, dlds, Linv + 256 * k);
         if (!ok && threadIdx.x == 0) atomicOr(&a.st->fail[it], 1);
     }
     __syncthreads();
-    panel_column(L, np, tl, pptr, k, dlds, kSolveWaves);
+    panel_column(L, np, tl, p0, p1, k, dlds, kSolveWaves);
 }
 
 __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int it) {
@@ -904,7 +912,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
     double* L = a.L + a.comp_loff[comp];
     solve_damp(a, comp, s_lambda, L, np, kSolveThreads);
     __syncthreads();
-    factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, a.tl, a.tl + hdr[kHdrPanel], 0, lds + kPanelStride, lds);
+    const int* pptr = a.tl + hdr[kHdrPanel];
+    factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, a.tl, pptr[0], pptr[1], 0, lds + kPanelStride, lds);
 }
 
 // Workgroup 0's look-ahead in launch k: column k + 1 kept in LDS from its step-k update to its panel.
@@ -914,7 +923,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
 // operations, same order as factor_column over global memory.  sm: diagonal tile | L_kk^-1 | POTRF
 // columns (2 tiles) | ps panel images | tile row -> slot (nt + 1) | updated flags (ps).
 __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt, const int* tl,
-                                 const int* hdr, int k, int la_beg, int la_end, double* sm, int ps) {
+                                 int p0, int p1, int k, int la_beg, int la_end, double* sm, int ps) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
     double* dtile = sm;
     double* dlds = sm + kPanelStride;
@@ -922,8 +931,7 @@ __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Li
     double* pan = sm + 4 * kPanelStride;
     int* slot_of = reinterpret_cast<int*>(pan + (size_t)ps * kPanelStride);
     int* upd = slot_of + nt + 1;
-    const int* pptr = tl + hdr[kHdrPanel];
-    const int c1 = k + 1, p0 = pptr[c1], pn = pptr[c1 + 1] - p0;
+    const int c1 = k + 1, pn = p1 - p0;
     const bool in_lds = pn <= ps;
     for (int q = tid; q < pn; q += kSolveThreads) {
         slot_of[tl[p0 + q]] = q;
@@ -982,31 +990,42 @@ __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Li
 }
 
 // launch k of the factorisation (k = 0 .. max_nt - 2): blockIdx.x = component * G + g; ps: LDS panel
-// images of workgroup 0's look-ahead (0: the look-ahead over global memory, factor_column)
-__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int it, int k, int G, int ps) {
+// images of workgroup 0's look-ahead (0: the look-ahead over global memory, factor_column).  The
+// step's list bounds come as the launch argument sd for a one-component plan (sd.nt > 0), else from
+// the plan's descriptor table — loaded with the run flags, so the tile lists are the first dependent
+// loads.
+__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int it, int k, int G, int ps, FacStep sd) {
+    const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
+    if (sd.nt == 0) {
+        const int* d = a.fac_steps + 8 * ((size_t)comp * a.fac_nk + k);
+        const int4 d0 = *reinterpret_cast<const int4*>(d), d1 = *reinterpret_cast<const int4*>(d + 4);
+        sd.loff = (long long)(((unsigned long long)(unsigned)d0.y << 32) | (unsigned)d0.x);
+        sd.la_beg = d0.z;
+        sd.split = d0.w;
+        sd.t_end = d1.x;
+        sd.p0 = d1.y;
+        sd.p1 = d1.z;
+        sd.nt = d1.w;
+    }
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (k_sba_fac_begin's decision)
     extern __shared__ __attribute__((aligned(32))) double sm[];
-    const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
-    const int* hdr = a.comp_hdr + kHdrN * comp;
-    const int nt = hdr[kHdrNt], np = 16 * nt;
+    const int nt = sd.nt, np = 16 * nt;
     if (k + 1 >= nt) return;
-    double* L = a.L + a.comp_loff[comp];
+    double* L = a.L + sd.loff;
+    double* Linv = a.Linv + sd.loff;
     const int* tl = a.tl;
-    const int* tptr = tl + hdr[kHdrTrail];
-    const int split = tl[hdr[kHdrTrailSplit] + k];
     if (g == 0) {
-        if (G == 1) trail_tiles(L, np, tl, k, split, tptr[k + 1], 1, kSolveWaves);
+        if (G == 1) trail_tiles(L, np, tl, k, sd.split, sd.t_end, 1, kSolveWaves);
         if (ps > 0) {
-            lookahead_column(a, it, L, a.Linv + a.comp_loff[comp], np, nt, tl, hdr, k, tptr[k], split, sm, ps);
+            lookahead_column(a, it, L, Linv, np, nt, tl, sd.p0, sd.p1, k, sd.la_beg, sd.split, sm, ps);
         } else {
-            trail_tiles(L, np, tl, k, tptr[k], split, 1, kSolveWaves);
+            trail_tiles(L, np, tl, k, sd.la_beg, sd.split, 1, kSolveWaves);
             __syncthreads();
-            factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, tl, tl + hdr[kHdrPanel], k + 1, sm + kPanelStride,
-                          sm);
+            factor_column(a, it, L, Linv, np, tl, sd.p0, sd.p1, k + 1, sm + kPanelStride, sm);
         }
     } else {
-        trail_tiles(L, np, tl, k, split + (g - 1), tptr[k + 1], G - 1, kSolveWaves);
+        trail_tiles(L, np, tl, k, sd.split + (g - 1), sd.t_end, G - 1, kSolveWaves);
     }
 }
 
@@ -1166,6 +1185,8 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.dx = p->dx.as<double>();
     a.st = p->state.as<SBAState>();
     a.panel_slots = solve_panel_slots(p->max_np, p->max_panel);
+    a.fac_steps = p->fac_steps.as<int>();
+    a.fac_nk = std::max(p->max_nt - 1, 1);
     return a;
 }
 
@@ -1620,8 +1641,30 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     }
 
     
+    // the multi-workgroup factor's per-launch descriptors (FacStep: 8 ints per component and step)
+    {
+        const int fk = std::max(p->max_nt - 1, 1);
+        p->fac_steps_h.assign((size_t)8 * fk * std::max(p->n_comp, 1), 0);
+        for (int cc = 0; cc < p->n_comp; ++cc) {
+            const int* h = hdr.data() + (size_t)kHdrN * cc;
+            const int nt = h[kHdrNt];
+            for (int k = 0; k + 1 < nt; ++k) {
+                int* d = p->fac_steps_h.data() + 8 * ((size_t)cc * fk + k);
+                const unsigned long long lo = (unsigned long long)loff[cc];
+                d[0] = (int)(unsigned)(lo & 0xffffffffull);
+                d[1] = (int)(unsigned)(lo >> 32);
+                d[2] = tlist[h[kHdrTrail] + k];
+                d[3] = tlist[h[kHdrTrailSplit] + k];
+                d[4] = tlist[h[kHdrTrail] + k + 1];
+                d[5] = tlist[h[kHdrPanel] + k + 1];
+                d[6] = tlist[h[kHdrPanel] + k + 2];
+                d[7] = nt;
+            }
+        }
+    }
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
+    if ((rc = upload(c, p->fac_steps, p->fac_steps_h))) return rc;
     if ((rc = upload(c, p->kf_flags, flags))) return rc;
     if ((rc = upload(c, p->kf_comp, kcomp))) return rc;
     if ((rc = upload(c, p->kf_local, klocal))) return rc;
@@ -1740,9 +1783,21 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
         if (multi) {
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
                              c->stream, a, it));
-            for (int k = 0; k + 1 < p->max_nt; ++k)
+            for (int k = 0; k + 1 < p->max_nt; ++k) {
+                FacStep sd{};  // (one component: the step's bounds as launch arguments)
+                if (p->n_comp == 1) {
+                    const int* d = p->fac_steps_h.data() + 8 * (size_t)k;
+                    sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
+                    sd.la_beg = d[2];
+                    sd.split = d[3];
+                    sd.t_end = d[4];
+                    sd.p0 = d[5];
+                    sd.p1 = d[6];
+                    sd.nt = d[7];
+                }
                 VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_step, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads),
-                                 (uint32_t)la_lds, c->stream, a, it, k, G, la_ps));
+                                 (uint32_t)la_lds, c->stream, a, it, k, G, la_ps, sd));
+            }
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
                              (uint32_t)(p->max_np * sizeof(double)), c->stream, a, it));
         } else {

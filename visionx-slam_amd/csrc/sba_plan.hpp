@@ -33,6 +33,10 @@ struct vx_sba_plan {
     bool ran = false;
     bool from_dmap = false;
     vx::DevBuf lm_map_dev, kf_map_dev;  // dmap plans: slot -> resident landmark row, window row -> keyframe row
+    // the multi-workgroup factor's launch k per component: 8 ints {L offset lo, hi, look-ahead tiles
+    // [la_beg, split), rest [split, t_end), panel of column k + 1 [p0, p1), nt} (nt = 0: no step k)
+    std::vector<int> fac_steps_h;
+    vx::DevBuf fac_steps;
 };
 
 
