@@ -16,3 +16,6 @@ SBA_CFGS=C5-connected timeout -k 10 200 rocprofv3 --kernel-trace --output-format
 python3 scripts/sba_fac_trace.py $O/kt/kt_kernel_trace.csv > $O/sba_fac_trace.txt 2>&1
 rm -f $O/kt/kt_kernel_trace.csv
 cat $O/sba_fac_trace.txt
+for cols in 1 2; do
+  VX_SBA_FACTOR_COLS=$cols SBA_CFGS=C5-connected timeout -k 10 200 python3 scripts/sba_bench.py 10 > $O/sba_cols$cols.jsonl 2>&1 || exit 6
+done

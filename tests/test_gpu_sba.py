@@ -135,18 +135,21 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
     """The factorisation spread over G workgroups per component, one launch per tile step with the
     look-ahead column on workgroup 0 (k_sba_fac_begin / k_sba_fac_step / k_sba_backsub, the default),
     equals the one-workgroup k_sba_solve ($VX_SBA_FACTOR=single) bitwise, for one component, eight
-    independent ones and eight connected ones, with G = 1, 2 and the plan's own choice, and with the
-    look-ahead column in LDS (default) or over global memory ($VX_SBA_LOOKAHEAD_LDS=0)."""
+    independent ones and eight connected ones, with G = 1, 2, 3 and the plan's own choice, one tile
+    column per launch (k_sba_fac_step, its look-ahead column in LDS or over global memory) or two
+    (k_sba_fac_pair, the default)."""
     import vxslam
 
     name, nk, nl, ns, cf = cfg
     m = synth.make_ba_map(0x5EED0F00 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns, cross_frac=cf)
     opts = vxslam.default_sba_options(window=nk, iters=6)
     out = {}
-    for form, groups, la in (("single", None, "1"), ("multi", "1", "1"), ("multi", "2", "1"), ("multi", None, "1"),
-                             ("multi", "2", "0")):
+    for form, groups, la, cols in (("single", None, "1", "2"), ("multi", "1", "1", "1"), ("multi", "2", "1", "1"),
+                                   ("multi", None, "1", "1"), ("multi", "2", "0", "1"), ("multi", "1", "1", "2"),
+                                   ("multi", "3", "1", "2"), ("multi", None, "1", "2")):
         monkeypatch.setenv("VX_SBA_FACTOR", form)
         monkeypatch.setenv("VX_SBA_LOOKAHEAD_LDS", la)
+        monkeypatch.setenv("VX_SBA_FACTOR_COLS", cols)
         if groups:
             monkeypatch.setenv("VX_SBA_FACTOR_GROUPS", groups)
         else:
@@ -156,9 +159,9 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
         plan.run_async()
         st = plan.fetch(mm)
         plan.close()
-        out[(form, groups, la)] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
-                                   mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
-    ref = out[("single", None, "1")]
+        out[(form, groups, la, cols)] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
+                                         mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
+    ref = out[("single", None, "1", "2")]
     assert ref[1] >= 1
     for k, v in out.items():
         assert v == ref, k

@@ -138,6 +138,14 @@ struct SBAArgs {
     int panel_slots;        // k_sba_solve: LDS panel tiles (a step with more panel tiles reads global)
     const int* fac_steps;   // k_sba_fac_step descriptors (vx_sba_plan::fac_steps), fac_nk per component
     int fac_nk;
+    const int* fac_pairs;   // k_sba_fac_pair descriptors (vx_sba_plan::fac_pairs), fac_np per component
+    int fac_np;
+};
+
+// one launch of the two-column schedule for one component (vx_sba_plan::fac_pairs)
+struct FacPair {
+    long long loff;
+    int l1b, l1e, l2b, l2e, rb, re, p0, p1, q0, q1, nt, c0;
 };
 
 // one launch of the multi-workgroup factor for one component (vx_sba_plan::fac_steps)
@@ -899,7 +907,8 @@ __device__ __forceinline__ void factor_column(const SBAArgs& a, int it, double* 
     panel_column(L, np, tl, p0, p1, k, dlds, kSolveWaves);
 }
 
-__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int it) {
+// pair: also column 1 (step 0's update of it, then its factor) for the two-column schedule
+__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int it, int pair) {
     if (it > 0 && !a.st->active[it]) return;
     __shared__ int s_solve;
     __shared__ double s_lambda;
@@ -914,6 +923,13 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
     __syncthreads();
     const int* pptr = a.tl + hdr[kHdrPanel];
     factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, a.tl, pptr[0], pptr[1], 0, lds + kPanelStride, lds);
+    if (pair && nt > 1) {
+        const int* tptr = a.tl + hdr[kHdrTrail];
+        __syncthreads();
+        trail_tiles(L, np, a.tl, 0, tptr[0], a.tl[hdr[kHdrTrailSplit]], 1, kSolveWaves);
+        __syncthreads();
+        factor_column(a, it, L, a.Linv + a.comp_loff[comp], np, a.tl, pptr[1], pptr[2], 1, lds + kPanelStride, lds);
+    }
 }
 
 // Workgroup 0's look-ahead in launch k: column k + 1 kept in LDS from its step-k update to its panel.
@@ -1026,6 +1042,91 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int i
         }
     } else {
         trail_tiles(L, np, tl, k, sd.split + (g - 1), sd.t_end, G - 1, kSolveWaves);
+    }
+}
+
+// Tiles of the two-column schedule, entries i << 16 | c << 2 | mask, taking steps s0 (mask bit 0)
+// and s0 + 1 (bit 1) in that order — the per-tile sequence of the one-step schedule, one load and one
+// store instead of two; entries beg, beg + stride, ...; four per wave in flight
+__device__ __forceinline__ void masked_tiles(double* L, int np, const int* tl, int s0, int beg, int end, int stride,
+                                             int waves) {
+    const int wv = threadIdx.x >> 6;
+    const int cnt = end > beg ? (end - beg + stride - 1) / stride : 0;
+    for (int m0 = wv * 4; m0 < cnt; m0 += waves * 4) {
+        d4 c[4];
+        int ti[4], tj[4], mk[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ti[q] = -1;
+            if (m0 + q < cnt) {
+                const int e = tl[beg + (m0 + q) * stride];
+                ti[q] = e >> 16;
+                tj[q] = (e >> 2) & 0x3fff;
+                mk[q] = e & 3;
+                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (ti[q] < 0) continue;
+            if (mk[q] & 1)
+                c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * s0, L + (long long)(16 * tj[q]) * np + 16 * s0,
+                                  np, c[q]);
+            if (mk[q] & 2)
+                c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * (s0 + 1),
+                                  L + (long long)(16 * tj[q]) * np + 16 * (s0 + 1), np, c[q]);
+            store_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np, c[q]);
+        }
+    }
+}
+
+// Launch t of the two-column schedule (columns 0 and 1 factored by k_sba_fac_begin): steps 2t and
+// 2t + 1 are applied — workgroup 0 to columns c0 = 2t + 2 and c0 + 1 (phase 1), then it factors c0,
+// applies step c0 to column c0 + 1 (phase 2) and factors that; the other G - 1 workgroups apply both
+// steps to the columns beyond.  Every tile still receives its steps in ascending order, so the
+// factor is bitwise the one-step schedule's; half the launches.
+__global__ __launch_bounds__(kSolveThreads) void k_sba_fac_pair(SBAArgs a, int it, int t, int G, FacPair sd) {
+    const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
+    if (sd.nt == 0) {
+        const int* d = a.fac_pairs + 16 * ((size_t)comp * a.fac_np + t);
+        const int4 d0 = *reinterpret_cast<const int4*>(d), d1 = *reinterpret_cast<const int4*>(d + 4),
+                   d2 = *reinterpret_cast<const int4*>(d + 8), d3 = *reinterpret_cast<const int4*>(d + 12);
+        sd.loff = (long long)(((unsigned long long)(unsigned)d0.y << 32) | (unsigned)d0.x);
+        sd.l1b = d0.z;
+        sd.l1e = d0.w;
+        sd.l2b = d1.x;
+        sd.l2e = d1.y;
+        sd.rb = d1.z;
+        sd.re = d1.w;
+        sd.p0 = d2.x;
+        sd.p1 = d2.y;
+        sd.q0 = d2.z;
+        sd.q1 = d2.w;
+        sd.nt = d3.x;
+        sd.c0 = d3.y;
+    }
+    if (it > 0 && !a.st->active[it]) return;
+    if (!a.st->lm[(it + 1) & 1].do_solve) return;
+    __shared__ __attribute__((aligned(32))) double lds[3 * kPanelStride];
+    const int nt = sd.nt, np = 16 * nt, c0 = sd.c0;
+    if (c0 >= nt) return;
+    double* L = a.L + sd.loff;
+    double* Linv = a.Linv + sd.loff;
+    const int* tl = a.tl;
+    const int s0 = c0 - 2;
+    if (g == 0) {
+        masked_tiles(L, np, tl, s0, sd.l1b, sd.l1e, 1, kSolveWaves);
+        if (G == 1) masked_tiles(L, np, tl, s0, sd.rb, sd.re, 1, kSolveWaves);
+        __syncthreads();
+        factor_column(a, it, L, Linv, np, tl, sd.p0, sd.p1, c0, lds + kPanelStride, lds);
+        if (c0 + 1 < nt) {
+            __syncthreads();
+            trail_tiles(L, np, tl, c0, sd.l2b, sd.l2e, 1, kSolveWaves);
+            __syncthreads();
+            factor_column(a, it, L, Linv, np, tl, sd.q0, sd.q1, c0 + 1, lds + kPanelStride, lds);
+        }
+    } else {
+        masked_tiles(L, np, tl, s0, sd.rb + (g - 1), sd.re, G - 1, kSolveWaves);
     }
 }
 
@@ -1187,6 +1288,8 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.panel_slots = solve_panel_slots(p->max_np, p->max_panel);
     a.fac_steps = p->fac_steps.as<int>();
     a.fac_nk = std::max(p->max_nt - 1, 1);
+    a.fac_pairs = p->fac_pairs.as<int>();
+    a.fac_np = std::max(p->max_pairs, 1);
     return a;
 }
 
@@ -1556,6 +1659,8 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     p->n_lfactor_tiles = p->n_trail_updates = 0;
     p->max_panel = 1;
     p->max_nt = p->max_trail_rest = 0;
+    p->max_pairs = 0;
+    std::vector<std::vector<int>> pair_desc(std::max(p->n_comp, 1));
     {
         std::vector<std::vector<std::pair<int, int>>> cblk(p->n_comp);
         for (const int2& b : bij) {
@@ -1637,6 +1742,51 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                     if (NZ(k, m2)) tlist.push_back(m2);
             }
             tlist[bp + nt] = (int)tlist.size();
+            // the two-column schedule's lists (k_sba_fac_pair): launch t applies steps s0 = 2t and
+            // s0 + 1 (entries i << 16 | c << 2 | mask) — phase 1: columns c0 = 2t + 2, c0 + 1; phase 2:
+            // step c0 on column c0 + 1 (one-step entries); rest: the columns beyond
+            auto mask_of = [&](int i, int c, int s0) {
+                const bool a0 = (i == nt || NZ(i, s0)) && NZ(c, s0);
+                const bool a1 = (i == nt || NZ(i, s0 + 1)) && NZ(c, s0 + 1);
+                return (a0 ? 1 : 0) | (a1 ? 2 : 0);
+            };
+            auto& pd = pair_desc[cc];
+            for (int c0 = 2; c0 < nt; c0 += 2) {
+                const int s0 = c0 - 2, c1 = c0 + 1;
+                int d[16] = {0};
+                const unsigned long long lo = (unsigned long long)loff[cc];
+                d[0] = (int)(unsigned)(lo & 0xffffffffull);
+                d[1] = (int)(unsigned)(lo >> 32);
+                d[2] = (int)tlist.size();
+                for (int c = c0; c <= std::min(c1, nt - 1); ++c)
+                    for (int i = c; i <= nt; ++i) {
+                        const int mk = mask_of(i, c, s0);
+                        if (mk) tlist.push_back(i << 16 | c << 2 | mk);
+                    }
+                d[3] = (int)tlist.size();
+                d[4] = (int)tlist.size();
+                if (c1 < nt && NZ(c1, c0)) {
+                    for (int i = c1; i < nt; ++i)
+                        if (NZ(i, c0)) tlist.push_back(i << 16 | c1);
+                    tlist.push_back(nt << 16 | c1);
+                }
+                d[5] = (int)tlist.size();
+                d[6] = (int)tlist.size();
+                for (int j = c1 + 1; j < nt; ++j)
+                    for (int i = j; i <= nt; ++i) {
+                        const int mk = mask_of(i, j, s0);
+                        if (mk) tlist.push_back(i << 16 | j << 2 | mk);
+                    }
+                d[7] = (int)tlist.size();
+                d[8] = tlist[h[kHdrPanel] + c0];
+                d[9] = tlist[h[kHdrPanel] + c0 + 1];
+                d[10] = c1 < nt ? tlist[h[kHdrPanel] + c1] : 0;
+                d[11] = c1 < nt ? tlist[h[kHdrPanel] + c1 + 1] : 0;
+                d[12] = nt;
+                d[13] = c0;
+                pd.insert(pd.end(), d, d + 16);
+            }
+            p->max_pairs = std::max(p->max_pairs, (int)(pd.size() / 16));
         }
     }
 
@@ -1662,9 +1812,16 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
             }
         }
     }
+    {
+        const int fp = std::max(p->max_pairs, 1);
+        p->fac_pairs_h.assign((size_t)16 * fp * std::max(p->n_comp, 1), 0);
+        for (int cc = 0; cc < p->n_comp; ++cc)
+            std::copy(pair_desc[cc].begin(), pair_desc[cc].end(), p->fac_pairs_h.begin() + (size_t)16 * fp * cc);
+    }
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
     if ((rc = upload(c, p->fac_steps, p->fac_steps_h))) return rc;
+    if ((rc = upload(c, p->fac_pairs, p->fac_pairs_h))) return rc;
     if ((rc = upload(c, p->kf_flags, flags))) return rc;
     if ((rc = upload(c, p->kf_comp, kcomp))) return rc;
     if ((rc = upload(c, p->kf_local, klocal))) return rc;
@@ -1758,6 +1915,8 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
     // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
     const bool multi = factor_multi(p->max_nt);
     const int G = factor_groups(p->max_trail_rest);
+    // two tile columns per launch (default) or one ($VX_SBA_FACTOR_COLS=1)
+    const bool pair = !(std::getenv("VX_SBA_FACTOR_COLS") && std::atoi(std::getenv("VX_SBA_FACTOR_COLS")) == 1);
     // workgroup 0's look-ahead column in LDS when its panel fits ($VX_SBA_LOOKAHEAD_LDS=0: global)
     int la_ps = std::max(p->max_panel, 1);
     size_t la_lds = lookahead_lds_bytes(p->max_nt, la_ps);
@@ -1782,8 +1941,19 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
 #endif
         if (multi) {
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
-                             c->stream, a, it));
-            for (int k = 0; k + 1 < p->max_nt; ++k) {
+                             c->stream, a, it, pair ? 1 : 0));
+            for (int t = 0; pair && t < p->max_pairs; ++t) {
+                FacPair sd{};  // (one component: the launch's bounds as arguments)
+                if (p->n_comp == 1) {
+                    const int* d = p->fac_pairs_h.data() + 16 * (size_t)t;
+                    sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
+                    sd.l1b = d[2], sd.l1e = d[3], sd.l2b = d[4], sd.l2e = d[5], sd.rb = d[6], sd.re = d[7];
+                    sd.p0 = d[8], sd.p1 = d[9], sd.q0 = d[10], sd.q1 = d[11], sd.nt = d[12], sd.c0 = d[13];
+                }
+                VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_pair, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads), 0,
+                                 c->stream, a, it, t, G, sd));
+            }
+            for (int k = 0; !pair && k + 1 < p->max_nt; ++k) {
                 FacStep sd{};  // (one component: the step's bounds as launch arguments)
                 if (p->n_comp == 1) {
                     const int* d = p->fac_steps_h.data() + 8 * (size_t)k;

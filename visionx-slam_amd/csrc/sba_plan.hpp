@@ -37,6 +37,12 @@ struct vx_sba_plan {
     // [la_beg, split), rest [split, t_end), panel of column k + 1 [p0, p1), nt} (nt = 0: no step k)
     std::vector<int> fac_steps_h;
     vx::DevBuf fac_steps;
+    // the two-column schedule (launch t factors columns 2t + 2 and 2t + 3): 16 ints per component and
+    // launch {L offset lo, hi, phase-1 list [b, e), phase-2 list [b, e), rest [b, e), panel of c0
+    // [b, e), panel of c1 [b, e), nt, c0, 0}; max_pairs launches
+    std::vector<int> fac_pairs_h;
+    vx::DevBuf fac_pairs;
+    int max_pairs = 0;
 };
 
 
