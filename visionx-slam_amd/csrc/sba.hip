@@ -656,6 +656,14 @@ __device__ void solve_damp(const SBAArgs& a, int comp, double lambda, double* L,
 // on global memory; tiles beyond kBsPre per wave are read in place.  Same sums in the same order as
 // the plain loop (bitwise).
 constexpr int kBsPre = 4;
+// A workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding global
+// load (its workgroup-scope fence covers global memory), which would drain the prefetches issued
+// before it.  For phases that communicate through LDS alone.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 __device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, const int* tl, const int* bptr,
                                         int k, double (&li)[4], double (&tv)[kBsPre][4], int (&tm)[kBsPre]) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
@@ -682,7 +690,7 @@ __device__ void back_substitute(const double* L, const double* Linv, int np, int
     double li[4] = {0, 0, 0, 0}, tv[kBsPre][4];
     int tm[kBsPre];
     bs_load(L, Linv, np, tl, bptr, nt - 1, li, tv, tm);
-    __syncthreads();
+    lds_barrier();
     for (int k = nt - 1; k >= 0; --k) {
         double nli[4] = {0, 0, 0, 0}, ntv[kBsPre][4];
         int ntm[kBsPre];
@@ -696,7 +704,7 @@ __device__ void back_substitute(const double* L, const double* Linv, int np, int
             // (every lane's reads of y_k precede this write: the shuffles consumed them)
             if (r0 == 0) ys[16 * k + cl] = xk;
         }
-        __syncthreads();
+        lds_barrier();
         // y_m -= L_km^T x_k for the nonzero tiles of row k, one wave per tile
 #pragma unroll
         for (int j = 0; j < kBsPre; ++j) {
@@ -718,7 +726,7 @@ __device__ void back_substitute(const double* L, const double* Linv, int np, int
             p += __shfl_xor(p, 32, 64);
             if (r0 == 0) ys[16 * mm + cl] -= p;
         }
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int r = 0; r < 4; ++r) li[r] = nli[r];
 #pragma unroll
@@ -939,7 +947,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
 // operations, same order as factor_column over global memory.  sm: diagonal tile | L_kk^-1 | POTRF
 // columns (2 tiles) | ps panel images | tile row -> slot (nt + 1) | updated flags (ps).
 __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt, const int* tl,
-                                 int p0, int p1, int k, int la_beg, int la_end, double* sm, int ps) {
+                                 int p0, int p1, int k, int la_beg, int la_end, double* sm, int ps, bool kt) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
     double* dtile = sm;
     double* dlds = sm + kPanelStride;
@@ -954,6 +962,7 @@ __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Li
         if (in_lds) upd[q] = 0;
     }
     __syncthreads();
+    if (kt) VX_KT(2);
     // step k's update of column k + 1 (the diagonal tile is the first entry when the column has one)
     const bool diag = la_end > la_beg;
     const int cnt = la_end - la_beg;
@@ -983,13 +992,17 @@ __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Li
             }
         }
     }
-    __syncthreads();
+    if (kt) VX_KT(3);
+    if (in_lds) lds_barrier();  // (the look-ahead tiles went to LDS; otherwise to global memory)
+    else __syncthreads();
+    if (kt) VX_KT(4);
     if (wv == 0) {
         const bool ok = diag ? potrf_inv16(dtile, 16, lcol, dlds, Linv + 256 * c1)
                              : potrf_inv16(L + (long long)(16 * c1) * np + 16 * c1, np, lcol, dlds, Linv + 256 * c1);
         if (!ok && tid == 0) atomicOr(&a.st->fail[it], 1);
     }
-    __syncthreads();
+    lds_barrier();  // (L_kk^-1 in LDS)
+    if (kt) VX_KT(5);
     // the panel L_i,k+1 = A_i,k+1 L_k+1,k+1^-T: updated tiles from LDS, the others from global
     for (int q = wv; q < pn; q += kSolveWaves) {
         double* Aik = L + (long long)(16 * tl[p0 + q]) * np + 16 * c1;
@@ -1003,6 +1016,7 @@ __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Li
         c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, c, 0, 0, 0);
         store_acc(Aik, np, c);
     }
+    if (kt) VX_KT(6);
 }
 
 // launch k of the factorisation (k = 0 .. max_nt - 2): blockIdx.x = component * G + g; ps: LDS panel
@@ -1023,8 +1037,12 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int i
         sd.p1 = d1.z;
         sd.nt = d1.w;
     }
+    // trace build: the phases of launch k = nt / 2 (slots 0-7, workgroup 0 and the rest)
+    const bool kt = k == sd.nt / 2;
+    if (kt) VX_KT(0);
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (k_sba_fac_begin's decision)
+    if (kt) VX_KT(1);
     extern __shared__ __attribute__((aligned(32))) double sm[];
     const int nt = sd.nt, np = 16 * nt;
     if (k + 1 >= nt) return;
@@ -1034,7 +1052,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int i
     if (g == 0) {
         if (G == 1) trail_tiles(L, np, tl, k, sd.split, sd.t_end, 1, kSolveWaves);
         if (ps > 0) {
-            lookahead_column(a, it, L, Linv, np, nt, tl, sd.p0, sd.p1, k, sd.la_beg, sd.split, sm, ps);
+            lookahead_column(a, it, L, Linv, np, nt, tl, sd.p0, sd.p1, k, sd.la_beg, sd.split, sm, ps, kt);
         } else {
             trail_tiles(L, np, tl, k, sd.la_beg, sd.split, 1, kSolveWaves);
             __syncthreads();
@@ -1042,6 +1060,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_step(SBAArgs a, int i
         }
     } else {
         trail_tiles(L, np, tl, k, sd.split + (g - 1), sd.t_end, G - 1, kSolveWaves);
+        if (kt) VX_KT(7);
     }
 }
 
@@ -1143,7 +1162,9 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it
     const double* Linv = a.Linv + a.comp_loff[comp];
     const int* tl = a.tl;
     const int* bptr = tl + hdr[kHdrBack];
+    VX_KT(8);
     back_substitute(L, Linv, np, nt, tl, bptr, ys);
+    VX_KT(9);
     for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
     const int* cp = tl + hdr[kHdrCopy];
     const int ncp = hdr[kHdrNCopy];
