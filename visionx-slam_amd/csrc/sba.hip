@@ -650,91 +650,78 @@ __device__ void solve_damp(const SBAArgs& a, int comp, double lambda, double* L,
 }
 
 // Blocked back-substitution L^T x = y over the component's tile rows, descending (ys: y in LDS,
-// overwritten with x): x_k = L_kk^-T y_k by wave 0, then y_m -= L_km^T x_k over row k's nonzero tiles,
-// one wave per tile.  The operands of step k - 1 (L_kk^-1 and up to kBsPre tiles per wave) are
-// loaded while step k runs — they do not depend on x — so a step waits on LDS and two barriers, not
-// on global memory; tiles beyond kBsPre per wave are read in place.  Same sums in the same order as
-// the plain loop (bitwise).
-constexpr int kBsPre = 4;
-// A workgroup barrier that orders LDS only: __syncthreads() also waits for every outstanding global
-// load (its workgroup-scope fence covers global memory), which would drain the prefetches issued
-// before it.  For phases that communicate through LDS alone.
-__device__ __forceinline__ void lds_barrier() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+// overwritten with x): x_k = L_kk^-T y_k, then y_m -= L_km^T x_k over row k's nonzero tiles.  Lanes
+// work in 16-lane groups, lane c of a group forming column c's dot product over the 16 rows in order
+// (no cross-lane reduction); the 16 groups of the workgroup take one tile each per step, wave 0's
+// first group also x_k.  The operands of step k - 1 (L_kk^-1 and one tile per group) are loaded,
+// unconditionally (absent tiles read a valid one and are not used), while step k runs: they do not
+// depend on x, so a step waits on LDS and two barriers, not on global memory.  Rows with more than 16
+// nonzero tiles take the rest in place.
+constexpr int kBsGroups = kSolveThreads / 16;
+// tile column of this group's tile in row k (-1: none); its load is issued a step before the tile's
+__device__ __forceinline__ int bs_index(const int* tl, const int* bptr, int k) {
+    const int grp = threadIdx.x >> 4;
+    const int q = bptr[k] + grp;
+    return q < bptr[k + 1] ? tl[q] : -1;
 }
-__device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, const int* tl, const int* bptr,
-                                        int k, double (&li)[4], double (&tv)[kBsPre][4], int (&tm)[kBsPre]) {
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
-    if (wv == 0) {
-        const double* Li = Linv + 256 * k;
+__device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, int k, int tm, double (&li)[16],
+                                        double (&tv)[16]) {
+    const int c = threadIdx.x & 15;
+    const double* Li = Linv + 256 * k;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) li[r] = Li[(4 * r0 + r) * 16 + cl];
-    }
+    for (int r = 0; r < 16; ++r) li[r] = Li[r * 16 + c];  // (every group: uniform code, no branch)
+    const double* Lkm = L + (long long)(16 * k) * np + 16 * (tm >= 0 ? tm : k);
 #pragma unroll
-    for (int j = 0; j < kBsPre; ++j) {
-        const int q = bptr[k] + wv + kSolveWaves * j;
-        tm[j] = q < bptr[k + 1] ? tl[q] : -1;
-        if (tm[j] >= 0) {
-            const double* Lkm = L + (long long)(16 * k) * np + 16 * tm[j];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) tv[j][r] = Lkm[(long long)(4 * r0 + r) * np + cl];
-        }
-    }
+    for (int r = 0; r < 16; ++r) tv[r] = Lkm[(long long)r * np + c];
 }
-__device__ void back_substitute(const double* L, const double* Linv, int np, int nt, const int* tl, const int* bptr,
-                                double* ys) {
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
-    for (int c = tid; c < np; c += kSolveThreads) ys[c] = L[(long long)np * np + c];
-    double li[4] = {0, 0, 0, 0}, tv[kBsPre][4];
-    int tm[kBsPre];
-    bs_load(L, Linv, np, tl, bptr, nt - 1, li, tv, tm);
-    lds_barrier();
+// column c's dot product over 16 rows: four interleaved FMA chains, combined pairwise
+__device__ __forceinline__ double bs_dot(const double (&w)[16], const double* x) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r & 3] = fma(w[r], x[r], acc[r & 3]);
+    return (acc[0] + acc[1]) + (acc[2] + acc[3]);
+}
+__device__ __forceinline__ void back_substitute(const double* L, const double* Linv, int np, int nt, const int* tl,
+                                                const int* bptr, double* ys) {
+    const int tid = threadIdx.x, grp = tid >> 4, c = tid & 15;
+    for (int e = tid; e < np; e += kSolveThreads) ys[e] = L[(long long)np * np + e];
+    double li[16], tv[16];
+    int tm = bs_index(tl, bptr, nt - 1);
+    int tm1 = nt > 1 ? bs_index(tl, bptr, nt - 2) : -1;
+    bs_load(L, Linv, np, nt - 1, tm, li, tv);
+    __syncthreads();
     for (int k = nt - 1; k >= 0; --k) {
-        double nli[4] = {0, 0, 0, 0}, ntv[kBsPre][4];
-        int ntm[kBsPre];
-        if (k > 0) bs_load(L, Linv, np, tl, bptr, k - 1, nli, ntv, ntm);
-        if (wv == 0) {  // x_k = L_kk^-T y_k (wave 0 reads y_k before it writes x_k over it)
-            double xk = 0.0;
+        // operands of step k - 1 (index loaded a step ago) and the index of step k - 2
+        double nli[16], ntv[16];
+        bs_load(L, Linv, np, k > 0 ? k - 1 : 0, tm1, nli, ntv);
+        const int tm2 = k > 1 ? bs_index(tl, bptr, k - 2) : -1;
+        if (grp == 0) {  // x_k = L_kk^-T y_k (lane c: column c of L_kk^-1)
+            double yk[16];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) xk += li[r] * ys[16 * k + 4 * r0 + r];
-            xk += __shfl_xor(xk, 16, 64);
-            xk += __shfl_xor(xk, 32, 64);
-            // (every lane's reads of y_k precede this write: the shuffles consumed them)
-            if (r0 == 0) ys[16 * k + cl] = xk;
+            for (int r = 0; r < 16; ++r) yk[r] = ys[16 * k + r];
+            ys[16 * k + c] = bs_dot(li, yk);  // (the group's reads of y_k precede its writes)
         }
-        lds_barrier();
-        // y_m -= L_km^T x_k for the nonzero tiles of row k, one wave per tile
+        __syncthreads();
+        double xk[16];
 #pragma unroll
-        for (int j = 0; j < kBsPre; ++j) {
-            if (tm[j] < 0) continue;
-            double p = 0.0;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) p += tv[j][r] * ys[16 * k + 4 * r0 + r];
-            p += __shfl_xor(p, 16, 64);
-            p += __shfl_xor(p, 32, 64);
-            if (r0 == 0) ys[16 * tm[j] + cl] -= p;
-        }
-        for (int q = bptr[k] + wv + kSolveWaves * kBsPre; q < bptr[k + 1]; q += kSolveWaves) {
+        for (int r = 0; r < 16; ++r) xk[r] = ys[16 * k + r];
+        if (tm >= 0) ys[16 * tm + c] -= bs_dot(tv, xk);  // y_m -= L_km^T x_k
+        for (int q = bptr[k] + kBsGroups + grp; q < bptr[k + 1]; q += kBsGroups) {
             const int mm = tl[q];
             const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
-            double p = 0.0;
+            double w[16];
 #pragma unroll
-            for (int r = 4 * r0; r < 4 * r0 + 4; ++r) p += Lkm[(long long)r * np + cl] * ys[16 * k + r];
-            p += __shfl_xor(p, 16, 64);
-            p += __shfl_xor(p, 32, 64);
-            if (r0 == 0) ys[16 * mm + cl] -= p;
+            for (int r = 0; r < 16; ++r) w[r] = Lkm[(long long)r * np + c];
+            ys[16 * mm + c] -= bs_dot(w, xk);
         }
-        lds_barrier();
+        __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) li[r] = nli[r];
-#pragma unroll
-        for (int j = 0; j < kBsPre; ++j) {
-            tm[j] = ntm[j];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) tv[j][r] = ntv[j][r];
+        for (int r = 0; r < 16; ++r) {
+            li[r] = nli[r];
+            tv[r] = ntv[r];
         }
+        tm = tm1;
+        tm1 = tm2;
     }
 }
 
@@ -993,15 +980,14 @@ __device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Li
         }
     }
     if (kt) VX_KT(3);
-    if (in_lds) lds_barrier();  // (the look-ahead tiles went to LDS; otherwise to global memory)
-    else __syncthreads();
+    __syncthreads();
     if (kt) VX_KT(4);
     if (wv == 0) {
         const bool ok = diag ? potrf_inv16(dtile, 16, lcol, dlds, Linv + 256 * c1)
                              : potrf_inv16(L + (long long)(16 * c1) * np + 16 * c1, np, lcol, dlds, Linv + 256 * c1);
         if (!ok && tid == 0) atomicOr(&a.st->fail[it], 1);
     }
-    lds_barrier();  // (L_kk^-1 in LDS)
+    __syncthreads();
     if (kt) VX_KT(5);
     // the panel L_i,k+1 = A_i,k+1 L_k+1,k+1^-T: updated tiles from LDS, the others from global
     for (int q = wv; q < pn; q += kSolveWaves) {
