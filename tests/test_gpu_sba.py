@@ -137,7 +137,7 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
     equals the one-workgroup k_sba_solve ($VX_SBA_FACTOR=single) bitwise, for one component, eight
     independent ones and eight connected ones, with G = 1, 2, 3 and the plan's own choice, one tile
     column per launch (k_sba_fac_step, its look-ahead column in LDS or over global memory) or two
-    (k_sba_fac_pair, the default)."""
+    (k_sba_fac_pair, $VX_SBA_FACTOR_COLS=2)."""
     import vxslam
 
     name, nk, nl, ns, cf = cfg

@@ -1922,8 +1922,10 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
     // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
     const bool multi = factor_multi(p->max_nt);
     const int G = factor_groups(p->max_trail_rest);
-    // two tile columns per launch (default) or one ($VX_SBA_FACTOR_COLS=1)
-    const bool pair = !(std::getenv("VX_SBA_FACTOR_COLS") && std::atoi(std::getenv("VX_SBA_FACTOR_COLS")) == 1);
+    // one tile column per launch (default) or two ($VX_SBA_FACTOR_COLS=2: half the launches, but
+    // workgroup 0's chain per launch doubles — measured slower on the connected C5, 1137 against 1030
+    // us per LM iteration, profiles/r04/sba_cols*_r04j.jsonl)
+    const bool pair = std::getenv("VX_SBA_FACTOR_COLS") && std::atoi(std::getenv("VX_SBA_FACTOR_COLS")) == 2;
     // workgroup 0's look-ahead column in LDS when its panel fits ($VX_SBA_LOOKAHEAD_LDS=0: global)
     int la_ps = std::max(p->max_panel, 1);
     size_t la_lds = lookahead_lds_bytes(p->max_nt, la_ps);
