@@ -529,7 +529,7 @@ __device__ __forceinline__ void store_acc_opo(double* S, d4 v) {
 // lane, so the chain per column is readlane -> rsq (+2 Newton) -> mul -> LDS round trip -> fma.
 // L^-1 (lane i = column i, right-looking forward substitution over the LDS columns) is written as
 // an operand-order LDS image and row-major to Lg.  Returns false on a non-positive pivot.
-__device__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
+__device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
     const int lane = threadIdx.x & 63, i = lane & 15;
     double a[16];
 #pragma unroll
@@ -582,7 +582,7 @@ enum {
 
 // Levenberg-Marquardt decision (wave 0 of every workgroup computes it from the fixed-order totals,
 // identically; workgroup 0 of component 0 publishes the state): *s_solve / *s_lambda in LDS.
-__device__ void solve_decide(const SBAArgs& a, int it, bool publish, int* s_solve, double* s_lambda) {
+__device__ __forceinline__ void solve_decide(const SBAArgs& a, int it, bool publish, int* s_solve, double* s_lambda) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int n6 = 6 * a.nk;
     const double* rhs_g = a.red_sum + a.s_total;
@@ -632,7 +632,7 @@ __device__ void solve_decide(const SBAArgs& a, int it, bool publish, int* s_solv
 
 // k_sba_blocks wrote the component matrix straight into L (the all-reduce did, sharded): add the
 // damping on the diagonal, the identity on padding rows and the rhs tile row
-__device__ void solve_damp(const SBAArgs& a, int comp, double lambda, double* L, int np, int threads) {
+__device__ __forceinline__ void solve_damp(const SBAArgs& a, int comp, double lambda, double* L, int np, int threads) {
     const int n6 = 6 * a.nk;
     const double* rhs_g = a.red_sum + a.s_total;
     const int kq0 = a.comp_kf_ptr[comp], nc = 6 * (a.comp_kf_ptr[comp + 1] - kq0);
@@ -933,7 +933,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
 // panel overwrites the off-diagonal ones and only L_kk^-1 of a diagonal tile is read later.  Same
 // operations, same order as factor_column over global memory.  sm: diagonal tile | L_kk^-1 | POTRF
 // columns (2 tiles) | ps panel images | tile row -> slot (nt + 1) | updated flags (ps).
-__device__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt, const int* tl,
+__device__ __forceinline__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt, const int* tl,
                                  int p0, int p1, int k, int la_beg, int la_end, double* sm, int ps, bool kt) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
     double* dtile = sm;
