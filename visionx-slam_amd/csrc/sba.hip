@@ -524,9 +524,10 @@ __device__ __forceinline__ void store_acc_opo(double* S, d4 v) {
 
 // One wave: Cholesky of the symmetric 16x16 tile at A (lower triangle read) and the inverse of its
 // factor.  Lane i holds row i in registers.  Per column j the pivot comes from lane j
-// (v_readlane), every lane scales its entry, writes it to the LDS column image `lcol` and reads the
-// column back with broadcast ds_reads for its rank-1 update; the next pivot is updated by its own
-// lane, so the chain per column is readlane -> rsq (+2 Newton) -> mul -> LDS round trip -> fma.
+// (v_readlane), every lane scales its entry and takes the column's other entries from their lanes
+// by v_readlane for its rank-1 update — no LDS round trip on the chain, which per column is
+// readlane -> rsq (+ Newton) -> mul -> readlane -> fma; the column also goes to the LDS image
+// `lcol` for the inverse, off the chain.
 // L^-1 (lane i = column i, right-looking forward substitution over the LDS columns) is written as
 // an operand-order LDS image and row-major to Lg.  Returns false on a non-positive pivot.
 __device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
@@ -546,7 +547,7 @@ __device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lco
         a[j] = l;
         if (lane < 16) lcol[16 * j + i] = l;
 #pragma unroll
-        for (int c = j + 1; c < 16; ++c) a[c] = fma(-l, lcol[16 * j + c], a[c]);
+        for (int c = j + 1; c < 16; ++c) a[c] = fma(-l, rl(l, c), a[c]);  // (L[c][j] from lane c)
     }
     if (lane < 16) lcol[256 + i] = srow;
     double x[16];
