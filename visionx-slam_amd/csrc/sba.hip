@@ -140,6 +140,7 @@ struct SBAArgs {
     int fac_nk;
     const int* fac_pairs;   // k_sba_fac_pair descriptors (vx_sba_plan::fac_pairs), fac_np per component
     int fac_np;
+    int bs_np, bs_nt;       // k_sba_backsub's LDS: the largest component's np doubles, nt + 1 pointers
 };
 
 // one launch of the two-column schedule for one component (vx_sba_plan::fac_pairs)
@@ -659,18 +660,19 @@ __device__ __forceinline__ void solve_damp(const SBAArgs& a, int comp, double la
 // depend on x, so a step waits on LDS and two barriers, not on global memory.  Rows with more than 16
 // nonzero tiles take the rest in place.
 constexpr int kBsGroups = kSolveThreads / 16;
-// tile column of this group's tile in row k (-1: none); its load is issued a step before the tile's
-__device__ __forceinline__ int bs_index(const int* tl, const int* bptr, int k) {
-    const int grp = threadIdx.x >> 4;
-    const int q = bptr[k] + grp;
-    return q < bptr[k + 1] ? tl[q] : -1;
-}
-__device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, int k, int tm, double (&li)[16],
-                                        double (&tv)[16]) {
-    const int c = threadIdx.x & 15;
-    const double* Li = Linv + 256 * k;
+constexpr int kBsDepth = 3;  // steps of operands in flight
+// operands of step k: L_kk^-1 column c (wave 0 only: a wave-uniform branch) and the group's tile of
+// row k (absent: a valid tile, unused); sbp / sbl: the row pointers / tile columns in LDS
+__device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, int k, const int* sbp,
+                                        const int* sbl, double (&li)[16], double (&tv)[16], int& tm) {
+    const int grp = threadIdx.x >> 4, c = threadIdx.x & 15;
+    if ((threadIdx.x >> 6) == 0) {
+        const double* Li = Linv + 256 * k;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) li[r] = Li[r * 16 + c];  // (every group: uniform code, no branch)
+        for (int r = 0; r < 16; ++r) li[r] = Li[r * 16 + c];
+    }
+    const int q = sbp[k] + grp;
+    tm = q < sbp[k + 1] ? sbl[q] : -1;
     const double* Lkm = L + (long long)(16 * k) * np + 16 * (tm >= 0 ? tm : k);
 #pragma unroll
     for (int r = 0; r < 16; ++r) tv[r] = Lkm[(long long)r * np + c];
@@ -682,47 +684,56 @@ __device__ __forceinline__ double bs_dot(const double (&w)[16], const double* x)
     for (int r = 0; r < 16; ++r) acc[r & 3] = fma(w[r], x[r], acc[r & 3]);
     return (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
+// Blocked back-substitution L^T x = y over the component's tile rows, descending (ys: y in LDS,
+// overwritten with x): x_k = L_kk^-T y_k, then y_m -= L_km^T x_k over row k's nonzero tiles.  Lanes
+// work in 16-lane groups, lane c of a group forming column c's dot product (no cross-lane
+// reduction); the 16 groups take one tile each per step, wave 0's first group also x_k.  The
+// operands of step k - kBsDepth are loaded right after step k's use of their register stage (the
+// k loop unrolled by kBsDepth, so each stage keeps its registers): they do not depend on x, so a step
+// waits on LDS and two barriers, not on memory.  Rows of more than 16 tiles take the rest in place.
+// sbp / sbl: LDS for the back lists (nt + 1 pointers, then the tile columns).
 __device__ __forceinline__ void back_substitute(const double* L, const double* Linv, int np, int nt, const int* tl,
-                                                const int* bptr, double* ys) {
+                                                const int* bptr, double* ys, int* sbp, int* sbl) {
     const int tid = threadIdx.x, grp = tid >> 4, c = tid & 15;
+    const int b0 = bptr[0], nb = bptr[nt] - b0;
     for (int e = tid; e < np; e += kSolveThreads) ys[e] = L[(long long)np * np + e];
-    double li[16], tv[16];
-    int tm = bs_index(tl, bptr, nt - 1);
-    int tm1 = nt > 1 ? bs_index(tl, bptr, nt - 2) : -1;
-    bs_load(L, Linv, np, nt - 1, tm, li, tv);
+    for (int e = tid; e <= nt; e += kSolveThreads) sbp[e] = bptr[e] - b0;
+    for (int e = tid; e < nb; e += kSolveThreads) sbl[e] = tl[b0 + e];
     __syncthreads();
-    for (int k = nt - 1; k >= 0; --k) {
-        // operands of step k - 1 (index loaded a step ago) and the index of step k - 2
-        double nli[16], ntv[16];
-        bs_load(L, Linv, np, k > 0 ? k - 1 : 0, tm1, nli, ntv);
-        const int tm2 = k > 1 ? bs_index(tl, bptr, k - 2) : -1;
-        if (grp == 0) {  // x_k = L_kk^-T y_k (lane c: column c of L_kk^-1)
-            double yk[16];
+    double li[kBsDepth][16], tv[kBsDepth][16];
+    int tm[kBsDepth];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) yk[r] = ys[16 * k + r];
-            ys[16 * k + c] = bs_dot(li, yk);  // (the group's reads of y_k precede its writes)
+    for (int s = 0; s < kBsDepth; ++s) {
+        tm[s] = -1;
+        if (nt - 1 - s >= 0) bs_load(L, Linv, np, nt - 1 - s, sbp, sbl, li[s], tv[s], tm[s]);
+    }
+    for (int k0 = nt - 1; k0 >= 0; k0 -= kBsDepth) {
+#pragma unroll
+        for (int s = 0; s < kBsDepth; ++s) {
+            const int k = k0 - s;
+            if (k < 0) break;
+            if (grp == 0) {  // x_k = L_kk^-T y_k (lane c: column c of L_kk^-1)
+                double yk[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) yk[r] = ys[16 * k + r];
+                ys[16 * k + c] = bs_dot(li[s], yk);  // (the group's reads of y_k precede its writes)
+            }
+            __syncthreads();
+            double xk[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) xk[r] = ys[16 * k + r];
+            if (tm[s] >= 0) ys[16 * tm[s] + c] -= bs_dot(tv[s], xk);  // y_m -= L_km^T x_k
+            for (int q = sbp[k] + kBsGroups + grp; q < sbp[k + 1]; q += kBsGroups) {
+                const int mm = sbl[q];
+                const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
+                double w[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) w[r] = Lkm[(long long)r * np + c];
+                ys[16 * mm + c] -= bs_dot(w, xk);
+            }
+            if (k - kBsDepth >= 0) bs_load(L, Linv, np, k - kBsDepth, sbp, sbl, li[s], tv[s], tm[s]);
+            __syncthreads();
         }
-        __syncthreads();
-        double xk[16];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) xk[r] = ys[16 * k + r];
-        if (tm >= 0) ys[16 * tm + c] -= bs_dot(tv, xk);  // y_m -= L_km^T x_k
-        for (int q = bptr[k] + kBsGroups + grp; q < bptr[k + 1]; q += kBsGroups) {
-            const int mm = tl[q];
-            const double* Lkm = L + (long long)(16 * k) * np + 16 * mm;
-            double w[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) w[r] = Lkm[(long long)r * np + c];
-            ys[16 * mm + c] -= bs_dot(w, xk);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            li[r] = nli[r];
-            tv[r] = ntv[r];
-        }
-        tm = tm1;
-        tm1 = tm2;
     }
 }
 
@@ -739,8 +750,6 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     const double lambda = s_lambda;
     const int* hdr = a.comp_hdr + kHdrN * comp;
     const int nt = hdr[kHdrNt], np = 16 * nt;
-    const int kq0 = a.comp_kf_ptr[comp], nkc = a.comp_kf_ptr[comp + 1] - kq0;
-    const int nc = 6 * nkc;
     double* L = a.L + a.comp_loff[comp];
     double* Linv = a.Linv + a.comp_loff[comp];  // same offsets as L (>= 16 np per component)
     const int* tl = a.tl;
@@ -760,7 +769,6 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     bool ok = true;
     const int* pptr = tl + hdr[kHdrPanel];
     const int* tptr = tl + hdr[kHdrTrail];
-    const int* bptr = tl + hdr[kHdrBack];
     for (int k = 0; k < nt; ++k) {
         // trace slots: steps 0, 1 and nt / 2 (factor | panel | trailing update)
         const int kts = k == 0 ? 2 : (k == 1 ? 5 : (k == nt / 2 ? 8 : -1));
@@ -821,18 +829,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     }
     VX_KT(11);
     if (wv == 0 && lane == 0 && !ok) atomicOr(&a.st->fail[it], 1);
-    // ---- back-substitution L^T x = y (y = row np of the factored rhs tile row)
-    back_substitute(L, Linv, np, nt, tl, bptr, ys);
-    VX_KT(12);
-    for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
-    // the next assembly writes only S's blocks into L: clear every tile the factorisation touched
-    {
-        const int* cp = tl + hdr[kHdrCopy];
-        const int ncp = hdr[kHdrNCopy];
-        const d4 z = {0.0, 0.0, 0.0, 0.0};
-        for (int t = wv; t < ncp; t += kSolveWaves)
-            store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
-    }
+    // (the back-substitution, dx and the clearing of the touched tiles: k_sba_backsub)
 }
 
 // ------------------------------------------------------------------------- multi-workgroup factor
@@ -1139,7 +1136,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_pair(SBAArgs a, int i
 __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;
-    extern __shared__ __attribute__((aligned(32))) double ys[];  // np: y, then x
+    extern __shared__ __attribute__((aligned(32))) double ys[];  // np: y, then x | back lists
     const int tid = threadIdx.x, wv = tid >> 6;
     const int comp = blockIdx.x;
     const int* hdr = a.comp_hdr + kHdrN * comp;
@@ -1150,7 +1147,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it
     const int* tl = a.tl;
     const int* bptr = tl + hdr[kHdrBack];
     VX_KT(8);
-    back_substitute(L, Linv, np, nt, tl, bptr, ys);
+    int* sbp = reinterpret_cast<int*>(ys + a.bs_np);
+    back_substitute(L, Linv, np, nt, tl, bptr, ys, sbp, sbp + a.bs_nt + 1);
     VX_KT(9);
     for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
     const int* cp = tl + hdr[kHdrCopy];
@@ -1298,6 +1296,8 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.fac_nk = std::max(p->max_nt - 1, 1);
     a.fac_pairs = p->fac_pairs.as<int>();
     a.fac_np = std::max(p->max_pairs, 1);
+    a.bs_np = p->max_np;
+    a.bs_nt = std::max(p->max_nt, 1);
     return a;
 }
 
@@ -1668,6 +1668,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     p->max_panel = 1;
     p->max_nt = p->max_trail_rest = 0;
     p->max_pairs = 0;
+    p->max_back = 0;
     std::vector<std::vector<int>> pair_desc(std::max(p->n_comp, 1));
     {
         std::vector<std::vector<std::pair<int, int>>> cblk(p->n_comp);
@@ -1750,6 +1751,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                     if (NZ(k, m2)) tlist.push_back(m2);
             }
             tlist[bp + nt] = (int)tlist.size();
+            p->max_back = std::max(p->max_back, tlist[bp + nt] - tlist[bp]);
             // the two-column schedule's lists (k_sba_fac_pair): launch t applies steps s0 = 2t and
             // s0 + 1 (entries i << 16 | c << 2 | mask) — phase 1: columns c0 = 2t + 2, c0 + 1; phase 2:
             // step c0 on column c0 + 1 (one-step entries); rest: the columns beyond
@@ -1921,6 +1923,10 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
     const int upd_blocks = (std::max(p->n_opt, p->nk) + kUpdThreads - 1) / kUpdThreads;
     // the factorisation: one launch per tile step over G workgroups per component (components of
     // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
+    const size_t bs_lds = (size_t)p->max_np * sizeof(double) + ((size_t)a.bs_nt + 1 + p->max_back) * sizeof(int);
+    if (bs_lds > 64 * 1024)
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs_lds));
     const bool multi = factor_multi(p->max_nt);
     const int G = factor_groups(p->max_trail_rest);
     // one tile column per launch (default) or two ($VX_SBA_FACTOR_COLS=2: half the launches, but
@@ -1978,12 +1984,12 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
                 VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_step, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads),
                                  (uint32_t)la_lds, c->stream, a, it, k, G, la_ps, sd));
             }
-            VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
-                             (uint32_t)(p->max_np * sizeof(double)), c->stream, a, it));
         } else {
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
                              (uint32_t)lds, c->stream, a, it));
         }
+        VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+                         (uint32_t)bs_lds, c->stream, a, it));
         VX_HIP(c, launch(c, kStSbaUpdate, k_sba_update, dim3(std::max(upd_blocks, 1)), dim3(kUpdThreads), 0,
                          c->stream, a, it));
     }

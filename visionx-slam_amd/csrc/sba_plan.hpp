@@ -43,6 +43,7 @@ struct vx_sba_plan {
     std::vector<int> fac_pairs_h;
     vx::DevBuf fac_pairs;
     int max_pairs = 0;
+    int max_back = 0;  // most back-substitution tiles of one component (k_sba_backsub stages the lists in LDS)
 };
 
 
