@@ -931,10 +931,8 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_begin(SBAArgs a, int 
 // panel overwrites the off-diagonal ones and only L_kk^-1 of a diagonal tile is read later.  Same
 // operations, same order as factor_column over global memory.  sm: diagonal tile | L_kk^-1 | POTRF
 // columns (2 tiles) | ps panel images | tile row -> slot (nt + 1) | updated flags (ps).
-constexpr int kPanPre = 6;  // panel tiles per wave whose global operands are loaded at the start
-__device__ __forceinline__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt,
-                                                 const int* tl, int p0, int p1, int k, int la_beg, int la_end,
-                                                 double* sm, int ps, bool kt) {
+__device__ __forceinline__ void lookahead_column(const SBAArgs& a, int it, double* L, double* Linv, int np, int nt, const int* tl,
+                                 int p0, int p1, int k, int la_beg, int la_end, double* sm, int ps, bool kt) {
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63, r0 = lane >> 4, cl = lane & 15;
     double* dtile = sm;
     double* dlds = sm + kPanelStride;
@@ -944,31 +942,6 @@ __device__ __forceinline__ void lookahead_column(const SBAArgs& a, int it, doubl
     int* upd = slot_of + nt + 1;
     const int c1 = k + 1, pn = p1 - p0;
     const bool in_lds = pn <= ps;
-    const bool diag = la_end > la_beg;
-    const int cnt = la_end - la_beg;
-    // ---- every global operand this launch reads, issued up front (none depends on its results):
-    // the first round of look-ahead tiles (C = A_i,k+1, the operand L_ik, the common L_k+1,k) and the
-    // panel tiles' own values (used where step k did not touch the tile)
-    d4 c[4];
-    double4 av[4];
-    int ti[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int m = wv * 4 + q;
-        ti[q] = m < cnt ? tl[la_beg + m] >> 16 : -1;
-        if (ti[q] >= 0) {
-            c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * c1, np);
-            av[q] = *reinterpret_cast<const double4*>(L + (long long)(16 * ti[q]) * np + 16 * k + (long long)cl * np + 4 * r0);
-        }
-    }
-    const double4 bv = *reinterpret_cast<const double4*>(L + (long long)(16 * c1) * np + 16 * k + (long long)cl * np + 4 * r0);
-    double4 pg[kPanPre];
-#pragma unroll
-    for (int j = 0; j < kPanPre; ++j) {
-        const int q = wv + kSolveWaves * j;
-        if (q < pn)
-            pg[j] = *reinterpret_cast<const double4*>(L + (long long)(16 * tl[p0 + q]) * np + 16 * c1 + (long long)cl * np + 4 * r0);
-    }
     for (int q = tid; q < pn; q += kSolveThreads) {
         slot_of[tl[p0 + q]] = q;
         if (in_lds) upd[q] = 0;
@@ -976,34 +949,32 @@ __device__ __forceinline__ void lookahead_column(const SBAArgs& a, int it, doubl
     __syncthreads();
     if (kt) VX_KT(2);
     // step k's update of column k + 1 (the diagonal tile is the first entry when the column has one)
-    auto finish = [&](int i, d4 v) {
-        if (i == c1) {
-            store_acc(dtile, 16, v);
-        } else if (in_lds) {
-            const int sl = slot_of[i];
-            store_acc_opo(pan + (size_t)sl * kPanelStride, v);
-            if (lane == 0) upd[sl] = 1;
-        } else {
-            store_acc(L + (long long)(16 * i) * np + 16 * c1, np, v);
-        }
-    };
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if (ti[q] < 0) continue;
-        c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[q].x, bv.x, c[q], 0, 0, 0);
-        c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[q].y, bv.y, c[q], 0, 0, 0);
-        c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[q].z, bv.z, c[q], 0, 0, 0);
-        c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-av[q].w, bv.w, c[q], 0, 0, 0);
-        finish(ti[q], c[q]);
-    }
-    for (int m0 = kSolveWaves * 4 + wv * 4; m0 < cnt; m0 += kSolveWaves * 4) {  // (more than 16: rare)
+    const bool diag = la_end > la_beg;
+    const int cnt = la_end - la_beg;
+    for (int m0 = wv * 4; m0 < cnt; m0 += kSolveWaves * 4) {
+        d4 c[4];
+        int ti[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            if (m0 + q >= cnt) continue;
-            const int i = tl[la_beg + m0 + q] >> 16;
-            d4 v = load_acc(L + (long long)(16 * i) * np + 16 * c1, np);
-            v = mfma_abt_g(L + (long long)(16 * i) * np + 16 * k, L + (long long)(16 * c1) * np + 16 * k, np, v);
-            finish(i, v);
+            ti[q] = -1;
+            if (m0 + q < cnt) {
+                ti[q] = tl[la_beg + m0 + q] >> 16;
+                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * c1, np);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (ti[q] < 0) continue;
+            c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * k, L + (long long)(16 * c1) * np + 16 * k, np, c[q]);
+            if (ti[q] == c1) {
+                store_acc(dtile, 16, c[q]);
+            } else if (in_lds) {
+                const int sl = slot_of[ti[q]];
+                store_acc_opo(pan + (size_t)sl * kPanelStride, c[q]);
+                if (lane == 0) upd[sl] = 1;
+            } else {
+                store_acc(L + (long long)(16 * ti[q]) * np + 16 * c1, np, c[q]);
+            }
         }
     }
     if (kt) VX_KT(3);
@@ -1016,26 +987,18 @@ __device__ __forceinline__ void lookahead_column(const SBAArgs& a, int it, doubl
     }
     __syncthreads();
     if (kt) VX_KT(5);
-    // the panel L_i,k+1 = A_i,k+1 L_k+1,k+1^-T: updated tiles from LDS, the others as loaded above
-    const double4 dv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
-    auto panel_tile = [&](int q, double4 g) {
+    // the panel L_i,k+1 = A_i,k+1 L_k+1,k+1^-T: updated tiles from LDS, the others from global
+    for (int q = wv; q < pn; q += kSolveWaves) {
         double* Aik = L + (long long)(16 * tl[p0 + q]) * np + 16 * c1;
-        const double4 x = (in_lds && upd[q]) ? *reinterpret_cast<const double4*>(pan + (size_t)q * kPanelStride + 4 * lane) : g;
-        d4 v = {0.0, 0.0, 0.0, 0.0};
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(x.x, dv.x, v, 0, 0, 0);
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(x.y, dv.y, v, 0, 0, 0);
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(x.z, dv.z, v, 0, 0, 0);
-        v = __builtin_amdgcn_mfma_f64_16x16x4f64(x.w, dv.w, v, 0, 0, 0);
-        store_acc(Aik, np, v);
-    };
-#pragma unroll
-    for (int j = 0; j < kPanPre; ++j) {
-        const int q = wv + kSolveWaves * j;
-        if (q < pn) panel_tile(q, pg[j]);
-    }
-    for (int q = wv + kSolveWaves * kPanPre; q < pn; q += kSolveWaves) {
-        const double* Aik = L + (long long)(16 * tl[p0 + q]) * np + 16 * c1;
-        panel_tile(q, *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0));
+        const double4 av = (in_lds && upd[q]) ? *reinterpret_cast<const double4*>(pan + (size_t)q * kPanelStride + 4 * lane)
+                                              : *reinterpret_cast<const double4*>(Aik + (long long)cl * np + 4 * r0);
+        const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
+        d4 c = {0.0, 0.0, 0.0, 0.0};
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.z, bv.z, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, c, 0, 0, 0);
+        store_acc(Aik, np, c);
     }
     if (kt) VX_KT(6);
 }
