@@ -757,10 +757,10 @@ def main():
     # lcm(frames, 3E, 4E) frames) and replayed from C — one binding call per step instead of ~8 per
     # frame.  --no-seq keeps the per-frame calls.
     host_path = "per-frame ctypes calls"
+    seqs = []
     if not skip and not args.diag_nodep and not args.no_seq:
         period = int(np.lcm.reduce([args.frames, 3 * E, 4 * E]))
         n_seq = int(np.lcm(period, F)) // F
-        seqs = []
         for k in range(n_seq):
             sq = vxslam.Seq()
             for f in range(F):
@@ -967,6 +967,8 @@ def main():
             "stages_us": {k: round(v[0] * 1e3, 2) for k, v in stages.items()},
         }
         print(json.dumps(out), flush=True)
+    for sq in seqs:  # (before the contexts their calls name)
+        sq.close()
     plan.close()
     for e in ev_e + ev_m:
         e.close()

@@ -17,6 +17,9 @@
 // contexts may be issued concurrently — which is what the sequential replay's streams see anyway.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -59,7 +62,20 @@ struct vx_seq {
     bool stop = false;
     uint64_t gen = 0;
 
-    ~vx_seq() { shutdown(); }
+    // $VX_SEQ_TIMING=1: host time per op kind over the single-thread replays, printed at destroy
+    bool timing = false;
+    double t_kind[5] = {0, 0, 0, 0, 0};
+    long long n_kind[5] = {0, 0, 0, 0, 0};
+    ~vx_seq() {
+        shutdown();
+        if (timing) {
+            static const char* names[5] = {"wait", "record", "extract", "match", "ba_run"};
+            for (int k = 0; k < 5; ++k)
+                if (n_kind[k])
+                    std::fprintf(stderr, "[vx_seq] %-8s %9lld calls %8.2f us/call\n", names[k], n_kind[k],
+                                 t_kind[k] / (double)n_kind[k]);
+        }
+    }
     void shutdown() {
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -201,6 +217,8 @@ extern "C" {
 int vx_seq_create(vx_seq** out) {
     if (!out) return VX_ERR_INVALID;
     *out = new vx_seq();
+    const char* e = std::getenv("VX_SEQ_TIMING");
+    (*out)->timing = e && e[0] == '1';
     return VX_OK;
 }
 
@@ -274,6 +292,17 @@ int vx_seq_run(vx_seq* s, int* failed_op) {
     if (!s) return VX_ERR_INVALID;
     if (s->threads > 1) return run_parallel(s, failed_op);
     for (size_t i = 0; i < s->ops.size(); ++i) {
+        if (s->timing) {
+            const auto t0 = std::chrono::steady_clock::now();
+            const int rc = run_op(s->ops[i]);
+            s->t_kind[s->ops[i].kind] += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+            ++s->n_kind[s->ops[i].kind];
+            if (rc != VX_OK) {
+                if (failed_op) *failed_op = (int)i;
+                return rc;
+            }
+            continue;
+        }
         const int rc = run_op(s->ops[i]);
         if (rc != VX_OK) {
             if (failed_op) *failed_op = (int)i;
