@@ -20,6 +20,20 @@ __global__ void k_noop(int* p) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && p[0] == 12345) p[1] = 1;
 }
 
+struct Big {
+    double* p[40];
+    int v[32];
+};  // ~450 bytes of kernel arguments, like k_ba_iter's BAArgs + FusedArgs
+__global__ void k_big(Big b, int it) {
+    if (threadIdx.x == 0 && blockIdx.x == 0 && b.v[it & 31] == 12345) b.p[0][0] = 1.0;
+}
+extern __shared__ double dyn_lds[];
+__global__ void k_lds(int* p) {
+    dyn_lds[threadIdx.x] = 1.0;
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x == 0 && p[0] == 12345) p[1] = (int)dyn_lds[5];
+}
+
 using clk = std::chrono::steady_clock;
 static double us_since(clk::time_point t0) { return std::chrono::duration<double, std::micro>(clk::now() - t0).count(); }
 
@@ -64,6 +78,37 @@ int main() {
                     tot / (kRounds * kBatch / 4) / n);
         CK(hipGraphExecDestroy(x));
         CK(hipGraphDestroy(g));
+    }
+    // graphs of 6 nodes with large kernel arguments / 96 KB of dynamic LDS
+    {
+        Big b{};
+        b.p[0] = reinterpret_cast<double*>(d);
+        CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lds), hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024));
+        for (int variant = 0; variant < 2; ++variant) {
+            hipGraph_t g;
+            hipGraphExec_t x;
+            CK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+            for (int i = 0; i < 6; ++i) {
+                if (variant == 0) hipLaunchKernelGGL(k_big, dim3(129), dim3(512), 0, s, b, i);
+                else hipLaunchKernelGGL(k_lds, dim3(129), dim3(512), 96 * 1024, s, d);
+            }
+            CK(hipStreamEndCapture(s, &g));
+            CK(hipGraphInstantiate(&x, g, nullptr, nullptr, 0));
+            double tot = 0;
+            for (int w = 0; w < 2; ++w) {
+                tot = 0;
+                for (int r = 0; r < kRounds; ++r) {
+                    auto t0 = clk::now();
+                    for (int i = 0; i < kBatch / 4; ++i) CK(hipGraphLaunch(x, s));
+                    tot += us_since(t0);
+                    CK(hipStreamSynchronize(s));
+                }
+            }
+            std::printf("graph of 6 nodes, %s %7.2f us/launch\n", variant == 0 ? "450 B args     " : "96 KB dyn LDS  ",
+                        tot / (kRounds * kBatch / 4));
+            CK(hipGraphExecDestroy(x));
+            CK(hipGraphDestroy(g));
+        }
     }
     // events
     hipEvent_t ev;
