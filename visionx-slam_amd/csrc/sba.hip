@@ -117,7 +117,6 @@ struct SBAArgs {
     const int* kf_ptr;      // nk + 1 into kf_obs
     const int* kf_obs;
     const int2* blk_ij;
-    const int* blk_order;   // k_sba_blocks: workgroup slot -> block (see there)
     const int* blk_ptr;
     const int2* pairs;
     const int* comp_kf_ptr; // component -> keyframe list (comp_kf)
@@ -327,15 +326,8 @@ __device__ __forceinline__ void load18(const double* src, double* v) {
 __global__ __launch_bounds__(kBlkThreads) void k_sba_blocks(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     __shared__ double red[kBlkThreads / 64][64];
-    // Workgroups are dispatched to the eight XCDs round robin (workgroup g on XCD g mod 8); slot
-    // g mod 8 * (its share) + g / 8 makes each XCD take one contiguous run of blk_order, which lists
-    // the blocks row by row (keyframe i's diagonal block, then its (i, j < i) blocks).  The blocks of
-    // a row all read the Y rows of keyframe i's observations (and neighbouring rows share W rows):
-    // grouped on one XCD they meet in its L2 instead of each fetching them again.
-    const int nbk = gridDim.x, per = nbk >> 3, rem = nbk & 7, x = blockIdx.x & 7, kx = blockIdx.x >> 3;
-    const int b = a.blk_order[(x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + kx];
-    const int tid = threadIdx.x;
-    if (blockIdx.x == 0 && tid == 0) a.st->fail[it] = 0;
+    const int tid = threadIdx.x, b = blockIdx.x;
+    if (b == 0 && tid == 0) a.st->fail[it] = 0;
     const int2 ij = a.blk_ij[b];
     const int i = ij.x, j = ij.y;
     const bool diag = i == j;
@@ -1281,7 +1273,6 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.kf_ptr = p->kf_ptr.as<int>();
     a.kf_obs = p->kf_obs.as<int>();
     a.blk_ij = p->blk_ij.as<int2>();
-    a.blk_order = p->blk_order.as<int>();
     a.blk_ptr = p->blk_ptr.as<int>();
     a.pairs = p->pairs.as<int2>();
     a.comp_kf_ptr = p->comp_kf_ptr.as<int>();
@@ -1837,23 +1828,8 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         for (int cc = 0; cc < p->n_comp; ++cc)
             std::copy(pair_desc[cc].begin(), pair_desc[cc].end(), p->fac_pairs_h.begin() + (size_t)16 * fp * cc);
     }
-    // k_sba_blocks' order: row by row (diagonal block i, then the (i, j < i) blocks in block order)
-    std::vector<int> border;
-    {
-        std::vector<int> rcnt(nk + 1, 0);
-        for (size_t b = (size_t)nk; b < bij.size(); ++b) ++rcnt[bij[b].x + 1];
-        for (int r = 0; r < nk; ++r) rcnt[r + 1] += rcnt[r] + 1;  // (+1: the row's diagonal block)
-        border.assign(bij.size(), 0);
-        std::vector<int> at(nk);
-        for (int r = 0; r < nk; ++r) {
-            at[r] = rcnt[r];
-            border[at[r]++] = r;
-        }
-        for (size_t b = (size_t)nk; b < bij.size(); ++b) border[at[bij[b].x]++] = (int)b;
-    }
     VX_HIP(c, hipSetDevice(c->device));
     int rc;
-    if ((rc = upload(c, p->blk_order, border))) return rc;
     if ((rc = upload(c, p->fac_steps, p->fac_steps_h))) return rc;
     if ((rc = upload(c, p->fac_pairs, p->fac_pairs_h))) return rc;
     if ((rc = upload(c, p->kf_flags, flags))) return rc;

@@ -35,7 +35,6 @@ struct vx_sba_plan {
     vx::DevBuf lm_map_dev, kf_map_dev;  // dmap plans: slot -> resident landmark row, window row -> keyframe row
     // the multi-workgroup factor's launch k per component: 8 ints {L offset lo, hi, look-ahead tiles
     // [la_beg, split), rest [split, t_end), panel of column k + 1 [p0, p1), nt} (nt = 0: no step k)
-    vx::DevBuf blk_order;  // k_sba_blocks: blocks row by row (diagonal first), XCD by XCD
     std::vector<int> fac_steps_h;
     vx::DevBuf fac_steps;
     // the two-column schedule (launch t factors columns 2t + 2 and 2t + 3): 16 ints per component and
