@@ -449,6 +449,13 @@ int vx_sba_plan_system(vx_ctx* ctx, vx_sba_plan* plan, double* S, double* rhs, i
  * into the map's rows with vx_sba_plan_apply_dmap (stream ordered, no host synchronisation). */
 int vx_sba_plan_create_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_ref, const vx_sba_options* opt,
                             vx_sba_plan** out);
+/* Rebuild a plan made by vx_sba_plan_create_dmap in place for the map's current state and ref_kf_id,
+ * with the plan's options: its device buffers and host staging are reused (grown when the window
+ * needs more), so a drop-in that keeps one plan per backend pays no allocation or release per
+ * Backend::Optimize() (the reference builds its problem per call, core/backend/local_ba.cpp:42-108).
+ * The plan's captured run graph is dropped (the next run is eager).  On error the plan is left
+ * unusable (status set, no run) until a successful rebuild. */
+int vx_sba_plan_rebuild_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_ref, vx_sba_plan* plan);
 int vx_sba_plan_apply_dmap(vx_ctx* ctx, vx_sba_plan* plan, vx_dmap* map);
 int vx_sba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                         const vx_sba_options* opt, vx_sba_stats* stats);

@@ -1,6 +1,8 @@
 """Schur-complement BA plan build: host build from the snapshot (vx_sba_plan_create) against the
-device build from the resident map (vx_sba_plan_create_dmap), and one run of the plan; median ms of
-5 after one warm-up (the device buffers exist), at C3 and the connected C5 rig.
+device build from the resident map (vx_sba_plan_create_dmap; create + close per build, so each
+build allocates and releases the plan's buffers), the same plan rebuilt in place
+(vx_sba_plan_rebuild_dmap: buffers reused, the drop-in's per-Optimize cost), and one run of the
+plan; median ms of 5 after one warm-up, at C3 and the connected C5 rig.
 
     python scripts/sba_plan_time.py [out.json]"""
 import json
@@ -44,11 +46,15 @@ for name, (nk, nl, ns, cf) in {"C3": (50, 20000, 1, 0.0), "C5-connected": (200, 
     p = dm.sba_plan(opts)
     info = p.info()
 
+    def rebuild():
+        dm.sba_plan_rebuild(p)
+
     def run():
         p.run_async()
         p.fetch()
 
-    r = {"plan_host_ms": med(host), "plan_device_ms": med(dev), "run_ms": med(run), "info": info}
+    r = {"plan_host_ms": med(host), "plan_device_ms": med(dev), "plan_device_rebuild_ms": med(rebuild),
+         "run_ms": med(run), "info": info}
     p.run_async()
     st = p.fetch()
     r["iterations"], r["accepted"] = int(st.iterations), int(st.accepted)

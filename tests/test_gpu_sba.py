@@ -193,6 +193,20 @@ def test_sba_plan_from_resident_map(ctx, oracle, cfg):
     pd.apply(dm)
     pose, pos = dm.download()
     assert np.array_equal(pose, m2["kf_pose"].reshape(-1, 7)) and np.array_equal(pos, m2["lm_pos"].reshape(-1, 3))
+    # vx_sba_plan_rebuild_dmap: the same plan object rebuilt in place for the map's new state, and
+    # again for an earlier reference keyframe (a shifted window), runs bitwise as a fresh plan does
+    ids = sorted(int(x) for x in np.asarray(m["kf_id"]).ravel())
+    for ref in (m["ref_kf_id"], ids[len(ids) * 3 // 4]):
+        dm.sba_plan_rebuild(pd, ref_kf_id=ref)
+        fresh = dm.sba_plan(opts, ref_kf_id=ref)
+        assert pd.info() == fresh.info()
+        pd.run_async()
+        fresh.run_async()
+        a, b = pd.fetch(), fresh.fetch()
+        for f in ("status", "iterations", "accepted", "n_window_kf", "n_landmarks", "initial_cost", "final_cost"):
+            assert getattr(a, f) == getattr(b, f), (ref, f)
+        assert list(a.cost) == list(b.cost) and list(a.step) == list(b.step)
+        fresh.close()
     pd.close(), ps.close(), dm.close()
     # the snapshot plan against the restatement (the dmap plan equals it bitwise)
     m3 = vxslam.map_reorder(m, kf_order, lm_order)

@@ -28,6 +28,8 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include "vx_sort.hpp"
+
 #include "ba_plan.hpp"
 
 namespace vx {
@@ -578,11 +580,11 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     unsigned bits = 1;
     while ((1 << bits) <= nk) ++bits;
     size_t tb = 0;
-    VX_HIP(c, rocprim::radix_sort_pairs(nullptr, tb, key, keys2, iota, order, no, 0, bits, s));
+    VX_HIP(c, rocprim::radix_sort_pairs<OnesweepSort>(nullptr, tb, key, keys2, iota, order, no, 0, bits, s));
     size_t tb2 = 0;
     VX_HIP(c, rocprim::exclusive_scan(nullptr, tb2, cntS, cntScan, 0, no + 1, rocprim::plus<int>(), s));
     VX_HIP(c, S.fb_tmp.ensure(std::max<size_t>(std::max(tb, tb2), 16)));
-    VX_HIP(c, rocprim::radix_sort_pairs(S.fb_tmp.p, tb, key, keys2, iota, order, no, 0, bits, s));
+    VX_HIP(c, rocprim::radix_sort_pairs<OnesweepSort>(S.fb_tmp.p, tb, key, keys2, iota, order, no, 0, bits, s));
     hipLaunchKernelGGL(k_fb_sorted, dim3(grid(n_opt)), dim3(kT), 0, s, (const int*)order, (const int*)keys2, n_opt,
                        lptr, (const u64*)mask, W, ft, cntS, maskS, counters);
     VX_LAUNCH_CHECK(c, "fused build: sorted order");

@@ -47,6 +47,8 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include "vx_sort.hpp"
+
 #include "vx_internal.hpp"
 #include "ba_common.hpp"
 #include "ba_plan.hpp"
@@ -593,11 +595,10 @@ struct SbaArgs {
     int* v2;
     int* pc;                  // per optimised slot: pairs (scan input)
     const int* pptr;
-    int* kcnt;                // per (i, j) key: pairs
+    int* kcnt;                // per (i, j) key, i > j: 1 if a landmark joins keyframes i and j
     int* oflag;
     const int* orank;
     int* bidx;
-    int* bcnt;
     int2* bij;
     int* ekey;
     unsigned long long* eval;
@@ -652,8 +653,11 @@ __device__ __forceinline__ int sb_pairs(const SbaArgs& a, int s) {
             if (kEmit) {
                 a.ekey[base + c] = a.bidx[key];
                 a.eval[base + c] = (unsigned long long)(unsigned)a1 | ((unsigned long long)(unsigned)a2 << 32);
-            } else {
-                atomicAdd(&a.kcnt[key], 1);
+            } else if (j != i && !a.kcnt[key]) {
+                // an off-diagonal block exists: a flag, not a count (a count per pair was one global
+                // atomic per pair, ~1700 of them on each diagonal key; the pairs per block come from
+                // the sorted pair list instead, k_sb_bptr)
+                a.kcnt[key] = 1;
             }
             ++c;
         }
@@ -699,8 +703,17 @@ __global__ __launch_bounds__(kT) void k_sb_btab(SbaArgs a) {
     else if (a.kcnt[key] > 0) b = a.nk + a.orank[key];
     a.bidx[key] = b;
     if (b < 0) return;
-    a.bcnt[b] = a.kcnt[key];
     a.bij[b] = make_int2(i, j);
+}
+
+// block b's pairs [blk_ptr[b], blk_ptr[b + 1]) from the pairs sorted by block (empty blocks: the
+// diagonal blocks of fixed or unobserved keyframes): position p starts every block in (key[p - 1], key[p]]
+__global__ __launch_bounds__(kT) void k_sb_bptr(const int* __restrict__ key, int n_pairs, int n_blocks,
+                                                int* __restrict__ blk_ptr) {
+    const int p = blockIdx.x * kT + threadIdx.x;
+    if (p > n_pairs) return;
+    const int k0 = p > 0 ? key[p - 1] : -1, k1 = p < n_pairs ? key[p] : n_blocks;
+    for (int b = k0 + 1; b <= k1; ++b) blk_ptr[b] = p;
 }
 
 __global__ __launch_bounds__(kT) void k_sb_pemit(SbaArgs a) {
@@ -731,9 +744,9 @@ unsigned bits_for(int64_t v) {  // radix bits holding [0, v]
 template <class K, class V>
 int sort_pairs(vx_ctx* c, DevBuf& tmp, K* ki, K* ko, V* vi, V* vo, size_t n, unsigned bits) {
     size_t bytes = 0;
-    VX_HIP(c, rocprim::radix_sort_pairs(nullptr, bytes, ki, ko, vi, vo, n, 0, bits, c->stream));
+    VX_HIP(c, rocprim::radix_sort_pairs<OnesweepSort>(nullptr, bytes, ki, ko, vi, vo, n, 0, bits, c->stream));
     VX_HIP(c, grow(tmp, std::max<size_t>(bytes, 16)));
-    VX_HIP(c, rocprim::radix_sort_pairs(tmp.p, bytes, ki, ko, vi, vo, n, 0, bits, c->stream));
+    VX_HIP(c, rocprim::radix_sort_pairs<OnesweepSort>(tmp.p, bytes, ki, ko, vi, vo, n, 0, bits, c->stream));
     return VX_OK;
 }
 
@@ -840,6 +853,7 @@ int lean_optimize(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_
 
 // The Schur plan's tables from the resident map (see above); p->opt set by the caller
 int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba_plan* p) {
+    const PlanClock clk;
     const vx_sba_options& o = p->opt;
     p->status = 1;
     p->from_dmap = true;
@@ -855,6 +869,7 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
         return set_error(c, VX_ERR_INVALID, "vx_sba_plan_create_dmap: window of %d keyframes (max 448)", nk);
     int rc;
     if ((rc = lean_build_core(c, m, o.min_point_observations, 1, false, 0, true, K))) return rc;
+    clk.mark("sba core enqueued");
     auto& L = m->lean;
     auto& B = m->sba;
     const int nf = K.nf;
@@ -870,7 +885,6 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     for (DevBuf* d : {&B.pkey, &B.pval, &B.skey, &B.perm, &B.k2, &B.v2}) VX_HIP(c, grow(*d, fN * 4));
     for (DevBuf* d : {&B.scnt, &B.pc, &B.pptr}) VX_HIP(c, grow(*d, lN * 4));
     for (DevBuf* d : {&B.kcnt, &B.oflag, &B.orank, &B.bidx}) VX_HIP(c, grow(*d, ((size_t)n2 + 1) * 4));
-    VX_HIP(c, grow(B.bcnt, ((size_t)n2 + nk + 1) * 4));
     VX_HIP(c, p->blk_ij.ensure(((size_t)n2 + nk + 1) * 8));
     VX_HIP(c, p->blk_ptr.ensure(((size_t)n2 + nk + 1) * 4));
     VX_HIP(c, p->obs_uv.ensure(fN * 16));
@@ -880,7 +894,6 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     VX_HIP(c, p->lm_ptr.ensure(lN * 4));
     VX_HIP(c, hipMemsetAsync(B.scnt.p, 0, lN * 4, sm));
     VX_HIP(c, hipMemsetAsync(B.kcnt.p, 0, ((size_t)n2 + 1) * 4, sm));
-    VX_HIP(c, hipMemsetAsync(B.bcnt.p, 0, ((size_t)n2 + nk + 1) * 4, sm));
     SbaArgs a{};
     a.nk = nk;
     a.nf = nf;
@@ -910,7 +923,6 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     a.oflag = B.oflag.as<int>();
     a.orank = B.orank.as<int>();
     a.bidx = B.bidx.as<int>();
-    a.bcnt = B.bcnt.as<int>();
     a.bij = p->blk_ij.as<int2>();
     // observations: stable sort by (optimised slot | n_opt), landmark pointers
     hipLaunchKernelGGL(k_sb_keys, dim3(grid(nf)), dim3(kT), 0, sm, a);
@@ -933,12 +945,12 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     if ((rc = scan_ex<int>(c, L.tmp, a.oflag, B.orank.as<int>(), n2))) return rc;
     hipLaunchKernelGGL(k_sb_btab, dim3(grid(n2)), dim3(kT), 0, sm, a);
     VX_LAUNCH_CHECK(c, "k_sb_btab");
-    if ((rc = scan_ex<int>(c, L.tmp, a.bcnt, p->blk_ptr.as<int>(), (int64_t)n2 + nk))) return rc;
     // ---- read-back 1: the counts
     VX_HIP(c, B.rb.ensure(kDynInts * 4 + ((size_t)n2 + nk + 1) * 8));
     int* H = static_cast<int*>(B.rb.p);
     VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
     VX_HIP(c, hipStreamSynchronize(sm));
+    clk.mark("sba read-back 1 (counts)");
     p->n_landmarks_global = H[kDynGlobal];
     if (H[kDynStatus]) return VX_OK;  // no optimisable landmark (local_ba.cpp:106-108)
     const int n_opt = H[kDynNOpt], n_lm = H[kDynNLm], n_obs = H[kDynPoseObs], n_oo = H[kDynSbaOo];
@@ -968,6 +980,9 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     if (n_pairs && (rc = sort_pairs(c, B.tmp, a.ekey, B.ekey2.as<int>(), a.eval, p->pairs.as<unsigned long long>(),
                                     (size_t)n_pairs, bits_for(n_blocks))))
         return rc;
+    hipLaunchKernelGGL(k_sb_bptr, dim3(grid(n_pairs + 1)), dim3(kT), 0, sm, (const int*)B.ekey2.as<int>(),
+                       (int)n_pairs, n_blocks, p->blk_ptr.as<int>());
+    VX_LAUNCH_CHECK(c, "k_sb_bptr");
     // k_sba_lm workgroups
     a.q = kSbaLmThreads - max_obs;
     VX_HIP(c, p->lm_blk.ensure(((size_t)(n_oo + n_opt) / std::max(a.q, 1) + 3) * 4));
@@ -1002,7 +1017,9 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
         lptr_h.resize((size_t)n_opt + 1);
         VX_HIP(c, hipMemcpyAsync(lptr_h.data(), p->lm_ptr.p, lptr_h.size() * 4, hipMemcpyDeviceToHost, sm));
     }
+    clk.mark("sba pairs enqueued");
     VX_HIP(c, hipStreamSynchronize(sm));
+    clk.mark("sba read-back 2 (blocks)");
     if (!lptr_h.empty()) {  // greedy packing on the host, as build_sba_plan does
         std::vector<int> blk{0};
         int n_o = 0, n_l = 0;
@@ -1023,7 +1040,7 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
         p->n_lm_blocks = n_opt ? H[kDynSbaLmBlocks] : 0;
     }
     const std::vector<int2> bij(HB, HB + n_blocks);
-    return sba_plan_finish(c, p, flags, bij);
+    return sba_plan_finish(c, p, flags, bij, &clk);
 }
 }  // namespace vx
 

@@ -293,17 +293,6 @@ __global__ __launch_bounds__(kT) void k_lm_gather(const int* inv, int n, const d
 
 inline unsigned grid(long long n) { return (unsigned)std::max(1ll, (n + kT - 1) / kT); }
 
-// $VX_PLAN_TIMING: host timestamps of the plan build's stages on stderr (ms since the build began)
-struct PlanClock {
-    bool on = getenv("VX_PLAN_TIMING") != nullptr;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-    void mark(const char* what) const {
-        if (on)
-            fprintf(stderr, "[vx plan] %-28s %.3f ms\n", what,
-                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-    }
-};
-
 template <class T>
 int up(vx_ctx* c, DevBuf& d, const T* h, size_t n) {
     VX_HIP(c, d.ensure(std::max<size_t>(1, n) * sizeof(T)));

@@ -14,6 +14,8 @@
 
 #include <rocprim/rocprim.hpp>
 
+#include "vx_sort.hpp"
+
 #include "dmap.hpp"
 
 namespace vx {
@@ -212,10 +214,10 @@ int dmap_build_csr(vx_ctx* c, vx_dmap* m) {
         unsigned bits = 1;
         while ((1ll << bits) <= nl) ++bits;
         size_t bytes = 0;
-        VX_HIP(c, rocprim::radix_sort_pairs(nullptr, bytes, m->obs_lm.as<int>(), m->sort_keys2.as<int>(),
+        VX_HIP(c, rocprim::radix_sort_pairs<OnesweepSort>(nullptr, bytes, m->obs_lm.as<int>(), m->sort_keys2.as<int>(),
                                             m->sort_vals.as<int>(), m->sort_vals2.as<int>(), (size_t)n, 0, bits, s));
         VX_HIP(c, m->tmp.ensure(std::max<size_t>(bytes, 16)));
-        VX_HIP(c, rocprim::radix_sort_pairs(m->tmp.p, bytes, m->obs_lm.as<int>(), m->sort_keys2.as<int>(),
+        VX_HIP(c, rocprim::radix_sort_pairs<OnesweepSort>(m->tmp.p, bytes, m->obs_lm.as<int>(), m->sort_keys2.as<int>(),
                                             m->sort_vals.as<int>(), m->sort_vals2.as<int>(), (size_t)n, 0, bits, s));
     }
     size_t bytes = 0;

@@ -1608,8 +1608,12 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
 
 }  // namespace
 
-int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, const std::vector<int2>& bij) {
+int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, const std::vector<int2>& bij,
+                    const PlanClock* clk) {
     const int nk = p->nk, n_opt = p->n_opt;
+    auto mark = [clk](const char* w) {
+        if (clk) clk->mark(w);
+    };
 
     // ---- connected components of the free keyframes' covisibility graph
     // (over the off-diagonal blocks: two free keyframes share a block exactly when a landmark's
@@ -1656,8 +1660,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     p->s_total = soff;
     p->l_total = lo;
     p->comp_loff_h = loff;
-
-    
+    mark("sba components");
 
     // ---- symbolic tile factorisation per component: which 16 x 16 tiles of L are nonzero (the
     // pattern of S's blocks plus Cholesky fill), and per step the panel / trailing-update / back-
@@ -1800,7 +1803,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         }
     }
 
-    
+    mark("sba symbolic factorisation");
     // the multi-workgroup factor's per-launch descriptors (FacStep: 8 ints per component and step)
     {
         const int fk = std::max(p->max_nt - 1, 1);
@@ -1829,19 +1832,41 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
             std::copy(pair_desc[cc].begin(), pair_desc[cc].end(), p->fac_pairs_h.begin() + (size_t)16 * fp * cc);
     }
     VX_HIP(c, hipSetDevice(c->device));
-    int rc;
-    if ((rc = upload(c, p->fac_steps, p->fac_steps_h))) return rc;
-    if ((rc = upload(c, p->fac_pairs, p->fac_pairs_h))) return rc;
-    if ((rc = upload(c, p->kf_flags, flags))) return rc;
-    if ((rc = upload(c, p->kf_comp, kcomp))) return rc;
-    if ((rc = upload(c, p->kf_local, klocal))) return rc;
-    if ((rc = upload(c, p->comp_kf_ptr, p->comp_kf_ptr_h))) return rc;
-    if ((rc = upload(c, p->comp_kf, p->comp_kf_h))) return rc;
-    if ((rc = upload(c, p->comp_off, p->comp_off_h))) return rc;
-    if ((rc = upload(c, p->comp_loff, loff))) return rc;
-    if ((rc = upload(c, p->comp_np, p->comp_np_h))) return rc;
-    if ((rc = upload(c, p->comp_hdr, hdr))) return rc;
-    if ((rc = upload(c, p->tl, tlist))) return rc;
+    // the tables through one pinned staging block, copied on the plan's stream (ordered before its
+    // runs; a rebuild synchronises before it rewrites the block)
+    {
+        size_t tot = 0;
+        auto add = [&](const auto& v) { tot += (std::max<size_t>(1, v.size()) * sizeof(v[0]) + 255) & ~(size_t)255; };
+        add(p->fac_steps_h), add(p->fac_pairs_h), add(flags), add(kcomp), add(klocal), add(p->comp_kf_ptr_h);
+        add(p->comp_kf_h), add(p->comp_off_h), add(loff), add(p->comp_np_h), add(hdr), add(tlist);
+        VX_HIP(c, p->stage.ensure(tot, true));
+        unsigned char* st = static_cast<unsigned char*>(p->stage.p);
+        size_t off = 0;
+        hipError_t e = hipSuccess;
+        auto put = [&](DevBuf& d, const auto& v) {
+            const size_t n = v.size() * sizeof(v[0]);
+            if (e == hipSuccess) e = d.ensure(std::max<size_t>(1, v.size()) * sizeof(v[0]));
+            if (e == hipSuccess && n) {
+                std::memcpy(st + off, v.data(), n);
+                e = hipMemcpyAsync(d.p, st + off, n, hipMemcpyHostToDevice, c->stream);
+            }
+            off += (std::max<size_t>(1, v.size()) * sizeof(v[0]) + 255) & ~(size_t)255;
+        };
+        put(p->fac_steps, p->fac_steps_h);
+        put(p->fac_pairs, p->fac_pairs_h);
+        put(p->kf_flags, flags);
+        put(p->kf_comp, kcomp);
+        put(p->kf_local, klocal);
+        put(p->comp_kf_ptr, p->comp_kf_ptr_h);
+        put(p->comp_kf, p->comp_kf_h);
+        put(p->comp_off, p->comp_off_h);
+        put(p->comp_loff, loff);
+        put(p->comp_np, p->comp_np_h);
+        put(p->comp_hdr, hdr);
+        put(p->tl, tlist);
+        VX_HIP(c, e);
+    }
+    mark("sba uploads");
     VX_HIP(c, p->pose.ensure((size_t)nk * 2 * 8 * sizeof(double)));
     VX_HIP(c, p->lm.ensure((size_t)std::max(n_opt, 1) * 2 * 4 * sizeof(double)));
     VX_HIP(c, p->wy.ensure((size_t)std::max(p->n_oo, 1) * kWy * sizeof(double)));
@@ -1850,16 +1875,17 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     // D | kf_cost]; unsharded, k_sba_solve factors it in place, sharded it factors the all-reduced copy
     const size_t red_n = (size_t)p->l_total + (size_t)nk * 14;
     VX_HIP(c, p->red.ensure(red_n * sizeof(double)));
-    VX_HIP(c, hipMemset(p->red.p, 0, red_n * sizeof(double)));
+    VX_HIP(c, hipMemsetAsync(p->red.p, 0, red_n * sizeof(double), c->stream));
     if (p->shard_count > 1) {
         VX_HIP(c, p->red_sum.ensure(red_n * sizeof(double)));
-        VX_HIP(c, hipMemset(p->red_sum.p, 0, red_n * sizeof(double)));
+        VX_HIP(c, hipMemsetAsync(p->red_sum.p, 0, red_n * sizeof(double), c->stream));
     }
     VX_HIP(c, p->Linv.ensure((size_t)std::max<long long>(p->l_total, 1) * sizeof(double)));
     VX_HIP(c, p->dx.ensure((size_t)nk * 6 * sizeof(double)));
-    VX_HIP(c, hipMemset(p->dx.p, 0, (size_t)nk * 6 * sizeof(double)));
+    VX_HIP(c, hipMemsetAsync(p->dx.p, 0, (size_t)nk * 6 * sizeof(double), c->stream));
     VX_HIP(c, p->state.ensure(sizeof(SBAState)));
-    VX_HIP(c, hipMemset(p->state.p, 0, sizeof(SBAState)));
+    VX_HIP(c, hipMemsetAsync(p->state.p, 0, sizeof(SBAState), c->stream));
+    mark("sba solve buffers");
     return VX_OK;
 }
 
@@ -2079,6 +2105,24 @@ int vx_sba_plan_create_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, co
         return rc;
     }
     *out = p;
+    return VX_OK;
+}
+
+int vx_sba_plan_rebuild_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba_plan* p) {
+    if (!c || !p || !m || p->c != c || m->c != c)
+        return c ? set_error(c, VX_ERR_INVALID, "vx_sba_plan_rebuild_dmap: bad arguments") : VX_ERR_INVALID;
+    if (!p->from_dmap) return set_error(c, VX_ERR_STATE, "plan was not built from a vx_dmap");
+    // the previous build's staged uploads and any run of the plan are complete before its buffers
+    // and staging are rewritten (a no-op after the fetch that normally precedes a rebuild)
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    p->graph.reset();
+    p->ran = false;
+    const int rc = build_sba_plan_dmap(c, m, ref, has_ref, p);
+    if (rc) {
+        (void)hipStreamSynchronize(c->stream);
+        p->status = 1;
+        return rc;
+    }
     return VX_OK;
 }
 

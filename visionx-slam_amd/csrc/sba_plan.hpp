@@ -44,6 +44,7 @@ struct vx_sba_plan {
     vx::DevBuf fac_pairs;
     int max_pairs = 0;
     int max_back = 0;  // most back-substitution tiles of one component (k_sba_backsub stages the lists in LDS)
+    vx::PinnedBuf stage;  // host staging of the finish's table uploads (sba_plan_finish)
 };
 
 
@@ -53,5 +54,6 @@ constexpr int kSbaLmThreads = 256;  // k_sba_lm: max observations (and landmarks
 // observation, landmark, pair and block tables on the device; flags (bit0 camera, bit1 fixed) and
 // the block list (i, j) on the host.  Covisibility components, the symbolic tile factorisation, their
 // uploads and the run buffers.
-int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, const std::vector<int2>& bij);
+int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, const std::vector<int2>& bij,
+                    const PlanClock* clk = nullptr);
 }  // namespace vx

@@ -157,6 +157,12 @@ OwnedGraph::~OwnedGraph() {
     if (exec) (void)hipGraphExecDestroy(exec);
 }
 
+void OwnedGraph::reset() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    exec = nullptr;
+    seen = false;
+}
+
 }  // namespace vx
 
 static const char* kStageNames[vx::kStCount] = {

@@ -5,7 +5,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -17,6 +19,17 @@
 #endif
 
 namespace vx {
+
+// $VX_PLAN_TIMING: host timestamps of a plan build's stages on stderr (ms since the build began)
+struct PlanClock {
+    bool on = std::getenv("VX_PLAN_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void mark(const char* what) const {
+        if (on)
+            std::fprintf(stderr, "[vx plan] %-28s %.3f ms\n", what,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    }
+};
 
 constexpr int kMaxLevels = 12;
 
@@ -296,6 +309,7 @@ struct OwnedGraph {
     OwnedGraph(const OwnedGraph&) = delete;
     OwnedGraph& operator=(const OwnedGraph&) = delete;
     ~OwnedGraph();
+    void reset();  // forget the captured sequence (the next run is eager, then captured again)
 };
 int graph_run_owned(vx_ctx* c, OwnedGraph& g, int (*enqueue)(vx_ctx*, void*), void* arg);
 

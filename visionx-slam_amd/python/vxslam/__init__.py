@@ -91,7 +91,7 @@ EXPORTS = [
     "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run", "vx_ba_optimize_dmap",
-    "vx_ba_dmap_results", "vx_sba_plan_create_dmap", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
+    "vx_ba_dmap_results", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
     "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run", "vx_seq_set_threads",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
     "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
@@ -924,6 +924,13 @@ class DMap:
         self.ctx._check(lib().vx_sba_plan_create_dmap(self.ctx.handle, self._h,
                                                       C.c_uint64(0 if ref_kf_id is None else int(ref_kf_id)),
                                                       0 if ref_kf_id is None else 1, C.byref(opts), C.byref(plan._h)))
+        return plan
+
+    def sba_plan_rebuild(self, plan: "SBAPlan", ref_kf_id=None) -> "SBAPlan":
+        """vx_sba_plan_rebuild_dmap: rebuild a plan of this map in place (its buffers reused)."""
+        self.ctx._check(lib().vx_sba_plan_rebuild_dmap(self.ctx.handle, self._h,
+                                                       C.c_uint64(0 if ref_kf_id is None else int(ref_kf_id)),
+                                                       0 if ref_kf_id is None else 1, plan._h))
         return plan
 
     def results(self):
