@@ -48,6 +48,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include "vx_sort.hpp"
+#include "vx_copy.hpp"
 
 #include "vx_internal.hpp"
 #include "ba_common.hpp"
@@ -575,7 +576,7 @@ int lean_build_core(vx_ctx* c, vx_dmap* m, int min_point, int q, bool lstage, in
 struct SbaArgs {
     int nk, nf;
     int64_t nl;
-    int pad_key, pad_kf;
+    int pad_kf;
     const int* dyn_r;
     int* dyn;
     const int* plm;
@@ -583,9 +584,8 @@ struct SbaArgs {
     const double2* puv;
     const int* kflags;        // window row flags (bit1: fixed)
     int* pkey;
-    int* pval;
     const int* skey;
-    const int* perm;
+    int* perm;
     int* scnt;                // per optimised slot: observations (scan input)
     const int* lm_ptr;
     double2* obs_uv;
@@ -606,18 +606,42 @@ struct SbaArgs {
     int q;
 };
 
+// The observations in (optimised slot | n_opt) order, stable — what a radix sort by that key gives —
+// without the sort (three onesweep passes over every observation): per slot a count (scanned into
+// lm_ptr) and a cursor, each slot's few observations then put back in index order (k_sb_fix); the
+// fixed landmarks' observations (key n_opt) at the exclusive scan of their flags, in index order.
 __global__ __launch_bounds__(kT) void k_sb_keys(SbaArgs a) {
     const int o = blockIdx.x * kT + threadIdx.x;
     if (o >= a.nf) return;
     const int n_obs = a.dyn[kDynPoseObs], n_opt = a.dyn[kDynNOpt];
-    int key = a.pad_key;
+    int fixed = 0;
     if (o < n_obs) {
         const int s = a.plm[o];
-        key = s < n_opt ? s : n_opt;
         if (s < n_opt) atomicAdd(&a.scnt[s], 1);
+        else fixed = 1;
     }
-    a.pkey[o] = key;
-    a.pval[o] = o;
+    a.pkey[o] = fixed;  // (scan input: the fixed observations' ranks)
+}
+
+__global__ __launch_bounds__(kT) void k_sb_scatter(SbaArgs a) {
+    const int o = blockIdx.x * kT + threadIdx.x;
+    if (o >= a.dyn_r[kDynPoseObs]) return;
+    const int n_opt = a.dyn_r[kDynNOpt], s = a.plm[o];
+    const int p = s < n_opt ? a.lm_ptr[s] + atomicSub(&a.scnt[s], 1) - 1 : a.lm_ptr[n_opt] + a.skey[o];
+    a.perm[p] = o;
+}
+
+// each optimised slot's observations (at most kSbaLmThreads) in ascending index order
+__global__ __launch_bounds__(kT) void k_sb_fix(SbaArgs a) {
+    const int s = blockIdx.x * kT + threadIdx.x;
+    if (s >= a.dyn_r[kDynNOpt]) return;
+    const int p0 = a.lm_ptr[s], p1 = a.lm_ptr[s + 1];
+    for (int i = p0 + 1; i < p1; ++i) {
+        const int v = a.perm[i];
+        int j = i;
+        for (; j > p0 && a.perm[j - 1] > v; --j) a.perm[j] = a.perm[j - 1];
+        a.perm[j] = v;
+    }
 }
 
 __global__ __launch_bounds__(kT) void k_sb_obs(SbaArgs a) {
@@ -882,7 +906,7 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     VX_HIP(c, hipMemcpyAsync(p->kf_flags.p, flags.data(), (size_t)nk * 4, hipMemcpyHostToDevice, sm));
     const size_t fN = (size_t)nf + 1, lN = (size_t)nl + 2;
     const int n2 = nk * nk;
-    for (DevBuf* d : {&B.pkey, &B.pval, &B.skey, &B.perm, &B.k2, &B.v2}) VX_HIP(c, grow(*d, fN * 4));
+    for (DevBuf* d : {&B.pkey, &B.skey, &B.perm, &B.k2, &B.v2}) VX_HIP(c, grow(*d, fN * 4));
     for (DevBuf* d : {&B.scnt, &B.pc, &B.pptr}) VX_HIP(c, grow(*d, lN * 4));
     for (DevBuf* d : {&B.kcnt, &B.oflag, &B.orank, &B.bidx}) VX_HIP(c, grow(*d, ((size_t)n2 + 1) * 4));
     VX_HIP(c, p->blk_ij.ensure(((size_t)n2 + nk + 1) * 8));
@@ -898,7 +922,6 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     a.nk = nk;
     a.nf = nf;
     a.nl = nl;
-    a.pad_key = (int)((1ll << bits_for(nl + 1)) - 1);
     a.pad_kf = (int)((1ll << bits_for(nk)) - 1);
     a.dyn = K.a.dyn;
     a.dyn_r = K.a.dyn;
@@ -907,7 +930,6 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     a.puv = K.a.puv;
     a.kflags = p->kf_flags.as<int>();
     a.pkey = B.pkey.as<int>();
-    a.pval = B.pval.as<int>();
     a.skey = B.skey.as<int>();
     a.perm = B.perm.as<int>();
     a.scnt = B.scnt.as<int>();
@@ -924,13 +946,14 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     a.orank = B.orank.as<int>();
     a.bidx = B.bidx.as<int>();
     a.bij = p->blk_ij.as<int2>();
-    // observations: stable sort by (optimised slot | n_opt), landmark pointers
+    // observations in stable (optimised slot | n_opt) order, landmark pointers
     hipLaunchKernelGGL(k_sb_keys, dim3(grid(nf)), dim3(kT), 0, sm, a);
     VX_LAUNCH_CHECK(c, "k_sb_keys");
-    if (nf && (rc = sort_pairs(c, B.tmp, a.pkey, B.skey.as<int>(), a.pval, B.perm.as<int>(), (size_t)nf,
-                               bits_for(a.pad_key))))
-        return rc;
     if ((rc = scan_ex<int>(c, L.tmp, a.scnt, p->lm_ptr.as<int>(), nl))) return rc;
+    if ((rc = scan_ex<int>(c, L.tmp, a.pkey, B.skey.as<int>(), nf))) return rc;
+    hipLaunchKernelGGL(k_sb_scatter, dim3(grid(nf)), dim3(kT), 0, sm, a);
+    hipLaunchKernelGGL(k_sb_fix, dim3(grid(nl)), dim3(kT), 0, sm, a);
+    VX_LAUNCH_CHECK(c, "k_sb_scatter / k_sb_fix");
     hipLaunchKernelGGL(k_sb_obs, dim3(grid(nf)), dim3(kT), 0, sm, a);
     VX_LAUNCH_CHECK(c, "k_sb_obs");
     // keyframe lists: observation indices by window row, ascending within a row
@@ -999,14 +1022,15 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     VX_HIP(c, p->lm0.ensure((size_t)std::max(n_lm, 1) * 32));
     VX_HIP(c, p->lm_map_dev.ensure((size_t)std::max(n_lm, 1) * 4));
     VX_HIP(c, p->kf_map_dev.ensure((size_t)nk * 4));
-    VX_HIP(c, hipMemcpyAsync(p->pose0.p, K.a.kf_pose0, (size_t)nk * 64, hipMemcpyDeviceToDevice, sm));
-    VX_HIP(c, hipMemcpyAsync(p->intr.p, K.a.kf_intr, (size_t)nk * 32, hipMemcpyDeviceToDevice, sm));
-    VX_HIP(c, hipMemcpyAsync(p->kf_ptr.p, K.a.kf_obs_ptr, ((size_t)nk + 1) * 4, hipMemcpyDeviceToDevice, sm));
-    if (n_lm) {
-        VX_HIP(c, hipMemcpyAsync(p->lm0.p, K.a.lm_pos0, (size_t)n_lm * 32, hipMemcpyDeviceToDevice, sm));
-        VX_HIP(c, hipMemcpyAsync(p->lm_map_dev.p, K.a.inv, (size_t)n_lm * 4, hipMemcpyDeviceToDevice, sm));
+    {  // (one launch for the six copies)
+        MultiCopy mc;
+        bool ok = mc.add(p->pose0.p, K.a.kf_pose0, (size_t)nk * 64) && mc.add(p->intr.p, K.a.kf_intr, (size_t)nk * 32) &&
+                  mc.add(p->kf_ptr.p, K.a.kf_obs_ptr, ((size_t)nk + 1) * 4) &&
+                  mc.add(p->lm0.p, K.a.lm_pos0, (size_t)n_lm * 32) && mc.add(p->lm_map_dev.p, K.a.inv, (size_t)n_lm * 4) &&
+                  mc.add(p->kf_map_dev.p, K.a.win, (size_t)nk * 4);
+        if (!ok) return set_error(c, VX_ERR_STATE, "sba plan: unaligned table copy");
+        VX_HIP(c, mc.launch(sm));
     }
-    VX_HIP(c, hipMemcpyAsync(p->kf_map_dev.p, K.a.win, (size_t)nk * 4, hipMemcpyDeviceToDevice, sm));
     // ---- read-back 2: the workgroup count and the block list (the host's components and symbolic
     // factorisation need it)
     int2* HB = reinterpret_cast<int2*>(H + kDynInts);

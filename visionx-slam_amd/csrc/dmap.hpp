@@ -69,7 +69,7 @@ struct vx_dmap {
     } lean;
     // scratch of the Schur plan build from this map (vx_sba_plan_create_dmap)
     struct SbaScratch {
-        vx::DevBuf pkey, pval, skey, perm, k2, v2, scnt, pc, pptr, kcnt, oflag, orank, bidx, ekey, eval, ekey2, tmp;
+        vx::DevBuf pkey, skey, perm, k2, v2, scnt, pc, pptr, kcnt, oflag, orank, bidx, ekey, eval, ekey2, tmp;
         vx::PinnedBuf rb;
     } sba;
     ~vx_dmap();

@@ -49,6 +49,7 @@
 #include "ba_common.hpp"
 #include "sba_plan.hpp"
 #include "dmap.hpp"
+#include "vx_copy.hpp"
 
 namespace vx {
 namespace {
@@ -1832,25 +1833,30 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
             std::copy(pair_desc[cc].begin(), pair_desc[cc].end(), p->fac_pairs_h.begin() + (size_t)16 * fp * cc);
     }
     VX_HIP(c, hipSetDevice(c->device));
-    // the tables through one pinned staging block, copied on the plan's stream (ordered before its
-    // runs; a rebuild synchronises before it rewrites the block)
+    // the tables through one pinned staging block: one copy to the device, one launch scattering it
+    // into the plan's buffers (a rebuild synchronises before it rewrites the block)
     {
+        auto pad = [](size_t b) { return (b + 255) & ~(size_t)255; };
         size_t tot = 0;
-        auto add = [&](const auto& v) { tot += (std::max<size_t>(1, v.size()) * sizeof(v[0]) + 255) & ~(size_t)255; };
+        auto add = [&](const auto& v) { tot += pad(std::max<size_t>(1, v.size()) * sizeof(v[0])); };
         add(p->fac_steps_h), add(p->fac_pairs_h), add(flags), add(kcomp), add(klocal), add(p->comp_kf_ptr_h);
         add(p->comp_kf_h), add(p->comp_off_h), add(loff), add(p->comp_np_h), add(hdr), add(tlist);
         VX_HIP(c, p->stage.ensure(tot, true));
+        VX_HIP(c, p->stage_dev.ensure(tot));
         unsigned char* st = static_cast<unsigned char*>(p->stage.p);
+        unsigned char* sd = static_cast<unsigned char*>(p->stage_dev.p);
         size_t off = 0;
         hipError_t e = hipSuccess;
+        MultiCopy mc;
+        bool ok = true;
         auto put = [&](DevBuf& d, const auto& v) {
             const size_t n = v.size() * sizeof(v[0]);
-            if (e == hipSuccess) e = d.ensure(std::max<size_t>(1, v.size()) * sizeof(v[0]));
+            if (e == hipSuccess) e = d.ensure(std::max<size_t>(1, n));
             if (e == hipSuccess && n) {
                 std::memcpy(st + off, v.data(), n);
-                e = hipMemcpyAsync(d.p, st + off, n, hipMemcpyHostToDevice, c->stream);
+                ok = ok && mc.add(d.p, sd + off, n);
             }
-            off += (std::max<size_t>(1, v.size()) * sizeof(v[0]) + 255) & ~(size_t)255;
+            off += pad(std::max<size_t>(1, n));
         };
         put(p->fac_steps, p->fac_steps_h);
         put(p->fac_pairs, p->fac_pairs_h);
@@ -1865,6 +1871,9 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         put(p->comp_hdr, hdr);
         put(p->tl, tlist);
         VX_HIP(c, e);
+        if (!ok) return set_error(c, VX_ERR_STATE, "sba plan: table staging");
+        VX_HIP(c, hipMemcpyAsync(sd, st, off, hipMemcpyHostToDevice, c->stream));
+        VX_HIP(c, mc.launch(c->stream));
     }
     mark("sba uploads");
     VX_HIP(c, p->pose.ensure((size_t)nk * 2 * 8 * sizeof(double)));
