@@ -167,6 +167,36 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
         assert v == ref, k
 
 
+def test_sba_diagonal_block_split(ctx, oracle, monkeypatch):
+    """k_sba_blocks with each diagonal block over D workgroups (partial sums added in part order by
+    k_sba_blocks_diag) against one workgroup per block: the same run up to the summation order of the
+    reduced system's diagonal blocks (same iterations, accept decisions and observation counts, costs
+    within 1e-9), deterministic run to run, and pinned to the restatement."""
+    import vxslam
+
+    m = synth.make_ba_map(0x5EED0D00, 50, 20000)
+    opts = vxslam.default_sba_options(window=50, iters=6)
+    res = {}
+    for d in ("1", "3", "3", "8"):
+        monkeypatch.setenv("VX_SBA_DIAG_SPLIT", d)
+        mm = m.copy()
+        plan = ctx.sba_plan(mm, opts)
+        plan.run_async()
+        st = plan.fetch(mm)
+        plan.close()
+        r = (st.iterations, st.accepted, list(st.obs), list(st.step), list(st.cost), mm["kf_pose"].copy())
+        if d in res:  # repeat: bitwise
+            assert r[:5] == res[d][:5] and np.array_equal(r[5], res[d][5])
+        res[d] = r
+    base = res["1"]
+    for d in ("3", "8"):
+        assert res[d][:4] == base[:4], d
+        np.testing.assert_allclose(res[d][4], base[4], rtol=1e-9)
+        np.testing.assert_allclose(res[d][5], base[5], rtol=0, atol=1e-9)
+    monkeypatch.setenv("VX_SBA_DIAG_SPLIT", "3")
+    _case(ctx, oracle, m.copy(), dict(window=50, iters=6))
+
+
 @pytest.mark.parametrize("cfg", [("C3", 50, 20000, 1, 0.0), ("C5s", 96, 16000, 8, 0.03)])
 def test_sba_plan_from_resident_map(ctx, oracle, cfg):
     """vx_sba_plan_create_dmap builds the Schur plan's tables on the device from the resident map

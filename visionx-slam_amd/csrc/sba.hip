@@ -129,6 +129,8 @@ struct SBAArgs {
     const int* tl;          // tile programs
     double* wy;             // n_oo x kWy
     double* lm_sys;         // n_opt x kLmSys
+    int diag_split;         // k_sba_blocks workgroups per diagonal block (D)
+    double* bpart;          // D > 1: nk x D x kBlkTerms partial sums of the diagonal blocks
     double* red;            // local: S blocks | rhs (6 nk) | D (6 nk) | kf_cost (2 nk)
     const double* red_sum;  // == red unless sharded
     long long s_total;      // doubles of all component matrices
@@ -324,11 +326,38 @@ __device__ __forceinline__ void load18(const double* src, double* v) {
     }
 }
 
+// block b's reduced terms v (thread tid < kBlkTerms holds term tid): the 6x6 block into the
+// component matrix, a diagonal block's rhs / D / cost rows
+__device__ __forceinline__ void blocks_write(const SBAArgs& a, int i, int j, bool diag, int tid, double v) {
+    const int n6 = 6 * a.nk;
+    double* rhs = a.red + a.s_total;
+    if (tid < 36) {
+        const int c = a.kf_comp[i];
+        if (c < 0) return;  // a fixed keyframe's block: its row is the identity (k_sba_solve)
+        const int np = a.comp_np[c];
+        const int li = a.kf_local[i], lj = a.kf_local[j];
+        const int r = tid / 6, cc = tid - 6 * r;
+        a.red[a.comp_loff[c] + (long long)(6 * li + r) * np + 6 * lj + cc] = v;
+    } else if (diag) {
+        if (tid < 42) rhs[6 * i + tid - 36] = v;
+        else if (tid < 48) rhs[n6 + 6 * i + tid - 42] = v;
+        else rhs[2 * n6 + 2 * i + tid - 48] = v;
+    }
+}
+
+// Workgroups [0, nk D): the diagonal blocks, D per keyframe (workgroup x: keyframe x mod nk, part
+// x / nk) — a diagonal block walks all its keyframe's observations (~1300-1700 at C3 / C5) and as
+// many self pairs, a chain of dependent loads per 256 of them that set the launch's length; the D
+// parts' sums land in bpart and k_sba_blocks_diag adds them in part order.  Then one workgroup per
+// off-diagonal block.
 __global__ __launch_bounds__(kBlkThreads) void k_sba_blocks(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     __shared__ double red[kBlkThreads / 64][64];
-    const int tid = threadIdx.x, b = blockIdx.x;
-    if (b == 0 && tid == 0) a.st->fail[it] = 0;
+    const int tid = threadIdx.x, D = a.diag_split, nd = a.nk * D;
+    if (blockIdx.x == 0 && tid == 0) a.st->fail[it] = 0;
+    const int x = blockIdx.x;
+    const int b = x < nd ? x % a.nk : a.nk + (x - nd);
+    const int part = x < nd ? x / a.nk : 0, pstride = x < nd ? D * kBlkThreads : kBlkThreads;
     const int2 ij = a.blk_ij[b];
     const int i = ij.x, j = ij.y;
     const bool diag = i == j;
@@ -344,7 +373,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_sba_blocks(SBAArgs a, int it) {
         for (int q = 0; q < 8; ++q) T[q] = Tb[8 * i + q];
 #pragma unroll
         for (int q = 0; q < 4; ++q) C[q] = a.intr[4 * i + q];
-        for (int idx = a.kf_ptr[i] + tid; idx < a.kf_ptr[i + 1]; idx += kBlkThreads) {
+        for (int idx = a.kf_ptr[i] + part * kBlkThreads + tid; idx < a.kf_ptr[i + 1]; idx += pstride) {
             const int o = a.kf_obs[idx];
             const int s = a.obs_lm[o];
             const double* P = (s < a.n_opt ? Pb : a.lm0) + 4 * (long long)s;
@@ -374,7 +403,7 @@ __global__ __launch_bounds__(kBlkThreads) void k_sba_blocks(SBAArgs a, int it) {
             }
         }
     }
-    for (int p = a.blk_ptr[b] + tid; p < a.blk_ptr[b + 1]; p += kBlkThreads) {
+    for (int p = a.blk_ptr[b] + part * kBlkThreads + tid; p < a.blk_ptr[b + 1]; p += pstride) {
         const int2 pr = a.pairs[p];
         double Y[18], W[18];
         load18(a.wy + (long long)pr.x * kWy + 18, Y);
@@ -406,20 +435,22 @@ __global__ __launch_bounds__(kBlkThreads) void k_sba_blocks(SBAArgs a, int it) {
     double v = red[0][tid];
 #pragma unroll
     for (int w2 = 1; w2 < kBlkThreads / 64; ++w2) v += red[w2][tid];
-    const int n6 = 6 * a.nk;
-    double* rhs = a.red + a.s_total;
-    if (tid < 36) {
-        const int c = a.kf_comp[i];
-        if (c < 0) return;  // a fixed keyframe's block: its row is the identity (k_sba_solve)
-        const int np = a.comp_np[c];
-        const int li = a.kf_local[i], lj = a.kf_local[j];
-        const int r = tid / 6, cc = tid - 6 * r;
-        a.red[a.comp_loff[c] + (long long)(6 * li + r) * np + 6 * lj + cc] = v;
-    } else if (diag) {
-        if (tid < 42) rhs[6 * i + tid - 36] = v;
-        else if (tid < 48) rhs[n6 + 6 * i + tid - 42] = v;
-        else rhs[2 * n6 + 2 * i + tid - 48] = v;
+    if (diag && D > 1) {
+        a.bpart[((long long)i * D + part) * kBlkTerms + tid] = v;
+        return;
     }
+    blocks_write(a, i, j, diag, tid, v);
+}
+
+// D > 1: the diagonal blocks' parts summed in part order (deterministic), then written as above
+__global__ __launch_bounds__(64) void k_sba_blocks_diag(SBAArgs a, int it) {
+    if (it > 0 && !a.st->active[it]) return;
+    const int i = blockIdx.x, tid = threadIdx.x, D = a.diag_split;
+    if (tid >= kBlkTerms) return;
+    const double* bp = a.bpart + (long long)i * D * kBlkTerms + tid;
+    double v = bp[0];
+    for (int d = 1; d < D; ++d) v += bp[(long long)d * kBlkTerms];
+    blocks_write(a, i, i, true, tid, v);
 }
 
 // ------------------------------------------------------------------------- k_sba_solve
@@ -1285,6 +1316,8 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.tl = p->tl.as<int>();
     a.wy = p->wy.as<double>();
     a.lm_sys = p->lm_sys.as<double>();
+    a.diag_split = p->diag_split;
+    a.bpart = p->bpart.as<double>();
     a.red = p->red.as<double>();
     a.red_sum = p->shard_count > 1 ? p->red_sum.as<double>() : p->red.as<double>();
     a.s_total = p->l_total;
@@ -1889,6 +1922,13 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         VX_HIP(c, p->red_sum.ensure(red_n * sizeof(double)));
         VX_HIP(c, hipMemsetAsync(p->red_sum.p, 0, red_n * sizeof(double), c->stream));
     }
+    // k_sba_blocks: D workgroups per diagonal block, ~512 of its keyframe's observations each, where
+    // the diagonal blocks are the launch's long pole — few off-diagonal blocks (measured, r04z: C3
+    // 40.9 -> 34.2 us per launch, C5 97.6 -> 92.1; the connected C5's 2318 off-diagonal blocks
+    // 96.7 -> 101.3, so it keeps D = 1).  $VX_SBA_DIAG_SPLIT overrides; 1 = the round-3 form.
+    p->diag_split = p->n_blocks <= 8 * nk ? std::max(1, std::min(8, (int)((p->n_obs / std::max(nk, 1) + 511) / 512))) : 1;
+    if (const char* e = std::getenv("VX_SBA_DIAG_SPLIT")) p->diag_split = std::max(1, std::min(8, std::atoi(e)));
+    VX_HIP(c, p->bpart.ensure((size_t)nk * p->diag_split * kBlkTerms * sizeof(double)));
     VX_HIP(c, p->Linv.ensure((size_t)std::max<long long>(p->l_total, 1) * sizeof(double)));
     VX_HIP(c, p->dx.ensure((size_t)nk * 6 * sizeof(double)));
     VX_HIP(c, hipMemsetAsync(p->dx.p, 0, (size_t)nk * 6 * sizeof(double), c->stream));
@@ -1982,7 +2022,10 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
     for (int it = 0; it < p->opt.max_iterations; ++it) {
         if (p->n_lm_blocks > 0)
             VX_HIP(c, launch(c, kStSbaLandmark, k_sba_lm, dim3(p->n_lm_blocks), dim3(kLmThreads), 0, c->stream, a, it));
-        VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks, dim3(p->n_blocks), dim3(kBlkThreads), 0, c->stream, a, it));
+        VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks, dim3(p->n_blocks + p->nk * (p->diag_split - 1)),
+                         dim3(kBlkThreads), 0, c->stream, a, it));
+        if (p->diag_split > 1)
+            VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks_diag, dim3(p->nk), dim3(64), 0, c->stream, a, it));
 #ifndef VX_NO_RCCL
         if (sharded) {
             ProfScope ps(c, kStSbaAllreduce);

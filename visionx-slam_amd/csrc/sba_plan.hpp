@@ -44,6 +44,8 @@ struct vx_sba_plan {
     vx::DevBuf fac_pairs;
     int max_pairs = 0;
     int max_back = 0;  // most back-substitution tiles of one component (k_sba_backsub stages the lists in LDS)
+    int diag_split = 1;  // k_sba_blocks workgroups per diagonal block (sba_plan_finish)
+    vx::DevBuf bpart;    // their partial sums
     vx::PinnedBuf stage;  // host staging of the finish's table uploads (sba_plan_finish) ...
     vx::DevBuf stage_dev;  // ... and its device copy, scattered into the tables by one launch
 };
