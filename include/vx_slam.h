@@ -457,6 +457,13 @@ int vx_sba_plan_create_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int h
  * unusable (status set, no run) until a successful rebuild. */
 int vx_sba_plan_rebuild_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_ref, vx_sba_plan* plan);
 int vx_sba_plan_apply_dmap(vx_ctx* ctx, vx_sba_plan* plan, vx_dmap* map);
+/* Test hook, the Schur counterpart of vx_ba_shard_emulate_run: the n shard plans of one window
+ * (vx_sba_plan_create with shard_rank r of n, all on ctx; every shard's block structure is the whole
+ * window's) run as n ranks would on one device — per iteration every shard's landmark stage and
+ * blocks, then their reduced systems summed element-wise in rank order into every shard in place of
+ * the ncclAllReduce, then every shard's (identical) factorisation, back-substitution and update.
+ * Fetch each plan afterwards. */
+int vx_sba_shard_emulate_run(vx_ctx* ctx, vx_sba_plan* const* plans, int n);
 int vx_sba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                         const vx_sba_options* opt, vx_sba_stats* stats);
 

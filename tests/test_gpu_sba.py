@@ -197,6 +197,54 @@ def test_sba_diagonal_block_split(ctx, oracle, monkeypatch):
     _case(ctx, oracle, m.copy(), dict(window=50, iters=6))
 
 
+@pytest.mark.parametrize("cfg", [("C3", 50, 20000, 1, 0.0), ("rig8c", 96, 16000, 8, 0.03)])
+def test_sba_shard_emulation(ctx, cfg):
+    """The landmark-sharded Schur BA (SURVEY 8(e) "BA Schur mode": each rank's partial reduced system,
+    an all-reduce of the dense pose system, the factorisation replicated) run on one device by
+    vx_sba_shard_emulate_run with the all-reduce as a rank-order sum: every shard has the whole
+    window's block structure (same blocks, tiles and components), every shard ends with bitwise the
+    same poses and LM record, and the shards' landmarks together with the poses are the unsharded
+    run's (same decisions, costs within 1e-9, states within the north_star tolerance)."""
+    import vxslam
+
+    name, nk, nl, ns, cf = cfg
+    m = synth.make_ba_map(0x5EED05A0 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns, cross_frac=cf)
+    opts = vxslam.default_sba_options(window=nk, iters=6)
+    mu = m.copy()
+    pu = ctx.sba_plan(mu, opts)
+    pu.run_async()
+    su = pu.fetch(mu)
+    iu = pu.info()
+    pu.close()
+    assert su.status == 0 and su.accepted >= 2
+    for n in (2, 3):
+        plans = [ctx.sba_plan(m, opts, shard_rank=r, shard_count=n) for r in range(n)]
+        infos = [p.info() for p in plans]
+        for k in ("n_kf", "n_blocks", "n", "n_tiles", "n_comp"):
+            assert len({i[k] for i in infos}) == 1 and infos[0][k] == iu[k], (n, k, infos, iu)
+        assert sum(i["n_opt"] for i in infos) == iu["n_opt"]
+        ctx.sba_shard_emulate(plans)
+        outs, sts = [], []
+        for p in plans:
+            mm = m.copy()
+            sts.append(p.fetch(mm))
+            outs.append(mm)
+            p.close()
+        for st, mm in zip(sts[1:], outs[1:]):
+            assert (st.iterations, st.accepted, list(st.step), list(st.cost)) == \
+                (sts[0].iterations, sts[0].accepted, list(sts[0].step), list(sts[0].cost))
+            assert np.array_equal(mm["kf_pose"], outs[0]["kf_pose"])
+        st = sts[0]
+        assert (st.iterations, st.accepted, list(st.step), list(st.obs)) == \
+            (su.iterations, su.accepted, list(su.step), list(su.obs)), n
+        np.testing.assert_allclose(list(st.cost), list(su.cost), rtol=1e-9)
+        pg, pc = outs[0]["kf_pose"].copy(), mu["kf_pose"].copy()
+        pg[:, :4], pc[:, :4] = _canon(pg[:, :4]), _canon(pc[:, :4])
+        assert (np.abs(pg - pc) / np.maximum(np.abs(pc), 1e-3)).max() <= RTOL
+        merged = m["lm_pos"] + sum(mm["lm_pos"] - m["lm_pos"] for mm in outs)  # (each landmark: one owner)
+        assert (np.abs(merged - mu["lm_pos"]) / np.maximum(np.abs(mu["lm_pos"]), 1e-3)).max() <= RTOL
+
+
 @pytest.mark.parametrize("cfg", [("C3", 50, 20000, 1, 0.0), ("C5s", 96, 16000, 8, 0.03)])
 def test_sba_plan_from_resident_map(ctx, oracle, cfg):
     """vx_sba_plan_create_dmap builds the Schur plan's tables on the device from the resident map

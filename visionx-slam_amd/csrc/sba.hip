@@ -1586,6 +1586,35 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     std::vector<int> kcnt((size_t)nkey, 0);
     for (int t = 0; t < T; ++t)
         for (int64_t key = 0; key < nkey; ++key) kcnt[key] += kc[t][key];
+    // Sharded: the block structure is the whole window's, the same on every rank (the all-reduce
+    // sums the ranks' component matrices element by element, and the symbolic factorisation must
+    // cover every block any rank fills); a rank's own pairs fill part of it, the rest of its blocks
+    // stay empty.  The off-diagonal blocks of the co-observations of every optimised landmark.
+    std::vector<char> gblk;
+    if (p->shard_count > 1) {
+        gblk.assign((size_t)nkey, 0);
+        std::vector<char> is_opt(m->n_lm, 0);
+        for (int l : W.opt_all) is_opt[l] = 1;
+        std::vector<int> head(m->n_lm, -1), nxt, row;  // per landmark: its observations' keyframe rows
+        for (int r = 0; r < nk; ++r) {
+            if (!(flags[r] & 1) || (flags[r] & 2)) continue;  // (free keyframes only form blocks)
+            const int64_t f0 = m->kf_feat_ptr[win[r]];
+            for (int64_t i = 0; i < fbase[r + 1] - fbase[r]; ++i) {
+                if (m->feat_flags[f0 + i] & 2) continue;
+                const int l = wfeat_l[(size_t)(wfbase[r] + i)];
+                if (l < 0 || m->lm_bad[l] || !is_opt[l]) continue;
+                nxt.push_back(head[l]);
+                row.push_back(r);
+                head[l] = (int)row.size() - 1;
+            }
+        }
+        for (int l : W.opt_all)
+            for (int e1 = head[l]; e1 >= 0; e1 = nxt[e1])
+                for (int e2 = nxt[e1]; e2 >= 0; e2 = nxt[e2]) {
+                    const int i = std::max(row[e1], row[e2]), j = std::min(row[e1], row[e2]);
+                    if (i != j) gblk[(size_t)i * nk + j] = 1;
+                }
+    }
     std::vector<int2> bij;
     std::vector<int> bptr{0};
     std::vector<int> kpos((size_t)nkey, -1);  // output offset of each block key
@@ -1599,7 +1628,7 @@ int build_sba_plan(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int has_
     }
     for (int64_t key = 0; key < nkey; ++key) {
         const int i = (int)(key / nk), j = (int)(key % nk);
-        if (i == j || kcnt[key] == 0) continue;
+        if (i == j || (kcnt[key] == 0 && (gblk.empty() || !gblk[key]))) continue;
         bij.push_back(make_int2(i, j));
         kpos[key] = (int)total;
         total += kcnt[key];
@@ -1976,6 +2005,105 @@ int factor_groups(int max_trail_rest) {
     return std::max(1, std::min(g, 128));
 }
 
+// The launch configuration of a plan's run (the factor form, LDS sizes), fixed per run.
+struct SbaRunCfg {
+    SBAArgs a;
+    size_t lds = 0, bs_lds = 0, la_lds = 0, red_n = 0;
+    int upd_blocks = 1, G = 1, la_ps = 0;
+    bool multi = false, pair = false;
+};
+
+int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
+    r.a = make_args(p);
+    const SBAArgs& a = r.a;
+    r.lds = solve_lds_bytes(p->max_np, a.panel_slots);
+    if (r.lds > 64 * 1024)
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_solve),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.lds));
+    r.upd_blocks = (std::max(p->n_opt, p->nk) + kUpdThreads - 1) / kUpdThreads;
+    // the factorisation: one launch per tile step over G workgroups per component (components of
+    // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
+    r.bs_lds = (size_t)p->max_np * sizeof(double) + ((size_t)a.bs_nt + 1 + p->max_back) * sizeof(int);
+    if (r.bs_lds > 64 * 1024)
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.bs_lds));
+    r.multi = factor_multi(p->max_nt);
+    r.G = factor_groups(p->max_trail_rest);
+    // one tile column per launch (default) or two ($VX_SBA_FACTOR_COLS=2: half the launches, but
+    // workgroup 0's chain per launch doubles — measured slower on the connected C5, 1137 against 1030
+    // us per LM iteration, profiles/r04/sba_cols*_r04j.jsonl)
+    r.pair = std::getenv("VX_SBA_FACTOR_COLS") && std::atoi(std::getenv("VX_SBA_FACTOR_COLS")) == 2;
+    // workgroup 0's look-ahead column in LDS when its panel fits ($VX_SBA_LOOKAHEAD_LDS=0: global)
+    r.la_ps = std::max(p->max_panel, 1);
+    r.la_lds = lookahead_lds_bytes(p->max_nt, r.la_ps);
+    if (r.la_lds > 160 * 1024 || (std::getenv("VX_SBA_LOOKAHEAD_LDS") && std::atoi(std::getenv("VX_SBA_LOOKAHEAD_LDS")) == 0)) {
+        r.la_ps = 0;
+        r.la_lds = 4 * kPanelStride * sizeof(double);
+    }
+    if (r.multi && r.la_lds > 64 * 1024)
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_fac_step),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.la_lds));
+    r.red_n = (size_t)p->l_total + (size_t)p->nk * 14;
+    return VX_OK;
+}
+
+// iteration it, part 1: the landmark stage and the reduced system's blocks (this shard's share)
+int sba_assemble(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
+    const SBAArgs& a = r.a;
+    if (p->n_lm_blocks > 0)
+        VX_HIP(c, launch(c, kStSbaLandmark, k_sba_lm, dim3(p->n_lm_blocks), dim3(kLmThreads), 0, c->stream, a, it));
+    VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks, dim3(p->n_blocks + p->nk * (p->diag_split - 1)),
+                     dim3(kBlkThreads), 0, c->stream, a, it));
+    if (p->diag_split > 1)
+        VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks_diag, dim3(p->nk), dim3(64), 0, c->stream, a, it));
+    return VX_OK;
+}
+
+// iteration it, part 2 (on the summed system, sharded: identical on every rank): the LM decision,
+// the factorisation, back-substitution and the update
+int sba_solve_step(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
+    const SBAArgs& a = r.a;
+    const int G = r.G;
+    if (r.multi) {
+        VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
+                         c->stream, a, it, r.pair ? 1 : 0));
+        for (int t = 0; r.pair && t < p->max_pairs; ++t) {
+            FacPair sd{};  // (one component: the launch's bounds as arguments)
+            if (p->n_comp == 1) {
+                const int* d = p->fac_pairs_h.data() + 16 * (size_t)t;
+                sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
+                sd.l1b = d[2], sd.l1e = d[3], sd.l2b = d[4], sd.l2e = d[5], sd.rb = d[6], sd.re = d[7];
+                sd.p0 = d[8], sd.p1 = d[9], sd.q0 = d[10], sd.q1 = d[11], sd.nt = d[12], sd.c0 = d[13];
+            }
+            VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_pair, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads), 0,
+                             c->stream, a, it, t, G, sd));
+        }
+        for (int k = 0; !r.pair && k + 1 < p->max_nt; ++k) {
+            FacStep sd{};  // (one component: the step's bounds as launch arguments)
+            if (p->n_comp == 1) {
+                const int* d = p->fac_steps_h.data() + 8 * (size_t)k;
+                sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
+                sd.la_beg = d[2];
+                sd.split = d[3];
+                sd.t_end = d[4];
+                sd.p0 = d[5];
+                sd.p1 = d[6];
+                sd.nt = d[7];
+            }
+            VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_step, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads),
+                             (uint32_t)r.la_lds, c->stream, a, it, k, G, r.la_ps, sd));
+        }
+    } else {
+        VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+                         (uint32_t)r.lds, c->stream, a, it));
+    }
+    VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+                     (uint32_t)r.bs_lds, c->stream, a, it));
+    VX_HIP(c, launch(c, kStSbaUpdate, k_sba_update, dim3(std::max(r.upd_blocks, 1)), dim3(kUpdThreads), 0,
+                     c->stream, a, it));
+    return VX_OK;
+}
+
 int sba_run(vx_ctx* c, vx_sba_plan* p) {
     if (p->status != 0) {
         p->ran = true;
@@ -1990,89 +2118,37 @@ int sba_run(vx_ctx* c, vx_sba_plan* p) {
         return set_error(c, VX_ERR_COMM, "built without RCCL");
 #endif
     }
-    const SBAArgs a = make_args(p);
-    const size_t lds = solve_lds_bytes(p->max_np, a.panel_slots);
-    if (lds > 64 * 1024)
-        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_solve),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const int upd_blocks = (std::max(p->n_opt, p->nk) + kUpdThreads - 1) / kUpdThreads;
-    // the factorisation: one launch per tile step over G workgroups per component (components of
-    // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
-    const size_t bs_lds = (size_t)p->max_np * sizeof(double) + ((size_t)a.bs_nt + 1 + p->max_back) * sizeof(int);
-    if (bs_lds > 64 * 1024)
-        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)bs_lds));
-    const bool multi = factor_multi(p->max_nt);
-    const int G = factor_groups(p->max_trail_rest);
-    // one tile column per launch (default) or two ($VX_SBA_FACTOR_COLS=2: half the launches, but
-    // workgroup 0's chain per launch doubles — measured slower on the connected C5, 1137 against 1030
-    // us per LM iteration, profiles/r04/sba_cols*_r04j.jsonl)
-    const bool pair = std::getenv("VX_SBA_FACTOR_COLS") && std::atoi(std::getenv("VX_SBA_FACTOR_COLS")) == 2;
-    // workgroup 0's look-ahead column in LDS when its panel fits ($VX_SBA_LOOKAHEAD_LDS=0: global)
-    int la_ps = std::max(p->max_panel, 1);
-    size_t la_lds = lookahead_lds_bytes(p->max_nt, la_ps);
-    if (la_lds > 160 * 1024 || (std::getenv("VX_SBA_LOOKAHEAD_LDS") && std::atoi(std::getenv("VX_SBA_LOOKAHEAD_LDS")) == 0)) {
-        la_ps = 0;
-        la_lds = 4 * kPanelStride * sizeof(double);
-    }
-    if (multi && la_lds > 64 * 1024)
-        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_fac_step),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)la_lds));
-    const size_t red_n = (size_t)p->l_total + (size_t)p->nk * 14;
+    SbaRunCfg r;
+    int rc;
+    if ((rc = sba_prepare(c, p, r))) return rc;
     for (int it = 0; it < p->opt.max_iterations; ++it) {
-        if (p->n_lm_blocks > 0)
-            VX_HIP(c, launch(c, kStSbaLandmark, k_sba_lm, dim3(p->n_lm_blocks), dim3(kLmThreads), 0, c->stream, a, it));
-        VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks, dim3(p->n_blocks + p->nk * (p->diag_split - 1)),
-                         dim3(kBlkThreads), 0, c->stream, a, it));
-        if (p->diag_split > 1)
-            VX_HIP(c, launch(c, kStSbaBlocks, k_sba_blocks_diag, dim3(p->nk), dim3(64), 0, c->stream, a, it));
+        if ((rc = sba_assemble(c, p, r, it))) return rc;
 #ifndef VX_NO_RCCL
         if (sharded) {
             ProfScope ps(c, kStSbaAllreduce);
-            ncclResult_t r = ncclAllReduce(p->red.p, p->red_sum.p, red_n, ncclDouble, ncclSum, c->comm, c->stream);
-            if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(r));
+            ncclResult_t nr = ncclAllReduce(p->red.p, p->red_sum.p, r.red_n, ncclDouble, ncclSum, c->comm, c->stream);
+            if (nr != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllReduce: %s", ncclGetErrorString(nr));
         }
 #endif
-        if (multi) {
-            VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
-                             c->stream, a, it, pair ? 1 : 0));
-            for (int t = 0; pair && t < p->max_pairs; ++t) {
-                FacPair sd{};  // (one component: the launch's bounds as arguments)
-                if (p->n_comp == 1) {
-                    const int* d = p->fac_pairs_h.data() + 16 * (size_t)t;
-                    sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
-                    sd.l1b = d[2], sd.l1e = d[3], sd.l2b = d[4], sd.l2e = d[5], sd.rb = d[6], sd.re = d[7];
-                    sd.p0 = d[8], sd.p1 = d[9], sd.q0 = d[10], sd.q1 = d[11], sd.nt = d[12], sd.c0 = d[13];
-                }
-                VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_pair, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads), 0,
-                                 c->stream, a, it, t, G, sd));
-            }
-            for (int k = 0; !pair && k + 1 < p->max_nt; ++k) {
-                FacStep sd{};  // (one component: the step's bounds as launch arguments)
-                if (p->n_comp == 1) {
-                    const int* d = p->fac_steps_h.data() + 8 * (size_t)k;
-                    sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
-                    sd.la_beg = d[2];
-                    sd.split = d[3];
-                    sd.t_end = d[4];
-                    sd.p0 = d[5];
-                    sd.p1 = d[6];
-                    sd.nt = d[7];
-                }
-                VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_step, dim3(std::max(p->n_comp, 1) * G), dim3(kSolveThreads),
-                                 (uint32_t)la_lds, c->stream, a, it, k, G, la_ps, sd));
-            }
-        } else {
-            VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
-                             (uint32_t)lds, c->stream, a, it));
-        }
-        VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
-                         (uint32_t)bs_lds, c->stream, a, it));
-        VX_HIP(c, launch(c, kStSbaUpdate, k_sba_update, dim3(std::max(upd_blocks, 1)), dim3(kUpdThreads), 0,
-                         c->stream, a, it));
+        if ((rc = sba_solve_step(c, p, r, it))) return rc;
     }
     p->ran = true;
     return VX_OK;
+}
+
+// the shards' reduced systems summed in rank order into every shard's all-reduce target (the
+// emulated ncclAllReduce of vx_sba_shard_emulate_run)
+constexpr int kMaxSbaEmuShards = 8;
+struct RedPtrs {
+    const double* src[kMaxSbaEmuShards];
+    double* dst[kMaxSbaEmuShards];
+};
+__global__ void k_sba_sum_shards(RedPtrs p, int n, long long len) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    double s = p.src[0][i];
+    for (int r = 1; r < n; ++r) s += p.src[r][i];
+    for (int r = 0; r < n; ++r) p.dst[r][i] = s;
 }
 
 // the best state of a finished run (LM selection of the last iteration) into the resident rows
@@ -2157,6 +2233,43 @@ int vx_sba_plan_create_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, co
         return rc;
     }
     *out = p;
+    return VX_OK;
+}
+
+int vx_sba_shard_emulate_run(vx_ctx* c, vx_sba_plan* const* plans, int n) {
+    if (!c || !plans || n < 1 || n > kMaxSbaEmuShards)
+        return c ? set_error(c, VX_ERR_INVALID, "vx_sba_shard_emulate_run: bad arguments") : VX_ERR_INVALID;
+    vx_sba_plan* p0 = plans[0];
+    for (int r = 0; r < n; ++r) {
+        const vx_sba_plan* p = plans[r];
+        if (!p || p->c != c || p->shard_count != n || p->shard_rank != r)
+            return set_error(c, VX_ERR_INVALID, "shard %d: plan of another context or shard layout", r);
+        if (p->status != p0->status || p->nk != p0->nk || p->l_total != p0->l_total || p->n_blocks != p0->n_blocks ||
+            p->opt.max_iterations != p0->opt.max_iterations)
+            return set_error(c, VX_ERR_INVALID, "shard %d: plan built from another window", r);
+    }
+    if (p0->status != 0) {
+        for (int r = 0; r < n; ++r) plans[r]->ran = true;
+        return VX_OK;
+    }
+    std::vector<SbaRunCfg> cfg(n);
+    RedPtrs rp{};
+    int rc;
+    for (int r = 0; r < n; ++r) {
+        if ((rc = sba_prepare(c, plans[r], cfg[r]))) return rc;
+        rp.src[r] = plans[r]->red.as<double>();
+        rp.dst[r] = plans[r]->red_sum.as<double>();
+    }
+    const long long len = (long long)cfg[0].red_n;
+    for (int it = 0; it < p0->opt.max_iterations; ++it) {
+        for (int r = 0; r < n; ++r)
+            if ((rc = sba_assemble(c, plans[r], cfg[r], it))) return rc;
+        hipLaunchKernelGGL(k_sba_sum_shards, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, c->stream, rp, n, len);
+        VX_LAUNCH_CHECK(c, "k_sba_sum_shards");
+        for (int r = 0; r < n; ++r)
+            if ((rc = sba_solve_step(c, plans[r], cfg[r], it))) return rc;
+    }
+    for (int r = 0; r < n; ++r) plans[r]->ran = true;
     return VX_OK;
 }
 

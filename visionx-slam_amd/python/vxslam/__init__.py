@@ -91,7 +91,7 @@ EXPORTS = [
     "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run", "vx_ba_optimize_dmap",
-    "vx_ba_dmap_results", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
+    "vx_ba_dmap_results", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_shard_emulate_run", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
     "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run", "vx_seq_set_threads",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
     "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
@@ -643,6 +643,12 @@ class Context:
         return SBAPlan(self, m, opts, ref_kf_id, shard_rank, shard_count)
 
     # ---------------------------------------------------------------- multi-GPU
+    def sba_shard_emulate(self, plans):
+        """vx_sba_shard_emulate_run: the Schur shard plans run on this one device as the ranks of a
+        sharded Schur BA would, the all-reduce of the reduced system replaced by a rank-order sum."""
+        arr = (C.c_void_p * len(plans))(*[pl._h.value for pl in plans])
+        self._check(lib().vx_sba_shard_emulate_run(self._h, arr, len(plans)))
+
     def ba_shard_emulate(self, plans):
         """vx_ba_shard_emulate_run: the shard plans (rank r of len(plans)) run on this one device
         as the ranks of a sharded LocalBA would, the all-reduce replaced by a rank-order sum."""
