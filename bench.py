@@ -4,7 +4,7 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C3]
     torchrun --nproc-per-node N ... bench.py --gpus N ...
 
-One step = four rounds of the pipeline: F frames (F = 4 x the extraction contexts, 12 by default;
+One step = eight rounds of the pipeline: F frames (F = 8 x the extraction contexts, 24 by default;
 --frames-per-step), each through the hot path, everything resident in HBM before timing starts:
   1. ORBExtractor::Extract of a 640x480 BGR8 frame (n_features 2000 at C3)   -> slot i % 3
   2. ORBMatcher::Match(previous frame, this frame): BF Hamming kNN-2 + ratio -> matches
@@ -498,6 +498,31 @@ def cpu_baseline_mt(cfg, frames_host, ba_map, n_frames):
                       f"non-setup share {b_run / max(b_run + b_setup, 1e-12):.3f}; oracle/ C++ restatement"}
 
 
+# ----------------------------------------------------------------------------- host placement
+def idlest_cpus(n, window_s=0.3):
+    """The n logical CPUs of this process's affinity set with the least busy time over window_s
+    (/proc/stat deltas), or None where that is not readable."""
+    def snap():
+        d = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    v = [int(x) for x in line.split()[1:]]
+                    d[int(line.split()[0][3:])] = (sum(v), v[3] + v[4])  # (total, idle + iowait)
+        return d
+    try:
+        allowed = os.sched_getaffinity(0)
+        a = snap()
+        time.sleep(window_s)
+        b = snap()
+    except (OSError, AttributeError, ValueError):
+        return None
+    busy = {c: 1.0 - (b[c][1] - a[c][1]) / max(1, b[c][0] - a[c][0]) for c in b if c in a and c in allowed}
+    if len(busy) <= n:
+        return None
+    return sorted(sorted(busy, key=lambda c: busy[c])[:n])
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -532,12 +557,16 @@ def main():
                     help="extraction contexts (with --streams 3): frames alternate between them, so the "
                          "extraction of frame t+1 overlaps frame t's; Match and LocalBA stay in frame order")
     ap.add_argument("--frames-per-step", type=int, default=0,
-                    help="frames per timed step (default: four times the extraction contexts with --streams 3, "
-                         "i.e. four rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
+                    help="frames per timed step (default: eight times the extraction contexts with --streams 3, "
+                         "i.e. eight rounds of the pipeline, else 1); every frame runs Extract, Match and LocalBA")
     ap.add_argument("--seq-threads", type=int, default=1,
                     help="> 1: each context's recorded calls replayed on a host thread of its own (vx_seq_set_threads)")
     ap.add_argument("--no-seq", action="store_true",
                     help="timed steps through per-frame binding calls instead of one recorded vx_seq per step")
+    ap.add_argument("--pin-host", default="auto", choices=("auto", "off"),
+                    help="auto (one process): run on the 8 least-busy host CPUs, chosen before the GPU is "
+                         "initialised (the enqueueing thread and the HIP runtime's threads inherit them); the "
+                         "CPU baseline legs run on the whole affinity set again (DESIGN.md §17)")
     ap.add_argument("--match-ctx", default="extract", choices=("extract", "own"),
                     help="with --streams 3: Match(t) on frame t's extraction context right after Extract(t) "
                          "(default: one hardware queue fewer; measured 0.073 vs 0.073-0.076 ms/frame, steadier) "
@@ -549,6 +578,14 @@ def main():
             ap.error(f"--config: neither a workload ({', '.join(sorted(CONFIGS))}) nor a file: {args.config}")
         args.config_file, args.config = args.config, "C3"
 
+    # host placement (on a shared GPU host, unpinned runs fell into a mode where every
+    # HIP call cost 2-5x more; pinned to idle CPUs they did not)
+    full_affinity, host_cpus = None, None
+    if args.pin_host == "auto" and args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        host_cpus = idlest_cpus(8)
+        if host_cpus:
+            full_affinity = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, host_cpus)
     dist = Dist(args.gpus)
     import torch
 
@@ -741,12 +778,13 @@ def main():
         for c in ctxs:
             c.synchronize()
 
-    # One timed step = F frames, four rounds of the pipeline (F = 4 E by default): each of them runs
+    # One timed step = F frames, eight rounds of the pipeline (F = 8 E by default): each of them runs
     # Extract, Match and LocalBA.  With one frame per step the pipeline's fill (one frame's whole
-    # latency, ~0.19 ms at C3) weighed ~10 % in the driver's 20-step run; over 20 x 12 frames it is
-    # < 1 % (measured 20-step / 2000-step: 1.5-4.6 % with 12 frames, 1-6 % with 6, box noise ~2 %;
-    # scripts/gpu_r03_short_vs_long.sh)
-    F = args.frames_per_step if args.frames_per_step > 0 else (4 * E if args.streams == 3 else 1)
+    # latency, ~0.19 ms at C3) weighed ~10 % in the driver's 20-step run; measured 20-step / 2000-step:
+    # 1.5-4.6 % with 12 frames, 1-6 % with 6, box noise ~2 % (scripts/gpu_r03_short_vs_long.sh); 24
+    # frames against 12, alternating: 20-step runs 0.0688-0.0699 against 0.0694-0.0711 ms/frame,
+    # 2000-step runs the same (scripts/gpu_fps_ab.sh, profiles/r04/host/fps_ab.txt)
+    F = args.frames_per_step if args.frames_per_step > 0 else (8 * E if args.streams == 3 else 1)
 
     def fstep(i):
         for f in range(F):
@@ -888,6 +926,8 @@ def main():
             pass
 
     cpu = None
+    if full_affinity:  # (the CPU legs: every core this process may use, as before)
+        os.sched_setaffinity(0, full_affinity)
     if dist.rank == 0 and N == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfg, frames_host, ba_map, args.cpu_sample)
         cpu["multi_thread"] = cpu_baseline_mt(cfg, frames_host, ba_map, args.cpu_sample)
@@ -941,6 +981,7 @@ def main():
             # GPU pipeline cannot run faster than this
             "host_enqueue_ms_per_step": round(enqueue_ms, 4),
             "host_path": host_path,
+            "host_cpus": host_cpus,
             # untimed steps run before the warm-up so that every step of the timed region replays
             # captured graphs (see the pre-warm above)
             "prewarm_steps": prewarm,
