@@ -292,11 +292,16 @@ def timed_loop(step, steps, warmup, sync, dist):
 
     for i in range(warmup):
         step(i)
+    late = os.environ.get("VX_BENCH_GC_LATE") == "1"
+    if not late:  # (the collection overlaps the warm-up's tail on the device instead of idling it)
+        gc.collect()
+        gc.disable()
     sync()
     dist.barrier()
     sync()
-    gc.collect()
-    gc.disable()
+    if late:
+        gc.collect()
+        gc.disable()
     try:
         t0 = time.perf_counter()
         for i in range(steps):
