@@ -45,7 +45,11 @@ CONFIGS = {
     "C2": (480, 640, 1000, 10, 2000),
     "C3": (480, 640, 2000, 50, 20000),
     "C4": (960, 1280, 4000, 100, 50000),
+    # C5: 8 camera streams of 640x480 / 2000 ORB (per camera), one global 200 KF / 100k window
+    # solved by the Schur-complement BA (bench_c5 below)
+    "C5": (480, 640, 2000, 200, 100000),
 }
+C5_CAMERAS = 8
 
 
 def log(*a):
@@ -528,6 +532,267 @@ def idlest_cpus(n, window_s=0.3):
     return sorted(sorted(busy, key=lambda c: busy[c])[:n])
 
 
+# ----------------------------------------------------------------------------- config C5
+def sba_shard_result(m_after, lm_ids, rank, N, st, vxslam):
+    """What a rank's sharded Schur BA run left in its copy of the map (vx_sba_plan_fetch): every window
+    pose (all ranks solve all of them) and the positions of the landmarks of its shard."""
+    own = np.nonzero(np.array([vxslam.ba_shard_of(int(i), N) == rank for i in lm_ids]))[0] if N > 1 else \
+        np.arange(len(lm_ids))
+    return {"pose": np.asarray(m_after["kf_pose"]).reshape(-1, 7).copy(), "lm_idx": own.astype(np.int64),
+            "lm_pos": np.asarray(m_after["lm_pos"]).reshape(-1, 3)[own].copy(),
+            "iterations": int(st.iterations), "accepted": int(st.accepted),
+            "steps": [int(x) for x in list(st.step)[:int(st.iterations)]],
+            "cost": [float(x) for x in list(st.cost)[:int(st.iterations)]]}
+
+
+def sba_parity_vs_unsharded(shards, ref, tol=1e-4):
+    """The sharded Schur BA (one sba_shard_result per rank) against the unsharded run of the same
+    window: the same LM decisions (iterations, accepted, per-iteration step codes), costs to 1e-9, every
+    rank's poses bitwise equal (they solve from the same all-reduced system), poses and the landmark
+    shards' positions within tol relative (quaternion sign canonicalised), the shards a partition."""
+    def canon(q):
+        q = np.array(q, np.float64)
+        q[q[:, 3] < 0, :4] *= -1
+        return q
+
+    def rel(a, b):
+        return float((np.abs(a - b) / np.maximum(np.abs(b), 1e-3)).max()) if a.size else 0.0
+
+    idx = np.concatenate([s["lm_idx"] for s in shards])
+    partition = np.array_equal(np.sort(idx), ref["lm_idx"])
+    pos = np.concatenate([s["lm_pos"] for s in shards])
+    max_rel_lm = rel(pos[np.argsort(idx, kind="stable")], ref["lm_pos"]) if partition else float("inf")
+    ranks_agree = all(np.array_equal(s["pose"], shards[0]["pose"]) for s in shards)
+    max_rel_pose = max(rel(canon(s["pose"]), canon(ref["pose"])) for s in shards)
+    same_lm = all((s["iterations"], s["accepted"], s["steps"]) == (ref["iterations"], ref["accepted"], ref["steps"])
+                  for s in shards)
+    cost_rel = max((abs(a - b) / max(abs(b), 1e-30) for s in shards for a, b in zip(s["cost"], ref["cost"])),
+                   default=0.0)
+    out = {"max_rel_pose": max_rel_pose, "max_rel_landmark": max_rel_lm, "max_rel_cost": cost_rel,
+           "iterations": int(ref["iterations"]), "accepted": int(ref["accepted"]), "same_lm_decisions": bool(same_lm),
+           "shards_partition": bool(partition), "ranks_agree": bool(ranks_agree)}
+    out["ok"] = bool(partition and ranks_agree and same_lm and cost_rel <= 1e-9 and max_rel_pose <= tol
+                     and max_rel_lm <= tol)
+    return out
+
+
+def cpu_baseline_c5(frames_host, ba_map, opts_cpu, nf, rig_steps):
+    """The CPU restatement (oracle/, one thread) on a bounded sample of C5: per rig step the 8 cameras'
+    extract + match against the camera's previous frame and one Schur BA of the global window."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as O
+
+    O.build()
+    n = len(frames_host)
+    prev = [O.orb_extract(frames_host[(n - C5_CAMERAS + c) % n], nf)[1] for c in range(C5_CAMERAS)]
+    t_fe = t_ba = 0.0
+    for t in range(rig_steps):
+        t0 = time.perf_counter()
+        for c in range(C5_CAMERAS):
+            _, d = O.orb_extract(frames_host[(t * C5_CAMERAS + c) % n], nf)
+            O.match(prev[c], d)
+            prev[c] = d
+        t1 = time.perf_counter()
+        O.sba_optimize(ba_map.copy(), opts_cpu)
+        t_ba += time.perf_counter() - t1
+        t_fe += t1 - t0
+    per_frame = 1e3 * (t_fe + t_ba) / (rig_steps * C5_CAMERAS)
+    return {"value": round(per_frame, 3), "unit": "ms/frame", "cores": 1, "kind": "port", "host": host_cpu(),
+            "sample": f"{rig_steps} rig steps of C5 ({rig_steps * C5_CAMERAS} camera frames: extract + match "
+                      f"{1e3 * t_fe / rig_steps:.1f} ms and Schur BA {1e3 * t_ba / rig_steps:.1f} ms per rig step), "
+                      "oracle/ C++ restatement (sba_oracle.cpp: the same Schur system, dense Cholesky), 1 thread"}
+
+
+def bench_c5(args):
+    """BASELINE configs[4]: 8 camera streams of 640x480 BGR8 (2000 ORB each) on one rig, one global
+    window of 200 KF / 100k landmarks solved by the Schur-complement joint BA with the MFMA dense pose
+    solve (vx_sba_*).  The cameras are split over the N ranks (8 / N each); a
+    rig step is: batched extraction of the rank's cameras (one launch per kernel), batched matching
+    of each against its previous frame, then the Schur BA of the step, landmark-sharded over the
+    ranks with one RCCL all-reduce of the reduced pose system per LM iteration (sba.hip).  Frontend
+    and BA run on two contexts; BA(t) waits for Match(t), so the frontend of step t + 1 overlaps
+    BA(t).  One bench step = one rig step; value = elapsed / camera frames (ms/frame)."""
+    full_affinity, host_cpus = None, None
+    if args.pin_host == "auto" and args.gpus == 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        host_cpus = idlest_cpus(8)
+        if host_cpus:
+            full_affinity = os.sched_getaffinity(0)
+            os.sched_setaffinity(0, host_cpus)
+    dist = Dist(args.gpus)
+    import torch
+
+    import vxslam
+    from vxslam import synth
+
+    torch.cuda.set_device(dist.local_rank)
+    N, rank = dist.world, dist.rank
+    if C5_CAMERAS % N:
+        raise SystemExit(f"C5: {C5_CAMERAS} cameras do not split over {N} ranks")
+    cams = C5_CAMERAS // N
+    h, w, nf, nk, nl = CONFIGS["C5"]
+    front, back = vxslam.Context(dist.local_rank), vxslam.Context(dist.local_rank)
+    params = vxslam.default_orb_params(n_features=nf)
+    T = 4  # time steps cycled
+    # camera c of the rig at time step t: frame t * 8 + c of the rig's sequence; this rank's cameras
+    # are rank * cams .. rank * cams + cams - 1
+    rig_host = synth.make_frames(0xC5, T * C5_CAMERAS, h, w)
+    mine = [t * C5_CAMERAS + rank * cams + c for t in range(T) for c in range(cams)]
+    pool = torch.from_numpy(np.ascontiguousarray(rig_host[mine])).cuda()
+    m = synth.make_ba_map(0x5EED00C5, nk, nl, n_streams=C5_CAMERAS, n_old_kf=2 * C5_CAMERAS,
+                          cross_frac=args.c5_cross)
+    opts = vxslam.default_sba_options(window=nk, iters=args.c5_iters)
+    rccl = None
+    if N > 1:
+        uid = dist.broadcast_bytes(vxslam.Context.comm_unique_id() if rank == 0 else None)
+        back.comm_init(uid, N, rank)
+        nr, rk = back.comm_info()
+        infos = dist.gather((nr, rk))
+        rccl = {"nranks": nr, "world_size": N, "ranks": [list(x) for x in infos] if infos else None}
+        if nr != N or rk != rank:
+            raise SystemExit(f"rank {rank}: RCCL communicator reports {nr} ranks / rank {rk}")
+    plan = back.sba_plan(m, opts, shard_rank=rank, shard_count=N)
+    info = plan.info()
+    work = plan.factor_work()
+    parity = None
+    if N > 1:  # the sharded run against the unsharded one, before anything is timed
+        mine_r = []
+        for r in range(2):
+            ms = m.copy()
+            plan.run_async()
+            st_s = plan.fetch(ms)
+            mine_r.append(sba_shard_result(ms, m["lm_id"], rank, N, st_s, vxslam))
+        shards = dist.gather(mine_r)
+        if rank == 0:
+            mu = m.copy()
+            pu = back.sba_plan(mu, opts)
+            pu.run_async()
+            st_u = pu.fetch(mu)
+            pu.close()
+            ref = sba_shard_result(mu, m["lm_id"], 0, 1, st_u, vxslam)
+            parity = sba_parity_vs_unsharded([s[1] for s in shards], ref)
+            parity["first_run"] = sba_parity_vs_unsharded([s[0] for s in shards], ref)["ok"]
+            parity["ok"] = bool(parity["ok"] and parity["first_run"])
+            log(f"[bench C5] sharded vs unsharded Schur BA: {parity}")
+        sharded_parity_gate(parity, dist, args)
+    ev = front.event()
+
+    def extract(t):
+        bank, base = t % 2, (t % T) * cams
+        front.orb_extract_batch_async(pool[base].data_ptr(), cams, pool.stride(0), w, h, 3, pool.stride(1), bank,
+                                      params)
+
+    def step(t):
+        bank = t % 2
+        extract(t)
+        front.match_batch_async([(front.batch_device(1 - bank, c), front.batch_device(bank, c)) for c in range(cams)])
+        front.record(ev)
+        back.wait_event(ev)
+        plan.run_async()
+
+    def sync():
+        front.synchronize()
+        back.synchronize()
+
+    extract(-1)  # (bank 1: step 0's previous frames)
+    for t in range(6):  # pre-warm: graphs captured, plan buffers touched
+        step(t)
+    sync()
+    stages = {}
+    if not args.no_profile:
+        for c in (front, back):
+            c.prof_enable(True)
+        nw = max(args.warmup, 3)
+        for t in range(nw):
+            step(t)
+        sync()
+        prof = {}
+        for c in (front, back):
+            for k, v in c.prof_read(reset=True).items():
+                if v[1]:
+                    a, n = prof.get(k, (0.0, 0))
+                    prof[k] = (a + v[0], n + v[1])
+            c.prof_enable(False)
+        stages = {k: (v[0] / max(v[1], 1), v[1] / nw) for k, v in prof.items() if v[1]}
+    elapsed = timed_loop(step, args.steps, args.warmup, sync, dist)
+    st = plan.fetch(None)
+    lat = []
+    for t in range(5):
+        sync()
+        t0 = time.perf_counter()
+        step(args.steps + args.warmup + t)
+        sync()
+        lat.append(time.perf_counter() - t0)
+    frames_total = args.steps * C5_CAMERAS
+    value = 1e3 * elapsed / frames_total
+    # roofline of the dominant stage: the dense pose solve on MFMA (FP64 flops of the symbolic tile
+    # factorisation, vx_sba_plan_factor_work) or the Schur reduction (bytes of its W / Y gathers)
+    roofline = None
+    if stages:
+        dominant = max(stages, key=lambda k: stages[k][0] * stages[k][1])
+        ms_step = stages[dominant][0] * stages[dominant][1]
+        its = int(st.iterations)
+        steps_c = [int(x) for x in list(st.step)[:its]]
+        # factorisations per run: every iteration before the last that is not a rejection (the LM
+        # loop re-assembles without solving after a rejected step, sba_oracle.cpp)
+        n_fac = sum(1 for i in range(max(its - 1, 0)) if steps_c[i] != 0)
+        if dominant == "sba_solve" and n_fac:
+            tfs = work["flops"] * n_fac / (ms_step * 1e-3) / 1e12
+            roofline = {"kernel": "sba_solve", "hip_kernel": "k_sba_fac_step / k_sba_solve + k_sba_backsub",
+                        "bound": "mfma", "achieved": round(tfs, 4), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": round(tfs / FP64_PEAK_TFS, 6), "traffic": None,
+                        "flops_per_factorisation": int(work["flops"]), "factorisations_per_step": n_fac,
+                        "solve_ms_per_step": round(ms_step, 4), "factor_tiles": work,
+                        "note": "v_mfma_f64_16x16x4 tiles; the factor is a chain of dependent tile steps "
+                                "(latency-bound, DESIGN.md §18)"}
+        else:
+            roofline = {"kernel": dominant, "bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": None, "traffic": None, "stage_ms_per_step": round(ms_step, 4)}
+    cpu = None
+    if full_affinity:
+        os.sched_setaffinity(0, full_affinity)
+    if rank == 0 and N == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import pyoracle as O
+
+        oc = O.sba_options(window=nk, iters=args.c5_iters)
+        cpu = cpu_baseline_c5(rig_host, m, oc, nf, max(2, args.cpu_sample // 10))
+    if rank == 0:
+        for k, (ms, n) in sorted(stages.items(), key=lambda kv: -kv[1][0] * kv[1][1]):
+            log(f"[bench C5] stage {k:18s} {ms * 1e3:9.2f} us/launch x {n:6.2f} launches/step")
+        out = {
+            "metric": "ms/frame (feature-extract+match + BA solve), C5 rig: 8 x 640×480 cameras, 200 KF / 100k pts, "
+                      "Schur + MFMA dense pose solve",
+            "value": round(value, 4), "unit": "ms/frame", "n_gpus": N, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": False, "scaling": "strong",
+            "vs_baseline": None, "dtype": "u8/i32 (FAST, pyramid, BRIEF), f32 (Harris, blur, angle), f64 (BA)",
+            "data": "synthetic",
+            "config": {"workload": (f"C5: per step one rig step — {C5_CAMERAS} cameras x {w}x{h} BGR8 "
+                                    f"({cams} per rank: batched extract of {nf} ORB + batched kNN-2 match vs the "
+                                    f"camera's previous frame), then ONE Schur-complement BA (<= {args.c5_iters} LM "
+                                    f"iterations) of the global {nk} KF / {nl} landmark window "
+                                    f"({info['n_comp']} covisibility component(s), cross_frac {args.c5_cross}), "
+                                    f"landmark-sharded over {N} GPU(s)" +
+                                    (" with one RCCL all-reduce of the reduced pose system per iteration" if N > 1
+                                     else "")),
+                       "frames_per_step": C5_CAMERAS, "parallelism": f"cameras x{N} ranks; Schur BA: landmark shards x{N}",
+                       "ba_window_kf": nk, "ba_landmarks": nl, "orb_features": nf, "plan": info,
+                       "scaling": "strong"},
+            "ms_per_rig_step": round(1e3 * elapsed / args.steps, 4),
+            "latency_ms_per_rig_step": round(1e3 * float(np.median(lat)), 4),
+            "host_cpus": host_cpus, "parity_vs_unsharded": parity, "rccl": rccl,
+            "work_per_step": {"sba_iterations": int(st.iterations), "sba_accepted": int(st.accepted),
+                              "sba_initial_cost": float(st.initial_cost), "sba_final_cost": float(st.final_cost)},
+            "roofline": roofline, "cpu_baseline": cpu,
+            "stages_us": {k: round(v[0] * 1e3, 2) for k, v in stages.items()},
+        }
+        print(json.dumps(out), flush=True)
+    plan.close()
+    ev.close()
+    back.close()
+    front.close()
+    dist.close()
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -535,8 +800,18 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="C3",
-                    help="workload C2 / C3 / C4, or a key=value file with the reference's flag names "
+                    help="workload C2 / C3 / C4 / C5, or a key=value file with the reference's flag names "
                          "(apps/main.cpp --config; its ba_* keys set the LocalBA options below)")
+    ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
+                    help="N > 1: weak = per-rank work fixed (each rank its own camera stream, one global "
+                         "window of N x the config's keyframes / landmarks); strong = total work fixed (the "
+                         "config's window as BASELINE states it, landmark-sharded over the N ranks, the "
+                         "step's frames split over the ranks)")
+    ap.add_argument("--c5-cross", type=float, default=0.03,
+                    help="C5: share of landmarks seen by two neighbouring cameras of the rig (0.03: the 8 "
+                         "streams form ONE covisibility component, a 1188 x 1188 dense pose system; 0: 8 "
+                         "independent components)")
+    ap.add_argument("--c5-iters", type=int, default=8, help="C5: Schur BA Levenberg-Marquardt iterations")
     # the reference runner's LocalBA flags (apps/main.cpp:42-47, config/default.cfg), same names;
     # unset: the workload's values (window = the config's keyframes, the reference defaults otherwise)
     for k, typ in BA_FLAGS.items():
@@ -578,6 +853,8 @@ def main():
                          "or on a context of its own")
     args = ap.parse_args()
     args.config_file = None
+    if args.config == "C5":
+        return bench_c5(args)
     if args.config not in CONFIGS:
         if not os.path.isfile(args.config):
             ap.error(f"--config: neither a workload ({', '.join(sorted(CONFIGS))}) nor a file: {args.config}")
@@ -628,13 +905,16 @@ def main():
     cfg = CONFIGS[args.config]
     h, w, nf, nk, nl = cfg
     N = dist.world
+    # weak: the window grows with N (every rank adds its camera stream's keyframes and landmarks);
+    # strong: the config's window, its landmarks sharded over the N ranks
+    NW = N if args.scaling == "weak" else 1
 
     # ---- inputs resident in HBM before timing
     frames_host = synth.make_frames(0x5EED0000 + 31 * dist.rank + 3, args.frames, h, w)
     frames_dev = torch.from_numpy(frames_host).cuda()
     params = vxslam.default_orb_params(n_features=nf)
-    ba_map = synth.make_ba_map(0x5EED0003, nk * N, nl * N, n_streams=N, n_old_kf=2 * N)
-    ba_flags = resolve_ba_flags(args, nk * N)
+    ba_map = synth.make_ba_map(0x5EED0003, nk * NW, nl * NW, n_streams=NW, n_old_kf=2 * NW)
+    ba_flags = resolve_ba_flags(args, nk * NW)
     opts = vxslam.default_ba_options(window=ba_flags["ba_window_size"], iters=ba_flags["ba_iterations"],
                                      min_pose=ba_flags["ba_min_pose_observations"],
                                      min_point=ba_flags["ba_min_point_observations"],
@@ -740,7 +1020,8 @@ def main():
         if not args.diag_nodep:
             bctx.wait_event(ev_m[i % (4 * E)])
         if skip != "ba":
-            plan.run_async()
+            for _ in range(BA_PER_FRAME):
+                plan.run_async()
 
     # Host fast path of step(): the same C-ABI calls in the same order through pre-bound ctypes
     # functions, every argument object built once.  Through the wrappers the per-frame host enqueue
@@ -774,7 +1055,8 @@ def main():
             rc |= f_match(m, q[0], q[1], q[2], t[0], t[1], t[2], ratio)
             rc |= f_rec(m, evM[i % (4 * E)])
             rc |= f_wait(bh, evM[i % (4 * E)])
-            rc |= f_run(bh, ph)
+            for _ in range(BA_PER_FRAME):
+                rc |= f_run(bh, ph)
             if rc:
                 raise RuntimeError(f"frame {i}: a C-ABI call failed ({rc}): "
                                    f"{L.vx_last_error(x).decode()} {L.vx_last_error(bh).decode()}")
@@ -790,6 +1072,15 @@ def main():
     # frames against 12, alternating: 20-step runs 0.0688-0.0699 against 0.0694-0.0711 ms/frame,
     # 2000-step runs the same (scripts/gpu_fps_ab.sh, profiles/r04/host/fps_ab.txt)
     F = args.frames_per_step if args.frames_per_step > 0 else (8 * E if args.streams == 3 else 1)
+    # strong scaling: the step's F frames are split over the ranks (F / N each), and every frame's
+    # LocalBA is one joint run of all ranks (each over its landmark shard), so a rank runs the
+    # sharded window N times per local frame: per step F extractions / matches in all and F
+    # LocalBA runs, whatever N
+    BA_PER_FRAME = N if args.scaling == "strong" else 1
+    if args.scaling == "strong":
+        if F % N:
+            raise SystemExit(f"--scaling strong: {F} frames per step do not split over {N} ranks")
+        F //= N
 
     def fstep(i):
         for f in range(F):
@@ -821,7 +1112,8 @@ def main():
                 sq.match(mx, slot[loc(i - 1)], slot[loc(i)], 0.8)
                 sq.record(mx, ev_m[i % (4 * E)])
                 sq.wait(bctx, ev_m[i % (4 * E)])
-                sq.ba_run(bctx, plan)
+                for _ in range(BA_PER_FRAME):
+                    sq.ba_run(bctx, plan)
             if args.seq_threads > 1:
                 sq.set_threads(args.seq_threads)
             seqs.append(sq)
@@ -954,14 +1246,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": False,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "u8/i32 (FAST, pyramid, BRIEF), f32 (Harris, blur, angle), f64 (BA)",
             "data": "synthetic",
             "config": {
                 "workload": (f"{args.config}: per rank and step {F} {w}x{h} BGR8 frame(s), each: {nf} ORB, kNN-2 "
-                             f"Hamming match vs the previous frame, one LocalBA window of {nk * N} KF / {nl * N} "
-                             f"landmarks (<= 5 alternating iterations), landmark-sharded over {N} GPU(s)"),
+                             f"Hamming match vs the previous frame, then {BA_PER_FRAME} run(s) of one LocalBA window "
+                             f"of {nk * NW} KF / {nl * NW} landmarks (<= 5 alternating iterations), "
+                             f"landmark-sharded over {N} GPU(s)" +
+                             (f" ({args.scaling} scaling: {F * N} frames and {F * N} joint LocalBA runs per step "
+                              f"in all)" if N > 1 else "")),
+                "scaling": args.scaling,
                 "frames_per_step": F * N,
                 "parallelism": f"frames: 1 per rank; BA: landmark shards x{N}" + (" + RCCL all-reduce" if N > 1 else ""),
                 "streams": {1: "1: Extract, Match, LocalBA back to back",
@@ -971,8 +1267,8 @@ def main():
                                 if mon else f"{2 + E}: Extract x{E} (frames alternate) | Match | LocalBA")
                                + ", device events (LocalBA(t) after Match(t): Match and LocalBA in frame order; "
                                  "Extract(t) after the last Match reading its slot)"}[args.streams],
-                "ba_window_kf": nk * N,
-                "ba_landmarks": nl * N,
+                "ba_window_kf": nk * NW,
+                "ba_landmarks": nl * NW,
                 "orb_features": nf,
                 # LocalBA::Options of this run under the reference runner's flag names
                 # (apps/main.cpp:42-47; --config FILE / --ba_* flags)

@@ -395,6 +395,11 @@ int vx_ba_optimize_dmap(vx_ctx* ctx, vx_dmap* map, uint64_t ref_kf_id, int has_r
  * exceeds its cap (the counts are set either way). */
 int vx_ba_dmap_results(vx_ctx* ctx, vx_dmap* map, int cap_kf, int64_t* kf_rows, double* kf_pose7, int cap_lm,
                        int64_t* lm_rows, double* lm_pos3, int* n_kf, int* n_lm);
+/* on != 0: every following vx_ba_optimize_dmap also copies its results (both pose buffers, the
+ * optimised positions and their rows, sized by the call's capacities) into pinned host memory before
+ * its one synchronisation, so vx_ba_dmap_results then only copies on the host — no device call, no
+ * second synchronisation (what a drop-in that writes every result back wants; default off). */
+int vx_dmap_prefetch_results(vx_dmap* map, int on);
 
 /* ---------------------------------------------------------------- Schur-complement joint BA
  * NOT a reference entry point: the reference's LocalBA alternates per-keyframe and per-landmark
@@ -439,6 +444,11 @@ void vx_sba_plan_destroy(vx_sba_plan* plan);
 /* out8 = {n_kf, n_opt (local landmarks), n_obs, n_pairs, n_blocks, n (= 6 n_kf), nonzero 16x16
  * tiles of the Cholesky factors (symbolic factorisation, rhs row included), n_components} */
 int vx_sba_plan_info(const vx_sba_plan* plan, int64_t* out8);
+/* The dense pose solve's symbolic work (all components; the rhs row's tiles left out): out4 =
+ * {nonzero tiles of L, trailing-update tile products (16x16x16 each), diagonal tiles (one POTRF
+ * each), off-diagonal panel tiles (one TRSM each)} -> algorithmic FP64 flops of one factorisation
+ * 2*16^3 * updates + 16^3 * panel + 16^3/3 * diagonal (bench.py's MFMA roofline for config C5). */
+int vx_sba_plan_factor_work(const vx_sba_plan* plan, int64_t* out4);
 /* The reduced system of the LAST assembly of the last run (S row-major n x n, lower triangle
  * meaningful, damping included; rhs n), for verification against the restatement. */
 int vx_sba_plan_system(vx_ctx* ctx, vx_sba_plan* plan, double* S, double* rhs, int n);

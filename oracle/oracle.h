@@ -162,6 +162,14 @@ int orc_sba_optimize_map(orc_map_view* map, uint64_t ref_kf_id, int has_ref,
  * assembled at the map's current state with damping `lambda`; n = 6 * window keyframes. */
 int orc_sba_system(const orc_map_view* map, uint64_t ref_kf_id, int has_ref,
                    const orc_sba_options* opt, double lambda, double* S, double* rhs, int n);
+/* One landmark shard's partial reduced system (csrc/sba.hip's sharded run before its ncclAllReduce):
+ * the observations of landmarks with splitmix64(id) mod shard_count == shard_rank only, without the
+ * pose damping and the fixed-keyframe gauge; HTd (n) = the shard's pose-block diagonals,
+ * cost_count = {cost, valid observations}.  Summed over the ranks and finished (damping, gauge) it is
+ * orc_sba_system's system. */
+int orc_sba_system_shard(const orc_map_view* map, uint64_t ref_kf_id, int has_ref, const orc_sba_options* opt,
+                         double lambda, int shard_rank, int shard_count, double* S, double* rhs, double* HTd,
+                         double* cost_count, int n);
 
 /* ---- keyframe-insertion landmark creation (landmark_oracle.cpp), same contract as vx_slam.h */
 int orc_depth_landmarks(const double* feat_uv, const uint8_t* feat_has_lm, int n_feat, const void* depth,

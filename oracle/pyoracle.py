@@ -317,6 +317,25 @@ def sba_system(m, opts=None, lam=None, ref_kf_id=None):
     return S, rhs
 
 
+def sba_system_shard(m, shard_rank, shard_count, opts=None, lam=None, ref_kf_id=None):
+    """One landmark shard's partial reduced system before the all-reduce (no pose damping, no gauge):
+    (S_part, rhs_part, pose-block diagonals, cost, valid observations), or None on an early return."""
+    if opts is None:
+        opts = sba_options(window=m.get("window", 5))
+    lam = opts.lambda_init if lam is None else lam
+    v = map_view(m)
+    ref, has_ref = _ref(m, ref_kf_id)
+    nk = min(int(opts.window_size), m.n_kf)
+    n = 6 * nk
+    S, rhs, htd, cc = np.zeros((n, n)), np.zeros(n), np.zeros(n), np.zeros(2)
+    rc = lib().orc_sba_system_shard(C.byref(v), ref, has_ref, C.byref(opts), C.c_double(lam), int(shard_rank),
+                                    int(shard_count), _p(S), _p(rhs), _p(htd), _p(cc), n)
+    if rc == 1:
+        return None
+    assert rc == 0, rc
+    return S, rhs, htd, float(cc[0]), int(cc[1])
+
+
 # ---------------------------------------------------------------------------- landmark creation
 DEPTH_TYPES = {np.dtype(np.uint16): 0, np.dtype(np.float32): 1, np.dtype(np.float64): 2}
 

@@ -152,8 +152,20 @@ struct System {
 
 // One assembly at state X with damping lambda: cost, reduced pose system S x = rhs and the
 // per-landmark / per-observation blocks the back-substitution needs.
+// Sharded form (shard_count > 1, csrc/sba.hip): only the observations of this rank's landmarks
+// (splitmix64(landmark id) mod shard_count == shard_rank, optimised and fixed alike) are assembled,
+// and with finish = false the pose damping and the fixed-keyframe gauge are left out — they are
+// applied once after the all-reduce of the ranks' partial systems; HTd (n) then receives this
+// shard's pose-block diagonals, which that damping needs summed over the ranks too.
+inline uint64_t splitmix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
 void assemble(const orc_map_view* m, const Problem& P, const orc_sba_options* o, const State& X, double lambda,
-              System& sys) {
+              System& sys, int shard_rank = 0, int shard_count = 1, bool finish = true, double* HTd = nullptr) {
     const int nk = P.nk, n = 6 * nk;
     const int n_opt = (int)P.opt.size();
     const int n_oo = P.lm_ptr[n_opt];
@@ -173,6 +185,7 @@ void assemble(const orc_map_view* m, const Problem& P, const orc_sba_options* o,
     const double rho_gate = me <= delta ? me * me : 2.0 * delta * me - delta * delta;
     for (int i = 0; i < (int)P.obs.size(); ++i) {
         const Obs& ob = P.obs[i];
+        if (shard_count > 1 && (int)(splitmix64(m->lm_id[ob.lm]) % (uint64_t)shard_count) != shard_rank) continue;
         const int k = P.win[ob.kf];
         const double* ci = m->kf_intr + 4 * k;
         const Cam cam{ci[0], ci[1], ci[2], ci[3]};
@@ -261,6 +274,10 @@ void assemble(const orc_map_view* m, const Problem& P, const orc_sba_options* o,
                             Y1[3 * a] * W2[3 * b] + Y1[3 * a + 1] * W2[3 * b + 1] + Y1[3 * a + 2] * W2[3 * b + 2];
             }
         }
+    if (HTd)
+        for (int r = 0; r < nk; ++r)
+            for (int a = 0; a < 6; ++a) HTd[6 * r + a] = HT[36 * r + 7 * a];
+    if (!finish) return;
     // pose damping and the gauge: fixed keyframes get identity rows / columns and rhs 0
     for (int r = 0; r < nk; ++r) {
         if (P.fixed[r]) {
@@ -330,6 +347,22 @@ extern "C" int orc_sba_system(const orc_map_view* m, uint64_t ref, int has_ref, 
     assemble(m, P, o, initial_state(m, P), lambda, sys);
     for (size_t i = 0; i < sys.S.size(); ++i) S[i] = sys.S[i];
     for (int i = 0; i < n; ++i) rhs[i] = sys.rhs[i];
+    return 0;
+}
+
+extern "C" int orc_sba_system_shard(const orc_map_view* m, uint64_t ref, int has_ref, const orc_sba_options* o,
+                                    double lambda, int shard_rank, int shard_count, double* S, double* rhs,
+                                    double* HTd, double* cost_count, int n) {
+    Problem P;
+    build(m, ref, has_ref, o, P);
+    if (P.status != 0) return 1;
+    if (n != 6 * P.nk || shard_count < 1 || shard_rank < 0 || shard_rank >= shard_count) return -1;
+    System sys;
+    assemble(m, P, o, initial_state(m, P), lambda, sys, shard_rank, shard_count, false, HTd);
+    for (size_t i = 0; i < sys.S.size(); ++i) S[i] = sys.S[i];
+    for (int i = 0; i < n; ++i) rhs[i] = sys.rhs[i];
+    cost_count[0] = sys.cost;
+    cost_count[1] = sys.count;
     return 0;
 }
 

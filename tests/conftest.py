@@ -42,3 +42,11 @@ def ctx():
     c = vxslam.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture
+def slot_sums(monkeypatch):
+    """The fused LocalBA with its per-keyframe partial slots (VX_BA_ATOMIC_ROWS=0, read at plan
+    build) instead of the default row sums by float atomics: every run bitwise the same, for the
+    tests that compare two runs (or two plan builds) bit for bit."""
+    monkeypatch.setenv("VX_BA_ATOMIC_ROWS", "0")

@@ -8,6 +8,7 @@
 //   adapter_driver ba_calls <dir> <window> <iters> <ref_id or -1> <reps> resident|snapshot
 //                  (LocalBA::Optimize with a DeviceMap attached, or on the snapshot path; the first
 //                  call dumped like `ba`, then the median ms of `reps` further calls)
+//   adapter_driver flatten_time <dir> <window> <reps>   (LocalBA::Flatten alone: median ms, host only)
 //   adapter_driver depth <dir>                     (KeyFrameLandmarks::CreateLandmarksFromDepth)
 //   adapter_driver triangulate <dir> <min_deg> <max_err>   (TriangulateWithLastKeyFrame)
 //   adapter_driver pnp <dir> <iterations> <reproj_err>    (solvePnPRansac as TrackWithPnP calls it)
@@ -231,6 +232,25 @@ static int cmd_ba_calls(char** a) {
     return 0;
 }
 
+// LocalBA::Flatten alone (the snapshot path's host gather, no device): median ms of `reps` calls
+static int cmd_flatten_time(char** a) {
+    const std::string dir = a[0];
+    const int window = std::atoi(a[1]), reps = std::atoi(a[2]);
+    BaInput in = build_map(dir);
+    std::vector<double> ms;
+    size_t n_lm = 0;
+    FlatMap f;  // (reused, as LocalBA::Optimize's snapshot path reuses its own)
+    for (int r = 0; r < reps; ++r) {
+        const auto t0 = std::chrono::steady_clock::now();
+        LocalBA::Flatten(*in.map, nullptr, window, f);
+        ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+        n_lm = f.lm_id.size();
+    }
+    std::sort(ms.begin(), ms.end());
+    std::printf("%zu %.4f\n", n_lm, ms[ms.size() / 2]);
+    return 0;
+}
+
 static BaInput build_map(const std::string& dir) {
     auto rd64 = [&](const char* n) { return read_bin<uint64_t>(dir + "/" + n + ".bin"); };
     auto rdd = [&](const char* n) { return read_bin<double>(dir + "/" + n + ".bin"); };
@@ -426,6 +446,7 @@ int main(int argc, char** argv) {
         if (cmd == "match" && argc >= 7) return cmd_match(argv + 2);
         if (cmd == "ba" && argc >= 6) return cmd_ba(argc - 2, argv + 2);
         if (cmd == "ba_calls" && argc >= 8) return cmd_ba_calls(argv + 2);
+        if (cmd == "flatten_time" && argc >= 5) return cmd_flatten_time(argv + 2);
         if (cmd == "depth" && argc >= 3) return cmd_depth(argv + 2);
         if (cmd == "triangulate" && argc >= 5) return cmd_triangulate(argv + 2);
         if (cmd == "pnp" && argc >= 5) return cmd_pnp(argv + 2);

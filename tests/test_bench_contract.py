@@ -103,3 +103,67 @@ def test_ba_flags_reference_names(tmp_path):
                        timeout=120)
     for k in bench.BA_FLAGS:
         assert f"--{k}" in r.stdout
+
+
+def _json_line(args):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_c4_strong_scaling_line():
+    """--config C4 --scaling strong: BASELINE configs[3]'s fixed 100 KF / 50k window (at N = 1 the
+    same work as the default C4 line), the mode echoed in the line."""
+    d = _json_line(["--config", "C4", "--scaling", "strong", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
+    assert d["scaling"] == "strong" and d["config"]["scaling"] == "strong"
+    assert d["config"]["ba_window_kf"] == 100 and d["config"]["ba_landmarks"] == 50000
+    assert d["config"]["workload"].startswith("C4") and d["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_c5_line():
+    """--config C5: 8 cameras + the Schur BA of the 200 KF / 100k window; the MFMA roofline of the dense
+    pose solve (FP64 flops of the symbolic tile factorisation) when it dominates."""
+    d = _json_line(["--config", "C5", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"])
+    assert d["config"]["workload"].startswith("C5") and d["config"]["frames_per_step"] == 8
+    assert d["config"]["ba_window_kf"] == 200 and d["config"]["ba_landmarks"] == 100000
+    assert d["unit"] == "ms/frame" and d["value"] > 0 and d["work_per_step"]["sba_iterations"] >= 2
+    rf = d["roofline"]
+    assert rf is not None
+    if rf["bound"] == "mfma":
+        assert rf["unit"] == "TFLOP/s" and 0 < rf["frac"] < 1 and rf["flops_per_factorisation"] > 0
+
+
+def test_sba_parity_field_logic():
+    """bench.py's C5 N > 1 gate on made-up shard results: a correct split passes; a shard off by
+    1e-3, a missing landmark, ranks disagreeing bitwise or a different LM decision fail."""
+    import numpy as np
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    rng = np.random.default_rng(3)
+    pose = rng.normal(size=(6, 7))
+    pos = rng.normal(size=(10, 3)) + 5
+    ref = {"pose": pose, "lm_idx": np.arange(10), "lm_pos": pos, "iterations": 4, "accepted": 3,
+           "steps": [2, 1, 1, 0], "cost": [10.0, 8.0, 7.0, 7.5]}
+    own = [np.array([0, 2, 4, 6, 8]), np.array([1, 3, 5, 7, 9])]
+    shards = [dict(ref, lm_idx=o, lm_pos=pos[o]) for o in own]
+    assert bench.sba_parity_vs_unsharded(shards, ref)["ok"]
+    bad = [dict(s) for s in shards]
+    bad[1]["lm_pos"] = bad[1]["lm_pos"] * (1 + 1e-3)
+    assert not bench.sba_parity_vs_unsharded(bad, ref)["ok"]
+    bad = [dict(s) for s in shards]
+    bad[0]["lm_idx"], bad[0]["lm_pos"] = bad[0]["lm_idx"][1:], bad[0]["lm_pos"][1:]
+    assert not bench.sba_parity_vs_unsharded(bad, ref)["shards_partition"]
+    bad = [dict(s) for s in shards]
+    bad[1]["pose"] = pose.copy()
+    bad[1]["pose"][0, 4] += 1e-12
+    assert not bench.sba_parity_vs_unsharded(bad, ref)["ranks_agree"]
+    bad = [dict(s) for s in shards]
+    bad[0]["steps"] = [2, 1, 0, 0]
+    assert not bench.sba_parity_vs_unsharded(bad, ref)["same_lm_decisions"]

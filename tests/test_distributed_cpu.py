@@ -214,3 +214,55 @@ def _gate_worker(rank, world, port):
 
 def test_bench_parity_gate_failing_branch():
     _spawn(_gate_worker)
+
+
+def _sba_shard_worker(rank, world, port):
+    """The Schur-complement BA's sharded reduction (csrc/sba.hip: every rank assembles the reduced
+    pose system from its own landmark shard, one ncclAllReduce sums the ranks' systems, damping and
+    the fixed-keyframe gauge are applied once after it) with gloo standing in for RCCL: the partial
+    systems of the restatement, all-reduced and finished, equal its unsharded system."""
+    dist = _init(rank, world, port)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+
+    import pyoracle as O
+    from vxslam import synth
+
+    nk = 8
+    m = synth.make_ba_map(29, nk, 1500, n_streams=2, n_old_kf=4)
+    opts = O.sba_options(window=nk, iters=4)
+    lam = 3e-3
+    S, rhs, htd, cost, cnt = O.sba_system_shard(m, rank, world, opts, lam)
+    # every observation belongs to exactly one shard, so no rank holds everything
+    full = O.sba_system_shard(m, 0, 1, opts, lam)
+    assert 0 < cnt < full[4]
+    buf = torch.from_numpy(np.concatenate([S.ravel(), rhs, htd, [cost, cnt]]))
+    dist.all_reduce(buf)  # (the GPU: one ncclAllReduce(sum, f64) of the same blocks per LM iteration)
+    n = 6 * nk
+    b = buf.numpy()
+    Ss, rs, hs = b[: n * n].reshape(n, n).copy(), b[n * n: n * n + n].copy(), b[n * n + n: n * n + 2 * n]
+    assert int(round(b[-1])) == full[4] and abs(b[-2] - full[3]) <= 1e-9 * full[3]
+    # finish once, after the reduction: fixed rows (the oldest fixed_keyframes window rows; every synth
+    # keyframe has a camera) get the identity and rhs 0, the free rows the Marquardt damping
+    for r in range(nk):
+        sl = slice(6 * r, 6 * r + 6)
+        if r < opts.fixed_keyframes:
+            Ss[sl, :] = 0.0
+            Ss[:, sl] = 0.0
+            Ss[sl, sl] = np.eye(6)
+            rs[sl] = 0.0
+        else:
+            Ss[sl, sl] += np.diag(lam * hs[sl] + 1e-6)
+    Sref, rref = O.sba_system(m, opts, lam)
+    tol = 1e-9 * np.abs(Sref).max()
+    assert np.abs(np.tril(Ss) - np.tril(Sref)).max() <= tol
+    assert np.abs(rs - rref).max() <= 1e-9 * np.abs(rref).max()
+    # the shards' landmark sets partition the window's: the rank totals of valid observations add up
+    counts = torch.tensor([cnt], dtype=torch.int64)
+    dist.all_reduce(counts)
+    assert int(counts.item()) == full[4]
+    dist.destroy_process_group()
+
+
+def test_sharded_schur_system_allreduce():
+    _spawn(_sba_shard_worker)

@@ -26,7 +26,7 @@ def _run(plan):
 
 
 @pytest.mark.parametrize("cfg", [("C2", 10, 2000, 1), ("C3", 50, 20000, 1), ("C5s", 40, 8000, 4)])
-def test_dmap_plan_equals_snapshot_plan(ctx, cfg):
+def test_dmap_plan_equals_snapshot_plan(ctx, cfg, slot_sums):
     name, nk, nl, ns = cfg
     m = synth.make_ba_map(0xD0 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
     dm = vxslam.DMap(ctx)
@@ -94,7 +94,7 @@ class _Mirror:
         return sub
 
 
-def test_dmap_incremental_updates(ctx):
+def test_dmap_incremental_updates(ctx, slot_sums):
     """Keyframes arrive one by one with plans in between; feature / bad-flag / pose edits go to
     both representations; every plan equals the snapshot plan of the map as it stands."""
     m = synth.make_ba_map(0xD7, 12, 3000, n_old_kf=2)
@@ -157,7 +157,7 @@ def test_dmap_errors(ctx):
 
 
 @pytest.mark.parametrize("compact", [False, True], ids=["tombstones", "compacted"])
-def test_dmap_culling_and_reobservation(ctx, monkeypatch, compact):
+def test_dmap_culling_and_reobservation(ctx, monkeypatch, compact, slot_sums):
     """The map edits of culling and re-association (tracking.cpp:652-773, landmark.h:32-40,
     map.cpp:15-23) on the resident map: Tracking::RemoveKeyFrame of a window keyframe
     (RemoveObservation of each of its landmarks + feature reset + Map::RemoveKeyFrame),
@@ -338,8 +338,9 @@ def _assert_close(pose_g, pos_g, pose_c, pos_c, st_g, st_c):
 def _oracle_on(oracle, m2, opts_kw, ref):
     mc = m2.copy()
     st = oracle.ba_optimize(mc, oracle.ba_options(**opts_kw), ref_kf_id=ref)
-    if st.status == 0 and st.gate_margin < 1e-8:
-        pytest.skip(f"gate margin {st.gate_margin} too small for a stable comparison")
+    # a BASELINE config must never drop out of the comparison silently: a fixed seed whose residuals
+    # come within 1e-8 of the 5 px gate fails here (reseed the case) instead of being skipped
+    assert st.status != 0 or st.gate_margin >= 1e-8, f"gate margin {st.gate_margin}: reseed this case"
     return mc, st
 
 
@@ -477,3 +478,59 @@ def test_dmap_optimize_edges(ctx):
     st = dm.optimize(vxslam.default_ba_options(window=5, iters=2))
     assert st.status == 1 and st.n_window_kf == 2 and st.n_landmarks == 0
     dm.close()
+
+
+def test_dmap_results_invalidated_by_sba_plan(ctx, oracle):
+    """a Schur plan built from the resident map reuses the lean build's scratch, so a
+    LocalBA result from before it is no longer reported (VX_ERR_STATE) instead of naming rows of
+    the Schur build; the next vx_ba_optimize_dmap reports again, against the restatement."""
+    m = synth.make_ba_map(0xE3, 10, 2000, n_old_kf=2)
+    kw = dict(window=10, iters=3)
+    dm = vxslam.DMap(ctx)
+    kf_order, lm_order = vxslam.dmap_load(dm, m)
+    m2 = vxslam.map_reorder(m, kf_order, lm_order)
+    st = dm.optimize(vxslam.default_ba_options(**kw), ref_kf_id=m["ref_kf_id"])
+    assert st.status == 0
+    kr, kp, lr, lp = dm.results()
+    assert len(lr) == st.n_landmarks
+    sp = dm.sba_plan(vxslam.default_sba_options(window=10, iters=2), ref_kf_id=m["ref_kf_id"])
+    with pytest.raises(vxslam.VxError):
+        dm.results()
+    sp.close()
+    # the next LocalBA call (from the scattered state) reports again and matches the restatement
+    pose, pos = dm.download()
+    m2["kf_pose"], m2["lm_pos"] = pose.copy(), pos.copy()
+    st2 = dm.optimize(vxslam.default_ba_options(**kw), ref_kf_id=m["ref_kf_id"])
+    mc, sc = _oracle_on(oracle, m2, kw, m["ref_kf_id"])
+    pose, pos = dm.download()
+    _assert_close(pose, pos, mc["kf_pose"].reshape(-1, 7), mc["lm_pos"].reshape(-1, 3), st2, sc)
+    kr, kp, lr, lp = dm.results()
+    assert np.array_equal(kp, pose[kr]) and np.array_equal(lp, pos[lr])
+    dm.close()
+
+
+def test_dmap_prefetched_results_equal(ctx):
+    """vx_dmap_prefetch_results: the results copied back with the optimize call's own synchronisation
+    are the ones vx_ba_dmap_results reads from the device otherwise (the lean build is deterministic:
+    two maps loaded alike give bitwise-equal runs), call after call, and a Schur plan build on the map
+    still invalidates them."""
+    m = synth.make_ba_map(0xE5, 12, 2500, n_old_kf=2)
+    kw = dict(window=12, iters=4)
+    maps = [vxslam.DMap(ctx), vxslam.DMap(ctx)]
+    for d in maps:
+        vxslam.dmap_load(d, m)
+    maps[1].prefetch_results(True)
+    for _ in range(2):
+        out = []
+        for d in maps:
+            st = d.optimize(vxslam.default_ba_options(**kw), ref_kf_id=m["ref_kf_id"])
+            assert st.status == 0
+            out.append(d.results())
+        for a, b in zip(*out):
+            assert np.array_equal(a, b)
+    sp = maps[1].sba_plan(vxslam.default_sba_options(window=12, iters=2), ref_kf_id=m["ref_kf_id"])
+    with pytest.raises(vxslam.VxError):
+        maps[1].results()
+    sp.close()
+    for d in maps:
+        d.close()

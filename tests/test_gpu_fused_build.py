@@ -40,7 +40,7 @@ def _check_equal(ctx, m, opts, run=True, **kw):
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
-def test_device_layout_equals_host_packing(ctx, cfg):
+def test_device_layout_equals_host_packing(ctx, cfg, slot_sums):
     nk, nl, _ = synth.ba_config(cfg)
     m = synth.make_ba_map(0x5EED0003, nk, nl)
     lay = _check_equal(ctx, m, vxslam.default_ba_options(window=nk))
@@ -49,19 +49,19 @@ def test_device_layout_equals_host_packing(ctx, cfg):
 
 
 @pytest.mark.parametrize("nk,nl,streams", [(100, 30000, 4), (200, 50000, 8), (440, 60000, 8)])
-def test_device_layout_wide_windows(ctx, nk, nl, streams):
+def test_device_layout_wide_windows(ctx, nk, nl, streams, slot_sums):
     m = synth.make_ba_map(0x5EED0100 + nk, nk, nl, n_streams=streams, n_old_kf=2 * streams)
     _check_equal(ctx, m, vxslam.default_ba_options(window=nk), run=nk <= 200)
 
 
-def test_device_layout_narrow_cap(ctx, monkeypatch):
+def test_device_layout_narrow_cap(ctx, monkeypatch, slot_sums):
     monkeypatch.setenv("VX_BA_FUSED_CAP", "96")
     m = synth.make_ba_map(0x5EED0004, 50, 20000)
     lay = _check_equal(ctx, m, vxslam.default_ba_options(window=50))
     assert lay["workgroups"] > 500
 
 
-def test_device_layout_untouched_keyframe(ctx):
+def test_device_layout_untouched_keyframe(ctx, slot_sums):
     """A window keyframe without features (no pose- or landmark-stage observation): no workgroup
     touches it, so workgroup 0 owns it with an empty entry."""
     m = synth.make_ba_map(0x5EED0005, 12, 3000)

@@ -235,8 +235,9 @@ def _ba_case(ctx, oracle, m, opts_kw, ref=None):
 
     mc = m.copy()
     st_c = oracle.ba_optimize(mc, oracle.ba_options(**opts_kw), ref_kf_id=ref)
-    if st_c.status == 0 and st_c.gate_margin < 1e-8:
-        pytest.skip(f"gate margin {st_c.gate_margin} too small for a stable comparison")
+    # never skipped: a fixed seed whose residuals come within 1e-8 of the gate fails (reseed the case),
+    # so no BASELINE config can drop out of the comparison silently
+    assert st_c.status != 0 or st_c.gate_margin >= 1e-8, f"gate margin {st_c.gate_margin}: reseed this case"
     mg = m.copy()
     st_g = ctx.ba_optimize(mg, vxslam.default_ba_options(**opts_kw), ref_kf_id=ref)
     _assert_ba_close(mg, mc, st_g, st_c)
@@ -296,8 +297,7 @@ def test_ba_large_windows(ctx, oracle, nk, nl, ns, global_poses):
     m = synth.make_ba_map(0x5EED0100 + nk, nk, nl, n_streams=ns, n_old_kf=2 * ns)
     mc = m.copy()
     st_c = oracle.ba_optimize(mc, oracle.ba_options(window=nk))
-    if st_c.gate_margin < 1e-8:
-        pytest.skip(f"gate margin {st_c.gate_margin} too small for a stable comparison")
+    assert st_c.gate_margin >= 1e-8, f"gate margin {st_c.gate_margin}: reseed this case"  # (never skipped)
     plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk), global_poses=global_poses)
     plan.run_async()
     mg = m.copy()
@@ -307,20 +307,40 @@ def test_ba_large_windows(ctx, oracle, nk, nl, ns, global_poses):
     _assert_ba_close(mg, mc, st_g, st_c)
 
 
-def test_ba_plan_is_repeatable(ctx, oracle):
+def _runs_agree(a, b, sa, sb, bitwise):
+    """Two LocalBA runs of one plan: the same iterations and per-iteration observation counts, and
+    bitwise-equal results (partial slots) or equal to rounding (row sums by float atomics, whose sum
+    order is the atomics' arrival order).  The reference's step sign (b = -J^T e, local_ba.cpp:156,224)
+    makes the iteration expand differences, so last-bit sum differences reach ~1e-8 relative in the
+    positions after five iterations (measured 6e-9 at C3): the bound is 1e-6, two decades under the
+    parity tolerance."""
+    assert (sa.iterations, list(sa.obs[:16])) == (sb.iterations, list(sb.obs[:16]))
+    if bitwise:
+        assert np.array_equal(a["kf_pose"], b["kf_pose"]) and np.array_equal(a["lm_pos"], b["lm_pos"])
+        assert list(sa.cost[:16]) == list(sb.cost[:16])
+        return
+    for x, y in ((a["kf_pose"], b["kf_pose"]), (a["lm_pos"], b["lm_pos"])):
+        assert (np.abs(x - y) / np.maximum(np.abs(y), 1e-3)).max() <= 1e-6
+    for x, y in zip(sa.cost[:sa.iterations], sb.cost[:sb.iterations]):
+        assert abs(x - y) <= 1e-9 * abs(y)
+
+
+@pytest.mark.parametrize("sums", ["atomic", "slots"])
+def test_ba_plan_is_repeatable(ctx, oracle, monkeypatch, sums):
     import vxslam
 
+    monkeypatch.setenv("VX_BA_ATOMIC_ROWS", "1" if sums == "atomic" else "0")
     nk, nl, ns = synth.ba_config("C3")
     m = synth.make_ba_map(77, nk, nl)
     plan = ctx.ba_plan(m, vxslam.default_ba_options(window=nk))
-    outs = []
+    outs, sts = [], []
     for _ in range(3):
         plan.run_async()
         mm = m.copy()
-        plan.fetch(mm)
+        sts.append(plan.fetch(mm))
         outs.append(mm)
-    for o in outs[1:]:
-        assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
+    for o, s in zip(outs[1:], sts[1:]):
+        _runs_agree(o, outs[0], s, sts[0], bitwise=sums == "slots")
     info = plan.info()
     assert info["n_kf"] == nk and info["n_pose_obs"] > 50000
 
@@ -384,12 +404,14 @@ def test_frontend_backend_contexts_overlap(ctx, oracle):
         mctx.close()
 
 
-def test_graph_replay_matches_eager(ctx, oracle):
+@pytest.mark.parametrize("sums", ["atomic", "slots"])
+def test_graph_replay_matches_eager(ctx, oracle, monkeypatch, sums):
     """The async entry points replay hipGraphs after their second identical call: results of
     replayed extraction / matching / LocalBA runs equal the eager path and the restatement."""
     import torch
     import vxslam
 
+    monkeypatch.setenv("VX_BA_ATOMIC_ROWS", "1" if sums == "atomic" else "0")
     c = vxslam.Context(0)
     try:
         frames = synth.make_frames(0x5EED0077, 2, 480, 640)
@@ -399,7 +421,7 @@ def test_graph_replay_matches_eager(ctx, oracle):
         nk, nl, _ = synth.ba_config("C2")
         m = synth.make_ba_map(91, nk, nl)
         plan = c.ba_plan(m, vxslam.default_ba_options(window=nk))
-        outs = []
+        outs, sts = [], []
         for rep in range(4):  # rep 0 eager, rep 1 captured, reps 2-3 replayed
             for s in range(2):
                 c.orb_extract_async(d[s].data_ptr(), 640, 480, 3, 640 * 3, s, p)
@@ -412,10 +434,10 @@ def test_graph_replay_matches_eager(ctx, oracle):
                 _assert_orb_equal(*c.orb_fetch(s), *kc[s])
             assert np.array_equal(c.match_fetch(), oracle.match(kc[0][1], kc[1][1]))
             mm = m.copy()
-            plan.fetch(mm)
+            sts.append(plan.fetch(mm))
             outs.append(mm)
-        for o in outs[1:]:
-            assert np.array_equal(o["kf_pose"], outs[0]["kf_pose"]) and np.array_equal(o["lm_pos"], outs[0]["lm_pos"])
+        for o, s in zip(outs[1:], sts[1:]):
+            _runs_agree(o, outs[0], s, sts[0], bitwise=sums == "slots")
         captured, launched = c.graph_counts()
         assert captured >= 4 and launched >= 8, (captured, launched)
         plan.close()
@@ -438,7 +460,7 @@ def _plan_result(ctx, m, opts, ref, rank, count, host_build):
 
 
 @pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
-def test_device_plan_build_equals_host_build(ctx, cfg):
+def test_device_plan_build_equals_host_build(ctx, cfg, slot_sums):
     """vx_ba_plan_create builds the window / landmark set / CSRs on the GPU (ba_window.hip); the
     host restatement (VX_PLAN_HOST_BUILD) gives the same plan: identical counts and bitwise
     identical LocalBA results."""
@@ -539,7 +561,7 @@ def test_failed_plan_build_then_destroy(monkeypatch):
     c.close()
 
 
-def test_seq_replay_matches_direct_calls(ctx, oracle):
+def test_seq_replay_matches_direct_calls(ctx, oracle, slot_sums):
     """vx_seq: a recorded list of async calls over two contexts (extract into a slot, event record /
     wait across the contexts, match, a LocalBA plan run) replayed by vx_seq_run gives exactly what the
     same calls made one by one give — and replays again identically (the bench's timed steps)."""

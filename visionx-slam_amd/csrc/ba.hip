@@ -663,7 +663,7 @@ constexpr int kFK = kBaFusedK;
 // Threads per fused workgroup (= its landmark-stage observation / landmark capacity): 512, or 1024
 // for windows whose 512-thread packing needs more workgroups than the device has CUs (fewer,
 // larger workgroups: shorter per-keyframe slot lists; measured).
-constexpr int kFTSmall = kBaFTSmall, kFTLarge = kBaFTLarge;
+constexpr int kFTSmall = kBaFTSmall, kFTLarge = kBaFTLarge, kFTNarrow = kBaFTNarrow;
 
 // Fused layout (ba.hip build_fused).  Per workgroup b: landmarks and landmark-stage observations at
 // the fixed bases b * kFT (padded), so their loads do not wait for the workgroup table; keyframe
@@ -696,7 +696,24 @@ struct FusedArgs {
     double* epose;          // [(b * kFK + j) * 16] the workgroup's copy of entry j's pose T 8 | C 4 | flags:
                             // every workgroup solving the entry computes the same pose, so each keeps
                             // its own and reads it back at a fixed address (no keyframe-row indirection)
+    // Row sums by float atomics (unsharded plans; the default, $VX_BA_ATOMIC_ROWS=0 for slots):
+    // launch it >= 0 adds its pose-stage partials (iteration it + 1) straight into per-row sums
+    // arow[it % 3] (n_kf x kStride, float atomics executed at the memory side) instead of partial
+    // slots, so the next launch combines ONE row per entry instead of re-summing the row's maxl slots
+    // (sum order = arrival order: results agree to rounding, not bitwise, run to run; every workgroup
+    // of a launch still reads the same row, so the redundant pose solves agree bitwise).  Launch it
+    // zeroes arow[(it + 1) % 3], the buffer launch it + 1 accumulates into (last read by launch
+    // it - 1).  With apro (plans of >= 2 iterations) the prologue accumulates into arow[3], which
+    // launch 0 reads and the run's last launch zeroes for the next run (the plan build zeroes it
+    // first); without it the prologue writes slots, which launch 0 combines.
+    double* arow;
+    int n_kf, apro;
 };
+
+// the arow buffer launch `it` reads (combine), accumulates into (pose stage of it + 1) and zeroes
+__device__ __forceinline__ int arow_rd(int it) { return it == 0 ? 3 : (it - 1) % 3; }
+__device__ __forceinline__ int arow_wr(bool pro, int it) { return pro ? 3 : it % 3; }
+__device__ __forceinline__ int arow_zero(bool pro, int it) { return pro ? 0 : (it + 1) % 3; }
 
 // LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), kFK loaded
 // entry states (T 8 | C 4 | flags), 9 x kFT observation terms, kFT counted flags, 3 x kFT landmark
@@ -759,11 +776,15 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // per-entry pose copies (f.epose) and fused-order landmark positions (f.lpos) in the 512-thread
     // kernel; the 1024-thread one (128 VGPRs) keeps the indirect reads of the published poses and
     // positions, whose longer live ranges it cannot afford
-    constexpr bool kEcopy = kFT == kFTSmall;
+    constexpr bool kEcopy = kFT <= kFTSmall;
     // highest wave priority: in the pipeline, extraction waves share these SIMDs, and the launch's
     // dependent FP64 chains are what the frame waits for (instruction-issue arbitration prefers
     // higher-priority waves; the co-resident waves fill the gaps of the chains)
     __builtin_amdgcn_s_setprio(3);
+    if (!kPro && f.arow && f.apro && it == a.max_iter - 1) {  // (arow[3] for the next run's prologue)
+        double* z = f.arow + (size_t)3 * f.n_kf * kStride;
+        for (int i = blockIdx.x * kFT + threadIdx.x; i < f.n_kf * kStride; i += (int)gridDim.x * kFT) z[i] = 0.0;
+    }
     // (an iteration after the stop returns before its first write, below: its loads are issued
     // first so the flag's latency overlaps theirs)
     if (!kEcopy && !kPro && it > 0 && !a.state->active[it]) return;
@@ -861,6 +882,10 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
     const bool has_o = !kPro && tid < n_ob, own = tid < n_lm;
     if (!kPro && it > 0 && !act) return;  // iteration after the stop: no global write
+    if (f.arow) {  // the buffer the NEXT launch accumulates into (see FusedArgs::arow)
+        double* z = f.arow + (size_t)arow_zero(kPro, it) * f.n_kf * kStride;
+        for (int i = b * kFT + tid; i < f.n_kf * kStride; i += (int)gridDim.x * kFT) z[i] = 0.0;
+    }
     if (kPro && kEcopy) f.lpos[base + tid] = make_double4(PL.x, PL.y, PL.z, 0.0);
     lpos[3 * tid] = PL.x;
     lpos[3 * tid + 1] = PL.y;
@@ -881,8 +906,12 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 kslot[j * kLdsStride + t] = f.rowpart[(size_t)(e.x & 0x3fffffff) * kStride + t];
                 continue;
             }
+            if (f.arow && (it > 0 || f.apro)) {  // the row summed by the previous launch's atomics
+                kslot[j * kLdsStride + t] = f.arow[((size_t)arow_rd(it) * f.n_kf + (e.x & 0x3fffffff)) * kStride + t];
+                continue;
+            }
             const double* src = part_in + ((size_t)(e.x & 0x3fffffff) * f.maxl) * kStride + t;
-            constexpr int kCB = kFT == kFTSmall ? 32 : 16;  // slots per batch of loads (one round at C3)
+            constexpr int kCB = kFT <= kFTSmall ? 32 : 16;  // slots per batch of loads (one round at C3)
             double acc = 0.0;
             for (int i0 = 0; i0 < e.y; i0 += kCB) {
                 double v[kCB];
@@ -896,10 +925,11 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         // ---- stop rule of iteration it (workgroup 0): totals over every partial slot
         if (b == f.stop_b) {
             double tot = 0.0, cnt = 0.0;
-            if (f.rowpart) {
+            if (f.rowpart || (f.arow && (it > 0 || f.apro))) {
+                const double* rows = f.rowpart ? f.rowpart : f.arow + (size_t)arow_rd(it) * f.n_kf * kStride;
                 for (int q = tid; q < a.n_kf; q += kFT) {
-                    tot += f.rowpart[(size_t)q * kStride + 27];
-                    cnt += f.rowpart[(size_t)q * kStride + 28];
+                    tot += rows[(size_t)q * kStride + 27];
+                    cnt += rows[(size_t)q * kStride + 28];
                 }
             } else {
                 const double2* cp = f.costpart + (size_t)(it & 1) * f.n_part;
@@ -974,7 +1004,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     if (!kPro) {
         double h[9];
         const D3 PO{lpos[3 * orec.y], lpos[3 * orec.y + 1], lpos[3 * orec.y + 2]};
-        const bool ok = obs_terms<kFT == kFTSmall>(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride,
+        const bool ok = obs_terms<kFT <= kFTSmall>(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride,
                                                    kslot + 17, kLdsStride, h);
 #pragma unroll
         for (int j = 0; j < 9; ++j) terms[j * kFT + tid] = h[j];
@@ -1086,16 +1116,22 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
             }
             const bool valid = e.z + 64 * q + lane < e.w;
-            if (kFT == kFTSmall || valid) {  // (512: padding lanes run too, weight 0 — no branch)
+            if (kFT <= kFTSmall || valid) {  // (256 / 512: padding lanes run too, weight 0 — no branch)
                 const int code = (int)P4.w;
                 const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]}
                                        : D3{P4.x, P4.y, P4.z};
-                pose_obs_accum<kFT == kFTSmall>(a, T, R, C, P, uv, v, valid);
+                pose_obs_accum<kFT <= kFTSmall>(a, T, R, C, P, uv, v, valid);
             }
         }
         }
         if (j == wv) FKT(7);
         const double tot = wave_sum32(v);
+        if (f.arow && (!kPro || f.apro)) {  // (iteration it + 1's row sums, see FusedArgs::arow)
+            if ((lane & 1) == 0 && (lane >> 1) < kNTerms)
+                unsafeAtomicAdd(f.arow + ((size_t)arow_wr(kPro, it) * f.n_kf + (e.x & 0x3fffffff)) * kStride + (lane >> 1),
+                                tot);
+            continue;
+        }
         if ((lane & 1) == 0) part_out[(size_t)dst * kStride + (lane >> 1)] = (lane >> 1) < kNTerms ? tot : 0.0;
         if (lane == 54 || lane == 56)  // terms 27 (cost) and 28 (observations)
             reinterpret_cast<double*>(f.costpart + (size_t)((it + 1) & 1) * f.n_part + dst)[(lane - 54) >> 1] = tot;
@@ -1293,13 +1329,23 @@ bool fused_eligible(const vx_ba_plan* p) {
     return true;
 }
 
+// $VX_BA_ATOMIC_ROWS=0: the fused LocalBA's per-keyframe partial slots (every run bitwise the
+// same) instead of row sums by float atomics (FusedArgs::arow; read at plan build)
+bool ba_atomic_rows() {
+    const char* e = getenv("VX_BA_ATOMIC_ROWS");
+    return !(e && e[0] == '0');
+}
+
 // 1024 threads when 512-thread workgroups would outnumber the compute units (their count is within a
 // few percent of the landmark-stage observations / 512: whole landmarks of <= 5 observations);
 // VX_BA_FUSED_THREADS / VX_BA_FUSED_CAP override for sweeps
 int fused_threads(vx_ctx* c, int64_t n_lobs, int* cap) {
     if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
     int ft = n_lobs > (int64_t)c->n_cus * (kFTSmall - 16) ? kFTLarge : kFTSmall;
-    if (const char* e = getenv("VX_BA_FUSED_THREADS")) ft = atoi(e) == kFTLarge ? kFTLarge : kFTSmall;
+    if (const char* e = getenv("VX_BA_FUSED_THREADS")) {
+        const int v = atoi(e);
+        ft = v == kFTLarge ? kFTLarge : v == kFTNarrow ? kFTNarrow : kFTSmall;
+    }
     *cap = ft;
     if (const char* e = getenv("VX_BA_FUSED_CAP")) *cap = std::min(ft, std::max(64, atoi(e)));
     return ft;
@@ -1346,6 +1392,14 @@ int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp
     const size_t cost_bytes = 2 * (size_t)p->n_kf * maxl * sizeof(double2);
     VX_HIP(c, p->f_costpart.ensure(cost_bytes));
     VX_HIP(c, hipMemsetAsync(p->f_costpart.p, 0, cost_bytes, c->stream));
+    // row sums by float atomics (FusedArgs::arow): unsharded plans, unless $VX_BA_ATOMIC_ROWS=0
+    // (partial slots: every run bitwise the same)
+    p->f_atomic = p->shard_count <= 1 && ba_atomic_rows();
+    if (p->f_atomic) {
+        const size_t ab = 4 * (size_t)p->n_kf * kStride * sizeof(double);
+        VX_HIP(c, p->f_arow.ensure(ab));
+        VX_HIP(c, hipMemsetAsync(p->f_arow.p, 0, ab, c->stream));
+    }
     p->f_stop_b = stop_b;
     p->f_blocks = nb;
     p->f_maxl = maxl;
@@ -1789,9 +1843,8 @@ int landmark_stage(vx_ctx* c, const vx_ba_plan* p, const BAArgs& a, int it, bool
     if (lds_poses) {
         const size_t lds = landmark_solve_lds(p);
         if (lds > 64 * 1024) {  // up to ~154 KB at kMaxKfLds keyframes (gfx950: 160 KB per workgroup)
-            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
-                                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            VX_HIP(c, attr);
+            static std::atomic<uint64_t> done{0};
+            VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_landmark_solve), 160 * 1024, done));
         }
         VX_HIP(c, launch(c, kStBaLandmark, k_landmark_solve, dim3(p->n_lm_blocks), dim3(kLmBlock), (uint32_t)lds,
                          c->stream, a, it));
@@ -1856,6 +1909,9 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
     f.stop_b = p->f_stop_b;
     f.lpos = p->f_lpos.as<double4>();
     f.epose = p->f_epose.as<double>();
+    f.arow = p->f_atomic && p->shard_count <= 1 ? p->f_arow.as<double>() : nullptr;
+    f.n_kf = p->n_kf;
+    f.apro = p->opt.max_iterations >= 2;
     return f;
 }
 
@@ -1874,15 +1930,10 @@ template <int kFT>
 int fused_launch_t(vx_ctx* c, vx_ba_plan* p, const BAArgs& a, const FusedArgs& f, int it) {
     constexpr int lds = (int)fused_lds(kFT);
     constexpr int lds_c = (int)fused_lds_cmp(kFTSmall);
-    static const hipError_t a0 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<true, kFT>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    static const hipError_t a1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false, kFT>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    static const hipError_t a2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ba_iter<false, kFTSmall, true>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds_c);
-    VX_HIP(c, a0);
-    VX_HIP(c, a1);
-    VX_HIP(c, a2);
+    static std::atomic<uint64_t> d0{0}, d1{0}, d2{0};  // (per device: ADVICE r4)
+    VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_ba_iter<true, kFT>), lds, d0));
+    VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_ba_iter<false, kFT>), lds, d1));
+    VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_ba_iter<false, kFTSmall, true>), lds_c, d2));
     if (it < 0)
         VX_HIP(c, launch(c, kStBaPrologue, k_ba_iter<true, kFT>, dim3(p->f_blocks), dim3(kFT), (uint32_t)lds, c->stream,
                          a, f, -1));
@@ -1895,7 +1946,9 @@ int fused_launch_t(vx_ctx* c, vx_ba_plan* p, const BAArgs& a, const FusedArgs& f
     return VX_OK;
 }
 int fused_launch(vx_ctx* c, vx_ba_plan* p, const BAArgs& a, const FusedArgs& f, int it) {
-    return p->f_threads == kFTLarge ? fused_launch_t<kFTLarge>(c, p, a, f, it) : fused_launch_t<kFTSmall>(c, p, a, f, it);
+    if (p->f_threads == kFTLarge) return fused_launch_t<kFTLarge>(c, p, a, f, it);
+    if (p->f_threads == kFTNarrow) return fused_launch_t<kFTNarrow>(c, p, a, f, it);
+    return fused_launch_t<kFTSmall>(c, p, a, f, it);
 }
 // sharded fused path: the rows of the partial buffer iteration it reads (parity it & 1) -> f_rowpart
 int fused_row_sum(vx_ctx* c, vx_ba_plan* p, int it) {
@@ -2028,9 +2081,8 @@ int ba_run_dyn(vx_ctx* c, const DynPlan& d) {
     a.dyn = d.dyn;
     const size_t lds = (size_t)d.n_kf * kLdsStride * sizeof(double) + (size_t)kLmBlock * (9 * sizeof(double) + sizeof(int));
     if (lds > 64 * 1024) {
-        static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_landmark_solve),
-                                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        VX_HIP(c, attr);
+        static std::atomic<uint64_t> done{0};
+        VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_landmark_solve), 160 * 1024, done));
     }
     for (int it = 0; it < d.opt.max_iterations; ++it) {
         VX_HIP(c, launch(c, kStBaPose, k_pose_kf, dim3(d.n_kf * d.n_split), dim3(kPoseBlock), 0, c->stream, a, it));

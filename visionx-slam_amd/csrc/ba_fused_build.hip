@@ -590,10 +590,9 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p) {
     VX_LAUNCH_CHECK(c, "fused build: sorted order");
     VX_HIP(c, rocprim::exclusive_scan(S.fb_tmp.p, tb2, cntS, cntScan, 0, no + 1, rocprim::plus<int>(), s));
     const size_t next_lds = (size_t)(kT + cap) * (W * sizeof(u64) + 2 * sizeof(int)) + sizeof(int);
-    static const hipError_t attr = hipFuncSetAttribute(
-        reinterpret_cast<const void*>(&k_fb_next), hipFuncAttributeMaxDynamicSharedMemorySize,
-        (int)((kT + kBaFTLarge) * (kMaxW * sizeof(u64) + 2 * sizeof(int)) + sizeof(int)));
-    VX_HIP(c, attr);
+    static std::atomic<uint64_t> attr_done{0};
+    VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_fb_next),
+                            (int)((kT + kBaFTLarge) * (kMaxW * sizeof(u64) + 2 * sizeof(int)) + sizeof(int)), attr_done));
     hipLaunchKernelGGL(k_fb_next, dim3(grid(n_opt)), dim3(kT), (uint32_t)next_lds, s, (const int*)cntScan,
                        (const int*)keys2, (const u64*)maskS, n_opt, W, cap, (const int*)counters, next);
     hipLaunchKernelGGL(k_fb_chain, dim3(1), dim3(1024), 0, s, (const int*)next, n_opt, starts, counters);

@@ -853,12 +853,26 @@ int lean_optimize(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_
                            (const double*)L.lm_pos.as<double>(), m->kf_pose.as<double>(), m->lm_pos.as<double>());
         VX_LAUNCH_CHECK(c, "k_lb_apply");
     }
-    // the end: the header (and the iteration state) back — the call's only synchronisation
+    // the end: the header (and the iteration state) back — the call's only synchronisation; with
+    // vx_dmap_prefetch_results the results too (both pose parities, positions and rows by capacity)
     const size_t sb = ba_state_bytes();
     VX_HIP(c, L.rb_host.ensure(kDynInts * 4 + sb));
     int* H = static_cast<int*>(L.rb_host.p);
     VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
     if (o.max_iterations > 0) VX_HIP(c, hipMemcpyAsync(H + kDynInts, L.state.p, sb, hipMemcpyDeviceToHost, sm));
+    L.prefetched = false;
+    if (L.prefetch && o.max_iterations > 0) {
+        const size_t pose_b = 2 * (size_t)nk * 64, pos_b = (size_t)nl * 32, rows_b = (size_t)nl * 4;
+        VX_HIP(c, L.res_host.ensure(pose_b + pos_b + rows_b + 64, true));
+        uint8_t* R = static_cast<uint8_t*>(L.res_host.p);
+        VX_HIP(c, hipMemcpyAsync(R, L.kf_pose.p, pose_b, hipMemcpyDeviceToHost, sm));
+        if (nl) {
+            VX_HIP(c, hipMemcpyAsync(R + pose_b, L.lm_pos.p, pos_b, hipMemcpyDeviceToHost, sm));
+            VX_HIP(c, hipMemcpyAsync(R + pose_b + pos_b, a.inv, rows_b, hipMemcpyDeviceToHost, sm));
+        }
+        L.prefetched = true;
+        L.pf_nl = nl;
+    }
     VX_HIP(c, hipStreamSynchronize(sm));
     s.status = H[kDynStatus];
     s.n_landmarks = H[kDynGlobal];
@@ -881,6 +895,10 @@ int build_sba_plan_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, vx_sba
     const vx_sba_options& o = p->opt;
     p->status = 1;
     p->from_dmap = true;
+    // this build reuses (and may reallocate) the lean core's scratch that vx_ba_dmap_results reads
+    // (inv, lm_pos0, kf_pose0, win): a LocalBA result from before it can no longer be reported
+    // (vx_ba_dmap_results then fails with VX_ERR_STATE until the next vx_ba_optimize_dmap)
+    m->lean.ran = false;
     const int n_kf = (int)m->kf_id.size();
     std::vector<int> win = n_kf > 0 ? dmap_select_window(m, ref, has_ref, o.window_size) : std::vector<int>{};
     const int nk = (int)win.size();
@@ -1087,6 +1105,7 @@ int vx_ba_optimize_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const 
         L.fallback = nullptr;
     }
     L.ran = false;
+    L.prefetched = false;
     // $VX_LEAN=0: always the general build (ba_window.hip), for A/B runs
     const char* e = getenv("VX_LEAN");
     bool fb = e && e[0] == '0';
@@ -1117,6 +1136,12 @@ int vx_ba_optimize_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const 
     return VX_OK;
 }
 
+int vx_dmap_prefetch_results(vx_dmap* m, int on) {
+    if (!m) return VX_ERR_INVALID;
+    m->lean.prefetch = on != 0;
+    return VX_OK;
+}
+
 int vx_ba_dmap_results(vx_ctx* c, vx_dmap* m, int cap_kf, int64_t* kf_rows, double* kf_pose7, int cap_lm,
                        int64_t* lm_rows, double* lm_pos3, int* n_kf, int* n_lm) {
     if (!c || !m || m->c != c || !n_kf || !n_lm) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_dmap_results: bad arguments") : VX_ERR_INVALID;
@@ -1127,8 +1152,24 @@ int vx_ba_dmap_results(vx_ctx* c, vx_dmap* m, int cap_kf, int64_t* kf_rows, doub
     *n_lm = changed ? L.n_opt : 0;
     if (!changed) return VX_OK;
     if (cap_kf < *n_kf || cap_lm < *n_lm) return set_error(c, VX_ERR_CAPACITY, "need %d keyframes / %d landmarks", *n_kf, *n_lm);
-    VX_HIP(c, hipSetDevice(c->device));
     const int nk = L.nk, n = L.n_opt;
+    if (L.prefetched && !L.fallback && n <= L.pf_nl) {  // (vx_dmap_prefetch_results: host copies only)
+        const double* pose = reinterpret_cast<const double*>(L.res_host.p) + (size_t)(L.iterations & 1) * nk * 8;
+        const double* pos = reinterpret_cast<const double*>(L.res_host.p) + 2 * (size_t)nk * 8;
+        const int* rows = reinterpret_cast<const int*>(pos + (size_t)L.pf_nl * 4);
+        for (int r = 0; r < nk; ++r) {
+            if (kf_rows) kf_rows[r] = L.win_rows[r];
+            if (kf_pose7)
+                for (int j = 0; j < 7; ++j) kf_pose7[7 * r + j] = pose[8 * (size_t)r + j];
+        }
+        for (int i = 0; i < n; ++i) {
+            if (lm_rows) lm_rows[i] = rows[i];
+            if (lm_pos3)
+                for (int j = 0; j < 3; ++j) lm_pos3[3 * (size_t)i + j] = pos[4 * (size_t)i + j];
+        }
+        return VX_OK;
+    }
+    VX_HIP(c, hipSetDevice(c->device));
     // one pinned staging block (poses, positions, landmark rows), one synchronisation
     const size_t pose_b = (size_t)nk * 64, pos_b = (size_t)n * 32, rows_b = (size_t)n * 4;
     VX_HIP(c, L.res_host.ensure(pose_b + pos_b + rows_b + 64, true));

@@ -44,6 +44,8 @@ struct vx_ba_plan {
     vx::DevBuf f_rowpart;                                         // sharded: all-reduced per-row partials
     vx::DevBuf f_lpos, f_epose;  // k_ba_iter's fused-order landmark positions and per-entry pose copies
     vx::DevBuf f_costpart;       // compact {cost, observations} of every partial slot (stop rule)
+    vx::DevBuf f_arow;           // $VX_BA_ATOMIC_ROWS: 3 rotating n_kf x 32 per-row sums (float atomics)
+    bool f_atomic = false;
     int f_stop_b = 0;            // workgroup running the stop rule
     vx::PinnedBuf f_stage;                                        // their host staging block
     FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
@@ -59,7 +61,7 @@ struct vx_dmap;
     X(kf_pose0) X(kf_pose) X(kf_intr) X(kf_rot) X(kf_flags) X(kf_obs_ptr) X(kf_part) X(kf_cost) X(lm_pos0) \
     X(lm_pos) X(pobs_uv) X(pobs_lm) X(lobs_ptr) X(lobs_kf) X(lobs_lm) X(lm_blk) X(lobs_uv) X(state)       \
     X(kf_map_dev) X(lm_map_dev) X(f_tab) X(f_lobs_uv) X(f_pobs_uv) X(f_pobs_p) X(f_part) X(f_rowpart)    \
-    X(f_stage) X(f_lpos) X(f_epose) X(f_costpart)
+    X(f_stage) X(f_lpos) X(f_epose) X(f_costpart) X(f_arow)
 
 namespace vx {
 // a new plan of context c (buffers adopted from a parked plan when there is one)
@@ -97,6 +99,7 @@ int build_fused_device(vx_ctx* c, vx_ba_plan* p);
 constexpr int kBaFusedK = 64;      // keyframes per fused workgroup
 constexpr int kFusedMaxGroups = 8192;  // most fused workgroups of a plan (host and device builds alike)
 constexpr int kBaFTSmall = 512, kBaFTLarge = 1024;  // threads per fused workgroup
+constexpr int kBaFTNarrow = 256;                     // (opt-in, $VX_BA_FUSED_THREADS=256)
 constexpr int kBaStride = 32;      // doubles per partial block
 constexpr int kBaMaxKfLds = 448;   // most window keyframes of the LDS-pose / fused kernels
 // whether the plan can take the fused layout at all (window size, options, $VX_BA_FUSED)

@@ -66,6 +66,9 @@ struct vx_dmap {
         std::vector<int> win_rows;         // its keyframe rows
         bool ran = false;
         vx_ba_plan* fallback = nullptr;    // the last call's plan when it took the general build
+        bool prefetch = false;             // vx_dmap_prefetch_results
+        bool prefetched = false;           // res_host holds the last call's results (lean build)
+        int64_t pf_nl = 0;                 // (their landmark capacity)
     } lean;
     // scratch of the Schur plan build from this map (vx_sba_plan_create_dmap)
     struct SbaScratch {

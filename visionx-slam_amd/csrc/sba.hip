@@ -1730,7 +1730,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     // substitution tile lists k_sba_solve walks.  A sliding window's covisibility is banded, so
     // most tiles of the dense matrix are never touched.
     std::vector<int> hdr((size_t)kHdrN * std::max(p->n_comp, 1), 0), tlist;
-    p->n_lfactor_tiles = p->n_trail_updates = 0;
+    p->n_lfactor_tiles = p->n_trail_updates = p->n_trail_rhs = 0;
     p->max_panel = 1;
     p->max_nt = p->max_trail_rest = 0;
     p->max_pairs = 0;
@@ -1792,6 +1792,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                     for (int i = k + 1; i < nt; ++i)
                         if (NZ(i, k)) tlist.push_back(i << 16 | (k + 1));
                     tlist.push_back(nt << 16 | (k + 1));
+                    ++p->n_trail_rhs;
                 }
                 split[k] = (int)tlist.size();
                 for (int i = k + 1; i < nt; ++i)
@@ -1799,7 +1800,10 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                         for (int j = k + 2; j <= i; ++j)
                             if (NZ(j, k)) tlist.push_back(i << 16 | j);
                 for (int j = k + 2; j < nt; ++j)
-                    if (NZ(j, k)) tlist.push_back(nt << 16 | j);
+                    if (NZ(j, k)) {
+                        tlist.push_back(nt << 16 | j);
+                        ++p->n_trail_rhs;
+                    }
                 p->n_trail_updates += (int)tlist.size() - tlist[tp + k];
                 p->max_trail_rest = std::max(p->max_trail_rest, (int)tlist.size() - split[k]);
             }
@@ -2366,6 +2370,17 @@ int vx_sba_plan_info(const vx_sba_plan* p, int64_t* out8) {
     const int64_t v[8] = {p->nk, p->n_opt, p->n_obs, p->n_pairs, p->n_blocks, 6 * (int64_t)p->nk,
                           p->n_lfactor_tiles, p->n_comp};
     for (int i = 0; i < 8; ++i) out8[i] = v[i];
+    return VX_OK;
+}
+
+int vx_sba_plan_factor_work(const vx_sba_plan* p, int64_t* out4) {
+    if (!p || !out4) return VX_ERR_INVALID;
+    int64_t diag = 0;
+    for (int np : p->comp_np_h) diag += np / 16;
+    // (algorithmic: the rhs row's tiles — one per column, and their updates — are left out)
+    const int64_t v[4] = {p->n_lfactor_tiles - diag, p->n_trail_updates - p->n_trail_rhs, diag,
+                          p->n_lfactor_tiles - diag - diag};
+    for (int i = 0; i < 4; ++i) out4[i] = v[i];
     return VX_OK;
 }
 

@@ -25,6 +25,7 @@ struct vx_sba_plan {
     std::vector<int> comp_kf_ptr_h, comp_kf_h, comp_np_h;
     std::vector<long long> comp_off_h, comp_loff_h;
     int64_t n_lfactor_tiles = 0, n_trail_updates = 0;  // symbolic factorisation (all components)
+    int64_t n_trail_rhs = 0;  // (of the updates: those of the rhs row)
     vx::OwnedGraph graph;  // the run's launch sequence, replayed by hipGraphLaunch
     vx::DevBuf pose0, pose, intr, kf_flags, kf_comp, kf_local, lm0, lm, obs_uv, obs_kf, obs_lm, lm_ptr, lm_blk,
         kf_ptr, kf_obs, blk_ij, blk_ptr, pairs, comp_kf_ptr, comp_kf, comp_off, comp_loff, comp_np, comp_hdr, tl, wy,

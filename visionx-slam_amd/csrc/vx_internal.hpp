@@ -5,6 +5,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
@@ -312,6 +313,17 @@ struct OwnedGraph {
     void reset();  // forget the captured sequence (the next run is eager, then captured again)
 };
 int graph_run_owned(vx_ctx* c, OwnedGraph& g, int (*enqueue)(vx_ctx*, void*), void* arg);
+
+// A kernel's >64 KB dynamic-LDS attribute, set once per DEVICE (hipFuncSetAttribute applies to the
+// current device only; a function-local static would set it on whichever device came first).
+// `done` is a per-call-site bit set of the devices already configured.
+inline hipError_t lds_attr_once(int device, const void* fn, int bytes, std::atomic<uint64_t>& done) {
+    const uint64_t bit = (device >= 0 && device < 64) ? (1ull << device) : 0;
+    if (bit && (done.load(std::memory_order_acquire) & bit)) return hipSuccess;
+    const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess && bit) done.fetch_or(bit, std::memory_order_release);
+    return e;
+}
 
 }  // namespace vx
 

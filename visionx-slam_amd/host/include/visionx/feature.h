@@ -87,8 +87,16 @@ struct FlatMap {
     std::vector<int64_t> lm_obs_ptr;
     std::vector<uint64_t> obs_kf_id, obs_feat_idx;
     std::vector<Frame::Ptr> frames;        // keyframes in kf_id order
-    std::vector<Landmark::Ptr> landmarks;  // landmarks in lm_id order
+    std::vector<Landmark::Ptr> landmarks;  // landmarks in lm_id order (first reference in the window)
     vx_map_view view();                    // pointers into the vectors above
+    // (Flatten's working arrays, kept with their capacity between calls)
+    std::vector<uint8_t> scratch_has;
+    std::vector<uint64_t> scratch_ids, scratch_tmp;
+    std::vector<Landmark*> scratch_obj;
+    std::vector<int64_t> scratch_cnt;
+    std::vector<uint64_t> scratch_key, scratch_hash;
+    std::vector<uint32_t> scratch_first;
+    std::vector<uint8_t> scratch_firstocc;
 };
 
 class DeviceMap;
@@ -109,11 +117,14 @@ public:
     // vx_ba_optimize_dmap call on the resident map — no Flatten, no snapshot upload — and then
     // writes the window poses and optimised positions back into the Frame / Landmark objects
     // (Frame::SetPose / Landmark::SetPosition, local_ba.cpp:173,237).  nullptr: the snapshot path.
-    void UseDeviceMap(std::shared_ptr<DeviceMap> dm) { dmap_ = std::move(dm); }
+    // (turns on vx_dmap_prefetch_results: the results come back with Optimize's one synchronisation)
+    void UseDeviceMap(std::shared_ptr<DeviceMap> dm);
 
     // The keyframes SelectKeyFrames picks (local_ba.cpp:42-62), every landmark their features
     // reference, and those landmarks' full observation maps.
     static FlatMap Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size);
+    // the same into `out`, reusing its capacity (what Optimize's snapshot path does call after call)
+    static void Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size, FlatMap& out);
     const vx_ba_stats& LastStats() const { return stats_; }
 
 private:
@@ -124,6 +135,7 @@ private:
     std::shared_ptr<DeviceMap> dmap_;
     std::vector<int64_t> kf_rows_, lm_rows_;
     std::vector<double> kf_out_, lm_out_;
+    FlatMap flat_;  // the snapshot path's window, reused call after call
 };
 
 namespace vxhost {

@@ -2,13 +2,14 @@
 #include "visionx/feature.h"
 
 #include "visionx/device_map.h"
+#include "host_pool.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
-#include <unordered_set>
 
 namespace visionx {
 
@@ -216,10 +217,93 @@ vx_map_view FlatMap::view() {
     return v;
 }
 
+// Distinct landmark ids of the window's features in first-occurrence order (the order of the first
+// feature referencing each: deterministic, like the device plan's fixed-landmark numbering).  The
+// hash space is split into one region per part, so every part dedupes its own ids in its own table
+// region without atomics; each part scans the features in order, so the first insert of an id is its
+// first occurrence, which it marks.  `hash` = the features' id hashes (0 for no landmark).
+static uint64_t mix64(uint64_t x) {
+    x += 0x9e3779b97f4a7c15ull;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector<uint8_t>& has,
+                         const std::vector<uint64_t>& hash, std::vector<uint8_t>& firstocc, FlatMap& f,
+                         std::vector<uint64_t>& ids) {
+    auto& pool = vxhost::Pool::Get();
+    const size_t nf = feat_lm.size();
+    const int parts = std::max(1, pool.Threads());
+    size_t per = 64;  // slots per region: >= 2 x the ids a region can receive (all of them, worst case)
+    while (per < 2 * nf / (size_t)parts + 64) per <<= 1;
+    f.scratch_key.resize(per * (size_t)parts);
+    f.scratch_first.resize(per * (size_t)parts);  // (occupancy flags)
+    pool.For((size_t)parts, 1, [&](size_t a, size_t b) {
+        for (size_t t = a; t < b; ++t) {
+            uint64_t* key = f.scratch_key.data() + t * per;
+            uint32_t* used = f.scratch_first.data() + t * per;
+            std::fill(used, used + per, 0u);
+            size_t n_in = 0;
+            for (size_t o = 0; o < nf; ++o) {
+                // region = the high hash bits scaled to [0, parts) (no division), slot = the low bits
+                if (!has[o] || (size_t)(((hash[o] >> 32) * (uint64_t)parts) >> 32) != t) continue;
+                const uint64_t id = feat_lm[o];
+                size_t h = (size_t)hash[o] & (per - 1);
+                for (;;) {
+                    if (!used[h]) {  // first occurrence
+                        used[h] = 1;
+                        key[h] = id;
+                        firstocc[o] = 1;
+                        ++n_in;
+                        break;
+                    }
+                    if (key[h] == id) break;
+                    h = (h + 1) & (per - 1);
+                }
+                if (2 * n_in > per) std::abort();  // (cannot happen: per >= 2 x the ids of the region)
+            }
+        }
+    });
+    ids.clear();
+    for (size_t o = 0; o < nf; ++o)
+        if (firstocc[o]) ids.push_back(feat_lm[o]);
+}
+
 FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size) {
     FlatMap f;
+    Flatten(map, ref_kf, window_size, f);
+    return f;
+}
+
+// The snapshot gather (local_ba.cpp:42-104 walks the same objects): keyframes by SelectKeyFrames,
+// their features copied to per-keyframe offsets in parallel, the referenced landmark ids made
+// distinct (first-occurrence order), then each landmark's position, bad flag and observation map read in parallel
+// (two passes: counts, then the observation rows at their prefix offsets).  `f` keeps its
+// capacity from call to call.  Landmarks are found in Map::Landmarks() (read-only; the reference's
+// LocalBA runs on the tracking thread, which is also the one that edits the map).
+void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size, FlatMap& f) {
+    auto& pool = vxhost::Pool::Get();
+    static const bool timing = std::getenv("VX_FLATTEN_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* w) {
+        if (timing)
+            std::fprintf(stderr, "[flatten] %s %.3f ms\n", w,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
+    // (every array below is resized to this call's sizes and then fully written: resizing without
+    // clearing first keeps the elements of the previous call instead of zero-filling them)
+    f.frames.clear();
     const auto& all = map.KeyFrames();
-    if (all.empty()) return f;
+    if (all.empty()) {
+        f.landmarks.clear();
+        for (auto* v : {&f.kf_id, &f.lm_id, &f.feat_lm_id, &f.obs_kf_id, &f.obs_feat_idx}) v->clear();
+        for (auto* v : {&f.kf_pose, &f.kf_intr, &f.feat_uv, &f.lm_pos}) v->clear();
+        for (auto* v : {&f.kf_has_cam, &f.feat_flags, &f.lm_bad}) v->clear();
+        f.kf_feat_ptr.clear();
+        f.lm_obs_ptr.clear();
+        return;
+    }
     // SelectKeyFrames (local_ba.cpp:42-62)
     const uint64_t max_id = ref_kf ? ref_kf->Id() : all.rbegin()->first;
     const int window = std::max(1, window_size);
@@ -228,45 +312,111 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
         f.frames.push_back(it->second);
     }
     std::reverse(f.frames.begin(), f.frames.end());
-    std::unordered_set<uint64_t> lm_ids;
-    f.kf_feat_ptr.push_back(0);
-    for (const auto& kf : f.frames) {
-        const SE3d T = kf->Pose();
-        f.kf_id.push_back(kf->Id());
-        f.kf_pose.insert(f.kf_pose.end(), {T.qx, T.qy, T.qz, T.qw, T.tx, T.ty, T.tz});
-        const auto cam = kf->GetCamera();
-        f.kf_has_cam.push_back(cam ? 1 : 0);
-        if (cam)
-            f.kf_intr.insert(f.kf_intr.end(), {cam->fx(), cam->fy(), cam->cx(), cam->cy()});
-        else
-            f.kf_intr.insert(f.kf_intr.end(), {0.0, 0.0, 0.0, 0.0});
-        for (const auto& feat : kf->Features()) {
-            f.feat_uv.push_back(feat.position.x);
-            f.feat_uv.push_back(feat.position.y);
-            f.feat_lm_id.push_back(feat.landmark_id_);
-            f.feat_flags.push_back((feat.has_landmark ? 1 : 0) | (feat.is_outlier ? 2 : 0));
-            if (feat.has_landmark) lm_ids.insert(feat.landmark_id_);
+    const size_t nk = f.frames.size();
+    f.kf_feat_ptr.assign(nk + 1, 0);
+    f.kf_id.resize(nk);
+    f.kf_pose.resize(7 * nk);
+    f.kf_intr.resize(4 * nk);
+    f.kf_has_cam.resize(nk);
+    for (size_t k = 0; k < nk; ++k) f.kf_feat_ptr[k + 1] = f.kf_feat_ptr[k] + (int64_t)f.frames[k]->Features().size();
+    const size_t nf = (size_t)f.kf_feat_ptr[nk];
+    f.feat_uv.resize(2 * nf);
+    f.feat_lm_id.resize(nf);
+    f.feat_flags.resize(nf);
+    std::vector<uint8_t>& has = f.scratch_has;
+    has.resize(nf);
+    std::vector<uint8_t>& firstocc = f.scratch_firstocc;
+    firstocc.resize(nf);
+    std::vector<uint64_t>& hash = f.scratch_hash;
+    hash.resize(nf);
+    pool.For(nk, 1, [&](size_t k0, size_t k1) {
+        for (size_t k = k0; k < k1; ++k) {
+            const auto& kf = f.frames[k];
+            const SE3d T = kf->Pose();
+            f.kf_id[k] = kf->Id();
+            const double pose[7] = {T.qx, T.qy, T.qz, T.qw, T.tx, T.ty, T.tz};
+            std::copy(pose, pose + 7, &f.kf_pose[7 * k]);
+            const auto cam = kf->GetCamera();
+            f.kf_has_cam[k] = cam ? 1 : 0;
+            const double intr[4] = {cam ? cam->fx() : 0.0, cam ? cam->fy() : 0.0, cam ? cam->cx() : 0.0,
+                                    cam ? cam->cy() : 0.0};
+            std::copy(intr, intr + 4, &f.kf_intr[4 * k]);
+            size_t o = (size_t)f.kf_feat_ptr[k];
+            for (const auto& feat : kf->Features()) {
+                f.feat_uv[2 * o] = feat.position.x;
+                f.feat_uv[2 * o + 1] = feat.position.y;
+                f.feat_lm_id[o] = feat.landmark_id_;
+                f.feat_flags[o] = (feat.has_landmark ? 1 : 0) | (feat.is_outlier ? 2 : 0);
+                has[o] = feat.has_landmark ? 1 : 0;
+                hash[o] = feat.has_landmark ? mix64(feat.landmark_id_) : 0ull;
+                firstocc[o] = 0;
+                ++o;
+            }
         }
-        f.kf_feat_ptr.push_back((int64_t)f.feat_uv.size() / 2);
-    }
-    std::vector<uint64_t> ids(lm_ids.begin(), lm_ids.end());
-    std::sort(ids.begin(), ids.end());
-    f.lm_obs_ptr.push_back(0);
-    for (uint64_t id : ids) {
-        auto lm = map.GetLandmark(id);
-        if (!lm) continue;  // GetLandmark -> nullptr: treated as absent, like local_ba.cpp:96-97,135-136
-        const Vec3d p = lm->Position();
-        f.landmarks.push_back(lm);
-        f.lm_id.push_back(id);
-        f.lm_pos.insert(f.lm_pos.end(), {p.x, p.y, p.z});
-        f.lm_bad.push_back(lm->IsBad() ? 1 : 0);
-        for (const auto& [kid, fidx] : lm->Observations()) {
-            f.obs_kf_id.push_back(kid);
-            f.obs_feat_idx.push_back((uint64_t)fidx);
+    });
+    lap("features");
+    // the landmark ids the window's features reference, distinct, in first-occurrence order
+    std::vector<uint64_t>& ids = f.scratch_ids;
+    distinct_ids(f.feat_lm_id, has, hash, firstocc, f, ids);
+    lap("ids");
+    // per landmark: the object (absent ids are skipped, as GetLandmark -> nullptr in
+    // local_ba.cpp:96-97,135-136), position, bad flag, observation count
+    const size_t nid = ids.size();
+    const auto& lms = map.Landmarks();
+    std::vector<Landmark*>& obj = f.scratch_obj;
+    std::vector<int64_t>& cnt = f.scratch_cnt;
+    obj.assign(nid, nullptr);
+    cnt.assign(nid + 1, 0);
+    f.landmarks.resize(nid);
+    pool.For(nid, 512, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            auto it = lms.find(ids[i]);
+            if (it == lms.end() || !it->second) {
+                f.landmarks[i].reset();
+                continue;
+            }
+            obj[i] = it->second.get();
+            f.landmarks[i] = it->second;
+            cnt[i + 1] = (int64_t)it->second->Observations().size();
         }
-        f.lm_obs_ptr.push_back((int64_t)f.obs_kf_id.size());
-    }
-    return f;
+    });
+    lap("lookups");
+    size_t nl = 0;
+    for (size_t i = 0; i < nid; ++i)  // (compact the found ones, keep ascending ids)
+        if (obj[i]) {
+            ids[nl] = ids[i];
+            obj[nl] = obj[i];
+            f.landmarks[nl] = std::move(f.landmarks[i]);
+            cnt[nl + 1] = cnt[i + 1];
+            ++nl;
+        }
+    f.landmarks.resize(nl);
+    f.lm_obs_ptr.resize(nl + 1);
+    f.lm_obs_ptr[0] = 0;
+    for (size_t i = 0; i < nl; ++i) f.lm_obs_ptr[i + 1] = f.lm_obs_ptr[i] + cnt[i + 1];
+    f.lm_id.assign(ids.begin(), ids.begin() + (std::ptrdiff_t)nl);
+    f.lm_pos.resize(3 * nl);
+    f.lm_bad.resize(nl);
+    f.obs_kf_id.resize((size_t)f.lm_obs_ptr[nl]);
+    f.obs_feat_idx.resize((size_t)f.lm_obs_ptr[nl]);
+    pool.For(nl, 512, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            if (i + 4 < b) __builtin_prefetch(obj[i + 4]);
+            const Landmark* lm = obj[i];
+            const Vec3d p = lm->Position();
+            f.lm_pos[3 * i] = p.x;
+            f.lm_pos[3 * i + 1] = p.y;
+            f.lm_pos[3 * i + 2] = p.z;
+            f.lm_bad[i] = lm->IsBad() ? 1 : 0;
+            size_t o = (size_t)f.lm_obs_ptr[i];
+            for (const auto& [kid, fidx] : lm->Observations()) {
+                f.obs_kf_id[o] = kid;
+                f.obs_feat_idx[o] = (uint64_t)fidx;
+                ++o;
+            }
+        }
+    });
+    lap("landmarks");
 }
 
 vx_ba_options LocalBA::VxOptions() const {
@@ -278,6 +428,11 @@ vx_ba_options LocalBA::VxOptions() const {
     o.huber_delta = options_.huber_delta;
     o.max_reproj_error = options_.max_reproj_error;
     return o;
+}
+
+void LocalBA::UseDeviceMap(std::shared_ptr<DeviceMap> dm) {
+    dmap_ = std::move(dm);
+    if (dmap_) check(dmap_->context(), vx_dmap_prefetch_results(dmap_->handle(), 1), "vx_dmap_prefetch_results");
 }
 
 void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
@@ -299,7 +454,8 @@ void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
                                 lm_out_.data(), &nk, &nl);
     }
     check(c, rc, "vx_ba_dmap_results");
-    // Frame::SetPose / Landmark::SetPosition (local_ba.cpp:173,237) on the host objects
+    // Frame::SetPose / Landmark::SetPosition (local_ba.cpp:173,237) on the host objects (the
+    // landmarks over the host pool: each SetPosition takes only that landmark's mutex)
     for (int i = 0; i < nk; ++i) {
         const double* p = &kf_out_[7 * (size_t)i];
         SE3d T;
@@ -307,9 +463,11 @@ void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
         T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
         if (const auto& fr = dm.FrameAt(kf_rows_[i])) fr->SetPose(T);
     }
-    for (int i = 0; i < nl; ++i)
-        if (const auto& lm = dm.LandmarkAt(lm_rows_[i]))
-            lm->SetPosition(Vec3d(lm_out_[3 * (size_t)i], lm_out_[3 * (size_t)i + 1], lm_out_[3 * (size_t)i + 2]));
+    vxhost::Pool::Get().For((size_t)nl, 1024, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i)
+            if (const auto& lm = dm.LandmarkAt(lm_rows_[i]))
+                lm->SetPosition(Vec3d(lm_out_[3 * i], lm_out_[3 * i + 1], lm_out_[3 * i + 2]));
+    });
 }
 
 void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
@@ -320,7 +478,8 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
         OptimizeResident(ref_kf);
         return;
     }
-    FlatMap f = Flatten(*map, ref_kf, options_.window_size);
+    FlatMap& f = flat_;
+    Flatten(*map, ref_kf, options_.window_size, f);
     if (f.frames.size() < 2) return;                            // local_ba.cpp:73-75
     const vx_ba_options o = VxOptions();
     vx_map_view v = f.view();
@@ -335,8 +494,10 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
         T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
         f.frames[i]->SetPose(T);
     }
-    for (size_t i = 0; i < f.landmarks.size(); ++i)
-        f.landmarks[i]->SetPosition(Vec3d(f.lm_pos[3 * i], f.lm_pos[3 * i + 1], f.lm_pos[3 * i + 2]));
+    vxhost::Pool::Get().For(f.landmarks.size(), 1024, [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i)
+            f.landmarks[i]->SetPosition(Vec3d(f.lm_pos[3 * i], f.lm_pos[3 * i + 1], f.lm_pos[3 * i + 2]));
+    });
 }
 
 }  // namespace visionx

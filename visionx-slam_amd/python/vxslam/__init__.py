@@ -91,7 +91,7 @@ EXPORTS = [
     "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run", "vx_ba_optimize_dmap",
-    "vx_ba_dmap_results", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_shard_emulate_run", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
+    "vx_ba_dmap_results", "vx_dmap_prefetch_results", "vx_sba_plan_factor_work", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_shard_emulate_run", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
     "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run", "vx_seq_set_threads",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
     "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
@@ -939,6 +939,10 @@ class DMap:
                                                        0 if ref_kf_id is None else 1, plan._h))
         return plan
 
+    def prefetch_results(self, on=True):
+        """vx_dmap_prefetch_results: optimize() brings its results back with its one synchronisation."""
+        self.ctx._check(lib().vx_dmap_prefetch_results(self._h, 1 if on else 0))
+
     def results(self):
         """vx_ba_dmap_results: (keyframe rows, their poses (n, 7), landmark rows, positions (n, 3)) the
         last optimize() changed."""
@@ -983,6 +987,14 @@ class SBAPlan:
         assert lib().vx_sba_plan_info(self._h, _p(out)) == 0
         keys = ["n_kf", "n_opt", "n_obs", "n_pairs", "n_blocks", "n", "n_tiles", "n_comp"]
         return {k: int(v) for k, v in zip(keys, out)}
+
+    def factor_work(self):
+        """vx_sba_plan_factor_work: the dense pose solve's tiles and its FP64 flops per factorisation."""
+        out = np.zeros(4, np.int64)
+        assert lib().vx_sba_plan_factor_work(self._h, _p(out)) == 0
+        d = dict(zip(["l_tiles", "updates", "diag", "panel"], (int(x) for x in out)))
+        d["flops"] = 2 * 16 ** 3 * d["updates"] + 16 ** 3 * d["panel"] + (16 ** 3 // 3) * d["diag"]
+        return d
 
     def run_async(self):
         self.ctx._check(lib().vx_sba_plan_run_async(self.ctx.handle, self._h))
