@@ -1102,7 +1102,7 @@ def main():
                 ci, si = loc(i)
                 x = ectxs[ci]
                 sq.wait(x, ev_m[(i - 3 * E + 1) % (4 * E)])
-                sq.extract(x, params, frames_dev[i % args.frames].data_ptr(), w, h, 3, w * 3, si)
+                sq.extract(x, params, frames_dev[i % args.frames].data_ptr(), w, h, 3, w * 3, si, owner=frames_dev)
                 sq.record(x, ev_e[ci])
                 mx = x if mon else mctx
                 if mon and E > 1:

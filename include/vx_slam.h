@@ -343,7 +343,8 @@ int vx_dmap_add_landmarks(vx_dmap* map, int n, const uint64_t* lm_id, const doub
 /* Landmark::AddObservation(kf_id, feat_idx) on existing landmarks (VX_ERR_INVALID for unknown ids).
  * Like observations_[keyframe_id] = feature_idx (landmark.h:32-35), a (landmark, keyframe) pair
  * already present keeps its place and takes the new feature index; a landmark never holds two
- * observations from one keyframe. */
+ * observations from one keyframe.  Each new pair takes an observation id for the map's life (8 B of
+ * device memory per pair ever added; compaction reclaims rows, not ids). */
 int vx_dmap_add_observations(vx_dmap* map, int n, const uint64_t* lm_id, const uint64_t* kf_id,
                              const uint64_t* feat_idx);
 /* Landmark::RemoveObservation(kf_id) (landmark.h:37-40): the pair stops counting towards

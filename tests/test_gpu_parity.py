@@ -612,7 +612,7 @@ def test_seq_replay_matches_direct_calls(ctx, oracle, slot_sums):
     e.close(), b.close()
 
 
-def test_seq_threads_replay(ctx, oracle):
+def test_seq_threads_replay(ctx, oracle, slot_sums):
     """vx_seq_set_threads(>1): each context's calls on a host thread of its own, the cross-context
     event order kept on the host — the bench's 3-extraction-context pipeline over 24 frames gives the
     same matches and LocalBA statistics as the single-thread replay."""
@@ -664,6 +664,23 @@ def test_seq_threads_replay(ctx, oracle):
                         list(plan.fetch().obs))
         sq.close()
     assert out[1] == out[4]
+    # a call failing on one context's thread: the error is reported, the lanes waiting on its events
+    # issue nothing more, and the contexts stay usable for the next good replay
+    bad = vxslam.Seq()
+    bad.extract(ex[0], p, fd[0].data_ptr(), 640, 480, 2, 640 * 3, 0)  # 2 channels: VX_ERR_INVALID
+    bad.record(ex[0], ev_e[0])
+    bad.wait(bc, ev_e[0])
+    bad.ba_run(bc, plan)
+    bad.set_threads(2)
+    with pytest.raises(vxslam.VxError):
+        bad.run()
+    bad.close()
+    sq = build(4)
+    sq.run()
+    for c in ex + [bc]:
+        c.synchronize()
+    assert [ex[ci].match_fetch().tobytes() for ci in range(E)] == out[1][0]
+    sq.close()
     for x in ev_e + ev_m + [plan]:
         x.close()
     for c in ex + [bc]:

@@ -34,7 +34,11 @@ struct vx_dmap {
     };
     std::unordered_map<std::pair<int, uint64_t>, int64_t, PairHash> obs_index;
     int64_t n_lm = 0, n_obs = 0;                 // rows (removed ones included)
-    int64_t n_ids = 0;                           // observation ids issued
+    // observation ids issued.  id_row (8 B per id) grows with every observation ever added:
+    // compaction shrinks the rows, not the ids (re-issuing them would rewrite obs_index on the host
+    // at every compaction).  10^7 observations added over a map's life = 80 MB of HBM, ~0.03 % of
+    // the 288 GB; a session that must bound it recreates the vx_dmap (documented growth).
+    int64_t n_ids = 0;
     int64_t n_kf_live = 0, n_lm_live = 0, n_obs_live = 0;
     std::vector<int> lm_obs_live;                // live observations per landmark row
     std::vector<uint8_t> lm_removed;             // 1 after Map::RemoveLandmark (row kept as dead storage)

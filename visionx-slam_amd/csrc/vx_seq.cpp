@@ -155,6 +155,11 @@ void run_lane(vx_seq* s, int l, uint64_t g) {
                     if (s->err.load(std::memory_order_relaxed)) break;  // (a failed lane marks its ops)
                     std::this_thread::yield();
                 }
+            // another lane failed: its ops were marked issued without running, so this op's
+            // cross-context order is no longer guaranteed — issue nothing more
+            if (s->err.load(std::memory_order_acquire)) failed = true;
+        }
+        if (!failed) {
             const int rc = run_op(s->ops[i]);
             if (rc != VX_OK) {
                 failed = true;

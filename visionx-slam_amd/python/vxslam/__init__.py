@@ -769,21 +769,28 @@ class Seq:
         if lib().vx_seq_create(C.byref(self._h)) != VX_OK:
             raise VxError(VX_ERR_INVALID, "vx_seq_create failed")
         self._ctxs = {}
+        # every object whose raw handle or device memory a recorded call names (events, plans, the
+        # tensors behind image pointers when given): the header requires them to outlive the
+        # sequence, so the sequence holds them until close()
+        self._keep = []
 
-    def _add(self, rc, ctx):
+    def _add(self, rc, ctx, *keep):
         if rc != VX_OK:
             raise VxError(rc, "vx_seq: bad arguments")
         self._ctxs[len(self)] = ctx
+        self._keep.extend(k for k in keep if k is not None)
 
     def wait(self, ctx, ev):
-        self._add(lib().vx_seq_wait(self._h, ctx.handle, ev._h), ctx)
+        self._add(lib().vx_seq_wait(self._h, ctx.handle, ev._h), ctx, ev)
 
     def record(self, ctx, ev):
-        self._add(lib().vx_seq_record(self._h, ctx.handle, ev._h), ctx)
+        self._add(lib().vx_seq_record(self._h, ctx.handle, ev._h), ctx, ev)
 
-    def extract(self, ctx, params, d_img, w, h, ch, stride, slot):
+    def extract(self, ctx, params, d_img, w, h, ch, stride, slot, owner=None):
+        """d_img: a device pointer (int); owner: the object holding that memory (e.g. the torch
+        tensor), kept alive with the sequence."""
         self._add(lib().vx_seq_extract(self._h, ctx.handle, C.byref(params), C.c_void_p(d_img), w, h, ch, stride, slot),
-                  ctx)
+                  ctx, owner, params)
 
     def match(self, ctx, q, t, ratio=0.8):
         """q / t: (desc, count, cap) device triples (Context.slot_device)."""
@@ -791,7 +798,7 @@ class Seq:
                                      C.c_void_p(t[1]), t[2], C.c_float(ratio)), ctx)
 
     def ba_run(self, ctx, plan):
-        self._add(lib().vx_seq_ba_run(self._h, ctx.handle, plan._h), ctx)
+        self._add(lib().vx_seq_ba_run(self._h, ctx.handle, plan._h), ctx, plan)
 
     def __len__(self):
         return lib().vx_seq_length(self._h)
@@ -812,6 +819,7 @@ class Seq:
         if self._h:
             lib().vx_seq_destroy(self._h)
             self._h = C.c_void_p()
+        self._keep = []
 
     def __del__(self):
         try:
