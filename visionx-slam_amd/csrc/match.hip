@@ -76,8 +76,8 @@ __global__ __launch_bounds__(kQB) void k_knn_partial(const uint8_t* __restrict__
 // merged per query by one wave (LDS transpose, then DPP), then the ratio test.
 // The merge of two lexicographic top-2s is exact in any order, so the result is the sequential
 // scan's (the chunked kernels above stay for comparison: VX_MATCH_CHUNKED=1).
-constexpr int kRQ = 8;     // queries per workgroup
-constexpr int kRT = 512;   // threads per workgroup
+constexpr int kRQ = 8;     // queries per workgroup (default shape)
+constexpr int kRT = 512;   // threads per workgroup (default shape)
 
 __device__ __forceinline__ void top2_merge(unsigned& k1, unsigned& k2, unsigned o1, unsigned o2) {
     const unsigned n2 = min(max(k1, o1), min(k2, o2));
@@ -94,37 +94,40 @@ __device__ __forceinline__ void top2_dpp(unsigned& k1, unsigned& k2) {
     top2_merge(k1, k2, o1, o2);
 }
 
-static_assert(kRT / 64 == kRQ, "k_knn_rows: one wave per query in the reduction");
-
+// RQ queries (wave-uniform operands) against the whole train set by RT threads; then the LDS
+// transpose, each wave reducing RQ / (RT / 64) queries.  The workgroups take query groups
+// blockIdx.x, blockIdx.x + gridDim.x, ... (a grid smaller than the capacity's query groups loops).
+template <int RQ, int RT>
 __device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, int nq, const uint8_t* __restrict__ t,
-                                         int nt, float ratio, unsigned* __restrict__ best, uint2 (*tr)[kRT]) {
-    const int q0 = blockIdx.x * kRQ;
-    if (q0 >= nq) return;  // block-uniform
+                                         int nt, float ratio, unsigned* __restrict__ best, uint2 (*tr)[RT]) {
+    constexpr int kW = RT / 64, kQPW = RQ / kW;
+    static_assert(RQ % kW == 0, "k_knn_rows: whole queries per reducing wave");
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-    uint4 A0[kRQ], A1[kRQ];
+    for (int q0 = blockIdx.x * RQ; q0 < nq; q0 += gridDim.x * RQ) {  // (block-uniform)
+    uint4 A0[RQ], A1[RQ];
 #pragma unroll
-    for (int i = 0; i < kRQ; ++i) {
+    for (int i = 0; i < RQ; ++i) {
         const int qi = min(q0 + i, nq - 1);  // (past the end: a copy of the last query, not written)
         A0[i] = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[0];
         A1[i] = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[1];
     }
-    unsigned k1[kRQ], k2[kRQ];
+    unsigned k1[RQ], k2[RQ];
 #pragma unroll
-    for (int i = 0; i < kRQ; ++i) k1[i] = k2[i] = kNone;
-    for (int r0 = tid; r0 < nt; r0 += 4 * kRT) {
+    for (int i = 0; i < RQ; ++i) k1[i] = k2[i] = kNone;
+    for (int r0 = tid; r0 < nt; r0 += 4 * RT) {
         uint4 B0[4], B1[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int row = min(r0 + j * kRT, nt - 1);
+            const int row = min(r0 + j * RT, nt - 1);
             B0[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[0];
             B1[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[1];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int row = r0 + j * kRT;
+            const int row = r0 + j * RT;
             const unsigned tag = row < nt ? (unsigned)row : 0u;
 #pragma unroll
-            for (int i = 0; i < kRQ; ++i) {
+            for (int i = 0; i < RQ; ++i) {
                 unsigned d = __builtin_popcount(A0[i].x ^ B0[j].x);
                 d += __builtin_popcount(A0[i].y ^ B0[j].y);
                 d += __builtin_popcount(A0[i].z ^ B0[j].z);
@@ -139,41 +142,49 @@ __device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, int nq, 
             }
         }
     }
-    // transpose through LDS: wave w then reduces query w — 8 entries per lane, then the 64 lanes by
-    // DPP (xor 1, xor 2, half-row and row mirrors, row broadcasts 15 / 31: lane 63 ends with all)
+    // transpose through LDS: wave w then reduces queries w * kQPW .. — RT / 64 entries per lane,
+    // then the 64 lanes by DPP (xor 1, xor 2, half-row and row mirrors, row broadcasts 15 / 31:
+    // lane 63 ends with all)
 #pragma unroll
-    for (int i = 0; i < kRQ; ++i) tr[i][tid] = make_uint2(k1[i], k2[i]);
+    for (int i = 0; i < RQ; ++i) tr[i][tid] = make_uint2(k1[i], k2[i]);
     __syncthreads();
-    unsigned a1 = kNone, a2 = kNone;
 #pragma unroll
-    for (int g = 0; g < kRT / 64; ++g) {
-        const uint2 v = tr[wv][64 * g + lane];
-        top2_merge(a1, a2, v.x, v.y);
-    }
-    top2_dpp<0xB1>(a1, a2);        // quad_perm [1,0,3,2]
-    top2_dpp<0x4E>(a1, a2);        // quad_perm [2,3,0,1]
-    top2_dpp<0x141>(a1, a2);       // row_half_mirror
-    top2_dpp<0x140>(a1, a2);       // row_mirror
-    top2_dpp<0x142, 0xA>(a1, a2);  // row_bcast:15 into rows 1, 3
-    top2_dpp<0x143, 0xC>(a1, a2);  // row_bcast:31 into rows 2, 3
-    if (lane == 63 && q0 + wv < nq) {
-        bool keep = false;
-        if (a2 != kNone) {  // knn.size() == 2 (orb_matcher.cpp:28)
-            const float d1 = (float)(a1 >> 22), d2 = (float)(a2 >> 22);
-            keep = d1 < ratio * d2;  // orb_matcher.cpp:33
+    for (int qq = 0; qq < kQPW; ++qq) {
+        const int qw = wv * kQPW + qq;
+        unsigned a1 = kNone, a2 = kNone;
+#pragma unroll
+        for (int g = 0; g < RT / 64; ++g) {
+            const uint2 v = tr[qw][64 * g + lane];
+            top2_merge(a1, a2, v.x, v.y);
         }
-        best[q0 + wv] = keep ? a1 : kNone;
+        top2_dpp<0xB1>(a1, a2);        // quad_perm [1,0,3,2]
+        top2_dpp<0x4E>(a1, a2);        // quad_perm [2,3,0,1]
+        top2_dpp<0x141>(a1, a2);       // row_half_mirror
+        top2_dpp<0x140>(a1, a2);       // row_mirror
+        top2_dpp<0x142, 0xA>(a1, a2);  // row_bcast:15 into rows 1, 3
+        top2_dpp<0x143, 0xC>(a1, a2);  // row_bcast:31 into rows 2, 3
+        if (lane == 63 && q0 + qw < nq) {
+            bool keep = false;
+            if (a2 != kNone) {  // knn.size() == 2 (orb_matcher.cpp:28)
+                const float d1 = (float)(a1 >> 22), d2 = (float)(a2 >> 22);
+                keep = d1 < ratio * d2;  // orb_matcher.cpp:33
+            }
+            best[q0 + qw] = keep ? a1 : kNone;
+        }
+    }
+    __syncthreads();  // (the next group's transpose overwrites tr)
     }
 }
 
-__global__ __launch_bounds__(kRT) void k_knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p,
-                                                  int nq_host, const uint8_t* __restrict__ t,
-                                                  const int* __restrict__ nt_p, int nt_host, float ratio,
-                                                  unsigned* __restrict__ best) {
-    __shared__ uint2 tr[kRQ][kRT];  // the threads' top-2s, query-major (32 KB)
+template <int RQ, int RT>
+__global__ __launch_bounds__(RT) void k_knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p,
+                                                 int nq_host, const uint8_t* __restrict__ t,
+                                                 const int* __restrict__ nt_p, int nt_host, float ratio,
+                                                 unsigned* __restrict__ best) {
+    __shared__ uint2 tr[RQ][RT];  // the threads' top-2s, query-major
     const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
     const int nt = nt_p ? min(*nt_p, nt_host) : nt_host;
-    knn_rows(q, nq, t, nt, ratio, best, tr);
+    knn_rows<RQ, RT>(q, nq, t, nt, ratio, best, tr);
 }
 
 // Batched matching (vx_match_batch_async): pair blockIdx.y's sets from the table, per-pair results
@@ -190,7 +201,7 @@ __global__ __launch_bounds__(kRT) void k_knn_rows_batch(PairTab tab, int q_cap, 
     __shared__ uint2 tr[kRQ][kRT];
     const int p = blockIdx.y;
     const int nq = min(*tab.nq[p], q_cap), nt = min(*tab.nt[p], t_cap);
-    knn_rows(tab.q[p], nq, tab.t[p], nt, ratio, best + (long long)p * q_cap, tr);
+    knn_rows<kRQ, kRT>(tab.q[p], nq, tab.t[p], nt, ratio, best + (long long)p * q_cap, tr);
 }
 
 // Exclusive block scan: wave prefix by __shfl_up, then the NT/64 wave totals from LDS (two
@@ -301,8 +312,41 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact_batch(const unsigne
                 out_count + 4 * p, sh);
 }
 
+// k_knn_rows' shape: $VX_MATCH_SHAPE = "<queries>x<threads>" (8x512 default; 4x256, 16x512,
+// 16x1024 for A/B runs) and $VX_MATCH_GRID = workgroups (0: one per query group of the capacity;
+// fewer: the groups are looped over), read once
+template <int RQ, int RT>
+int knn_rows_launch_t(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt, const int* dnt,
+                      int nt_host, int q_cap, float ratio, unsigned* best, int grid_cap) {
+    int g = (q_cap + RQ - 1) / RQ;
+    if (grid_cap > 0) g = std::min(g, grid_cap);
+    VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows<RQ, RT>, dim3(std::max(g, 1)), dim3(RT), 0, c->stream, dq, dnq,
+                     nq_host, dt, dnt, nt_host, ratio, best));
+    return VX_OK;
+}
+int knn_rows_launch(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt, const int* dnt,
+                    int nt_host, int q_cap, float ratio, unsigned* best) {
+    static const int shape = [] {
+        const char* e = getenv("VX_MATCH_SHAPE");
+        if (!e) return 0;
+        const std::string v(e);
+        return v == "4x256" ? 1 : v == "16x512" ? 2 : v == "16x1024" ? 3 : 0;
+    }();
+    static const int grid_cap = [] {
+        const char* e = getenv("VX_MATCH_GRID");
+        return e ? atoi(e) : 0;
+    }();
+    switch (shape) {
+        case 1: return knn_rows_launch_t<4, 256>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        case 2: return knn_rows_launch_t<16, 512>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        case 3: return knn_rows_launch_t<16, 1024>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        default: return knn_rows_launch_t<kRQ, kRT>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+    }
+}
+
 int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt,
                   const int* dnt, int nt_host, int q_cap, int t_cap, float ratio) {
+    int rc;
     const int n_chunks = (t_cap + kTC - 1) / kTC;
     const int q_stride = q_cap;
     VX_HIP(c, c->partial.ensure((size_t)n_chunks * q_stride * sizeof(uint2) + (size_t)q_cap * sizeof(unsigned) + 16));
@@ -315,8 +359,7 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
     }();
     if (!chunked) {
         unsigned* best = reinterpret_cast<unsigned*>(c->partial.as<uint2>() + (size_t)n_chunks * q_stride);
-        VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows, dim3((q_cap + kRQ - 1) / kRQ), dim3(kRT), 0, c->stream, dq,
-                         dnq, nq_host, dt, dnt, nt_host, ratio, best));
+        if ((rc = knn_rows_launch(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best))) return rc;
         ProfScope ps(c, kStMatchMerge);
         hipLaunchKernelGGL(k_knn_compact, dim3(1), dim3(kMergeBlock), 0, c->stream, best, dnq, nq_host,
                            c->matches.as<vx_match>(), c->match_count.as<int>());

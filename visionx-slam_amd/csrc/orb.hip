@@ -1883,32 +1883,58 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         const int c0 = base + tid * cpt;
         int cnts[kCellsPer];
         int tot = 0;
+        // slots 0 and 1 of the thread's cells are loaded with the counts, not after them: most cells
+        // hold 0-2 records, so most records come without a second dependent global load (the slots
+        // are valid memory whatever the count; a stale one is never used)
+        CandRec sp0[kCellsPer], sp1[kCellsPer];
 #pragma unroll
-        for (int j = 0; j < kCellsPer; ++j) cnts[j] = (j < cpt && c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
+        for (int j = 0; j < kCellsPer; ++j) {
+            const bool ok = j < cpt && c0 + j < ncell;
+            cnts[j] = ok ? cell_count[cbase + c0 + j] : 0;
+            sp0[j] = ok ? cand[cand_at(cbase + c0 + j, 0, a.fs_cells)] : CandRec{};
+            sp1[j] = ok ? cand[cand_at(cbase + c0 + j, 1, a.fs_cells)] : CandRec{};
+        }
 #pragma unroll
         for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
-        auto rec_index = [&](int k) {
-            int j = 0, i = k;
+        auto rec_cell = [&](int k, int& i) {  // the cell (0..kCellsPer) and slot i of the thread's k-th record
+            int j = 0;
+            i = k;
 #pragma unroll
             for (int jj = 0; jj < kCellsPer; ++jj)
                 if (j == jj && i >= cnts[jj]) {
                     i -= cnts[jj];
                     j = jj + 1;
                 }
+            return j;
+        };
+        auto rec_index = [&](int k) {
+            int i;
+            const int j = rec_cell(k, i);
             return cand_at(cbase + c0 + j, i, a.fs_cells);
+        };
+        auto rec_get = [&](int k) -> CandRec {
+            int i;
+            const int j = rec_cell(k, i);
+            if (i >= 2) return cand[cand_at(cbase + c0 + j, i, a.fs_cells)];
+            CandRec r{};
+#pragma unroll
+            for (int jj = 0; jj < kCellsPer; ++jj)
+                if (jj == j) r = i == 0 ? sp0[jj] : sp1[jj];
+            return r;
         };
         CandRec rr[kRecBatch];
 #pragma unroll
-        for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? cand[rec_index(k)] : CandRec{};
+        for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? rec_get(k) : CandRec{};
         int btot;
         int pos = n0 + block_scan_excl<kStlNT>(tot, sw, btot);
         auto put = [&](const CandRec& r) {
             kept[pos] = r;
             const unsigned e = ((unsigned)r.score << 24) | (unsigned)pos;
-            gA1[pos] = e;
-            if (pos < kRgCap32) {
+            if (pos < kRgCap32) {  // (the global copy only when the level outgrows the LDS: below)
                 lA1[pos] = e;
                 lhk[pos] = harris_key(r.harris);
+            } else {
+                gA1[pos] = e;
             }
             ++pos;
         };
@@ -1919,6 +1945,10 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         n0 += uni(btot);
     }
     __syncthreads();
+    if (n0 > kRgCap32) {  // the whole pass-1 array then lives in the global scratch
+        for (int i = tid; i < kRgCap32; i += kStlNT) gA1[i] = lA1[i];
+        __syncthreads();
+    }
     VX_KT(9);
     // ---- retainBest(2q) by FAST score (u32 elements; beyond the engine's capacity the first
     // passes run over the global scratch with mailboxes of n0 / 2 + 1 each after it)
