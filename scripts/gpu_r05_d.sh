@@ -12,7 +12,9 @@ tail -1 $O/par.log
 timeout -k 10 300 $T tests/test_gpu_stl_order.py tests/test_gpu_orb_stages.py tests/test_gpu_batch.py -m gpu > $O/orb.log 2>&1 || { tail -30 $O/orb.log; exit 2; }
 tail -1 $O/orb.log
 VX_LIB=visionx-slam_amd/lib/libvxslam_trace.so timeout -k 10 120 python3 scripts/ktrace_select.py > $O/ktrace_select.txt 2>&1 || { tail -20 $O/ktrace_select.txt; exit 9; }
+VX_SEL_TAILN=0 VX_LIB=visionx-slam_amd/lib/libvxslam_trace.so timeout -k 10 120 python3 scripts/ktrace_select.py > $O/ktrace_select_tailn0.txt 2>&1 || { tail -20 $O/ktrace_select_tailn0.txt; exit 9; }
 head -10 $O/ktrace_select.txt
+head -3 $O/ktrace_select_tailn0.txt
 ( timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d $O/kt -o kt -- python3 scripts/ba_alone.py > $O/kt.log 2>&1 ) || { tail -20 $O/kt.log; exit 5; }
 python3 scripts/ba_iter_durations.py "$(find $O/kt -name 'kt_kernel_trace.csv' | head -1)" > $O/durations.txt 2>&1
 rm -f $(find $O/kt -name '*.csv')

@@ -45,6 +45,8 @@ VX_KP_TABLE();
 
 __constant__ signed char c_pattern[1024];
 __constant__ int c_umax[16];
+// the selection's register-resident steps over 2 / 4 blocks (rg_tailN; $VX_SEL_TAILN=0: wave passes)
+__constant__ int c_sel_tailn;
 // ICAngles row masks: row lane (v = lane - 15), byte k of the 32-byte window starting at u = -15
 // is 0xff iff |k - 15| <= umax[|v|] (row 31 empty)
 __constant__ __attribute__((aligned(16))) unsigned c_icmask[32][8];
@@ -1641,6 +1643,100 @@ __device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int
     l = f0 + ll;
 }
 
+// The same register-resident introselect steps over NB blocks (a range of <= 64 NB elements on wave
+// 0): lane i of block j holds A[f0 + 64 j + i] for the whole tail, a step's range is the window
+// [lf, ll) of those positions.  Pivot candidates come from v_readlane of every block and a scalar
+// select by the (uniform) block index — no register array is indexed at run time, so nothing goes
+// to scratch — and the cut from the L / R ballots.  Only the swapped pairs go through the
+// mailboxes.  Stops when the window fits the next narrower engine (<= 32 NB, written back: the
+// caller continues there), at <= 3 or at the depth limit; f / l the window, A updated.
+template <int NB, class T>
+__device__ __forceinline__ void rg_tailN(T* __restrict__ A, int& f, int& l, int nth, int& depth, bool& heap,
+                                         const RgLds& E) {
+    const int lane = threadIdx.x & 63;
+    const int f0 = f, n0 = l - f;
+    T v[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) v[j] = A[f0 + min(64 * j + lane, n0 - 1)];
+    T* eb = E.bl<T>();
+    constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
+    const int kth = nth - f0;
+    int lf = 0, ll = n0;
+    auto rd = [&](int p) -> T {  // A[f0 + p], p uniform
+        T r = T(0);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const T x = rdl(v[j], p & 63);
+            r = (j == (p >> 6)) ? x : r;
+        }
+        return r;
+    };
+    while (ll - lf > 32 * NB && ll - lf > 3) {
+        if (depth == 0) {
+            heap = true;
+            break;
+        }
+        --depth;
+        const int a = lf + 1, b = lf + (ll - lf) / 2, c = ll - 1;
+        const T vf = rd(lf), va = rd(a), vb = rd(b), vc = rd(c);
+        T pv;
+        const int m = stl_median(a, b, c, va, vb, vc, pv);
+        const unsigned P = sel_key(pv);
+        bool il[NB], ir[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const int x = 64 * j + lane;
+            v[j] = x == lf ? pv : x == m ? vf : v[j];
+            const bool in = x > lf && x < ll;
+            const unsigned k = sel_key(v[j]);
+            il[j] = in && k <= P;
+            ir[j] = in && k >= P;
+        }
+        int ra[NB], rb[NB];
+        rg_ranks(il, ir, 0, 0, ra, rb);
+        int nr = 0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) nr += __popcll(__ballot(ir[j]));
+        const int K = rg_crossing(il, ir, ra, rb, 0, 0, nr);
+        const int hr = K > 0 ? nr - K : INT_MAX;
+        bool sw[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
+            sw[j] = sl || sr;
+            eb[sl ? ra[j] : sr ? kBr + (nr - 1 - rb[j]) : kTv + lane] = v[j];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        T nv[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
+            nv[j] = eb[sl ? kBr + ra[j] : sr ? nr - 1 - rb[j] : kTv + lane];
+        }
+        int cut = INT_MAX;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const u64 cl = __ballot(il[j] && ra[j] == K), cr = __ballot(ir[j] && rb[j] == hr);
+            if (cl) cut = min(cut, 64 * j + __ffsll((long long)cl) - 1);
+            if (cr) cut = min(cut, 64 * j + __ffsll((long long)cr) - 1);
+        }
+        cut = min(max(cut, lf + 1), ll);  // (clamped: memory-safe whatever happens)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) v[j] = sw[j] ? nv[j] : v[j];
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (next step's mailbox writes after these reads)
+        __builtin_amdgcn_wave_barrier();
+        if (cut <= kth) lf = cut;
+        else ll = cut;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+        if (64 * j + lane < n0) A[f0 + 64 * j + lane] = v[j];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    f = f0 + lf;
+    l = f0 + ll;
+}
+
 // libstdc++'s closing __insertion_sort of A[0, n) (n <= 3; a stable sort by key, descending):
 // every lane of the calling wave reads the elements, lane 0 writes them back
 template <class T>
@@ -1780,6 +1876,12 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
                 VX_KP((5 << 24) | (l - f));
                 rg_tail64(A, f, l, nth, depth, heap, E);
                 break;
+            }
+            if (c_sel_tailn && l - f <= 256) {  // register-resident steps over 4 / 2 blocks, then the above
+                VX_KP((6 << 24) | (l - f));
+                if (l - f > 128) rg_tailN<4>(A, f, l, nth, depth, heap, E);
+                else rg_tailN<2>(A, f, l, nth, depth, heap, E);
+                continue;
             }
             if (depth == 0) {
                 heap = true;
@@ -2422,6 +2524,9 @@ int upload_constants(vx_ctx* c) {
             if (k - 15 >= -d && k - 15 <= d) icmask[r][k >> 2] |= 0xffu << (8 * (k & 3));
     }
     VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icmask, sizeof(icmask)));
+    const char* tn = std::getenv("VX_SEL_TAILN");
+    const int tailn = tn && tn[0] == '0' ? 0 : 1;
+    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_sel_tailn), &tailn, sizeof(tailn)));
     // the selection kernels' 160 KB of dynamic LDS, per device (set with the device current; a failure
     // is reported every time, since the device is only marked done after it succeeded: ADVICE r3)
     VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_stl), hipFuncAttributeMaxDynamicSharedMemorySize,
