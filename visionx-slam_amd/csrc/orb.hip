@@ -1857,7 +1857,9 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
         if (cut <= nth) f = cut;
         else l = cut;
     }
-    while (!heap && l - f > kRgWave) {
+    // (wave 0's register-resident steps take ranges up to 512; team passes the longer ones)
+    const int wave_cap = c_sel_tailn ? 512 : kRgWave;
+    while (!heap && l - f > wave_cap) {
         if (depth == 0) {
             heap = true;
             break;
@@ -1877,9 +1879,10 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
                 rg_tail64(A, f, l, nth, depth, heap, E);
                 break;
             }
-            if (c_sel_tailn && l - f <= 256) {  // register-resident steps over 4 / 2 blocks, then the above
+            if (c_sel_tailn && l - f <= 512) {  // register-resident steps over 8 / 4 / 2 blocks, then the above
                 VX_KP((6 << 24) | (l - f));
-                if (l - f > 128) rg_tailN<4>(A, f, l, nth, depth, heap, E);
+                if (l - f > 256) rg_tailN<8>(A, f, l, nth, depth, heap, E);
+                else if (l - f > 128) rg_tailN<4>(A, f, l, nth, depth, heap, E);
                 else rg_tailN<2>(A, f, l, nth, depth, heap, E);
                 continue;
             }
