@@ -559,38 +559,37 @@ __device__ __forceinline__ void store_acc_opo(double* S, d4 v) {
 // factor.  Lane i holds row i in registers.  Per column j the pivot comes from lane j
 // (v_readlane), every lane scales its entry and takes the column's other entries from their lanes
 // by v_readlane for its rank-1 update — no LDS round trip on the chain, which per column is
-// readlane -> rsq (+ Newton) -> mul -> readlane -> fma; the column also goes to the LDS image
-// `lcol` for the inverse, off the chain.
-// L^-1 (lane i = column i, right-looking forward substitution over the LDS columns) is written as
-// an operand-order LDS image and row-major to Lg.  Returns false on a non-positive pivot.
+// readlane -> rsq (+ Newton) -> mul -> readlane -> fma.
+// L^-1 (lane i = column i): the forward substitution's step j needs only column j of L and its
+// 1 / L_jj — the same readlanes and the same (uniform) reciprocal square root the factor's column
+// j uses — so it runs inside the same loop, its two-op chain beside the factor's (the same
+// operations in the same order per lane as a separate substitution after the factor: bitwise the
+// same L^-1).  Written as an operand-order LDS image and row-major to Lg.  Returns false on a
+// non-positive pivot.  (lcol: unused scratch, kept for the callers' LDS layout.)
 __device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
+    (void)lcol;
     const int lane = threadIdx.x & 63, i = lane & 15;
     double a[16];
 #pragma unroll
     for (int c = 0; c < 16; ++c) a[c] = c <= i ? A[(long long)i * ld + c] : A[(long long)c * ld + i];
-    double srow = 0.0;  // lane i: 1 / L_ii
+    double x[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = r == i ? 1.0 : 0.0;
     bool ok = true;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const double d = rl(a[j], j);
         ok = ok && d > 0.0 && d < 1e300;
-        const double r = frsq(d > 0.0 ? d : 1.0);
-        if (i == j) srow = r;
+        const double r = frsq(d > 0.0 ? d : 1.0);  // (uniform: 1 / L_jj)
         const double l = a[j] * r;  // L[i][j] for i >= j
         a[j] = l;
-        if (lane < 16) lcol[16 * j + i] = l;
+        x[j] *= r;
 #pragma unroll
-        for (int c = j + 1; c < 16; ++c) a[c] = fma(-l, rl(l, c), a[c]);  // (L[c][j] from lane c)
-    }
-    if (lane < 16) lcol[256 + i] = srow;
-    double x[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) x[r] = r == i ? 1.0 : 0.0;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        x[j] *= lcol[256 + j];
-#pragma unroll
-        for (int m = j + 1; m < 16; ++m) x[m] = fma(-lcol[16 * j + m], x[j], x[m]);
+        for (int c = j + 1; c < 16; ++c) {
+            const double lc = rl(l, c);  // L[c][j] from lane c
+            a[c] = fma(-l, lc, a[c]);
+            x[c] = fma(-lc, x[j], x[c]);
+        }
     }
     if (lane < 16) {
 #pragma unroll
