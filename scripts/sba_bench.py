@@ -45,6 +45,17 @@ for cfg, (nk, nl, ns), cf in CFGS:
     plan.fetch()
     prof = ctx.prof_read()
     ctx.prof_enable(False)
+    # the dense pose solve on MFMA: algorithmic FP64 flops of the symbolic tile
+    # factorisation (vx_sba_plan_factor_work) per factorisation, times the factorisations of the run
+    # (every iteration before the last that is not a rejection), over the run's sba_solve time
+    work = plan.factor_work()
+    steps = [int(x) for x in list(st.step)[:st.iterations]]
+    n_fac = sum(1 for i in range(max(st.iterations - 1, 0)) if steps[i] != 0)
+    solve_ms = prof.get("sba_solve", (0.0, 0))[0]
+    tfs = work["flops"] * n_fac / (solve_ms * 1e-3) / 1e12 if solve_ms > 0 else None
+    mfma = {"flops_per_factorisation": work["flops"], "factorisations": n_fac, "solve_ms_per_run": round(solve_ms, 4),
+            "achieved_tflops": round(tfs, 4) if tfs else None, "peak_tflops": 78.6,
+            "fp64_frac": round(tfs / 78.6, 6) if tfs else None, "tiles": work}
     print(json.dumps({"config": cfg, "window_kf": nk, "landmarks": nl, "streams": ns, "plan": plan.info(),
                       "ms_per_optimize": round(ms, 4), "iterations": st.iterations, "accepted": st.accepted,
                       "cost": [round(st.initial_cost, 1), round(st.final_cost, 1)],
@@ -53,7 +64,8 @@ for cfg, (nk, nl, ns), cf in CFGS:
                       "kernel_us_per_launch": {k: round(v[0] * 1e3 / v[1], 2) for k, v in prof.items()
                                                if k.startswith("sba") and v[1]},
                       "kernel_us_per_iteration": {k: round(v[0] * 1e3 / max(st.iterations, 1), 2)
-                                                  for k, v in prof.items() if k.startswith("sba") and v[1]}}),
+                                                  for k, v in prof.items() if k.startswith("sba") and v[1]},
+                      "mfma_fp64": mfma}),
           flush=True)
     plan.close()
 ctx.close()
