@@ -874,60 +874,13 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
             }
         }
     }
-    // (c') with row sums by atomics the entry's thread reads its row itself, as soon as its entry
-    // record is in: no combine phase, no LDS round trip and no barrier before the pose solve
-    // (the 1024-thread layout keeps the combine and its waves' own rounds: 128 VGPRs leave no room
-    // for the row in registers or the waves' round table)
-    constexpr bool kLean = kFT <= kFTSmall;
-    const bool drow = kLean && !kPro && arow && (it > 0 || f.apro);
-    double Sd[kNTerms];
-    if (drow && tid < kFK && ke.x >= 0) {
-        const double* rp = arow + ((size_t)arow_rd(it) * f.n_kf + (ke.x & 0x3fffffff)) * kStride;
-#pragma unroll
-        for (int t = 0; t < kNTerms; ++t) Sd[t] = rp[t];
-    }
     // (d) this wave's first pose-stage round (round r + 1 is requested when round r is consumed)
     const bool pose_next = kPro || it + 1 < a.max_iter;
-    // With row sums by atomics (FusedArgs::arow) a keyframe entry's pose-stage rounds need not stay
-    // on one wave: every wave's partial is added to the row.  The workgroup's rounds (the waves'
-    // lists, wave-major, as laid out) are then dealt to the waves in contiguous ranges of
-    // ceil-balanced length — wave w takes rounds [w R / kFW, (w + 1) R / kFW) of the R in all —
-    // so the busiest wave runs ceil(R / kFW) rounds instead of its entries' (4 of 11 at C3), and
-    // each wave flushes one partial per entry segment it touches.
-    const bool bal = kLean && arow && (!kPro || f.apro);
-    int wr_s[kFW], wr_n[kFW];  // every wave's {start, rounds} (uniform)
-    int bk0 = 0, bk1 = 0, bwp = 0, brw = 0;
-#pragma unroll
-    for (int i = 0; i < kFW / 2; ++i) {
-        const int4 w4 = kLean ? f.blk[(size_t)b * (1 + kFW / 2) + 1 + i] : make_int4(0, 0, 0, 0);
-        wr_s[2 * i] = w4.x, wr_n[2 * i] = w4.y, wr_s[2 * i + 1] = w4.z, wr_n[2 * i + 1] = w4.w;
-    }
-    if (bal) {
-        int R = 0;
-#pragma unroll
-        for (int i = 0; i < kFW; ++i) R += wr_n[i];
-        bk0 = wv * R / kFW;
-        bk1 = (wv + 1) * R / kFW;
-        // (wave, round) of round bk0
-        int rem = bk0;
-        bwp = kFW;
-#pragma unroll
-        for (int i = 0; i < kFW; ++i) {
-            if (bwp == kFW && rem < wr_n[i]) bwp = i;
-            if (bwp == kFW) rem -= wr_n[i];
-        }
-        brw = rem;
-        if (bwp == kFW) bk1 = bk0;  // (no rounds: R == 0 or beyond the end)
-    }
     double2 u0 = make_double2(0, 0);
     double4 p0 = make_double4(0, 0, 0, 0);
-    if (pose_next && (bal ? bk0 < bk1 : wrounds > 0)) {
-        int a0 = wstart;
-#pragma unroll
-        for (int i = 0; i < kFW; ++i)
-            if (bal && i == bwp) a0 = wr_s[i] + 64 * brw;
-        u0 = f.pobs_uv[a0 + lane];
-        p0 = f.pobs_p[a0 + lane];
+    if (pose_next && wrounds > 0) {
+        u0 = f.pobs_uv[wstart + lane];
+        p0 = f.pobs_p[wstart + lane];
     }
     const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
     const bool has_o = !kPro && tid < n_ob, own = tid < n_lm;
@@ -948,7 +901,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     __syncthreads();  // s_ke / s_kd
     if (!kPro) {
         // ---- combine: S of entry j, term t = the row's partial slots summed in slot order
-        for (int pr = tid; !drow && pr < n_ent * kNTerms; pr += kFT) {
+        for (int pr = tid; pr < n_ent * kNTerms; pr += kFT) {
             const int j = pr / kNTerms, t = pr - j * kNTerms;
             const int4 e = s_ke[j];
             if (e.x < 0) continue;  // a hole in the entry positions
@@ -1004,7 +957,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
             }
         }
     }
-    if (!drow) __syncthreads();  // (kslot's combined rows)
+    __syncthreads();
     FKT(2);
     // ---- pose solve of the entries (local_ba.cpp:163-173); owners publish
     if (ke.x >= 0) {
@@ -1018,7 +971,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         if (!kPro) {
             double S[kNTerms];
 #pragma unroll
-            for (int t = 0; t < kNTerms; ++t) S[t] = drow ? Sd[t] : sl[t];
+            for (int t = 0; t < kNTerms; ++t) S[t] = sl[t];
             solve_pose(a, (int)ts[12], S, T, R);
             if (ke.x & (1 << 30)) {
                 double* Tout = pose_out(a, it) + 8 * (size_t)(ke.x & 0x3fffffff);
@@ -1040,17 +993,15 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
 #pragma unroll
         for (int j = 0; j < 4; ++j) sl[17 + j] = C[j];
     }
-    auto stop_from_red = [&] {
+    if (!kPro && b == f.stop_b && tid == 0) {
         double tot = 0.0, cnt = 0.0;
         for (int w2 = 0; w2 < kFW; ++w2) {
             tot += red[w2];
             cnt += red[kFW + w2];
         }
         stop_rule(a, it, tot, (int)cnt);
-    };
-    if (!kPro && !drow && b == f.stop_b && tid == 0) stop_from_red();
+    }
     __syncthreads();
-    if (drow && b == f.stop_b && tid == 0) stop_from_red();  // (red[] complete only after this barrier)
     FKT(3);
     // ---- landmark stage of iteration it (local_ba.cpp:176-238)
     if (!kPro) {
@@ -1081,82 +1032,6 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     FKT(4);
     // ---- pose stage of iteration it + 1: wave wv takes entries wv, wv + kFW, ...
     if (!pose_next) return;
-    if (bal) {  // (balanced rounds, see (d) above)
-        if (bk0 >= bk1) return;
-        int wp = bwp, rw = brw;  // the current round: round rw of wave wp's list
-        // its entry: positions wp, wp + kFW, ... hold wave wp's entries; q = the round within it
-        int j = wp, q = rw;
-        auto rounds_of = [&](int jj) {
-            const int4 e = s_ke[jj];
-            return (e.w - e.z + 63) >> 6;
-        };
-        while (q >= rounds_of(j)) {
-            q -= rounds_of(j);
-            j += kFW;
-        }
-        double v[kStride];
-#pragma unroll
-        for (int t = 0; t < kStride; ++t) v[t] = 0.0;
-        for (int k = bk0; k < bk1; ++k) {
-            const double2 uv = u0;
-            const double4 P4 = p0;
-            const int4 e = s_ke[j];
-            const int nr = (e.w - e.z + 63) >> 6;
-            // the next round (wave-major) and its prefetch
-            int nwp = wp, nrw = rw + 1;
-            int wn = 0;
-#pragma unroll
-            for (int i = 0; i < kFW; ++i)
-                if (i == wp) wn = wr_n[i];
-            if (nrw >= wn) {
-                nrw = 0;
-                nwp = kFW;
-#pragma unroll
-                for (int i = 0; i < kFW; ++i)
-                    if (nwp == kFW && i > wp && wr_n[i] > 0) nwp = i;
-            }
-            if (k + 1 < bk1) {
-                int an = 0;
-#pragma unroll
-                for (int i = 0; i < kFW; ++i)
-                    if (i == nwp) an = wr_s[i] + 64 * nrw;
-                u0 = f.pobs_uv[an + lane];
-                p0 = f.pobs_p[an + lane];
-            }
-            const bool valid = e.z + 64 * q + lane < e.w;
-            {
-                const double* T = kslot + j * kLdsStride;
-                const int code = (int)P4.w;
-                const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]}
-                                       : D3{P4.x, P4.y, P4.z};
-                pose_obs_accum<kFT <= kFTSmall>(a, T, T + 8, T + 17, P, uv, v, valid);
-            }
-            ++q;
-            const bool entry_done = q == nr;
-            if (entry_done || k + 1 == bk1) {  // flush this segment's partial into the entry's row
-                const double tot = wave_sum32(v);
-                if ((lane & 1) == 0 && (lane >> 1) < kNTerms)
-                    unsafeAtomicAdd(arow + ((size_t)arow_wr(kPro, it) * f.n_kf + (e.x & 0x3fffffff)) * kStride +
-                                        (lane >> 1),
-                                    tot);
-#pragma unroll
-                for (int t = 0; t < kStride; ++t) v[t] = 0.0;
-            }
-            if (k + 1 == bk1) break;
-            if (nwp != wp) {  // next wave's list: its first entry with rounds
-                wp = nwp;
-                j = wp;
-                q = 0;
-                while (rounds_of(j) == 0) j += kFW;
-            } else if (entry_done) {
-                j += kFW;
-                q = 0;
-                while (rounds_of(j) == 0) j += kFW;
-            }
-            rw = nrw;
-        }
-        return;
-    }
     int r = 0;
     FKT(6);
     for (int j = wv; j < n_ent; j += kFW) {

@@ -45,8 +45,11 @@ VX_KP_TABLE();
 
 __constant__ signed char c_pattern[1024];
 __constant__ int c_umax[16];
-// the selection's register-resident steps over 2 / 4 blocks (rg_tailN; $VX_SEL_TAILN=0: wave passes)
+// A/B switches of the selection (measured, off by default): register-resident introselect steps
+// over 2 / 4 / 8 blocks (rg_tailN, $VX_SEL_TAILN=1) and the gather's slot 0-1 loads issued with the
+// cell counts ($VX_SEL_SPEC=1)
 __constant__ int c_sel_tailn;
+__constant__ int c_sel_spec;
 // ICAngles row masks: row lane (v = lane - 15), byte k of the 32-byte window starting at u = -15
 // is 0xff iff |k - 15| <= umax[|v|] (row 31 empty)
 __constant__ __attribute__((aligned(16))) unsigned c_icmask[32][8];
@@ -884,7 +887,13 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
             int kc = 0;
 #pragma unroll
             for (int k = 0; k < kRecBatch; ++k) kc += (k < tot && rr[k].score >= thr1) ? 1 : 0;
-            for (int k = kRecBatch; k < tot; ++k) kc += cand[rec_index(k)].score >= thr1 ? 1 : 0;
+            for (int k0 = kRecBatch; k0 < tot; k0 += kRecBatch) {  // (a batch of loads at a time)
+                CandRec rb[kRecBatch];
+#pragma unroll
+                for (int k = 0; k < kRecBatch; ++k) rb[k] = k0 + k < tot ? cand[rec_index(k0 + k)] : CandRec{};
+#pragma unroll
+                for (int k = 0; k < kRecBatch; ++k) kc += (k0 + k < tot && rb[k].score >= thr1) ? 1 : 0;
+            }
             if (base == 0) VX_KT(10);
             int btot;
             int pos = K1 + block_scan_excl<kSelBlock>(kc, sw, btot);
@@ -897,9 +906,13 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 #pragma unroll
             for (int k = 0; k < kRecBatch; ++k)
                 if (k < tot && rr[k].score >= thr1) put(rr[k]);
-            for (int k = kRecBatch; k < tot; ++k) {
-                const CandRec r = cand[rec_index(k)];
-                if (r.score >= thr1) put(r);
+            for (int k0 = kRecBatch; k0 < tot; k0 += kRecBatch) {
+                CandRec rb[kRecBatch];
+#pragma unroll
+                for (int k = 0; k < kRecBatch; ++k) rb[k] = k0 + k < tot ? cand[rec_index(k0 + k)] : CandRec{};
+#pragma unroll
+                for (int k = 0; k < kRecBatch; ++k)
+                    if (k0 + k < tot && rb[k].score >= thr1) put(rb[k]);
             }
             K1 += btot;
         }
@@ -1996,8 +2009,8 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         for (int j = 0; j < kCellsPer; ++j) {
             const bool ok = j < cpt && c0 + j < ncell;
             cnts[j] = ok ? cell_count[cbase + c0 + j] : 0;
-            sp0[j] = ok ? cand[cand_at(cbase + c0 + j, 0, a.fs_cells)] : CandRec{};
-            sp1[j] = ok ? cand[cand_at(cbase + c0 + j, 1, a.fs_cells)] : CandRec{};
+            sp0[j] = ok && c_sel_spec ? cand[cand_at(cbase + c0 + j, 0, a.fs_cells)] : CandRec{};
+            sp1[j] = ok && c_sel_spec ? cand[cand_at(cbase + c0 + j, 1, a.fs_cells)] : CandRec{};
         }
 #pragma unroll
         for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
@@ -2020,7 +2033,7 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         auto rec_get = [&](int k) -> CandRec {
             int i;
             const int j = rec_cell(k, i);
-            if (i >= 2) return cand[cand_at(cbase + c0 + j, i, a.fs_cells)];
+            if (i >= 2 || !c_sel_spec) return cand[cand_at(cbase + c0 + j, i, a.fs_cells)];
             CandRec r{};
 #pragma unroll
             for (int jj = 0; jj < kCellsPer; ++jj)
@@ -2046,7 +2059,15 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
 #pragma unroll
         for (int k = 0; k < kRecBatch; ++k)
             if (k < tot) put(rr[k]);
-        for (int k = kRecBatch; k < tot; ++k) put(cand[rec_index(k)]);
+        // further records a batch of loads at a time (a thread over a textured half row holds 10-20:
+        // one load per put would expose a memory latency per record on the level's longest thread)
+        for (int k0 = kRecBatch; k0 < tot; k0 += kRecBatch) {
+#pragma unroll
+            for (int k = 0; k < kRecBatch; ++k) rr[k] = k0 + k < tot ? cand[rec_index(k0 + k)] : CandRec{};
+#pragma unroll
+            for (int k = 0; k < kRecBatch; ++k)
+                if (k0 + k < tot) put(rr[k]);
+        }
         n0 += uni(btot);
     }
     __syncthreads();
@@ -2528,8 +2549,11 @@ int upload_constants(vx_ctx* c) {
     }
     VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icmask, sizeof(icmask)));
     const char* tn = std::getenv("VX_SEL_TAILN");
-    const int tailn = tn && tn[0] == '0' ? 0 : 1;
+    const int tailn = tn && tn[0] == '1' ? 1 : 0;
     VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_sel_tailn), &tailn, sizeof(tailn)));
+    const char* sp = std::getenv("VX_SEL_SPEC");
+    const int spec = sp && sp[0] == '1' ? 1 : 0;
+    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_sel_spec), &spec, sizeof(spec)));
     // the selection kernels' 160 KB of dynamic LDS, per device (set with the device current; a failure
     // is reported every time, since the device is only marked done after it succeeded: ADVICE r3)
     VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_stl), hipFuncAttributeMaxDynamicSharedMemorySize,
