@@ -136,8 +136,9 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
     look-ahead column on workgroup 0 (k_sba_fac_begin / k_sba_fac_step / k_sba_backsub, the default),
     equals the one-workgroup k_sba_solve ($VX_SBA_FACTOR=single) bitwise, for one component, eight
     independent ones and eight connected ones, with G = 1, 2, 3 and the plan's own choice, one tile
-    column per launch (k_sba_fac_step, its look-ahead column in LDS or over global memory) or two
-    (k_sba_fac_pair, $VX_SBA_FACTOR_COLS=2)."""
+    column per launch (k_sba_fac_step, its look-ahead column in LDS or over global memory), two
+    (k_sba_fac_pair, $VX_SBA_FACTOR_COLS=2) or blocks of up to four factored in LDS (k_sba_fac_blk,
+    $VX_SBA_FACTOR=block; $VX_SBA_FACTOR=multi keeps one column per launch)."""
     import vxslam
 
     name, nk, nl, ns, cf = cfg
@@ -146,7 +147,8 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
     out = {}
     for form, groups, la, cols in (("single", None, "1", "2"), ("multi", "1", "1", "1"), ("multi", "2", "1", "1"),
                                    ("multi", None, "1", "1"), ("multi", "2", "0", "1"), ("multi", "1", "1", "2"),
-                                   ("multi", "3", "1", "2"), ("multi", None, "1", "2")):
+                                   ("multi", "3", "1", "2"), ("multi", None, "1", "2"), ("block", "1", "1", "1"),
+                                   ("block", "2", "1", "1"), ("block", "5", "1", "1"), ("block", None, "1", "1")):
         monkeypatch.setenv("VX_SBA_FACTOR", form)
         monkeypatch.setenv("VX_SBA_LOOKAHEAD_LDS", la)
         monkeypatch.setenv("VX_SBA_FACTOR_COLS", cols)

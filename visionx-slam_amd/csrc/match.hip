@@ -97,10 +97,9 @@ __device__ __forceinline__ void top2_dpp(unsigned& k1, unsigned& k2) {
 // RQ queries (wave-uniform operands) against the whole train set by RT threads; then the LDS
 // transpose, each wave reducing RQ / (RT / 64) queries.  The workgroups take query groups
 // blockIdx.x, blockIdx.x + gridDim.x, ... (a grid smaller than the capacity's query groups loops).
-// nq / nt: the counts (device), nq_cap / nt_cap: the buffers' rows.  The first group's queries and
-// the first pass's train rows are requested before the counts arrive — rows below the capacities
-// are valid memory, and a row past a count is never used — so the kernel waits on one memory latency,
-// not two; the first pass's train rows stay in registers for every group of the workgroup.
+// nq / nt: the counts (device), nq_cap / nt_cap: the buffers' rows.  (Requesting the first
+// operands before the counts arrive was measured in round 5: 5.2 us uncapped, 6.8 capped, no change
+// in the pipeline — not kept.)
 template <int RQ, int RT>
 __device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p, int nq_cap,
                                          const uint8_t* __restrict__ t, const int* __restrict__ nt_p, int nt_cap,
@@ -116,19 +115,11 @@ __device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, const in
             A1[i] = reinterpret_cast<const uint4*>(q + (long long)qi * 32)[1];
         }
     };
-    uint4 A0[RQ], A1[RQ], F0[4], F1[4];
-    int q0 = blockIdx.x * RQ;
-    if (q0 < nq_cap) load_q(q0, A0, A1, nq_cap);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = min(tid + j * RT, max(nt_cap, 1) - 1);
-        F0[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[0];
-        F1[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[1];
-    }
+    uint4 A0[RQ], A1[RQ];
     const int nq = nq_p ? min(*nq_p, nq_cap) : nq_cap;
     const int nt = nt_p ? min(*nt_p, nt_cap) : nt_cap;
-    for (; q0 < nq; q0 += gridDim.x * RQ) {  // (block-uniform)
-    if (q0 != (int)blockIdx.x * RQ) load_q(q0, A0, A1, nq);
+    for (int q0 = blockIdx.x * RQ; q0 < nq; q0 += gridDim.x * RQ) {  // (block-uniform)
+    load_q(q0, A0, A1, nq);
     unsigned k1[RQ], k2[RQ];
 #pragma unroll
     for (int i = 0; i < RQ; ++i) k1[i] = k2[i] = kNone;
@@ -136,14 +127,9 @@ __device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, const in
         uint4 B0[4], B1[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if (r0 == tid) {
-                B0[j] = F0[j];
-                B1[j] = F1[j];
-            } else {
-                const int row = min(r0 + j * RT, nt - 1);
-                B0[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[0];
-                B1[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[1];
-            }
+            const int row = min(r0 + j * RT, nt - 1);
+            B0[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[0];
+            B1[j] = reinterpret_cast<const uint4*>(t + (long long)row * 32)[1];
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -199,36 +185,13 @@ __device__ __forceinline__ void knn_rows(const uint8_t* __restrict__ q, const in
     }
 }
 
-template <int NT>
-__device__ int scan_excl(int v, int* sh, int& total);
-template <int NT>
-__device__ void knn_compact(const unsigned* __restrict__ best, int nq, vx_match* __restrict__ out,
-                            int* __restrict__ out_count, int* sh);
-
-// kFuse: the ordered compaction runs in the workgroup that finishes last (an arrival counter at
-// out_count[1], zero between launches: the last workgroup resets it) instead of a launch of its own;
-// the release / acquire fences around the counter make every workgroup's best[] visible to it.
-template <int RQ, int RT, bool kFuse>
+template <int RQ, int RT>
 __global__ __launch_bounds__(RT) void k_knn_rows(const uint8_t* __restrict__ q, const int* __restrict__ nq_p,
                                                  int nq_host, const uint8_t* __restrict__ t,
                                                  const int* __restrict__ nt_p, int nt_host, float ratio,
-                                                 unsigned* __restrict__ best, vx_match* __restrict__ out,
-                                                 int* __restrict__ out_count) {
+                                                 unsigned* __restrict__ best) {
     __shared__ uint2 tr[RQ][RT];  // the threads' top-2s, query-major
     knn_rows<RQ, RT>(q, nq_p, nq_host, t, nt_p, nt_host, ratio, best, tr);
-    if constexpr (kFuse) {
-        __shared__ int s_last;
-        __shared__ int sh[RT / 64];
-        __threadfence();  // (release: this workgroup's best[])
-        __syncthreads();
-        if (threadIdx.x == 0) s_last = atomicAdd(out_count + 1, 1) == (int)gridDim.x - 1;
-        __syncthreads();
-        if (!s_last) return;
-        __threadfence();  // (acquire: every workgroup's best[])
-        const int nq = nq_p ? min(*nq_p, nq_host) : nq_host;
-        knn_compact<RT>(best, nq, out, out_count, sh);
-        if (threadIdx.x == 0) out_count[1] = 0;
-    }
 }
 
 // Batched matching (vx_match_batch_async): pair blockIdx.y's sets from the table, per-pair results
@@ -250,7 +213,7 @@ __global__ __launch_bounds__(kRT) void k_knn_rows_batch(PairTab tab, int q_cap, 
 // Exclusive block scan: wave prefix by __shfl_up, then the NT/64 wave totals from LDS (two
 // barriers per call instead of a Hillis-Steele pass per doubling step).
 template <int NT>
-__device__ int scan_excl(int v, int* sh, int& total) {
+__device__ __forceinline__ int scan_excl(int v, int* sh, int& total) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int x = v;
 #pragma unroll
@@ -309,16 +272,23 @@ __global__ __launch_bounds__(kMergeQB) void k_knn_merge(const uint2* __restrict_
 }
 
 // Ordered compaction (ascending query index) of the per-query results, one block.
+// nq_p: the device count (null: cap), cap: the results' capacity.  The first pass's entries are
+// requested before the count arrives (entries below the capacity are valid memory; those past the
+// count are dropped after): one dependent memory latency before the scan instead of two.
 template <int NT>
-__device__ void knn_compact(const unsigned* __restrict__ best, int nq, vx_match* __restrict__ out,
-                            int* __restrict__ out_count, int* sh) {
+__device__ __forceinline__ void knn_compact(const unsigned* __restrict__ best, const int* __restrict__ nq_p, int cap,
+                                            vx_match* __restrict__ out, int* __restrict__ out_count, int* sh) {
     int written = 0;
+    unsigned k0[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) k0[j] = 4 * (int)threadIdx.x + j < cap ? best[4 * threadIdx.x + j] : kNone;
+    const int nq = nq_p ? min(*nq_p, cap) : cap;
     // 4 consecutive queries per thread (one pass up to 4 NT queries: one load latency, one scan)
     for (int base = 0; base < nq; base += 4 * NT) {
         const int q4 = base + 4 * threadIdx.x;
         unsigned k[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) k[j] = q4 + j < nq ? best[q4 + j] : kNone;
+        for (int j = 0; j < 4; ++j) k[j] = q4 + j < nq ? (base == 0 ? k0[j] : best[q4 + j]) : kNone;
         int n4 = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) n4 += k[j] != kNone;
@@ -343,7 +313,7 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact(const unsigned* __r
                                                              vx_match* __restrict__ out,
                                                              int* __restrict__ out_count) {
     __shared__ int sh[kMergeBlock / 64];
-    knn_compact<kMergeBlock>(best, nq_p ? min(*nq_p, nq_host) : nq_host, out, out_count, sh);
+    knn_compact<kMergeBlock>(best, nq_p, nq_host, out, out_count, sh);
 }
 
 // one workgroup per pair: matches of pair p at out + p * q_cap, its count at out_count[4 p]
@@ -352,7 +322,7 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact_batch(const unsigne
                                                                    int* __restrict__ out_count) {
     __shared__ int sh[kMergeBlock / 64];
     const int p = blockIdx.x;
-    knn_compact<kMergeBlock>(best + (long long)p * q_cap, min(*tab.nq[p], q_cap), out + (long long)p * q_cap,
+    knn_compact<kMergeBlock>(best + (long long)p * q_cap, tab.nq[p], q_cap, out + (long long)p * q_cap,
                 out_count + 4 * p, sh);
 }
 
@@ -361,23 +331,18 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact_batch(const unsigne
 // workgroup per CU by default: the query count is on the device, so an uncapped grid ($VX_MATCH_GRID=0)
 // is sized for the capacity and most of its workgroups only read the count and leave (C3's
 // 2000-of-4254: 6.64 us uncapped, 4.92 us capped, profiles/r05/match_shapes.txt)
-// fuse: the compaction in the last workgroup (k_knn_rows<.., true>; out / out_count: the results)
 template <int RQ, int RT>
 int knn_rows_launch_t(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt, const int* dnt,
-                      int nt_host, int q_cap, float ratio, unsigned* best, int grid_cap, bool fuse, vx_match* out,
-                      int* out_count) {
+                      int nt_host, int q_cap, float ratio, unsigned* best, int grid_cap) {
     int g = (q_cap + RQ - 1) / RQ;
     if (grid_cap > 0) g = std::min(g, grid_cap);
-    if (fuse)
-        VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows<RQ, RT, true>, dim3(std::max(g, 1)), dim3(RT), 0, c->stream, dq,
-                         dnq, nq_host, dt, dnt, nt_host, ratio, best, out, out_count));
-    else
-        VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows<RQ, RT, false>, dim3(std::max(g, 1)), dim3(RT), 0, c->stream,
-                         dq, dnq, nq_host, dt, dnt, nt_host, ratio, best, out, out_count));
+    VX_HIP(c, launch(c, kStMatchPartial, k_knn_rows<RQ, RT>, dim3(std::max(g, 1)), dim3(RT), 0, c->stream, dq, dnq,
+                     nq_host, dt, dnt, nt_host, ratio, best));
     return VX_OK;
 }
 int knn_rows_launch(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, const uint8_t* dt, const int* dnt,
-                    int nt_host, int q_cap, float ratio, unsigned* best, bool fuse, vx_match* out, int* out_count) {
+                    int nt_host, int q_cap, float ratio, unsigned* best) {
+
     static const int shape = [] {
         const char* e = getenv("VX_MATCH_SHAPE");
         if (!e) return 0;
@@ -391,14 +356,10 @@ int knn_rows_launch(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, c
     if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
     const int grid_cap = grid_env >= 0 ? grid_env : c->n_cus;
     switch (shape) {
-        case 1: return knn_rows_launch_t<4, 256>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap, fuse, out,
-                                                          out_count);
-        case 2: return knn_rows_launch_t<16, 512>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap, fuse, out,
-                                                          out_count);
-        case 3: return knn_rows_launch_t<16, 1024>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap, fuse, out,
-                                                          out_count);
-        default: return knn_rows_launch_t<kRQ, kRT>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap, fuse, out,
-                                                          out_count);
+        case 1: return knn_rows_launch_t<4, 256>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        case 2: return knn_rows_launch_t<16, 512>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        case 3: return knn_rows_launch_t<16, 1024>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        default: return knn_rows_launch_t<kRQ, kRT>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
     }
 }
 
@@ -416,20 +377,8 @@ int match_enqueue(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, con
         return e && e[0] == '1';
     }();
     if (!chunked) {
-        // $VX_MATCH_FUSE=1: the compaction in k_knn_rows' last workgroup (its arrival counter is
-        // match_count[1], zeroed with the buffer at context creation)
-        static const bool fuse = [] {
-            const char* e = getenv("VX_MATCH_FUSE");
-            return e && e[0] == '1';
-        }();
         unsigned* best = reinterpret_cast<unsigned*>(c->partial.as<uint2>() + (size_t)n_chunks * q_stride);
-        if ((rc = knn_rows_launch(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, fuse,
-                                  c->matches.as<vx_match>(), c->match_count.as<int>())))
-            return rc;
-        if (fuse) {
-            c->match_valid = true;
-            return VX_OK;
-        }
+        if ((rc = knn_rows_launch(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best))) return rc;
         ProfScope ps(c, kStMatchMerge);
         hipLaunchKernelGGL(k_knn_compact, dim3(1), dim3(kMergeBlock), 0, c->stream, best, dnq, nq_host,
                            c->matches.as<vx_match>(), c->match_count.as<int>());

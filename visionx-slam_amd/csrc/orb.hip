@@ -45,11 +45,6 @@ VX_KP_TABLE();
 
 __constant__ signed char c_pattern[1024];
 __constant__ int c_umax[16];
-// A/B switches of the selection (measured, off by default): register-resident introselect steps
-// over 2 / 4 / 8 blocks (rg_tailN, $VX_SEL_TAILN=1) and the gather's slot 0-1 loads issued with the
-// cell counts ($VX_SEL_SPEC=1)
-__constant__ int c_sel_tailn;
-__constant__ int c_sel_spec;
 // ICAngles row masks: row lane (v = lane - 15), byte k of the 32-byte window starting at u = -15
 // is 0xff iff |k - 15| <= umax[|v|] (row 31 empty)
 __constant__ __attribute__((aligned(16))) unsigned c_icmask[32][8];
@@ -1656,100 +1651,6 @@ __device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int
     l = f0 + ll;
 }
 
-// The same register-resident introselect steps over NB blocks (a range of <= 64 NB elements on wave
-// 0): lane i of block j holds A[f0 + 64 j + i] for the whole tail, a step's range is the window
-// [lf, ll) of those positions.  Pivot candidates come from v_readlane of every block and a scalar
-// select by the (uniform) block index — no register array is indexed at run time, so nothing goes
-// to scratch — and the cut from the L / R ballots.  Only the swapped pairs go through the
-// mailboxes.  Stops when the window fits the next narrower engine (<= 32 NB, written back: the
-// caller continues there), at <= 3 or at the depth limit; f / l the window, A updated.
-template <int NB, class T>
-__device__ __forceinline__ void rg_tailN(T* __restrict__ A, int& f, int& l, int nth, int& depth, bool& heap,
-                                         const RgLds& E) {
-    const int lane = threadIdx.x & 63;
-    const int f0 = f, n0 = l - f;
-    T v[NB];
-#pragma unroll
-    for (int j = 0; j < NB; ++j) v[j] = A[f0 + min(64 * j + lane, n0 - 1)];
-    T* eb = E.bl<T>();
-    constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
-    const int kth = nth - f0;
-    int lf = 0, ll = n0;
-    auto rd = [&](int p) -> T {  // A[f0 + p], p uniform
-        T r = T(0);
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const T x = rdl(v[j], p & 63);
-            r = (j == (p >> 6)) ? x : r;
-        }
-        return r;
-    };
-    while (ll - lf > 32 * NB && ll - lf > 3) {
-        if (depth == 0) {
-            heap = true;
-            break;
-        }
-        --depth;
-        const int a = lf + 1, b = lf + (ll - lf) / 2, c = ll - 1;
-        const T vf = rd(lf), va = rd(a), vb = rd(b), vc = rd(c);
-        T pv;
-        const int m = stl_median(a, b, c, va, vb, vc, pv);
-        const unsigned P = sel_key(pv);
-        bool il[NB], ir[NB];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const int x = 64 * j + lane;
-            v[j] = x == lf ? pv : x == m ? vf : v[j];
-            const bool in = x > lf && x < ll;
-            const unsigned k = sel_key(v[j]);
-            il[j] = in && k <= P;
-            ir[j] = in && k >= P;
-        }
-        int ra[NB], rb[NB];
-        rg_ranks(il, ir, 0, 0, ra, rb);
-        int nr = 0;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) nr += __popcll(__ballot(ir[j]));
-        const int K = rg_crossing(il, ir, ra, rb, 0, 0, nr);
-        const int hr = K > 0 ? nr - K : INT_MAX;
-        bool sw[NB];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
-            sw[j] = sl || sr;
-            eb[sl ? ra[j] : sr ? kBr + (nr - 1 - rb[j]) : kTv + lane] = v[j];
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        T nv[NB];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
-            nv[j] = eb[sl ? kBr + ra[j] : sr ? nr - 1 - rb[j] : kTv + lane];
-        }
-        int cut = INT_MAX;
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const u64 cl = __ballot(il[j] && ra[j] == K), cr = __ballot(ir[j] && rb[j] == hr);
-            if (cl) cut = min(cut, 64 * j + __ffsll((long long)cl) - 1);
-            if (cr) cut = min(cut, 64 * j + __ffsll((long long)cr) - 1);
-        }
-        cut = min(max(cut, lf + 1), ll);  // (clamped: memory-safe whatever happens)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) v[j] = sw[j] ? nv[j] : v[j];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (next step's mailbox writes after these reads)
-        __builtin_amdgcn_wave_barrier();
-        if (cut <= kth) lf = cut;
-        else ll = cut;
-    }
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-        if (64 * j + lane < n0) A[f0 + 64 * j + lane] = v[j];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    f = f0 + lf;
-    l = f0 + ll;
-}
-
 // libstdc++'s closing __insertion_sort of A[0, n) (n <= 3; a stable sort by key, descending):
 // every lane of the calling wave reads the elements, lane 0 writes them back
 template <class T>
@@ -1870,9 +1771,7 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
         if (cut <= nth) f = cut;
         else l = cut;
     }
-    // (wave 0's register-resident steps take ranges up to 512; team passes the longer ones)
-    const int wave_cap = c_sel_tailn ? 512 : kRgWave;
-    while (!heap && l - f > wave_cap) {
+    while (!heap && l - f > kRgWave) {
         if (depth == 0) {
             heap = true;
             break;
@@ -1891,13 +1790,6 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
                 VX_KP((5 << 24) | (l - f));
                 rg_tail64(A, f, l, nth, depth, heap, E);
                 break;
-            }
-            if (c_sel_tailn && l - f <= 512) {  // register-resident steps over 8 / 4 / 2 blocks, then the above
-                VX_KP((6 << 24) | (l - f));
-                if (l - f > 256) rg_tailN<8>(A, f, l, nth, depth, heap, E);
-                else if (l - f > 128) rg_tailN<4>(A, f, l, nth, depth, heap, E);
-                else rg_tailN<2>(A, f, l, nth, depth, heap, E);
-                continue;
             }
             if (depth == 0) {
                 heap = true;
@@ -2001,48 +1893,23 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         const int c0 = base + tid * cpt;
         int cnts[kCellsPer];
         int tot = 0;
-        // slots 0 and 1 of the thread's cells are loaded with the counts, not after them: most cells
-        // hold 0-2 records, so most records come without a second dependent global load (the slots
-        // are valid memory whatever the count; a stale one is never used)
-        CandRec sp0[kCellsPer], sp1[kCellsPer];
 #pragma unroll
-        for (int j = 0; j < kCellsPer; ++j) {
-            const bool ok = j < cpt && c0 + j < ncell;
-            cnts[j] = ok ? cell_count[cbase + c0 + j] : 0;
-            sp0[j] = ok && c_sel_spec ? cand[cand_at(cbase + c0 + j, 0, a.fs_cells)] : CandRec{};
-            sp1[j] = ok && c_sel_spec ? cand[cand_at(cbase + c0 + j, 1, a.fs_cells)] : CandRec{};
-        }
+        for (int j = 0; j < kCellsPer; ++j) cnts[j] = (j < cpt && c0 + j < ncell) ? cell_count[cbase + c0 + j] : 0;
 #pragma unroll
         for (int j = 0; j < kCellsPer; ++j) tot += cnts[j];
-        auto rec_cell = [&](int k, int& i) {  // the cell (0..kCellsPer) and slot i of the thread's k-th record
-            int j = 0;
-            i = k;
+        auto rec_index = [&](int k) {  // the thread's k-th record: cell j of its cells, slot i
+            int j = 0, i = k;
 #pragma unroll
             for (int jj = 0; jj < kCellsPer; ++jj)
                 if (j == jj && i >= cnts[jj]) {
                     i -= cnts[jj];
                     j = jj + 1;
                 }
-            return j;
-        };
-        auto rec_index = [&](int k) {
-            int i;
-            const int j = rec_cell(k, i);
             return cand_at(cbase + c0 + j, i, a.fs_cells);
-        };
-        auto rec_get = [&](int k) -> CandRec {
-            int i;
-            const int j = rec_cell(k, i);
-            if (i >= 2 || !c_sel_spec) return cand[cand_at(cbase + c0 + j, i, a.fs_cells)];
-            CandRec r{};
-#pragma unroll
-            for (int jj = 0; jj < kCellsPer; ++jj)
-                if (jj == j) r = i == 0 ? sp0[jj] : sp1[jj];
-            return r;
         };
         CandRec rr[kRecBatch];
 #pragma unroll
-        for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? rec_get(k) : CandRec{};
+        for (int k = 0; k < kRecBatch; ++k) rr[k] = k < tot ? cand[rec_index(k)] : CandRec{};
         int btot;
         int pos = n0 + block_scan_excl<kStlNT>(tot, sw, btot);
         auto put = [&](const CandRec& r) {
@@ -2548,12 +2415,6 @@ int upload_constants(vx_ctx* c) {
             if (k - 15 >= -d && k - 15 <= d) icmask[r][k >> 2] |= 0xffu << (8 * (k & 3));
     }
     VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), icmask, sizeof(icmask)));
-    const char* tn = std::getenv("VX_SEL_TAILN");
-    const int tailn = tn && tn[0] == '1' ? 1 : 0;
-    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_sel_tailn), &tailn, sizeof(tailn)));
-    const char* sp = std::getenv("VX_SEL_SPEC");
-    const int spec = sp && sp[0] == '1' ? 1 : 0;
-    VX_HIP(c, hipMemcpyToSymbol(HIP_SYMBOL(c_sel_spec), &spec, sizeof(spec)));
     // the selection kernels' 160 KB of dynamic LDS, per device (set with the device current; a failure
     // is reported every time, since the device is only marked done after it succeeded: ADVICE r3)
     VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_select_stl), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -143,6 +143,8 @@ struct SBAArgs {
     int fac_nk;
     const int* fac_pairs;   // k_sba_fac_pair descriptors (vx_sba_plan::fac_pairs), fac_np per component
     int fac_np;
+    const int* fac_blks;    // k_sba_fac_blk descriptors (vx_sba_plan::fac_blks), fac_nb per component
+    int fac_nb;
     int bs_np, bs_nt;       // k_sba_backsub's LDS: the largest component's np doubles, nt + 1 pointers
 };
 
@@ -156,6 +158,14 @@ struct FacPair {
 struct FacStep {
     long long loff;
     int la_beg, split, t_end, p0, p1, nt;
+};
+
+// one launch of the blocked factor for one component (vx_sba_plan::fac_blks, 16 ints): block t's
+// columns [K0, K0 + W) and tile list, block t - 1's columns and tile list (its steps' pattern), the
+// trailing tiles block t - 1's steps update beyond block t (entries i << 16 | j << 4 | step mask)
+struct FacBlk {
+    long long loff;
+    int K0, W, bt_beg, bt_end, pb_beg, pb_end, K0p, Wp, tr_beg, tr_end, nt;
 };
 
 // ------------------------------------------------------------------------- state selection
@@ -566,12 +576,13 @@ __device__ __forceinline__ void store_acc_opo(double* S, d4 v) {
 // operations in the same order per lane as a separate substitution after the factor: bitwise the
 // same L^-1).  Written as an operand-order LDS image and row-major to Lg.  Returns false on a
 // non-positive pivot.  (lcol: unused scratch, kept for the callers' LDS layout.)
-__device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
-    (void)lcol;
+// rd(r, c): element (r, c) of the tile, lower triangle read (c <= r)
+template <class Rd>
+__device__ __forceinline__ bool potrf_inv16_t(Rd rd, double* lds_inv, double* Lg) {
     const int lane = threadIdx.x & 63, i = lane & 15;
     double a[16];
 #pragma unroll
-    for (int c = 0; c < 16; ++c) a[c] = c <= i ? A[(long long)i * ld + c] : A[(long long)c * ld + i];
+    for (int c = 0; c < 16; ++c) a[c] = c <= i ? rd(i, c) : rd(c, i);
     double x[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) x[r] = r == i ? 1.0 : 0.0;
@@ -599,6 +610,10 @@ __device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lco
         }
     }
     return ok;
+}
+__device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
+    (void)lcol;
+    return potrf_inv16_t([&](int r, int c) { return A[(long long)r * ld + c]; }, lds_inv, Lg);
 }
 
 // Per-component tile program (host symbolic factorisation, vx_sba_plan): int offsets into a.tl.
@@ -1164,6 +1179,217 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_pair(SBAArgs a, int i
     }
 }
 
+// ------------------------------------------------------------------------- blocked factor
+// The same right-looking tiled Cholesky in blocks of up to kFbW tile columns, one launch per block
+// (round 5: the one-launch-per-column form spent ~13 us per column on workgroup 0's chain, most of it
+// global round trips and the launch).  Launch t: workgroup 0 loads every tile of block t's columns
+// (at most the plan's LDS capacity), applies block t - 1's steps to them on the way in (the
+// look-ahead), and factors the block in LDS — per column POTRF + L^-1 of the diagonal tile, the panel
+// L_ic = A_ic L_cc^-T (written to the factor in global memory as well), then the column's steps on the
+// block's later columns — while G - 1 workgroups apply block t - 1's steps to the tiles beyond block t.
+// Every tile receives its steps in ascending order with the same operations (MFMA operands read in
+// operand order from LDS instead of global memory: the same values), so the factor is bitwise the
+// one-column forms' and the single workgroup's.  Launch 0 also takes the LM decision and the damping.
+constexpr int kFbThreads = 512;
+constexpr int kFbWaves = kFbThreads / 64;
+constexpr int kFbW = 4;       // tile columns per block (4-bit step masks)
+constexpr int kFbCap = 72;    // LDS tiles of a block (operand order, 2 KB each)
+
+__device__ __forceinline__ d4 load_acc_opo(const double* S) {
+    const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
+    d4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = S[opo(r0 + 4 * r, c)];
+    return v;
+}
+
+// trailing tiles of launch t: entries i << 16 | j << 4 | mask, steps k0 + s for the mask's bits s in
+// ascending order; entries beg, beg + stride, ...; four per wave in flight
+__device__ __forceinline__ void blk_trail(double* L, int np, const int* tl, int k0, int beg, int end, int stride,
+                                          int waves) {
+    const int wv = threadIdx.x >> 6;
+    const int cnt = end > beg ? (end - beg + stride - 1) / stride : 0;
+    for (int m0 = wv * 4; m0 < cnt; m0 += waves * 4) {
+        d4 c[4];
+        int ti[4], tj[4], mk[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ti[q] = -1;
+            if (m0 + q < cnt) {
+                const int e = tl[beg + (m0 + q) * stride];
+                ti[q] = e >> 16;
+                tj[q] = (e >> 4) & 0xfff;
+                mk[q] = e & 15;
+                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (ti[q] < 0) continue;
+            for (int s = 0; s < kFbW; ++s)
+                if ((mk[q] >> s) & 1)
+                    c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * (k0 + s),
+                                      L + (long long)(16 * tj[q]) * np + 16 * (k0 + s), np, c[q]);
+            store_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np, c[q]);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, int t, int G, int cap, FacBlk sd) {
+    const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
+    if (sd.nt == 0) {
+        const int* d = a.fac_blks + 16 * ((size_t)comp * a.fac_nb + t);
+        const int4 d0 = *reinterpret_cast<const int4*>(d), d1 = *reinterpret_cast<const int4*>(d + 4),
+                   d2 = *reinterpret_cast<const int4*>(d + 8), d3 = *reinterpret_cast<const int4*>(d + 12);
+        sd.loff = (long long)(((unsigned long long)(unsigned)d0.y << 32) | (unsigned)d0.x);
+        sd.K0 = d0.z;
+        sd.W = d0.w;
+        sd.bt_beg = d1.x;
+        sd.bt_end = d1.y;
+        sd.pb_beg = d1.z;
+        sd.pb_end = d1.w;
+        sd.K0p = d2.x;
+        sd.Wp = d2.y;
+        sd.tr_beg = d2.z;
+        sd.tr_end = d2.w;
+        sd.nt = d3.x;
+    }
+    if (it > 0 && !a.st->active[it]) return;
+    const int nt = sd.nt, np = 16 * nt;
+    if (nt == 0) return;  // (this component has no block t)
+    // trace build: launch nt / 8 (slots 10-15 workgroup 0: entry, tables, look-ahead, column 0's
+    // POTRF, panel, block done; 7: another workgroup's trailing tiles)
+    const bool kt = t == nt / 8;
+    if (kt) VX_KT(10);
+    double* L = a.L + sd.loff;
+    double* Linv = a.Linv + sd.loff;
+    const int* tl = a.tl;
+    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    if (t == 0) {
+        if (g != 0) return;
+        __shared__ int s_solve;
+        __shared__ double s_lambda;
+        solve_decide(a, it, comp == 0, &s_solve, &s_lambda);
+        if (!s_solve) return;
+        solve_damp(a, comp, s_lambda, L, np, kFbThreads);
+        __syncthreads();
+    } else {
+        if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (launch 0's decision)
+        if (g > 0 || G == 1) {
+            const int gg = G == 1 ? 0 : g - 1, GG = G == 1 ? 1 : G - 1;
+            blk_trail(L, np, tl, sd.K0p, sd.tr_beg + gg, sd.tr_end, GG, kFbWaves);
+            if (kt && g > 0) VX_KT(7);
+            if (g > 0) return;
+        }
+    }
+    extern __shared__ __attribute__((aligned(32))) double sm[];
+    const int K0 = sd.K0, W = sd.W, n = sd.bt_end - sd.bt_beg, n1 = nt + 1;
+    double* T = sm;                                   // cap tiles, operand order
+    double* dlds = sm + (size_t)cap * kPanelStride;   // L_cc^-1 of the current column
+    int* ent = reinterpret_cast<int*>(dlds + kPanelStride);  // cap entries i << 16 | c
+    int* rs = ent + cap;                              // kFbW x n1: slot of (i, K0 + cc), -1: none
+    int* pz = rs + kFbW * n1;                         // kFbW x n1: tile (i, K0p + cc) of block t - 1 nonzero
+    int* cb = pz + kFbW * n1;                         // kFbW + 1: first slot of column cc (its diagonal)
+    for (int x = tid; x < kFbW * n1; x += kFbThreads) {
+        rs[x] = -1;
+        pz[x] = 0;
+    }
+    __syncthreads();
+    for (int s = tid; s < n; s += kFbThreads) {
+        const int e = tl[sd.bt_beg + s];
+        ent[s] = e;
+        rs[((e & 0xffff) - K0) * n1 + (e >> 16)] = s;
+    }
+    for (int s = tid; t > 0 && s < sd.pb_end - sd.pb_beg; s += kFbThreads) {
+        const int e = tl[sd.pb_beg + s];
+        pz[((e & 0xffff) - sd.K0p) * n1 + (e >> 16)] = 1;
+    }
+    __syncthreads();
+    if (tid <= W) cb[tid] = tid < W ? rs[tid * n1 + K0 + tid] : n;
+    if (kt) VX_KT(11);
+    // block t's tiles into LDS with block t - 1's steps (tile (i, j), step k: NZ(i, k) and NZ(j, k);
+    // the rhs row i = nt is in every column's list)
+    for (int m0 = wv * 4; m0 < n; m0 += kFbWaves * 4) {
+        d4 c[4];
+        int ti[4], tj[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            ti[q] = -1;
+            if (m0 + q < n) {
+                const int e = ent[m0 + q];
+                ti[q] = e >> 16;
+                tj[q] = e & 0xffff;
+                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (ti[q] < 0) continue;
+            for (int s = 0; t > 0 && s < sd.Wp; ++s)
+                if (pz[s * n1 + ti[q]] && pz[s * n1 + tj[q]]) {
+                    const int k = sd.K0p + s;
+                    c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * k, L + (long long)(16 * tj[q]) * np + 16 * k,
+                                      np, c[q]);
+                }
+            store_acc_opo(T + (size_t)(m0 + q) * kPanelStride, c[q]);
+        }
+    }
+    __syncthreads();
+    if (kt) VX_KT(12);
+    bool ok = true;
+    for (int cc = 0; cc < W; ++cc) {
+        const int c = K0 + cc, s0 = cb[cc], s1 = cb[cc + 1];
+        if (wv == 0) {
+            const double* D = T + (size_t)s0 * kPanelStride;
+            ok = potrf_inv16_t([&](int r, int q) { return D[opo(r, q)]; }, dlds, Linv + 256 * c) && ok;
+        }
+        __syncthreads();
+        if (kt && cc == 0) VX_KT(13);
+        // the panel L_ic = A_ic L_cc^-T (rows below the diagonal, the rhs row last): in place and to
+        // the factor
+        for (int s = s0 + 1 + wv; s < s1; s += kFbWaves) {
+            double* S = T + (size_t)s * kPanelStride;
+            const double4 av = *reinterpret_cast<const double4*>(S + 4 * lane);
+            const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
+            d4 r = {0.0, 0.0, 0.0, 0.0};
+            r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, r, 0, 0, 0);
+            r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, r, 0, 0, 0);
+            r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.z, bv.z, r, 0, 0, 0);
+            r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, r, 0, 0, 0);
+            store_acc_opo(S, r);
+            store_acc(L + (long long)(16 * (ent[s] >> 16)) * np + 16 * c, np, r);
+        }
+        __syncthreads();
+        if (kt && cc == 0) VX_KT(14);
+        if (cc + 1 == W) break;
+        // step c on the block's later columns c2: tiles (i, c2), i >= c2, for NZ(c2, c) — rows of
+        // column c from the slot of (c2, c) on
+        int tot = 0;
+        for (int c2 = c + 1; c2 < K0 + W; ++c2) {
+            const int sc = rs[cc * n1 + c2];
+            tot += sc >= 0 ? s1 - sc : 0;
+        }
+        for (int p = wv; p < tot; p += kFbWaves) {
+            int q = p, c2 = c + 1, sc = -1;
+            for (; c2 < K0 + W; ++c2) {
+                sc = rs[cc * n1 + c2];
+                const int len = sc >= 0 ? s1 - sc : 0;
+                if (q < len) break;
+                q -= len;
+            }
+            const int s = sc + q;  // L_ic, with L_c2c at sc
+            const int dst = rs[(c2 - K0) * n1 + (ent[s] >> 16)];
+            double* Dt = T + (size_t)dst * kPanelStride;
+            d4 acc = load_acc_opo(Dt);
+            acc = mfma_abt(T + (size_t)s * kPanelStride, T + (size_t)sc * kPanelStride, acc, true);
+            store_acc_opo(Dt, acc);
+        }
+        __syncthreads();
+    }
+    if (kt) VX_KT(15);
+    if (wv == 0 && lane == 0 && !ok) atomicOr(&a.st->fail[it], 1);
+}
+
 __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;
@@ -1329,6 +1555,8 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.fac_nk = std::max(p->max_nt - 1, 1);
     a.fac_pairs = p->fac_pairs.as<int>();
     a.fac_np = std::max(p->max_pairs, 1);
+    a.fac_blks = p->fac_blks.as<int>();
+    a.fac_nb = std::max(p->max_blks, 1);
     a.bs_np = p->max_np;
     a.bs_nt = std::max(p->max_nt, 1);
     return a;
@@ -1733,8 +1961,10 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     p->max_panel = 1;
     p->max_nt = p->max_trail_rest = 0;
     p->max_pairs = 0;
+    p->max_blks = p->max_blk_trail = 0;
+    p->blk_ok = p->n_comp > 0;
     p->max_back = 0;
-    std::vector<std::vector<int>> pair_desc(std::max(p->n_comp, 1));
+    std::vector<std::vector<int>> pair_desc(std::max(p->n_comp, 1)), blk_desc(std::max(p->n_comp, 1));
     {
         std::vector<std::vector<std::pair<int, int>>> cblk(p->n_comp);
         for (const int2& b : bij) {
@@ -1866,6 +2096,64 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                 pd.insert(pd.end(), d, d + 16);
             }
             p->max_pairs = std::max(p->max_pairs, (int)(pd.size() / 16));
+            // the blocked factor (k_sba_fac_blk): blocks of up to kFbW columns whose tiles (the
+            // diagonal, the panel rows, the rhs row) fit kFbCap LDS tiles; per block its tile list
+            // (column-major, rows ascending), then per launch t >= 1 the tiles beyond block t that block
+            // t - 1's steps update (step mask bit s: NZ(i, K0p + s) and NZ(j, K0p + s), the rhs row
+            // always nonzero)
+            {
+                auto col_tiles = [&](int c) { return tlist[h[kHdrPanel] + c + 1] - tlist[h[kHdrPanel] + c] + 1; };
+                std::vector<int> bk0, bw, bb, be;
+                for (int c = 0; c < nt && p->blk_ok;) {
+                    int w = 0, tiles = 0;
+                    while (c + w < nt && w < kFbW && tiles + col_tiles(c + w) <= kFbCap) tiles += col_tiles(c + w++);
+                    if (w == 0) {
+                        p->blk_ok = false;  // one column's panel exceeds the block LDS
+                        break;
+                    }
+                    bk0.push_back(c);
+                    bw.push_back(w);
+                    bb.push_back((int)tlist.size());
+                    for (int q = c; q < c + w; ++q) {
+                        tlist.push_back(q << 16 | q);
+                        for (int x = tlist[h[kHdrPanel] + q]; x < tlist[h[kHdrPanel] + q + 1]; ++x)
+                            tlist.push_back(tlist[x] << 16 | q);
+                    }
+                    be.push_back((int)tlist.size());
+                    c += w;
+                }
+                auto& bd = blk_desc[cc];
+                const unsigned long long lo = (unsigned long long)loff[cc];
+                for (size_t b = 0; p->blk_ok && b < bk0.size(); ++b) {
+                    int d[16] = {0};
+                    d[0] = (int)(unsigned)(lo & 0xffffffffull);
+                    d[1] = (int)(unsigned)(lo >> 32);
+                    d[2] = bk0[b];
+                    d[3] = bw[b];
+                    d[4] = bb[b];
+                    d[5] = be[b];
+                    d[12] = nt;
+                    if (b > 0) {
+                        const int k0 = bk0[b - 1], wp = bw[b - 1];
+                        d[6] = bb[b - 1];
+                        d[7] = be[b - 1];
+                        d[8] = k0;
+                        d[9] = wp;
+                        d[10] = (int)tlist.size();
+                        for (int j = bk0[b] + bw[b]; j < nt; ++j)
+                            for (int i = j; i <= nt; ++i) {
+                                int mk = 0;
+                                for (int sx = 0; sx < wp; ++sx)
+                                    if ((i == nt || NZ(i, k0 + sx)) && NZ(j, k0 + sx)) mk |= 1 << sx;
+                                if (mk) tlist.push_back(i << 16 | j << 4 | mk);
+                            }
+                        d[11] = (int)tlist.size();
+                        p->max_blk_trail = std::max(p->max_blk_trail, d[11] - d[10]);
+                    }
+                    bd.insert(bd.end(), d, d + 16);
+                }
+                p->max_blks = std::max(p->max_blks, (int)(bd.size() / 16));
+            }
         }
     }
 
@@ -1897,6 +2185,12 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         for (int cc = 0; cc < p->n_comp; ++cc)
             std::copy(pair_desc[cc].begin(), pair_desc[cc].end(), p->fac_pairs_h.begin() + (size_t)16 * fp * cc);
     }
+    {
+        const int fb = std::max(p->max_blks, 1);
+        p->fac_blks_h.assign((size_t)16 * fb * std::max(p->n_comp, 1), 0);
+        for (int cc = 0; p->blk_ok && cc < p->n_comp; ++cc)
+            std::copy(blk_desc[cc].begin(), blk_desc[cc].end(), p->fac_blks_h.begin() + (size_t)16 * fb * cc);
+    }
     VX_HIP(c, hipSetDevice(c->device));
     // the tables through one pinned staging block: one copy to the device, one launch scattering it
     // into the plan's buffers (a rebuild synchronises before it rewrites the block)
@@ -1904,7 +2198,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         auto pad = [](size_t b) { return (b + 255) & ~(size_t)255; };
         size_t tot = 0;
         auto add = [&](const auto& v) { tot += pad(std::max<size_t>(1, v.size()) * sizeof(v[0])); };
-        add(p->fac_steps_h), add(p->fac_pairs_h), add(flags), add(kcomp), add(klocal), add(p->comp_kf_ptr_h);
+        add(p->fac_steps_h), add(p->fac_pairs_h), add(p->fac_blks_h), add(flags), add(kcomp), add(klocal), add(p->comp_kf_ptr_h);
         add(p->comp_kf_h), add(p->comp_off_h), add(loff), add(p->comp_np_h), add(hdr), add(tlist);
         VX_HIP(c, p->stage.ensure(tot, true));
         VX_HIP(c, p->stage_dev.ensure(tot));
@@ -1925,6 +2219,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
         };
         put(p->fac_steps, p->fac_steps_h);
         put(p->fac_pairs, p->fac_pairs_h);
+        put(p->fac_blks, p->fac_blks_h);
         put(p->kf_flags, flags);
         put(p->kf_comp, kcomp);
         put(p->kf_local, klocal);
@@ -1997,8 +2292,20 @@ size_t lookahead_lds_bytes(int max_nt, int ps) {
 bool factor_multi(int max_nt) {
     const char* e = std::getenv("VX_SBA_FACTOR");
     if (e && std::strcmp(e, "single") == 0) return false;
-    if (e && std::strcmp(e, "multi") == 0) return true;
+    if (e && (std::strcmp(e, "multi") == 0 || std::strcmp(e, "block") == 0)) return true;
     return max_nt > 32;
+}
+// the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, the default where every
+// column fits its LDS) or one column per launch ($VX_SBA_FACTOR=multi)
+bool factor_blocked(const vx_sba_plan* p) {
+    const char* e = std::getenv("VX_SBA_FACTOR");
+    if (e && std::strcmp(e, "multi") == 0) return false;
+    return p->blk_ok;
+}
+// k_sba_fac_blk's LDS: the block's tiles, L^-1, the entries and the two slot tables
+size_t blk_lds_bytes(int max_nt) {
+    return ((size_t)kFbCap + 1) * kPanelStride * sizeof(double) +
+           ((size_t)kFbCap + 2 * kFbW * ((size_t)max_nt + 1) + kFbW + 1) * sizeof(int);
 }
 // workgroups per component and step: workgroup 0 takes the look-ahead column, the others about 8
 // trailing tiles each (two per wave); $VX_SBA_FACTOR_GROUPS overrides
@@ -2011,9 +2318,9 @@ int factor_groups(int max_trail_rest) {
 // The launch configuration of a plan's run (the factor form, LDS sizes), fixed per run.
 struct SbaRunCfg {
     SBAArgs a;
-    size_t lds = 0, bs_lds = 0, la_lds = 0, red_n = 0;
-    int upd_blocks = 1, G = 1, la_ps = 0;
-    bool multi = false, pair = false;
+    size_t lds = 0, bs_lds = 0, la_lds = 0, red_n = 0, blk_lds = 0;
+    int upd_blocks = 1, G = 1, la_ps = 0, Gb = 1;
+    bool multi = false, pair = false, blk = false;
 };
 
 int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
@@ -2046,6 +2353,16 @@ int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
     if (r.multi && r.la_lds > 64 * 1024)
         VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_fac_step),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.la_lds));
+    r.blk = r.multi && !r.pair && factor_blocked(p);
+    if (r.blk) {
+        r.blk_lds = blk_lds_bytes(p->max_nt);
+        static std::atomic<uint64_t> blk_attr{0};
+        VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_sba_fac_blk), (int)r.blk_lds, blk_attr));
+        // workgroup 0 factors the block, the others take ~32 trailing tiles each (4 per wave in flight)
+        r.Gb = 1 + (p->max_blk_trail + 31) / 32;
+        if (const char* e = std::getenv("VX_SBA_FACTOR_GROUPS")) r.Gb = std::atoi(e);
+        r.Gb = std::max(1, std::min(r.Gb, 128));
+    }
     r.red_n = (size_t)p->l_total + (size_t)p->nk * 14;
     return VX_OK;
 }
@@ -2067,7 +2384,19 @@ int sba_assemble(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
 int sba_solve_step(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
     const SBAArgs& a = r.a;
     const int G = r.G;
-    if (r.multi) {
+    if (r.blk) {
+        for (int t = 0; t < p->max_blks; ++t) {
+            FacBlk sd{};  // (one component: the launch's bounds as arguments)
+            if (p->n_comp == 1) {
+                const int* d = p->fac_blks_h.data() + 16 * (size_t)t;
+                sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
+                sd.K0 = d[2], sd.W = d[3], sd.bt_beg = d[4], sd.bt_end = d[5], sd.pb_beg = d[6], sd.pb_end = d[7];
+                sd.K0p = d[8], sd.Wp = d[9], sd.tr_beg = d[10], sd.tr_end = d[11], sd.nt = d[12];
+            }
+            VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_blk, dim3(std::max(p->n_comp, 1) * r.Gb), dim3(kFbThreads),
+                             (uint32_t)r.blk_lds, c->stream, a, it, t, r.Gb, kFbCap, sd));
+        }
+    } else if (r.multi) {
         VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
                          c->stream, a, it, r.pair ? 1 : 0));
         for (int t = 0; r.pair && t < p->max_pairs; ++t) {

@@ -44,6 +44,13 @@ struct vx_sba_plan {
     std::vector<int> fac_pairs_h;
     vx::DevBuf fac_pairs;
     int max_pairs = 0;
+    // the blocked factor (k_sba_fac_blk; launch t factors block t of up to 4 tile columns): 16 ints
+    // per component and launch (FacBlk); max_blks launches; blk_ok: every column fits the block LDS;
+    // max_blk_trail: most trailing tiles of one launch
+    std::vector<int> fac_blks_h;
+    vx::DevBuf fac_blks;
+    int max_blks = 0, max_blk_trail = 0;
+    bool blk_ok = false;
     int max_back = 0;  // most back-substitution tiles of one component (k_sba_backsub stages the lists in LDS)
     int diag_split = 1;  // k_sba_blocks workgroups per diagonal block (sba_plan_finish)
     vx::DevBuf bpart;    // their partial sums

@@ -203,9 +203,7 @@ int vx_create_ex(int device, int priority, const uint32_t* cu_mask, int mask_wor
         (cu_mask && mask_words > 0)
             ? hipExtStreamCreateWithCUMask(&c->stream, (uint32_t)mask_words, cu_mask)
             : hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, priority > 0 ? greatest : least);
-    // the match count / arrival counter (k_knn_rows' fused compaction keeps [1] at zero between
-    // launches), zeroed once here: no capture ever contains its first initialisation
-    if (se != hipSuccess || c->match_count.ensure(16) != hipSuccess || hipMemset(c->match_count.p, 0, 16) != hipSuccess) {
+    if (se != hipSuccess) {
         vx_destroy(c);
         return VX_ERR_HIP;
     }
