@@ -20,6 +20,7 @@ from ktrace_ba import read  # noqa: E402
 
 
 def main():
+    os.environ.setdefault("VX_SBA_FACTOR", "block")  # (read per run by the plan)
     ctx = vxslam.Context(0)
     m = synth.make_ba_map(0x5EED0000 + 200, 200, 100000, n_streams=8, n_old_kf=16, cross_frac=0.03)
     plan = ctx.sba_plan(m, vxslam.default_sba_options(window=200, iters=2))

@@ -611,6 +611,55 @@ __device__ __forceinline__ bool potrf_inv16_t(Rd rd, double* lds_inv, double* Lg
     }
     return ok;
 }
+// The same factor + inverse with four lanes per row (lane 4 i + q: row i, columns 4 q .. 4 q + 3):
+// per column j the pivot comes by v_readlane, L_ij = a_ij / L_jj is formed on the quad lane that holds
+// column j and spread over its quad by a quad_perm DPP move, and each lane takes the L_cj of its own
+// four columns from lanes 4 c by ds_bpermute — four FMAs per lane per column instead of fifteen, and
+// four permutes instead of fifteen scalar broadcasts.  Every element sees the same operations in the
+// same order as potrf_inv16_t: bitwise the same L^-1.
+template <int J>
+__device__ __forceinline__ double quad_bcast(double v) {
+    constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);  // quad_perm [J, J, J, J]
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+template <class Rd>
+__device__ __forceinline__ bool potrf_inv16_quad(Rd rd, double* lds_inv, double* Lg) {
+    const int lane = threadIdx.x & 63, i = lane >> 2, q = lane & 3;
+    double a[4], x[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int c = 4 * q + m;
+        a[m] = c <= i ? rd(i, c) : rd(c, i);
+        x[m] = c == i ? 1.0 : 0.0;
+    }
+    bool ok = true;
+    static_for<0, 16>([&](auto jc) {
+        constexpr int j = decltype(jc)::value, jq = j >> 2, jm = j & 3;
+        const double d = rl(a[jm], 4 * j + jq);
+        ok = ok && d > 0.0 && d < 1e300;
+        const double r = frsq(d > 0.0 ? d : 1.0);  // (uniform: 1 / L_jj)
+        const double l = quad_bcast<jq>(a[jm] * r);  // L[i][j] for i >= j
+        if (q == jq) x[jm] *= r;
+        const double xj = quad_bcast<jq>(x[jm]);
+        double lc[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) lc[m] = __shfl(l, 4 * (4 * q + m), 64);  // L[c][j] from quad c
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            if (4 * q + m > j) {
+                a[m] = fma(-l, lc[m], a[m]);
+                x[m] = fma(-lc[m], xj, x[m]);
+            }
+    });
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        lds_inv[opo(4 * q + m, i)] = x[m];
+        Lg[(4 * q + m) * 16 + i] = x[m];
+    }
+    return ok;
+}
 __device__ __forceinline__ bool potrf_inv16(const double* A, int ld, double* lcol, double* lds_inv, double* Lg) {
     (void)lcol;
     return potrf_inv16_t([&](int r, int c) { return A[(long long)r * ld + c]; }, lds_inv, Lg);
@@ -1193,7 +1242,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_pair(SBAArgs a, int i
 constexpr int kFbThreads = 512;
 constexpr int kFbWaves = kFbThreads / 64;
 constexpr int kFbW = 4;       // tile columns per block (4-bit step masks)
-constexpr int kFbCap = 72;    // LDS tiles of a block (operand order, 2 KB each)
+constexpr int kFbCap = 60;    // LDS tiles of a block (operand order, 2 KB each)
 
 __device__ __forceinline__ d4 load_acc_opo(const double* S) {
     const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
@@ -1260,7 +1309,6 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     // trace build: launch nt / 8 (slots 10-15 workgroup 0: entry, tables, look-ahead, column 0's
     // POTRF, panel, block done; 7: another workgroup's trailing tiles)
     const bool kt = t == nt / 8;
-    if (kt) VX_KT(10);
     double* L = a.L + sd.loff;
     double* Linv = a.Linv + sd.loff;
     const int* tl = a.tl;
@@ -1275,6 +1323,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         __syncthreads();
     } else {
         if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (launch 0's decision)
+        if (kt) VX_KT(10);
         if (g > 0 || G == 1) {
             const int gg = G == 1 ? 0 : g - 1, GG = G == 1 ? 1 : G - 1;
             blk_trail(L, np, tl, sd.K0p, sd.tr_beg + gg, sd.tr_end, GG, kFbWaves);
@@ -1286,7 +1335,8 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     const int K0 = sd.K0, W = sd.W, n = sd.bt_end - sd.bt_beg, n1 = nt + 1;
     double* T = sm;                                   // cap tiles, operand order
     double* dlds = sm + (size_t)cap * kPanelStride;   // L_cc^-1 of the current column
-    int* ent = reinterpret_cast<int*>(dlds + kPanelStride);  // cap entries i << 16 | c
+    double* Bst = dlds + kPanelStride;                // kFbW x kFbW: L(K0 + cc, K0p + q), operand order
+    int* ent = reinterpret_cast<int*>(Bst + kFbW * kFbW * kPanelStride);  // cap entries i << 16 | c
     int* rs = ent + cap;                              // kFbW x n1: slot of (i, K0 + cc), -1: none
     int* pz = rs + kFbW * n1;                         // kFbW x n1: tile (i, K0p + cc) of block t - 1 nonzero
     int* cb = pz + kFbW * n1;                         // kFbW + 1: first slot of column cc (its diagonal)
@@ -1308,30 +1358,70 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     if (tid <= W) cb[tid] = tid < W ? rs[tid * n1 + K0 + tid] : n;
     if (kt) VX_KT(11);
     // block t's tiles into LDS with block t - 1's steps (tile (i, j), step k: NZ(i, k) and NZ(j, k);
-    // the rhs row i = nt is in every column's list)
-    for (int m0 = wv * 4; m0 < n; m0 += kFbWaves * 4) {
-        d4 c[4];
-        int ti[4], tj[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ti[q] = -1;
-            if (m0 + q < n) {
-                const int e = ent[m0 + q];
-                ti[q] = e >> 16;
-                tj[q] = e & 0xffff;
-                c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
-            }
+    // the rhs row i = nt is in every column's list).  Row by row: the block's B operands
+    // L(K0 + cc, K0p + q) are staged in LDS once, and per row a wave issues its A operands
+    // L(i, K0p + q) and its tiles together — one memory round trip per row, not one per step and tile.
+    if (t == 0) {
+        for (int m = wv; m < n; m += kFbWaves) {
+            const int e = ent[m];
+            store_acc_opo(T + (size_t)m * kPanelStride, load_acc(L + (long long)(16 * (e >> 16)) * np + 16 * (e & 0xffff), np));
         }
+    } else {
+        const int r0 = lane >> 4, cl = lane & 15, Wp = sd.Wp, K0p = sd.K0p;
+        for (int x = wv; x < W * Wp; x += kFbWaves) {
+            const int cc = x / Wp, q = x - cc * Wp;
+            *reinterpret_cast<double4*>(Bst + (size_t)(cc * kFbW + q) * kPanelStride + 4 * lane) =
+                *reinterpret_cast<const double4*>(L + (long long)(16 * (K0 + cc) + cl) * np + 16 * (K0p + q) + 4 * r0);
+        }
+        __syncthreads();
+        // rows of the wave: K0 + wv, K0 + wv + kFbWaves, ... that hold a tile of the block; row r + 1's
+        // operands are requested before row r's products (software-pipelined: one exposed round trip)
+        auto has_row = [&](int i) {
+            bool any = false;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (ti[q] < 0) continue;
-            for (int s = 0; t > 0 && s < sd.Wp; ++s)
-                if (pz[s * n1 + ti[q]] && pz[s * n1 + tj[q]]) {
-                    const int k = sd.K0p + s;
-                    c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * k, L + (long long)(16 * tj[q]) * np + 16 * k,
-                                      np, c[q]);
-                }
-            store_acc_opo(T + (size_t)(m0 + q) * kPanelStride, c[q]);
+            for (int cc = 0; cc < kFbW; ++cc) any = any || (cc < W && rs[cc * n1 + i] >= 0);
+            return any;
+        };
+        auto next_row = [&](int i) {
+            while (i <= nt && !has_row(i)) i += kFbWaves;
+            return i;
+        };
+        auto fetch = [&](int i, double4 (&ao)[kFbW], d4 (&acc)[kFbW]) {
+#pragma unroll
+            for (int q = 0; q < kFbW; ++q)
+                ao[q] = *reinterpret_cast<const double4*>(L + (long long)(16 * i + cl) * np + 16 * (K0p + min(q, Wp - 1)) + 4 * r0);
+#pragma unroll
+            for (int cc = 0; cc < kFbW; ++cc)
+                if (cc < W && rs[cc * n1 + i] >= 0) acc[cc] = load_acc(L + (long long)(16 * i) * np + 16 * (K0 + cc), np);
+        };
+        double4 ao[kFbW], ao2[kFbW];
+        d4 acc[kFbW], acc2[kFbW];
+        int i = next_row(K0 + wv);
+        if (i <= nt) fetch(i, ao, acc);
+        while (i <= nt) {
+            const int i2 = next_row(i + kFbWaves);
+            if (i2 <= nt) fetch(i2, ao2, acc2);
+#pragma unroll
+            for (int cc = 0; cc < kFbW; ++cc) {
+                const int sl = cc < W ? rs[cc * n1 + i] : -1;
+                if (sl < 0) continue;
+#pragma unroll
+                for (int q = 0; q < kFbW; ++q)
+                    if (q < Wp && pz[q * n1 + i] && pz[q * n1 + K0 + cc]) {  // (the order of mfma_abt_g)
+                        const double4 bv = *reinterpret_cast<const double4*>(Bst + (size_t)(cc * kFbW + q) * kPanelStride + 4 * lane);
+                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].x, bv.x, acc[cc], 0, 0, 0);
+                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].y, bv.y, acc[cc], 0, 0, 0);
+                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].z, bv.z, acc[cc], 0, 0, 0);
+                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].w, bv.w, acc[cc], 0, 0, 0);
+                    }
+                store_acc_opo(T + (size_t)sl * kPanelStride, acc[cc]);
+            }
+#pragma unroll
+            for (int q = 0; q < kFbW; ++q) {
+                ao[q] = ao2[q];
+                acc[q] = acc2[q];
+            }
+            i = i2;
         }
     }
     __syncthreads();
@@ -1341,7 +1431,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         const int c = K0 + cc, s0 = cb[cc], s1 = cb[cc + 1];
         if (wv == 0) {
             const double* D = T + (size_t)s0 * kPanelStride;
-            ok = potrf_inv16_t([&](int r, int q) { return D[opo(r, q)]; }, dlds, Linv + 256 * c) && ok;
+            ok = potrf_inv16_quad([&](int r, int q) { return D[opo(r, q)]; }, dlds, Linv + 256 * c) && ok;
         }
         __syncthreads();
         if (kt && cc == 0) VX_KT(13);
@@ -2295,16 +2385,15 @@ bool factor_multi(int max_nt) {
     if (e && (std::strcmp(e, "multi") == 0 || std::strcmp(e, "block") == 0)) return true;
     return max_nt > 32;
 }
-// the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, the default where every
-// column fits its LDS) or one column per launch ($VX_SBA_FACTOR=multi)
+// the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, $VX_SBA_FACTOR=block,
+// where every column fits its LDS) or one column per launch (the default: DESIGN.md §22)
 bool factor_blocked(const vx_sba_plan* p) {
     const char* e = std::getenv("VX_SBA_FACTOR");
-    if (e && std::strcmp(e, "multi") == 0) return false;
-    return p->blk_ok;
+    return e && std::strcmp(e, "block") == 0 && p->blk_ok;
 }
-// k_sba_fac_blk's LDS: the block's tiles, L^-1, the entries and the two slot tables
+// k_sba_fac_blk's LDS: the block's tiles, L^-1, the staged B operands, the entries and the two slot tables
 size_t blk_lds_bytes(int max_nt) {
-    return ((size_t)kFbCap + 1) * kPanelStride * sizeof(double) +
+    return ((size_t)kFbCap + 1 + kFbW * kFbW) * kPanelStride * sizeof(double) +
            ((size_t)kFbCap + 2 * kFbW * ((size_t)max_nt + 1) + kFbW + 1) * sizeof(int);
 }
 // workgroups per component and step: workgroup 0 takes the look-ahead column, the others about 8
