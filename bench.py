@@ -737,7 +737,7 @@ def bench_c5(args):
         n_fac = sum(1 for i in range(max(its - 1, 0)) if steps_c[i] != 0)
         if dominant == "sba_solve" and n_fac:
             tfs = work["flops"] * n_fac / (ms_step * 1e-3) / 1e12
-            roofline = {"kernel": "sba_solve", "hip_kernel": "k_sba_fac_step / k_sba_solve + k_sba_backsub",
+            roofline = {"kernel": "sba_solve", "hip_kernel": "k_sba_fac_blk (k_sba_fac_step, k_sba_solve) + k_sba_backsub",
                         "bound": "mfma", "achieved": round(tfs, 4), "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                         "frac": round(tfs / FP64_PEAK_TFS, 6), "traffic": None,
                         "flops_per_factorisation": int(work["flops"]), "factorisations_per_step": n_fac,

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Phase timestamps of the blocked Schur factor (trace build) on the connected C5 window: launch
-t = nt / 8 of k_sba_fac_blk (workgroup 0: 11 slot tables, 12 look-ahead tiles in LDS, 13 column 0's
-POTRF + inverse, 14 its panel, 15 the block done; the other workgroups: 7 their trailing tiles).
+t = nt / 8 of k_sba_fac_blk (workgroup 0: 11 slot tables, 14 B operands staged, 0-7 each wave's
+look-ahead rows, 12 look-ahead tiles in LDS, 13 column 0's POTRF + inverse, 15 the block done; the
+other workgroups: 7 their trailing tiles).
 
     make -C visionx-slam_amd trace && VX_LIB=visionx-slam_amd/lib/libvxslam_trace.so \\
         python3 scripts/ktrace_sba_blk.py
@@ -30,9 +31,10 @@ def main():
     ctx.synchronize()
     tr, cy = read("vx_ktrace_read_sba")
     b0 = tr[0]
-    names = {11: "tables", 12: "look-ahead", 13: "col0 POTRF", 14: "col0 panel", 15: "block done"}
+    names = {11: "tables", 14: "B staged", 12: "look-ahead", 13: "col0 POTRF", 15: "block done"}
     print("k_sba_fac_blk workgroup 0 (us from entry):",
-          " ".join(f"{names[s]} {(b0[s] - b0[10]) / 100:.2f}" for s in range(11, 16) if b0[s] > 0))
+          " ".join(f"{names[s]} {(b0[s] - b0[10]) / 100:.2f}" for s in (11, 14, 12, 13, 15) if b0[s] > 0))
+    print("  per wave, look-ahead rows done:", " ".join(f"{(b0[w] - b0[10]) / 100:.2f}" for w in range(8) if b0[w] > 0))
     rest = [b for b in range(1, tr.shape[0]) if tr[b, 10] > 0 and tr[b, 7] > 0]
     if rest:
         d = np.array([(tr[b, 7] - tr[b, 10]) / 100 for b in rest])

@@ -36,7 +36,7 @@ disp = collections.defaultdict(lambda: collections.defaultdict(float))
 meta = {}
 for r in rows:
     nm = r["Kernel_Name"]
-    if not any(k in nm for k in ("k_sba_fac_begin", "k_sba_fac_step", "k_sba_backsub")):
+    if not any(k in nm for k in ("k_sba_fac_begin", "k_sba_fac_step", "k_sba_fac_blk", "k_sba_backsub")):
         continue
     d = int(r["Dispatch_Id"])
     disp[d][r["Counter_Name"]] += float(r["Counter_Value"])

@@ -1306,8 +1306,9 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     if (it > 0 && !a.st->active[it]) return;
     const int nt = sd.nt, np = 16 * nt;
     if (nt == 0) return;  // (this component has no block t)
-    // trace build: launch nt / 8 (slots 10-15 workgroup 0: entry, tables, look-ahead, column 0's
-    // POTRF, panel, block done; 7: another workgroup's trailing tiles)
+    // trace build: launch nt / 8 (workgroup 0: 10 entry, 11 tables, 14 B operands staged, 0-7 each
+    // wave's look-ahead rows, 12 look-ahead, 13 column 0's POTRF, 15 block done; 7 of another
+    // workgroup: its trailing tiles)
     const bool kt = t == nt / 8;
     double* L = a.L + sd.loff;
     double* Linv = a.Linv + sd.loff;
@@ -1368,12 +1369,6 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         }
     } else {
         const int r0 = lane >> 4, cl = lane & 15, Wp = sd.Wp, K0p = sd.K0p;
-        for (int x = wv; x < W * Wp; x += kFbWaves) {
-            const int cc = x / Wp, q = x - cc * Wp;
-            *reinterpret_cast<double4*>(Bst + (size_t)(cc * kFbW + q) * kPanelStride + 4 * lane) =
-                *reinterpret_cast<const double4*>(L + (long long)(16 * (K0 + cc) + cl) * np + 16 * (K0p + q) + 4 * r0);
-        }
-        __syncthreads();
         // rows of the wave: K0 + wv, K0 + wv + kFbWaves, ... that hold a tile of the block; row r + 1's
         // operands are requested before row r's products (software-pipelined: one exposed round trip)
         auto has_row = [&](int i) {
@@ -1397,7 +1392,14 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         double4 ao[kFbW], ao2[kFbW];
         d4 acc[kFbW], acc2[kFbW];
         int i = next_row(K0 + wv);
-        if (i <= nt) fetch(i, ao, acc);
+        if (i <= nt) fetch(i, ao, acc);  // (the first row's round trip overlaps the B staging)
+        for (int x = wv; x < W * Wp; x += kFbWaves) {
+            const int cc = x / Wp, q = x - cc * Wp;
+            *reinterpret_cast<double4*>(Bst + (size_t)(cc * kFbW + q) * kPanelStride + 4 * lane) =
+                *reinterpret_cast<const double4*>(L + (long long)(16 * (K0 + cc) + cl) * np + 16 * (K0p + q) + 4 * r0);
+        }
+        __syncthreads();
+        if (kt) VX_KT(14);
         while (i <= nt) {
             const int i2 = next_row(i + kFbWaves);
             if (i2 <= nt) fetch(i2, ao2, acc2);
@@ -1423,6 +1425,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
             }
             i = i2;
         }
+        if (kt) VX_KTW(0, kFbWaves);  // (per wave: its look-ahead rows done)
     }
     __syncthreads();
     if (kt) VX_KT(12);
@@ -1450,7 +1453,6 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
             store_acc(L + (long long)(16 * (ent[s] >> 16)) * np + 16 * c, np, r);
         }
         __syncthreads();
-        if (kt && cc == 0) VX_KT(14);
         if (cc + 1 == W) break;
         // step c on the block's later columns c2: tiles (i, c2), i >= c2, for NZ(c2, c) — rows of
         // column c from the slot of (c2, c) on
@@ -2385,11 +2387,13 @@ bool factor_multi(int max_nt) {
     if (e && (std::strcmp(e, "multi") == 0 || std::strcmp(e, "block") == 0)) return true;
     return max_nt > 32;
 }
-// the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, $VX_SBA_FACTOR=block,
-// where every column fits its LDS) or one column per launch (the default: DESIGN.md §22)
+// the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, the default where every
+// column fits its LDS: connected C5 786 against 937 us per LM iteration) or one column
+// per launch ($VX_SBA_FACTOR=multi)
 bool factor_blocked(const vx_sba_plan* p) {
     const char* e = std::getenv("VX_SBA_FACTOR");
-    return e && std::strcmp(e, "block") == 0 && p->blk_ok;
+    if (e && std::strcmp(e, "multi") == 0) return false;
+    return p->blk_ok;
 }
 // k_sba_fac_blk's LDS: the block's tiles, L^-1, the staged B operands, the entries and the two slot tables
 size_t blk_lds_bytes(int max_nt) {
