@@ -401,6 +401,14 @@ int vx_ba_dmap_results(vx_ctx* ctx, vx_dmap* map, int cap_kf, int64_t* kf_rows, 
  * its one synchronisation, so vx_ba_dmap_results then only copies on the host — no device call, no
  * second synchronisation (what a drop-in that writes every result back wants; default off). */
 int vx_dmap_prefetch_results(vx_dmap* map, int on);
+/* The same results without a copy, with prefetching on: pointers into the pinned block the last
+ * vx_ba_optimize_dmap filled, valid until the next vx_ba_optimize_dmap / vx_dmap_* call on the map —
+ * *n_kf keyframe rows (int32) with their poses (8 doubles each: qx qy qz qw tx ty tz, pad), *n_lm
+ * landmark rows (int32) with their positions (4 doubles each: x y z, pad); both counts 0 (pointers
+ * NULL) when nothing was optimised.  VX_ERR_STATE when the results were not prefetched (prefetching
+ * off, or a run that fell back to a built plan): use vx_ba_dmap_results then. */
+int vx_ba_dmap_results_view(vx_ctx* ctx, vx_dmap* map, const int32_t** kf_rows, const double** kf_pose8,
+                            const int32_t** lm_rows, const double** lm_pos4, int* n_kf, int* n_lm);
 
 /* ---------------------------------------------------------------- Schur-complement joint BA
  * NOT a reference entry point: the reference's LocalBA alternates per-keyframe and per-landmark

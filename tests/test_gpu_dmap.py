@@ -528,6 +528,10 @@ def test_dmap_prefetched_results_equal(ctx):
             out.append(d.results())
         for a, b in zip(*out):
             assert np.array_equal(a, b)
+        for a, b in zip(out[1], maps[1].results_view()):  # (vx_ba_dmap_results_view: in place)
+            assert np.array_equal(a, b)
+    with pytest.raises(vxslam.VxError):  # (not prefetched)
+        maps[0].results_view()
     sp = maps[1].sba_plan(vxslam.default_sba_options(window=12, iters=2), ref_kf_id=m["ref_kf_id"])
     with pytest.raises(vxslam.VxError):
         maps[1].results()

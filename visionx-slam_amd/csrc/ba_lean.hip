@@ -1142,6 +1142,28 @@ int vx_dmap_prefetch_results(vx_dmap* m, int on) {
     return VX_OK;
 }
 
+int vx_ba_dmap_results_view(vx_ctx* c, vx_dmap* m, const int32_t** kf_rows, const double** kf_pose8,
+                            const int32_t** lm_rows, const double** lm_pos4, int* n_kf, int* n_lm) {
+    if (!c || !m || m->c != c || !n_kf || !n_lm || !kf_rows || !kf_pose8 || !lm_rows || !lm_pos4)
+        return c ? set_error(c, VX_ERR_INVALID, "vx_ba_dmap_results_view: bad arguments") : VX_ERR_INVALID;
+    auto& L = m->lean;
+    if (!L.ran) return set_error(c, VX_ERR_STATE, "no vx_ba_optimize_dmap to report");
+    const bool changed = L.status == 0 && L.iterations > 0;
+    *n_kf = changed ? L.nk : 0;
+    *n_lm = changed ? L.n_opt : 0;
+    *kf_rows = *lm_rows = nullptr;
+    *kf_pose8 = *lm_pos4 = nullptr;
+    if (!changed) return VX_OK;
+    if (!L.prefetched || L.fallback || L.n_opt > L.pf_nl)
+        return set_error(c, VX_ERR_STATE, "results not prefetched (vx_dmap_prefetch_results): use vx_ba_dmap_results");
+    const double* base = reinterpret_cast<const double*>(L.res_host.p);
+    *kf_rows = L.win_rows.data();
+    *kf_pose8 = base + (size_t)(L.iterations & 1) * L.nk * 8;
+    *lm_pos4 = base + 2 * (size_t)L.nk * 8;
+    *lm_rows = reinterpret_cast<const int32_t*>(*lm_pos4 + (size_t)L.pf_nl * 4);
+    return VX_OK;
+}
+
 int vx_ba_dmap_results(vx_ctx* c, vx_dmap* m, int cap_kf, int64_t* kf_rows, double* kf_pose7, int cap_lm,
                        int64_t* lm_rows, double* lm_pos3, int* n_kf, int* n_lm) {
     if (!c || !m || m->c != c || !n_kf || !n_lm) return c ? set_error(c, VX_ERR_INVALID, "vx_ba_dmap_results: bad arguments") : VX_ERR_INVALID;

@@ -134,6 +134,7 @@ private:
     vx_ba_stats stats_{};
     std::shared_ptr<DeviceMap> dmap_;
     std::vector<int64_t> kf_rows_, lm_rows_;
+    std::vector<int32_t> kr32_, lr32_;  // (the copying fallback's rows, as the view's)
     std::vector<double> kf_out_, lm_out_;
     FlatMap flat_;  // the snapshot path's window, reused call after call
 };

@@ -437,37 +437,59 @@ void LocalBA::UseDeviceMap(std::shared_ptr<DeviceMap> dm) {
 
 void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
     DeviceMap& dm = *dmap_;
+    static const bool timing = std::getenv("VX_RESIDENT_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (timing)
+            fprintf(stderr, "[vx resident] %s %.1f us\n", what,
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    };
     dm.Flush();
+    lap("flush");
     vx_ctx* c = dm.context();
     const vx_ba_options o = VxOptions();
     check(c, vx_ba_optimize_dmap(c, dm.handle(), ref_kf ? ref_kf->Id() : 0, ref_kf ? 1 : 0, &o, &stats_),
           "vx_ba_optimize_dmap");
-    int nk = 0, nl = 0;
-    int rc = vx_ba_dmap_results(c, dm.handle(), (int)kf_rows_.size(), kf_rows_.data(), kf_out_.data(),
+    lap("optimize");
+    // the results in place in the pinned block the call filled (vx_ba_dmap_results_view; prefetching
+    // is on from UseDeviceMap), the copying vx_ba_dmap_results otherwise
+    const int32_t *kr = nullptr, *lr = nullptr;
+    const double *kp = nullptr, *lp = nullptr;
+    int nk = 0, nl = 0, ks = 8, ls = 4;
+    int rc = vx_ba_dmap_results_view(c, dm.handle(), &kr, &kp, &lr, &lp, &nk, &nl);
+    if (rc == VX_ERR_STATE) {
+        rc = vx_ba_dmap_results(c, dm.handle(), (int)kf_rows_.size(), kf_rows_.data(), kf_out_.data(),
                                 (int)lm_rows_.size(), lm_rows_.data(), lm_out_.data(), &nk, &nl);
-    if (rc == VX_ERR_CAPACITY) {  // (the buffers keep the largest window seen)
-        kf_rows_.resize(nk);
-        kf_out_.resize(7 * (size_t)nk);
-        lm_rows_.resize(nl);
-        lm_out_.resize(3 * (size_t)nl);
-        rc = vx_ba_dmap_results(c, dm.handle(), nk, kf_rows_.data(), kf_out_.data(), nl, lm_rows_.data(),
-                                lm_out_.data(), &nk, &nl);
+        if (rc == VX_ERR_CAPACITY) {  // (the buffers keep the largest window seen)
+            kf_rows_.resize(nk);
+            kf_out_.resize(7 * (size_t)nk);
+            lm_rows_.resize(nl);
+            lm_out_.resize(3 * (size_t)nl);
+            rc = vx_ba_dmap_results(c, dm.handle(), nk, kf_rows_.data(), kf_out_.data(), nl, lm_rows_.data(),
+                                    lm_out_.data(), &nk, &nl);
+        }
+        check(c, rc, "vx_ba_dmap_results");
+        kr32_.assign(kf_rows_.begin(), kf_rows_.begin() + nk);
+        lr32_.assign(lm_rows_.begin(), lm_rows_.begin() + nl);
+        kr = kr32_.data(), kp = kf_out_.data(), lr = lr32_.data(), lp = lm_out_.data(), ks = 7, ls = 3;
     }
-    check(c, rc, "vx_ba_dmap_results");
+    check(c, rc, "vx_ba_dmap_results_view");
+    lap("results");
     // Frame::SetPose / Landmark::SetPosition (local_ba.cpp:173,237) on the host objects (the
     // landmarks over the host pool: each SetPosition takes only that landmark's mutex)
     for (int i = 0; i < nk; ++i) {
-        const double* p = &kf_out_[7 * (size_t)i];
+        const double* p = kp + (size_t)ks * i;
         SE3d T;
         T.qx = p[0]; T.qy = p[1]; T.qz = p[2]; T.qw = p[3];
         T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
-        if (const auto& fr = dm.FrameAt(kf_rows_[i])) fr->SetPose(T);
+        if (const auto& fr = dm.FrameAt(kr[i])) fr->SetPose(T);
     }
     vxhost::Pool::Get().For((size_t)nl, 1024, [&](size_t a, size_t b) {
         for (size_t i = a; i < b; ++i)
-            if (const auto& lm = dm.LandmarkAt(lm_rows_[i]))
-                lm->SetPosition(Vec3d(lm_out_[3 * i], lm_out_[3 * i + 1], lm_out_[3 * i + 2]));
+            if (const auto& lm = dm.LandmarkAt(lr[i]))
+                lm->SetPosition(Vec3d(lp[ls * i], lp[ls * i + 1], lp[ls * i + 2]));
     });
+    lap("write-back");
 }
 
 void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {

@@ -91,7 +91,7 @@ EXPORTS = [
     "vx_dmap_remove_observations", "vx_dmap_remove_keyframe", "vx_dmap_remove_landmarks", "vx_dmap_set_features",
     "vx_dmap_set_landmark_bad", "vx_dmap_set_poses", "vx_dmap_counts", "vx_dmap_live_counts", "vx_dmap_download",
     "vx_ba_plan_create_dmap", "vx_ba_plan_apply_dmap", "vx_ba_shard_emulate_run", "vx_ba_optimize_dmap",
-    "vx_ba_dmap_results", "vx_dmap_prefetch_results", "vx_sba_plan_factor_work", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_shard_emulate_run", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
+    "vx_ba_dmap_results", "vx_ba_dmap_results_view", "vx_dmap_prefetch_results", "vx_sba_plan_factor_work", "vx_sba_plan_create_dmap", "vx_sba_plan_rebuild_dmap", "vx_sba_shard_emulate_run", "vx_sba_plan_apply_dmap", "vx_seq_create", "vx_seq_destroy", "vx_seq_wait", "vx_seq_record", "vx_seq_extract",
     "vx_seq_match", "vx_seq_ba_run", "vx_seq_length", "vx_seq_run", "vx_seq_set_threads",
     "vx_orb_extract_batch_async", "vx_orb_batch_fetch", "vx_orb_batch_device", "vx_match_batch_async",
     "vx_match_batch_fetch", "vx_orb_extract_batch", "vx_match_knn2_ratio_batch", "vx_orb_set_order",
@@ -964,6 +964,23 @@ class DMap:
         self.ctx._check(lib().vx_ba_dmap_results(self.ctx.handle, self._h, len(kr), _p(kr), _p(kp), len(lr), _p(lr),
                                                  _p(lp), C.byref(nk), C.byref(nl)))
         return kr[:nk.value], kp[:nk.value], lr[:nl.value], lp[:nl.value]
+
+    def results_view(self):
+        """vx_ba_dmap_results_view (prefetching on): the same four arrays as results(), read from the
+        pinned block the last optimize() filled (copied here; the C++ adapter reads them in place)."""
+        kr, lr = C.POINTER(C.c_int32)(), C.POINTER(C.c_int32)()
+        kp, lp = C.POINTER(C.c_double)(), C.POINTER(C.c_double)()
+        nk, nl = C.c_int(0), C.c_int(0)
+        self.ctx._check(lib().vx_ba_dmap_results_view(self.ctx.handle, self._h, C.byref(kr), C.byref(kp), C.byref(lr),
+                                                      C.byref(lp), C.byref(nk), C.byref(nl)))
+        n, m = nk.value, nl.value
+        if n == 0 and m == 0:
+            return (np.zeros(0, np.int64), np.zeros((0, 7)), np.zeros(0, np.int64), np.zeros((0, 3)))
+        k_rows = np.ctypeslib.as_array(kr, (n,)).astype(np.int64)
+        k_pose = np.ctypeslib.as_array(kp, (n, 8))[:, :7].copy()
+        l_rows = np.ctypeslib.as_array(lr, (m,)).astype(np.int64)
+        l_pos = np.ctypeslib.as_array(lp, (m, 4))[:, :3].copy()
+        return k_rows, k_pose, l_rows, l_pos
 
     def close(self):
         if self._h:
