@@ -7,10 +7,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstddef>
 #include <cstdlib>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -28,6 +30,18 @@ public:
     }
     int Threads() const { return (int)workers_.size() + 1; }
 
+    // Wake the workers into their spin phase ahead of a job the caller knows is coming (the LocalBA
+    // write-back after the device call): a sleeping worker's futex wake costs tens of microseconds,
+    // which a job over ~20k landmarks cannot hide.
+    void Prime() {
+        if (workers_.empty()) return;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            ++prime_;
+        }
+        cv_.notify_all();
+    }
+
     // fn(begin, end) over [0, n) in chunks of at least min_chunk items; returns when every chunk is done
     void For(size_t n, size_t min_chunk, const std::function<void(size_t, size_t)>& fn) {
         if (n == 0) return;
@@ -37,73 +51,103 @@ public:
             return;
         }
         std::lock_guard<std::mutex> serial(submit_);
+        // each job has its own counters: a worker that arrives after the job is done only finds
+        // next >= n (it never calls fn then), whatever job runs next
+        auto job = std::make_shared<Job>();
+        job->fn = &fn;
+        job->n = n;
+        job->chunk = (n + parts - 1) / parts;
         {
             std::lock_guard<std::mutex> lk(m_);
-            fn_ = &fn;
-            n_ = n;
-            chunk_ = (n + parts - 1) / parts;
-            next_.store(0, std::memory_order_relaxed);
-            busy_ = (int)workers_.size();
-            ++gen_;
+            cur_ = job;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
-        Work();
-        std::unique_lock<std::mutex> lk(m_);
-        done_cv_.wait(lk, [&] { return busy_ == 0; });
-        fn_ = nullptr;
+        Run(*job);
+        while (job->done.load(std::memory_order_acquire) < n) Relax();
     }
 
     Pool(const Pool&) = delete;
     Pool& operator=(const Pool&) = delete;
 
 private:
+    struct Job {
+        const std::function<void(size_t, size_t)>* fn = nullptr;
+        size_t n = 0, chunk = 1;
+        std::atomic<size_t> next{0}, done{0};
+    };
     Pool() {
         int want = 8;
         cpu_set_t set;
         if (sched_getaffinity(0, sizeof(set), &set) == 0) want = std::min(want, CPU_COUNT(&set));
         if (const char* e = std::getenv("VX_HOST_THREADS")) want = std::max(1, std::atoi(e));
+        if (const char* e = std::getenv("VX_HOST_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
         for (int i = 1; i < want; ++i) workers_.emplace_back([this] { Loop(); });
     }
     ~Pool() {
         {
             std::lock_guard<std::mutex> lk(m_);
             stop_ = true;
-            ++gen_;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto& t : workers_) t.join();
     }
-    void Work() {
+    static void Relax() { __builtin_ia32_pause(); }
+    static void Run(Job& j) {
         for (;;) {
-            const size_t b = next_.fetch_add(chunk_, std::memory_order_relaxed);
-            if (b >= n_) return;
-            (*fn_)(b, std::min(n_, b + chunk_));
+            const size_t b = j.next.fetch_add(j.chunk, std::memory_order_acq_rel);
+            if (b >= j.n) return;
+            const size_t e = std::min(j.n, b + j.chunk);
+            (*j.fn)(b, e);
+            j.done.fetch_add(e - b, std::memory_order_acq_rel);
         }
     }
+    // A worker spins for spin_us_ ($VX_HOST_SPIN_US, default 0) after a job or a Prime() before it
+    // sleeps again.
     void Loop() {
-        unsigned long long seen = 0;
+        unsigned long long seen = 0, pseen = 0;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            seen = gen_.load(std::memory_order_relaxed);
+            pseen = prime_;
+        }
         for (;;) {
+            bool job = false;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (unsigned it = 0;; ++it) {
+                if (gen_.load(std::memory_order_acquire) != seen) {
+                    job = true;
+                    break;
+                }
+                if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
+                Relax();
+            }
+            std::shared_ptr<Job> j;
             {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return gen_ != seen; });
-                seen = gen_;
+                if (!job) {
+                    cv_.wait(lk, [&] { return gen_.load(std::memory_order_relaxed) != seen || prime_ != pseen; });
+                    pseen = prime_;
+                    if (gen_.load(std::memory_order_relaxed) == seen) continue;  // (a Prime(): spin)
+                }
+                seen = gen_.load(std::memory_order_relaxed);
                 if (stop_) return;
+                j = cur_;
             }
-            Work();
-            std::lock_guard<std::mutex> lk(m_);
-            if (--busy_ == 0) done_cv_.notify_one();
+            if (j) Run(*j);
         }
     }
 
     std::vector<std::thread> workers_;
     std::mutex submit_, m_;
-    std::condition_variable cv_, done_cv_;
-    const std::function<void(size_t, size_t)>* fn_ = nullptr;
-    size_t n_ = 0, chunk_ = 1;
-    std::atomic<size_t> next_{0};
-    int busy_ = 0;
-    unsigned long long gen_ = 0;
+    std::condition_variable cv_;
+    std::shared_ptr<Job> cur_;
+    std::atomic<unsigned long long> gen_{0};
+    unsigned long long prime_ = 0;
     bool stop_ = false;
+    int spin_us_ = 0;  // ($VX_HOST_SPIN_US: 300 measured slower on the GPU box, whose CPU quota a spinning
+                       // worker eats into)
 };
 
 }  // namespace vxhost
