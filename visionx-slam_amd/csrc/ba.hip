@@ -708,6 +708,7 @@ struct FusedArgs {
     // first); without it the prologue writes slots, which launch 0 combines.
     double* arow;
     int n_kf, apro;
+    int drow;  // rows read by the entries' own threads, no combine phase ($VX_BA_DROW=0: the combine)
 };
 
 // the arow buffer launch `it` reads (combine), accumulates into (pose stage of it + 1) and zeroes
@@ -874,6 +875,17 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
             }
         }
     }
+    // (c') with the rows summed by atomics the entry's own thread (wave 0) reads its row as soon as its
+    // entry record is in and solves without the combine phase or the first barrier: the other waves
+    // meet it at the barrier after the solve (round 5: the combine's LDS round trip and two barriers
+    // off the launch's path)
+    const bool drow = !kPro && f.drow && arow && (it > 0 || f.apro);
+    double Sd[kNTerms];
+    if (drow && tid < kFK && ke.x >= 0) {
+        const double* rp = arow + ((size_t)arow_rd(it) * f.n_kf + (ke.x & 0x3fffffff)) * kStride;
+#pragma unroll
+        for (int t = 0; t < kNTerms; ++t) Sd[t] = rp[t];
+    }
     // (d) this wave's first pose-stage round (round r + 1 is requested when round r is consumed)
     const bool pose_next = kPro || it + 1 < a.max_iter;
     double2 u0 = make_double2(0, 0);
@@ -898,10 +910,10 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         s_kd[tid] = kd;
     }
     FKT(1);
-    __syncthreads();  // s_ke / s_kd
+    if (!drow) __syncthreads();  // s_ke / s_kd
     if (!kPro) {
         // ---- combine: S of entry j, term t = the row's partial slots summed in slot order
-        for (int pr = tid; pr < n_ent * kNTerms; pr += kFT) {
+        for (int pr = tid; !drow && pr < n_ent * kNTerms; pr += kFT) {
             const int j = pr / kNTerms, t = pr - j * kNTerms;
             const int4 e = s_ke[j];
             if (e.x < 0) continue;  // a hole in the entry positions
@@ -957,7 +969,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
             }
         }
     }
-    __syncthreads();
+    if (!drow) __syncthreads();  // (kslot's combined rows, red[])
     FKT(2);
     // ---- pose solve of the entries (local_ba.cpp:163-173); owners publish
     if (ke.x >= 0) {
@@ -971,7 +983,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
         if (!kPro) {
             double S[kNTerms];
 #pragma unroll
-            for (int t = 0; t < kNTerms; ++t) S[t] = sl[t];
+            for (int t = 0; t < kNTerms; ++t) S[t] = drow ? Sd[t] : sl[t];
             solve_pose(a, (int)ts[12], S, T, R);
             if (ke.x & (1 << 30)) {
                 double* Tout = pose_out(a, it) + 8 * (size_t)(ke.x & 0x3fffffff);
@@ -993,15 +1005,17 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
 #pragma unroll
         for (int j = 0; j < 4; ++j) sl[17 + j] = C[j];
     }
-    if (!kPro && b == f.stop_b && tid == 0) {
+    auto stop_from_red = [&] {
         double tot = 0.0, cnt = 0.0;
         for (int w2 = 0; w2 < kFW; ++w2) {
             tot += red[w2];
             cnt += red[kFW + w2];
         }
         stop_rule(a, it, tot, (int)cnt);
-    }
+    };
+    if (!kPro && !drow && b == f.stop_b && tid == 0) stop_from_red();
     __syncthreads();
+    if (drow && b == f.stop_b && tid == 0) stop_from_red();  // (every wave's red[] is in after the barrier)
     FKT(3);
     // ---- landmark stage of iteration it (local_ba.cpp:176-238)
     if (!kPro) {
@@ -1915,6 +1929,11 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
     f.arow = p->f_atomic && p->shard_count <= 1 ? p->f_arow.as<double>() : nullptr;
     f.n_kf = p->n_kf;
     f.apro = p->opt.max_iterations >= 2;
+    static const int drow_env = [] {
+        const char* e = getenv("VX_BA_DROW");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    f.drow = drow_env;
     return f;
 }
 
