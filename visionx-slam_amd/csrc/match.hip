@@ -327,7 +327,7 @@ __global__ __launch_bounds__(kMergeBlock) void k_knn_compact_batch(const unsigne
 }
 
 // k_knn_rows' shape: $VX_MATCH_SHAPE = "<queries>x<threads>" (8x512 default; 4x256, 16x512,
-// 16x1024 for A/B runs) and $VX_MATCH_GRID = workgroups, read once.  The grid is capped at one
+// 16x1024, 8x256, 4x128 for A/B runs) and $VX_MATCH_GRID = workgroups, read once.  The grid is capped at one
 // workgroup per CU by default: the query count is on the device, so an uncapped grid ($VX_MATCH_GRID=0)
 // is sized for the capacity and most of its workgroups only read the count and leave (C3's
 // 2000-of-4254: 6.64 us uncapped, 4.92 us capped, profiles/r05/match_shapes.txt)
@@ -347,7 +347,7 @@ int knn_rows_launch(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, c
         const char* e = getenv("VX_MATCH_SHAPE");
         if (!e) return 0;
         const std::string v(e);
-        return v == "4x256" ? 1 : v == "16x512" ? 2 : v == "16x1024" ? 3 : 0;
+        return v == "4x256" ? 1 : v == "16x512" ? 2 : v == "16x1024" ? 3 : v == "8x256" ? 4 : v == "4x128" ? 5 : 0;
     }();
     static const int grid_env = [] {
         const char* e = getenv("VX_MATCH_GRID");
@@ -359,6 +359,8 @@ int knn_rows_launch(vx_ctx* c, const uint8_t* dq, const int* dnq, int nq_host, c
         case 1: return knn_rows_launch_t<4, 256>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
         case 2: return knn_rows_launch_t<16, 512>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
         case 3: return knn_rows_launch_t<16, 1024>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        case 4: return knn_rows_launch_t<8, 256>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
+        case 5: return knn_rows_launch_t<4, 128>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
         default: return knn_rows_launch_t<kRQ, kRT>(c, dq, dnq, nq_host, dt, dnt, nt_host, q_cap, ratio, best, grid_cap);
     }
 }
