@@ -146,6 +146,7 @@ struct SBAArgs {
     const int* fac_blks;    // k_sba_fac_blk descriptors (vx_sba_plan::fac_blks), fac_nb per component
     int fac_nb;
     int bs_np, bs_nt;       // k_sba_backsub's LDS: the largest component's np doubles, nt + 1 pointers
+    int n_comp;             // covisibility components (k_sba_update clears their factors' touched tiles)
 };
 
 // one launch of the two-column schedule for one component (vx_sba_plan::fac_pairs)
@@ -755,7 +756,7 @@ __device__ __forceinline__ void solve_damp(const SBAArgs& a, int comp, double la
 // depend on x, so a step waits on LDS and two barriers, not on global memory.  Rows with more than 16
 // nonzero tiles take the rest in place.
 constexpr int kBsGroups = kSolveThreads / 16;
-constexpr int kBsDepth = 3;  // steps of operands in flight
+constexpr int kBsDepth = 3;  // steps of operands in flight (default; $VX_SBA_BS_DEPTH=6 for A/B)
 // operands of step k: L_kk^-1 column c (wave 0 only: a wave-uniform branch) and the group's tile of
 // row k (absent: a valid tile, unused); sbp / sbl: the row pointers / tile columns in LDS
 __device__ __forceinline__ void bs_load(const double* L, const double* Linv, int np, int k, const int* sbp,
@@ -787,6 +788,7 @@ __device__ __forceinline__ double bs_dot(const double (&w)[16], const double* x)
 // k loop unrolled by kBsDepth, so each stage keeps its registers): they do not depend on x, so a step
 // waits on LDS and two barriers, not on memory.  Rows of more than 16 tiles take the rest in place.
 // sbp / sbl: LDS for the back lists (nt + 1 pointers, then the tile columns).
+template <int kBsD>
 __device__ __forceinline__ void back_substitute(const double* L, const double* Linv, int np, int nt, const int* tl,
                                                 const int* bptr, double* ys, int* sbp, int* sbl) {
     const int tid = threadIdx.x, grp = tid >> 4, c = tid & 15;
@@ -795,16 +797,16 @@ __device__ __forceinline__ void back_substitute(const double* L, const double* L
     for (int e = tid; e <= nt; e += kSolveThreads) sbp[e] = bptr[e] - b0;
     for (int e = tid; e < nb; e += kSolveThreads) sbl[e] = tl[b0 + e];
     __syncthreads();
-    double li[kBsDepth][16], tv[kBsDepth][16];
-    int tm[kBsDepth];
+    double li[kBsD][16], tv[kBsD][16];
+    int tm[kBsD];
 #pragma unroll
-    for (int s = 0; s < kBsDepth; ++s) {
+    for (int s = 0; s < kBsD; ++s) {
         tm[s] = -1;
         if (nt - 1 - s >= 0) bs_load(L, Linv, np, nt - 1 - s, sbp, sbl, li[s], tv[s], tm[s]);
     }
-    for (int k0 = nt - 1; k0 >= 0; k0 -= kBsDepth) {
+    for (int k0 = nt - 1; k0 >= 0; k0 -= kBsD) {
 #pragma unroll
-        for (int s = 0; s < kBsDepth; ++s) {
+        for (int s = 0; s < kBsD; ++s) {
             const int k = k0 - s;
             if (k < 0) break;
             if (grp == 0) {  // x_k = L_kk^-T y_k (lane c: column c of L_kk^-1)
@@ -826,7 +828,7 @@ __device__ __forceinline__ void back_substitute(const double* L, const double* L
                 for (int r = 0; r < 16; ++r) w[r] = Lkm[(long long)r * np + c];
                 ys[16 * mm + c] -= bs_dot(w, xk);
             }
-            if (k - kBsDepth >= 0) bs_load(L, Linv, np, k - kBsDepth, sbp, sbl, li[s], tv[s], tm[s]);
+            if (k - kBsD >= 0) bs_load(L, Linv, np, k - kBsD, sbp, sbl, li[s], tv[s], tm[s]);
             __syncthreads();
         }
     }
@@ -1482,6 +1484,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     if (wv == 0 && lane == 0 && !ok) atomicOr(&a.st->fail[it], 1);
 }
 
+template <int kBsD>
 __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     if (!a.st->lm[(it + 1) & 1].do_solve) return;
@@ -1497,19 +1500,33 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it
     const int* bptr = tl + hdr[kHdrBack];
     VX_KT(8);
     int* sbp = reinterpret_cast<int*>(ys + a.bs_np);
-    back_substitute(L, Linv, np, nt, tl, bptr, ys, sbp, sbp + a.bs_nt + 1);
+    back_substitute<kBsD>(L, Linv, np, nt, tl, bptr, ys, sbp, sbp + a.bs_nt + 1);
     VX_KT(9);
     for (int c = tid; c < nc; c += kSolveThreads) a.dx[6 * a.comp_kf[kq0 + c / 6] + c % 6] = ys[c];
-    const int* cp = tl + hdr[kHdrCopy];
-    const int ncp = hdr[kHdrNCopy];
-    const d4 z = {0.0, 0.0, 0.0, 0.0};
-    for (int t = wv; t < ncp; t += kSolveWaves)
-        store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
+    (void)wv;
+    // (the clearing of the touched tiles: k_sba_update, over all its workgroups)
 }
 
 // ------------------------------------------------------------------------- k_sba_update
 __global__ __launch_bounds__(kUpdThreads) void k_sba_update(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
+    // every component's factor tiles back to zero for the next assembly (k_sba_blocks writes only
+    // the nonzero blocks): the copy lists spread over the launch's waves — in k_sba_backsub's one
+    // workgroup per component these were ~2 MB of stores from one CU.  Unconditional: after an
+    // iteration without a factorisation the tiles hold the assembled blocks, which the next assembly
+    // rewrites anyway.
+    {
+        const int gw = (blockIdx.x * kUpdThreads + threadIdx.x) >> 6, nw = gridDim.x * (kUpdThreads / 64);
+        const d4 z = {0.0, 0.0, 0.0, 0.0};
+        for (int comp = 0; comp < a.n_comp; ++comp) {
+            const int* hdr = a.comp_hdr + kHdrN * comp;
+            const int np = 16 * hdr[kHdrNt], ncp = hdr[kHdrNCopy];
+            const int* cp = a.tl + hdr[kHdrCopy];
+            double* L = a.L + a.comp_loff[comp];
+            for (int t = gw; t < ncp; t += nw)
+                store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
+        }
+    }
     const LMVars v = a.st->lm[(it + 1) & 1];
     if (!v.do_solve) return;
     const int t = blockIdx.x * kUpdThreads + threadIdx.x;
@@ -1630,6 +1647,7 @@ SBAArgs make_args(vx_sba_plan* p) {
     a.comp_loff = p->comp_loff.as<long long>();
     a.comp_np = p->comp_np.as<int>();
     a.comp_hdr = p->comp_hdr.as<int>();
+    a.n_comp = p->n_comp;
     a.tl = p->tl.as<int>();
     a.wy = p->wy.as<double>();
     a.lm_sys = p->lm_sys.as<double>();
@@ -2412,7 +2430,7 @@ int factor_groups(int max_trail_rest) {
 struct SbaRunCfg {
     SBAArgs a;
     size_t lds = 0, bs_lds = 0, la_lds = 0, red_n = 0, blk_lds = 0;
-    int upd_blocks = 1, G = 1, la_ps = 0, Gb = 1;
+    int upd_blocks = 1, G = 1, la_ps = 0, Gb = 1, bs_depth = 3;
     bool multi = false, pair = false, blk = false;
 };
 
@@ -2427,9 +2445,13 @@ int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
     // the factorisation: one launch per tile step over G workgroups per component (components of
     // more than 32 tile columns), or the whole factor in one workgroup per component (the round-3 form)
     r.bs_lds = (size_t)p->max_np * sizeof(double) + ((size_t)a.bs_nt + 1 + p->max_back) * sizeof(int);
-    if (r.bs_lds > 64 * 1024)
-        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub),
+    r.bs_depth = std::getenv("VX_SBA_BS_DEPTH") && std::atoi(std::getenv("VX_SBA_BS_DEPTH")) == 6 ? 6 : kBsDepth;
+    if (r.bs_lds > 64 * 1024) {
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub<kBsDepth>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.bs_lds));
+        VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub<6>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.bs_lds));
+    }
     r.multi = factor_multi(p->max_nt);
     r.G = factor_groups(p->max_trail_rest);
     // one tile column per launch (default) or two ($VX_SBA_FACTOR_COLS=2: half the launches, but
@@ -2522,7 +2544,7 @@ int sba_solve_step(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
         VX_HIP(c, launch(c, kStSbaSolve, k_sba_solve, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
                          (uint32_t)r.lds, c->stream, a, it));
     }
-    VX_HIP(c, launch(c, kStSbaSolve, k_sba_backsub, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
+    VX_HIP(c, launch(c, kStSbaSolve, r.bs_depth == 6 ? k_sba_backsub<6> : k_sba_backsub<kBsDepth>, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads),
                      (uint32_t)r.bs_lds, c->stream, a, it));
     VX_HIP(c, launch(c, kStSbaUpdate, k_sba_update, dim3(std::max(r.upd_blocks, 1)), dim3(kUpdThreads), 0,
                      c->stream, a, it));
