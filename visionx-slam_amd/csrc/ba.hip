@@ -827,14 +827,19 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     }
     // (b) the landmark it owns (its position goes to LDS for the observations of the landmark):
     // fused-order copy at a fixed address (the prologue reads the slot's initial position)
-    const int lslot = f.lm_slot[base + tid];
+    // (iterations of the 512-thread layout: only the workgroup's B.x landmark threads load — the
+    // padding rows of the other ~70 % were ~1.8 MB per launch of HBM traffic; the loads wait for B,
+    // which the solving wave's row loads outlast anyway.  The prologue keeps them unconditional: its
+    // first barrier waits for them.)
+    const bool lm_load = kPro || !kEcopy || tid < B.x;
+    const int lslot = lm_load ? f.lm_slot[base + tid] : 0;
     int2 run = make_int2(0, 0);
-    if (!kPro) run = f.lm_run[base + tid];
-    D3 PL;
+    if (!kPro && lm_load) run = f.lm_run[base + tid];
+    D3 PL{0.0, 0.0, 0.0};
     if (kPro || !kEcopy) {
         const double* P = kPro ? a.lm_pos0 + 4 * (size_t)lslot : lm_in(a, it, lslot);
         PL = {P[0], P[1], P[2]};
-    } else {
+    } else if (lm_load) {
         const double* P = reinterpret_cast<const double*>(f.lpos + base + tid);
         PL = {P[0], P[1], P[2]};
     }
@@ -1129,8 +1134,26 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
             const double2 uv = u0;
             const double4 P4 = p0;
             if (r + 1 < wrounds) {
-                u0 = f.pobs_uv[wstart + 64 * (r + 1) + lane];
-                p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
+                // only the lanes of the next round that hold an observation load (the entries'
+                // 64-aligned padding stays in memory): the next round is this entry's or the first
+                // of the wave's next entry with rounds
+                int lim = e.w - (e.z + 64 * (q + 1));
+                if (q + 1 >= nr) {
+                    int jn = j + kFW;
+                    int4 en = s_ke[jn < kFK ? jn : j];
+                    while (jn < n_ent && ((en.w - en.z + 63) >> 6) == 0) {
+                        jn += kFW;
+                        en = s_ke[jn < kFK ? jn : j];
+                    }
+                    lim = en.w - en.z;
+                }
+                if (lane < lim) {
+                    u0 = f.pobs_uv[wstart + 64 * (r + 1) + lane];
+                    p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
+                } else {
+                    u0 = make_double2(0.0, 0.0);
+                    p0 = make_double4(0.0, 0.0, 0.0, 0.0);
+                }
             }
             const bool valid = e.z + 64 * q + lane < e.w;
             if (kFT <= kFTSmall || valid) {  // (256 / 512: padding lanes run too, weight 0 — no branch)
