@@ -1511,11 +1511,11 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_backsub(SBAArgs a, int it
 __global__ __launch_bounds__(kUpdThreads) void k_sba_update(SBAArgs a, int it) {
     if (it > 0 && !a.st->active[it]) return;
     // every component's factor tiles back to zero for the next assembly (k_sba_blocks writes only
-    // the nonzero blocks): the copy lists spread over the launch's waves — in k_sba_backsub's one
-    // workgroup per component these were ~2 MB of stores from one CU.  Unconditional: after an
-    // iteration without a factorisation the tiles hold the assembled blocks, which the next assembly
-    // rewrites anyway.
-    {
+    // the nonzero blocks) when this iteration factored: the copy lists spread over the launch's waves
+    // — in k_sba_backsub's one workgroup per component these were ~2 MB of stores from one CU.  (A
+    // failed factor counts: workgroup 0 below clears do_solve then, so the others go by the flag.)
+    const LMVars v0 = a.st->lm[(it + 1) & 1];
+    if (v0.do_solve || a.st->fail[it]) {
         const int gw = (blockIdx.x * kUpdThreads + threadIdx.x) >> 6, nw = gridDim.x * (kUpdThreads / 64);
         const d4 z = {0.0, 0.0, 0.0, 0.0};
         for (int comp = 0; comp < a.n_comp; ++comp) {
@@ -1527,7 +1527,7 @@ __global__ __launch_bounds__(kUpdThreads) void k_sba_update(SBAArgs a, int it) {
                 store_acc(L + (long long)(16 * (cp[t] >> 16)) * np + 16 * (cp[t] & 0xffff), np, z);
         }
     }
-    const LMVars v = a.st->lm[(it + 1) & 1];
+    const LMVars v = v0;
     if (!v.do_solve) return;
     const int t = blockIdx.x * kUpdThreads + threadIdx.x;
     if (a.st->fail[it]) {  // a component's Cholesky failed: discard the step, damp harder
