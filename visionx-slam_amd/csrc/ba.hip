@@ -709,6 +709,7 @@ struct FusedArgs {
     double* arow;
     int n_kf, apro;
     int drow;  // rows read by the entries' own threads, no combine phase ($VX_BA_DROW=0: the combine)
+    int padskip;  // no loads for padding rows / lanes ($VX_BA_PADSKIP=0: every row and lane loads)
 };
 
 // the arow buffer launch `it` reads (combine), accumulates into (pose stage of it + 1) and zeroes
@@ -831,7 +832,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // padding rows of the other ~70 % were ~1.8 MB per launch of HBM traffic; the loads wait for B,
     // which the solving wave's row loads outlast anyway.  The prologue keeps them unconditional: its
     // first barrier waits for them.)
-    const bool lm_load = kPro || !kEcopy || tid < B.x;
+    const bool lm_load = kPro || !kEcopy || !f.padskip || tid < B.x;
     const int lslot = lm_load ? f.lm_slot[base + tid] : 0;
     int2 run = make_int2(0, 0);
     if (!kPro && lm_load) run = f.lm_run[base + tid];
@@ -1137,8 +1138,8 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 // only the lanes of the next round that hold an observation load (the entries'
                 // 64-aligned padding stays in memory): the next round is this entry's or the first
                 // of the wave's next entry with rounds
-                int lim = e.w - (e.z + 64 * (q + 1));
-                if (q + 1 >= nr) {
+                int lim = f.padskip ? e.w - (e.z + 64 * (q + 1)) : 64;
+                if (f.padskip && q + 1 >= nr) {
                     int jn = j + kFW;
                     int4 en = s_ke[jn < kFK ? jn : j];
                     while (jn < n_ent && ((en.w - en.z + 63) >> 6) == 0) {
@@ -1957,6 +1958,11 @@ FusedArgs make_fused_args(vx_ba_plan* p) {
         return e && e[0] == '0' ? 0 : 1;
     }();
     f.drow = drow_env;
+    static const int padskip_env = [] {
+        const char* e = getenv("VX_BA_PADSKIP");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    f.padskip = padskip_env;
     return f;
 }
 
