@@ -166,7 +166,7 @@ struct FacStep {
 // trailing tiles block t - 1's steps update beyond block t (entries i << 16 | j << 4 | step mask)
 struct FacBlk {
     long long loff;
-    int K0, W, bt_beg, bt_end, pb_beg, pb_end, K0p, Wp, tr_beg, tr_end, nt;
+    int K0, W, bt_beg, bt_end, pb_beg, pb_end, K0p, Wp, tr_beg, tr_end, nt, la_beg, la_end;
 };
 
 // ------------------------------------------------------------------------- state selection
@@ -1254,39 +1254,73 @@ __device__ __forceinline__ d4 load_acc_opo(const double* S) {
     return v;
 }
 
-// trailing tiles of launch t: entries i << 16 | j << 4 | mask, steps k0 + s for the mask's bits s in
-// ascending order; entries beg, beg + stride, ...; four per wave in flight
-__device__ __forceinline__ void blk_trail(double* L, int np, const int* tl, int k0, int beg, int end, int stride,
-                                          int waves) {
-    const int wv = threadIdx.x >> 6;
+// Tiles of launch t: entries i << 16 | j << 4 | mask, steps k0 + s for the mask's bits s in ascending
+// order (entries beg, beg + stride, ...), two tiles per wave at a time with every operand of their
+// steps requested together (one memory round trip per pair of tiles, not one per step)
+__device__ __forceinline__ void blk_tiles_pf(double* L, int np, const int* tl, int k0, int beg, int end, int stride,
+                                             int waves) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, r0 = lane >> 4, cl = lane & 15;
     const int cnt = end > beg ? (end - beg + stride - 1) / stride : 0;
-    for (int m0 = wv * 4; m0 < cnt; m0 += waves * 4) {
-        d4 c[4];
-        int ti[4], tj[4], mk[4];
+    for (int m0 = wv * 2; m0 < cnt; m0 += waves * 2) {
+        d4 c[2];
+        int ti[2], tj[2], mk[2];
+        double4 A[2][kFbW], B[2][kFbW];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            ti[q] = -1;
+        for (int q = 0; q < 2; ++q) {
+            mk[q] = 0;
+            ti[q] = tj[q] = 0;
             if (m0 + q < cnt) {
                 const int e = tl[beg + (m0 + q) * stride];
                 ti[q] = e >> 16;
                 tj[q] = (e >> 4) & 0xfff;
                 mk[q] = e & 15;
                 c[q] = load_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np);
+#pragma unroll
+                for (int s = 0; s < kFbW; ++s)
+                    if ((mk[q] >> s) & 1) {
+                        A[q][s] = *reinterpret_cast<const double4*>(L + (long long)(16 * ti[q] + cl) * np + 16 * (k0 + s) + 4 * r0);
+                        B[q][s] = *reinterpret_cast<const double4*>(L + (long long)(16 * tj[q] + cl) * np + 16 * (k0 + s) + 4 * r0);
+                    }
             }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (ti[q] < 0) continue;
+        for (int q = 0; q < 2; ++q) {
+            if (m0 + q >= cnt) continue;
+#pragma unroll
             for (int s = 0; s < kFbW; ++s)
-                if ((mk[q] >> s) & 1)
-                    c[q] = mfma_abt_g(L + (long long)(16 * ti[q]) * np + 16 * (k0 + s),
-                                      L + (long long)(16 * tj[q]) * np + 16 * (k0 + s), np, c[q]);
+                if ((mk[q] >> s) & 1) {  // (the order of mfma_abt_g)
+                    c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-A[q][s].x, B[q][s].x, c[q], 0, 0, 0);
+                    c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-A[q][s].y, B[q][s].y, c[q], 0, 0, 0);
+                    c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-A[q][s].z, B[q][s].z, c[q], 0, 0, 0);
+                    c[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(-A[q][s].w, B[q][s].w, c[q], 0, 0, 0);
+                }
             store_acc(L + (long long)(16 * ti[q]) * np + 16 * tj[q], np, c[q]);
         }
     }
 }
 
-__global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, int t, int G, int cap, FacBlk sd) {
+// The look-ahead as a launch of its own (before k_sba_fac_blk's launch t >= 1, $VX_SBA_FACTOR_LA
+// default): block t - 1's steps applied to block t's tiles by G workgroups, so workgroup 0 of the
+// factor launch loads block t finished instead of running ~2 MFLOP of updates on its one CU.
+__global__ __launch_bounds__(kFbThreads) void k_sba_fac_upd(SBAArgs a, int it, int t, int G, FacBlk sd) {
+    const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
+    if (sd.nt == 0) {
+        const int* d = a.fac_blks + 16 * ((size_t)comp * a.fac_nb + t);
+        const int4 d0 = *reinterpret_cast<const int4*>(d), d2 = *reinterpret_cast<const int4*>(d + 8),
+                   d3 = *reinterpret_cast<const int4*>(d + 12);
+        sd.loff = (long long)(((unsigned long long)(unsigned)d0.y << 32) | (unsigned)d0.x);
+        sd.K0p = d2.x;
+        sd.nt = d3.x;
+        sd.la_beg = d3.y;
+        sd.la_end = d3.z;
+    }
+    if (it > 0 && !a.st->active[it]) return;
+    if (sd.nt == 0 || t == 0) return;
+    if (!a.st->lm[(it + 1) & 1].do_solve) return;  // (launch 0's decision)
+    blk_tiles_pf(a.L + sd.loff, 16 * sd.nt, a.tl, sd.K0p, sd.la_beg + g, sd.la_end, G, kFbWaves);
+}
+
+__global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, int t, int G, int cap, int split, FacBlk sd) {
     const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
     if (sd.nt == 0) {
         const int* d = a.fac_blks + 16 * ((size_t)comp * a.fac_nb + t);
@@ -1304,6 +1338,8 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         sd.tr_beg = d2.z;
         sd.tr_end = d2.w;
         sd.nt = d3.x;
+        sd.la_beg = d3.y;
+        sd.la_end = d3.z;
     }
     if (it > 0 && !a.st->active[it]) return;
     const int nt = sd.nt, np = 16 * nt;
@@ -1329,7 +1365,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         if (kt) VX_KT(10);
         if (g > 0 || G == 1) {
             const int gg = G == 1 ? 0 : g - 1, GG = G == 1 ? 1 : G - 1;
-            blk_trail(L, np, tl, sd.K0p, sd.tr_beg + gg, sd.tr_end, GG, kFbWaves);
+            blk_tiles_pf(L, np, tl, sd.K0p, sd.tr_beg + gg, sd.tr_end, GG, kFbWaves);
             if (kt && g > 0) VX_KT(7);
             if (g > 0) return;
         }
@@ -1353,7 +1389,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
         ent[s] = e;
         rs[((e & 0xffff) - K0) * n1 + (e >> 16)] = s;
     }
-    for (int s = tid; t > 0 && s < sd.pb_end - sd.pb_beg; s += kFbThreads) {
+    for (int s = tid; t > 0 && !split && s < sd.pb_end - sd.pb_beg; s += kFbThreads) {
         const int e = tl[sd.pb_beg + s];
         pz[((e & 0xffff) - sd.K0p) * n1 + (e >> 16)] = 1;
     }
@@ -1364,7 +1400,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     // the rhs row i = nt is in every column's list).  Row by row: the block's B operands
     // L(K0 + cc, K0p + q) are staged in LDS once, and per row a wave issues its A operands
     // L(i, K0p + q) and its tiles together — one memory round trip per row, not one per step and tile.
-    if (t == 0) {
+    if (t == 0 || split) {  // (split: k_sba_fac_upd applied block t - 1's steps in a launch of its own)
         for (int m = wv; m < n; m += kFbWaves) {
             const int e = ent[m];
             store_acc_opo(T + (size_t)m * kPanelStride, load_acc(L + (long long)(16 * (e >> 16)) * np + 16 * (e & 0xffff), np));
@@ -2071,7 +2107,7 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
     p->max_panel = 1;
     p->max_nt = p->max_trail_rest = 0;
     p->max_pairs = 0;
-    p->max_blks = p->max_blk_trail = 0;
+    p->max_blks = p->max_blk_trail = p->max_blk_la = 0;
     p->blk_ok = p->n_comp > 0;
     p->max_back = 0;
     std::vector<std::vector<int>> pair_desc(std::max(p->n_comp, 1)), blk_desc(std::max(p->n_comp, 1));
@@ -2259,6 +2295,18 @@ int sba_plan_finish(vx_ctx* c, vx_sba_plan* p, const std::vector<int>& flags, co
                             }
                         d[11] = (int)tlist.size();
                         p->max_blk_trail = std::max(p->max_blk_trail, d[11] - d[10]);
+                        // block t's own tiles with block t - 1's steps (the look-ahead when it runs as
+                        // a launch of its own, k_sba_fac_upd)
+                        d[13] = (int)tlist.size();
+                        for (int x = bb[b]; x < be[b]; ++x) {
+                            const int i = tlist[x] >> 16, j = tlist[x] & 0xffff;
+                            int mk = 0;
+                            for (int sx = 0; sx < wp; ++sx)
+                                if ((i == nt || NZ(i, k0 + sx)) && NZ(j, k0 + sx)) mk |= 1 << sx;
+                            if (mk) tlist.push_back(i << 16 | j << 4 | mk);
+                        }
+                        d[14] = (int)tlist.size();
+                        p->max_blk_la = std::max(p->max_blk_la, d[14] - d[13]);
                     }
                     bd.insert(bd.end(), d, d + 16);
                 }
@@ -2430,7 +2478,8 @@ int factor_groups(int max_trail_rest) {
 struct SbaRunCfg {
     SBAArgs a;
     size_t lds = 0, bs_lds = 0, la_lds = 0, red_n = 0, blk_lds = 0;
-    int upd_blocks = 1, G = 1, la_ps = 0, Gb = 1, bs_depth = 3;
+    int upd_blocks = 1, G = 1, la_ps = 0, Gb = 1, bs_depth = 3, Gu = 1;
+    int blk_split = 1;  // k_sba_fac_upd before each block launch ($VX_SBA_FACTOR_LA=wg0: workgroup 0's look-ahead)
     bool multi = false, pair = false, blk = false;
 };
 
@@ -2477,6 +2526,9 @@ int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
         r.Gb = 1 + (p->max_blk_trail + 31) / 32;
         if (const char* e = std::getenv("VX_SBA_FACTOR_GROUPS")) r.Gb = std::atoi(e);
         r.Gb = std::max(1, std::min(r.Gb, 128));
+        const char* la = std::getenv("VX_SBA_FACTOR_LA");
+        r.blk_split = la && std::strcmp(la, "wg0") == 0 ? 0 : 1;
+        r.Gu = std::max(1, std::min(256, (p->max_blk_la + 15) / 16));  // (two tiles per wave)
     }
     r.red_n = (size_t)p->l_total + (size_t)p->nk * 14;
     return VX_OK;
@@ -2507,9 +2559,13 @@ int sba_solve_step(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
                 sd.loff = (long long)(((unsigned long long)(unsigned)d[1] << 32) | (unsigned)d[0]);
                 sd.K0 = d[2], sd.W = d[3], sd.bt_beg = d[4], sd.bt_end = d[5], sd.pb_beg = d[6], sd.pb_end = d[7];
                 sd.K0p = d[8], sd.Wp = d[9], sd.tr_beg = d[10], sd.tr_end = d[11], sd.nt = d[12];
+                sd.la_beg = d[13], sd.la_end = d[14];
             }
+            if (r.blk_split && t > 0)
+                VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_upd, dim3(std::max(p->n_comp, 1) * r.Gu), dim3(kFbThreads), 0,
+                                 c->stream, a, it, t, r.Gu, sd));
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_blk, dim3(std::max(p->n_comp, 1) * r.Gb), dim3(kFbThreads),
-                             (uint32_t)r.blk_lds, c->stream, a, it, t, r.Gb, kFbCap, sd));
+                             (uint32_t)r.blk_lds, c->stream, a, it, t, r.Gb, kFbCap, r.blk_split, sd));
         }
     } else if (r.multi) {
         VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,

@@ -49,7 +49,7 @@ struct vx_sba_plan {
     // max_blk_trail: most trailing tiles of one launch
     std::vector<int> fac_blks_h;
     vx::DevBuf fac_blks;
-    int max_blks = 0, max_blk_trail = 0;
+    int max_blks = 0, max_blk_trail = 0, max_blk_la = 0;  // (max_blk_la: most look-ahead tiles of one launch)
     bool blk_ok = false;
     int max_back = 0;  // most back-substitution tiles of one component (k_sba_backsub stages the lists in LDS)
     int diag_split = 1;  // k_sba_blocks workgroups per diagonal block (sba_plan_finish)
