@@ -614,10 +614,13 @@ __device__ __forceinline__ bool potrf_inv16_t(Rd rd, double* lds_inv, double* Lg
 }
 // The same factor + inverse with four lanes per row (lane 4 i + q: row i, columns 4 q .. 4 q + 3):
 // per column j the pivot comes by v_readlane, L_ij = a_ij / L_jj is formed on the quad lane that holds
-// column j and spread over its quad by a quad_perm DPP move, and each lane takes the L_cj of its own
-// four columns from lanes 4 c by ds_bpermute — four FMAs per lane per column instead of fifteen, and
-// four permutes instead of fifteen scalar broadcasts.  Every element sees the same operations in the
-// same order as potrf_inv16_t: bitwise the same L^-1.
+// column j and spread over its quad by a quad_perm DPP move, and each lane forms the L_cj of its own
+// four columns from row j's copies a_jc (ds_bpermute from lane 4 j + q, issued before the pivot's
+// square root) — four FMAs per lane per column instead of fifteen, and four permutes instead of
+// fifteen scalar broadcasts.  The whole symmetric tile is held and every update is symmetric
+// (fma(-L_ik, L_ck, a_ic) and fma(-L_ck, L_ik, a_ci) round the same product), so a_jc == a_cj
+// bitwise and every element sees the same operations in the same order as potrf_inv16_t: bitwise
+// the same L^-1.
 template <int J>
 __device__ __forceinline__ double quad_bcast(double v) {
     constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);  // quad_perm [J, J, J, J]
@@ -640,13 +643,18 @@ __device__ __forceinline__ bool potrf_inv16_quad(Rd rd, double* lds_inv, double*
         constexpr int j = decltype(jc)::value, jq = j >> 2, jm = j & 3;
         const double d = rl(a[jm], 4 * j + jq);
         ok = ok && d > 0.0 && d < 1e300;
+        // row j's entries a_jc (c > j), taken before the pivot is known: the permute overlaps the
+        // reciprocal square root's chain instead of following it
+        double aj[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) aj[m] = __shfl(a[m], 4 * j + q, 64);
         const double r = frsq(d > 0.0 ? d : 1.0);  // (uniform: 1 / L_jj)
         const double l = quad_bcast<jq>(a[jm] * r);  // L[i][j] for i >= j
         if (q == jq) x[jm] *= r;
         const double xj = quad_bcast<jq>(x[jm]);
         double lc[4];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) lc[m] = __shfl(l, 4 * (4 * q + m), 64);  // L[c][j] from quad c
+        for (int m = 0; m < 4; ++m) lc[m] = aj[m] * r;  // L[c][j] = a_jc / L_jj (a_jc == a_cj bitwise, below)
 #pragma unroll
         for (int m = 0; m < 4; ++m)
             if (4 * q + m > j) {
@@ -1467,21 +1475,30 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     }
     __syncthreads();
     if (kt) VX_KT(12);
+    // Per column c: the panel (all waves), a barrier, step c on the block's later columns (waves 1..),
+    // a barrier.  The next column's POTRF + inverse runs on wave 0 beside step c's updates: its
+    // diagonal tile's last step is the product of the panel tile L_(c+1)c with itself, which wave 0
+    // forms first in the panel phase and applies at once — so the column chain is panel + max(POTRF,
+    // updates), not POTRF + panel + updates.  (Two L_cc^-1 buffers alternate: dlds and the staging
+    // area Bst, free after the look-ahead.  Every tile sees the same operations in the same order.)
     bool ok = true;
+    double* dl[2] = {dlds, Bst};
+    if (wv == 0) {
+        const double* D = T + (size_t)cb[0] * kPanelStride;
+        ok = potrf_inv16_quad([&](int r, int q) { return D[opo(r, q)]; }, dl[0], Linv + 256 * K0);
+    }
+    __syncthreads();
+    if (kt) VX_KT(13);
     for (int cc = 0; cc < W; ++cc) {
         const int c = K0 + cc, s0 = cb[cc], s1 = cb[cc + 1];
-        if (wv == 0) {
-            const double* D = T + (size_t)s0 * kPanelStride;
-            ok = potrf_inv16_quad([&](int r, int q) { return D[opo(r, q)]; }, dlds, Linv + 256 * c) && ok;
-        }
-        __syncthreads();
-        if (kt && cc == 0) VX_KT(13);
+        const double* dc = dl[cc & 1];
+        const int sn = cc + 1 < W ? rs[cc * n1 + c + 1] : -1;  // slot of L_(c+1)c (wave 0's)
         // the panel L_ic = A_ic L_cc^-T (rows below the diagonal, the rhs row last): in place and to
         // the factor
-        for (int s = s0 + 1 + wv; s < s1; s += kFbWaves) {
+        auto panel = [&](int s) {
             double* S = T + (size_t)s * kPanelStride;
             const double4 av = *reinterpret_cast<const double4*>(S + 4 * lane);
-            const double4 bv = *reinterpret_cast<const double4*>(dlds + 4 * lane);
+            const double4 bv = *reinterpret_cast<const double4*>(dc + 4 * lane);
             d4 r = {0.0, 0.0, 0.0, 0.0};
             r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.x, bv.x, r, 0, 0, 0);
             r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.y, bv.y, r, 0, 0, 0);
@@ -1489,30 +1506,45 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
             r = __builtin_amdgcn_mfma_f64_16x16x4f64(av.w, bv.w, r, 0, 0, 0);
             store_acc_opo(S, r);
             store_acc(L + (long long)(16 * (ent[s] >> 16)) * np + 16 * c, np, r);
+        };
+        if (wv == 0 && sn >= 0) {
+            panel(sn);
+            double* Dt = T + (size_t)cb[cc + 1] * kPanelStride;  // step c on the diagonal tile of c + 1
+            d4 acc = load_acc_opo(Dt);
+            acc = mfma_abt(T + (size_t)sn * kPanelStride, T + (size_t)sn * kPanelStride, acc, true);
+            store_acc_opo(Dt, acc);
         }
+        for (int s = s0 + 1 + wv; s < s1; s += kFbWaves)
+            if (s != sn) panel(s);
         __syncthreads();
         if (cc + 1 == W) break;
-        // step c on the block's later columns c2: tiles (i, c2), i >= c2, for NZ(c2, c) — rows of
-        // column c from the slot of (c2, c) on
-        int tot = 0;
-        for (int c2 = c + 1; c2 < K0 + W; ++c2) {
-            const int sc = rs[cc * n1 + c2];
-            tot += sc >= 0 ? s1 - sc : 0;
-        }
-        for (int p = wv; p < tot; p += kFbWaves) {
-            int q = p, c2 = c + 1, sc = -1;
-            for (; c2 < K0 + W; ++c2) {
-                sc = rs[cc * n1 + c2];
-                const int len = sc >= 0 ? s1 - sc : 0;
-                if (q < len) break;
-                q -= len;
+        if (wv == 0) {
+            const double* D = T + (size_t)cb[cc + 1] * kPanelStride;
+            ok = potrf_inv16_quad([&](int r, int q) { return D[opo(r, q)]; }, dl[(cc + 1) & 1], Linv + 256 * (c + 1)) && ok;
+        } else {
+            // step c on the block's later columns c2: tiles (i, c2), i >= c2, for NZ(c2, c) — rows of
+            // column c from the slot of (c2, c) on (the diagonal tile of c + 1: wave 0's, above)
+            int tot = 0;
+            for (int c2 = c + 1; c2 < K0 + W; ++c2) {
+                const int sc = rs[cc * n1 + c2];
+                tot += sc >= 0 ? s1 - sc : 0;
             }
-            const int s = sc + q;  // L_ic, with L_c2c at sc
-            const int dst = rs[(c2 - K0) * n1 + (ent[s] >> 16)];
-            double* Dt = T + (size_t)dst * kPanelStride;
-            d4 acc = load_acc_opo(Dt);
-            acc = mfma_abt(T + (size_t)s * kPanelStride, T + (size_t)sc * kPanelStride, acc, true);
-            store_acc_opo(Dt, acc);
+            for (int p = wv - 1; p < tot; p += kFbWaves - 1) {
+                int q = p, c2 = c + 1, sc = -1;
+                for (; c2 < K0 + W; ++c2) {
+                    sc = rs[cc * n1 + c2];
+                    const int len = sc >= 0 ? s1 - sc : 0;
+                    if (q < len) break;
+                    q -= len;
+                }
+                if (c2 == c + 1 && q == 0) continue;
+                const int s = sc + q;  // L_ic, with L_c2c at sc
+                const int dst = rs[(c2 - K0) * n1 + (ent[s] >> 16)];
+                double* Dt = T + (size_t)dst * kPanelStride;
+                d4 acc = load_acc_opo(Dt);
+                acc = mfma_abt(T + (size_t)s * kPanelStride, T + (size_t)sc * kPanelStride, acc, true);
+                store_acc_opo(Dt, acc);
+            }
         }
         __syncthreads();
     }
