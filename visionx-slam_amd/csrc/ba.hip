@@ -772,6 +772,8 @@ __device__ __forceinline__ void pose_obs_terms(const double* C, double xx, doubl
         if (!kPro && it == 1) VX_KT(slot);     \
     } while (0)
 
+typedef int si4 __attribute__((ext_vector_type(4)));  // (an SGPR quad for the scalar loads below)
+
 template <bool kPro, int kFT, bool kCmp = false>
 __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) {
     constexpr int kFW = kFT / 64;  // waves per workgroup
@@ -815,36 +817,20 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     double* part_out = f.part + (size_t)((it + 1) & 1) * f.n_part * kStride;
     FKT(0);
     // ---- every load the launch needs, issued up front (at most two dependent levels); values
-    // needed only after the first barrier are parked in LDS, not held in registers
-    const int4 B = f.blk[(size_t)b * (1 + kFW / 2)];
-    const int4 WB = f.blk[(size_t)b * (1 + kFW / 2) + 1 + (wv >> 1)];
-    const int wstart = (wv & 1) ? WB.z : WB.x, wrounds = (wv & 1) ? WB.w : WB.y;
-    // (a) this thread's landmark-stage observation (padding rows are valid memory)
-    int4 orec = make_int4(0, 0, 0, 0);
-    double2 ouv = make_double2(1e300, 1e300);
-    if (!kPro) {
-        orec = f.lobs_rec[base + tid];
-        ouv = f.lobs_uv[base + tid];
-    }
-    // (b) the landmark it owns (its position goes to LDS for the observations of the landmark):
-    // fused-order copy at a fixed address (the prologue reads the slot's initial position)
-    // (iterations of the 512-thread layout: only the workgroup's B.x landmark threads load — the
-    // padding rows of the other ~70 % were ~1.8 MB per launch of HBM traffic; the loads wait for B,
-    // which the solving wave's row loads outlast anyway.  The prologue keeps them unconditional: its
-    // first barrier waits for them.)
-    const bool lm_load = kPro || !kEcopy || !f.padskip || tid < B.x;
-    const int lslot = lm_load ? f.lm_slot[base + tid] : 0;
-    int2 run = make_int2(0, 0);
-    if (!kPro && lm_load) run = f.lm_run[base + tid];
-    D3 PL{0.0, 0.0, 0.0};
-    if (kPro || !kEcopy) {
-        const double* P = kPro ? a.lm_pos0 + 4 * (size_t)lslot : lm_in(a, it, lslot);
-        PL = {P[0], P[1], P[2]};
-    } else if (lm_load) {
-        const double* P = reinterpret_cast<const double*>(f.lpos + base + tid);
-        PL = {P[0], P[1], P[2]};
-    }
-    // (c) the keyframe entry it solves: previous pose, intrinsics, flags -> tslot (the prologue
+    // needed only after the first barrier are parked in LDS, not held in registers.  Issue order
+    // matters: `s_waitcnt vmcnt` retires loads in issue order, so a value is waited for together with
+    // every load issued before it.  Wave 0's chain is the block record and its entry records, then
+    // the rows those name (drow), then the solve: the entry records and copies go right behind the
+    // block record, ahead of the landmark loads, and none of their values is used (no wait) before
+    // every independent load is in flight.
+    // (the block records by scalar loads — plan data no kernel writes — so that waiting for them
+    // (lgkmcnt, below) does not wait for the vector loads issued behind them; the compiler keeps
+    // them on the vector path, whose in-order vmcnt made the landmark loads wait for the rows)
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    si4 Bv, WBv;
+    asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(Bv) : "s"(f.blk + (size_t)b * (1 + kFW / 2)));
+    asm volatile("s_load_dwordx4 %0, %1, 0x0" : "=s"(WBv) : "s"(f.blk + (size_t)b * (1 + kFW / 2) + 1 + (wvu >> 1)));
+    // (c) the keyframe entry it solves: previous pose, intrinsics, flags (the prologue
     // gathers them by keyframe row into the workgroup's entry copy; later launches read the copy)
     int4 ke = make_int4(-1, 0, 0, 0);
     int kd = -1;
@@ -852,34 +838,23 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     if (tid < kFK) {
         ke = KE[2 * tid];
         kd = KE[2 * tid + 1].x;
-        // (the copy is read whether or not the entry exists — unused entries are valid memory — so
-        // the load does not wait for the entry table)
-        if (ke.x >= 0 || (!kPro && kEcopy)) {
-            if (kPro || !kEcopy) {
-                const int row = ke.x & 0x3fffffff;
-                const double* Tin = (kPro ? a.kf_pose0 : pose_in(a, it)) + 8 * (size_t)row;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ev[j] = Tin[j];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) ev[8 + j] = a.kf_intr[4 * row + j];
-                ev[12] = (double)a.kf_flags[row];
-            } else {
-                const double4* E4 = reinterpret_cast<const double4*>(f.epose + ((size_t)b * kFK + tid) * 16);
-                const double4 e0 = E4[0], e1 = E4[1], e2 = E4[2];
-                ev[0] = e0.x, ev[1] = e0.y, ev[2] = e0.z, ev[3] = e0.w;
-                ev[4] = e1.x, ev[5] = e1.y, ev[6] = e1.z, ev[7] = e1.w;
-                ev[8] = e2.x, ev[9] = e2.y, ev[10] = e2.z, ev[11] = e2.w;
-                ev[12] = reinterpret_cast<const double*>(E4 + 3)[0];
-            }
-            double* ts = tslot + tid * kTStride;  // (LDS: harmless if the iteration is not live)
-#pragma unroll
-            for (int j = 0; j < 13; ++j) ts[j] = ev[j];
-            if (kPro && kEcopy) {
-                double* E = f.epose + ((size_t)b * kFK + tid) * 16;
-#pragma unroll
-                for (int j = 0; j < 13; ++j) E[j] = ev[j];
-            }
+        if (!kPro && kEcopy) {
+            // (the copy is read whether or not the entry exists — unused entries are valid memory —
+            // so the load does not wait for the entry table)
+            const double4* E4 = reinterpret_cast<const double4*>(f.epose + ((size_t)b * kFK + tid) * 16);
+            const double4 e0 = E4[0], e1 = E4[1], e2 = E4[2];
+            ev[0] = e0.x, ev[1] = e0.y, ev[2] = e0.z, ev[3] = e0.w;
+            ev[4] = e1.x, ev[5] = e1.y, ev[6] = e1.z, ev[7] = e1.w;
+            ev[8] = e2.x, ev[9] = e2.y, ev[10] = e2.z, ev[11] = e2.w;
+            ev[12] = reinterpret_cast<const double*>(E4 + 3)[0];
         }
+    }
+    // (a) this thread's landmark-stage observation (padding rows are valid memory)
+    int4 orec = make_int4(0, 0, 0, 0);
+    double2 ouv = make_double2(1e300, 1e300);
+    if (!kPro) {
+        orec = f.lobs_rec[base + tid];
+        ouv = f.lobs_uv[base + tid];
     }
     // (c') with the rows summed by atomics the entry's own thread (wave 0) reads its row as soon as its
     // entry record is in and solves without the combine phase or the first barrier: the other waves
@@ -892,6 +867,37 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
 #pragma unroll
         for (int t = 0; t < kNTerms; ++t) Sd[t] = rp[t];
     }
+    // (c) the prologue / 1024-thread layout: the entry's state by keyframe row
+    if ((kPro || !kEcopy) && tid < kFK && ke.x >= 0) {
+        const int row = ke.x & 0x3fffffff;
+        const double* Tin = (kPro ? a.kf_pose0 : pose_in(a, it)) + 8 * (size_t)row;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ev[j] = Tin[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ev[8 + j] = a.kf_intr[4 * row + j];
+        ev[12] = (double)a.kf_flags[row];
+    }
+    // (b) the landmark it owns (its position goes to LDS for the observations of the landmark):
+    // fused-order copy at a fixed address (the prologue reads the slot's initial position)
+    // (iterations of the 512-thread layout: only the workgroup's B.x landmark threads load — the
+    // padding rows of the other ~70 % were ~1.8 MB per launch of HBM traffic; the loads wait for B,
+    // which the solving wave's row loads outlast anyway.  The prologue keeps them unconditional: its
+    // first barrier waits for them.)
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(Bv), "+s"(WBv));  // (the block records, above)
+    const int4 B = make_int4(Bv.x, Bv.y, Bv.z, Bv.w), WB = make_int4(WBv.x, WBv.y, WBv.z, WBv.w);
+    const int wstart = (wvu & 1) ? WB.z : WB.x, wrounds = (wvu & 1) ? WB.w : WB.y;
+    const bool lm_load = kPro || !kEcopy || !f.padskip || tid < B.x;
+    int lslot = lm_load ? f.lm_slot[base + tid] : 0;
+    int2 run = make_int2(0, 0);
+    if (!kPro && lm_load) run = f.lm_run[base + tid];
+    D3 PL{0.0, 0.0, 0.0};
+    if (kPro || !kEcopy) {
+        const double* P = kPro ? a.lm_pos0 + 4 * (size_t)lslot : lm_in(a, it, lslot);
+        PL = {P[0], P[1], P[2]};
+    } else if (lm_load) {
+        const double* P = reinterpret_cast<const double*>(f.lpos + base + tid);
+        PL = {P[0], P[1], P[2]};
+    }
     // (d) this wave's first pose-stage round (round r + 1 is requested when round r is consumed)
     const bool pose_next = kPro || it + 1 < a.max_iter;
     double2 u0 = make_double2(0, 0);
@@ -899,6 +905,15 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     if (pose_next && wrounds > 0) {
         u0 = f.pobs_uv[wstart + lane];
         p0 = f.pobs_p[wstart + lane];
+    }
+    // (the entry's state stays in the solving thread's registers: an LDS copy here would wait for
+    // every load issued so far — the waits merge conservatively over the branches above)
+    if (tid < kFK && (ke.x >= 0 || (!kPro && kEcopy))) {
+        if (kPro && kEcopy) {
+            double* E = f.epose + ((size_t)b * kFK + tid) * 16;
+#pragma unroll
+            for (int j = 0; j < 13; ++j) E[j] = ev[j];
+        }
     }
     const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
     const bool has_o = !kPro && tid < n_ob, own = tid < n_lm;
@@ -980,17 +995,16 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     // ---- pose solve of the entries (local_ba.cpp:163-173); owners publish
     if (ke.x >= 0) {
         double* sl = kslot + tid * kLdsStride;
-        const double* ts = tslot + tid * kTStride;
         double T[8], R[9], C[4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) T[j] = ts[j];
+        for (int j = 0; j < 8; ++j) T[j] = ev[j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) C[j] = ts[8 + j];
+        for (int j = 0; j < 4; ++j) C[j] = ev[8 + j];
         if (!kPro) {
             double S[kNTerms];
 #pragma unroll
             for (int t = 0; t < kNTerms; ++t) S[t] = drow ? Sd[t] : sl[t];
-            solve_pose(a, (int)ts[12], S, T, R);
+            solve_pose(a, (int)ev[12], S, T, R);
             if (ke.x & (1 << 30)) {
                 double* Tout = pose_out(a, it) + 8 * (size_t)(ke.x & 0x3fffffff);
 #pragma unroll
@@ -1041,6 +1055,9 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
                 for (int j = 0; j < 9; ++j) hs[j] += terms[j * kFT + r];
                 obs += tcount[r];
             }
+            // (lslot made opaque until here: otherwise its address arithmetic is hoisted next to its
+            // load, whose wait — vmcnt, in issue order — then holds wave 0 for the rows behind it)
+            asm volatile("" : "+v"(lslot));
             PL = lm_update(a, lslot, PL, hs, obs);
             if (kEcopy) f.lpos[base + tid] = make_double4(PL.x, PL.y, PL.z, 0.0);
             lpos[3 * tid] = PL.x;
