@@ -35,6 +35,24 @@ vx_ctx* ThreadContext() {
 }
 }  // namespace vxhost
 
+// the landmark write-back's software prefetch: distance in landmarks, and the object's three lines
+// (shared_ptr control block + id / position, then the observation map and the mutex)
+// ($VX_WB_PREFETCH=0: none, for A/B runs)
+static size_t LmAhead() {
+    static const size_t d = [] {
+        const char* e = std::getenv("VX_WB_PREFETCH");
+        return e && e[0] == '0' ? (size_t)0 : (size_t)16;
+    }();
+    return d;
+}
+static inline void PrefetchObject(const void* p) {
+    if (!p) return;
+    const char* c = static_cast<const char*>(p);
+    __builtin_prefetch(c, 1);
+    __builtin_prefetch(c + 64, 1);
+    __builtin_prefetch(c + 128, 1);
+}
+
 static void check(vx_ctx* c, int rc, const char* what) {
     if (rc != VX_OK) throw std::runtime_error(std::string(what) + ": " + vx_last_error(c));
 }
@@ -484,10 +502,17 @@ void LocalBA::OptimizeResident(const Frame::Ptr& ref_kf) {
         T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
         if (const auto& fr = dm.FrameAt(kr[i])) fr->SetPose(T);
     }
+    // (software prefetch LmAhead() / twice that landmarks ahead: each SetPosition's lock is a
+    // serialising instruction, so without it every landmark object's cache misses are paid one
+    // after the other — 2.4x on a cold 20k-landmark loop, scripts/probe/writeback_prefetch.cpp)
+    const size_t ahead = LmAhead();
     vxhost::Pool::Get().For((size_t)nl, 1024, [&](size_t a, size_t b) {
-        for (size_t i = a; i < b; ++i)
+        for (size_t i = a; i < b; ++i) {
+            if (ahead && i + 2 * ahead < b) __builtin_prefetch(&dm.LandmarkAt(lr[i + 2 * ahead]));
+            if (ahead && i + ahead < b) PrefetchObject(dm.LandmarkAt(lr[i + ahead]).get());
             if (const auto& lm = dm.LandmarkAt(lr[i]))
                 lm->SetPosition(Vec3d(lp[ls * i], lp[ls * i + 1], lp[ls * i + 2]));
+        }
     });
     lap("write-back");
 }
@@ -516,9 +541,12 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
         T.tx = p[4]; T.ty = p[5]; T.tz = p[6];
         f.frames[i]->SetPose(T);
     }
+    const size_t ahead = LmAhead();
     vxhost::Pool::Get().For(f.landmarks.size(), 1024, [&](size_t a, size_t b) {
-        for (size_t i = a; i < b; ++i)
+        for (size_t i = a; i < b; ++i) {
+            if (ahead && i + ahead < b) PrefetchObject(f.landmarks[i + ahead].get());
             f.landmarks[i]->SetPosition(Vec3d(f.lm_pos[3 * i], f.lm_pos[3 * i + 1], f.lm_pos[3 * i + 2]));
+        }
     });
 }
 
