@@ -343,11 +343,27 @@ __global__ __launch_bounds__(kT) void k_lb_lfill(LeanArgs a) {
 }
 
 // the finished run into the resident rows (the last iteration's ping-pong pose buffer)
+// pack (optional): the call's read-back in one block — dyn and the iteration state (hdr_words ints),
+// then (res_off >= 0) at res_off both pose parities, the positions and the landmark rows by capacity
+// nl — so that one copy brings it back instead of five (each a ~3.5 µs blit launch on the call's path)
 __global__ __launch_bounds__(kT) void k_lb_apply(const int* dyn, const int* iters, int nk, const int* win,
                                                  const double* kf_pose, const int* inv, int64_t nl,
-                                                 const double* lm_pos, double* map_pose, double* map_pos) {
-    if (dyn[kDynStatus]) return;
+                                                 const double* lm_pos, double* map_pose, double* map_pos,
+                                                 uint8_t* pack, const int* state, int hdr_words, int64_t res_off) {
     const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (pack) {
+        int* ph = reinterpret_cast<int*>(pack);
+        if (i < kDynInts) ph[i] = dyn[i];
+        else if (i < hdr_words) ph[i] = state[i - kDynInts];
+        double* pr = reinterpret_cast<double*>(pack + (res_off >= 0 ? res_off : 0));
+        for (int64_t k = i; res_off >= 0 && k < 16 * (int64_t)nk; k += (int64_t)gridDim.x * kT) pr[k] = kf_pose[k];
+        if (res_off >= 0 && i < nl) {
+            const double4 v = reinterpret_cast<const double4*>(lm_pos)[i];
+            reinterpret_cast<double4*>(pr + 16 * (int64_t)nk)[i] = v;
+            reinterpret_cast<int*>(pr + 16 * (int64_t)nk + 4 * nl)[i] = inv[i];
+        }
+    }
+    if (dyn[kDynStatus]) return;
     if (i < nk) {
         const double* src = kf_pose + (size_t)(*iters & 1) * nk * 8 + 8 * i;
         for (int j = 0; j < 7; ++j) map_pose[7 * (int64_t)win[i] + j] = src[j];
@@ -846,32 +862,39 @@ int lean_optimize(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_
     d.dyn = a.dyn;
     if (o.max_iterations > 0) {
         if ((rc = ba_run_dyn(c, d))) return rc;
-        // (the apply takes the last iteration's pose buffer from BAState::iterations on the device)
-        const int* iters = reinterpret_cast<const int*>(static_cast<const uint8_t*>(L.state.p) + ba_state_iter_offset());
-        hipLaunchKernelGGL(k_lb_apply, dim3(grid(std::max<long long>(nk, nl))), dim3(kT), 0, sm, (const int*)a.dyn,
-                           iters, nk, a.win, (const double*)L.kf_pose.as<double>(), (const int*)a.inv, nl,
-                           (const double*)L.lm_pos.as<double>(), m->kf_pose.as<double>(), m->lm_pos.as<double>());
-        VX_LAUNCH_CHECK(c, "k_lb_apply");
     }
     // the end: the header (and the iteration state) back — the call's only synchronisation; with
-    // vx_dmap_prefetch_results the results too (both pose parities, positions and rows by capacity)
+    // vx_dmap_prefetch_results the results too (both pose parities, positions and rows by capacity).
+    // After a run, k_lb_apply packs all of it into one device block and ONE copy brings it back.
     const size_t sb = ba_state_bytes();
-    VX_HIP(c, L.rb_host.ensure(kDynInts * 4 + sb));
-    int* H = static_cast<int*>(L.rb_host.p);
-    VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
-    if (o.max_iterations > 0) VX_HIP(c, hipMemcpyAsync(H + kDynInts, L.state.p, sb, hipMemcpyDeviceToHost, sm));
-    L.prefetched = false;
-    if (L.prefetch && o.max_iterations > 0) {
-        const size_t pose_b = 2 * (size_t)nk * 64, pos_b = (size_t)nl * 32, rows_b = (size_t)nl * 4;
-        VX_HIP(c, L.res_host.ensure(pose_b + pos_b + rows_b + 64, true));
-        uint8_t* R = static_cast<uint8_t*>(L.res_host.p);
-        VX_HIP(c, hipMemcpyAsync(R, L.kf_pose.p, pose_b, hipMemcpyDeviceToHost, sm));
-        if (nl) {
-            VX_HIP(c, hipMemcpyAsync(R + pose_b, L.lm_pos.p, pos_b, hipMemcpyDeviceToHost, sm));
-            VX_HIP(c, hipMemcpyAsync(R + pose_b + pos_b, a.inv, rows_b, hipMemcpyDeviceToHost, sm));
-        }
-        L.prefetched = true;
+    const size_t hdr_b = kDynInts * 4 + sb, hdr_pad = (hdr_b + 63) & ~(size_t)63;
+    const bool pf = L.prefetch && o.max_iterations > 0;
+    const size_t pose_b = 2 * (size_t)nk * 64, pos_b = (size_t)nl * 32, rows_b = (size_t)nl * 4;
+    const size_t pack_b = o.max_iterations > 0 ? (pf ? hdr_pad + pose_b + pos_b + rows_b : hdr_b) : 0;
+    int* H = nullptr;
+    if (o.max_iterations > 0) {
+        VX_HIP(c, grow(L.pack, pack_b));
+        // (the apply takes the last iteration's pose buffer from BAState::iterations on the device)
+        const int* iters = reinterpret_cast<const int*>(static_cast<const uint8_t*>(L.state.p) + ba_state_iter_offset());
+        hipLaunchKernelGGL(k_lb_apply, dim3(grid(std::max<long long>(std::max<long long>(nk, nl), (long long)hdr_b / 4))),
+                           dim3(kT), 0, sm, (const int*)a.dyn, iters, nk, a.win, (const double*)L.kf_pose.as<double>(),
+                           (const int*)a.inv, nl, (const double*)L.lm_pos.as<double>(), m->kf_pose.as<double>(),
+                           m->lm_pos.as<double>(), L.pack.as<uint8_t>(), L.state.as<int>(), (int)(hdr_b / 4),
+                           pf ? (int64_t)hdr_pad : (int64_t)-1);
+        VX_LAUNCH_CHECK(c, "k_lb_apply");
+        PinnedBuf& dst = pf ? L.res_host : L.rb_host;
+        VX_HIP(c, dst.ensure(pack_b + 64, pf));  // (the results' block host-cached, as before)
+        VX_HIP(c, hipMemcpyAsync(dst.p, L.pack.p, pack_b, hipMemcpyDeviceToHost, sm));
+        H = static_cast<int*>(dst.p);
+    } else {
+        VX_HIP(c, L.rb_host.ensure(hdr_b));
+        H = static_cast<int*>(L.rb_host.p);
+        VX_HIP(c, hipMemcpyAsync(H, a.dyn, kDynInts * 4, hipMemcpyDeviceToHost, sm));
+    }
+    L.prefetched = pf;
+    if (pf) {
         L.pf_nl = nl;
+        L.res_off = hdr_pad;
     }
     VX_HIP(c, hipStreamSynchronize(sm));
     s.status = H[kDynStatus];
@@ -1156,7 +1179,7 @@ int vx_ba_dmap_results_view(vx_ctx* c, vx_dmap* m, const int32_t** kf_rows, cons
     if (!changed) return VX_OK;
     if (!L.prefetched || L.fallback || L.n_opt > L.pf_nl)
         return set_error(c, VX_ERR_STATE, "results not prefetched (vx_dmap_prefetch_results): use vx_ba_dmap_results");
-    const double* base = reinterpret_cast<const double*>(L.res_host.p);
+    const double* base = reinterpret_cast<const double*>(static_cast<const uint8_t*>(L.res_host.p) + L.res_off);
     *kf_rows = L.win_rows.data();
     *kf_pose8 = base + (size_t)(L.iterations & 1) * L.nk * 8;
     *lm_pos4 = base + 2 * (size_t)L.nk * 8;
@@ -1176,8 +1199,9 @@ int vx_ba_dmap_results(vx_ctx* c, vx_dmap* m, int cap_kf, int64_t* kf_rows, doub
     if (cap_kf < *n_kf || cap_lm < *n_lm) return set_error(c, VX_ERR_CAPACITY, "need %d keyframes / %d landmarks", *n_kf, *n_lm);
     const int nk = L.nk, n = L.n_opt;
     if (L.prefetched && !L.fallback && n <= L.pf_nl) {  // (vx_dmap_prefetch_results: host copies only)
-        const double* pose = reinterpret_cast<const double*>(L.res_host.p) + (size_t)(L.iterations & 1) * nk * 8;
-        const double* pos = reinterpret_cast<const double*>(L.res_host.p) + 2 * (size_t)nk * 8;
+        const double* base = reinterpret_cast<const double*>(static_cast<const uint8_t*>(L.res_host.p) + L.res_off);
+        const double* pose = base + (size_t)(L.iterations & 1) * nk * 8;
+        const double* pos = base + 2 * (size_t)nk * 8;
         const int* rows = reinterpret_cast<const int*>(pos + (size_t)L.pf_nl * 4);
         for (int r = 0; r < nk; ++r) {
             if (kf_rows) kf_rows[r] = L.win_rows[r];

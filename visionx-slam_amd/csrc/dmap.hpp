@@ -64,7 +64,9 @@ struct vx_dmap {
         vx::DevBuf win, f_l, f_code, f_pv, f_back, pscan, wuv, l_ref, l_pv, l_cnt, key, ex, l_slot, inv, cnt, mask,
             lobs_ptr, lm_pos0, lm_pos, puv, plm, lkf, llm, luv, lm_blk, kf_pose0, kf_pose, kf_intr, kf_rot, kf_flags,
             kf_obs_ptr, kf_part, kf_cost, state, dyn, tmp, pkf;
+        vx::DevBuf pack;                   // the call's read-back packed by k_lb_apply: header | results
         vx::PinnedBuf win_host, rb_host, res_host;  // (res_host: vx_ba_dmap_results staging)
+        size_t res_off = 0;                // (prefetched results: their offset in res_host)
         int nk = 0;                        // window of the last call (0: none)
         int status = 1, n_opt = 0, iterations = 0;
         std::vector<int> win_rows;         // its keyframe rows
