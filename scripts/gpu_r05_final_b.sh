@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/r05fe
+O=gpurun_out/${OUT:-r05ff}
 mkdir -p $O
 TAG=r05 bash scripts/gpu_bench.sh > $O/gpu_bench.log 2>&1 || { tail -30 $O/gpu_bench.log; exit 2; }
 tail -5 $O/gpu_bench.log
