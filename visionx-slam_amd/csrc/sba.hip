@@ -624,8 +624,9 @@ __device__ __forceinline__ bool potrf_inv16_t(Rd rd, double* lds_inv, double* Lg
 template <int J>
 __device__ __forceinline__ double quad_bcast(double v) {
     constexpr int ctrl = J | (J << 2) | (J << 4) | (J << 6);  // quad_perm [J, J, J, J]
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), ctrl, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), ctrl, 0xF, 0xF, false);
+    // (every lane has a source inside its quad: no "old" operand to initialise)
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, true);
     return __hiloint2double(hi, lo);
 }
 template <class Rd>
@@ -648,7 +649,9 @@ __device__ __forceinline__ bool potrf_inv16_quad(Rd rd, double* lds_inv, double*
         double aj[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) aj[m] = __shfl(a[m], 4 * j + q, 64);
-        const double r = frsq(d > 0.0 ? d : 1.0);  // (uniform: 1 / L_jj)
+        // (uniform: 1 / L_jj; |d| as a free source modifier instead of a select on the chain — a
+        // non-positive pivot fails the factorisation either way, and the step is rejected)
+        const double r = frsq(fabs(d));
         const double l = quad_bcast<jq>(a[jm] * r);  // L[i][j] for i >= j
         if (q == jq) x[jm] *= r;
         const double xj = quad_bcast<jq>(x[jm]);
