@@ -1412,10 +1412,21 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     // L(K0 + cc, K0p + q) are staged in LDS once, and per row a wave issues its A operands
     // L(i, K0p + q) and its tiles together — one memory round trip per row, not one per step and tile.
     if (t == 0 || split) {  // (split: k_sba_fac_upd applied block t - 1's steps in a launch of its own)
+        // LDS-DMA (global_load_lds, 16 B a lane, no registers): two loads a tile, every tile of the
+        // wave requested back to back.  Lane l of a load writes LDS doubles 2l, 2l + 1 = operand-order
+        // positions of (row (l >> 1) & 15, columns 4 g + 2 (l & 1) .. + 1), g = 2 h + (l >> 5): a 16-byte
+        // piece of one tile row in global memory, so the opo image is built by the source addresses.
+        const int row = (lane >> 1) & 15, cc = 2 * (lane & 1);
         for (int m = wv; m < n; m += kFbWaves) {
             const int e = ent[m];
-            store_acc_opo(T + (size_t)m * kPanelStride, load_acc(L + (long long)(16 * (e >> 16)) * np + 16 * (e & 0xffff), np));
+            const double* src = L + (long long)(16 * (e >> 16) + row) * np + 16 * (e & 0xffff) + cc;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + 4 * (2 * h + (lane >> 5))),
+                    (__attribute__((address_space(3))) void*)(T + (size_t)m * kPanelStride + 128 * h), 16, 0, 0);
         }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes, before the barrier below)
     } else {
         const int r0 = lane >> 4, cl = lane & 15, Wp = sd.Wp, K0p = sd.K0p;
         // rows of the wave: K0 + wv, K0 + wv + kFbWaves, ... that hold a tile of the block; row r + 1's
