@@ -717,12 +717,11 @@ __device__ __forceinline__ int arow_rd(int it) { return it == 0 ? 3 : (it - 1) %
 __device__ __forceinline__ int arow_wr(bool pro, int it) { return pro ? 3 : it % 3; }
 __device__ __forceinline__ int arow_zero(bool pro, int it) { return pro ? 0 : (it + 1) % 3; }
 
-// LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), kFK loaded
-// entry states (T 8 | C 4 | flags), 9 x kFT observation terms, kFT counted flags, 3 x kFT landmark
-// positions, the block-0 totals
-constexpr int kTStride = 13;
+// LDS layout of k_ba_iter (dynamic): kFK keyframe slots (S, then T 8 | R 9 | C 4), 9 x kFT
+// observation terms, kFT counted flags, 3 x kFT landmark positions, the block-0 totals (the entry's
+// loaded state stays in its solving thread's registers)
 constexpr size_t fused_lds(int ft) {
-    return (size_t)kFK * (kLdsStride + kTStride) * sizeof(double) + (size_t)9 * ft * sizeof(double) +
+    return (size_t)kFK * kLdsStride * sizeof(double) + (size_t)9 * ft * sizeof(double) +
            (size_t)ft * sizeof(int) + (size_t)3 * ft * sizeof(double) + (size_t)2 * (ft / 64) * sizeof(double);
 }
 static_assert(fused_lds(kFTLarge) <= 160 * 1024, "k_ba_iter LDS exceeds gfx950's 160 KB per workgroup");
@@ -804,8 +803,7 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     __shared__ int4 s_ke[kFK];
     __shared__ int s_kd[kFK];
     double* kslot = fl;                                  // [kFK][kLdsStride]
-    double* tslot = kslot + kFK * kLdsStride;            // [kFK][kTStride]
-    double* terms = tslot + kFK * kTStride;              // [9][kFT]
+    double* terms = kslot + kFK * kLdsStride;            // [9][kFT]
     int* tcount = reinterpret_cast<int*>(terms + 9 * kFT);
     double* lpos = terms + 9 * kFT + kFT / 2;            // [kFT][3] (after kFT ints)
     double* red = lpos + 3 * kFT;                        // [2][kFW]
