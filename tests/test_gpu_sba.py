@@ -163,18 +163,6 @@ def test_sba_multi_workgroup_factor_bitwise(ctx, monkeypatch, cfg):
         plan.close()
         out[(form, groups, la, cols)] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
                                          mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
-    # the blocked factor with workgroup 0's own look-ahead instead of k_sba_fac_upd's launch
-    monkeypatch.setenv("VX_SBA_FACTOR", "block")
-    monkeypatch.setenv("VX_SBA_FACTOR_LA", "wg0")
-    monkeypatch.delenv("VX_SBA_FACTOR_GROUPS", raising=False)
-    mm = m.copy()
-    plan = ctx.sba_plan(mm, opts)
-    plan.run_async()
-    st = plan.fetch(mm)
-    plan.close()
-    out[("block", "wg0")] = (st.iterations, st.accepted, list(st.cost), list(st.obs), list(st.step),
-                             mm["kf_pose"].tobytes(), mm["lm_pos"].tobytes())
-    monkeypatch.delenv("VX_SBA_FACTOR_LA", raising=False)
     ref = out[("single", None, "1", "2")]
     assert ref[1] >= 1
     for k, v in out.items():

@@ -1245,8 +1245,9 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_pair(SBAArgs a, int i
 // The same right-looking tiled Cholesky in blocks of up to kFbW tile columns, one launch per block
 // (round 5: the one-launch-per-column form spent ~13 us per column on workgroup 0's chain, most of it
 // global round trips and the launch).  Launch t: workgroup 0 loads every tile of block t's columns
-// (at most the plan's LDS capacity), applies block t - 1's steps to them on the way in (the
-// look-ahead), and factors the block in LDS — per column POTRF + L^-1 of the diagonal tile, the panel
+// (at most kFbCap tiles), which k_sba_fac_upd's launch just before brought up to date with block
+// t - 1's steps (the look-ahead), and factors the block in LDS — per column POTRF + L^-1 of the
+// diagonal tile, the panel
 // L_ic = A_ic L_cc^-T (written to the factor in global memory as well), then the column's steps on the
 // block's later columns — while G - 1 workgroups apply block t - 1's steps to the tiles beyond block t.
 // Every tile receives its steps in ascending order with the same operations (MFMA operands read in
@@ -1255,7 +1256,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_fac_pair(SBAArgs a, int i
 constexpr int kFbThreads = 512;
 constexpr int kFbWaves = kFbThreads / 64;
 constexpr int kFbW = 4;       // tile columns per block (4-bit step masks)
-constexpr int kFbCap = 60;    // LDS tiles of a block (operand order, 2 KB each)
+constexpr int kFbCap = 60;    // LDS tiles of a block (operand order, 2 KB each; 72 measured no faster: 19 blocks of 19.3 µs against 24 of 14.8)
 
 __device__ __forceinline__ d4 load_acc_opo(const double* S) {
     const int lane = threadIdx.x & 63, r0 = lane >> 4, c = lane & 15;
@@ -1310,9 +1311,10 @@ __device__ __forceinline__ void blk_tiles_pf(double* L, int np, const int* tl, i
     }
 }
 
-// The look-ahead as a launch of its own (before k_sba_fac_blk's launch t >= 1, $VX_SBA_FACTOR_LA
-// default): block t - 1's steps applied to block t's tiles by G workgroups, so workgroup 0 of the
-// factor launch loads block t finished instead of running ~2 MFLOP of updates on its one CU.
+// The look-ahead as a launch of its own (before k_sba_fac_blk's launch t >= 1): block t - 1's steps
+// applied to block t's tiles by G workgroups, so workgroup 0 of the factor launch loads block t
+// finished instead of running ~2 MFLOP of updates on its one CU (round 5: 711 -> 617 µs per LM
+// iteration at the connected C5; workgroup 0's own row-wise look-ahead has been removed since).
 __global__ __launch_bounds__(kFbThreads) void k_sba_fac_upd(SBAArgs a, int it, int t, int G, FacBlk sd) {
     const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
     if (sd.nt == 0) {
@@ -1331,7 +1333,7 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_upd(SBAArgs a, int it, i
     blk_tiles_pf(a.L + sd.loff, 16 * sd.nt, a.tl, sd.K0p, sd.la_beg + g, sd.la_end, G, kFbWaves);
 }
 
-__global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, int t, int G, int cap, int split, FacBlk sd) {
+__global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, int t, int G, int cap, FacBlk sd) {
     const int comp = blockIdx.x / G, g = blockIdx.x - comp * G;
     if (sd.nt == 0) {
         const int* d = a.fac_blks + 16 * ((size_t)comp * a.fac_nb + t);
@@ -1385,37 +1387,26 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     const int K0 = sd.K0, W = sd.W, n = sd.bt_end - sd.bt_beg, n1 = nt + 1;
     double* T = sm;                                   // cap tiles, operand order
     double* dlds = sm + (size_t)cap * kPanelStride;   // L_cc^-1 of the current column
-    double* Bst = dlds + kPanelStride;                // kFbW x kFbW: L(K0 + cc, K0p + q), operand order
-    int* ent = reinterpret_cast<int*>(Bst + kFbW * kFbW * kPanelStride);  // cap entries i << 16 | c
+    double* dl2 = dlds + kPanelStride;                // ... and of the next (the two alternate)
+    int* ent = reinterpret_cast<int*>(dl2 + kPanelStride);  // cap entries i << 16 | c
     int* rs = ent + cap;                              // kFbW x n1: slot of (i, K0 + cc), -1: none
-    int* pz = rs + kFbW * n1;                         // kFbW x n1: tile (i, K0p + cc) of block t - 1 nonzero
-    int* cb = pz + kFbW * n1;                         // kFbW + 1: first slot of column cc (its diagonal)
-    for (int x = tid; x < kFbW * n1; x += kFbThreads) {
-        rs[x] = -1;
-        pz[x] = 0;
-    }
+    int* cb = rs + kFbW * n1;                         // kFbW + 1: first slot of column cc (its diagonal)
+    for (int x = tid; x < kFbW * n1; x += kFbThreads) rs[x] = -1;
     __syncthreads();
     for (int s = tid; s < n; s += kFbThreads) {
         const int e = tl[sd.bt_beg + s];
         ent[s] = e;
         rs[((e & 0xffff) - K0) * n1 + (e >> 16)] = s;
     }
-    for (int s = tid; t > 0 && !split && s < sd.pb_end - sd.pb_beg; s += kFbThreads) {
-        const int e = tl[sd.pb_beg + s];
-        pz[((e & 0xffff) - sd.K0p) * n1 + (e >> 16)] = 1;
-    }
     __syncthreads();
     if (tid <= W) cb[tid] = tid < W ? rs[tid * n1 + K0 + tid] : n;
     if (kt) VX_KT(11);
-    // block t's tiles into LDS with block t - 1's steps (tile (i, j), step k: NZ(i, k) and NZ(j, k);
-    // the rhs row i = nt is in every column's list).  Row by row: the block's B operands
-    // L(K0 + cc, K0p + q) are staged in LDS once, and per row a wave issues its A operands
-    // L(i, K0p + q) and its tiles together — one memory round trip per row, not one per step and tile.
-    if (t == 0 || split) {  // (split: k_sba_fac_upd applied block t - 1's steps in a launch of its own)
-        // LDS-DMA (global_load_lds, 16 B a lane, no registers): two loads a tile, every tile of the
-        // wave requested back to back.  Lane l of a load writes LDS doubles 2l, 2l + 1 = operand-order
-        // positions of (row (l >> 1) & 15, columns 4 g + 2 (l & 1) .. + 1), g = 2 h + (l >> 5): a 16-byte
-        // piece of one tile row in global memory, so the opo image is built by the source addresses.
+    // block t's tiles into LDS (block t - 1's steps: k_sba_fac_upd, the launch before) by LDS-DMA
+    // (global_load_lds, 16 B a lane, no registers): two loads a tile, every tile of the wave requested
+    // back to back.  Lane l of a load writes LDS doubles 2l, 2l + 1 = operand-order positions of (row
+    // (l >> 1) & 15, columns 4 g + 2 (l & 1) .. + 1), g = 2 h + (l >> 5): a 16-byte piece of one tile row
+    // in global memory, so the opo image is built by the source addresses.
+    {
         const int row = (lane >> 1) & 15, cc = 2 * (lane & 1);
         for (int m = wv; m < n; m += kFbWaves) {
             const int e = ent[m];
@@ -1427,65 +1418,6 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
                     (__attribute__((address_space(3))) void*)(T + (size_t)m * kPanelStride + 128 * h), 16, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA writes, before the barrier below)
-    } else {
-        const int r0 = lane >> 4, cl = lane & 15, Wp = sd.Wp, K0p = sd.K0p;
-        // rows of the wave: K0 + wv, K0 + wv + kFbWaves, ... that hold a tile of the block; row r + 1's
-        // operands are requested before row r's products (software-pipelined: one exposed round trip)
-        auto has_row = [&](int i) {
-            bool any = false;
-#pragma unroll
-            for (int cc = 0; cc < kFbW; ++cc) any = any || (cc < W && rs[cc * n1 + i] >= 0);
-            return any;
-        };
-        auto next_row = [&](int i) {
-            while (i <= nt && !has_row(i)) i += kFbWaves;
-            return i;
-        };
-        auto fetch = [&](int i, double4 (&ao)[kFbW], d4 (&acc)[kFbW]) {
-#pragma unroll
-            for (int q = 0; q < kFbW; ++q)
-                ao[q] = *reinterpret_cast<const double4*>(L + (long long)(16 * i + cl) * np + 16 * (K0p + min(q, Wp - 1)) + 4 * r0);
-#pragma unroll
-            for (int cc = 0; cc < kFbW; ++cc)
-                if (cc < W && rs[cc * n1 + i] >= 0) acc[cc] = load_acc(L + (long long)(16 * i) * np + 16 * (K0 + cc), np);
-        };
-        double4 ao[kFbW], ao2[kFbW];
-        d4 acc[kFbW], acc2[kFbW];
-        int i = next_row(K0 + wv);
-        if (i <= nt) fetch(i, ao, acc);  // (the first row's round trip overlaps the B staging)
-        for (int x = wv; x < W * Wp; x += kFbWaves) {
-            const int cc = x / Wp, q = x - cc * Wp;
-            *reinterpret_cast<double4*>(Bst + (size_t)(cc * kFbW + q) * kPanelStride + 4 * lane) =
-                *reinterpret_cast<const double4*>(L + (long long)(16 * (K0 + cc) + cl) * np + 16 * (K0p + q) + 4 * r0);
-        }
-        __syncthreads();
-        if (kt) VX_KT(14);
-        while (i <= nt) {
-            const int i2 = next_row(i + kFbWaves);
-            if (i2 <= nt) fetch(i2, ao2, acc2);
-#pragma unroll
-            for (int cc = 0; cc < kFbW; ++cc) {
-                const int sl = cc < W ? rs[cc * n1 + i] : -1;
-                if (sl < 0) continue;
-#pragma unroll
-                for (int q = 0; q < kFbW; ++q)
-                    if (q < Wp && pz[q * n1 + i] && pz[q * n1 + K0 + cc]) {  // (the order of mfma_abt_g)
-                        const double4 bv = *reinterpret_cast<const double4*>(Bst + (size_t)(cc * kFbW + q) * kPanelStride + 4 * lane);
-                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].x, bv.x, acc[cc], 0, 0, 0);
-                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].y, bv.y, acc[cc], 0, 0, 0);
-                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].z, bv.z, acc[cc], 0, 0, 0);
-                        acc[cc] = __builtin_amdgcn_mfma_f64_16x16x4f64(-ao[q].w, bv.w, acc[cc], 0, 0, 0);
-                    }
-                store_acc_opo(T + (size_t)sl * kPanelStride, acc[cc]);
-            }
-#pragma unroll
-            for (int q = 0; q < kFbW; ++q) {
-                ao[q] = ao2[q];
-                acc[q] = acc2[q];
-            }
-            i = i2;
-        }
-        if (kt) VX_KTW(0, kFbWaves);  // (per wave: its look-ahead rows done)
     }
     __syncthreads();
     if (kt) VX_KT(12);
@@ -1493,10 +1425,10 @@ __global__ __launch_bounds__(kFbThreads) void k_sba_fac_blk(SBAArgs a, int it, i
     // a barrier.  The next column's POTRF + inverse runs on wave 0 beside step c's updates: its
     // diagonal tile's last step is the product of the panel tile L_(c+1)c with itself, which wave 0
     // forms first in the panel phase and applies at once — so the column chain is panel + max(POTRF,
-    // updates), not POTRF + panel + updates.  (Two L_cc^-1 buffers alternate: dlds and the staging
-    // area Bst, free after the look-ahead.  Every tile sees the same operations in the same order.)
+    // updates), not POTRF + panel + updates.  (Two L_cc^-1 buffers alternate, dlds and dl2.  Every tile
+    // sees the same operations in the same order.)
     bool ok = true;
-    double* dl[2] = {dlds, Bst};
+    double* dl[2] = {dlds, dl2};
     if (wv == 0) {
         const double* D = T + (size_t)cb[0] * kPanelStride;
         ok = potrf_inv16_quad([&](int r, int q) { return D[opo(r, q)]; }, dl[0], Linv + 256 * K0);
@@ -2502,15 +2434,16 @@ bool factor_multi(int max_nt) {
 // the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, the default where every
 // column fits its LDS: connected C5 786 against 937 us per LM iteration) or one column
 // per launch ($VX_SBA_FACTOR=multi)
+// k_sba_fac_blk's LDS: the block's tiles, the two L_cc^-1, the entries and the slot table
+size_t blk_lds_bytes(int max_nt) {
+    return ((size_t)kFbCap + 2) * kPanelStride * sizeof(double) +
+           ((size_t)kFbCap + kFbW * ((size_t)max_nt + 1) + kFbW + 1) * sizeof(int);
+}
+constexpr int kLdsMax = 160 * 1024 - 256;  // (dynamic LDS: the kernel's static variables take the rest)
 bool factor_blocked(const vx_sba_plan* p) {
     const char* e = std::getenv("VX_SBA_FACTOR");
     if (e && std::strcmp(e, "multi") == 0) return false;
-    return p->blk_ok;
-}
-// k_sba_fac_blk's LDS: the block's tiles, L^-1, the staged B operands, the entries and the two slot tables
-size_t blk_lds_bytes(int max_nt) {
-    return ((size_t)kFbCap + 1 + kFbW * kFbW) * kPanelStride * sizeof(double) +
-           ((size_t)kFbCap + 2 * kFbW * ((size_t)max_nt + 1) + kFbW + 1) * sizeof(int);
+    return p->blk_ok && blk_lds_bytes(p->max_nt) <= (size_t)kLdsMax;  // (larger components: one column per launch)
 }
 // workgroups per component and step: workgroup 0 takes the look-ahead column, the others about 8
 // trailing tiles each (two per wave); $VX_SBA_FACTOR_GROUPS overrides
@@ -2525,7 +2458,6 @@ struct SbaRunCfg {
     SBAArgs a;
     size_t lds = 0, bs_lds = 0, la_lds = 0, red_n = 0, blk_lds = 0;
     int upd_blocks = 1, G = 1, la_ps = 0, Gb = 1, bs_depth = 3, Gu = 1;
-    int blk_split = 1;  // k_sba_fac_upd before each block launch ($VX_SBA_FACTOR_LA=wg0: workgroup 0's look-ahead)
     bool multi = false, pair = false, blk = false;
 };
 
@@ -2567,13 +2499,12 @@ int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
     if (r.blk) {
         r.blk_lds = blk_lds_bytes(p->max_nt);
         static std::atomic<uint64_t> blk_attr{0};
-        VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_sba_fac_blk), (int)r.blk_lds, blk_attr));
+        // (the attribute at the most any plan launches with: it is set once per device)
+        VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_sba_fac_blk), kLdsMax, blk_attr));
         // workgroup 0 factors the block, the others take ~32 trailing tiles each (4 per wave in flight)
         r.Gb = 1 + (p->max_blk_trail + 31) / 32;
         if (const char* e = std::getenv("VX_SBA_FACTOR_GROUPS")) r.Gb = std::atoi(e);
         r.Gb = std::max(1, std::min(r.Gb, 128));
-        const char* la = std::getenv("VX_SBA_FACTOR_LA");
-        r.blk_split = la && std::strcmp(la, "wg0") == 0 ? 0 : 1;
         r.Gu = std::max(1, std::min(256, (p->max_blk_la + 15) / 16));  // (two tiles per wave)
     }
     r.red_n = (size_t)p->l_total + (size_t)p->nk * 14;
@@ -2607,11 +2538,11 @@ int sba_solve_step(vx_ctx* c, vx_sba_plan* p, const SbaRunCfg& r, int it) {
                 sd.K0p = d[8], sd.Wp = d[9], sd.tr_beg = d[10], sd.tr_end = d[11], sd.nt = d[12];
                 sd.la_beg = d[13], sd.la_end = d[14];
             }
-            if (r.blk_split && t > 0)
+            if (t > 0)
                 VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_upd, dim3(std::max(p->n_comp, 1) * r.Gu), dim3(kFbThreads), 0,
                                  c->stream, a, it, t, r.Gu, sd));
             VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_blk, dim3(std::max(p->n_comp, 1) * r.Gb), dim3(kFbThreads),
-                             (uint32_t)r.blk_lds, c->stream, a, it, t, r.Gb, kFbCap, r.blk_split, sd));
+                             (uint32_t)r.blk_lds, c->stream, a, it, t, r.Gb, kFbCap, sd));
         }
     } else if (r.multi) {
         VX_HIP(c, launch(c, kStSbaSolve, k_sba_fac_begin, dim3(std::max(p->n_comp, 1)), dim3(kSolveThreads), 0,
