@@ -2502,10 +2502,18 @@ int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
         // (the attribute at the most any plan launches with: it is set once per device)
         VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_sba_fac_blk), kLdsMax, blk_attr));
         // workgroup 0 factors the block, the others take ~32 trailing tiles each (4 per wave in flight)
-        r.Gb = 1 + (p->max_blk_trail + 31) / 32;
+        // the look-ahead launch: one tile per workgroup (its wave 0), the launch spread over as many
+        // CUs as block t has look-ahead tiles — each tile is a chain of up to 16 dependent MFMAs, so
+        // tiles sharing a wave or a CU wait on each other (connected C5: 5.78 -> 5.17 ms per
+        // optimisation against 16 tiles per workgroup; 64-thread workgroups measured the same,
+        // DESIGN.md §22).  $VX_SBA_UPD_TILES / $VX_SBA_BLK_TILES: tiles per look-ahead / helper
+        // workgroup, for sweeps.
+        const int bt = std::getenv("VX_SBA_BLK_TILES") ? std::max(1, std::atoi(std::getenv("VX_SBA_BLK_TILES"))) : 32;
+        const int ut = std::getenv("VX_SBA_UPD_TILES") ? std::max(1, std::atoi(std::getenv("VX_SBA_UPD_TILES"))) : 1;
+        r.Gb = 1 + (p->max_blk_trail + bt - 1) / bt;
         if (const char* e = std::getenv("VX_SBA_FACTOR_GROUPS")) r.Gb = std::atoi(e);
         r.Gb = std::max(1, std::min(r.Gb, 128));
-        r.Gu = std::max(1, std::min(256, (p->max_blk_la + 15) / 16));  // (two tiles per wave)
+        r.Gu = std::max(1, std::min(1024, (p->max_blk_la + ut - 1) / ut));
     }
     r.red_n = (size_t)p->l_total + (size_t)p->nk * 14;
     return VX_OK;
