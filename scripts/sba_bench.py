@@ -60,7 +60,7 @@ for cfg, (nk, nl, ns), cf in CFGS:
                       "ms_per_optimize": round(ms, 4), "iterations": st.iterations, "accepted": st.accepted,
                       "cost": [round(st.initial_cost, 1), round(st.final_cost, 1)],
                       "plan_build_ms_host": round(build_ms, 2), "plan_build_ms_host_first": round(builds[0], 2),
-                      "factor": os.environ.get("VX_SBA_FACTOR", "auto: blocked multi-workgroup above 32 tile columns"),
+                      "factor": os.environ.get("VX_SBA_FACTOR", "auto: blocked multi-workgroup where the block LDS fits"),
                       "kernel_us_per_launch": {k: round(v[0] * 1e3 / v[1], 2) for k, v in prof.items()
                                                if k.startswith("sba") and v[1]},
                       "kernel_us_per_iteration": {k: round(v[0] * 1e3 / max(st.iterations, 1), 2)

@@ -2425,11 +2425,16 @@ size_t lookahead_lds_bytes(int max_nt, int ps) {
     return (size_t)(4 + ps) * kPanelStride * sizeof(double) + (size_t)(max_nt + 1 + ps) * sizeof(int);
 }
 
-bool factor_multi(int max_nt) {
+bool factor_blocked(const vx_sba_plan* p);
+// Round 5: with one look-ahead tile per workgroup the blocked form is ahead at every size measured —
+// C3 (19 tile columns) 144 -> 94 us per LM iteration, C5 (eight components of 10) 83 -> 55
+// (`profiles/r05/sba_factor_block_small_r05az.txt`) — so it is the default wherever its LDS holds a
+// block; otherwise one column per launch above 32 tile columns, the single workgroup below.
+bool factor_multi(const vx_sba_plan* p) {
     const char* e = std::getenv("VX_SBA_FACTOR");
     if (e && std::strcmp(e, "single") == 0) return false;
     if (e && (std::strcmp(e, "multi") == 0 || std::strcmp(e, "block") == 0)) return true;
-    return max_nt > 32;
+    return factor_blocked(p) || p->max_nt > 32;
 }
 // the multi-workgroup factor in blocks of up to kFbW columns (k_sba_fac_blk, the default where every
 // column fits its LDS: connected C5 786 against 937 us per LM iteration) or one column
@@ -2479,7 +2484,7 @@ int sba_prepare(vx_ctx* c, vx_sba_plan* p, SbaRunCfg& r) {
         VX_HIP(c, hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sba_backsub<6>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)r.bs_lds));
     }
-    r.multi = factor_multi(p->max_nt);
+    r.multi = factor_multi(p);
     r.G = factor_groups(p->max_trail_rest);
     // one tile column per launch (default) or two ($VX_SBA_FACTOR_COLS=2: half the launches, but
     // workgroup 0's chain per launch doubles — measured slower on the connected C5, 1137 against 1030
