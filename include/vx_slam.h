@@ -240,7 +240,7 @@ typedef struct {
     const uint64_t* feat_lm_id;  /* Feature::landmark_id_ */
     const uint8_t* feat_flags;   /* bit0 has_landmark, bit1 is_outlier */
     int32_t n_lm;
-    const uint64_t* lm_id;
+    const uint64_t* lm_id;       /* distinct ids in any order (not necessarily sorted: lookups hash them) */
     double* lm_pos;              /* 3 per landmark */
     const uint8_t* lm_bad;
     const int64_t* lm_obs_ptr;   /* n_lm + 1, CSR of (kf id, feature index) observations */
@@ -267,6 +267,12 @@ typedef struct {
 } vx_ba_stats;
 
 void vx_ba_default_options(vx_ba_options* o);
+/* Reproducibility: unsharded windows sum each keyframe's normal-equation row with FP64 float
+ * atomics by default (arrival order), so two runs of the same input agree to rounding (~1e-8
+ * relative in the positions after five iterations; residuals move < 1e-7 px), not bit for bit.
+ * Set $VX_BA_ATOMIC_ROWS=0 before the plan is built for per-workgroup partial slots summed in a fixed
+ * order: bitwise-repeatable runs, ~7 % slower LocalBA.  Sharded plans always use
+ * the slots. */
 int vx_ba_optimize_map(vx_ctx* ctx, vx_map_view* map, uint64_t ref_kf_id, int has_ref,
                        const vx_ba_options* opt, vx_ba_stats* stats);
 

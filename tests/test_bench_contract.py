@@ -64,6 +64,25 @@ def test_bench_json_line():
     rf = d["roofline"]
     assert rf["bound"] == "hbm" and rf["peak"] == 8000.0 and 0 < rf["frac"] < 1
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-4
+    # frac follows from the bytes and the profiling pass's per-dispatch average (stages_us)
+    assert abs(rf["avg_launch_us"] - d["stages_us"][rf["kernel"]]) <= 0.01
+    assert abs(rf["frac"] - rf["bytes_per_launch"] / (rf["avg_launch_us"] * 1e-6) / 8e12) <= 2e-4
+
+
+def test_committed_bench_roofline_matches_committed_profile():
+    """The C3 bench line printed under rocprofv3 this round and the --kernel-trace --stats summary of
+    the same command (profiles/r06): the line's roofline fraction is within 5 % of the algorithmic
+    bytes / rocprof's average duration of that kernel / 8 TB/s."""
+    d = json.loads(open(os.path.join(ROOT, "profiles", "r06", "bench_c3_rocprof_r06.json")).read().strip().splitlines()[-1])
+    rf = d["roofline"]
+    assert rf["hip_kernel"] == "k_ba_iter" and rf["kernel"] == "ba_iter"
+    # the iteration launches (k_ba_iter<false, ...>); the prologue (k_ba_iter<true, ...>) is its own stage
+    with open(os.path.join(ROOT, "profiles", "r06", "kernel_stats_bench_c3_r06.csv")) as f:
+        rows = [r for r in csv.DictReader(f) if "k_ba_iter<false" in r["Name"]]
+    assert len(rows) == 1
+    avg_us = float(rows[0]["AverageNs"]) / 1e3
+    frac_prof = rf["bytes_per_launch"] / (avg_us * 1e-6) / 8e12
+    assert abs(rf["frac"] - frac_prof) <= 0.05 * frac_prof, (rf["frac"], frac_prof, avg_us, rf["avg_launch_us"])
 
 
 def test_cpu_baseline_mt_small():

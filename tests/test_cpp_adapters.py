@@ -60,6 +60,62 @@ def test_flatten_selects_the_reference_window(driver, oracle, tmp_path):
         assert flat_lm == ref_ids
 
 
+def _mix64(x):
+    """feature.cpp's id hash (splitmix64 finaliser), for choosing ids that all land in one region."""
+    M = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    return x ^ (x >> 31)
+
+
+def _one_keyframe_map(ids, seed):
+    """One keyframe whose every feature names its own landmark (an RGB-D keyframe with depth
+    everywhere): as many distinct landmark ids as features."""
+    rng = np.random.default_rng(seed)
+    nf = len(ids)
+    m = synth.BAMap()
+    m["kf_id"] = np.array([11], np.uint64)
+    m["kf_pose"] = np.array([[0, 0, 0, 1, 0, 0, 0]], np.float64)
+    m["kf_intr"] = np.array([[525.0, 525.0, 319.5, 239.5]])
+    m["kf_has_cam"] = np.ones(1, np.uint8)
+    m["kf_feat_ptr"] = np.array([0, nf], np.int64)
+    m["feat_uv"] = rng.uniform([0, 0], [640, 480], size=(nf, 2))
+    m["feat_lm_id"] = np.asarray(ids, np.uint64)
+    m["feat_flags"] = np.ones(nf, np.uint8)
+    m["lm_id"] = np.asarray(ids, np.uint64)
+    m["lm_pos"] = rng.uniform([-1, -1, 1], [1, 1, 5], size=(nf, 3))
+    m["lm_bad"] = np.zeros(nf, np.uint8)
+    m["lm_obs_ptr"] = np.arange(nf + 1, dtype=np.int64)
+    m["obs_kf_id"] = np.full(nf, 11, np.uint64)
+    m["obs_feat_idx"] = np.arange(nf, dtype=np.uint64)
+    return m
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_flatten_distinct_landmark_window(driver, tmp_path, monkeypatch, threads):
+    """LocalBA::Flatten's id dedup (feature.cpp distinct_ids) on windows where every feature has its
+    own landmark: at the feature counts where a hash region's share sits at its table's half-load
+    boundary, and with every id hashed into ONE region (its table must grow, not abort)."""
+    monkeypatch.setenv("VX_HOST_THREADS", str(threads))
+    rng = np.random.default_rng(5)
+    cases = [rng.choice(1 << 62, size=n, replace=False).astype(np.uint64) for n in (1790, 3700, 3800, 9000)]
+    skew, x = [], 1
+    while len(skew) < 3000:  # ids whose region (high hash bits scaled to 8 parts) is region 0
+        if ((_mix64(x) >> 32) * 8) >> 32 == 0:
+            skew.append(x)
+        x += 1
+    cases.append(np.array(skew, np.uint64))
+    for i, ids in enumerate(cases):
+        d = tmp_path / str(i)
+        d.mkdir()
+        dump_map(_one_keyframe_map(ids, i), d)
+        n_kf, n_lm, n_obs = map(int, run(driver, "ba", d, 5, 5, 11, "flatten"))
+        flat_lm = np.fromfile(os.path.join(d, "flat_lm_id.out"), np.uint64)
+        assert n_kf == 1 and n_lm == len(ids) and n_obs == len(ids)
+        assert np.array_equal(flat_lm, ids)  # first-occurrence order = feature order here
+
+
 @pytest.mark.gpu
 def test_adapter_extract_and_match(driver, oracle, tmp_path):
     frames = synth.make_frames(91, 2)

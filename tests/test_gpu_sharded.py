@@ -72,7 +72,9 @@ def test_sharded_localba_bench_windows(ctx, oracle, n, ba_path):
     _assert_ba_close(got, one, stats[0], st1)
     mc = m.copy()
     stc = oracle.ba_optimize(mc, oracle.ba_options(window=nk))
-    assert stc.gate_margin >= 1e-8, f"gate margin {stc.gate_margin}: reseed this case"  # (never skipped)
+    # (never skipped; sharded plans sum their rows in slot order, bitwise run to run, so the margin
+    # only has to cover GPU-vs-CPU rounding: 1e-7 px, the 8-way window's is 2.4e-7)
+    assert stc.gate_margin >= 1e-7, f"gate margin {stc.gate_margin}: reseed this case"
     _assert_ba_close(got, mc, stats[0], stc)
 
 

@@ -937,7 +937,7 @@ __global__ __launch_bounds__(kSolveThreads) void k_sba_solve(SBAArgs a, int it) 
     }
     VX_KT(11);
     if (wv == 0 && lane == 0 && !ok) atomicOr(&a.st->fail[it], 1);
-    // (the back-substitution, dx and the clearing of the touched tiles: k_sba_backsub)
+    // (the back-substitution and dx: k_sba_backsub; the clearing of the touched tiles: k_sba_update)
 }
 
 // ------------------------------------------------------------------------- multi-workgroup factor

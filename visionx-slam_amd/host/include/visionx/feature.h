@@ -87,7 +87,7 @@ struct FlatMap {
     std::vector<int64_t> lm_obs_ptr;
     std::vector<uint64_t> obs_kf_id, obs_feat_idx;
     std::vector<Frame::Ptr> frames;        // keyframes in kf_id order
-    std::vector<Landmark::Ptr> landmarks;  // landmarks in lm_id order (first reference in the window)
+    std::vector<Landmark::Ptr> landmarks;  // parallel to lm_id: first-reference order in the window, NOT ascending ids
     vx_map_view view();                    // pointers into the vectors above
     // (Flatten's working arrays, kept with their capacity between calls)
     std::vector<uint8_t> scratch_has;

@@ -253,21 +253,27 @@ static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector
     auto& pool = vxhost::Pool::Get();
     const size_t nf = feat_lm.size();
     const int parts = std::max(1, pool.Threads());
-    size_t per = 64;  // slots per region: >= 2 x the ids a region can receive (all of them, worst case)
+    // slots per region: ~2 x a region's average share of the features.  A region that receives more
+    // ids than half its slots (a window whose features nearly all name distinct landmarks, or an
+    // unlucky spread over the regions) moves to a private table of twice the size, its keys re-inserted
+    size_t per = 64;
     while (per < 2 * nf / (size_t)parts + 64) per <<= 1;
     f.scratch_key.resize(per * (size_t)parts);
     f.scratch_first.resize(per * (size_t)parts);  // (occupancy flags)
     pool.For((size_t)parts, 1, [&](size_t a, size_t b) {
+        std::vector<uint64_t> own_key;  // a grown region's table (rare)
+        std::vector<uint32_t> own_used;
         for (size_t t = a; t < b; ++t) {
             uint64_t* key = f.scratch_key.data() + t * per;
             uint32_t* used = f.scratch_first.data() + t * per;
-            std::fill(used, used + per, 0u);
+            size_t cap = per;
+            std::fill(used, used + cap, 0u);
             size_t n_in = 0;
             for (size_t o = 0; o < nf; ++o) {
                 // region = the high hash bits scaled to [0, parts) (no division), slot = the low bits
                 if (!has[o] || (size_t)(((hash[o] >> 32) * (uint64_t)parts) >> 32) != t) continue;
                 const uint64_t id = feat_lm[o];
-                size_t h = (size_t)hash[o] & (per - 1);
+                size_t h = (size_t)hash[o] & (cap - 1);
                 for (;;) {
                     if (!used[h]) {  // first occurrence
                         used[h] = 1;
@@ -277,9 +283,24 @@ static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector
                         break;
                     }
                     if (key[h] == id) break;
-                    h = (h + 1) & (per - 1);
+                    h = (h + 1) & (cap - 1);
                 }
-                if (2 * n_in > per) std::abort();  // (cannot happen: per >= 2 x the ids of the region)
+                if (2 * n_in > cap) {  // keep the load <= 1/2: double the table, re-insert its keys
+                    std::vector<uint64_t> nk(2 * cap);
+                    std::vector<uint32_t> nu(2 * cap, 0u);
+                    for (size_t s = 0; s < cap; ++s) {
+                        if (!used[s]) continue;
+                        size_t g = (size_t)mix64(key[s]) & (2 * cap - 1);
+                        while (nu[g]) g = (g + 1) & (2 * cap - 1);
+                        nu[g] = 1;
+                        nk[g] = key[s];
+                    }
+                    own_key.swap(nk);
+                    own_used.swap(nu);
+                    key = own_key.data();
+                    used = own_used.data();
+                    cap *= 2;
+                }
             }
         }
     });
@@ -400,7 +421,7 @@ void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size,
     });
     lap("lookups");
     size_t nl = 0;
-    for (size_t i = 0; i < nid; ++i)  // (compact the found ones, keep ascending ids)
+    for (size_t i = 0; i < nid; ++i)  // (compact the found ones, keep first-occurrence order)
         if (obj[i]) {
             ids[nl] = ids[i];
             obj[nl] = obj[i];

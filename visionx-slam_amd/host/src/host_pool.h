@@ -30,18 +30,6 @@ public:
     }
     int Threads() const { return (int)workers_.size() + 1; }
 
-    // Wake the workers into their spin phase ahead of a job the caller knows is coming (the LocalBA
-    // write-back after the device call): a sleeping worker's futex wake costs tens of microseconds,
-    // which a job over ~20k landmarks cannot hide.
-    void Prime() {
-        if (workers_.empty()) return;
-        {
-            std::lock_guard<std::mutex> lk(m_);
-            ++prime_;
-        }
-        cv_.notify_all();
-    }
-
     // fn(begin, end) over [0, n) in chunks of at least min_chunk items; returns when every chunk is done
     void For(size_t n, size_t min_chunk, const std::function<void(size_t, size_t)>& fn) {
         if (n == 0) return;
@@ -103,14 +91,12 @@ private:
             j.done.fetch_add(e - b, std::memory_order_acq_rel);
         }
     }
-    // A worker spins for spin_us_ ($VX_HOST_SPIN_US, default 0) after a job or a Prime() before it
-    // sleeps again.
+    // A worker spins for spin_us_ ($VX_HOST_SPIN_US, default 0) after a job before it sleeps again.
     void Loop() {
-        unsigned long long seen = 0, pseen = 0;
+        unsigned long long seen = 0;
         {
             std::lock_guard<std::mutex> lk(m_);
             seen = gen_.load(std::memory_order_relaxed);
-            pseen = prime_;
         }
         for (;;) {
             bool job = false;
@@ -126,11 +112,7 @@ private:
             std::shared_ptr<Job> j;
             {
                 std::unique_lock<std::mutex> lk(m_);
-                if (!job) {
-                    cv_.wait(lk, [&] { return gen_.load(std::memory_order_relaxed) != seen || prime_ != pseen; });
-                    pseen = prime_;
-                    if (gen_.load(std::memory_order_relaxed) == seen) continue;  // (a Prime(): spin)
-                }
+                if (!job) cv_.wait(lk, [&] { return gen_.load(std::memory_order_relaxed) != seen; });
                 seen = gen_.load(std::memory_order_relaxed);
                 if (stop_) return;
                 j = cur_;
@@ -144,7 +126,6 @@ private:
     std::condition_variable cv_;
     std::shared_ptr<Job> cur_;
     std::atomic<unsigned long long> gen_{0};
-    unsigned long long prime_ = 0;
     bool stop_ = false;
     int spin_us_ = 0;  // ($VX_HOST_SPIN_US: 300 measured slower on the GPU box, whose CPU quota a spinning
                        // worker eats into)
