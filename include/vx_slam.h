@@ -308,6 +308,12 @@ int vx_ba_plan_info(const vx_ba_plan* plan, int64_t* out8);
  * keyframe}.  A sharded plan runs the fused kernel only when every rank has the layout (decided by
  * one all-reduce on its first run). */
 int vx_ba_plan_layout(const vx_ba_plan* plan, int64_t* out4);
+/* 1 when the plan's runs are ONE persistent launch per window (k_ba_win: unsharded float-atomic
+ * plans whose workgroups fit on the device at once; $VX_BA_PERSIST=0 disables it), 0 when they are
+ * one launch per iteration.  A persistent run whose bounded waits ran out (its workgroups could not
+ * all be resident, e.g. another persistent window held the compute units) is re-run by
+ * vx_ba_plan_fetch with the per-iteration launches, which the plan keeps from then on. */
+int vx_ba_plan_persistent(const vx_ba_plan* plan);
 /* Test hook: the fused layout's index tables (workgroup headers, landmark slots and runs,
  * landmark-stage records, keyframe entries, landmark- and pose-stage observation sources, pose
  * codes) copied back to back into dst; *bytes = their total size (dst NULL: the size only).  The

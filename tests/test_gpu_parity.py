@@ -265,12 +265,49 @@ def test_ba_golden_gpu(ctx, case):
     assert (np.abs(mp["lm_pos"] - ref["lm_pos"]) / np.maximum(np.abs(ref["lm_pos"]), 1e-3)).max() <= BA_RTOL
 
 
+@pytest.mark.parametrize("persist", ["1", "0"])
 @pytest.mark.parametrize("cfg", ["C2", "C3", "C4", "C5"])
-def test_ba_baseline_configs(ctx, oracle, cfg):
+def test_ba_baseline_configs(ctx, oracle, monkeypatch, cfg, persist):
+    """Every BASELINE window against the restatement, with the persistent window (k_ba_win, where
+    the plan takes it) and with one launch per iteration (k_ba_iter, $VX_BA_PERSIST=0)."""
+    monkeypatch.setenv("VX_BA_PERSIST", persist)
     nk, nl, ns = synth.ba_config(cfg)
     m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=ns * 2)
     st = _ba_case(ctx, oracle, m, dict(window=nk))
     assert st.status == 0 and st.iterations >= 2
+
+
+def test_ba_window_persistent_fault_fallback(ctx, oracle, monkeypatch):
+    """k_ba_win at C3 (one launch per window), and its fault path: with one arrival that never comes
+    ($VX_BA_WIN_TEST_FAULT) every bounded wait runs out, the workgroups leave, and vx_ba_plan_fetch
+    re-runs the window with the per-iteration launches, which the plan then keeps — results against
+    the restatement both times."""
+    import vxslam
+
+    nk, nl, ns = synth.ba_config("C3")
+    m = synth.make_ba_map(0x5EED0000 + nk, nk, nl, n_streams=ns, n_old_kf=ns * 2)
+    mc = m.copy()
+    st_c = oracle.ba_optimize(mc, oracle.ba_options(window=nk))
+    opts = vxslam.default_ba_options(window=nk)
+    plan = ctx.ba_plan(m, opts)
+    assert plan.persistent()
+    for _ in range(3):  # (eager, captured, replayed: the run's parity alternates)
+        plan.run_async()
+        mg = m.copy()
+        _assert_ba_close(mg, mc, plan.fetch(mg), st_c)
+    plan.close()
+    monkeypatch.setenv("VX_BA_WIN_TEST_FAULT", "1")
+    plan = ctx.ba_plan(m, opts)
+    assert plan.persistent()
+    plan.run_async()
+    mg = m.copy()
+    st = plan.fetch(mg)
+    assert not plan.persistent()
+    _assert_ba_close(mg, mc, st, st_c)
+    plan.run_async()
+    mg = m.copy()
+    _assert_ba_close(mg, mc, plan.fetch(mg), st_c)
+    plan.close()
 
 
 def test_ba_variants(ctx, oracle):

@@ -72,7 +72,7 @@ VX_KT_TABLE();
 struct BAState {
     int active[kMaxIter + 1];  // active[it]: iteration it runs
     int iterations;
-    int pad;
+    int fault;                 // k_ba_win: a bounded wait ran out (the run is void; fetch re-runs it)
     double last_cost;
     double cost[16];
     int obs[16];
@@ -1196,6 +1196,340 @@ __global__ __launch_bounds__(kFT) void k_ba_iter(BAArgs a, FusedArgs f, int it) 
     FKT(5);
 }
 
+// ------------------------------------------------------------------ persistent window (k_ba_win)
+// The prologue and every iteration of one LocalBA window in ONE launch (round 6, VERDICT r5 #2a).
+// k_ba_iter's workgroups already exchange nothing but the keyframe rows: a workgroup solves the poses
+// of its own <= kFK keyframe entries from their rows, updates its own landmarks and adds the next
+// iteration's pose-stage terms of its landmarks' observations into those rows.  So the launch
+// boundary between iterations is replaced by point-to-point hand-offs, not a grid barrier:
+//   - iteration i's rows R_i are their own buffer (no reuse inside a run), summed by float atomics
+//     (memory side); after its atomics every wave waits for them (vmcnt(0)), the workgroup meets at a
+//     barrier, and one lane per entry adds 1 to the entry row's arrival counter cnt[i][row], one lane
+//     to done[i] (agent-scope atomics);
+//   - a workgroup solves entry row k of iteration i once cnt[i][k] reaches nprod[k] (the number of
+//     workgroups with an entry on row k, counted at plan build), polled by the entry's own lane with
+//     sc1 loads, and reads the row with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1: atomic
+//     producer, sc1-polled counter, sc1 payload loads; no line of R_i is in any cache before it is
+//     complete: fresh buffers, kernel-start invalidate);
+//   - the stop rule of iteration i - 1 (whether iteration i runs) needs every row of R_(i-1): wave 1
+//     polls done[i - 1] == workgroups (one iteration of slack: almost always already true), sums the
+//     rows' cost / count terms in a fixed order and decides — every workgroup the same, from the
+//     same values; workgroup 0 writes the run's statistics.
+// Everything a workgroup loads that no iteration changes (block / entry records, landmark-stage
+// observations, the landmarks' slots and runs, the first pose-stage round) is loaded once; the
+// entries' poses and the landmark positions stay in registers / LDS.  Buffers by run parity (the
+// run's generation, w.gen): a run zeroes the other parity's rows and counters for the next run (plain
+// stores, written back at the kernel's end).  Every workgroup must be resident at once (nb <= CUs,
+// one 512-thread workgroup per CU); every wait is bounded (kWinSpinTicks): a wait that runs out sets
+// the state's fault flag, every workgroup leaves, and vx_ba_plan_fetch re-runs the window with the
+// per-iteration launches (plan->win_off) — two persistent windows on one device at once could
+// otherwise hold each other's compute units.
+struct WinArgs {
+    double* rows;      // [2][max_iter][n_kf][kStride]
+    int* cnt;          // [2][max_iter][n_kf] arrivals per row
+    int* done;         // [2][max_iter][32] workgroups done with iteration i's pose stage (own lines)
+    const int* nprod;  // [n_kf] workgroups with an entry on the row
+    int* gen;          // run generation (parity = gen & 1), bumped by workgroup 0 at the run's end
+    int* fault;        // set when a wait ran out (every workgroup then leaves)
+};
+constexpr long long kWinSpinTicks = 20'000'000;  // 200 ms of the 100 MHz wall clock
+
+__device__ __forceinline__ int ld_sc1(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void add_agent(int* p, int v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// lanes with want: spin until *p >= target (each lane its own counter); false when the wait ran out
+// or another workgroup reported a fault
+__device__ __forceinline__ bool win_wait(const int* p, int target, bool want, int* fault) {
+    const long long t0 = wall_clock64();
+    bool ok = true;
+    __builtin_amdgcn_s_setprio(0);  // (a polling wave leaves the SIMD to co-resident waves)
+    for (int k = 0;; ++k) {
+        const bool pend = want && ok && ld_sc1(p) < target;
+        if (!__any(pend)) break;
+        if ((k & 15) == 15) {
+            if (ld_sc1(fault) || wall_clock64() - t0 > kWinSpinTicks) {
+                if (pend) ok = false;
+                if ((threadIdx.x & 63) == 0) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_s_setprio(3);
+    return __all(ok);
+}
+
+template <int kFT>
+__global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w) {
+    constexpr int kFW = kFT / 64;
+    static_assert(kFW >= 2, "k_ba_win: wave 1 runs the stop rule");
+    __builtin_amdgcn_s_setprio(3);
+    extern __shared__ __attribute__((aligned(16))) double fl[];
+    __shared__ int4 s_ke[kFK];
+    __shared__ int s_act, s_fault;
+    double* kslot = fl;                                  // [kFK][kLdsStride]
+    double* terms = kslot + kFK * kLdsStride;            // [9][kFT]
+    int* tcount = reinterpret_cast<int*>(terms + 9 * kFT);
+    double* lpos = terms + 9 * kFT + kFT / 2;            // [kFT][3]
+    const int tid = threadIdx.x, b = blockIdx.x, wv = tid >> 6, lane = tid & 63;
+    const size_t base = (size_t)b * kFT;
+    const int4* KE = f.kent + (size_t)b * kFK * 2;
+    const int M = a.max_iter, nk = a.n_kf, nb = (int)gridDim.x;
+    const size_t rows_per = (size_t)M * nk * kStride;
+    // ---- loads: the run generation, then everything the window keeps (k_ba_iter's prologue loads
+    // plus the landmark-stage records its iteration launches load again and again)
+    const int par = w.gen[0] & 1;
+    double* const R = w.rows + (size_t)par * rows_per;
+    int* const cnt = w.cnt + (size_t)par * M * nk;
+    int* const done = w.done + (size_t)par * M * 32;
+    const int wvu = __builtin_amdgcn_readfirstlane(wv);
+    const int4 B = f.blk[(size_t)b * (1 + kFW / 2)];
+    const int4 WB = f.blk[(size_t)b * (1 + kFW / 2) + 1 + (wvu >> 1)];
+    int4 ke = make_int4(-1, 0, 0, 0);
+    if (tid < kFK) ke = KE[2 * tid];
+    const int4 orec = f.lobs_rec[base + tid];
+    const double2 ouv = f.lobs_uv[base + tid];
+    int lslot = f.lm_slot[base + tid];
+    const int2 run = f.lm_run[base + tid];
+    D3 PL;
+    {
+        const double* P = a.lm_pos0 + 4 * (size_t)lslot;
+        PL = {P[0], P[1], P[2]};
+    }
+    const int wstart = (wvu & 1) ? WB.z : WB.x, wrounds = (wvu & 1) ? WB.w : WB.y;
+    // (each wave's first pose-stage round, requested again before every pose stage: kept in
+    // registers across the loop it would cost the registers the landmark stage needs)
+    double2 u0 = make_double2(0, 0);
+    double4 p0 = make_double4(0, 0, 0, 0);
+    auto first_round = [&] {
+        if (wrounds > 0) {
+            u0 = f.pobs_uv[wstart + lane];
+            p0 = f.pobs_p[wstart + lane];
+        }
+    };
+    first_round();
+    // the entry's state lives in its LDS slot (T 8 | R 9 | C 4 | flags), not in registers
+    double ev[13];
+    int np = 0;
+    const int row = ke.x & 0x3fffffff;
+    if (tid < kFK && ke.x >= 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ev[j] = a.kf_pose0[8 * (size_t)row + j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ev[8 + j] = a.kf_intr[4 * row + j];
+        ev[12] = (double)a.kf_flags[row];
+        np = w.nprod[row];
+    }
+    // the next run's buffers (the other parity) zeroed; its rows were last read by the previous run
+    {
+        double* Ro = w.rows + (size_t)(par ^ 1) * rows_per;
+        for (size_t i = (size_t)b * kFT + tid; i < rows_per; i += (size_t)nb * kFT) Ro[i] = 0.0;
+        int* co = w.cnt + (size_t)(par ^ 1) * M * nk;
+        for (int i = b * kFT + tid; i < M * nk; i += nb * kFT) co[i] = 0;
+        int* dn = w.done + (size_t)(par ^ 1) * M * 32;
+        for (int i = b * kFT + tid; i < M * 32; i += nb * kFT) dn[i] = 0;
+    }
+    if (b == 0 && tid < 16) {  // (the statistics of this run, as stop_rule(0) starts them)
+        a.state->cost[tid] = 0.0;
+        a.state->obs[tid] = 0;
+    }
+    const int n_lm = B.x, n_ob = B.y, n_ent = B.z;
+    const bool has_o = tid < n_ob, own = tid < n_lm;
+    lpos[3 * tid] = PL.x;
+    lpos[3 * tid + 1] = PL.y;
+    lpos[3 * tid + 2] = PL.z;
+    if (tid < kFK) s_ke[tid] = ke;
+    if (tid == 0) s_fault = 0;
+    if (tid < kFK && ke.x >= 0) {  // iteration 0's pose stage reads the initial poses
+        double Rm[9];
+        rot_from_quat(ev, Rm);
+        double* sl = kslot + tid * kLdsStride;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sl[j] = ev[j];
+#pragma unroll
+        for (int j = 0; j < 9; ++j) sl[8 + j] = Rm[j];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sl[17 + j] = ev[8 + j];
+        sl[21] = ev[12];
+    }
+    __syncthreads();
+
+    // ---- pose stage of iteration `itn` from the poses in kslot and the landmarks in lpos, added into
+    // R_itn; then the hand-off (every wave's atomics retired, barrier, one arrival per entry row)
+    auto pose_stage = [&](int itn) {
+        int r = 0;
+        double* const Rn = R + (size_t)itn * nk * kStride;
+        for (int j = wv; j < n_ent; j += kFW) {
+            const int4 e = s_ke[j];
+            const int nr = (e.w - e.z + 63) >> 6;
+            if (nr == 0) continue;
+            const double* T = kslot + j * kLdsStride;
+            const double* Rr = T + 8;
+            const double* C = T + 17;
+            double v[kStride];
+#pragma unroll
+            for (int t = 0; t < kStride; ++t) v[t] = 0.0;
+            for (int q = 0; q < nr; ++q, ++r) {
+                const double2 uv = u0;
+                const double4 P4 = p0;
+                if (r + 1 < wrounds) {
+                    int lim = e.w - (e.z + 64 * (q + 1));
+                    if (q + 1 >= nr) {  // the wave's next entry with rounds
+                        int jn = j + kFW;
+                        int4 en = s_ke[jn < kFK ? jn : j];
+                        while (jn < n_ent && ((en.w - en.z + 63) >> 6) == 0) {
+                            jn += kFW;
+                            en = s_ke[jn < kFK ? jn : j];
+                        }
+                        lim = en.w - en.z;
+                    }
+                    if (lane < lim) {
+                        u0 = f.pobs_uv[wstart + 64 * (r + 1) + lane];
+                        p0 = f.pobs_p[wstart + 64 * (r + 1) + lane];
+                    } else {
+                        u0 = make_double2(0.0, 0.0);
+                        p0 = make_double4(0.0, 0.0, 0.0, 0.0);
+                    }
+                }
+                const bool valid = e.z + 64 * q + lane < e.w;
+                const int code = (int)P4.w;
+                const D3 P = code >= 0 ? D3{lpos[3 * code], lpos[3 * code + 1], lpos[3 * code + 2]} : D3{P4.x, P4.y, P4.z};
+                pose_obs_accum<true>(a, T, Rr, C, P, uv, v, valid);
+            }
+            const double tot = wave_sum32(v);
+            if ((lane & 1) == 0 && (lane >> 1) < kNTerms)
+                unsafeAtomicAdd(Rn + (size_t)(e.x & 0x3fffffff) * kStride + (lane >> 1), tot);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's adds are done at the memory side)
+        __syncthreads();
+        if (tid < kFK && ke.x >= 0) add_agent(cnt + (size_t)itn * nk + row, 1);
+        if (tid == kFK) add_agent(done + (size_t)itn * 32, 1);
+    };
+    // ---- stop rule of iteration ip (local_ba.cpp:240-247) from every row of R_ip, by wave 1 of every
+    // workgroup (the same values summed in the same order: the same decision everywhere)
+    double last = 1.7976931348623157e308;
+    auto decide = [&](int ip) -> int {
+        if (!win_wait(done + (size_t)ip * 32, nb, lane == 0, w.fault)) return -1;
+        double tot = 0.0, cn = 0.0;
+        for (int q = lane; q < nk; q += 64) {
+            tot += ld_sc1(R + ((size_t)ip * nk + q) * kStride + 27);
+            cn += ld_sc1(R + ((size_t)ip * nk + q) * kStride + 28);
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) {
+            tot += __shfl_xor(tot, m, 64);
+            cn += __shfl_xor(cn, m, 64);
+        }
+        const int tobs = (int)cn;
+        const bool stop = tobs == 0 || fabs(last - tot) < 1e-6 * last;
+        if (!stop) last = tot;
+        if (b == 0 && lane == 0) {
+            BAState* s = a.state;
+            if (ip < 16) {
+                s->cost[ip] = tot;
+                s->obs[ip] = tobs;
+            }
+            s->iterations = ip + 1;
+            s->last_cost = last;
+            if (!stop && ip + 1 < M)
+                s->active[ip + 1] = 1;
+            else
+                for (int k = ip + 1; k <= M; ++k) s->active[k] = 0;
+        }
+        return stop ? 0 : 1;
+    };
+
+    pose_stage(0);  // (iteration 0's pose stage: k_ba_iter's prologue)
+    for (int it = 0; it < M; ++it) {
+        // ---- A: wave 0 waits for its entries' rows of R_it, reads and solves them; wave 1 decides
+        // whether iteration it runs (the stop rule of it - 1)
+        if (wv == 0) {
+            const bool want = tid < kFK && ke.x >= 0;
+            const bool ok = win_wait(cnt + (size_t)it * nk + row, np, want, w.fault);
+            if (!ok && lane == 0) s_fault = 1;
+            if (want && ok) {
+                double S[kNTerms];
+                const double* rp = R + ((size_t)it * nk + row) * kStride;
+#pragma unroll
+                for (int t = 0; t < kNTerms; ++t) S[t] = ld_sc1(rp + t);
+                double* sl = kslot + tid * kLdsStride;
+                double T[8], Rm[9];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) T[j] = sl[j];
+                solve_pose(a, (int)sl[21], S, T, Rm);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) sl[j] = T[j];
+#pragma unroll
+                for (int j = 0; j < 9; ++j) sl[8 + j] = Rm[j];
+            }
+        } else if (wv == 1) {
+            const int act = it == 0 ? 1 : decide(it - 1);
+            if (lane == 0) {
+                s_act = act > 0;
+                if (act < 0) s_fault = 1;
+            }
+        }
+        __syncthreads();
+        if (s_fault || !s_act) break;
+        if (tid < kFK && ke.x >= 0 && (ke.x & (1 << 30))) {  // the owner publishes the pose
+            double* Tout = pose_out(a, it) + 8 * (size_t)row;
+            const double* sl = kslot + tid * kLdsStride;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) Tout[j] = sl[j];
+        }
+        if (it + 1 < M) first_round();
+        // ---- landmark stage of iteration it (local_ba.cpp:176-238), as k_ba_iter
+        {
+            double h[9];
+            const D3 PO{lpos[3 * orec.y], lpos[3 * orec.y + 1], lpos[3 * orec.y + 2]};
+            const bool ok = obs_terms<true>(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride, kslot + 17,
+                                            kLdsStride, h);
+#pragma unroll
+            for (int j = 0; j < 9; ++j) terms[j * kFT + tid] = h[j];
+            tcount[tid] = (has_o && ok) ? 1 : 0;
+            __syncthreads();
+            if (own) {
+                double hs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+                int obs = 0;
+                for (int q = run.x; q < run.y; ++q) {
+#pragma unroll
+                    for (int j = 0; j < 9; ++j) hs[j] += terms[j * kFT + q];
+                    obs += tcount[q];
+                }
+                PL = lm_update(a, lslot, PL, hs, obs);
+                lpos[3 * tid] = PL.x;
+                lpos[3 * tid + 1] = PL.y;
+                lpos[3 * tid + 2] = PL.z;
+            }
+            __syncthreads();
+        }
+        if (it + 1 < M) pose_stage(it + 1);
+    }
+    // ---- the last iteration's statistics (a stop inside the loop wrote them), then the next run's
+    // parity; workgroup 0 gets here only after every workgroup's first arrival (its waits above), so
+    // every workgroup has read the generation
+    if (b == 0 && wv == 1 && !s_fault && s_act) {
+        const int r = decide(M - 1);
+        if (r < 0 && lane == 0) s_fault = 1;
+    }
+    if (b == 0 && wv == 1 && lane == 0 && !s_fault) w.gen[0] = w.gen[0] + 1;
+}
+
+// plan build: nprod[row] = workgroups with an entry on the row (the arrivals k_ba_win waits for)
+// (bias: $VX_BA_WIN_TEST_FAULT=1 adds one arrival to row 0 that never comes, so the run's waits run
+// out: the test of the fault path, tests/test_gpu_parity.py)
+__global__ void k_win_nprod(const int4* kent, int nb, int* nprod, int bias) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nb * kFK) return;
+    const int x = kent[2 * (size_t)i].x;
+    if (x >= 0) atomicAdd(nprod + (x & 0x3fffffff), 1);
+    if (i == 0) atomicAdd(nprod, bias);
+}
+
 // sharded plans: each keyframe row's partial slots summed in slot order (the slots of a row no group
 // fills are 0) -> rowpart, which the per-iteration all-reduce then sums over the ranks
 __global__ void k_row_sum(const double* part, int n_kf, int maxl, double* rowpart) {
@@ -1332,6 +1666,8 @@ int alloc_run_buffers(vx_ctx* c, vx_ba_plan* p) {
     VX_HIP(c, p->kf_cost.ensure(nk * 2 * sizeof(double)));
     VX_HIP(c, p->lm_pos.ensure((size_t)std::max(p->n_lm, 1) * 4 * sizeof(double)));
     VX_HIP(c, p->state.ensure(sizeof(BAState)));
+    // (the fault word is read by every fetch; a recycled state block may hold anything)
+    VX_HIP(c, hipMemsetAsync(p->state.p, 0, sizeof(BAState), c->stream));
     return VX_OK;
 }
 
@@ -1383,6 +1719,13 @@ bool fused_eligible(const vx_ba_plan* p) {
     if (const char* e = getenv("VX_BA_FUSED"))
         if (e[0] == '0') return false;
     return true;
+}
+
+// $VX_BA_PERSIST=0: the fused LocalBA as one launch per iteration (k_ba_iter) instead of the
+// persistent window (k_ba_win; read at plan build)
+bool ba_persist() {
+    const char* e = getenv("VX_BA_PERSIST");
+    return !(e && e[0] == '0');
 }
 
 // $VX_BA_ATOMIC_ROWS=0: the fused LocalBA's per-keyframe partial slots (every run bitwise the
@@ -1455,6 +1798,34 @@ int fused_finish(vx_ctx* c, vx_ba_plan* p, int nb, int ft, int maxl, size_t n_pp
         const size_t ab = 4 * (size_t)p->n_kf * kStride * sizeof(double);
         VX_HIP(c, p->f_arow.ensure(ab));
         VX_HIP(c, hipMemsetAsync(p->f_arow.p, 0, ab, c->stream));
+    }
+    // persistent window (k_ba_win): unsharded atomic-row plans of 512-thread workgroups that are all
+    // resident at once (one per CU); $VX_BA_PERSIST=0 keeps the per-iteration launches
+    p->f_persist = false;
+    p->win_off = false;
+    if (!c->n_cus) c->n_cus = std::max(vx_device_cus(c->device), 1);
+    if (p->f_atomic && ft == kFTSmall && nb <= c->n_cus && p->opt.max_iterations >= 1 &&
+        p->opt.max_iterations <= kMaxIter && ba_persist()) {
+        const size_t M = (size_t)p->opt.max_iterations, nk = (size_t)p->n_kf;
+        size_t at = 0;
+        auto take = [&](size_t bytes) {
+            const size_t o = at;
+            at += (bytes + 255) & ~(size_t)255;
+            return o;
+        };
+        p->win_rows_off = take(2 * M * nk * kStride * sizeof(double));
+        p->win_cnt_off = take(2 * M * nk * sizeof(int));
+        p->win_done_off = take(2 * M * 32 * sizeof(int));
+        p->win_nprod_off = take(nk * sizeof(int));
+        p->win_gen_off = take(sizeof(int));
+        VX_HIP(c, p->f_win.ensure(at));
+        VX_HIP(c, hipMemsetAsync(p->f_win.p, 0, at, c->stream));
+        hipLaunchKernelGGL(k_win_nprod, dim3((unsigned)((nb * kFK + 255) / 256)), dim3(256), 0, c->stream,
+                           reinterpret_cast<const int4*>(T + F.kent), nb,
+                           reinterpret_cast<int*>(p->f_win.as<uint8_t>() + p->win_nprod_off),
+                           getenv("VX_BA_WIN_TEST_FAULT") ? 1 : 0);
+        VX_LAUNCH_CHECK(c, "k_win_nprod");
+        p->f_persist = true;
     }
     p->f_stop_b = stop_b;
     p->f_blocks = nb;
@@ -2027,14 +2398,36 @@ int fused_row_sum(vx_ctx* c, vx_ba_plan* p, int it) {
     return VX_OK;
 }
 
+WinArgs make_win_args(vx_ba_plan* p) {
+    uint8_t* W = p->f_win.as<uint8_t>();
+    WinArgs w{};
+    w.rows = reinterpret_cast<double*>(W + p->win_rows_off);
+    w.cnt = reinterpret_cast<int*>(W + p->win_cnt_off);
+    w.done = reinterpret_cast<int*>(W + p->win_done_off);
+    w.nprod = reinterpret_cast<const int*>(W + p->win_nprod_off);
+    w.gen = reinterpret_cast<int*>(W + p->win_gen_off);
+    w.fault = reinterpret_cast<int*>(p->state.as<uint8_t>() + offsetof(BAState, fault));
+    return w;
+}
+
+bool win_active(const vx_ba_plan* p) { return p->fused && p->f_persist && !p->win_off && p->shard_count <= 1; }
+
 // the fused path: prologue (iteration 0's pose stage) + one k_ba_iter per iteration (sharded: each
-// preceded by the row sums and their all-reduce)
+// preceded by the row sums and their all-reduce), or the whole window as one k_ba_win launch
 int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
     const BAArgs a = make_args(p);
     const FusedArgs f = make_fused_args(p);
     int rc;
     if ((rc = reset_if_no_iterations(c, p, a))) return rc;
     if (p->opt.max_iterations == 0) return VX_OK;
+    if (win_active(p)) {
+        constexpr int lds = (int)fused_lds(kFTSmall);
+        static std::atomic<uint64_t> dw{0};
+        VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_ba_win<kFTSmall>), lds, dw));
+        VX_HIP(c, launch(c, kStBaWin, k_ba_win<kFTSmall>, dim3(p->f_blocks), dim3(kFTSmall), (uint32_t)lds, c->stream,
+                         a, f, make_win_args(p)));
+        return VX_OK;
+    }
     if ((rc = fused_launch(c, p, a, f, -1))) return rc;
     for (int it = 0; it < p->opt.max_iterations; ++it) {
         if (p->shard_count > 1) {
@@ -2397,6 +2790,18 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
         std::vector<double> pose((size_t)p->n_kf * 8), lm((size_t)std::max(p->n_opt, 1) * 4);
         VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
         VX_HIP(c, hipStreamSynchronize(c->stream));
+        if (hs.fault && win_active(p)) {
+            // a persistent window whose wait ran out (its workgroups could not all be resident at
+            // once): the run is void; the plan keeps the per-iteration launches from now on and
+            // runs the window again
+            p->win_off = true;
+            p->graph.reset();
+            VX_HIP(c, hipMemsetAsync(p->state.as<uint8_t>() + offsetof(BAState, fault), 0, sizeof(int), c->stream));
+            int rc = plan_run(c, p);
+            if (rc) return rc;
+            VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
+            VX_HIP(c, hipStreamSynchronize(c->stream));
+        }
         // the poses of the last iteration run are in ping-pong buffer (iterations & 1)
         const double* fin = p->kf_pose.as<double>() + (size_t)(hs.iterations & 1) * p->n_kf * 8;
         VX_HIP(c, hipMemcpyAsync(pose.data(), fin, pose.size() * sizeof(double), hipMemcpyDeviceToHost,
@@ -2494,6 +2899,8 @@ int vx_ba_plan_layout(const vx_ba_plan* p, int64_t* out4) {
     out4[3] = p->fused ? p->f_maxl : 0;
     return VX_OK;
 }
+
+int vx_ba_plan_persistent(const vx_ba_plan* p) { return p && win_active(p) ? 1 : 0; }
 
 int vx_ba_plan_fused_tables(vx_ctx* c, const vx_ba_plan* p, void* dst, size_t cap, size_t* bytes) {
     if (!c || !p || !bytes || p->c != c) return VX_ERR_INVALID;

@@ -171,7 +171,8 @@ static const char* kStageNames[vx::kStCount] = {
     "ba_pose_sum",    "ba_allreduce",  "ba_pose_solve",   "ba_landmark",    "orb_pyramid",
     "sba_landmark",   "sba_blocks",    "sba_solve",       "sba_update",     "sba_allreduce",
     "lm_depth",       "lm_triangulate", "lm_compact",  "pnp_hypotheses", "pnp_refine",
-    "em_hypotheses",  "em_select",     "ba_iter",         "ba_prologue"};
+    "em_hypotheses",  "em_select",     "ba_iter",         "ba_prologue",
+    "ba_window"};
 
 extern "C" {
 

@@ -65,6 +65,7 @@ enum Stage : int {
     kStEmSelect,
     kStBaIter,        // fused LocalBA iteration (k_ba_iter)
     kStBaPrologue,    // iteration 0's pose stage of the fused path
+    kStBaWin,         // the whole LocalBA window in one persistent launch (k_ba_win)
     kStCount
 };
 

@@ -82,7 +82,7 @@ EXPORTS = [
     "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
     "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
     "vx_match_device_async", "vx_match_fetch", "vx_ba_default_options", "vx_ba_optimize_map", "vx_ba_plan_create",
-    "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info", "vx_ba_plan_layout", "vx_ba_plan_fused_tables",
+    "vx_ba_plan_run_async", "vx_ba_plan_fetch", "vx_ba_plan_destroy", "vx_ba_plan_info", "vx_ba_plan_layout", "vx_ba_plan_persistent", "vx_ba_plan_fused_tables",
     "vx_ba_plan_inspect", "vx_ba_shard_of", "vx_comm_unique_id", "vx_comm_init", "vx_comm_info", "vx_prof_enable", "vx_prof_count", "vx_prof_name",
     "vx_prof_read", "vx_sba_default_options", "vx_sba_plan_create", "vx_sba_plan_run_async",
     "vx_sba_plan_fetch", "vx_sba_plan_destroy", "vx_sba_plan_info", "vx_sba_plan_system",
@@ -726,6 +726,10 @@ class BAPlan:
         out = np.zeros(4, np.int64)
         self.ctx._check(lib().vx_ba_plan_layout(self._h, _p(out)))
         return {k: int(v) for k, v in zip(["fused", "threads", "workgroups", "max_slots"], out)}
+
+    def persistent(self) -> bool:
+        """vx_ba_plan_persistent: runs are one persistent k_ba_win launch per window."""
+        return bool(lib().vx_ba_plan_persistent(self._h))
 
     def fused_tables(self) -> bytes:
         """vx_ba_plan_fused_tables: the fused layout's index tables, back to back (test hook)."""
