@@ -38,7 +38,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HIP_KERNEL = {"orb_pyramid": "k_pyramid", "orb_fast_harris": "k_fast", "orb_select": "k_select_stl",
               "orb_blur": "k_blur", "orb_describe": "k_describe", "match_partial": "k_knn_rows",
               "match_merge": "k_knn_compact", "ba_pose_partial": "k_pose_kf",
-              "ba_landmark": "k_landmark_solve", "ba_iter": "k_ba_iter", "ba_prologue": "k_ba_iter"}
+              "ba_landmark": "k_landmark_solve", "ba_iter": "k_ba_iter", "ba_prologue": "k_ba_iter",
+              "ba_window": "k_ba_win"}
 
 CONFIGS = {
     # name: (height, width, n_features, n_kf, n_lm)
@@ -138,6 +139,8 @@ def stage_bytes(stage, geo, counts):
                 counts["n_kf"] * 320)
     if stage == "ba_prologue":  # iteration 0's pose stage
         return counts["n_pose_obs"] * 44 + counts["n_kf"] * (56 + 32 + 232)
+    if stage == "ba_window":    # k_ba_win: the prologue + the iterations the window ran, one launch
+        return stage_bytes("ba_prologue", geo, counts) + counts["ba_iters"] * stage_bytes("ba_iter", geo, counts)
     return None
 
 
@@ -154,6 +157,8 @@ def stage_flops(stage, counts):
         lm = stage == "ba_iter"
         return (132 * counts["n_pose_obs"] + (80 * counts["n_lm_obs"] + 50 * counts["n_opt"] if lm else 0) +
                 400 * counts["n_kf"])
+    if stage == "ba_window":
+        return stage_flops("ba_prologue", counts) + counts["ba_iters"] * stage_flops("ba_iter", counts)
     return None
 
 
@@ -1187,7 +1192,8 @@ def main():
     counts = {"n_kp": len(kps), "n_cand": measured_candidates(vxslam, frames_host[last % args.frames], params),
               "n_q": len(kps), "n_t": len(kps),
               "n_match": len(matches), "n_pose_obs": info["n_pose_obs"], "n_lm_obs": info["n_lm_obs"],
-              "n_split": info["n_split"], "n_opt": info["n_opt"], "n_kf": info["n_kf"]}
+              "n_split": info["n_split"], "n_opt": info["n_opt"], "n_kf": info["n_kf"],
+              "ba_iters": int(st.iterations)}
 
     frames_total = args.steps * F * N
     ms_per_step = 1e3 * elapsed / args.steps

@@ -1231,8 +1231,15 @@ struct WinArgs {
     const int* nprod;  // [n_kf] workgroups with an entry on the row
     int* gen;          // run generation (parity = gen & 1), bumped by workgroup 0 at the run's end
     int* fault;        // set when a wait ran out (every workgroup then leaves)
+    int wsig;          // hand-off wave by wave ($VX_BA_WIN_WSIG=1) or after a workgroup barrier (default)
+    int naps;          // s_sleep 1 between a row poll's loads ($VX_BA_WIN_NAPS, default 1)
 };
 constexpr long long kWinSpinTicks = 20'000'000;  // 200 ms of the 100 MHz wall clock
+// k_ba_win's LDS: k_ba_iter's plus a second set of pose slots
+constexpr size_t win_lds(int ft) {
+    return fused_lds(ft) + (size_t)kFK * kLdsStride * sizeof(double) + (size_t)ft * (16 + 16 + 12);
+}
+static_assert(win_lds(kFTSmall) <= 160 * 1024, "k_ba_win LDS exceeds gfx950's 160 KB per workgroup");
 
 __device__ __forceinline__ int ld_sc1(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 __device__ __forceinline__ double ld_sc1(const double* p) {
@@ -1243,7 +1250,7 @@ __device__ __forceinline__ void add_agent(int* p, int v) {
 }
 // lanes with want: spin until *p >= target (each lane its own counter); false when the wait ran out
 // or another workgroup reported a fault
-__device__ __forceinline__ bool win_wait(const int* p, int target, bool want, int* fault) {
+__device__ __forceinline__ bool win_wait(const int* p, int target, bool want, int* fault, int naps = 1) {
     const long long t0 = wall_clock64();
     bool ok = true;
     __builtin_amdgcn_s_setprio(0);  // (a polling wave leaves the SIMD to co-resident waves)
@@ -1257,7 +1264,7 @@ __device__ __forceinline__ bool win_wait(const int* p, int target, bool want, in
                 break;
             }
         }
-        __builtin_amdgcn_s_sleep(1);
+        for (int z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(1);
     }
     __builtin_amdgcn_s_setprio(3);
     return __all(ok);
@@ -1270,11 +1277,19 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
     __builtin_amdgcn_s_setprio(3);
     extern __shared__ __attribute__((aligned(16))) double fl[];
     __shared__ int4 s_ke[kFK];
-    __shared__ int s_act, s_fault;
-    double* kslot = fl;                                  // [kFK][kLdsStride]
-    double* terms = kslot + kFK * kLdsStride;            // [9][kFT]
+    __shared__ int s_act, s_fault, s_waves;
+    // two pose-slot sets (T 8 | R 9 | C 4 | flags per entry): iteration it solves from set (it - 1) & 1
+    // into set it & 1, so a wave still in the previous pose stage (no barrier closes it) reads poses
+    // the solve does not overwrite
+    double* const ks0 = fl;                              // [2][kFK][kLdsStride]
+    double* terms = ks0 + 2 * kFK * kLdsStride;          // [9][kFT]
     int* tcount = reinterpret_cast<int*>(terms + 9 * kFT);
     double* lpos = terms + 9 * kFT + kFT / 2;            // [kFT][3]
+    // the landmark stage's per-thread records, loop-invariant: parked in LDS, not in registers
+    // (k_ba_win keeps far more state live across its loop than one k_ba_iter launch)
+    int4* s_orec = reinterpret_cast<int4*>(lpos + 3 * kFT);      // [kFT]
+    double2* s_ouv = reinterpret_cast<double2*>(s_orec + kFT);    // [kFT]
+    int* s_run = reinterpret_cast<int*>(s_ouv + kFT);             // [kFT][3]: r0, r1, slot
     const int tid = threadIdx.x, b = blockIdx.x, wv = tid >> 6, lane = tid & 63;
     const size_t base = (size_t)b * kFT;
     const int4* KE = f.kent + (size_t)b * kFK * 2;
@@ -1291,13 +1306,13 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
     const int4 WB = f.blk[(size_t)b * (1 + kFW / 2) + 1 + (wvu >> 1)];
     int4 ke = make_int4(-1, 0, 0, 0);
     if (tid < kFK) ke = KE[2 * tid];
-    const int4 orec = f.lobs_rec[base + tid];
-    const double2 ouv = f.lobs_uv[base + tid];
-    int lslot = f.lm_slot[base + tid];
-    const int2 run = f.lm_run[base + tid];
+    const int4 orec0 = f.lobs_rec[base + tid];
+    const double2 ouv0 = f.lobs_uv[base + tid];
+    const int lslot0 = f.lm_slot[base + tid];
+    const int2 run0 = f.lm_run[base + tid];
     D3 PL;
     {
-        const double* P = a.lm_pos0 + 4 * (size_t)lslot;
+        const double* P = a.lm_pos0 + 4 * (size_t)lslot0;
         PL = {P[0], P[1], P[2]};
     }
     const int wstart = (wvu & 1) ? WB.z : WB.x, wrounds = (wvu & 1) ? WB.w : WB.y;
@@ -1342,27 +1357,39 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
     lpos[3 * tid] = PL.x;
     lpos[3 * tid + 1] = PL.y;
     lpos[3 * tid + 2] = PL.z;
+    s_orec[tid] = orec0;
+    s_ouv[tid] = ouv0;
+    s_run[3 * tid] = run0.x;
+    s_run[3 * tid + 1] = run0.y;
+    s_run[3 * tid + 2] = lslot0;
     if (tid < kFK) s_ke[tid] = ke;
-    if (tid == 0) s_fault = 0;
-    if (tid < kFK && ke.x >= 0) {  // iteration 0's pose stage reads the initial poses
+    if (tid == 0) {
+        s_fault = 0;
+        s_waves = 0;
+    }
+    if (tid < kFK && ke.x >= 0) {  // iteration 0's pose stage reads the initial poses (set 1)
         double Rm[9];
         rot_from_quat(ev, Rm);
-        double* sl = kslot + tid * kLdsStride;
+        double* sl = ks0 + (kFK + tid) * kLdsStride;
+        double* sl0 = ks0 + tid * kLdsStride;
 #pragma unroll
         for (int j = 0; j < 8; ++j) sl[j] = ev[j];
 #pragma unroll
         for (int j = 0; j < 9; ++j) sl[8 + j] = Rm[j];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sl[17 + j] = ev[8 + j];
-        sl[21] = ev[12];
+        for (int j = 0; j < 4; ++j) sl[17 + j] = sl0[17 + j] = ev[8 + j];
+        sl[21] = sl0[21] = ev[12];
     }
     __syncthreads();
 
-    // ---- pose stage of iteration `itn` from the poses in kslot and the landmarks in lpos, added into
-    // R_itn; then the hand-off (every wave's atomics retired, barrier, one arrival per entry row)
+    // ---- pose stage of iteration `itn` from the poses in set (itn - 1) & 1 and the landmarks in lpos,
+    // added into R_itn; then the hand-off, wave by wave: an entry's terms come from one wave, so once
+    // that wave's atomics have retired (vmcnt(0)) it signals its own entries' rows — no barrier, the
+    // wave does not wait for the workgroup's slowest wave
     auto pose_stage = [&](int itn) {
         int r = 0;
         double* const Rn = R + (size_t)itn * nk * kStride;
+        const double* const kslot = ks0 + ((itn - 1) & 1) * kFK * kLdsStride;
         for (int j = wv; j < n_ent; j += kFW) {
             const int4 e = s_ke[j];
             const int nr = (e.w - e.z + 63) >> 6;
@@ -1405,9 +1432,20 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
                 unsafeAtomicAdd(Rn + (size_t)(e.x & 0x3fffffff) * kStride + (lane >> 1), tot);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's adds are done at the memory side)
-        __syncthreads();
-        if (tid < kFK && ke.x >= 0) add_agent(cnt + (size_t)itn * nk + row, 1);
-        if (tid == kFK) add_agent(done + (size_t)itn * 32, 1);
+        if (w.wsig) {
+            const int jl = wv + kFW * lane;  // lane l signals the wave's l-th entry
+            if (jl < n_ent) {
+                const int x = s_ke[jl].x;
+                if (x >= 0) add_agent(cnt + (size_t)itn * nk + (x & 0x3fffffff), 1);
+            }
+            // done[itn]: one arrival per workgroup, by its last wave (a monotonic LDS count: 8 arrivals
+            // per workgroup on one global word would serialise ~1000 atomics there per iteration)
+            if (lane == 0 && atomicAdd(&s_waves, 1) == (itn + 1) * kFW - 1) add_agent(done + (size_t)itn * 32, 1);
+        } else {  // (the workgroup's barrier, then one lane per entry)
+            __syncthreads();
+            if (tid < kFK && ke.x >= 0) add_agent(cnt + (size_t)itn * nk + row, 1);
+            if (tid == kFK) add_agent(done + (size_t)itn * 32, 1);
+        }
     };
     // ---- stop rule of iteration ip (local_ba.cpp:240-247) from every row of R_ip, by wave 1 of every
     // workgroup (the same values summed in the same order: the same decision everywhere)
@@ -1443,13 +1481,18 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
         return stop ? 0 : 1;
     };
 
+    VX_KT(0);
     pose_stage(0);  // (iteration 0's pose stage: k_ba_iter's prologue)
+    if (wv == 0) VX_KT(15);
     for (int it = 0; it < M; ++it) {
+        double* const kslot = ks0 + (it & 1) * kFK * kLdsStride;
+        const double* const kprev = ks0 + ((it + 1) & 1) * kFK * kLdsStride;
         // ---- A: wave 0 waits for its entries' rows of R_it, reads and solves them; wave 1 decides
         // whether iteration it runs (the stop rule of it - 1)
         if (wv == 0) {
             const bool want = tid < kFK && ke.x >= 0;
-            const bool ok = win_wait(cnt + (size_t)it * nk + row, np, want, w.fault);
+            const bool ok = win_wait(cnt + (size_t)it * nk + row, np, want, w.fault, w.naps);
+            if (it < 5) VX_KT(1 + 3 * it);
             if (!ok && lane == 0) s_fault = 1;
             if (want && ok) {
                 double S[kNTerms];
@@ -1457,10 +1500,11 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
 #pragma unroll
                 for (int t = 0; t < kNTerms; ++t) S[t] = ld_sc1(rp + t);
                 double* sl = kslot + tid * kLdsStride;
+                const double* sp = kprev + tid * kLdsStride;
                 double T[8], Rm[9];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) T[j] = sl[j];
-                solve_pose(a, (int)sl[21], S, T, Rm);
+                for (int j = 0; j < 8; ++j) T[j] = sp[j];
+                solve_pose(a, (int)sp[21], S, T, Rm);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) sl[j] = T[j];
 #pragma unroll
@@ -1474,6 +1518,7 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
             }
         }
         __syncthreads();
+        if (wv == 0 && it < 5) VX_KT(2 + 3 * it);
         if (s_fault || !s_act) break;
         if (tid < kFK && ke.x >= 0 && (ke.x & (1 << 30))) {  // the owner publishes the pose
             double* Tout = pose_out(a, it) + 8 * (size_t)row;
@@ -1485,6 +1530,8 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
         // ---- landmark stage of iteration it (local_ba.cpp:176-238), as k_ba_iter
         {
             double h[9];
+            const int4 orec = s_orec[tid];
+            const double2 ouv = s_ouv[tid];
             const D3 PO{lpos[3 * orec.y], lpos[3 * orec.y + 1], lpos[3 * orec.y + 2]};
             const bool ok = obs_terms<true>(a, PO, orec.x, ouv, kslot, kLdsStride, kslot + 8, kLdsStride, kslot + 17,
                                             kLdsStride, h);
@@ -1495,19 +1542,23 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
             if (own) {
                 double hs[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
                 int obs = 0;
-                for (int q = run.x; q < run.y; ++q) {
+                const int r0 = s_run[3 * tid], r1 = s_run[3 * tid + 1];
+                int lslot = s_run[3 * tid + 2];
+                const D3 P0{lpos[3 * tid], lpos[3 * tid + 1], lpos[3 * tid + 2]};
+                for (int q = r0; q < r1; ++q) {
 #pragma unroll
                     for (int j = 0; j < 9; ++j) hs[j] += terms[j * kFT + q];
                     obs += tcount[q];
                 }
-                PL = lm_update(a, lslot, PL, hs, obs);
-                lpos[3 * tid] = PL.x;
-                lpos[3 * tid + 1] = PL.y;
-                lpos[3 * tid + 2] = PL.z;
+                const D3 P1 = lm_update(a, lslot, P0, hs, obs);
+                lpos[3 * tid] = P1.x;
+                lpos[3 * tid + 1] = P1.y;
+                lpos[3 * tid + 2] = P1.z;
             }
             __syncthreads();
         }
         if (it + 1 < M) pose_stage(it + 1);
+        if (wv == 0 && it < 4) VX_KT(3 + 3 * it);
     }
     // ---- the last iteration's statistics (a stop inside the loop wrote them), then the next run's
     // parity; workgroup 0 gets here only after every workgroup's first arrival (its waits above), so
@@ -2407,6 +2458,16 @@ WinArgs make_win_args(vx_ba_plan* p) {
     w.nprod = reinterpret_cast<const int*>(W + p->win_nprod_off);
     w.gen = reinterpret_cast<int*>(W + p->win_gen_off);
     w.fault = reinterpret_cast<int*>(p->state.as<uint8_t>() + offsetof(BAState, fault));
+    static const int wsig = [] {
+        const char* e = getenv("VX_BA_WIN_WSIG");
+        return e && e[0] == '1' ? 1 : 0;
+    }();
+    w.wsig = wsig;
+    static const int naps = [] {
+        const char* e = getenv("VX_BA_WIN_NAPS");
+        return e ? std::max(1, atoi(e)) : 1;
+    }();
+    w.naps = naps;
     return w;
 }
 
@@ -2421,7 +2482,7 @@ int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
     if ((rc = reset_if_no_iterations(c, p, a))) return rc;
     if (p->opt.max_iterations == 0) return VX_OK;
     if (win_active(p)) {
-        constexpr int lds = (int)fused_lds(kFTSmall);
+        constexpr int lds = (int)win_lds(kFTSmall);
         static std::atomic<uint64_t> dw{0};
         VX_HIP(c, lds_attr_once(c->device, reinterpret_cast<const void*>(&k_ba_win<kFTSmall>), lds, dw));
         VX_HIP(c, launch(c, kStBaWin, k_ba_win<kFTSmall>, dim3(p->f_blocks), dim3(kFTSmall), (uint32_t)lds, c->stream,
@@ -2935,13 +2996,26 @@ int vx_ba_plan_fused_tables(vx_ctx* c, const vx_ba_plan* p, void* dst, size_t ca
 
 int vx_ba_optimize_map(vx_ctx* c, vx_map_view* m, uint64_t ref, int has_ref, const vx_ba_options* opt,
                        vx_ba_stats* st) {
+    // ($VX_OPT_TIMING=1: the call's phases on stderr, scripts/adapter_timing.py)
+    static const bool timing = getenv("VX_OPT_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (timing)
+            std::fprintf(stderr, "[vx optmap] %s %.1f us\n", what,
+                         std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    };
     vx_ba_plan* p = nullptr;
     int rc = vx_ba_plan_create(c, m, ref, has_ref, opt, 0, 1, &p);
+    lap("plan_create");
     if (rc) return rc;
     rc = vx_ba_plan_run_async(c, p);
+    if (timing) (void)hipStreamSynchronize(c->stream);
+    lap("run");
     if (!rc) rc = vx_ba_plan_fetch(c, p, m, st);
+    lap("fetch");
     (void)hipStreamSynchronize(c->stream);
     vx_ba_plan_destroy(p);
+    lap("destroy");
     return rc;
 }
 

@@ -546,13 +546,23 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
         OptimizeResident(ref_kf);
         return;
     }
+    // ($VX_RESIDENT_TIMING=1: the snapshot call's phases on stderr too, scripts/adapter_timing.py)
+    static const bool timing = std::getenv("VX_RESIDENT_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (timing)
+            fprintf(stderr, "[vx snapshot] %s %.1f us\n", what,
+                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    };
     FlatMap& f = flat_;
     Flatten(*map, ref_kf, options_.window_size, f);
+    lap("flatten");
     if (f.frames.size() < 2) return;                            // local_ba.cpp:73-75
     const vx_ba_options o = VxOptions();
     vx_map_view v = f.view();
     vx_ctx* c = vxhost::ThreadContext();
     check(c, vx_ba_optimize_map(c, &v, ref_kf ? ref_kf->Id() : 0, ref_kf ? 1 : 0, &o, &stats_), "vx_ba_optimize_map");
+    lap("optimize_map");
     if (stats_.status != 0) return;
     // scatter: Frame::SetPose / Landmark::SetPosition (local_ba.cpp:173,237)
     for (size_t i = 0; i < f.frames.size(); ++i) {
@@ -569,6 +579,7 @@ void LocalBA::Optimize(const Map::Ptr& map, const Frame::Ptr& ref_kf) {
             f.landmarks[i]->SetPosition(Vec3d(f.lm_pos[3 * i], f.lm_pos[3 * i + 1], f.lm_pos[3 * i + 2]));
         }
     });
+    lap("write-back");
 }
 
 }  // namespace visionx
