@@ -1231,8 +1231,6 @@ struct WinArgs {
     const int* nprod;  // [n_kf] workgroups with an entry on the row
     int* gen;          // run generation (parity = gen & 1), bumped by workgroup 0 at the run's end
     int* fault;        // set when a wait ran out (every workgroup then leaves)
-    int wsig;          // hand-off wave by wave ($VX_BA_WIN_WSIG=1) or after a workgroup barrier (default)
-    int naps;          // s_sleep 1 between a row poll's loads ($VX_BA_WIN_NAPS, default 1)
 };
 constexpr long long kWinSpinTicks = 20'000'000;  // 200 ms of the 100 MHz wall clock
 // k_ba_win's LDS: k_ba_iter's plus a second set of pose slots
@@ -1250,7 +1248,7 @@ __device__ __forceinline__ void add_agent(int* p, int v) {
 }
 // lanes with want: spin until *p >= target (each lane its own counter); false when the wait ran out
 // or another workgroup reported a fault
-__device__ __forceinline__ bool win_wait(const int* p, int target, bool want, int* fault, int naps = 1) {
+__device__ __forceinline__ bool win_wait(const int* p, int target, bool want, int* fault) {
     const long long t0 = wall_clock64();
     bool ok = true;
     __builtin_amdgcn_s_setprio(0);  // (a polling wave leaves the SIMD to co-resident waves)
@@ -1264,12 +1262,15 @@ __device__ __forceinline__ bool win_wait(const int* p, int target, bool want, in
                 break;
             }
         }
-        for (int z = 0; z < naps; ++z) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(1);  // (longer naps between polls measured the same: r06g)
     }
     __builtin_amdgcn_s_setprio(3);
     return __all(ok);
 }
 
+// (232 VGPRs, two waves per SIMD.  Sized for three — 168 VGPRs, so that a third wave of the other
+// streams' kernels fits beside it — it spills outside the observation rounds: LocalBA alone 0.067
+// against 0.054 ms, the C3 pipeline 0.074 against 0.063 ms/frame, r06i)
 template <int kFT>
 __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w) {
     constexpr int kFW = kFT / 64;
@@ -1277,7 +1278,7 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
     __builtin_amdgcn_s_setprio(3);
     extern __shared__ __attribute__((aligned(16))) double fl[];
     __shared__ int4 s_ke[kFK];
-    __shared__ int s_act, s_fault, s_waves;
+    __shared__ int s_act, s_fault;
     // two pose-slot sets (T 8 | R 9 | C 4 | flags per entry): iteration it solves from set (it - 1) & 1
     // into set it & 1, so a wave still in the previous pose stage (no barrier closes it) reads poses
     // the solve does not overwrite
@@ -1363,10 +1364,7 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
     s_run[3 * tid + 1] = run0.y;
     s_run[3 * tid + 2] = lslot0;
     if (tid < kFK) s_ke[tid] = ke;
-    if (tid == 0) {
-        s_fault = 0;
-        s_waves = 0;
-    }
+    if (tid == 0) s_fault = 0;
     if (tid < kFK && ke.x >= 0) {  // iteration 0's pose stage reads the initial poses (set 1)
         double Rm[9];
         rot_from_quat(ev, Rm);
@@ -1383,9 +1381,8 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
     __syncthreads();
 
     // ---- pose stage of iteration `itn` from the poses in set (itn - 1) & 1 and the landmarks in lpos,
-    // added into R_itn; then the hand-off, wave by wave: an entry's terms come from one wave, so once
-    // that wave's atomics have retired (vmcnt(0)) it signals its own entries' rows — no barrier, the
-    // wave does not wait for the workgroup's slowest wave
+    // added into R_itn; then the hand-off (every wave's atomics retired, barrier, one arrival per
+    // entry row).  (The barrier does not protect the pose slots: the next solve writes the other set.)
     auto pose_stage = [&](int itn) {
         int r = 0;
         double* const Rn = R + (size_t)itn * nk * kStride;
@@ -1432,20 +1429,11 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
                 unsafeAtomicAdd(Rn + (size_t)(e.x & 0x3fffffff) * kStride + (lane >> 1), tot);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's adds are done at the memory side)
-        if (w.wsig) {
-            const int jl = wv + kFW * lane;  // lane l signals the wave's l-th entry
-            if (jl < n_ent) {
-                const int x = s_ke[jl].x;
-                if (x >= 0) add_agent(cnt + (size_t)itn * nk + (x & 0x3fffffff), 1);
-            }
-            // done[itn]: one arrival per workgroup, by its last wave (a monotonic LDS count: 8 arrivals
-            // per workgroup on one global word would serialise ~1000 atomics there per iteration)
-            if (lane == 0 && atomicAdd(&s_waves, 1) == (itn + 1) * kFW - 1) add_agent(done + (size_t)itn * 32, 1);
-        } else {  // (the workgroup's barrier, then one lane per entry)
-            __syncthreads();
-            if (tid < kFK && ke.x >= 0) add_agent(cnt + (size_t)itn * nk + row, 1);
-            if (tid == kFK) add_agent(done + (size_t)itn * 32, 1);
-        }
+        // the hand-off after the workgroup's barrier, one lane per entry row (signalling wave by wave,
+        // each wave's entries as soon as its own adds retired, measured 35 % slower: r06e/r06g)
+        __syncthreads();
+        if (tid < kFK && ke.x >= 0) add_agent(cnt + (size_t)itn * nk + row, 1);
+        if (tid == kFK) add_agent(done + (size_t)itn * 32, 1);
     };
     // ---- stop rule of iteration ip (local_ba.cpp:240-247) from every row of R_ip, by wave 1 of every
     // workgroup (the same values summed in the same order: the same decision everywhere)
@@ -1491,7 +1479,7 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
         // whether iteration it runs (the stop rule of it - 1)
         if (wv == 0) {
             const bool want = tid < kFK && ke.x >= 0;
-            const bool ok = win_wait(cnt + (size_t)it * nk + row, np, want, w.fault, w.naps);
+            const bool ok = win_wait(cnt + (size_t)it * nk + row, np, want, w.fault);
             if (it < 5) VX_KT(1 + 3 * it);
             if (!ok && lane == 0) s_fault = 1;
             if (want && ok) {
@@ -2458,16 +2446,6 @@ WinArgs make_win_args(vx_ba_plan* p) {
     w.nprod = reinterpret_cast<const int*>(W + p->win_nprod_off);
     w.gen = reinterpret_cast<int*>(W + p->win_gen_off);
     w.fault = reinterpret_cast<int*>(p->state.as<uint8_t>() + offsetof(BAState, fault));
-    static const int wsig = [] {
-        const char* e = getenv("VX_BA_WIN_WSIG");
-        return e && e[0] == '1' ? 1 : 0;
-    }();
-    w.wsig = wsig;
-    static const int naps = [] {
-        const char* e = getenv("VX_BA_WIN_NAPS");
-        return e ? std::max(1, atoi(e)) : 1;
-    }();
-    w.naps = naps;
     return w;
 }
 
