@@ -824,6 +824,8 @@ def main():
     ap.add_argument("--frames", type=int, default=8, help="distinct frames cycled through")
     ap.add_argument("--cpu-sample", type=int, default=30, help="frames timed for the CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-drop-in", action="store_true",
+                    help="skip the per-keyframe drop-in timings (PMC tool runs: the C++ adapter subprocess)")
     ap.add_argument("--no-profile", action="store_true", help="skip the HIP-event roofline pass")
     ap.add_argument("--ba-cus", type=float, default=0.0,
                     help="fraction of the CUs reserved for the LocalBA context (disjoint CU masks; 0: shared)")
@@ -974,7 +976,7 @@ def main():
         bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N).close()
         plan_ms.append(1e3 * (time.perf_counter() - t0))
     plan_build_ms = float(np.median(plan_ms))
-    per_kf = per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam) if N == 1 else None
+    per_kf = per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam) if N == 1 and not args.no_drop_in else None
     torch.cuda.synchronize()
 
     # Pipeline.  Frame t: Extract(t) on extraction context t % E (E = --extract-ctx) into that

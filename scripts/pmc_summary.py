@@ -17,7 +17,8 @@ STAGE = {"k_gray": "orb_gray", "k_resize": "orb_resize", "k_pyramid": "orb_pyram
          "k_knn_partial": "match_partial", "k_knn_rows": "match_partial", "k_knn_merge": "match_merge",
          "k_knn_compact": "match_merge", "k_ba_reset": "ba_reset",
          "k_pose_kf": "ba_pose_partial", "k_landmark_solve": "ba_landmark", "k_pose_solve_g": "ba_landmark",
-         "k_landmark": "ba_landmark", "k_ba_iter": "ba_iter", "k_ba_prologue": "ba_prologue"}
+         "k_landmark": "ba_landmark", "k_ba_iter": "ba_iter", "k_ba_prologue": "ba_prologue",
+         "k_ba_win": "ba_window"}
 
 
 def agg(path, counter):

@@ -70,10 +70,12 @@ def test_bench_json_line():
 
 
 def test_committed_bench_roofline_matches_committed_profile():
-    """The C3 bench line printed under rocprofv3 this round and the --kernel-trace --stats summary of
-    the same command (profiles/r06): the line's roofline fraction is within 5 % of the algorithmic
-    bytes / rocprof's average duration of that kernel / 8 TB/s."""
-    d = json.loads(open(os.path.join(ROOT, "profiles", "r06", "bench_c3_rocprof_r06.json")).read().strip().splitlines()[-1])
+    """The committed C3 bench line of this round (the default command, unprofiled) and the rocprofv3
+    --kernel-trace --stats summary of the same command in the same session (profiles/r06): the
+    line's roofline fraction is within 5 % of the algorithmic bytes / rocprof's average duration of
+    that kernel / 8 TB/s.  (The line the profiled process prints itself, bench_c3_under_rocprof_r06.json,
+    is not compared: under the tracer the bench's own event-timed pass runs ~25 % longer.)"""
+    d = json.loads(open(os.path.join(ROOT, "profiles", "r06", "bench_c3_r06.json")).read().strip().splitlines()[-1])
     rf = d["roofline"]
     assert rf["hip_kernel"] in ("k_ba_iter", "k_ba_win")
     # k_ba_iter: the iteration launches (k_ba_iter<false, ...>; the prologue k_ba_iter<true, ...> is its
