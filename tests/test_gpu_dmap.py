@@ -54,6 +54,39 @@ def test_dmap_plan_equals_snapshot_plan(ctx, cfg, slot_sums):
     pd2.close(), ps2.close(), pd.close(), ps.close(), dm.close()
 
 
+def test_dmap_plan_persistent_fault_fallback(ctx, monkeypatch):
+    """vx_ba_plan_apply_dmap after a persistent window whose waits ran out ($VX_BA_WIN_TEST_FAULT: an
+    arrival that never comes): the apply re-runs the window with the per-iteration launches before it
+    scatters, so the resident map gets the same results as a snapshot plan's fetch."""
+    nk, nl = 50, 20000
+    m = synth.make_ba_map(0xD0 + nk, nk, nl, n_old_kf=2)
+    dm = vxslam.DMap(ctx)
+    kf_order, lm_order = vxslam.dmap_load(dm, m)
+    m2 = vxslam.map_reorder(m, kf_order, lm_order)
+    opts = vxslam.default_ba_options(window=nk, iters=5)
+    monkeypatch.setenv("VX_BA_PERSIST", "0")
+    ps = ctx.ba_plan(m2, opts, ref_kf_id=m["ref_kf_id"])
+    assert not ps.persistent()
+    ss = _run(ps)
+    monkeypatch.setenv("VX_BA_PERSIST", "1")
+    monkeypatch.setenv("VX_BA_WIN_TEST_FAULT", "1")
+    pd = dm.plan(opts, ref_kf_id=m["ref_kf_id"])
+    assert pd.persistent()
+    pd.run_async()
+    pd.apply(dm)
+    assert not pd.persistent()
+    ps.fetch(m2)
+    pose, pos = dm.download()
+    # (float-atomic row sums on both plans: equal to rounding, DESIGN.md §21)
+    for a, b in ((_canon(pose), _canon(m2["kf_pose"].reshape(-1, 7))), (pos, m2["lm_pos"].reshape(-1, 3))):
+        assert (np.abs(a - b) / np.maximum(np.abs(b), 1e-3)).max() <= 1e-6
+    sd = pd.fetch()
+    assert (sd.status, sd.iterations, list(sd.obs)) == (ss.status, ss.iterations, list(ss.obs))
+    for a, b in zip(sd.cost[:sd.iterations], ss.cost[:ss.iterations]):
+        assert abs(a - b) <= 1e-9 * abs(b)
+    pd.close(), ps.close(), dm.close()
+
+
 class _Mirror:
     """Feeds snapshot keyframe rows into a DMap one at a time and keeps the equivalent snapshot."""
 

@@ -2680,6 +2680,18 @@ int vx_ba_plan_apply_dmap(vx_ctx* c, vx_ba_plan* p, vx_dmap* m) {
     if (!p->from_dmap) return set_error(c, VX_ERR_STATE, "plan was not built from a vx_dmap");
     if (!p->ran) return set_error(c, VX_ERR_STATE, "plan not run");
     if (p->status != 0) return VX_OK;
+    if (win_active(p)) {  // (a persistent run whose waits ran out is void: run it again first)
+        int fault = 0;
+        VX_HIP(c, hipMemcpyAsync(&fault, p->state.as<uint8_t>() + offsetof(BAState, fault), sizeof fault,
+                                 hipMemcpyDeviceToHost, c->stream));
+        VX_HIP(c, hipStreamSynchronize(c->stream));
+        if (fault) {
+            p->win_off = true;
+            p->graph.reset();
+            VX_HIP(c, hipMemsetAsync(p->state.as<uint8_t>() + offsetof(BAState, fault), 0, sizeof(int), c->stream));
+            if (int rc = plan_run(c, p)) return rc;
+        }
+    }
     const int n = std::max(p->n_kf, p->n_opt);
     hipLaunchKernelGGL(k_apply_dmap, dim3((n + 255) / 256), dim3(256), 0, c->stream, (const BAState*)p->state.as<BAState>(),
                        (const double*)p->kf_pose.as<double>(), p->n_kf, (const double*)p->lm_pos.as<double>(), p->n_opt,
