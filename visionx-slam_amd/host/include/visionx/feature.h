@@ -95,8 +95,9 @@ struct FlatMap {
     std::vector<Landmark*> scratch_obj;
     std::vector<int64_t> scratch_cnt;
     std::vector<uint64_t> scratch_key, scratch_hash;
-    std::vector<uint32_t> scratch_first;
+    std::vector<uint32_t> scratch_first, scratch_bucket;
     std::vector<uint8_t> scratch_firstocc;
+    std::vector<int64_t> scratch_kreg;  // per (keyframe, hash region): feature counts, then bucket offsets
 };
 
 class DeviceMap;

@@ -238,8 +238,12 @@ vx_map_view FlatMap::view() {
 // Distinct landmark ids of the window's features in first-occurrence order (the order of the first
 // feature referencing each: deterministic, like the device plan's fixed-landmark numbering).  The
 // hash space is split into one region per part, so every part dedupes its own ids in its own table
-// region without atomics; each part scans the features in order, so the first insert of an id is its
-// first occurrence, which it marks.  `hash` = the features' id hashes (0 for no landmark).
+// without atomics.  The features pass (Flatten) counted each keyframe's features per region (kreg,
+// nk x parts); here they are bucketed by region in feature order (a parallel scatter over the
+// keyframes), so part t walks only its own bucket — ~1/parts of the features, not all of them — and
+// the first insert of an id is its first occurrence, which it marks.  Then the ids in feature order,
+// keyframe by keyframe in parallel.  `hash` = the features' id hashes; `reg` = their regions (0xff: no
+// landmark).
 static uint64_t mix64(uint64_t x) {
     x += 0x9e3779b97f4a7c15ull;
     x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -247,21 +251,60 @@ static uint64_t mix64(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector<uint8_t>& has,
+static inline uint8_t id_region(uint64_t hash, int parts) {  // the high hash bits scaled to [0, parts)
+    return (uint8_t)(((hash >> 32) * (uint64_t)parts) >> 32);
+}
+
+static int id_parts() { return std::min(std::max(1, vxhost::Pool::Get().Threads()), 64); }
+
+static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector<uint8_t>& reg,
                          const std::vector<uint64_t>& hash, std::vector<uint8_t>& firstocc, FlatMap& f,
                          std::vector<uint64_t>& ids) {
     auto& pool = vxhost::Pool::Get();
-    const size_t nf = feat_lm.size();
-    const int parts = std::max(1, pool.Threads());
-    // slots per region: ~2 x a region's average share of the features.  A region that receives more
-    // ids than half its slots (a window whose features nearly all name distinct landmarks, or an
-    // unlucky spread over the regions) moves to a private table of twice the size, its keys re-inserted
+    static const bool timing = std::getenv("VX_FLATTEN_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* w) {
+        if (timing)
+            std::fprintf(stderr, "[flatten-ids] %s %.3f ms\n", w,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    };
+    const size_t nk = f.kf_feat_ptr.size() - 1;
+    const int parts = id_parts();
+    // bucket offsets: region-major, keyframe-minor (so each bucket lists its features in order)
+    std::vector<int64_t>& kr = f.scratch_kreg;  // [k * parts + r]: count in, offset out
+    std::vector<int64_t> rbeg((size_t)parts + 1, 0);
+    {
+        int64_t at = 0;
+        for (int r = 0; r < parts; ++r) {
+            rbeg[(size_t)r] = at;
+            for (size_t k = 0; k < nk; ++k) {
+                const int64_t c = kr[k * parts + r];
+                kr[k * parts + r] = at;
+                at += c;
+            }
+        }
+        rbeg[(size_t)parts] = at;
+    }
+    f.scratch_bucket.resize((size_t)rbeg[(size_t)parts]);
+    uint32_t* bucket = f.scratch_bucket.data();
+    pool.For(nk, 1, [&](size_t k0, size_t k1) {
+        for (size_t k = k0; k < k1; ++k) {
+            int64_t* off = &kr[k * parts];
+            for (int64_t o = f.kf_feat_ptr[k]; o < f.kf_feat_ptr[k + 1]; ++o)
+                if (reg[o] != 0xff) bucket[off[reg[o]]++] = (uint32_t)o;
+        }
+    });
+    lap("scatter");
+    // slots per region: ~2 x its bucket.  (A region whose ids outgrow half its slots — every feature
+    // its own landmark — moves to a private table of twice the size, its keys re-inserted.)
     size_t per = 64;
-    while (per < 2 * nf / (size_t)parts + 64) per <<= 1;
+    int64_t most = 0;
+    for (int r = 0; r < parts; ++r) most = std::max(most, rbeg[(size_t)r + 1] - rbeg[(size_t)r]);
+    while (per < 2 * (size_t)most / 4 + 64) per <<= 1;  // (ids <= features; a quarter as a first guess)
     f.scratch_key.resize(per * (size_t)parts);
     f.scratch_first.resize(per * (size_t)parts);  // (occupancy flags)
     pool.For((size_t)parts, 1, [&](size_t a, size_t b) {
-        std::vector<uint64_t> own_key;  // a grown region's table (rare)
+        std::vector<uint64_t> own_key;  // a grown region's table
         std::vector<uint32_t> own_used;
         for (size_t t = a; t < b; ++t) {
             uint64_t* key = f.scratch_key.data() + t * per;
@@ -269,9 +312,8 @@ static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector
             size_t cap = per;
             std::fill(used, used + cap, 0u);
             size_t n_in = 0;
-            for (size_t o = 0; o < nf; ++o) {
-                // region = the high hash bits scaled to [0, parts) (no division), slot = the low bits
-                if (!has[o] || (size_t)(((hash[o] >> 32) * (uint64_t)parts) >> 32) != t) continue;
+            for (int64_t q = rbeg[t]; q < rbeg[t + 1]; ++q) {
+                const uint32_t o = bucket[q];
                 const uint64_t id = feat_lm[o];
                 size_t h = (size_t)hash[o] & (cap - 1);
                 for (;;) {
@@ -286,16 +328,16 @@ static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector
                     h = (h + 1) & (cap - 1);
                 }
                 if (2 * n_in > cap) {  // keep the load <= 1/2: double the table, re-insert its keys
-                    std::vector<uint64_t> nk(2 * cap);
+                    std::vector<uint64_t> nk2(2 * cap);
                     std::vector<uint32_t> nu(2 * cap, 0u);
                     for (size_t s = 0; s < cap; ++s) {
                         if (!used[s]) continue;
                         size_t g = (size_t)mix64(key[s]) & (2 * cap - 1);
                         while (nu[g]) g = (g + 1) & (2 * cap - 1);
                         nu[g] = 1;
-                        nk[g] = key[s];
+                        nk2[g] = key[s];
                     }
-                    own_key.swap(nk);
+                    own_key.swap(nk2);
                     own_used.swap(nu);
                     key = own_key.data();
                     used = own_used.data();
@@ -304,9 +346,25 @@ static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector
             }
         }
     });
-    ids.clear();
-    for (size_t o = 0; o < nf; ++o)
-        if (firstocc[o]) ids.push_back(feat_lm[o]);
+    lap("dedup");
+    // the ids in feature order: per keyframe counts, their prefix, then each keyframe's ids in place
+    std::vector<int64_t> kc(nk + 1, 0);
+    pool.For(nk, 1, [&](size_t k0, size_t k1) {
+        for (size_t k = k0; k < k1; ++k) {
+            int64_t c = 0;
+            for (int64_t o = f.kf_feat_ptr[k]; o < f.kf_feat_ptr[k + 1]; ++o) c += firstocc[o];
+            kc[k + 1] = c;
+        }
+    });
+    for (size_t k = 0; k < nk; ++k) kc[k + 1] += kc[k];
+    ids.resize((size_t)kc[nk]);
+    pool.For(nk, 1, [&](size_t k0, size_t k1) {
+        for (size_t k = k0; k < k1; ++k) {
+            int64_t at = kc[k];
+            for (int64_t o = f.kf_feat_ptr[k]; o < f.kf_feat_ptr[k + 1]; ++o)
+                if (firstocc[o]) ids[(size_t)at++] = feat_lm[o];
+        }
+    });
 }
 
 FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size) {
@@ -323,6 +381,7 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
 // LocalBA runs on the tracking thread, which is also the one that edits the map).
 void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size, FlatMap& f) {
     auto& pool = vxhost::Pool::Get();
+    vxhost::Pool::Hold hold(pool);  // (the passes below run back to back)
     static const bool timing = std::getenv("VX_FLATTEN_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* w) {
@@ -362,12 +421,14 @@ void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size,
     f.feat_uv.resize(2 * nf);
     f.feat_lm_id.resize(nf);
     f.feat_flags.resize(nf);
-    std::vector<uint8_t>& has = f.scratch_has;
-    has.resize(nf);
+    std::vector<uint8_t>& reg = f.scratch_has;  // (the feature's id hash region, 0xff: no landmark)
+    reg.resize(nf);
     std::vector<uint8_t>& firstocc = f.scratch_firstocc;
     firstocc.resize(nf);
     std::vector<uint64_t>& hash = f.scratch_hash;
     hash.resize(nf);
+    const int parts = id_parts();
+    f.scratch_kreg.assign(nk * (size_t)parts, 0);
     pool.For(nk, 1, [&](size_t k0, size_t k1) {
         for (size_t k = k0; k < k1; ++k) {
             const auto& kf = f.frames[k];
@@ -386,8 +447,9 @@ void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size,
                 f.feat_uv[2 * o + 1] = feat.position.y;
                 f.feat_lm_id[o] = feat.landmark_id_;
                 f.feat_flags[o] = (feat.has_landmark ? 1 : 0) | (feat.is_outlier ? 2 : 0);
-                has[o] = feat.has_landmark ? 1 : 0;
                 hash[o] = feat.has_landmark ? mix64(feat.landmark_id_) : 0ull;
+                reg[o] = feat.has_landmark ? id_region(hash[o], parts) : (uint8_t)0xff;
+                if (feat.has_landmark) ++f.scratch_kreg[k * (size_t)parts + reg[o]];
                 firstocc[o] = 0;
                 ++o;
             }
@@ -396,7 +458,7 @@ void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size,
     lap("features");
     // the landmark ids the window's features reference, distinct, in first-occurrence order
     std::vector<uint64_t>& ids = f.scratch_ids;
-    distinct_ids(f.feat_lm_id, has, hash, firstocc, f, ids);
+    distinct_ids(f.feat_lm_id, reg, hash, firstocc, f, ids);
     lap("ids");
     // per landmark: the object (absent ids are skipped, as GetLandmark -> nullptr in
     // local_ba.cpp:96-97,135-136), position, bad flag, observation count
@@ -440,7 +502,11 @@ void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size,
     f.obs_feat_idx.resize((size_t)f.lm_obs_ptr[nl]);
     pool.For(nl, 512, [&](size_t a, size_t b) {
         for (size_t i = a; i < b; ++i) {
-            if (i + 4 < b) __builtin_prefetch(obj[i + 4]);
+            if (i + 8 < b) PrefetchObject(obj[i + 8]);
+            if (i + 4 < b) {  // (the observation map's first node: its pointer is in the object, 4 later)
+                const auto& ob4 = obj[i + 4]->Observations();
+                if (!ob4.empty()) __builtin_prefetch(&*ob4.begin());
+            }
             const Landmark* lm = obj[i];
             const Vec3d p = lm->Position();
             f.lm_pos[3 * i] = p.x;
