@@ -11,4 +11,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/kt -o run -
 python3 scripts/win_pipeline_gaps.py $O/kt > $O/win_gaps.txt 2>&1 || { cat $O/win_gaps.txt; exit 4; }
 rm -rf $O/kt
 cat $O/win_gaps.txt
+timeout -k 10 300 python scripts/adapter_timing.py 20 > $O/adapter_timing.txt 2>&1 || { tail -30 $O/adapter_timing.txt; exit 6; }
+cat $O/adapter_timing.txt
 echo done

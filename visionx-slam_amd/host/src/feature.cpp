@@ -381,7 +381,6 @@ FlatMap LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_si
 // LocalBA runs on the tracking thread, which is also the one that edits the map).
 void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size, FlatMap& f) {
     auto& pool = vxhost::Pool::Get();
-    vxhost::Pool::Hold hold(pool);  // (the passes below run back to back)
     static const bool timing = std::getenv("VX_FLATTEN_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* w) {

@@ -30,16 +30,6 @@ public:
     }
     int Threads() const { return (int)workers_.size() + 1; }
 
-    // While held (a sequence of jobs back to back: Flatten's passes, the write-back), workers that
-    // finish a job spin for the next one instead of sleeping (a futex wake per job cost ~25 us each).
-    struct Hold {
-        Pool& p;
-        explicit Hold(Pool& q) : p(q) { p.hold_.fetch_add(1, std::memory_order_relaxed); }
-        ~Hold() { p.hold_.fetch_sub(1, std::memory_order_relaxed); }
-        Hold(const Hold&) = delete;
-        Hold& operator=(const Hold&) = delete;
-    };
-
     // fn(begin, end) over [0, n) in chunks of at least min_chunk items; returns when every chunk is done
     void For(size_t n, size_t min_chunk, const std::function<void(size_t, size_t)>& fn) {
         if (n == 0) return;
@@ -116,9 +106,7 @@ private:
                     job = true;
                     break;
                 }
-                if ((it & 255) == 0 && !hold_.load(std::memory_order_relaxed) &&
-                    std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_))
-                    break;
+                if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin_us_)) break;
                 Relax();
             }
             std::shared_ptr<Job> j;
@@ -138,7 +126,6 @@ private:
     std::condition_variable cv_;
     std::shared_ptr<Job> cur_;
     std::atomic<unsigned long long> gen_{0};
-    std::atomic<int> hold_{0};
     bool stop_ = false;
     int spin_us_ = 0;  // ($VX_HOST_SPIN_US: 300 measured slower on the GPU box, whose CPU quota a spinning
                        // worker eats into)
