@@ -2723,6 +2723,13 @@ int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
         return rc;
     }
     p->ran = true;
+    // the persistent window is ONE kernel: launched directly (a graph launch of one kernel node costs
+    // the host more and the stream extra packets, $VX_BA_WIN_GRAPH=1 for it)
+    static const bool win_graph = [] {
+        const char* e = std::getenv("VX_BA_WIN_GRAPH");
+        return e && e[0] == '1';
+    }();
+    if (win_active(p) && !win_graph && !c->prof) return plan_run(c, p);
     return graph_run_owned(c, p->graph, [](vx_ctx* cc, void* v) { return plan_run(cc, static_cast<vx_ba_plan*>(v)); }, p);
 }
 
