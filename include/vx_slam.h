@@ -101,6 +101,11 @@ int vx_create_ex(int device, int priority, const uint32_t* cu_mask, int mask_wor
 /* compute units of a device (the width of a CU mask) */
 int vx_device_cus(int device);
 void vx_destroy(vx_ctx* ctx);
+/* Page-locked, host-cached memory (hipHostMalloc): a vx_map_view whose arrays live in it is uploaded
+ * by DMA straight from the caller's arrays (pageable arrays are staged through the runtime's
+ * bounce buffers first).  visionx::FlatMap keeps its large arrays in it.  NULL on failure. */
+void* vx_host_alloc(size_t bytes);
+void vx_host_free(void* p);
 const char* vx_last_error(const vx_ctx* ctx);
 void* vx_stream(vx_ctx* ctx);          /* the context's hipStream_t */
 int vx_synchronize(vx_ctx* ctx);

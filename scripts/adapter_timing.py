@@ -45,3 +45,8 @@ with tempfile.TemporaryDirectory() as d:
             print(f"  {k}: median {np.median(v[1:] or v):.1f} us since the call's start")
         if r.returncode:
             print(r.stderr[-800:])
+    # the same calls without any timing switch (the laps above add synchronisations of their own)
+    for mode in ("resident", "snapshot"):
+        r = subprocess.run([drv, "ba_calls", d, "50", "5", "-1", str(reps), mode], capture_output=True, text=True,
+                           timeout=300)
+        print("untimed", mode, "rc", r.returncode, "stdout", r.stdout.strip())

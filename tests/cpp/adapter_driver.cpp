@@ -48,8 +48,8 @@ static std::vector<T> read_bin(const std::string& path) {
     return v;
 }
 
-template <class T>
-static void write_bin(const std::string& path, const std::vector<T>& v) {
+template <class T, class A>
+static void write_bin(const std::string& path, const std::vector<T, A>& v) {
     std::ofstream f(path, std::ios::binary);
     f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(T)));
 }

@@ -511,7 +511,9 @@ def test_graph_replay_matches_eager(ctx, oracle, monkeypatch, sums):
         for o, s in zip(outs[1:], sts[1:]):
             _runs_agree(o, outs[0], s, sts[0], bitwise=sums == "slots")
         captured, launched = c.graph_counts()
-        assert captured >= 4 and launched >= 8, (captured, launched)
+        # (a persistent-window plan is one kernel launched directly, not through a graph)
+        want = 3 if plan.persistent() else 4
+        assert captured >= want and launched >= 2 * want, (captured, launched)
         plan.close()
     finally:
         c.close()

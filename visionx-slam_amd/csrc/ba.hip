@@ -2844,10 +2844,24 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
     s.n_window_kf = p->n_window_kf;
     s.n_landmarks = p->n_landmarks_global;
     if (p->status == 0) {
+        // one synchronisation: the state, BOTH pose parities (the last iteration's is known only from
+        // the state) and the positions into one host-cached pinned block
+        const size_t sb = sizeof(BAState), pb = 2 * (size_t)p->n_kf * 8 * sizeof(double),
+                     lb = (size_t)p->n_opt * 4 * sizeof(double);
+        const size_t o_pose = (sb + 63) & ~(size_t)63, o_lm = o_pose + ((pb + 63) & ~(size_t)63);
+        VX_HIP(c, p->fetch_host.ensure(o_lm + lb + 64, true));
+        uint8_t* H = static_cast<uint8_t*>(p->fetch_host.p);
+        auto read_back = [&]() -> int {
+            VX_HIP(c, hipMemcpyAsync(H, p->state.p, sb, hipMemcpyDeviceToHost, c->stream));
+            VX_HIP(c, hipMemcpyAsync(H + o_pose, p->kf_pose.p, pb, hipMemcpyDeviceToHost, c->stream));
+            if (lb) VX_HIP(c, hipMemcpyAsync(H + o_lm, p->lm_pos.p, lb, hipMemcpyDeviceToHost, c->stream));
+            VX_HIP(c, hipStreamSynchronize(c->stream));
+            return VX_OK;
+        };
+        int rc = read_back();
+        if (rc) return rc;
         BAState hs;
-        std::vector<double> pose((size_t)p->n_kf * 8), lm((size_t)std::max(p->n_opt, 1) * 4);
-        VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
-        VX_HIP(c, hipStreamSynchronize(c->stream));
+        std::memcpy(&hs, H, sb);
         if (hs.fault && win_active(p)) {
             // a persistent window whose wait ran out (its workgroups could not all be resident at
             // once): the run is void; the plan keeps the per-iteration launches from now on and
@@ -2855,19 +2869,13 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
             p->win_off = true;
             p->graph.reset();
             VX_HIP(c, hipMemsetAsync(p->state.as<uint8_t>() + offsetof(BAState, fault), 0, sizeof(int), c->stream));
-            int rc = plan_run(c, p);
-            if (rc) return rc;
-            VX_HIP(c, hipMemcpyAsync(&hs, p->state.p, sizeof hs, hipMemcpyDeviceToHost, c->stream));
-            VX_HIP(c, hipStreamSynchronize(c->stream));
+            if ((rc = plan_run(c, p))) return rc;
+            if ((rc = read_back())) return rc;
+            std::memcpy(&hs, H, sb);
         }
         // the poses of the last iteration run are in ping-pong buffer (iterations & 1)
-        const double* fin = p->kf_pose.as<double>() + (size_t)(hs.iterations & 1) * p->n_kf * 8;
-        VX_HIP(c, hipMemcpyAsync(pose.data(), fin, pose.size() * sizeof(double), hipMemcpyDeviceToHost,
-                                 c->stream));
-        if (p->n_opt > 0)
-            VX_HIP(c, hipMemcpyAsync(lm.data(), p->lm_pos.p, (size_t)p->n_opt * 4 * sizeof(double),
-                                     hipMemcpyDeviceToHost, c->stream));
-        VX_HIP(c, hipStreamSynchronize(c->stream));
+        const double* pose = reinterpret_cast<const double*>(H + o_pose) + (size_t)(hs.iterations & 1) * p->n_kf * 8;
+        const double* lm = reinterpret_cast<const double*>(H + o_lm);
         if (c->prof) prof_collect(c);
         s.iterations = hs.iterations;
         for (int i = 0; i < 16; ++i) {

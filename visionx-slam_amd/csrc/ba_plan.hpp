@@ -53,6 +53,7 @@ struct vx_ba_plan {
     size_t win_rows_off = 0, win_cnt_off = 0, win_done_off = 0, win_nprod_off = 0, win_gen_off = 0;
     int f_stop_b = 0;            // workgroup running the stop rule
     vx::PinnedBuf f_stage;                                        // their host staging block
+    vx::PinnedBuf fetch_host;  // vx_ba_plan_fetch: the state, both pose parities and the positions, one copy each
     FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
     size_t f_npp = 0;                                             // pose-observation positions (padded)
 };
@@ -66,7 +67,7 @@ struct vx_dmap;
     X(kf_pose0) X(kf_pose) X(kf_intr) X(kf_rot) X(kf_flags) X(kf_obs_ptr) X(kf_part) X(kf_cost) X(lm_pos0) \
     X(lm_pos) X(pobs_uv) X(pobs_lm) X(lobs_ptr) X(lobs_kf) X(lobs_lm) X(lm_blk) X(lobs_uv) X(state)       \
     X(kf_map_dev) X(lm_map_dev) X(f_tab) X(f_lobs_uv) X(f_pobs_uv) X(f_pobs_p) X(f_part) X(f_rowpart)    \
-    X(f_stage) X(f_lpos) X(f_epose) X(f_costpart) X(f_arow) X(f_win)
+    X(f_stage) X(f_lpos) X(f_epose) X(f_costpart) X(f_arow) X(f_win) X(fetch_host)
 
 namespace vx {
 // a new plan of context c (buffers adopted from a parked plan when there is one)

@@ -365,22 +365,35 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
     const int nk = (int)win.size();
     p->n_window_kf = nk;
     if (nk < 2) return VX_OK;
-    // ---- window feature gather + keyframe tables (host: contiguous copies per keyframe)
+    const PlanClock clk;
+    // ---- window feature gather + keyframe tables (host: contiguous copies per keyframe).  A window
+    // of consecutive view rows (a snapshot of the window alone: visionx::LocalBA::Flatten) is uploaded
+    // straight from the view's arrays instead (page-locked there: one DMA each)
     std::vector<int> wptr(nk + 1, 0);
     for (int r = 0; r < nk; ++r) wptr[r + 1] = wptr[r] + (int)(m->kf_feat_ptr[win[r] + 1] - m->kf_feat_ptr[win[r]]);
     const int nf = wptr[nk];
-    std::vector<double> wuv((size_t)nf * 2);
-    std::vector<uint64_t> wlm(nf), wid(nk);
-    std::vector<uint8_t> wfl(nf), cam(nk);
+    bool consecutive = true;
+    for (int r = 1; r < nk; ++r) consecutive = consecutive && win[r] == win[0] + r;
+    const int64_t f_first = m->kf_feat_ptr[win[0]];
+    std::vector<double> wuv;
+    std::vector<uint64_t> wlm, wid(nk);
+    std::vector<uint8_t> wfl, cam(nk);
+    if (!consecutive) {
+        wuv.resize((size_t)nf * 2);
+        wlm.resize(nf);
+        wfl.resize(nf);
+    }
     std::vector<double> pose0((size_t)nk * 8, 0.0), intr((size_t)nk * 4, 0.0);
     std::vector<int> kf_flags(nk);
     int64_t mx = 0;
     for (int r = 0; r < nk; ++r) {
         const int k = win[r];
         const int64_t f0 = m->kf_feat_ptr[k], n = m->kf_feat_ptr[k + 1] - f0;
-        std::memcpy(&wuv[2 * (size_t)wptr[r]], m->feat_uv + 2 * f0, (size_t)n * 2 * sizeof(double));
-        std::memcpy(&wlm[wptr[r]], m->feat_lm_id + f0, (size_t)n * sizeof(uint64_t));
-        std::memcpy(&wfl[wptr[r]], m->feat_flags + f0, (size_t)n);
+        if (!consecutive) {
+            std::memcpy(&wuv[2 * (size_t)wptr[r]], m->feat_uv + 2 * f0, (size_t)n * 2 * sizeof(double));
+            std::memcpy(&wlm[wptr[r]], m->feat_lm_id + f0, (size_t)n * sizeof(uint64_t));
+            std::memcpy(&wfl[wptr[r]], m->feat_flags + f0, (size_t)n);
+        }
         wid[r] = m->kf_id[k];
         cam[r] = m->kf_has_cam[k] ? 1 : 0;
         kf_flags[r] = cam[r];
@@ -388,32 +401,50 @@ int build_plan_device(vx_ctx* c, const vx_map_view* m, uint64_t ref_kf_id, int h
         for (int j = 0; j < 4; ++j) intr[4 * r + j] = m->kf_intr[4 * k + j];
         if (cam[r]) {
             int64_t cnt = 0;
-            for (int64_t f = 0; f < n; ++f) cnt += wfl[wptr[r] + f] & 1;
+            const uint8_t* fl = m->feat_flags + f0;
+            for (int64_t f = 0; f < n; ++f) cnt += fl[f] & 1;
             mx = std::max(mx, cnt);
         }
     }
     p->n_split = ba_split(mx, p->shard_count);
     const int nl = m->n_lm;
     const int64_t nobs = nl > 0 ? m->lm_obs_ptr[nl] : 0;
+    clk.mark("device: window gathered");
     VX_HIP(c, hipSetDevice(c->device));
     vx_ctx::PlanScratch& B = c->plan_scratch;  // reused across this context's plan builds
     int rc;
-    if ((rc = up(c, B.wptr, wptr.data(), wptr.size()))) return rc;
-    if ((rc = up(c, B.wlm, wlm.data(), wlm.size()))) return rc;
-    if ((rc = up(c, B.wfl, wfl.data(), wfl.size()))) return rc;
-    if ((rc = up(c, B.cam, cam.data(), cam.size()))) return rc;
-    if ((rc = up(c, B.wid, wid.data(), wid.size()))) return rc;
-    if ((rc = up(c, B.wuv, wuv.data(), wuv.size()))) return rc;
+    // the keyframe-sized tables through one pinned block: ids, initial poses, intrinsics, feature
+    // offsets, camera flags
+    const size_t o_wid = 0, o_pose = o_wid + 8 * (size_t)nk, o_intr = o_pose + 64 * (size_t)nk,
+                 o_wptr = o_intr + 32 * (size_t)nk, o_cam = o_wptr + 4 * ((size_t)nk + 2), o_end = o_cam + (size_t)nk + 8;
+    VX_HIP(c, B.win_host.ensure(o_end, true));
+    VX_HIP(c, B.win.ensure(o_end));
+    {
+        uint8_t* H = static_cast<uint8_t*>(B.win_host.p);
+        std::memcpy(H + o_wid, wid.data(), 8 * (size_t)nk);
+        std::memcpy(H + o_pose, pose0.data(), 64 * (size_t)nk);
+        std::memcpy(H + o_intr, intr.data(), 32 * (size_t)nk);
+        std::memcpy(H + o_wptr, wptr.data(), 4 * ((size_t)nk + 1));
+        std::memcpy(H + o_cam, cam.data(), (size_t)nk);
+    }
+    VX_HIP(c, hipMemcpyAsync(B.win.p, B.win_host.p, o_end, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* WD = B.win.as<uint8_t>();
+    VX_HIP(c, p->kf_pose0.ensure(64 * (size_t)nk));
+    VX_HIP(c, p->kf_intr.ensure(32 * (size_t)nk));
+    VX_HIP(c, hipMemcpyAsync(p->kf_pose0.p, WD + o_pose, 64 * (size_t)nk, hipMemcpyDeviceToDevice, c->stream));
+    VX_HIP(c, hipMemcpyAsync(p->kf_intr.p, WD + o_intr, 32 * (size_t)nk, hipMemcpyDeviceToDevice, c->stream));
+    if ((rc = up(c, B.wlm, consecutive ? m->feat_lm_id + f_first : wlm.data(), (size_t)nf))) return rc;
+    if ((rc = up(c, B.wfl, consecutive ? m->feat_flags + f_first : wfl.data(), (size_t)nf))) return rc;
+    if ((rc = up(c, B.wuv, consecutive ? m->feat_uv + 2 * f_first : wuv.data(), 2 * (size_t)nf))) return rc;
     if ((rc = up(c, B.lid, m->lm_id, (size_t)nl))) return rc;
     if ((rc = up(c, B.bad, m->lm_bad, (size_t)nl))) return rc;
     if ((rc = up(c, B.optr, m->lm_obs_ptr, (size_t)nl + 1))) return rc;
     if ((rc = up(c, B.okf, m->obs_kf_id, (size_t)nobs))) return rc;
     if ((rc = up(c, B.ofi, m->obs_feat_idx, (size_t)nobs))) return rc;
     if ((rc = up(c, B.pos, m->lm_pos, (size_t)nl * 3))) return rc;
-    if ((rc = up(c, p->kf_pose0, pose0.data(), pose0.size()))) return rc;
-    if ((rc = up(c, p->kf_intr, intr.data(), intr.size()))) return rc;
-    BuildInputs in{nk, nf, nl, B.wptr.as<int>(), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(), B.cam.as<uint8_t>(),
-                   B.wid.as<uint64_t>(), B.wuv.as<double>(), B.lid.as<uint64_t>(), B.bad.as<uint8_t>(),
+    clk.mark("device: uploads queued");
+    BuildInputs in{nk, nf, nl, reinterpret_cast<const int*>(WD + o_wptr), B.wlm.as<uint64_t>(), B.wfl.as<uint8_t>(),
+                   WD + o_cam, reinterpret_cast<const uint64_t*>(WD + o_wid), B.wuv.as<double>(), B.lid.as<uint64_t>(), B.bad.as<uint8_t>(),
                    B.optr.as<int64_t>(), B.okf.as<uint64_t>(), B.ofi.as<uint64_t>(), B.pos.as<double>()};
     rc = build_core(c, in, win, kf_flags, p);
     VX_HIP(c, hipStreamSynchronize(c->stream));  // the host vectors above must outlive their async copies

@@ -212,6 +212,30 @@ int vx_create_ex(int device, int priority, const uint32_t* cu_mask, int mask_wor
     return VX_OK;
 }
 
+// (a 64-byte header records how the block was allocated: page-locked, or plain pageable memory when
+// the runtime has no device to lock pages for — a host-only build or test still gets working arrays)
+void* vx_host_alloc(size_t bytes) {
+    constexpr size_t kHdr = 64;
+    static const bool pageable = std::getenv("VX_HOST_PAGEABLE") != nullptr;  // (A/B switch)
+    void* p = nullptr;
+    uint32_t kind = 1;
+    if (pageable || hipHostMalloc(&p, bytes + kHdr, hipHostMallocNonCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        p = std::malloc(bytes + kHdr);
+        kind = 2;
+        if (!p) return nullptr;
+    }
+    *static_cast<uint32_t*>(p) = kind;
+    return static_cast<uint8_t*>(p) + kHdr;
+}
+
+void vx_host_free(void* q) {
+    if (!q) return;
+    void* p = static_cast<uint8_t*>(q) - 64;
+    if (*static_cast<uint32_t*>(p) == 1) (void)hipHostFree(p);
+    else std::free(p);
+}
+
 void vx_destroy(vx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);

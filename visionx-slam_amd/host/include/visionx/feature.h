@@ -73,19 +73,43 @@ private:
 };
 
 // Flattened window of a Map (what LocalBA::Optimize can read or write), laid out as vx_map_view.
+// Allocator of FlatMap's large arrays: page-locked host memory (vx_host_alloc), so that the
+// snapshot's upload in vx_ba_optimize_map is a DMA from these very arrays (pageable ones go through
+// the runtime's bounce buffers: ~0.5 ms of the C3 call).  The arrays keep their
+// capacity from call to call, so the (slow) page-locked allocation happens only while they grow.
+template <class T>
+struct PinnedAllocator {
+    using value_type = T;
+    PinnedAllocator() = default;
+    template <class U>
+    PinnedAllocator(const PinnedAllocator<U>&) {}
+    T* allocate(size_t n) {
+        void* p = vx_host_alloc(n * sizeof(T));
+        if (!p) throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { vx_host_free(p); }
+    template <class U>
+    bool operator==(const PinnedAllocator<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAllocator<U>&) const { return false; }
+};
+template <class T>
+using pinned_vector = std::vector<T, PinnedAllocator<T>>;
+
 struct FlatMap {
     std::vector<uint64_t> kf_id;
     std::vector<double> kf_pose, kf_intr;
     std::vector<uint8_t> kf_has_cam;
     std::vector<int64_t> kf_feat_ptr;
-    std::vector<double> feat_uv;
-    std::vector<uint64_t> feat_lm_id;
-    std::vector<uint8_t> feat_flags;
-    std::vector<uint64_t> lm_id;
-    std::vector<double> lm_pos;
-    std::vector<uint8_t> lm_bad;
-    std::vector<int64_t> lm_obs_ptr;
-    std::vector<uint64_t> obs_kf_id, obs_feat_idx;
+    pinned_vector<double> feat_uv;
+    pinned_vector<uint64_t> feat_lm_id;
+    pinned_vector<uint8_t> feat_flags;
+    pinned_vector<uint64_t> lm_id;
+    pinned_vector<double> lm_pos;
+    pinned_vector<uint8_t> lm_bad;
+    pinned_vector<int64_t> lm_obs_ptr;
+    pinned_vector<uint64_t> obs_kf_id, obs_feat_idx;
     std::vector<Frame::Ptr> frames;        // keyframes in kf_id order
     std::vector<Landmark::Ptr> landmarks;  // parallel to lm_id: first-reference order in the window, NOT ascending ids
     vx_map_view view();                    // pointers into the vectors above

@@ -257,7 +257,7 @@ static inline uint8_t id_region(uint64_t hash, int parts) {  // the high hash bi
 
 static int id_parts() { return std::min(std::max(1, vxhost::Pool::Get().Threads()), 64); }
 
-static void distinct_ids(const std::vector<uint64_t>& feat_lm, const std::vector<uint8_t>& reg,
+static void distinct_ids(const pinned_vector<uint64_t>& feat_lm, const std::vector<uint8_t>& reg,
                          const std::vector<uint64_t>& hash, std::vector<uint8_t>& firstocc, FlatMap& f,
                          std::vector<uint64_t>& ids) {
     auto& pool = vxhost::Pool::Get();
@@ -394,11 +394,20 @@ void LocalBA::Flatten(const Map& map, const Frame::Ptr& ref_kf, int window_size,
     const auto& all = map.KeyFrames();
     if (all.empty()) {
         f.landmarks.clear();
-        for (auto* v : {&f.kf_id, &f.lm_id, &f.feat_lm_id, &f.obs_kf_id, &f.obs_feat_idx}) v->clear();
-        for (auto* v : {&f.kf_pose, &f.kf_intr, &f.feat_uv, &f.lm_pos}) v->clear();
-        for (auto* v : {&f.kf_has_cam, &f.feat_flags, &f.lm_bad}) v->clear();
+        f.kf_id.clear();
+        f.kf_pose.clear();
+        f.kf_intr.clear();
+        f.kf_has_cam.clear();
         f.kf_feat_ptr.clear();
+        f.feat_uv.clear();
+        f.feat_lm_id.clear();
+        f.feat_flags.clear();
+        f.lm_id.clear();
+        f.lm_pos.clear();
+        f.lm_bad.clear();
         f.lm_obs_ptr.clear();
+        f.obs_kf_id.clear();
+        f.obs_feat_idx.clear();
         return;
     }
     // SelectKeyFrames (local_ba.cpp:42-62)

@@ -2,7 +2,10 @@
 // snapshot gather of LocalBA::Flatten and the result write-back into the Frame / Landmark objects).
 // Internal to libvxslam_host.  One job at a time (jobs from several threads are serialised); the
 // calling thread works on the job too.  $VX_HOST_THREADS sets the participants (default: up to 8,
-// at most the CPUs this process may use); 1 runs every job inline.
+// at most the CPUs this process may use); 1 runs every job inline.  The workers are bound to the
+// CPUs that share the creating thread's last-level cache (its CCD on an EPYC host): on the GPU box
+// (2 sockets, 16 L3 slices, affinity over all 256 CPUs) a free-floating worker lands on any slice,
+// and every array a job hands over then crosses slices or sockets ($VX_HOST_PIN=0: unbound).
 #pragma once
 
 #include <algorithm>
@@ -17,6 +20,11 @@
 #include <thread>
 #include <vector>
 
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include <pthread.h>
 #include <sched.h>
 
 namespace visionx {
@@ -71,6 +79,37 @@ private:
         if (const char* e = std::getenv("VX_HOST_THREADS")) want = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("VX_HOST_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
         for (int i = 1; i < want; ++i) workers_.emplace_back([this] { Loop(); });
+        const char* pin = std::getenv("VX_HOST_PIN");
+        if (!workers_.empty() && !(pin && pin[0] == '0')) {
+            cpu_set_t llc;
+            if (LlcCpus(&llc))
+                for (auto& t : workers_) (void)pthread_setaffinity_np(t.native_handle(), sizeof llc, &llc);
+        }
+    }
+    // the CPUs sharing the calling thread's last-level cache, within this process's affinity
+    static bool LlcCpus(cpu_set_t* out) {
+        const int cpu = sched_getcpu();
+        if (cpu < 0) return false;
+        char path[128];
+        std::snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+        FILE* f = std::fopen(path, "r");
+        if (!f) return false;
+        char buf[512] = {0};
+        const bool ok = std::fgets(buf, sizeof buf, f) != nullptr;
+        std::fclose(f);
+        if (!ok) return false;
+        cpu_set_t allowed;
+        if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+        CPU_ZERO(out);
+        for (char* tok = std::strtok(buf, ",\n"); tok; tok = std::strtok(nullptr, ",\n")) {
+            int a = -1, b = -1;
+            const int n = std::sscanf(tok, "%d-%d", &a, &b);
+            if (n < 1) continue;
+            if (n == 1) b = a;
+            for (int i = a; i <= b && i < CPU_SETSIZE; ++i)
+                if (i >= 0 && CPU_ISSET(i, &allowed)) CPU_SET(i, out);
+        }
+        return CPU_COUNT(out) >= 2;
     }
     ~Pool() {
         {

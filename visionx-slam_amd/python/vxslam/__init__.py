@@ -77,7 +77,7 @@ class SBAStats(C.Structure):
 
 
 EXPORTS = [
-    "vx_version", "vx_create", "vx_destroy", "vx_last_error", "vx_stream", "vx_synchronize",
+    "vx_version", "vx_create", "vx_destroy", "vx_host_alloc", "vx_host_free", "vx_last_error", "vx_stream", "vx_synchronize",
     "vx_stream_wait_ctx", "vx_event_create", "vx_event_record", "vx_event_wait", "vx_event_destroy",
     "vx_orb_default_params", "vx_orb_pattern", "vx_orb_extract", "vx_orb_extract_async",
     "vx_orb_fetch", "vx_orb_slot_device", "vx_match_knn2_ratio", "vx_match_slots_async",
