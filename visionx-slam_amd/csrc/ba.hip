@@ -2612,6 +2612,12 @@ using namespace vx;
 
 VX_KT_EXPORT(vx_ktrace_read_ba);
 
+namespace vx {
+// ba_lean.hip: vx_ba_optimize_map's one-call path (*fallback: the window needs a plan)
+int lean_optimize_view(vx_ctx* c, vx_map_view* v, uint64_t ref, int has_ref, const vx_ba_options& o, vx_ba_stats* st,
+                       bool* fallback);
+}  // namespace vx
+
 extern "C" {
 
 void vx_ba_default_options(vx_ba_options* o) {
@@ -3001,6 +3007,7 @@ int vx_ba_plan_fused_tables(vx_ctx* c, const vx_ba_plan* p, void* dst, size_t ca
 
 int vx_ba_optimize_map(vx_ctx* c, vx_map_view* m, uint64_t ref, int has_ref, const vx_ba_options* opt,
                        vx_ba_stats* st) {
+    if (!c) return VX_ERR_INVALID;
     // ($VX_OPT_TIMING=1: the call's phases on stderr, scripts/adapter_timing.py)
     static const bool timing = getenv("VX_OPT_TIMING") != nullptr;
     const auto t0 = std::chrono::steady_clock::now();
@@ -3009,6 +3016,18 @@ int vx_ba_optimize_map(vx_ctx* c, vx_map_view* m, uint64_t ref, int has_ref, con
             std::fprintf(stderr, "[vx optmap] %s %.1f us\n", what,
                          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     };
+    // the lean one-call build on the view loaded into the context's scratch map ($VX_OPTMAP_LEAN=0:
+    // always the plan below, for A/B runs); the plan for a window it does not take
+    static const bool lean_off = [] {
+        const char* e = getenv("VX_OPTMAP_LEAN");
+        return e && e[0] == '0';
+    }();
+    if (!lean_off && m && opt && opt->max_iterations >= 0 && opt->max_iterations <= 64) {
+        bool fb = false;
+        const int rc = lean_optimize_view(c, m, ref, has_ref, *opt, st, &fb);
+        lap("lean");
+        if (!fb) return rc;
+    }
     vx_ba_plan* p = nullptr;
     int rc = vx_ba_plan_create(c, m, ref, has_ref, opt, 0, 1, &p);
     lap("plan_create");

@@ -1115,6 +1115,110 @@ vx_dmap::~vx_dmap() {
 
 using namespace vx;
 
+namespace vx {
+namespace {
+// obs_lm of a view: the landmark row of each observation, from the landmark-major CSR pointers
+__global__ __launch_bounds__(kT) void k_view_obs_rows(const int64_t* __restrict__ optr, int64_t nl, int* __restrict__ obs_lm) {
+    const int64_t l = (int64_t)blockIdx.x * kT + threadIdx.x;
+    if (l >= nl) return;
+    for (int64_t o = optr[l]; o < optr[l + 1]; ++o) obs_lm[o] = (int)l;
+}
+
+template <class T>
+int view_up(vx_ctx* c, vx::DevBuf& d, const T* h, size_t n) {
+    VX_HIP(c, grow(d, std::max<size_t>(n, 1) * sizeof(T)));
+    if (n) VX_HIP(c, hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return VX_OK;
+}
+}  // namespace
+
+// vx_ba_optimize_map through the lean one-call build (round 6): the view is loaded into the
+// context's scratch vx_dmap — its arrays uploaded as they are (one DMA each when they are
+// page-locked, as visionx::FlatMap's are), the observation rows expanded from the CSR on the device,
+// the host mirrors the window selection reads copied — and lean_optimize runs on it with its single
+// synchronisation, the results coming back in the same copy (prefetch).  The general plan build
+// needs four synchronisations (ba_window.hip: counts, fused packing, fused entries; the fetch).
+// *fallback: a window the lean build does not take (the caller then builds a plan).
+int lean_optimize_view(vx_ctx* c, vx_map_view* v, uint64_t ref, int has_ref, const vx_ba_options& o, vx_ba_stats* st,
+                       bool* fallback) {
+    *fallback = false;
+    if (!c->snap_map) {
+        int rc = vx_dmap_create(c, &c->snap_map);
+        if (rc) return rc;
+    }
+    vx_dmap* m = c->snap_map;
+    const int nk = v->n_kf;
+    if (nk < 2 || v->n_lm < 0) {  // (nothing to select: the plan path's checks and early exits)
+        *fallback = true;
+        return VX_ERR_STATE;
+    }
+    const int64_t nl = v->n_lm, nf = v->kf_feat_ptr[nk], nobs = nl > 0 ? v->lm_obs_ptr[nl] : 0;
+    if (nl >= INT_MAX / 2 || nf >= INT_MAX / 2 || nobs >= INT_MAX / 2) {
+        *fallback = true;
+        return VX_ERR_STATE;
+    }
+    // host mirrors: keyframe ids / rows / cameras, every keyframe live; the valid-feature counts only
+    // for the window keyframes (the only ones lean_window reads)
+    m->kf_id.assign(v->kf_id, v->kf_id + nk);
+    m->kf_feat_ptr.assign(v->kf_feat_ptr, v->kf_feat_ptr + nk + 1);
+    m->kf_has_cam.resize(nk);
+    for (int k = 0; k < nk; ++k) m->kf_has_cam[k] = v->kf_has_cam[k] ? 1 : 0;
+    m->kf_alive.assign(nk, 1);
+    m->kf_valid_cnt.assign(nk, 0);
+    for (int k : dmap_select_window(m, ref, has_ref, o.window_size)) {
+        int cnt = 0;
+        for (int64_t f = v->kf_feat_ptr[k]; f < v->kf_feat_ptr[k + 1]; ++f) cnt += v->feat_flags[f] & 1;
+        m->kf_valid_cnt[k] = cnt;
+    }
+    m->n_lm = nl;
+    m->n_obs = nobs;
+    // device arrays
+    VX_HIP(c, hipSetDevice(c->device));
+    int rc;
+    if ((rc = view_up(c, m->kf_pose, v->kf_pose, 7 * (size_t)nk))) return rc;
+    if ((rc = view_up(c, m->kf_intr, v->kf_intr, 4 * (size_t)nk))) return rc;
+    if ((rc = view_up(c, m->feat_uv, v->feat_uv, 2 * (size_t)nf))) return rc;
+    if ((rc = view_up(c, m->feat_lm, v->feat_lm_id, (size_t)nf))) return rc;
+    if ((rc = view_up(c, m->feat_fl, v->feat_flags, (size_t)nf))) return rc;
+    if ((rc = view_up(c, m->lm_id, v->lm_id, (size_t)nl))) return rc;
+    if ((rc = view_up(c, m->lm_pos, v->lm_pos, 3 * (size_t)nl))) return rc;
+    if ((rc = view_up(c, m->lm_bad, v->lm_bad, (size_t)nl))) return rc;
+    if ((rc = view_up(c, m->obs_kf, v->obs_kf_id, (size_t)nobs))) return rc;
+    if ((rc = view_up(c, m->obs_fi, v->obs_feat_idx, (size_t)nobs))) return rc;
+    if ((rc = view_up(c, m->optr, v->lm_obs_ptr, (size_t)nl + 1))) return rc;
+    VX_HIP(c, grow(m->obs_lm, (size_t)std::max<int64_t>(nobs, 1) * 4));
+    if (nl) {
+        hipLaunchKernelGGL(k_view_obs_rows, dim3(grid(nl)), dim3(kT), 0, c->stream, (const int64_t*)m->optr.as<int64_t>(),
+                           nl, m->obs_lm.as<int>());
+        VX_LAUNCH_CHECK(c, "k_view_obs_rows");
+    }
+    // the id table of the previous view is stale: emptied, then refilled from row 0 (ht_sync)
+    if (m->ht_cap) {
+        hipLaunchKernelGGL(k_ht_clear, dim3(grid(m->ht_cap)), dim3(kT), 0, c->stream, m->ht_key.as<uint64_t>(), m->ht_cap);
+        VX_LAUNCH_CHECK(c, "k_ht_clear");
+    }
+    m->ht_rows = 0;
+    auto& L = m->lean;
+    L.ran = false;
+    L.prefetched = false;
+    L.prefetch = true;
+    vx_ba_stats s{};
+    rc = lean_optimize(c, m, ref, has_ref, o, &s, fallback);
+    if (*fallback || rc) return rc;
+    // the results into the view (Frame::SetPose / Landmark::SetPosition happen in the caller)
+    const int32_t *kr = nullptr, *lr = nullptr;
+    const double *kp = nullptr, *lp = nullptr;
+    int n_k = 0, n_l = 0;
+    if ((rc = vx_ba_dmap_results_view(c, m, &kr, &kp, &lr, &lp, &n_k, &n_l))) return rc;
+    for (int i = 0; i < n_k; ++i)
+        for (int j = 0; j < 7; ++j) v->kf_pose[7 * (size_t)kr[i] + j] = kp[8 * (size_t)i + j];
+    for (int i = 0; i < n_l; ++i)
+        for (int j = 0; j < 3; ++j) v->lm_pos[3 * (size_t)lr[i] + j] = lp[4 * (size_t)i + j];
+    if (st) *st = s;
+    return VX_OK;
+}
+}  // namespace vx
+
 extern "C" {
 
 int vx_ba_optimize_dmap(vx_ctx* c, vx_dmap* m, uint64_t ref, int has_ref, const vx_ba_options* opt, vx_ba_stats* st) {

@@ -243,6 +243,7 @@ void vx_destroy(vx_ctx* c) {
     for (auto& e : c->graphs.entries)
         if (e.exec) (void)hipGraphExecDestroy(e.exec);
     vx::prof_collect(c);
+    if (c->snap_map) vx_dmap_destroy(c->snap_map);
     vx::plan_pool_release(c);
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     for (auto e : {c->order_event})

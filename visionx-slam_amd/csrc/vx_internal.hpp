@@ -231,6 +231,7 @@ struct vx_ctx {
         vx::PinnedBuf win_host;            // the resident-map build's window tables, one upload ...
         vx::DevBuf win;                    // ... into one device block
     } plan_scratch;
+    vx_dmap* snap_map = nullptr;  // vx_ba_optimize_map's scratch map: the view loaded for the lean build (ba_lean.hip)
     // LocalBA plans of this context: parked buffer sets of destroyed plans (adopted by the next
     // vx_ba_plan_create) and the live plans (detached when the context goes first)
     std::vector<vx_ba_plan*> plan_husks, plan_live;
