@@ -179,6 +179,9 @@ def per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam):
 
     m = ba_map.copy()
 
+    def snap_call():
+        bctx.ba_optimize(m, opts)
+
     def snap():
         p = bctx.ba_plan(m, opts)
         p.run_async()
@@ -200,11 +203,14 @@ def per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam):
         dm.optimize(opts)
 
     try:
-        out = {"snapshot": med(snap), "resident": med(resident), "resident_one_call": med(one_call)}
+        out = {"snapshot": med(snap_call), "snapshot_plan": med(snap), "resident": med(resident),
+               "resident_one_call": med(one_call)}
     finally:
         dm.close()
     out["cpp_adapter"] = cpp_adapter_ms(ba_map, opts)
-    out["note"] = ("host wall clock of one LocalBA::Optimize, median of 7: snapshot = plan from the map snapshot "
+    out["note"] = ("host wall clock of one LocalBA::Optimize, median of 7: snapshot = vx_ba_optimize_map (the "
+                   "snapshot uploaded into the context's scratch device map, the one-call build, run and results in "
+                   "one synchronisation; pageable numpy arrays here); snapshot_plan = a plan from the map snapshot "
                    "(upload, device build) + run + download; resident = vx_ba_plan_create_dmap + run + "
                    "vx_ba_plan_apply_dmap; resident_one_call = vx_ba_optimize_dmap (ba_lean.hip: build, run and "
                    "scatter with no host synchronisation before the end); cpp_adapter = visionx::LocalBA::Optimize "
