@@ -73,18 +73,20 @@ private:
         std::atomic<size_t> next{0}, done{0};
     };
     Pool() {
-        int want = 8;
+        // participants: 8, or with the workers bound to an L3 slice every CPU of that slice up to 16
+        // (the GPU box's slices are 8 cores / 16 threads: 16 measured 4 % faster on the snapshot call,
+        // 2 % on the resident one, r06s); never more than the CPUs this process may use
+        const char* pin = std::getenv("VX_HOST_PIN");
+        cpu_set_t llc;
+        const bool bind = !(pin && pin[0] == '0') && LlcCpus(&llc);
+        int want = bind ? std::max(8, std::min(16, CPU_COUNT(&llc))) : 8;
         cpu_set_t set;
         if (sched_getaffinity(0, sizeof(set), &set) == 0) want = std::min(want, CPU_COUNT(&set));
         if (const char* e = std::getenv("VX_HOST_THREADS")) want = std::max(1, std::atoi(e));
         if (const char* e = std::getenv("VX_HOST_SPIN_US")) spin_us_ = std::max(0, std::atoi(e));
         for (int i = 1; i < want; ++i) workers_.emplace_back([this] { Loop(); });
-        const char* pin = std::getenv("VX_HOST_PIN");
-        if (!workers_.empty() && !(pin && pin[0] == '0')) {
-            cpu_set_t llc;
-            if (LlcCpus(&llc))
-                for (auto& t : workers_) (void)pthread_setaffinity_np(t.native_handle(), sizeof llc, &llc);
-        }
+        if (bind)
+            for (auto& t : workers_) (void)pthread_setaffinity_np(t.native_handle(), sizeof llc, &llc);
     }
     // the CPUs sharing the calling thread's last-level cache, within this process's affinity
     static bool LlcCpus(cpu_set_t* out) {
