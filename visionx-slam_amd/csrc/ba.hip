@@ -1480,7 +1480,9 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
         if (wv == 0) {
             const bool want = tid < kFK && ke.x >= 0;
             const bool ok = win_wait(cnt + (size_t)it * nk + row, np, want, w.fault);
+#ifndef VX_WIN_TRACE_LM
             if (it < 5) VX_KT(1 + 3 * it);
+#endif
             if (!ok && lane == 0) s_fault = 1;
             if (want && ok) {
                 double S[kNTerms];
@@ -1545,6 +1547,9 @@ __global__ __launch_bounds__(kFT) void k_ba_win(BAArgs a, FusedArgs f, WinArgs w
             }
             __syncthreads();
         }
+#ifdef VX_WIN_TRACE_LM  // (trace variant: slot 1 + 3 it = the landmark stage done instead of rows ready)
+        if (wv == 0 && it < 5) VX_KT(1 + 3 * it);
+#endif
         if (it + 1 < M) pose_stage(it + 1);
         if (wv == 0 && it < 4) VX_KT(3 + 3 * it);
     }
