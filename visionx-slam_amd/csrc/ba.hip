@@ -3021,13 +3021,17 @@ int vx_ba_optimize_map(vx_ctx* c, vx_map_view* m, uint64_t ref, int has_ref, con
             std::fprintf(stderr, "[vx optmap] %s %.1f us\n", what,
                          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     };
-    // the lean one-call build on the view loaded into the context's scratch map ($VX_OPTMAP_LEAN=0:
-    // always the plan below, for A/B runs); the plan for a window it does not take
-    static const bool lean_off = [] {
+    // the lean one-call build on the view loaded into the context's scratch map for windows of up to
+    // 64 keyframes; the plan below for larger ones (C3, 50: 0.37 against 0.62 ms; C4, 100: the plan's
+    // fused window wins, 0.93 against 1.20 ms, profiles/r06/bench_c4_r06.json) and for a window the
+    // lean build does not take.  $VX_OPTMAP_LEAN=0 / 1: always the plan / the lean build (A/B runs)
+    static const int lean_env = [] {
         const char* e = getenv("VX_OPTMAP_LEAN");
-        return e && e[0] == '0';
+        return e ? (e[0] == '0' ? 0 : 1) : -1;
     }();
-    if (!lean_off && m && opt && opt->max_iterations >= 0 && opt->max_iterations <= 64) {
+    const bool lean = m && opt && opt->max_iterations >= 0 && opt->max_iterations <= 64 &&
+                      (lean_env == 1 || (lean_env < 0 && std::min(opt->window_size, m->n_kf) <= 64));
+    if (lean) {
         bool fb = false;
         const int rc = lean_optimize_view(c, m, ref, has_ref, *opt, st, &fb);
         lap("lean");
