@@ -112,3 +112,17 @@ def test_sharded_plans_partition_the_window():
         assert sum(p["n_lm_obs"] for p in parts) == full["n_lm_obs"]
         for r, p in enumerate(parts):
             assert all(vxslam.ba_shard_of(int(m["lm_id"][l]), n) == r for l in p["lm_map_idx"])
+
+
+def test_host_alloc_round_trip():
+    """vx_host_alloc: page-locked host memory with a device, plain pageable memory without one (the
+    snapshot arrays of visionx::FlatMap use it); 64-byte aligned, writable, freed by vx_host_free."""
+    L = vxslam.lib()
+    for n in (1, 1000, 1 << 20):
+        p = L.vx_host_alloc(n)
+        assert p and p % 64 == 0
+        buf = (C.c_uint8 * n).from_address(p)
+        buf[n - 1], buf[0] = 9, 7
+        assert (buf[0], buf[n - 1]) == (7, 9 if n > 1 else 7)
+        L.vx_host_free(p)
+    L.vx_host_free(None)

@@ -759,3 +759,40 @@ def test_seq_threads_replay(ctx, oracle, slot_sums):
         x.close()
     for c in ex + [bc]:
         c.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,nk,nl,nold,window,ref", [
+    (0x5EED0301, 10, 2000, 2, 10, None),
+    (0x5EED0302, 20, 5000, 6, 12, None),      # view larger than the window: selection over the view
+    (0x5EED0303, 30, 8000, 4, 16, "mid"),     # reference keyframe inside the view (newer ones skipped)
+    (0x5EED0304, 50, 20000, 2, 50, None),     # C3
+])
+def test_optimize_map_lean_matches_plan(ctx, oracle, seed, nk, nl, nold, window, ref):
+    """vx_ba_optimize_map takes the lean one-call build for windows of <= 64 keyframes (the view
+    loaded into the context's scratch device map): same window, landmark set, stop
+    decisions and per-iteration observation counts as a plan built from the same view, results within
+    the parity tolerance of it and of the restatement."""
+    import vxslam
+
+    m = synth.make_ba_map(seed, nk, nl, n_old_kf=nold)
+    ref_id = None if ref is None else int(np.sort(m["kf_id"])[len(m["kf_id"]) // 2 + 2])
+    kw = dict(window=window)
+    mc = m.copy()
+    st_c = oracle.ba_optimize(mc, oracle.ba_options(**kw), ref_kf_id=ref_id)
+    assert st_c.status != 0 or st_c.gate_margin >= GATE_MARGIN, f"gate margin {st_c.gate_margin}: reseed this case"
+    ml = m.copy()
+    st_l = ctx.ba_optimize(ml, vxslam.default_ba_options(**kw), ref_kf_id=ref_id)
+    mp = m.copy()
+    plan = ctx.ba_plan(mp, vxslam.default_ba_options(**kw), ref_kf_id=ref_id)
+    plan.run_async()
+    st_p = plan.fetch(mp)
+    plan.close()
+    for a, b in ((st_l, st_p), (st_l, st_c)):
+        assert (a.status, a.n_window_kf, a.n_landmarks, a.iterations) == (b.status, b.n_window_kf, b.n_landmarks, b.iterations)
+        assert list(a.obs[:a.iterations]) == list(b.obs[:b.iterations])
+    _assert_ba_close(ml, mp, st_l, st_p)
+    _assert_ba_close(ml, mc, st_l, st_c)
+    # keyframes and landmarks outside the window / landmark set are left as they were
+    changed = np.any(ml["kf_pose"] != m["kf_pose"], axis=1)
+    assert changed.sum() <= st_l.n_window_kf

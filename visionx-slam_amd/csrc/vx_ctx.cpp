@@ -221,7 +221,7 @@ void* vx_host_alloc(size_t bytes) {
     uint32_t kind = 1;
     if (pageable || hipHostMalloc(&p, bytes + kHdr, hipHostMallocNonCoherent) != hipSuccess) {
         (void)hipGetLastError();
-        p = std::malloc(bytes + kHdr);
+        p = std::aligned_alloc(kHdr, (bytes + 2 * kHdr - 1) / kHdr * kHdr);  // (64-byte aligned either way)
         kind = 2;
         if (!p) return nullptr;
     }

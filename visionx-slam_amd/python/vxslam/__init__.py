@@ -118,6 +118,9 @@ def lib():
         L.vx_last_error.argtypes = [C.c_void_p]
         L.vx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
         L.vx_destroy.argtypes = [C.c_void_p]
+        L.vx_host_alloc.restype = C.c_void_p
+        L.vx_host_alloc.argtypes = [C.c_size_t]
+        L.vx_host_free.argtypes = [C.c_void_p]
         L.vx_stream.restype = C.c_void_p
         L.vx_stream.argtypes = [C.c_void_p]
         L.vx_synchronize.argtypes = [C.c_void_p]
