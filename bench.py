@@ -982,7 +982,18 @@ def main():
         bctx.ba_plan(ba_map, opts, shard_rank=dist.rank, shard_count=N).close()
         plan_ms.append(1e3 * (time.perf_counter() - t0))
     plan_build_ms = float(np.median(plan_ms))
-    per_kf = per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam) if N == 1 and not args.no_drop_in else None
+    per_kf = None
+    if N == 1 and not args.no_drop_in:
+        # (the C++ drop-in's subprocess inherits this process's CPUs: the whole affinity set, not the 8
+        # idlest CPUs the pipeline runs on — its host pool binds itself to one L3 slice of those)
+        pinned = os.sched_getaffinity(0)
+        if full_affinity:
+            os.sched_setaffinity(0, full_affinity)
+        try:
+            per_kf = per_keyframe_ms(bctx, ba_map, opts, dist, N, vxslam)
+        finally:
+            if full_affinity:
+                os.sched_setaffinity(0, pinned)
     torch.cuda.synchronize()
 
     # Pipeline.  Frame t: Extract(t) on extraction context t % E (E = --extract-ctx) into that

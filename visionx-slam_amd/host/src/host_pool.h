@@ -76,10 +76,12 @@ private:
         // participants: 8, or with the workers bound to an L3 slice every CPU of that slice up to 16
         // (the GPU box's slices are 8 cores / 16 threads: 16 measured 4 % faster on the snapshot call,
         // 2 % on the resident one, r06s); never more than the CPUs this process may use
+        // (a process confined to a few CPUs spread over slices leaves too few in the creating thread's
+        // slice: then the workers stay unbound rather than share two or three CPUs)
         const char* pin = std::getenv("VX_HOST_PIN");
         cpu_set_t llc;
-        const bool bind = !(pin && pin[0] == '0') && LlcCpus(&llc);
-        int want = bind ? std::max(8, std::min(16, CPU_COUNT(&llc))) : 8;
+        const bool bind = !(pin && pin[0] == '0') && LlcCpus(&llc) && CPU_COUNT(&llc) >= 8;
+        int want = bind ? std::min(16, CPU_COUNT(&llc)) : 8;
         cpu_set_t set;
         if (sched_getaffinity(0, sizeof(set), &set) == 0) want = std::min(want, CPU_COUNT(&set));
         if (const char* e = std::getenv("VX_HOST_THREADS")) want = std::max(1, std::atoi(e));
