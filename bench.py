@@ -839,6 +839,10 @@ def main():
                     help="diagnostics only (the JSON line is marked invalid): leave one stage out of every step")
     ap.add_argument("--diag-nodep", action="store_true",
                     help="diagnostics only (the JSON line is marked invalid): LocalBA(t) does not wait for Match(t)")
+    ap.add_argument("--ba-peer", action="store_true",
+                    help="N > 1: the sharded LocalBA's row sums by the one-shot peer reduction over xGMI "
+                         "($VX_BA_PEER=1: IPC-mapped blocks and generation flags, DESIGN.md §6) instead of one "
+                         "ncclAllReduce per iteration; verified on one GPU by emulation only")
     ap.add_argument("--ba-priority", type=int, default=0, choices=(0, 1),
                     help="stream priority of the LocalBA context (1: the device's greatest)")
     ap.add_argument("--grid-share", type=float, default=None,
@@ -865,6 +869,8 @@ def main():
                          "(default: one hardware queue fewer; measured 0.073 vs 0.073-0.076 ms/frame, steadier) "
                          "or on a context of its own")
     args = ap.parse_args()
+    if args.ba_peer:
+        os.environ["VX_BA_PEER"] = "1"
     args.config_file = None
     if args.config == "C5":
         return bench_c5(args)

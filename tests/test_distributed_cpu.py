@@ -266,3 +266,61 @@ def _sba_shard_worker(rank, world, port):
 
 def test_sharded_schur_system_allreduce():
     _spawn(_sba_shard_worker)
+
+
+def _peer_worker(rank, world, port):
+    """The peer reduction's protocol (ba.hip k_peer_publish / k_peer_gather, $VX_BA_PEER=1) between
+    processes: every rank's block in memory the others map (shared memory here, IPC over xGMI on the
+    GPUs; the names gathered over gloo as the IPC handles are over RCCL), rows double-buffered by
+    generation parity, a flag per block set after the rows; a rank waits for every flag >= gen, then
+    sums the blocks in rank order.  Ranks run at skewed, random speeds: no rank may read a block a
+    faster rank has already overwritten, and every sum must equal the all-reduce of the same rows."""
+    dist = _init(rank, world, port)
+    import time
+    from multiprocessing import shared_memory
+
+    import torch
+
+    nrow = 64
+    rng = np.random.default_rng(1000 + rank)
+    shm = shared_memory.SharedMemory(create=True, size=(2 * nrow + 1) * 8)
+    own = np.ndarray((2 * nrow + 1,), np.float64, buffer=shm.buf)
+    own[:] = 0.0
+    names = [None] * world
+    dist.all_gather_object(names, shm.name)  # (the IPC handle exchange)
+    peers = [shared_memory.SharedMemory(name=nm) for nm in names]
+    blocks = [np.ndarray((2 * nrow + 1,), np.float64, buffer=p.buf) for p in peers]
+    sent, summed = [], []
+    try:
+        for gen in range(1, 41):
+            rows = np.round(rng.normal(size=nrow) * 1e3) + gen * 1e6 + rank  # (exact in float64)
+            par = gen & 1
+            own[par * nrow:(par + 1) * nrow] = rows  # publish, then the flag
+            own[2 * nrow] = float(gen)
+            t0 = time.time()
+            while min(b[2 * nrow] for b in blocks) < gen:
+                assert time.time() - t0 < 20.0, "a flag did not arrive"
+                time.sleep(1e-4)
+            time.sleep(float(rng.random()) * 3e-3)  # (skew: a slow reader while the others run ahead)
+            got = blocks[0][par * nrow:(par + 1) * nrow].copy()
+            for b in blocks[1:]:
+                got += b[par * nrow:(par + 1) * nrow]
+            sent.append(rows)
+            summed.append(got)
+        # (compared only at the end: a collective per generation would hold the ranks in step)
+        ref = torch.from_numpy(np.stack(sent))
+        dist.all_reduce(ref)
+        bad = np.nonzero(~np.all(np.stack(summed) == ref.numpy(), axis=1))[0]
+        assert bad.size == 0, f"rank {rank}: generations {bad + 1} read an overwritten or stale block"
+        dist.barrier()
+    finally:
+        for p in peers:
+            p.close()
+        shm.close()
+        dist.barrier()
+        shm.unlink()
+        dist.destroy_process_group()
+
+
+def test_peer_reduction_protocol():
+    _spawn(_peer_worker)

@@ -182,3 +182,32 @@ def test_sharded_sequence_graph_replay(ctx, n, ba_path):
             assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2:] == b[2:]
     for p in plans:
         p.close()
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_sharded_peer_reduction_matches_rank_order_sum(ctx, monkeypatch, n):
+    """The one-shot peer reduction ($VX_BA_PEER=1: each shard publishes its row sums into its own
+    block with a generation flag, every shard waits for all flags and sums the blocks in rank order)
+    in place of the emulated all-reduce: bitwise the rank-order sum's results — poses, positions and
+    stop decisions — over repeated runs of the same plans (generations advancing, both parities)."""
+    nk, nl = 50 * n, 20000 * n
+    m = synth.make_ba_map(0x5EED0003, nk, nl, n_streams=n, n_old_kf=2 * n)
+    opts = vxslam.default_ba_options(window=nk)
+    monkeypatch.delenv("VX_BA_FUSED", raising=False)
+    monkeypatch.delenv("VX_BA_PEER", raising=False)
+    _, ref_outs, ref_stats = _shard_run(ctx, m, opts, n, "fused")
+    monkeypatch.setenv("VX_BA_PEER", "1")
+    plans = [ctx.ba_plan(m, opts, shard_rank=r, shard_count=n) for r in range(n)]
+    try:
+        for rep in range(3):  # (generations 5 rep + 1 .. 5 rep + 5: both parities, flags from earlier runs)
+            ctx.ba_shard_emulate(plans)
+            for p, ro, rs in zip(plans, ref_outs, ref_stats):
+                mm = m.copy()
+                st = p.fetch(mm)
+                assert (st.iterations, list(st.obs[:16]), list(st.cost[:16])) == \
+                       (rs.iterations, list(rs.obs[:16]), list(rs.cost[:16]))
+                assert np.array_equal(mm["kf_pose"], ro["kf_pose"])
+                assert np.array_equal(mm["lm_pos"], ro["lm_pos"])
+    finally:
+        for p in plans:
+            p.close()

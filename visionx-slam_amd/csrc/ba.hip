@@ -1586,6 +1586,65 @@ __global__ void k_row_sum(const double* part, int n_kf, int maxl, double* rowpar
     rowpart[i] = s;
 }
 
+// ---- one-shot peer reduction of a sharded window's row sums ($VX_BA_PEER=1, opt-in)
+// In place of the per-iteration ncclAllReduce (a ring of 2 (N - 1) dependent steps, latency-bound at
+// 100 KB: DESIGN.md §6): every rank publishes its row sums into a block of its own device memory that
+// every other rank has mapped (IPC over xGMI) and sets the block's flag to the iteration's
+// generation; every rank waits for all N flags and sums the ranks' rows in rank order — the same
+// values on every rank, and bitwise what the one-GPU emulation's k_sum_parts gives.  The rows are
+// double-buffered by generation parity: a rank rewrites parity p at generation g + 2 only after its
+// own wait for every flag >= g + 1, which each rank sets after it has read generation g.  Bounded
+// waits: a flag that does not come sets the state's fault (vx_ba_plan_fetch reports VX_ERR_COMM).
+constexpr int kMaxPeers = 16;
+constexpr long long kPeerSpinTicks = 20'000'000;  // 200 ms of the 100 MHz wall clock
+struct PeerPtrs {
+    const double* rows[kMaxPeers];
+    const unsigned long long* flag[kMaxPeers];
+};
+// this rank's row sums (k_row_sum's arithmetic: slots in slot order) -> its block (parity), then the flag
+__global__ __launch_bounds__(1024) void k_peer_publish(const double* part, int n_kf, int maxl, double* out,
+                                                      unsigned long long* flag, unsigned long long gen) {
+    const int n = n_kf * kStride;
+    for (int i = threadIdx.x; i < n; i += 1024) {
+        const int row = i / kStride, t = i - row * kStride;
+        const double* src = part + (size_t)row * maxl * kStride + t;
+        double s = 0.0;
+        for (int q = 0; q < maxl; ++q) s += src[(size_t)q * kStride];
+        out[i] = s;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// every rank's flag >= gen, then the ranks' rows (parity offset off) summed in rank order -> out
+__global__ __launch_bounds__(1024) void k_peer_gather(PeerPtrs pp, int n_ranks, int len, int off, unsigned long long gen,
+                                                     double* out, int* fault) {
+    __shared__ int s_bad;
+    if (threadIdx.x == 0) s_bad = 0;
+    __syncthreads();
+    if (threadIdx.x < n_ranks) {
+        const long long t0 = wall_clock64();
+        while (__hip_atomic_load(pp.flag[threadIdx.x], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < gen) {
+            if (wall_clock64() - t0 > kPeerSpinTicks) {
+                s_bad = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (threadIdx.x == 0) __hip_atomic_store(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    __threadfence_system();
+    for (int i = threadIdx.x; i < len; i += 1024) {
+        double s = __hip_atomic_load(pp.rows[0] + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        for (int r = 1; r < n_ranks; ++r) s += __hip_atomic_load(pp.rows[r] + off + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        out[i] = s;
+    }
+}
+
 // fused-order observation payloads: uv by plan index (-1: padding), pose records with the fixed
 // landmarks' positions
 __global__ void k_fused_gather(const int* lsrc, int nl, const double2* luv, double2* out_luv, const int* psrc,
@@ -2442,6 +2501,77 @@ int fused_row_sum(vx_ctx* c, vx_ba_plan* p, int it) {
     return VX_OK;
 }
 
+// the peer reduction of iteration it's row sums into f_rowpart (plans set up by peer_setup or the
+// emulation; every rank / shard of the window enqueues the same generations)
+size_t peer_len(const vx_ba_plan* p) { return (size_t)p->n_kf * kStride; }
+int peer_publish(vx_ctx* c, vx_ba_plan* p, int it, unsigned long long gen) {
+    const size_t len = peer_len(p);
+    double* blk = static_cast<double*>(p->peer_mem);
+    if (!blk) return set_error(c, VX_ERR_STATE, "peer reduction: no block of its own");
+    hipLaunchKernelGGL(k_peer_publish, dim3(1), dim3(1024), 0, c->stream,
+                       (const double*)(p->f_part.as<double>() + (size_t)(it & 1) * p->n_kf * p->f_maxl * kStride), p->n_kf,
+                       p->f_maxl, blk + (gen & 1) * len, reinterpret_cast<unsigned long long*>(blk + 2 * len), gen);
+    VX_LAUNCH_CHECK(c, "k_peer_publish");
+    return VX_OK;
+}
+int peer_gather(vx_ctx* c, vx_ba_plan* p, unsigned long long gen) {
+    const size_t len = peer_len(p);
+    const int n = (int)p->peer_base.size();
+    PeerPtrs pp{};
+    if (n < 1 || n > kMaxPeers) return set_error(c, VX_ERR_STATE, "peer reduction: %d ranks", n);
+    for (int r = 0; r < n; ++r) {
+        const double* b = static_cast<const double*>(p->peer_base[r]);
+        if (!b) return set_error(c, VX_ERR_STATE, "peer reduction: rank %d's block is not mapped", r);
+        pp.rows[r] = b;
+        pp.flag[r] = reinterpret_cast<const unsigned long long*>(b + 2 * len);
+    }
+    hipLaunchKernelGGL(k_peer_gather, dim3(1), dim3(1024), 0, c->stream, pp, n, (int)len, (int)((gen & 1) * len), gen,
+                       p->f_rowpart.as<double>(), reinterpret_cast<int*>(p->state.as<uint8_t>() + offsetof(BAState, fault)));
+    VX_LAUNCH_CHECK(c, "k_peer_gather");
+    return VX_OK;
+}
+size_t peer_bytes(const vx_ba_plan* p) { return ((2 * peer_len(p) + 8) * sizeof(double) + 4095) & ~(size_t)4095; }
+
+#ifndef VX_NO_RCCL
+// this rank's block (uncached device memory: the peers read it over xGMI), its IPC handle gathered
+// from every rank over RCCL, the peers' blocks opened; once per plan, at its first sharded run
+int peer_setup(vx_ctx* c, vx_ba_plan* p) {
+    const int n = p->shard_count, me = p->shard_rank;
+    if (n > kMaxPeers) return set_error(c, VX_ERR_INVALID, "$VX_BA_PEER: at most %d ranks", kMaxPeers);
+    const size_t bytes = peer_bytes(p);
+    VX_HIP(c, hipExtMallocWithFlags(&p->peer_mem, bytes, hipDeviceMallocUncached));
+    VX_HIP(c, hipMemsetAsync(p->peer_mem, 0, bytes, c->stream));  // (flags 0 before any rank can read them)
+    hipIpcMemHandle_t h;
+    VX_HIP(c, hipIpcGetMemHandle(&h, p->peer_mem));
+    DevBuf d;
+    VX_HIP(c, d.ensure((size_t)n * sizeof h));
+    VX_HIP(c, hipMemcpyAsync(d.as<uint8_t>() + (size_t)me * sizeof h, &h, sizeof h, hipMemcpyHostToDevice, c->stream));
+    ncclResult_t r = ncclAllGather(d.as<uint8_t>() + (size_t)me * sizeof h, d.p, sizeof h, ncclUint8, c->comm, c->stream);
+    if (r != ncclSuccess) return set_error(c, VX_ERR_COMM, "ncclAllGather (peer handles): %s", ncclGetErrorString(r));
+    std::vector<hipIpcMemHandle_t> all(n);
+    VX_HIP(c, hipMemcpyAsync(all.data(), d.p, (size_t)n * sizeof h, hipMemcpyDeviceToHost, c->stream));
+    VX_HIP(c, hipStreamSynchronize(c->stream));
+    p->peer_base.assign(n, nullptr);
+    for (int q = 0; q < n; ++q) {
+        if (q == me) {
+            p->peer_base[q] = p->peer_mem;
+            continue;
+        }
+        void* ptr = nullptr;
+        VX_HIP(c, hipIpcOpenMemHandle(&ptr, all[q], hipIpcMemLazyEnablePeerAccess));
+        p->peer_opened.push_back(ptr);
+        p->peer_base[q] = ptr;
+    }
+    p->peer = true;
+    return VX_OK;
+}
+#endif
+
+bool peer_requested() {
+    const char* e = getenv("VX_BA_PEER");
+    return e && e[0] == '1';
+}
+
 WinArgs make_win_args(vx_ba_plan* p) {
     uint8_t* W = p->f_win.as<uint8_t>();
     WinArgs w{};
@@ -2473,8 +2603,14 @@ int plan_run_fused(vx_ctx* c, vx_ba_plan* p) {
         return VX_OK;
     }
     if ((rc = fused_launch(c, p, a, f, -1))) return rc;
+#ifndef VX_NO_RCCL
+    if (p->shard_count > 1 && !p->peer && peer_requested() && (rc = peer_setup(c, p))) return rc;
+#endif
     for (int it = 0; it < p->opt.max_iterations; ++it) {
-        if (p->shard_count > 1) {
+        if (p->shard_count > 1 && p->peer) {  // the one-shot peer reduction
+            const unsigned long long gen = ++p->peer_gen;
+            if ((rc = peer_publish(c, p, it, gen)) || (rc = peer_gather(c, p, gen))) return rc;
+        } else if (p->shard_count > 1) {
 #ifndef VX_NO_RCCL
             if ((rc = fused_row_sum(c, p, it))) return rc;
             ProfScope ps(c, kStBaAllreduce);
@@ -2762,7 +2898,8 @@ int vx_ba_shard_emulate_run(vx_ctx* c, vx_ba_plan* const* plans, int n) {
     std::vector<uint64_t> key{0xE3u, (uint64_t)n};
     for (int r = 0; r < n; ++r) key.push_back((uint64_t)(uintptr_t)plans[r]);
     EmuArgs ea{plans, n};
-    if (plans[0]->status != 0 || !plans[0]->choice_made) return shard_emulate_enqueue(c, plans, n);  // (decides the kernels)
+    // (eager: the first run decides the kernels; the peer reduction's generations change every run)
+    if (plans[0]->status != 0 || !plans[0]->choice_made || peer_requested()) return shard_emulate_enqueue(c, plans, n);
     for (int r = 0; r < n; ++r) plans[r]->ran = true;
     return graph_run(c, key, [](vx_ctx* cc, void* v) {
         const EmuArgs* x = static_cast<const EmuArgs*>(v);
@@ -2807,14 +2944,39 @@ int shard_emulate_enqueue(vx_ctx* c, vx_ba_plan* const* plans, int n) {
             if ((rc = reset_if_no_iterations(c, plans[r], args[r]))) return rc;
         }
         const long long len = (long long)p0->n_kf * kStride;
+        // $VX_BA_PEER=1: the peer reduction's kernels in place of k_sum_parts, each shard's block in
+        // device memory of its own and every shard's base table naming all of them (the IPC mapping
+        // of a real multi-GPU run), generations as a real run counts them
+        const bool peer = peer_requested();
+        if (peer) {
+            for (int r = 0; r < n; ++r)
+                if (!plans[r]->peer_mem) {
+                    VX_HIP(c, hipMalloc(&plans[r]->peer_mem, peer_bytes(plans[r])));
+                    VX_HIP(c, hipMemsetAsync(plans[r]->peer_mem, 0, peer_bytes(plans[r]), c->stream));
+                }
+            for (int r = 0; r < n; ++r) {  // (every block allocated before any table names it)
+                plans[r]->peer_base.assign(n, nullptr);
+                for (int q = 0; q < n; ++q) plans[r]->peer_base[q] = plans[q]->peer_mem;
+            }
+        }
         if (p0->opt.max_iterations > 0)
             for (int r = 0; r < n; ++r)
                 if ((rc = fused_launch(c, plans[r], args[r], fargs[r], -1))) return rc;
         for (int it = 0; it < p0->opt.max_iterations; ++it) {
-            for (int r = 0; r < n; ++r)
-                if ((rc = fused_row_sum(c, plans[r], it))) return rc;
-            hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, c->stream, rows, n, len);
-            VX_LAUNCH_CHECK(c, "k_sum_parts");
+            if (peer) {
+                const unsigned long long gen = p0->peer_gen + 1;
+                for (int r = 0; r < n; ++r) {
+                    plans[r]->peer_gen = gen;
+                    if ((rc = peer_publish(c, plans[r], it, gen))) return rc;
+                }
+                for (int r = 0; r < n; ++r)
+                    if ((rc = peer_gather(c, plans[r], gen))) return rc;
+            } else {
+                for (int r = 0; r < n; ++r)
+                    if ((rc = fused_row_sum(c, plans[r], it))) return rc;
+                hipLaunchKernelGGL(k_sum_parts, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, c->stream, rows, n, len);
+                VX_LAUNCH_CHECK(c, "k_sum_parts");
+            }
             for (int r = 0; r < n; ++r)
                 if ((rc = fused_launch(c, plans[r], args[r], fargs[r], it))) return rc;
         }
@@ -2873,6 +3035,8 @@ int vx_ba_plan_fetch(vx_ctx* c, vx_ba_plan* p, vx_map_view* m, vx_ba_stats* st) 
         if (rc) return rc;
         BAState hs;
         std::memcpy(&hs, H, sb);
+        if (hs.fault && !p->peer_base.empty() && p->shard_count > 1)
+            return set_error(c, VX_ERR_COMM, "peer reduction: a rank's row sums did not arrive within 200 ms");
         if (hs.fault && win_active(p)) {
             // a persistent window whose wait ran out (its workgroups could not all be resident at
             // once): the run is void; the plan keeps the per-iteration launches from now on and
@@ -2929,6 +3093,8 @@ void vx_ba_plan_destroy(vx_ba_plan* p) {
             c->plan_husks.push_back(h);
         }
     }
+    for (void* q : p->peer_opened) (void)hipIpcCloseMemHandle(q);
+    if (p->peer_mem) (void)hipFree(p->peer_mem);
     delete p;
 }
 

@@ -54,6 +54,14 @@ struct vx_ba_plan {
     int f_stop_b = 0;            // workgroup running the stop rule
     vx::PinnedBuf f_stage;                                        // their host staging block
     vx::PinnedBuf fetch_host;  // vx_ba_plan_fetch: the state, both pose parities and the positions, one copy each
+    // sharded plans, $VX_BA_PEER=1: the one-shot peer reduction of the row sums in place of the
+    // per-iteration ncclAllReduce (ba.hip, k_peer_publish / k_peer_gather).  peer_mem: this rank's
+    // block ([2][n_kf x kStride] doubles by generation parity, then the flag); peer_base[r]: rank r's
+    // block as this device sees it (IPC-mapped, or another plan's block in the one-GPU emulation)
+    bool peer = false;
+    void* peer_mem = nullptr;
+    std::vector<void*> peer_base, peer_opened;
+    unsigned long long peer_gen = 0;
     FusedOffsets f_off;                                           // byte offsets of the tables in f_tab
     size_t f_npp = 0;                                             // pose-observation positions (padded)
 };
