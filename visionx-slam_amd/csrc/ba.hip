@@ -2538,6 +2538,9 @@ size_t peer_bytes(const vx_ba_plan* p) { return ((2 * peer_len(p) + 8) * sizeof(
 int peer_setup(vx_ctx* c, vx_ba_plan* p) {
     const int n = p->shard_count, me = p->shard_rank;
     if (n > kMaxPeers) return set_error(c, VX_ERR_INVALID, "$VX_BA_PEER: at most %d ranks", kMaxPeers);
+    if (c->nranks != n || c->rank != me)  // (the handle table is indexed by communicator rank)
+        return set_error(c, VX_ERR_INVALID, "$VX_BA_PEER: shard %d of %d on communicator rank %d of %d", me, n, c->rank,
+                         c->nranks);
     const size_t bytes = peer_bytes(p);
     VX_HIP(c, hipExtMallocWithFlags(&p->peer_mem, bytes, hipDeviceMallocUncached));
     VX_HIP(c, hipMemsetAsync(p->peer_mem, 0, bytes, c->stream));  // (flags 0 before any rank can read them)
@@ -2855,10 +2858,11 @@ int vx_ba_plan_run_async(vx_ctx* c, vx_ba_plan* p) {
     // rank and synchronises); later runs replay ONE hipGraph of the whole sequence, the per-iteration
     // k_row_sum -> ncclAllReduce -> k_ba_iter chain included (RCCL collectives are capturable: the
     // graph holds their kernels).  A capture that fails leaves the plan eager; $VX_SHARDED_GRAPHS=0
-    // keeps every sharded run eager.
+    // keeps every sharded run eager, and so does the peer reduction ($VX_BA_PEER=1).
     if (p->shard_count > 1) {
         const char* e = std::getenv("VX_SHARDED_GRAPHS");
-        if (!p->choice_made || p->graph_eager || (e && e[0] == '0')) return plan_run(c, p);
+        // (the peer reduction stays eager: its generations change from run to run)
+        if (!p->choice_made || p->graph_eager || p->peer || peer_requested() || (e && e[0] == '0')) return plan_run(c, p);
         const bool capturing = c->use_graphs && !c->prof && p->graph.seen && !p->graph.exec;
         p->ran = true;
         const int rc =
