@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel durations of the Schur solve from a rocprofv3 kernel trace (scripts/gpu_r05_v.sh), and
+"""Per-kernel durations of the Schur solve from a rocprofv3 kernel trace (scripts/jobs/gpu_r05_v.sh), and
 the time between consecutive launches of the factor (end of one to the start of the next).
 
     python3 scripts/sba_gaps.py <rocprofv3 output dir>
