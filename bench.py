@@ -1098,7 +1098,7 @@ def main():
     # One timed step = F frames, eight rounds of the pipeline (F = 8 E by default): each of them runs
     # Extract, Match and LocalBA.  With one frame per step the pipeline's fill (one frame's whole
     # latency, ~0.19 ms at C3) weighed ~10 % in the driver's 20-step run; measured 20-step / 2000-step:
-    # 1.5-4.6 % with 12 frames, 1-6 % with 6, box noise ~2 % (scripts/gpu_r03_short_vs_long.sh); 24
+    # 1.5-4.6 % with 12 frames, 1-6 % with 6, box noise ~2 % (scripts/jobs/gpu_r03_short_vs_long.sh); 24
     # frames against 12, alternating: 20-step runs 0.0688-0.0699 against 0.0694-0.0711 ms/frame,
     # 2000-step runs the same (scripts/gpu_fps_ab.sh, profiles/r04/host/fps_ab.txt)
     F = args.frames_per_step if args.frames_per_step > 0 else (8 * E if args.streams == 3 else 1)
@@ -1167,19 +1167,31 @@ def main():
 
     # ---- profiling pass (HIP events on the library stream, every stage) -> dominant kernel
     stages = {}
+    # (chunks of 5 steps, at least four: a stage's duration is the median of the chunks' averages —
+    # in one 5-step pass, the driver's --warmup 5, a run of persistent windows launched while the
+    # extraction kernels held the CUs they wait for once doubled the average, r06final2)
+    n_chunk = max(4, (args.warmup + 4) // 5)
+    n_prof = 5 * n_chunk
     if not args.no_profile:
         for c in ctxs:
             c.prof_enable(True)
-        for i in range(args.warmup):
-            fstep(i)
-        prof = {}
-        for c in ctxs:  # (a stage that runs on several contexts — the extraction ones — is summed)
-            for k, v in c.prof_read(reset=True).items():
-                if v[1]:
-                    t, n = prof.get(k, (0.0, 0))
-                    prof[k] = (t + v[0], n + v[1])
+        chunks = []
+        for ch in range(n_chunk):
+            for i in range(5):
+                fstep(5 * ch + i)
+            prof = {}
+            for c in ctxs:  # (a stage that runs on several contexts — the extraction ones — is summed)
+                for k, v in c.prof_read(reset=True).items():
+                    if v[1]:
+                        t, n = prof.get(k, (0.0, 0))
+                        prof[k] = (t + v[0], n + v[1])
+            chunks.append(prof)
+        for c in ctxs:
             c.prof_enable(False)
-        stages = {k: (v[0] / max(v[1], 1), v[1] / args.warmup) for k, v in prof.items() if v[1]}
+        for k in {k for p in chunks for k in p}:
+            per = [p[k][0] / p[k][1] for p in chunks if k in p and p[k][1]]
+            launches = sum(p[k][1] for p in chunks if k in p)
+            stages[k] = (float(np.median(per)), launches / n_prof)
 
     # ---- the timed region: no events inside (a timing event pair per launch costs ~25 % here)
     elapsed = timed_loop(fstep, args.steps, args.warmup, sync, dist)
@@ -1239,7 +1251,8 @@ def main():
             roofline = {"kernel": dominant, "hip_kernel": HIP_KERNEL.get(dominant), "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                         "bytes_per_launch": int(nbytes), "avg_launch_us": round(avg_ms * 1e3, 2),
-                        "avg_launch_us_source": "profiling pass (stages_us), per-dispatch timestamps",
+                        "avg_launch_us_source": "profiling pass (stages_us): per-dispatch timestamps, the median of "
+                                                f"{n_chunk} five-step chunks' averages",
                         "avg_launch_us_dominant_pass": round(1e3 * dom_prof[0] / dom_prof[1], 2),
                         "launches_per_step": round(dom_prof[1] / args.steps, 2),
                         "pass_ms_per_step": round(1e3 * elapsed_ev / args.steps, 4)}
