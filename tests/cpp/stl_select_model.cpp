@@ -93,10 +93,23 @@ static int pass(std::vector<u64>& A, int f0, int l, IsL isl, IsR isr) {
         if (isl(A[p]) && Lb[i] < K) boxL[Lb[i]] = A[p];
         if (isr(A[p]) && nR - 1 - Rb[i] < K) boxR[nR - 1 - Rb[i]] = A[p];
     }
+    // The device passes decide every swap without K: an L of rank Lb is swapped iff more than Lb R
+    // lie after it (Lb + Rb + isR < nR), an R iff more than its right rank of L lie before it
+    // (Lb + Rb >= nR); the cut is the first position that is an unswapped L or a swapped R.
+    int cut2 = INT32_MAX;
     for (int p = f0; p < l; ++p) {  // a position is never both a swapped L and a swapped R
         const int i = p - f0;
         const bool sl = isl(A[p]) && Lb[i] < K, sr = isr(A[p]) && nR - 1 - Rb[i] < K;
         if (sl && sr) { std::printf("position both swapped\n"); std::exit(3); }
+        const bool sl2 = isl(A[p]) && Lb[i] + Rb[i] + (int)isr(A[p]) < nR;
+        const bool sr2 = isr(A[p]) && Lb[i] + Rb[i] >= nR;
+        if (sl2 != sl || sr2 != sr) { std::printf("rank-sum swap rule differs\n"); std::exit(3); }
+        if (cut2 == INT32_MAX && ((isl(A[p]) && !sl2) || sr2)) cut2 = p;
+    }
+    if (cut2 != cut) { std::printf("first-position cut differs\n"); std::exit(3); }
+    for (int p = f0; p < l; ++p) {
+        const int i = p - f0;
+        const bool sl = isl(A[p]) && Lb[i] < K, sr = isr(A[p]) && nR - 1 - Rb[i] < K;
         if (sl) A[p] = boxR[Lb[i]];
         else if (sr) A[p] = boxL[nR - 1 - Rb[i]];
     }

@@ -1230,14 +1230,11 @@ __device__ __forceinline__ int team_pass(T* __restrict__ A, T* __restrict__ bl, 
 // NB blocks, a power of two fixed at compile time), partitions it there and writes back the
 // elements that moved: its instruction count follows the range, so the long tail of short
 // introselect steps stays cheap.  Ranges of up to kRgWave run on wave 0 alone (pivot candidates
-// are broadcast loads, the crossing and the cut come from ballots and scalar selects, the mailboxes
-// need no barrier); the last steps of a range of <= 64 stay in wave 0's registers (rg_tail64).
-// Longer ranges (up to RgCap: 8192 u32 / 4096 u64) run as team passes spread over kRgSpread waves
-// (16: four per SIMD, up to 8 blocks each): counts, crossing candidates and every L / R of rank
-// below the mailbox bound with its position go through LDS, three barriers a pass.
-// The crossing (per wave, the K of the Hoare formulation above): g(x) = #L in [lo, x) -
-// #R in [x, l) never decreases, K = max(#R from x*, #L before x* - 1) at the first x* with
-// g(x*) >= 0 (K = 0 when there is no R), read off the first nonzero per-block ballot of g >= 0.
+// are broadcast loads, the swaps and the cut come from lane ranks and ballots (swap_l / swap_r
+// below), the mailboxes need no barrier); the last steps of a range of <= 64 stay in wave 0's
+// registers (rg_tail64).  Longer ranges (up to RgCap: 8192 u32 / 4096 u64) run as team passes
+// spread over kRgSpread waves (16: four per SIMD, up to 8 blocks each): block counts, the swapped
+// elements and per-wave cut candidates go through LDS, three barriers a pass.
 template <class T> struct RgCap { static constexpr int v = sizeof(T) == 4 ? 8192 : 4096; };
 constexpr int kRgCap32 = 8192;                 // C4 level 0: ~6.9k FAST candidates
 #ifndef VX_SEL_WAVE
@@ -1255,8 +1252,8 @@ static_assert(kRgBytes % 16 == 0, "engine scratch alignment");
 static_assert(kRgCap32 <= 64 * 8 * kStlWaves && RgCap<u64>::v <= 64 * 8 * kStlWaves,
               "a team pass (<= 8 blocks a wave) must cover the engine's capacity: VX_SEL_THREADS >= 1024");
 
-// the engine's LDS: value mailboxes bl / br, position mailboxes lp / rp (team passes), a few ints
-// (per-wave counts and crossing candidates, results)
+// the engine's LDS: value mailboxes bl / br, (unused) position mailboxes lp / rp, a few ints
+// (per-wave counts and cut candidates, results)
 struct RgLds {
     unsigned char* p;
     template <class T> __device__ __forceinline__ T* bl() const { return reinterpret_cast<T*>(p); }
@@ -1269,13 +1266,10 @@ struct RgLds {
     template <class T> __device__ __forceinline__ T* tv() const {
         return reinterpret_cast<T*>(p + kRgTrash) + (threadIdx.x & 63);
     }
-    __device__ __forceinline__ int* ti() const { return reinterpret_cast<int*>(p + kRgTrash + 64 * 8) + (threadIdx.x & 63); }
     // the same as element indices from p (selects between LDS slots stay integer selects: a select
     // between pointers is turned into branches around each access)
     template <class T> static constexpr int kBr = kRgMail / (int)sizeof(T);
     template <class T> static constexpr int kTv = kRgTrash / (int)sizeof(T);
-    static constexpr int kS = (4 * kRgMail + 32) / 4, kLp = 2 * kRgMail / 4, kRp = 3 * kRgMail / 4;
-    static constexpr int kTi = (kRgTrash + 64 * 8) / 4;
 };
 
 // position x of the blocks starting at q0 := val (x anywhere; compares positions, never the block
@@ -1317,7 +1311,8 @@ __device__ __forceinline__ void rg_store(const T (&v)[NB], T* __restrict__ A, in
 
 // Per block the pass keeps the lane's L / R flags (lane masks; their ballots are the block's
 // masks), its L rank (#L before it in the range) and its R rank from the left, both from mbcnt
-// with the running prefix as base.  Block counts are scalar popcounts of the masks.
+// with the running prefix as base (ql / qr: the prefixes in, the totals out).  Block counts are
+// scalar popcounts of the masks.
 __device__ __forceinline__ int mbcnt(u64 m, int base) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, (unsigned)base));
 }
@@ -1338,7 +1333,7 @@ __device__ __forceinline__ void rg_masks(const T (&v)[NB], int q0, int lo, int l
     }
 }
 template <int NB>
-__device__ __forceinline__ void rg_ranks(const bool (&il)[NB], const bool (&ir)[NB], int ql, int qr, int (&ra)[NB],
+__device__ __forceinline__ void rg_ranks(const bool (&il)[NB], const bool (&ir)[NB], int& ql, int& qr, int (&ra)[NB],
                                          int (&rb)[NB]) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -1350,37 +1345,14 @@ __device__ __forceinline__ void rg_ranks(const bool (&il)[NB], const bool (&ir)[
     }
 }
 
-// The crossing in one wave's blocks (prefix counts ql / qr of the L / R before them, nr R in the
-// whole range): K if x* lies in them, else 0.  Per lane, g(x + 1) = #L + #R in [lo, x] - nr =
-// ra + rb + il + ir - nr never decreases along the range, so x* - 1 is the first set bit of the
-// first nonzero ballot(g(x + 1) >= 0); K = max(#R in [x*, l), #L in [lo, x* - 1)) from that
-// block's prefix counts and masks.  Branch-free: a scalar select chain over the blocks.
-template <int NB>
-__device__ __forceinline__ int rg_crossing(const bool (&il)[NB], const bool (&ir)[NB], const int (&ra)[NB],
-                                           const int (&rb)[NB], int ql, int qr, int nr) {
-    if (ql + qr - nr >= 0) return 0;  // g >= 0 already before these blocks: x* lies before them
-    u64 gx = 0, mlx = 0, mrx = 0;
-    int qlx = 0, qrx = 0;
-    bool found = false;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) {
-        const u64 ml = __ballot(il[j]), mr = __ballot(ir[j]);
-        const u64 g = __ballot(ra[j] + rb[j] + (int)il[j] + (int)ir[j] - nr >= 0);
-        const bool take = !found && g != 0ull;
-        gx = take ? g : gx;
-        mlx = take ? ml : mlx;
-        mrx = take ? mr : mrx;
-        qlx = take ? ql : qlx;
-        qrx = take ? qr : qrx;
-        found = found || g != 0ull;
-        ql += __popcll(ml);
-        qr += __popcll(mr);
-    }
-    if (!found) return 0;
-    const int t = __ffsll((long long)gx) - 1;
-    const u64 below = (1ull << t) - 1ull;
-    return max(nr - (qrx + __popcll(mrx & (below | (1ull << t)))), qlx + __popcll(mlx & below));
-}
+// Which elements a pass swaps, without the swap count K: the L of rank ra (#L before it) is swapped
+// iff more than ra R lie after it (ra + rb + ir < nr, rb = #R before it), an R iff more L than its
+// right rank (nr - 1 - rb) lie before it (ra + rb >= nr) — the k-th L from the left and the k-th R
+// from the right are exchanged exactly while the former lies left of the latter.  The cut
+// min(L[K], R[K - 1]) is the first position holding an unswapped L or a swapped R.  Both rules are
+// checked against the K-based formulation and the real STL by tests/cpp/stl_select_model.cpp.
+__device__ __forceinline__ bool swap_l(bool il, bool ir, int ra, int rb, int nr) { return il && ra + rb + (int)ir < nr; }
+__device__ __forceinline__ bool swap_r(bool ir, int ra, int rb, int nr) { return ir && ra + rb >= nr; }
 
 // inclusive prefix sum / max over each 16-lane row (DPP row shifts; lanes shifted in read 0)
 __device__ __forceinline__ int row_scan_add(int x) {
@@ -1402,15 +1374,14 @@ static_assert(kStlWaves <= 16, "team counts are scanned within one DPP row");
 // One pass by wave 0 alone over A[0, len) (A = the range's first element): kPivot, an
 // introselect step (median of (1, len / 2, len - 1) moved to 0, unguarded partition of [1, len)
 // around it, L = !(x > P), R = !(P > x)); otherwise std::partition of [0, len) by key >= thr
-// (L = key < thr, R = key >= thr).  Swap k < K exchanges the L of rank k with the R of rank k from
-// the right through the mailboxes (an element is swapped at most once: its L and R ranks are never
-// both < K).  Every LDS access is unconditional, lanes with nothing to move using their trash
-// slot: the pass is straight-line VALU + LDS code, no exec-mask branches.  Returns the cut
-// min(L[K], R[K - 1]) (relative to A; both candidates written to s[50] / s[51]); n_r = #R.
+// (L = key < thr, R = key >= thr).  The swapped L of rank k exchanges with the R of rank k from
+// the right through the mailboxes (swap_l / swap_r: an element is swapped at most once).  Every
+// LDS access is unconditional, lanes with nothing to move using their trash slot: the pass is
+// straight-line VALU + LDS code, no exec-mask branches.  Returns the cut min(L[K], R[K - 1])
+// (relative to A; the first unswapped L or swapped R, from the blocks' ballots); n_r = #R.
 template <int NB, bool kPivot, class T>
 __device__ __forceinline__ int rg_wave_pass(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
     const int lane = threadIdx.x & 63;
-    int* s = E.s();
     T v[NB];
     rg_load(v, A, 0, len);
     unsigned P = thr;
@@ -1425,51 +1396,47 @@ __device__ __forceinline__ int rg_wave_pass(T* __restrict__ A, int len, unsigned
         rg_put(v, 0, m, vf);
         lo = 1;
     }
-    bool il[NB], ir[NB];
+    bool il[NB], ir[NB], sl[NB], sr[NB];
     int ra[NB], rb[NB];
     rg_masks<NB, kPivot>(v, 0, lo, len, P, il, ir);
-    rg_ranks(il, ir, 0, 0, ra, rb);
-    int nr = 0;
-#pragma unroll
-    for (int j = 0; j < NB; ++j) nr += __popcll(__ballot(ir[j]));
-    const int K = rg_crossing(il, ir, ra, rb, 0, 0, nr);
-    const int hr = K > 0 ? nr - K : INT_MAX;  // the R with left rank >= hr are swapped; R[K - 1] has rank hr
-    T* eb = E.bl<T>();                          // element slots: bl, then br, then the trash
-    int* ei = reinterpret_cast<int*>(E.p);      // int slots: s, trash
+    int nl = 0, nr = 0;
+    rg_ranks(il, ir, nl, nr, ra, rb);
+    T* eb = E.bl<T>();  // element slots: bl, then br, then the trash
     constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
-    if (lane == 0) *reinterpret_cast<int2*>(s + 50) = make_int2(INT_MAX, INT_MAX);
+    int cut = INT_MAX;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-        const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
-        eb[sl ? ra[j] : sr ? kBr + (nr - 1 - rb[j]) : kTv + lane] = v[j];
-        ei[(il[j] && ra[j] == K) ? RgLds::kS + 50 : (ir[j] && rb[j] == hr) ? RgLds::kS + 51 : RgLds::kTi + lane] =
-            64 * j + lane;
+        sl[j] = swap_l(il[j], ir[j], ra[j], rb[j], nr);
+        sr[j] = swap_r(ir[j], ra[j], rb[j], nr);
+        eb[sl[j] ? ra[j] : sr[j] ? kBr + (nr - 1 - rb[j]) : kTv + lane] = v[j];
+        if (kPivot) {
+            const u64 c = __ballot((il[j] && !sl[j]) || sr[j]);
+            cut = (cut == INT_MAX && c != 0ull) ? 64 * j + __ffsll((long long)c) - 1 : cut;
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     T nv[NB];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {  // every read issued before the first store
-        const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr;
-        nv[j] = eb[sl ? kBr + ra[j] : sr ? nr - 1 - rb[j] : kTv + lane];
-    }
+    for (int j = 0; j < NB; ++j)  // every read issued before the first store
+        nv[j] = eb[sl[j] ? kBr + ra[j] : sr[j] ? nr - 1 - rb[j] : kTv + lane];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
         const int x = 64 * j + lane;
-        const bool sw = (il[j] && ra[j] < K) || (ir[j] && rb[j] >= hr);
+        const bool sw = sl[j] || sr[j];
         if (sw || (kPivot && (x == 0 || x == m))) A[x] = sw ? nv[j] : v[j];
     }
-    const int2 cc = *reinterpret_cast<const int2*>(s + 50);
-    const int cut = min(max(min(uni(cc.x), uni(cc.y)), 1), len);  // (clamped: memory-safe whatever happens)
+    cut = min(max(cut, 1), len);  // (clamped: memory-safe whatever happens)
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (the next pass reloads; global scratch too)
     n_r = nr;
     return cut;
 }
 
 // The same pass by the workgroup over A[0, len), len <= 64 NB kStlWaves: wave w holds the blocks
-// [NB w, NB (w + 1)); waves past the range only meet the barriers.  Before the second barrier every
-// L and every R of rank below hb = (len - lo) / 2 + 1 >= K goes to the mailboxes with its position
-// (the cut's candidates), so the swaps need no third exchange.  Branch-free LDS traffic as above.
+// [NB w, NB (w + 1)); waves past the range only meet the barriers.  After the first barrier (block
+// counts scanned over the waves) every swapped element goes to its mailbox and each wave posts its
+// first cut candidate (an unswapped L or a swapped R); after the second the swaps are read back and
+// the cut is the least candidate.  Branch-free LDS traffic as above.
 template <int NB, bool kPivot, class T>
 __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned thr, const RgLds& E, int& n_r) {
     constexpr int NW = kStlWaves;
@@ -1478,13 +1445,10 @@ __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned
     const int q0 = 64 * NB * w;
     const bool act = q0 < len;
     int* s = E.s();
-    int* lp = E.lp();
-    int* rp = E.rp();
     T* eb = E.bl<T>();
-    int* ei = reinterpret_cast<int*>(E.p);
     constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
     T v[NB];
-    bool il[NB], ir[NB];
+    bool il[NB], ir[NB], sl[NB], sr[NB];
     int ra[NB], rb[NB];
     unsigned P = thr;
     int lo = 0, m = -1;
@@ -1514,49 +1478,43 @@ __device__ __forceinline__ int rg_team_pass(T* __restrict__ A, int len, unsigned
     }
     if (lane == 0) *reinterpret_cast<int2*>(s + 2 * w) = make_int2(cl, cr);
     __syncthreads();
-    int pl, pr, nl, nr;
+    int pl, pr, nr;
     {
         const int2 c2 = lane < NW ? *reinterpret_cast<const int2*>(s + 2 * lane) : make_int2(0, 0);
-        const int sl = row_scan_add(c2.x), sr = row_scan_add(c2.y);
-        pl = w > 0 ? __builtin_amdgcn_readlane(sl, w - 1) : 0;
-        pr = w > 0 ? __builtin_amdgcn_readlane(sr, w - 1) : 0;
-        nl = __builtin_amdgcn_readlane(sl, NW - 1);
-        nr = __builtin_amdgcn_readlane(sr, NW - 1);
+        const int xl = row_scan_add(c2.x), xr = row_scan_add(c2.y);
+        pl = w > 0 ? __builtin_amdgcn_readlane(xl, w - 1) : 0;
+        pr = w > 0 ? __builtin_amdgcn_readlane(xr, w - 1) : 0;
+        nr = __builtin_amdgcn_readlane(xr, NW - 1);
     }
-    const int hb = (len - lo) / 2 + 1;
+    int cw = INT_MAX;  // this wave's first cut candidate
     if (act) {
         rg_ranks(il, ir, pl, pr, ra, rb);
-        const int km = rg_crossing(il, ir, ra, rb, pl, pr, nr);
-        if (lane == 0) s[2 * NW + w] = km;
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
-            const int x = q0 + 64 * j + lane, b = nr - 1 - rb[j];
-            const bool wl = il[j] && ra[j] < hb, wr = ir[j] && b < hb;
-            eb[wl ? ra[j] : kTv + lane] = v[j];
-            ei[wl ? RgLds::kLp + ra[j] : RgLds::kTi + lane] = x;
-            eb[wr ? kBr + b : kTv + lane] = v[j];
-            ei[wr ? RgLds::kRp + b : RgLds::kTi + lane] = x;
+            sl[j] = swap_l(il[j], ir[j], ra[j], rb[j], nr);
+            sr[j] = swap_r(ir[j], ra[j], rb[j], nr);
+            eb[sl[j] ? ra[j] : sr[j] ? kBr + (nr - 1 - rb[j]) : kTv + lane] = v[j];
+            if (kPivot) {
+                const u64 c = __ballot((il[j] && !sl[j]) || sr[j]);
+                cw = (cw == INT_MAX && c != 0ull) ? q0 + 64 * j + __ffsll((long long)c) - 1 : cw;
+            }
         }
-    } else if (lane == 0) {
-        s[2 * NW + w] = 0;
     }
+    if (kPivot && lane == 0) s[2 * NW + w] = INT_MAX - cw;  // (>= 0: max-reduced below)
     __syncthreads();
-    const int K = __builtin_amdgcn_readlane(row_scan_max(lane < NW ? s[2 * NW + lane] : 0), NW - 1);
-    int cut = K < nl ? uni(lp[K]) : INT_MAX;
-    if (K > 0) cut = min(cut, uni(rp[K - 1]));
-    cut = min(max(cut, 1), len);  // (clamped: memory-safe whatever happens)
+    int cut = len;
+    if (kPivot) {
+        cut = INT_MAX - __builtin_amdgcn_readlane(row_scan_max(lane < NW ? s[2 * NW + lane] : 0), NW - 1);
+        cut = min(max(cut, 1), len);  // (clamped: memory-safe whatever happens)
+    }
     if (act) {
-        const int hr = nr - K;
         T nv[NB];
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-            const bool sl = il[j] && ra[j] < K, sr = ir[j] && rb[j] >= hr && K > 0;
-            nv[j] = eb[sl ? kBr + ra[j] : sr ? nr - 1 - rb[j] : kTv + lane];
-        }
+        for (int j = 0; j < NB; ++j) nv[j] = eb[sl[j] ? kBr + ra[j] : sr[j] ? nr - 1 - rb[j] : kTv + lane];
 #pragma unroll
         for (int j = 0; j < NB; ++j) {
             const int x = q0 + 64 * j + lane;
-            const bool sw = (il[j] && ra[j] < K) || (ir[j] && rb[j] >= hr && K > 0);
+            const bool sw = sl[j] || sr[j];
             if (sw || (kPivot && (x == 0 || x == m))) A[x] = sw ? nv[j] : v[j];
         }
     }
@@ -1624,20 +1582,13 @@ __device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int
         const bool il = in && k <= P, ir = in && k >= P;
         const u64 ml = __ballot(il), mr = __ballot(ir);
         const int ra = mbcnt(ml, 0), rb = mbcnt(mr, 0), nr = __popcll(mr);
-        // crossing: the first range lane with g(x + 1) = ra + rb + il + ir - nr >= 0
-        const u64 g = __ballot(in && ra + rb + (int)il + (int)ir - nr >= 0);
-        const int t = g ? __ffsll((long long)g) - 1 : 63;
-        const u64 below = (1ull << t) - 1ull;
-        const int K = g ? max(nr - __popcll(mr & (below | (1ull << t))), __popcll(ml & below)) : 0;
-        const int hr = K > 0 ? nr - K : INT_MAX;
-        const bool sl = il && ra < K, sr = ir && rb >= hr;
+        const bool sl = swap_l(il, ir, ra, rb, nr), sr = swap_r(ir, ra, rb, nr);
         eb[sl ? ra : sr ? kBr + (nr - 1 - rb) : kTv + lane] = v;
+        const u64 cb = __ballot((il && !sl) || sr);  // the cut: the first unswapped L or swapped R
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         __builtin_amdgcn_wave_barrier();
         const T nv = eb[sl ? kBr + ra : sr ? nr - 1 - rb : kTv + lane];
-        const u64 cl = __ballot(il && ra == K), cr = __ballot(ir && rb == hr);
-        int cut = cl ? __ffsll((long long)cl) - 1 : INT_MAX;
-        if (cr) cut = min(cut, __ffsll((long long)cr) - 1);
+        int cut = cb ? __ffsll((long long)cb) - 1 : INT_MAX;
         cut = min(max(cut, lf + 1), ll);  // (clamped: memory-safe whatever happens)
         v = (sl || sr) ? nv : v;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (next step's mailbox writes after these reads)
