@@ -1559,18 +1559,20 @@ template <class T>
 __device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int nth, int& depth, bool& heap,
                                           const RgLds& E) {
     const int lane = threadIdx.x & 63;
-    const int f0 = f, n0 = l - f;
+    // (the range bounds are wave-uniform: declared so, the step's control flow and the pivot
+    // readlanes stay scalar instead of running under exec masks)
+    const int f0 = uni(f), n0 = uni(l) - f0;
     T v = A[f0 + min(lane, n0 - 1)];
     T* eb = E.bl<T>();
     constexpr int kBr = RgLds::kBr<T>, kTv = RgLds::kTv<T>;
-    const int kth = nth - f0;
-    int lf = 0, ll = n0;
+    const int kth = uni(nth) - f0;
+    int lf = 0, ll = n0, dep = uni(depth);
     while (ll - lf > 3) {
-        if (depth == 0) {
+        if (dep == 0) {
             heap = true;
             break;
         }
-        --depth;
+        --dep;
         const int a = lf + 1, b = lf + (ll - lf) / 2, c = ll - 1;
         const T vf = rdl(v, lf), va = rdl(v, a), vb = rdl(v, b), vc = rdl(v, c);
         T pv;
@@ -1589,7 +1591,7 @@ __device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int
         __builtin_amdgcn_wave_barrier();
         const T nv = eb[sl ? kBr + ra : sr ? nr - 1 - rb : kTv + lane];
         int cut = cb ? __ffsll((long long)cb) - 1 : INT_MAX;
-        cut = min(max(cut, lf + 1), ll);  // (clamped: memory-safe whatever happens)
+        cut = uni(min(max(cut, lf + 1), ll));  // (clamped: memory-safe whatever happens)
         v = (sl || sr) ? nv : v;
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (next step's mailbox writes after these reads)
         __builtin_amdgcn_wave_barrier();
@@ -1598,6 +1600,7 @@ __device__ __forceinline__ void rg_tail64(T* __restrict__ A, int& f, int& l, int
     }
     if (lane < n0) A[f0 + lane] = v;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    depth = dep;
     f = f0 + lf;
     l = f0 + ll;
 }
@@ -1735,7 +1738,7 @@ __device__ __forceinline__ void stl_nth_element(T* __restrict__ A, T* __restrict
         else l = cut;
     }
     VX_KT(2);
-    if ((threadIdx.x >> 6) == 0) {
+    if (uni((int)(threadIdx.x >> 6)) == 0) {  // (wave 0: a scalar branch)
         while (!heap && l - f > 3) {
             if (l - f <= 64) {  // the rest of the introselect in registers (rg_tail64)
                 VX_KP((5 << 24) | (l - f));
@@ -1788,7 +1791,7 @@ __device__ __forceinline__ int stl_retain_best(T* __restrict__ A, T* __restrict_
     } else if (len > kRgWave) {
         rg_team_any<false>(A + npts, len, thr, E, nr);
     } else {
-        if ((threadIdx.x >> 6) == 0) {
+        if (uni((int)(threadIdx.x >> 6)) == 0) {
             rg_wave_any<false>(A + npts, len, thr, E, nr);
             if (threadIdx.x == 0) s[60] = nr;
         }
@@ -1889,6 +1892,13 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         n0 += uni(btot);
     }
     __syncthreads();
+    // the output's bitmap of survivors (raster indices), in the engine's unused lp / rp region:
+    // cleared here, visible after the passes' barriers
+    unsigned* bm = reinterpret_cast<unsigned*>(E.lp());
+    const int nw32 = (n0 + 31) >> 5;
+    const bool bm_fits = 2 * nw32 * 4 <= 2 * kRgMail;
+    if (bm_fits)
+        for (int i = tid; i < nw32; i += kStlNT) bm[i] = 0u;
     if (n0 > kRgCap32) {  // the whole pass-1 array then lives in the global scratch
         for (int i = tid; i < kRgCap32; i += kStlNT) gA1[i] = lA1[i];
         __syncthreads();
@@ -1944,20 +1954,18 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         K2 = stl_retain_best(G2, G2 + K1, G2 + K1 + hb2, K1, q, E);
     }
     VX_KT(13);
-    for (int j = tid; j < K2; j += kStlNT) fin[j] = kept[(unsigned)(lds2 ? L2[j] : G2[j])];
+    // the first survivor record of each thread requested before the bitmap's barriers
+    auto sidx = [&](int j) { return (unsigned)(lds2 ? L2[j] : G2[j]); };
+    const CandRec f0 = tid < K2 ? kept[sidx(tid)] : CandRec{};
     if (tid == 0) level_count[l] = K2;
     // The survivors in raster order for k_describe's walk (rast[p] = output index of the p-th
     // survivor in raster order, over the dead pass-1 scratch): a bitmap of their raster indices in
-    // the engine's LDS (free now), word popcounts scanned, one rank per survivor.
+    // LDS (cleared after the gather), word popcounts scanned, one rank per survivor.
     int* rast = reinterpret_cast<int*>(gscr);
-    unsigned* bm = reinterpret_cast<unsigned*>(sdyn);
-    const int nw32 = (n0 + 31) >> 5;
     int* wpre = reinterpret_cast<int*>(bm + nw32);
-    if (2 * nw32 * 4 <= kRgBytes) {
-        for (int i = tid; i < nw32; i += kStlNT) bm[i] = 0u;
-        __syncthreads();
+    if (bm_fits) {
         for (int j = tid; j < K2; j += kStlNT) {
-            const unsigned idx = (unsigned)(lds2 ? L2[j] : G2[j]);
+            const unsigned idx = sidx(j);
             atomicOr(&bm[idx >> 5], 1u << (idx & 31u));
         }
         __syncthreads();
@@ -1971,12 +1979,14 @@ __global__ __launch_bounds__(kStlNT) void k_select_stl(const CandRec* __restrict
         }
         __syncthreads();
         for (int j = tid; j < K2; j += kStlNT) {
-            const unsigned idx = (unsigned)(lds2 ? L2[j] : G2[j]);
+            const unsigned idx = sidx(j);
             rast[wpre[idx >> 5] + __popc(bm[idx >> 5] & ((1u << (idx & 31u)) - 1u))] = j;
         }
     } else {
         for (int j = tid; j < K2; j += kStlNT) rast[j] = j;  // (no room: output order, no locality)
     }
+    if (tid < K2) fin[tid] = f0;
+    for (int j = tid + kStlNT; j < K2; j += kStlNT) fin[j] = kept[sidx(j)];
     VX_KT(15);
 }
 
