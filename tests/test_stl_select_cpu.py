@@ -3,7 +3,9 @@ standard library it restates, on the CPU.
 
 tests/cpp/stl_select_model.cpp restates the device algorithm (one parallel pass per Hoare
 partition: the k-th left stopper swaps with the k-th right stopper, K = max_x min(#L before x,
-#R at or after x), cut = min(L[K], R[K-1])) and compares its permutation with std::nth_element +
+#R at or after x), cut = min(L[K], R[K-1])), asserts on every pass that the device's K-free rules
+(an L of rank ra is swapped iff ra + rb + isR < nR, an R iff ra + rb >= nR; the cut is the first
+unswapped L or swapped R) pick the same swaps and cut, and compares its permutation with std::nth_element +
 std::partition (OpenCV KeyPointsFilter::retainBest, SURVEY.md App. A.3) on random, tie-heavy,
 sorted and McIlroy-adversarial inputs — the latter drive libstdc++ into its heap-select fallback.
 """
