@@ -1248,12 +1248,28 @@ __device__ __forceinline__ void add_agent(int* p, int v) {
 }
 // lanes with want: spin until *p >= target (each lane its own counter); false when the wait ran out
 // or another workgroup reported a fault
+#ifndef VX_WIN_POLLS
+#define VX_WIN_POLLS 1
+#endif
 __device__ __forceinline__ bool win_wait(const int* p, int target, bool want, int* fault) {
     const long long t0 = wall_clock64();
     bool ok = true;
     __builtin_amdgcn_s_setprio(0);  // (a polling wave leaves the SIMD to co-resident waves)
+    // VX_WIN_POLLS polls in flight: each pass issues the next poll before it checks the oldest (the
+    // loads are independent sc1 loads; the compiler waits for the oldest only).  Two or three in
+    // flight measured no faster than one (LocalBA alone 0.0508-0.0518 ms with three against
+    // 0.0498-0.0509 with one, r06s2 poll A/B): one stays the default
+    // (every lane loads — lanes without a wait read the fault word — so no exec-masked branch makes
+    // the compiler drain every load at its join)
+    const int* const pp = want ? p : fault;
+    int q[VX_WIN_POLLS];
+#pragma unroll
+    for (int i = 0; i + 1 < VX_WIN_POLLS; ++i) q[i] = ld_sc1(pp);
     for (int k = 0;; ++k) {
-        const bool pend = want && ok && ld_sc1(p) < target;
+        q[VX_WIN_POLLS - 1] = ld_sc1(pp);
+        const bool pend = want && ok && q[0] < target;
+#pragma unroll
+        for (int i = 0; i + 1 < VX_WIN_POLLS; ++i) q[i] = q[i + 1];
         if (!__any(pend)) break;
         if ((k & 15) == 15) {
             if (ld_sc1(fault) || wall_clock64() - t0 > kWinSpinTicks) {
