@@ -746,7 +746,10 @@ __device__ __forceinline__ float key2f(unsigned k) {
 
 constexpr int kSelBlock = 1024;
 constexpr int kCellsPer = 6;      // max cells per thread per gather pass
-constexpr int kRecBatch = 8;      // candidate records per thread loaded in one batch
+#ifndef VX_SEL_RECBATCH
+#define VX_SEL_RECBATCH 8
+#endif
+constexpr int kRecBatch = VX_SEL_RECBATCH;  // candidate records per thread loaded in one batch
 constexpr int kSelRecLds = 2048;  // survivors kept in LDS
 constexpr int kSelBins = 2048;    // one-pass select: histogram of the keys' top 11 bits
 
