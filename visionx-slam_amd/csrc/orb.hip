@@ -1075,9 +1075,11 @@ __global__ __launch_bounds__(kSelBlock) void k_select(const CandRec* __restrict_
 // value P, the left scanner stops at every x with !(x > P) ("L"), the right one at every x with
 // !(P > x) ("R"); swap k exchanges the k-th L from the left with the k-th R from the right for
 // k < K, K = max over x of min(#L before x, #R at or after x), and the returned cut is
-// min(L[K], R[K-1]).  std::partition is the same pairing with complementary predicates.  That
-// formulation is checked against the real STL (random, tie-heavy, sorted and McIlroy-adversarial
-// inputs reaching the heap select) by tests/cpp/stl_select_model.cpp.
+// min(L[K], R[K-1]).  std::partition is the same pairing with complementary predicates.  The
+// passes evaluate it without computing K (swap_l / swap_r below: each element's swap from its own
+// L / R ranks, the cut from ballots).  That formulation and the K-free rules are checked against the
+// real STL (random, tie-heavy, sorted and McIlroy-adversarial inputs reaching the heap select) by
+// tests/cpp/stl_select_model.cpp.
 //
 // The passes run on a register-resident engine (below): the range stays in registers across
 // them.  Elements are u32 (FAST score << 24 | raster index) for the first retainBest and u64
